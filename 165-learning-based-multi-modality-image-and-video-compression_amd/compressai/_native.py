@@ -1,0 +1,121 @@
+"""ctypes binding of libcai.so (the C ABI declared in include/cai.h).
+
+The product path has no fallback: if the library is missing or a call fails
+the error is raised (ValueError for argument/shape errors, RuntimeError for
+device errors), mirroring the reference's ``std::domain_error -> ValueError``
+convention (cpp_exts/ops/ops.cpp:46-64).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, Structure, c_char_p, c_float, c_int, c_int32, c_int64, c_size_t, c_void_p
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("CAI_LIB", os.path.join(_PKG_ROOT, "lib", "libcai.so"))
+
+CAI_OK, CAI_EINVAL, CAI_EDEVICE, CAI_EWORKSPACE = 0, 1, 2, 3
+F32, BF16 = 0, 1
+ACT_NONE, ACT_RELU, ACT_LEAKY = 0, 1, 2
+MASK_NONE, MASK_POS, MASK_LEAKY, MASK_SIGN = 0, 1, 2, 3
+Q_NOISE, Q_DEQUANTIZE, Q_SYMBOLS = 0, 1, 2
+
+
+class ConvGeom(Structure):
+    _fields_ = [(n, c_int32) for n in (
+        "batch", "in_c", "in_h", "in_w", "out_c", "out_h", "out_w",
+        "kernel", "stride", "pad", "output_padding", "transposed")]
+
+
+class EbParams(Structure):
+    _fields_ = [("matrix", c_void_p * 5), ("bias", c_void_p * 5), ("factor", c_void_p * 4), ("quantiles", c_void_p)]
+
+
+class EbGrads(Structure):
+    _fields_ = [("matrix", c_void_p * 5), ("bias", c_void_p * 5), ("factor", c_void_p * 4), ("quantiles", c_void_p)]
+
+
+# name -> (restype, argtypes)
+_P, _I, _I64, _F, _S = c_void_p, c_int, c_int64, c_float, c_size_t
+_G = POINTER(ConvGeom)
+SIGNATURES = {
+    "cai_last_error": (c_char_p, []),
+    "cai_version": (c_int, []),
+    "cai_abi_count": (c_int, []),
+    "cai_conv_packed_weight_bytes": (_S, [_G, _I, _I]),
+    "cai_conv_pack_weight": (_I, [_G, _I, _I, _P, _P, _P, _P]),
+    "cai_pack_nchw": (_I, [_P, c_int32, c_int32, c_int32, c_int32, _I, _P, c_int32, _P]),
+    "cai_conv_fwd": (_I, [_G, _I, _P, c_int32, c_int32, _P, _P, c_int32, _F, _P, _I, _I64, _I64, _I64, _I64, _P]),
+    "cai_conv_dgrad": (_I, [_G, _I, _P, c_int32, _P, _P, c_int32, c_int32, _F, _P, c_int32, _P]),
+    "cai_conv_wgrad_workspace_bytes": (_S, [_G, _I]),
+    "cai_conv_wgrad": (_I, [_G, _I, _P, c_int32, c_int32, c_int32, _P, c_int32, _P, _P, _P, _S, _P]),
+    "cai_gdn_reparam": (_I, [_P, _P, c_int32, _F, _F, _I, _P, _P, _P]),
+    "cai_gdn_fwd": (_I, [_I, _P, c_int32, _I64, c_int32, _P, _P, c_int32, _P, c_int32, _P]),
+    "cai_gdn_bwd": (_I, [_I, _P, c_int32, _P, c_int32, _I64, c_int32, _P, _P, c_int32, _P, c_int32, _P, _P]),
+    "cai_gdn_param_grad_workspace_bytes": (_S, [_I64, c_int32, _I]),
+    "cai_gdn_param_grad": (_I, [_I, _P, c_int32, _P, _I64, c_int32, _P, _P, _F, _F, _P, _P, _P, _S, _P]),
+    "cai_quantize": (_I, [_I, _I64, c_int32, _P, _I, c_int32, _P, c_int32, c_int32, _P, c_int32, _P, _I, c_int32, _P]),
+    "cai_gc_fwd": (_I, [_I, _I64, c_int32, _P, _I, c_int32, _P, c_int32, _P, c_int32, _I, _P, c_int32, _F, _F,
+                        _P, _I, c_int32, _P, c_int32, _P]),
+    "cai_gc_bwd": (_I, [_I, _I64, c_int32, _P, _I, c_int32, _P, c_int32, _P, c_int32, _I, _P, c_int32, _F, _F,
+                        _P, c_int32, _P, _I, c_int32, _P, c_int32, _P, c_int32, _P, c_int32, _P]),
+    "cai_eb_fwd": (_I, [_I, _I64, c_int32, POINTER(EbParams), _P, _I, c_int32, _P, c_int32, _F, _P, _I, c_int32,
+                        _P, c_int32, _P]),
+    "cai_eb_bwd": (_I, [_I, _I64, c_int32, POINTER(EbParams), _P, _I, c_int32, _P, c_int32, _F, _P, c_int32, _P,
+                        _I, c_int32, _P, c_int32, POINTER(EbGrads), _P]),
+    "cai_eb_aux_loss": (_I, [c_int32, POINTER(EbParams), _P, _P, _P, _P, _P]),
+    "cai_sum_log": (_I, [_P, _I64, c_int32, c_int32, _P, _P, _S, _P]),
+    "cai_sum_sqdiff": (_I, [_P, _P, _I64, _P, _P, _S, _P]),
+    "cai_reduce_workspace_bytes": (_S, [_I64]),
+    "cai_log_bwd": (_I, [_P, _I64, c_int32, c_int32, _P, _F, _P, _P]),
+    "cai_sqdiff_bwd": (_I, [_P, _P, _I64, _P, _F, _P, _P]),
+    "cai_sqnorm": (_I, [_P, _I64, _P, _P, _S, _P]),
+    "cai_adam": (_I, [_P, _P, _P, _P, _I64, _F, _F, _F, _F, _P, _P, _F, _P]),
+    "cai_act_bwd": (_I, [_I, _F, _P, c_int32, _P, c_int32, _P, c_int32, _I64, c_int32, _I, _P]),
+    "cai_cast": (_I, [_P, _I, _P, _I, _I64, _P]),
+}
+
+
+class _Lib:
+    def __init__(self):
+        self._lib = None
+
+    def load(self):
+        if self._lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(
+                    f"libcai.so not found at {LIB_PATH}: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                    " (there is no CPU fallback)")
+            lib = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            self._lib = lib
+        return self._lib
+
+    def __getattr__(self, name):
+        fn = getattr(self.load(), name)
+
+        if fn.restype is c_int and name not in ("cai_version", "cai_abi_count"):
+            def call(*args):
+                rc = fn(*args)
+                if rc != CAI_OK:
+                    msg = self.load().cai_last_error().decode(errors="replace")
+                    if rc in (CAI_EINVAL, CAI_EWORKSPACE):
+                        raise ValueError(f"{name}: {msg}")
+                    raise RuntimeError(f"{name}: {msg}")
+                return rc
+            return call
+        return fn
+
+
+lib = _Lib()
+
+
+def available() -> bool:
+    try:
+        lib.load()
+        return True
+    except (OSError, RuntimeError):
+        return False

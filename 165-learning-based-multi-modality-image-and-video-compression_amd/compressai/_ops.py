@@ -1,0 +1,476 @@
+"""Autograd functions over libcai (HIP kernels for gfx950).
+
+Tensor convention: activations travel between these functions as
+*pixel-major* tensors -- logical NCHW ``[B, C, H, W]`` with
+``torch.channels_last`` strides (element (p, c) at ``p*ld + c``).  A channel
+slice of a wider pixel-major tensor (``chunk(2, 1)``) is pixel-major with
+``ld > C`` and is consumed without a copy.
+
+Compute precision: inside ``torch.autocast("cuda")`` the conv / GDN operands
+are bf16 (fp32 MFMA accumulation) -- the counterpart of the reference's
+``torch.cuda.amp.autocast`` training (examples/train.py:172-173); outside it
+everything runs in exact fp32 (v_mfma_f32_16x16x4_f32), which is the mode the
+parity tests compare against the CPU oracle.  Likelihoods and losses are
+always fp32.
+
+Every op here launches HIP kernels on ``torch.cuda.current_stream()``; CPU
+tensors are rejected (there is no CPU fallback).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import Optional, Sequence, Tuple
+
+import torch
+
+from ._native import (ACT_NONE, BF16, F32, MASK_NONE, Q_DEQUANTIZE, Q_NOISE, ConvGeom, EbGrads, EbParams, lib)
+
+_VP = ctypes.c_void_p
+
+
+# ---------------------------------------------------------------------------
+# small helpers
+# ---------------------------------------------------------------------------
+
+def _stream() -> _VP:
+    return _VP(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t: Optional[torch.Tensor]) -> Optional[_VP]:
+    return None if t is None else _VP(t.data_ptr())
+
+
+def dcode(dtype: torch.dtype) -> int:
+    if dtype == torch.bfloat16:
+        return BF16
+    if dtype == torch.float32:
+        return F32
+    raise ValueError(f"unsupported dtype {dtype} (bf16 / fp32 only)")
+
+
+def compute_dtype() -> torch.dtype:
+    """bf16 inside torch.autocast('cuda'), exact fp32 otherwise."""
+    return torch.bfloat16 if torch.is_autocast_enabled("cuda") else torch.float32
+
+
+def _vec(dtype: torch.dtype) -> int:
+    return 8 if dtype == torch.bfloat16 else 4
+
+
+def _check_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise ValueError("compressai (MI355X build) runs on GPU tensors only; got a CPU tensor")
+
+
+def pixel_major_ld(t: torch.Tensor) -> Optional[int]:
+    """ld if the 4-D tensor is pixel-major (channel stride 1, pixel stride ld), else None."""
+    if t.dim() != 4:
+        return None
+    B, C, H, W = t.shape
+    s = t.stride()
+    if C > 1 and s[1] != 1:
+        return None
+    if W > 1:
+        ld = s[3]
+    elif H > 1:
+        ld = s[2]
+    elif B > 1:
+        ld = s[0]
+    else:
+        ld = C
+    if ld < C:
+        return None
+    if (W > 1 and s[3] != ld) or (H > 1 and s[2] != W * ld) or (B > 1 and s[0] != H * W * ld):
+        return None
+    return int(ld)
+
+
+def empty_pm(B: int, C: int, H: int, W: int, dtype, device, ld: Optional[int] = None) -> torch.Tensor:
+    """Pixel-major [B, C, H, W] tensor (ld = C unless a wider padded row is requested)."""
+    ld = C if ld is None else ld
+    buf = torch.empty((B, H, W, ld), dtype=dtype, device=device)
+    return buf.permute(0, 3, 1, 2)[:, :C]
+
+
+def to_pm(t: torch.Tensor, dtype: torch.dtype, vec: int) -> Tuple[torch.Tensor, int]:
+    """Pixel-major copy/view of a 4-D tensor with ld % vec == 0 (channels zero-padded when C % vec != 0)."""
+    B, C, H, W = t.shape
+    ld = pixel_major_ld(t)
+    if t.dtype == dtype and ld is not None and ld % vec == 0 and (C % vec == 0 or ld > C) and t.data_ptr() % 16 == 0:
+        if C % vec == 0 or _pad_is_zero_marked(t):
+            return t, ld
+    if C % vec == 0:
+        out = empty_pm(B, C, H, W, dtype, t.device)
+        out.copy_(t)
+        return out, C
+    cp = (C + 7) // 8 * 8
+    src = t.float().contiguous()
+    out = empty_pm(B, cp, H, W, dtype, t.device)
+    lib.cai_pack_nchw(_p(src), B, C, H, W, dcode(dtype), _p(out), cp, _stream())
+    view = out[:, :C]
+    _mark_pad_zero(view)
+    return view, cp
+
+
+_ZERO_PAD = "_cai_zero_pad"
+
+
+def _mark_pad_zero(t):
+    setattr(t, _ZERO_PAD, True)
+
+
+def _pad_is_zero_marked(t):
+    return getattr(t, _ZERO_PAD, False)
+
+
+def as_rows(t: torch.Tensor) -> Tuple[torch.Tensor, int, int, int]:
+    """(tensor, ld, npix, C): element (p, c) of the channel-first logical tensor at p*ld + c."""
+    C = t.shape[1]
+    if t.dim() == 4:
+        ld = pixel_major_ld(t)
+        if ld is not None:
+            npix = t.shape[0] * t.shape[2] * t.shape[3]
+            return t, ld, npix, C
+    r = t.movedim(1, -1).contiguous()
+    return r, C, r.numel() // max(C, 1), C
+
+
+def empty_rows_like(shape, dtype, device) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(logical tensor of `shape` (channel dim 1), its pixel-major buffer)."""
+    B, C = shape[0], shape[1]
+    buf = torch.empty((B, *shape[2:], C), dtype=dtype, device=device)
+    return buf.movedim(-1, 1), buf
+
+
+# ---------------------------------------------------------------------------
+# convolution
+# ---------------------------------------------------------------------------
+
+class ConvSpec:
+    """Static description of one Conv2d / ConvTranspose2d call site."""
+
+    __slots__ = ("k", "s", "p", "op", "transposed", "act", "act_param", "in_abs", "out_nchw32",
+                 "in_mask", "in_mask_param", "act_bwd_downstream")
+
+    def __init__(self, k, s, p, op=0, transposed=False, act=ACT_NONE, act_param=0.0, in_abs=False,
+                 out_nchw32=False, in_mask=MASK_NONE, in_mask_param=0.0, act_bwd_downstream=False):
+        self.k, self.s, self.p, self.op = int(k), int(s), int(p), int(op)
+        self.transposed = bool(transposed)
+        self.act, self.act_param = int(act), float(act_param)
+        self.in_abs = bool(in_abs)
+        self.out_nchw32 = bool(out_nchw32)
+        self.in_mask, self.in_mask_param = int(in_mask), float(in_mask_param)
+        self.act_bwd_downstream = bool(act_bwd_downstream)
+
+
+def conv_geom(spec: ConvSpec, B, cin, H, W, cout) -> ConvGeom:
+    if spec.transposed:
+        OH = (H - 1) * spec.s - 2 * spec.p + spec.k + spec.op
+        OW = (W - 1) * spec.s - 2 * spec.p + spec.k + spec.op
+    else:
+        OH = (H + 2 * spec.p - spec.k) // spec.s + 1
+        OW = (W + 2 * spec.p - spec.k) // spec.s + 1
+    return ConvGeom(B, cin, H, W, cout, OH, OW, spec.k, spec.s, spec.p, spec.op, int(spec.transposed))
+
+
+def _pack_weight(g: ConvGeom, dtype, direction: int, weight: torch.Tensor) -> torch.Tensor:
+    nbytes = lib.cai_conv_packed_weight_bytes(ctypes.byref(g), dcode(dtype), direction)
+    if nbytes == 0:
+        raise ValueError("conv: invalid geometry")
+    wp = torch.empty(nbytes, dtype=torch.uint8, device=weight.device)
+    w = weight.detach().float().contiguous()
+    lib.cai_conv_pack_weight(ctypes.byref(g), dcode(dtype), direction, _p(w), None, _p(wp), _stream())
+    return wp
+
+
+class ConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, spec: ConvSpec):
+        _check_cuda(x, weight, bias)
+        dt = compute_dtype()
+        vec = _vec(dt)
+        B, cin, H, W = x.shape
+        cout = weight.shape[1] if spec.transposed else weight.shape[0]
+        g = conv_geom(spec, B, cin, H, W, cout)
+        xpm, xld = to_pm(x, dt, vec)
+        wp = _pack_weight(g, dt, 0, weight)
+        b = bias.detach().float().contiguous() if bias is not None else None
+        if spec.out_nchw32:
+            y = torch.empty((B, cout, g.out_h, g.out_w), dtype=torch.float32, device=x.device)
+            ys = (cout * g.out_h * g.out_w, g.out_h * g.out_w, g.out_w, 1)
+            ydt = F32
+        else:
+            y = empty_pm(B, cout, g.out_h, g.out_w, dt, x.device)
+            ys = (g.out_h * g.out_w * cout, 1, g.out_w * cout, cout)
+            ydt = dcode(dt)
+        lib.cai_conv_fwd(ctypes.byref(g), dcode(dt), _p(xpm), xld, int(spec.in_abs), _p(wp), _p(b), spec.act,
+                         spec.act_param, _p(y), ydt, *ys, _stream())
+        ctx.spec, ctx.geom, ctx.dt, ctx.xld = spec, g, dt, xld
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(xpm, weight, y if spec.act != ACT_NONE else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xpm, weight, y = ctx.saved_tensors
+        spec, g, dt = ctx.spec, ctx.geom, ctx.dt
+        vec = _vec(dt)
+        code = dcode(dt)
+        st = _stream()
+        gpm, gld = to_pm(gy, dt, vec)
+        if spec.act != ACT_NONE and not spec.act_bwd_downstream:
+            mode = 1 if spec.act == 1 else 2
+            out = empty_pm(g.batch, g.out_c, g.out_h, g.out_w, dt, gy.device)
+            yld = pixel_major_ld(y)
+            lib.cai_act_bwd(mode, spec.act_param, _p(y), yld, _p(gpm), gld, _p(out), g.out_c,
+                            g.batch * g.out_h * g.out_w, g.out_c, code, st)
+            gpm, gld = out, g.out_c
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            wt = _pack_weight(g, dt, 1, weight)
+            ldx = (g.in_c + vec - 1) // vec * vec
+            dx = empty_pm(g.batch, g.in_c, g.in_h, g.in_w, dt, gy.device, ld=ldx)
+            aux = xpm if spec.in_mask != MASK_NONE else None
+            lib.cai_conv_dgrad(ctypes.byref(g), code, _p(gpm), gld, _p(wt), _p(dx), ldx, spec.in_mask,
+                               spec.in_mask_param, _p(aux), ctx.xld if aux is not None else 0, st)
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            nbytes = lib.cai_conv_wgrad_workspace_bytes(ctypes.byref(g), code)
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=gy.device)
+            dw = torch.empty(weight.shape, dtype=torch.float32, device=gy.device)
+            db = torch.empty(g.out_c, dtype=torch.float32, device=gy.device) if ctx.has_bias else None
+            lib.cai_conv_wgrad(ctypes.byref(g), code, _p(xpm), ctx.xld, int(spec.in_abs), 0, _p(gpm), gld, _p(dw),
+                               _p(db), _p(ws), nbytes, st)
+            if weight.dtype != torch.float32:
+                dw = dw.to(weight.dtype)
+        return dx, dw, db, None
+
+
+# ---------------------------------------------------------------------------
+# GDN / IGDN
+# ---------------------------------------------------------------------------
+
+class GdnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, beta_raw, gamma_raw, inverse: bool, beta_min: float, reparam_offset: float):
+        _check_cuda(x, beta_raw, gamma_raw)
+        dt = compute_dtype()
+        code = dcode(dt)
+        B, C, H, W = x.shape
+        xpm, xld = to_pm(x, dt, 8)
+        npix = B * H * W
+        st = _stream()
+        br = beta_raw.detach().float().contiguous()
+        gr = gamma_raw.detach().float().contiguous()
+        beta = torch.empty(C, dtype=torch.float32, device=x.device)
+        gop = torch.empty(2 * C * C, dtype=dt, device=x.device)
+        lib.cai_gdn_reparam(_p(br), _p(gr), C, beta_min, reparam_offset, code, _p(beta), _p(gop), st)
+        y = empty_pm(B, C, H, W, dt, x.device)
+        lib.cai_gdn_fwd(code, _p(xpm), xld, npix, C, _p(gop), _p(beta), int(inverse), _p(y), C, st)
+        ctx.save_for_backward(xpm, br, gr, beta, gop)
+        ctx.cfg = (dt, xld, int(inverse), float(beta_min), float(reparam_offset))
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xpm, br, gr, beta, gop = ctx.saved_tensors
+        dt, xld, inverse, beta_min, off = ctx.cfg
+        code = dcode(dt)
+        B, C, H, W = xpm.shape
+        npix = B * H * W
+        st = _stream()
+        gpm, gld = to_pm(gy, dt, 8)
+        dx = empty_pm(B, C, H, W, dt, gy.device)
+        u = torch.empty(npix * C, dtype=dt, device=gy.device)
+        lib.cai_gdn_bwd(code, _p(xpm), xld, _p(gpm), gld, npix, C, _p(gop), _p(beta), inverse, _p(dx), C, _p(u), st)
+        nbytes = lib.cai_gdn_param_grad_workspace_bytes(npix, C, code)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=gy.device)
+        dbr = torch.empty(C, dtype=torch.float32, device=gy.device)
+        dgr = torch.empty((C, C), dtype=torch.float32, device=gy.device)
+        lib.cai_gdn_param_grad(code, _p(xpm), xld, _p(u), npix, C, _p(br), _p(gr), beta_min, off, _p(dbr), _p(dgr),
+                               _p(ws), nbytes, st)
+        return dx, dbr, dgr, None, None, None
+
+
+# ---------------------------------------------------------------------------
+# entropy models
+# ---------------------------------------------------------------------------
+
+class GaussianFn(torch.autograd.Function):
+    """GaussianConditional.forward (entropy_models.py:715-731) as one fused kernel pair."""
+
+    @staticmethod
+    def forward(ctx, x, scales, means, noise, mode: int, scale_bound: float, lik_bound: float):
+        _check_cuda(x, scales, means, noise)
+        xr, xld, npix, C = as_rows(x)
+        if means is not None and means.dtype != scales.dtype:
+            means = means.to(scales.dtype)
+        sr, sld, _, _ = as_rows(scales)
+        mr, mld = (None, 0) if means is None else as_rows(means)[:2]
+        nr, nld = (None, 0) if noise is None else as_rows(noise)[:2]
+        smdt = dcode(scales.dtype)
+        q, qbuf = empty_rows_like(x.shape, x.dtype, x.device)
+        lik, lbuf = empty_rows_like(x.shape, torch.float32, x.device)
+        lib.cai_gc_fwd(mode, npix, C, _p(xr), dcode(x.dtype), xld, _p(sr), sld, _p(mr), mld, smdt, _p(nr), nld,
+                       scale_bound, lik_bound, _p(qbuf), dcode(x.dtype), C, _p(lbuf), C, _stream())
+        ctx.save_for_backward(xr, sr, mr, nr)
+        ctx.cfg = (mode, scale_bound, lik_bound, xld, sld, mld, nld, npix, C, x.shape, x.dtype, scales.shape,
+                   scales.dtype, means is not None)
+        return q, lik
+
+    @staticmethod
+    def backward(ctx, gq, glik):
+        xr, sr, mr, nr = ctx.saved_tensors
+        mode, sb, lb, xld, sld, mld, nld, npix, C, xshape, xdtype, sshape, sdtype, has_m = ctx.cfg
+        gl = gq_r = None
+        glld = gqld = 0
+        if glik is not None:
+            gl, glld = as_rows(glik.float())[:2]
+        if gq is not None:
+            gq_r, gqld = as_rows(gq)[:2]
+        dx, dxb = empty_rows_like(xshape, xdtype, xr.device)
+        ds, dsb = empty_rows_like(sshape, sdtype, xr.device)
+        dm, dmb = empty_rows_like(sshape, sdtype, xr.device) if has_m else (None, None)
+        lib.cai_gc_bwd(mode, npix, C, _p(xr), dcode(xdtype), xld, _p(sr), sld, _p(mr), mld, dcode(sdtype), _p(nr),
+                       nld, sb, lb, _p(gl), glld, _p(gq_r), dcode(gq_r.dtype) if gq_r is not None else F32, gqld,
+                       _p(dxb), C, _p(dsb), C, _p(dmb), C, _stream())
+        return dx, ds, dm, None, None, None, None
+
+
+def _eb_params(params: Sequence[torch.Tensor], quantiles: torch.Tensor) -> EbParams:
+    P = EbParams()
+    for i in range(5):
+        P.matrix[i] = params[i].data_ptr()
+        P.bias[i] = params[5 + i].data_ptr()
+    for i in range(4):
+        P.factor[i] = params[10 + i].data_ptr()
+    P.quantiles = quantiles.data_ptr()
+    return P
+
+
+class BottleneckFn(torch.autograd.Function):
+    """EntropyBottleneck.forward (entropy_models.py:495-540) minus the permutes."""
+
+    @staticmethod
+    def forward(ctx, x, quantiles, noise, mode: int, lik_bound: float, *params):
+        _check_cuda(x, quantiles, noise)
+        prm = [p.detach().float().contiguous() for p in params]
+        q_ = quantiles.detach().float().contiguous()
+        xr, xld, npix, C = as_rows(x)
+        nr, nld = (None, 0) if noise is None else as_rows(noise)[:2]
+        q, qbuf = empty_rows_like(x.shape, x.dtype, x.device)
+        lik, lbuf = empty_rows_like(x.shape, torch.float32, x.device)
+        P = _eb_params(prm, q_)
+        lib.cai_eb_fwd(mode, npix, C, ctypes.byref(P), _p(xr), dcode(x.dtype), xld, _p(nr), nld, lik_bound,
+                       _p(qbuf), dcode(x.dtype), C, _p(lbuf), C, _stream())
+        ctx.save_for_backward(xr, nr, q_, *prm)
+        ctx.cfg = (mode, lik_bound, xld, nld, npix, C, x.shape, x.dtype)
+        return q, lik
+
+    @staticmethod
+    def backward(ctx, gq, glik):
+        xr, nr, q_, *prm = ctx.saved_tensors
+        mode, lb, xld, nld, npix, C, xshape, xdtype = ctx.cfg
+        gl = gq_r = None
+        glld = gqld = 0
+        if glik is not None:
+            gl, glld = as_rows(glik.float())[:2]
+        if gq is not None:
+            gq_r, gqld = as_rows(gq)[:2]
+        dx, dxb = empty_rows_like(xshape, xdtype, xr.device)
+        grads = [torch.empty_like(p) for p in prm]
+        dq = torch.empty_like(q_)
+        G = EbGrads()
+        for i in range(5):
+            G.matrix[i] = grads[i].data_ptr()
+            G.bias[i] = grads[5 + i].data_ptr()
+        for i in range(4):
+            G.factor[i] = grads[10 + i].data_ptr()
+        G.quantiles = dq.data_ptr()
+        P = _eb_params(prm, q_)
+        lib.cai_eb_bwd(mode, npix, C, ctypes.byref(P), _p(xr), dcode(xdtype), xld, _p(nr), nld, lb, _p(gl), glld,
+                       _p(gq_r), dcode(gq_r.dtype) if gq_r is not None else F32, gqld, _p(dxb), C, ctypes.byref(G),
+                       _stream())
+        return (dx, dq, None, None, None, *grads)
+
+
+class BottleneckAuxFn(torch.autograd.Function):
+    """EntropyBottleneck.loss (entropy_models.py:450-454): gradient reaches only `quantiles`."""
+
+    @staticmethod
+    def forward(ctx, quantiles, target, *params):
+        _check_cuda(quantiles)
+        prm = [p.detach().float().contiguous() for p in params]
+        q_ = quantiles.detach().float().contiguous()
+        C = q_.shape[0]
+        t = target.float().contiguous()
+        loss = torch.empty((), dtype=torch.float32, device=quantiles.device)
+        P = _eb_params(prm, q_)
+        lib.cai_eb_aux_loss(C, ctypes.byref(P), _p(t), _p(loss), None, None, _stream())
+        ctx.save_for_backward(q_, t, *prm)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        q_, t, *prm = ctx.saved_tensors
+        C = q_.shape[0]
+        gl = g.float().contiguous().reshape(())
+        dq = torch.empty_like(q_)
+        P = _eb_params(prm, q_)
+        lib.cai_eb_aux_loss(C, ctypes.byref(P), _p(t), None, _p(gl), _p(dq), _stream())
+        return (dq, None, *([None] * len(prm)))
+
+
+# ---------------------------------------------------------------------------
+# rate-distortion loss (examples/train.py:68-82)
+# ---------------------------------------------------------------------------
+
+class RdLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x_hat, target, lmbda: float, npix: int, *liks):
+        _check_cuda(x_hat, target, *liks)
+        xh = x_hat.float().contiguous()
+        tg = target.float().contiguous()
+        n = xh.numel()
+        st = _stream()
+        sums = torch.empty(len(liks) + 1, dtype=torch.float32, device=xh.device)
+        rows = []
+        for i, l in enumerate(liks):
+            lr, ld, lp, C = as_rows(l.float())
+            rows.append((lr, ld, lp, C))
+            nb = lib.cai_reduce_workspace_bytes(lp * C)
+            ws = torch.empty(nb, dtype=torch.uint8, device=xh.device)
+            lib.cai_sum_log(_p(lr), lp, C, ld, _p(sums[i:i + 1]), _p(ws), nb, st)
+        nb = lib.cai_reduce_workspace_bytes(n)
+        ws = torch.empty(nb, dtype=torch.uint8, device=xh.device)
+        lib.cai_sum_sqdiff(_p(xh), _p(tg), n, _p(sums[-1:]), _p(ws), nb, st)
+        bpp_coef = 1.0 / (-math.log(2) * npix)
+        bpp = sums[:-1].sum() * bpp_coef
+        mse = sums[-1] / n
+        loss = lmbda * mse + bpp
+        ctx.save_for_backward(xh, tg, *[r[0] for r in rows])
+        ctx.cfg = (lmbda, bpp_coef, n, [(r[1], r[2], r[3]) for r in rows], [l.shape for l in liks], x_hat.shape)
+        return loss, mse, bpp
+
+    @staticmethod
+    def backward(ctx, gl, gm, gb):
+        xh, tg, *lrs = ctx.saved_tensors
+        lmbda, bpp_coef, n, meta, lshapes, xshape = ctx.cfg
+        zero = torch.zeros((), dtype=torch.float32, device=xh.device)
+        gl = zero if gl is None else gl.float()
+        gm = zero if gm is None else gm.float()
+        gb = zero if gb is None else gb.float()
+        gbt = (gb + gl).reshape(1).contiguous()
+        gmt = (gm + lmbda * gl).reshape(1).contiguous()
+        st = _stream()
+        dxh = torch.empty_like(xh)
+        lib.cai_sqdiff_bwd(_p(xh), _p(tg), n, _p(gmt), 2.0 / n, _p(dxh), st)
+        dliks = []
+        for lr, (ld, lp, C), shp in zip(lrs, meta, lshapes):
+            d, dbuf = empty_rows_like(shp, torch.float32, xh.device)
+            if ld != C:
+                raise ValueError("likelihood tensors must be dense pixel-major")
+            lib.cai_log_bwd(_p(lr), lp, C, ld, _p(gbt), bpp_coef, _p(dbuf), st)
+            dliks.append(d)
+        return (dxh.view(xshape), None, None, None, *dliks)

@@ -1,0 +1,244 @@
+"""EntropyModel / EntropyBottleneck / GaussianConditional on the HIP kernels.
+
+Reference: compressai/entropy_models/entropy_models.py (quantize :157-182,
+EntropyBottleneck :330-574, GaussianConditional :577-740).  Parameters,
+buffers, constructor arguments, ValueError checks and the
+``forward(...) -> (outputs, likelihoods)`` contract are kept; the forward
+and backward of the likelihood path are single fused kernels
+(cai_eb_fwd/_bwd, cai_gc_fwd/_bwd) instead of ~40 small torch ops, and
+training-mode noise is U(-1/2, 1/2) drawn with torch's generator exactly like
+the reference (``empty_like(x).uniform_(-0.5, 0.5)``), consumed by the kernel.
+
+The bitstream side (update / compress / decompress, C++ in the reference)
+is not on the hot path and is not provided in this round.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Any, Callable, List, Optional, Tuple, Union
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from .._native import F32, Q_DEQUANTIZE, Q_NOISE, Q_SYMBOLS, lib
+from .._ops import BottleneckAuxFn, BottleneckFn, GaussianFn, _check_cuda, _p, _stream, as_rows, dcode, empty_rows_like
+from ..ops import LowerBound
+
+__all__ = ["EntropyModel", "EntropyBottleneck", "GaussianConditional", "set_noise_source"]
+
+# ---------------------------------------------------------------------------
+# noise source: torch's generator by default; tests inject identical tensors
+# into this build and into the CPU oracle.
+# ---------------------------------------------------------------------------
+_noise_source: Optional[Callable[[torch.Tensor], torch.Tensor]] = None
+
+
+def set_noise_source(fn: Optional[Callable[[torch.Tensor], torch.Tensor]]):
+    """fn(x) -> fp32 noise tensor of x's logical shape (None restores U(-1/2,1/2))."""
+    global _noise_source
+    _noise_source = fn
+
+
+def _draw_noise(x: torch.Tensor) -> torch.Tensor:
+    if _noise_source is not None:
+        n = _noise_source(x)
+        if tuple(n.shape) != tuple(x.shape):
+            raise ValueError(f"noise source returned shape {tuple(n.shape)}, expected {tuple(x.shape)}")
+        return n.to(device=x.device, dtype=torch.float32)
+    return torch.empty_like(x, dtype=torch.float32).uniform_(-0.5, 0.5)
+
+
+class _QuantizeFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, means, noise, mode: int):
+        _check_cuda(x, means, noise)
+        xr, xld, npix, C = as_rows(x)
+        m = None
+        mld, mpc = 0, 0
+        if means is not None:
+            if means.numel() == C and means.dim() != x.dim():
+                m, mld, mpc = means.float().contiguous().reshape(C), 0, 1
+            else:
+                m, mld = as_rows(means.float().expand_as(x))[:2]
+        nr, nld = (None, 0) if noise is None else as_rows(noise)[:2]
+        odt = torch.int32 if mode == Q_SYMBOLS else x.dtype
+        out, obuf = empty_rows_like(x.shape, odt, x.device)
+        lib.cai_quantize(mode, npix, C, _p(xr), dcode(x.dtype), xld, _p(m), mld, mpc, _p(nr), nld, _p(obuf),
+                         dcode(x.dtype) if mode != Q_SYMBOLS else F32, C, _stream())
+        ctx.mode = mode
+        ctx.has_means = means is not None
+        ctx.mshape = None if means is None else means.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        if ctx.mode == Q_NOISE:
+            return g, None, None, None
+        gm = None
+        if ctx.has_means:
+            gm = g.float()
+            if tuple(gm.shape) != tuple(ctx.mshape):
+                gm = gm.sum_to_size(ctx.mshape)
+        return torch.zeros_like(g), gm, None, None
+
+
+class EntropyModel(nn.Module):
+    def __init__(self, likelihood_bound: float = 1e-9, entropy_coder: Optional[str] = None,
+                 entropy_coder_precision: int = 16):
+        super().__init__()
+        from .. import available_entropy_coders, get_entropy_coder
+
+        if entropy_coder is None:
+            entropy_coder = get_entropy_coder()
+        if not isinstance(entropy_coder, str):
+            raise ValueError(f'Invalid method type "{type(entropy_coder)}"')
+        if entropy_coder not in available_entropy_coders():
+            raise ValueError(f'Unknown entropy coder "{entropy_coder}" (available: {", ".join(available_entropy_coders())})')
+        self.entropy_coder = entropy_coder
+        self.entropy_coder_precision = int(entropy_coder_precision)
+        self.use_likelihood_bound = likelihood_bound > 0
+        if self.use_likelihood_bound:
+            self.likelihood_lower_bound = LowerBound(likelihood_bound)
+        self.register_buffer("_offset", torch.IntTensor())
+        self.register_buffer("_quantized_cdf", torch.IntTensor())
+        self.register_buffer("_cdf_length", torch.IntTensor())
+
+    @property
+    def offset(self):
+        return self._offset
+
+    @property
+    def quantized_cdf(self):
+        return self._quantized_cdf
+
+    @property
+    def cdf_length(self):
+        return self._cdf_length
+
+    def _lik_bound(self) -> float:
+        return float(self.likelihood_lower_bound.bound.item()) if self.use_likelihood_bound else 0.0
+
+    def forward(self, *args: Any) -> Any:
+        raise NotImplementedError()
+
+    def quantize(self, inputs: torch.Tensor, mode: str, means: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if mode not in ("noise", "dequantize", "symbols"):
+            raise ValueError(f'Invalid quantization mode: "{mode}"')
+        if mode == "noise":
+            return _QuantizeFn.apply(inputs, None, _draw_noise(inputs), Q_NOISE)
+        if mode == "dequantize":
+            return _QuantizeFn.apply(inputs, means, None, Q_DEQUANTIZE)
+        return _QuantizeFn.apply(inputs, means, None, Q_SYMBOLS)
+
+    @staticmethod
+    def dequantize(inputs: torch.Tensor, means: Optional[torch.Tensor] = None, dtype: torch.dtype = torch.float):
+        if means is not None:
+            out = inputs.type_as(means)
+            out += means
+            return out
+        return inputs.type(dtype)
+
+
+class EntropyBottleneck(EntropyModel):
+    _offset: torch.Tensor
+
+    def __init__(self, channels: int, *args: Any, tail_mass: float = 1e-9, init_scale: float = 10,
+                 filters: Tuple[int, ...] = (3, 3, 3, 3), **kwargs: Any):
+        super().__init__(*args, **kwargs)
+        self.channels = int(channels)
+        self.filters = tuple(int(f) for f in filters)
+        if self.filters != (3, 3, 3, 3):
+            raise ValueError("the fused EntropyBottleneck kernel implements filters=(3, 3, 3, 3)")
+        self.init_scale = float(init_scale)
+        self.tail_mass = float(tail_mass)
+        widths = (1,) + self.filters + (1,)
+        scale = self.init_scale ** (1 / (len(self.filters) + 1))
+        for i in range(len(self.filters) + 1):
+            init = np.log(np.expm1(1 / scale / widths[i + 1]))
+            self.register_parameter(f"_matrix{i:d}",
+                                    nn.Parameter(torch.Tensor(self.channels, widths[i + 1], widths[i]).fill_(init)))
+            b = torch.Tensor(self.channels, widths[i + 1], 1)
+            nn.init.uniform_(b, -0.5, 0.5)
+            self.register_parameter(f"_bias{i:d}", nn.Parameter(b))
+            if i < len(self.filters):
+                self.register_parameter(f"_factor{i:d}", nn.Parameter(torch.zeros(self.channels, widths[i + 1], 1)))
+        self.quantiles = nn.Parameter(
+            torch.Tensor([-self.init_scale, 0, self.init_scale]).repeat(self.channels, 1, 1))
+        target = np.log(2 / self.tail_mass - 1)
+        self.register_buffer("target", torch.Tensor([-target, 0, target]))
+
+    def _params(self) -> List[torch.Tensor]:
+        return ([getattr(self, f"_matrix{i}") for i in range(5)] + [getattr(self, f"_bias{i}") for i in range(5)]
+                + [getattr(self, f"_factor{i}") for i in range(4)])
+
+    def _get_medians(self) -> torch.Tensor:
+        return self.quantiles[:, :, 1:2]
+
+    def loss(self) -> torch.Tensor:
+        return BottleneckAuxFn.apply(self.quantiles, self.target, *self._params())
+
+    def forward(self, x: torch.Tensor, training: Optional[bool] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        if training is None:
+            training = self.training
+        if x.dim() < 2 or x.shape[1] != self.channels:
+            raise ValueError(f"expected [B, {self.channels}, ...] input, got {tuple(x.shape)}")
+        noise = _draw_noise(x) if training else None
+        return BottleneckFn.apply(x, self.quantiles, noise, Q_NOISE if training else Q_DEQUANTIZE,
+                                  self._lik_bound(), *self._params())
+
+    @staticmethod
+    def _build_indexes(size):
+        dims = len(size)
+        view_dims = np.ones((dims,), dtype=np.int64)
+        view_dims[1] = -1
+        return torch.arange(size[1]).view(*view_dims).int().repeat(size[0], 1, *size[2:])
+
+    def update(self, force: bool = False) -> bool:
+        raise NotImplementedError("CDF tables / rANS coding are not part of this round (SURVEY.md 8f-2/3)")
+
+
+class GaussianConditional(EntropyModel):
+    def __init__(self, scale_table: Optional[Union[List, Tuple]], *args: Any, scale_bound: float = 0.11,
+                 tail_mass: float = 1e-9, **kwargs: Any):
+        super().__init__(*args, **kwargs)
+        if not isinstance(scale_table, (type(None), list, tuple)):
+            raise ValueError(f'Invalid type for scale_table "{type(scale_table)}"')
+        if isinstance(scale_table, (list, tuple)) and len(scale_table) < 1:
+            raise ValueError(f'Invalid scale_table length "{len(scale_table)}"')
+        if scale_table and (list(scale_table) != sorted(scale_table) or any(s <= 0 for s in scale_table)):
+            raise ValueError(f'Invalid scale_table "({scale_table})"')
+        self.tail_mass = float(tail_mass)
+        if scale_bound is None and scale_table:
+            scale_bound = scale_table[0]
+        if scale_bound is None or scale_bound <= 0:
+            raise ValueError("Invalid parameters")
+        self.lower_bound_scale = LowerBound(scale_bound)
+        self.register_buffer("scale_table",
+                             torch.Tensor(tuple(float(s) for s in scale_table)) if scale_table else torch.Tensor())
+        self.register_buffer("scale_bound", torch.Tensor([float(scale_bound)]))
+
+    @staticmethod
+    def _prepare_scale_table(scale_table):
+        return torch.Tensor(tuple(float(s) for s in scale_table))
+
+    def forward(self, inputs: torch.Tensor, scales: torch.Tensor, means: Optional[torch.Tensor] = None,
+                training: Optional[bool] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        if training is None:
+            training = self.training
+        if scales.shape != inputs.shape or (means is not None and means.shape != inputs.shape):
+            raise ValueError("inputs, scales and means must have the same shape")
+        noise = _draw_noise(inputs) if training else None
+        sb = float(self.lower_bound_scale.bound.item())
+        return GaussianFn.apply(inputs, scales, means, noise, Q_NOISE if training else Q_DEQUANTIZE, sb,
+                                self._lik_bound())
+
+    def build_indexes(self, scales: torch.Tensor) -> torch.Tensor:
+        scales = torch.clamp_min(scales, float(self.lower_bound_scale.bound.item()))
+        indexes = scales.new_full(scales.size(), len(self.scale_table) - 1).int()
+        for s in self.scale_table[:-1]:
+            indexes -= (scales <= s).int()
+        return indexes
+
+    def update_scale_table(self, scale_table, force=False):
+        raise NotImplementedError("CDF tables / rANS coding are not part of this round (SURVEY.md 8f-2/3)")

@@ -1,0 +1,13 @@
+"""Model zoo (reference: compressai/zoo/__init__.py:30-56)."""
+from .image import bmshj2018_factorized, bmshj2018_hyperprior, cfgs, mbt2018, mbt2018_mean, model_architectures
+
+image_models = {
+    "bmshj2018-factorized": bmshj2018_factorized,
+    "bmshj2018-hyperprior": bmshj2018_hyperprior,
+    "mbt2018-mean": mbt2018_mean,
+    "mbt2018": mbt2018,
+}
+
+models = dict(image_models)
+
+__all__ = ["image_models", "models", "cfgs", "model_architectures"]

@@ -1,0 +1,98 @@
+// Shared helpers for the libcai HIP sources (gfx950 / CDNA4 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "cai.h"
+
+namespace cai {
+
+// ---------------------------------------------------------------------------
+// error handling: thread-local message, no global mutable state
+// ---------------------------------------------------------------------------
+void set_error(const char* fmt, ...);
+
+#define CAI_CHECK_ARG(cond, ...)            \
+    do {                                    \
+        if (!(cond)) {                      \
+            ::cai::set_error(__VA_ARGS__);  \
+            return CAI_EINVAL;              \
+        }                                   \
+    } while (0)
+
+#define CAI_LAUNCH_CHECK(what)                                                          \
+    do {                                                                                \
+        hipError_t e_ = hipGetLastError();                                              \
+        if (e_ != hipSuccess) {                                                         \
+            ::cai::set_error("%s: launch failed: %s", what, hipGetErrorString(e_));     \
+            return CAI_EDEVICE;                                                         \
+        }                                                                               \
+    } while (0)
+
+static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---------------------------------------------------------------------------
+// vector types
+// ---------------------------------------------------------------------------
+typedef __bf16 bf16;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+// native 16-byte vector (HIP's uint4 is a struct: selects on it lower through scratch)
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float to_f32(float v) { return v; }
+__device__ __forceinline__ float to_f32(bf16 v) { return (float)v; }
+template <typename T> __device__ __forceinline__ T from_f32(float v);
+template <> __device__ __forceinline__ float from_f32<float>(float v) { return v; }
+template <> __device__ __forceinline__ bf16 from_f32<bf16>(float v) { return (bf16)v; }
+
+// generic scalar load/store by runtime dtype code
+__device__ __forceinline__ float ld_any(const void* p, int dtype, int64_t i) {
+    return dtype == CAI_BF16 ? (float)reinterpret_cast<const bf16*>(p)[i] : reinterpret_cast<const float*>(p)[i];
+}
+__device__ __forceinline__ void st_any(void* p, int dtype, int64_t i, float v) {
+    if (dtype == CAI_BF16)
+        reinterpret_cast<bf16*>(p)[i] = (bf16)v;
+    else
+        reinterpret_cast<float*>(p)[i] = v;
+}
+
+static inline int dtype_size(int dtype) { return dtype == CAI_BF16 ? 2 : 4; }
+
+// ---------------------------------------------------------------------------
+// wave / block reductions (wave = 64 lanes)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// block of NT threads -> value valid in thread 0
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* smem) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) smem[w] = v;
+    __syncthreads();
+    float r = 0.f;
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 0; i < NT / 64; ++i) r += smem[i];
+    }
+    __syncthreads();
+    return r;
+}
+
+}  // namespace cai

@@ -1,0 +1,975 @@
+// Convolution / transposed convolution as implicit GEMM on CDNA4 MFMA.
+//
+// Replaces the nn.Conv2d / nn.ConvTranspose2d modules built by
+// compressai/models/utils.py:128-146 (conv k5 s2 p2, deconv k5 s2 p2 op1,
+// conv k3 s1 p1) and the 1x1 / masked 5x5 convs of google.py:467-478.
+//
+// One kernel family, two row-addressing modes:
+//   gather  : out[b,j,i]  = sum_{kh,kw,c} in[b, j*s-p+kh, i*s-p+kw, c] * W[n,kh,kw,c]
+//             (Conv2d forward, ConvTranspose2d input-gradient)
+//   phase   : the transposed (adjoint) op, decomposed by output phase
+//             (py,px) = (oy mod s, ox mod s) so every output row of a phase
+//             has the same tap list: taps kh = kh0 + s*a, input row
+//             iy = j + dy0 - a.  (Conv2d input-gradient, ConvTranspose2d forward)
+// Operands: activations pixel-major (NHWC) bf16 or fp32, weights pre-packed
+// per phase as [n][tap][c] rows (K contiguous).  A tile = BM output pixels x
+// 128 bytes of K, B tile = BN output channels x 128 bytes of K, both staged
+// global -> registers -> LDS (XOR-swizzled 16-byte slots, double buffered,
+// one barrier per K-tile).  MFMA: v_mfma_f32_16x16x32_bf16, or four
+// v_mfma_f32_16x16x4_f32 per 16-byte slot for the exact-fp32 parity path.
+// Epilogue: bias + ReLU/LeakyReLU or a gradient mask from an aux tensor,
+// staged through LDS as fp32 and stored 16 bytes per lane.
+//
+// wgrad: dW[n][tap][q] = sum_m G[m][n] * X[pix(m,tap)][q] with the pixel
+// dimension as K, split over workgroups (fp32 partial slabs + a fixed-order
+// reduce: deterministic).  Both operands arrive [pixel][channel]; bf16 MFMA
+// fragments are read with ds_read_b64_tr_b16 (hardware transpose).
+#include "common.hpp"
+
+#include <algorithm>
+#include <vector>
+
+namespace cai {
+
+template <typename T> struct OpT;
+template <> struct OpT<bf16> { static constexpr int VEC = 8; };
+template <> struct OpT<float> { static constexpr int VEC = 4; };
+
+constexpr int NT = 256;
+
+struct PhaseDesc {
+    int oy0, ox0;     // output offset of this phase
+    int OHg, OWg;     // GEMM row grid of this phase
+    int ntaps, ntx;   // taps, taps per kernel row
+    int dy0, dx0;     // input offset of tap 0
+    int K;            // ntaps * Cin_pad
+    int pad_;
+    int64_t w_off;    // element offset of this phase's packed weights
+};
+
+struct ConvArgs {
+    const void* x;
+    int B, IH, IW, x_ld, Cin_pad, in_abs;
+    const void* w;
+    int Kp, Npad;
+    int nphase;
+    int tap_sy, tap_sx;
+    int row_stride, out_step;
+    int out_h, out_w, Cout;
+    void* y;
+    int y_dtype, y_vec;
+    int64_t ysb, ysc, ysy, ysx;
+    const float* bias;
+    int act;
+    float act_param;
+    const void* aux;
+    int aux_ld, mask_mode;
+    float mask_param;
+    PhaseDesc ph[4];
+};
+
+__device__ __forceinline__ u32x4 abs_chunk(u32x4 v, int elem_bytes) {
+    const unsigned m = elem_bytes == 2 ? 0x7FFF7FFFu : 0x7FFFFFFFu;
+    v.x &= m; v.y &= m; v.z &= m; v.w &= m;
+    return v;
+}
+
+template <typename T>
+__device__ __forceinline__ u32x4 sq_chunk(u32x4 v);
+template <> __device__ __forceinline__ u32x4 sq_chunk<bf16>(u32x4 v) {
+    bf16x8 h = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const float f = (float)h[e];
+        h[e] = (bf16)(f * f);
+    }
+    return __builtin_bit_cast(u32x4, h);
+}
+template <> __device__ __forceinline__ u32x4 sq_chunk<float>(u32x4 v) {
+    f32x4 h = __builtin_bit_cast(f32x4, v);
+    h = h * h;
+    return __builtin_bit_cast(u32x4, h);
+}
+
+template <typename T>
+__device__ __forceinline__ f32x4 mma16(u32x4 a, u32x4 b, f32x4 c);
+template <> __device__ __forceinline__ f32x4 mma16<bf16>(u32x4 a, u32x4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                   0, 0);
+}
+template <> __device__ __forceinline__ f32x4 mma16<float>(u32x4 a, u32x4 b, f32x4 c) {
+    // the four k-values of a 16-byte slot go to four MFMAs; A and B use the
+    // same permutation of k so the sum is unchanged
+    const f32x4 av = __builtin_bit_cast(f32x4, a), bv = __builtin_bit_cast(f32x4, b);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], bv[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1], bv[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(av[2], bv[2], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(av[3], bv[3], c, 0, 0, 0);
+    return c;
+}
+
+__device__ __forceinline__ int swz(int row, int slot) { return slot ^ ((row >> 1) & 7); }
+
+__device__ __forceinline__ float apply_act(float v, int act, float prm) {
+    if (act == CAI_ACT_RELU) return v > 0.f ? v : 0.f;
+    if (act == CAI_ACT_LEAKY) return v > 0.f ? v : v * prm;
+    return v;
+}
+__device__ __forceinline__ float mask_val(int mode, float a, float prm) {
+    if (mode == CAI_MASK_POS) return a > 0.f ? 1.f : 0.f;
+    if (mode == CAI_MASK_LEAKY) return a > 0.f ? 1.f : prm;
+    if (mode == CAI_MASK_SIGN) return a > 0.f ? 1.f : (a < 0.f ? -1.f : 0.f);
+    return 1.f;
+}
+
+template <int BM_, int BN_, int WM_, int WN_>
+struct Cfg {
+    static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+};
+
+template <typename T, typename C>
+struct ConvSmem {
+    static constexpr int PIPE = 2 * (C::BM + C::BN) * 128;
+    static constexpr int EPI_STRIDE = C::BN + 4;
+    static constexpr int EPI = C::BM * EPI_STRIDE * 4;
+    static constexpr int BYTES = PIPE > EPI ? PIPE : EPI;
+};
+
+template <typename T>
+using gptr = const T __attribute__((address_space(1)))*;
+template <typename T>
+__device__ __forceinline__ gptr<T> to_global(const void* p) {
+    return (gptr<T>)(reinterpret_cast<uintptr_t>(p));
+}
+
+template <int N>
+struct U4 {
+    u32x4 v[N];
+};
+
+template <typename T, typename C>
+__global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(const ConvArgs a) {
+    constexpr int BM = C::BM, BN = C::BN, WM = C::WM, WN = C::WN;
+    constexpr int VEC = OpT<T>::VEC;
+    constexpr int BK = 128 / (int)sizeof(T);
+    constexpr int A_CH = BM * 8 / NT;
+    constexpr int B_CH = (BN * 8 + NT - 1) / NT;
+    constexpr int WTM = BM / WM, WTN = BN / WN;
+    constexpr int TM = WTM / 16, TN = WTN / 16;
+    static_assert(BM % 32 == 0 && WM * WN == 4 && WTM % 16 == 0 && WTN % 16 == 0, "bad tile");
+    using SM = ConvSmem<T, C>;
+    __shared__ __attribute__((aligned(16))) char smem[SM::BYTES];
+
+    // select the phase descriptor with uniform branches (a dynamic index into
+    // the by-value kernarg struct would be copied to scratch)
+    const int z = blockIdx.z;
+    const PhaseDesc P = z == 0 ? a.ph[0] : (z == 1 ? a.ph[1] : (z == 2 ? a.ph[2] : a.ph[3]));
+    const int plane = P.OHg * P.OWg;
+    const int Mph = a.B * plane;
+    const int m0 = blockIdx.x * BM;
+    if (m0 >= Mph) return;
+    const int n0 = blockIdx.y * BN;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    const int slot = tid & 7;
+
+    // ---- per-row gather state of this thread's A chunks (rows i*32 + tid/8) ----
+    int rbase[A_CH], ry[A_CH], rx[A_CH];
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+        const int m = m0 + i * (NT / 8) + (tid >> 3);
+        if (m < Mph) {
+            const int b = m / plane;
+            const int r = m - b * plane;
+            const int j = r / P.OWg;
+            rbase[i] = b * a.IH;
+            ry[i] = j * a.row_stride;
+            rx[i] = (r - j * P.OWg) * a.row_stride;
+        } else {
+            rbase[i] = 0;
+            ry[i] = -(1 << 28);   // forces the bounds test to fail
+            rx[i] = 0;
+        }
+    }
+    const gptr<T> X = to_global<T>(a.x);
+    // B chunks: row = id/8 of the tile, slot = id%8 == tid%8 (NT multiple of 8)
+    const gptr<T> W = to_global<T>(a.w) + P.w_off + slot * VEC;
+    int woff[B_CH];
+    bool wok[B_CH];
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+        const int row = (i * NT + tid) >> 3;
+        wok[i] = row < BN && n0 + row < a.Npad;
+        woff[i] = wok[i] ? (n0 + row) * a.Kp : 0;
+    }
+    const int nk = (P.K + BK - 1) / BK;
+    const u32x4 zero = u32x4{0u, 0u, 0u, 0u};
+    U4<A_CH> ra;
+    U4<B_CH> rw;
+
+#define CONV_LOAD_TILE(KT)                                                                                   \
+    {                                                                                                        \
+        const int k_ = (KT) * BK + slot * VEC;                                                               \
+        const int t_ = k_ / a.Cin_pad;                                                                       \
+        const int ci_ = k_ - t_ * a.Cin_pad;                                                                 \
+        const int ty_ = t_ / P.ntx;                                                                          \
+        int dy_ = P.dy0 + a.tap_sy * ty_;                                                                    \
+        const int dx_ = P.dx0 + a.tap_sx * (t_ - ty_ * P.ntx);                                               \
+        if (t_ >= P.ntaps) dy_ = -(1 << 28);                                                                 \
+        _Pragma("unroll") for (int i = 0; i < A_CH; ++i) {                                                   \
+            const int iy = ry[i] + dy_, ix = rx[i] + dx_;                                                    \
+            const bool ok = (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW;                 \
+            const int64_t off = ok ? ((int64_t)(rbase[i] + iy) * a.IW + ix) * a.x_ld + ci_ : 0;             \
+            u32x4 v = *reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(X + off);            \
+            if (a.in_abs) v = abs_chunk(v, sizeof(T));                                                       \
+            ra.v[i] = ok ? v : zero;                                                                         \
+        }                                                                                                    \
+        _Pragma("unroll") for (int i = 0; i < B_CH; ++i) {                                                   \
+            const u32x4 v = *reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(               \
+                W + woff[i] + (KT) * BK);                                                                    \
+            rw.v[i] = wok[i] ? v : zero;                                                                     \
+        }                                                                                                    \
+    }
+
+#define CONV_STORE_TILE(BUF)                                                                                 \
+    {                                                                                                        \
+        char* As_ = smem + (BUF) * (BM + BN) * 128;                                                          \
+        char* Bs_ = As_ + BM * 128;                                                                          \
+        _Pragma("unroll") for (int i = 0; i < A_CH; ++i) {                                                   \
+            const int row = i * (NT / 8) + (tid >> 3);                                                       \
+            *reinterpret_cast<u32x4*>(As_ + row * 128 + swz(row, slot) * 16) = ra.v[i];                      \
+        }                                                                                                    \
+        _Pragma("unroll") for (int i = 0; i < B_CH; ++i) {                                                   \
+            const int row = (i * NT + tid) >> 3;                                                             \
+            if (row < BN) *reinterpret_cast<u32x4*>(Bs_ + row * 128 + swz(row, slot) * 16) = rw.v[i];        \
+        }                                                                                                    \
+    }
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    CONV_LOAD_TILE(0);
+    CONV_STORE_TILE(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const bool more = kt + 1 < nk;
+        if (more) CONV_LOAD_TILE(kt + 1);
+        {
+            const char* As = smem + (kt & 1) * (BM + BN) * 128;
+            const char* Bs = As + BM * 128;
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const int ls = c * 4 + (lane >> 4);
+                u32x4 fa[TM], fb[TN];
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm) {
+                    const int row = wm * WTM + tm * 16 + (lane & 15);
+                    fa[tm] = *reinterpret_cast<const u32x4*>(As + row * 128 + swz(row, ls) * 16);
+                }
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) {
+                    const int row = wn * WTN + tn * 16 + (lane & 15);
+                    fb[tn] = *reinterpret_cast<const u32x4*>(Bs + row * 128 + swz(row, ls) * 16);
+                }
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mma16<T>(fa[tm], fb[tn], acc[tm][tn]);
+            }
+        }
+        if (more) CONV_STORE_TILE((kt + 1) & 1);
+        __syncthreads();
+    }
+#undef CONV_LOAD_TILE
+#undef CONV_STORE_TILE
+
+    // ---- epilogue: acc (+bias, act) -> LDS fp32 [BM][BN+4] ----
+    float* E = reinterpret_cast<float*>(smem);
+    constexpr int ES = SM::EPI_STRIDE;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int col = wn * WTN + tn * 16 + (lane & 15);
+            const int n = n0 + col;
+            const float bv = (a.bias && n < a.Cout) ? a.bias[n] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = wm * WTM + tm * 16 + (lane >> 4) * 4 + r;
+                E[row * ES + col] = apply_act(acc[tm][tn][r] + bv, a.act, a.act_param);
+            }
+        }
+    __syncthreads();
+
+    const T* AUX = reinterpret_cast<const T*>(a.aux);
+    if (a.y_vec) {
+        const bool obf = a.y_dtype == CAI_BF16;
+        const int VO = obf ? 8 : 4;
+        const int cpr = BN / VO;
+        for (int id = tid; id < BM * cpr; id += NT) {
+            const int row = id / cpr, cc = id - (id / cpr) * cpr;
+            const int m = m0 + row, n = n0 + cc * VO;
+            if (m >= Mph || n >= a.Cout) continue;
+            const int b = m / plane;
+            const int r = m - b * plane;
+            const int j = r / P.OWg;
+            const int oy = P.oy0 + a.out_step * j, ox = P.ox0 + a.out_step * (r - j * P.OWg);
+            const f32x4 lo = *reinterpret_cast<const f32x4*>(E + row * ES + cc * VO);
+            f32x4 hi = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (obf) hi = *reinterpret_cast<const f32x4*>(E + row * ES + cc * VO + 4);
+            float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            if (a.mask_mode) {
+                const int64_t pa = (((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.aux_ld + n;
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                    if (e < VO) v[e] *= mask_val(a.mask_mode, to_f32(AUX[pa + e]), a.mask_param);
+            }
+            const int64_t off = (int64_t)b * a.ysb + (int64_t)oy * a.ysy + (int64_t)ox * a.ysx + n;
+            if (obf) {
+                bf16x8 h;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) h[e] = (bf16)v[e];
+                *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(a.y) + off) = h;
+            } else {
+                *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.y) + off) = f32x4{v[0], v[1], v[2], v[3]};
+            }
+        }
+    } else {
+        for (int id = tid; id < BM * BN; id += NT) {
+            const int col = id / BM, row = id - (id / BM) * BM;
+            const int m = m0 + row, n = n0 + col;
+            if (m >= Mph || n >= a.Cout) continue;
+            const int b = m / plane;
+            const int r = m - b * plane;
+            const int j = r / P.OWg;
+            const int oy = P.oy0 + a.out_step * j, ox = P.ox0 + a.out_step * (r - j * P.OWg);
+            float v = E[row * ES + col];
+            if (a.mask_mode) {
+                const int64_t pa = (((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.aux_ld + n;
+                v *= mask_val(a.mask_mode, to_f32(AUX[pa]), a.mask_param);
+            }
+            st_any(a.y, a.y_dtype, (int64_t)b * a.ysb + (int64_t)n * a.ysc + (int64_t)oy * a.ysy + (int64_t)ox * a.ysx,
+                   v);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// weight packing: source [D0][D1][k][k] fp32 -> packed[ph][n][tap][c] (T)
+// ---------------------------------------------------------------------------
+struct PackArgs {
+    const float* w;
+    const float* mask;
+    void* out;
+    int D1, k;
+    int n_is_d0;
+    int Nreal, Creal, Cpad, Npad, Kp;
+    int nphase;
+    int ntaps[4], ntx[4], kh0[4], kw0[4], step;   // step = tap stride inside the kernel (s for phase, 1 for gather)
+    int64_t off[4];
+};
+
+template <typename T>
+__global__ void pack_weight_kernel(const PackArgs a) {
+    const int ph = blockIdx.z;
+    const int64_t total = (int64_t)a.Npad * a.Kp;
+    T* out = reinterpret_cast<T*>(a.out) + a.off[ph];
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int n = (int)(i / a.Kp);
+        const int kk = (int)(i - (int64_t)n * a.Kp);
+        const int t = kk / a.Cpad, c = kk - t * a.Cpad;
+        float v = 0.f;
+        if (n < a.Nreal && c < a.Creal && t < a.ntaps[ph]) {
+            const int kh = a.kh0[ph] + a.step * (t / a.ntx[ph]);
+            const int kw = a.kw0[ph] + a.step * (t % a.ntx[ph]);
+            const int d0 = a.n_is_d0 ? n : c, d1 = a.n_is_d0 ? c : n;
+            const int64_t src = (((int64_t)d0 * a.D1 + d1) * a.k + kh) * a.k + kw;
+            v = a.w[src];
+            if (a.mask) v *= a.mask[src];
+        }
+        out[i] = from_f32<T>(v);
+    }
+}
+
+template <typename T>
+__global__ void pack_nchw_kernel(const float* __restrict__ x, int B, int C, int HW, T* __restrict__ out, int ld) {
+    const int64_t total = (int64_t)B * HW * ld;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t p = i / ld;
+        const int c = (int)(i - p * ld);
+        const int64_t b = p / HW, s = p - b * HW;
+        out[i] = from_f32<T>(c < C ? x[(b * C + c) * HW + s] : 0.f);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// wgrad
+// ---------------------------------------------------------------------------
+struct WgradArgs {
+    const void* g;
+    int g_ld, Ng;
+    const void* x;
+    int x_ld, Cq_pad, in_abs, in_sq;
+    int B, Hg, Wg, Hx, Wx;
+    int k, s, p;
+    int ncols;
+    int64_t M;
+    int64_t split_len;
+    float* ws;
+};
+
+// LDS byte offset of 16-byte slot `slot` of row `row` in a [32][256 B] bf16 image
+// read by ds_read_b64_tr_b16 (rows 8g+q of a half-wave land on distinct slots)
+__device__ __forceinline__ int trswz(int row, int slot) {
+    return row * 256 + ((slot ^ (((row & 3) << 1) | (((row >> 3) & 1) << 3))) << 4);
+}
+
+typedef short __attribute__((address_space(3))) * lds_s16_ptr;
+
+__device__ __forceinline__ s16x4 ds_tr16(const char* base, int byte_off) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(base + byte_off));
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT, 2) void wgrad_kernel(const WgradArgs a) {
+    constexpr int VEC = OpT<T>::VEC;
+    constexpr int BKP = 32;                       // pixels per K-step
+    constexpr int ROWB = 128 * (int)sizeof(T);    // bytes per LDS row (128 channels)
+    constexpr int CPR = ROWB / 16;                // 16-byte chunks per row
+    constexpr int CH = BKP * CPR / NT;            // chunks per thread per operand
+    constexpr int OPB = BKP * ROWB;               // bytes per operand tile
+    __shared__ __attribute__((aligned(16))) char smem[4 * OPB];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+    const int c0 = blockIdx.x * 128;   // column tile (tap, q)
+    const int r0 = blockIdx.y * 128;   // row tile (G channel)
+    const int64_t mbeg = (int64_t)blockIdx.z * a.split_len;
+    int64_t mend = mbeg + a.split_len;
+    if (mend > a.M) mend = a.M;
+    if (mbeg >= mend) {
+        // empty split: still write zeros so the reduce reads defined data
+        for (int id = tid; id < 128 * 128; id += NT) {
+            const int rr = r0 + id / 128, cc = c0 + (id & 127);
+            if (rr < a.Ng && cc < a.ncols) a.ws[((int64_t)blockIdx.z * a.Ng + rr) * a.ncols + cc] = 0.f;
+        }
+        return;
+    }
+
+    // this thread's fixed chunk column
+    const int cc = tid % CPR;
+    const int gcol = r0 + cc * VEC;                 // G channel of the chunk
+    const int xcol = c0 + cc * VEC;                 // X (tap, q) column of the chunk
+    const int xt = xcol / a.Cq_pad, xq = xcol - xt * a.Cq_pad;
+    const int xkh = xt / a.k, xkw = xt - xkh * a.k;
+    const bool xvalid = xcol < a.ncols;
+    const bool gvalid = gcol < a.Ng;
+    const int plane = a.Hg * a.Wg;
+
+    const T* G = reinterpret_cast<const T*>(a.g);
+    const T* X = reinterpret_cast<const T*>(a.x);
+    u32x4 rg[CH], rx[CH];
+    const u32x4 zero = u32x4{0u, 0u, 0u, 0u};
+
+    auto load = [&](int64_t mb) {
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+            const int row = i * (NT / CPR) + tid / CPR;
+            const int64_t m = mb + row;
+            rg[i] = zero;
+            rx[i] = zero;
+            if (m < mend) {
+                if (gvalid) rg[i] = *reinterpret_cast<const u32x4*>(G + m * a.g_ld + gcol);
+                if (xvalid) {
+                    const int b = (int)(m / plane);
+                    const int r = (int)(m - (int64_t)b * plane);
+                    const int j = r / a.Wg;
+                    const int iy = j * a.s - a.p + xkh, ix = (r - j * a.Wg) * a.s - a.p + xkw;
+                    if ((unsigned)iy < (unsigned)a.Hx && (unsigned)ix < (unsigned)a.Wx) {
+                        u32x4 v = *reinterpret_cast<const u32x4*>(X + (((int64_t)b * a.Hx + iy) * a.Wx + ix) * a.x_ld + xq);
+                        if (a.in_abs) v = abs_chunk(v, sizeof(T));
+                        if (a.in_sq) v = sq_chunk<T>(v);
+                        rx[i] = v;
+                    }
+                }
+            }
+        }
+    };
+    auto store = [&](int buf) {
+        char* Gs = smem + buf * 2 * OPB;
+        char* Xs = Gs + OPB;
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+            const int row = i * (NT / CPR) + tid / CPR;
+            int off;
+            if constexpr (sizeof(T) == 2)
+                off = trswz(row, cc);
+            else
+                off = row * ROWB + cc * 16;
+            *reinterpret_cast<u32x4*>(Gs + off) = rg[i];
+            *reinterpret_cast<u32x4*>(Xs + off) = rx[i];
+        }
+    };
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto compute = [&](int buf) {
+        const char* Gs = smem + buf * 2 * OPB;
+        const char* Xs = Gs + OPB;
+        if constexpr (sizeof(T) == 2) {
+            const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p4 = i16 & 3;
+            u32x4 fa[4], fb[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int colA = wm * 64 + t * 16 + 4 * p4;   // element column (G channel within tile)
+                const int colB = wn * 64 + t * 16 + 4 * p4;
+                s16x4 a0 = ds_tr16(Gs, trswz(8 * g + q, colA >> 3) + ((colA & 7) << 1));
+                s16x4 a1 = ds_tr16(Gs, trswz(8 * g + 4 + q, colA >> 3) + ((colA & 7) << 1));
+                s16x4 b0 = ds_tr16(Xs, trswz(8 * g + q, colB >> 3) + ((colB & 7) << 1));
+                s16x4 b1 = ds_tr16(Xs, trswz(8 * g + 4 + q, colB >> 3) + ((colB & 7) << 1));
+                s16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+                s16x8 bv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+                fa[t] = __builtin_bit_cast(u32x4, av);
+                fb[t] = __builtin_bit_cast(u32x4, bv);
+            }
+#pragma unroll
+            for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < 4; ++tn) acc[tm][tn] = mma16<bf16>(fa[tm], fb[tn], acc[tm][tn]);
+        } else {
+            const float* Gf = reinterpret_cast<const float*>(Gs);
+            const float* Xf = reinterpret_cast<const float*>(Xs);
+#pragma unroll
+            for (int ks = 0; ks < BKP / 4; ++ks) {
+                const int row = ks * 4 + (lane >> 4);
+                float fa[4], fb[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    fa[t] = Gf[row * 128 + wm * 64 + t * 16 + (lane & 15)];
+                    fb[t] = Xf[row * 128 + wn * 64 + t * 16 + (lane & 15)];
+                }
+#pragma unroll
+                for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+                    for (int tn = 0; tn < 4; ++tn)
+                        acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[tm], fb[tn], acc[tm][tn], 0, 0, 0);
+            }
+        }
+    };
+
+    const int nsteps = (int)((mend - mbeg + BKP - 1) / BKP);
+    load(mbeg);
+    store(0);
+    __syncthreads();
+    for (int st = 0; st < nsteps; ++st) {
+        if (st + 1 < nsteps) load(mbeg + (int64_t)(st + 1) * BKP);
+        compute(st & 1);
+        if (st + 1 < nsteps) store((st + 1) & 1);
+        __syncthreads();
+    }
+
+    float* out = a.ws + (int64_t)blockIdx.z * a.Ng * a.ncols;
+#pragma unroll
+    for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < 4; ++tn) {
+            const int col = c0 + wn * 64 + tn * 16 + (lane & 15);
+            if (col >= a.ncols) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = r0 + wm * 64 + tm * 16 + (lane >> 4) * 4 + r;
+                if (row < a.Ng) out[(int64_t)row * a.ncols + col] = acc[tm][tn][r];
+            }
+        }
+}
+
+// dw[n][q][kh][kw] = sum_s ws[s][n][(kh*k+kw)*Cq_pad + q]
+__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int S, int Ng, int ncols, int Cq, int Cq_pad, int k,
+                                    float* __restrict__ dw) {
+    const int64_t total = (int64_t)Ng * Cq * k * k;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int kk = k * k;
+        const int64_t nq = i / kk;
+        const int t = (int)(i - nq * kk);
+        const int n = (int)(nq / Cq), q = (int)(nq - (int64_t)n * Cq);
+        const int64_t col = (int64_t)t * Cq_pad + q;
+        float s = 0.f;
+        for (int sp = 0; sp < S; ++sp) s += ws[((int64_t)sp * Ng + n) * ncols + col];
+        dw[i] = s;
+    }
+}
+
+// column sums: stage 1 partials[chunk][c], stage 2 fixed-order sum
+template <typename T>
+__global__ void colsum_stage1(const T* __restrict__ g, int64_t npix, int C, int ld, int64_t chunk,
+                              float* __restrict__ part) {
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int r = threadIdx.x >> 6;   // 4 row lanes
+    __shared__ float red[4][64];
+    const int64_t pb = blockIdx.y * chunk;
+    int64_t pe = pb + chunk;
+    if (pe > npix) pe = npix;
+    float s = 0.f;
+    if (c < C)
+        for (int64_t p = pb + r; p < pe; p += 4) s += to_f32(g[p * ld + c]);
+    red[r][threadIdx.x & 63] = s;
+    __syncthreads();
+    if (r == 0 && c < C) part[(int64_t)blockIdx.y * C + c] = red[0][threadIdx.x] + red[1][threadIdx.x] +
+                                                             red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+__global__ void colsum_stage2(const float* __restrict__ part, int nchunk, int C, float* __restrict__ out) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    float s = 0.f;
+    for (int i = 0; i < nchunk; ++i) s += part[(int64_t)i * C + c];
+    out[c] = s;
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+static int round_up(int v, int m) { return (v + m - 1) / m * m; }
+
+struct Plan {
+    bool phase;      // phase (transposed) mode vs gather mode
+    int nphase;
+    int kin_c;       // channels of the kernel input (K channels)
+    int kout_c;      // channels of the kernel output (N)
+    int in_h, in_w, out_h, out_w;
+    int Cin_pad, Npad, Kp;
+    int ntaps[4], ntx[4], kh0[4], kw0[4], dy0[4], dx0[4], oy0[4], ox0[4], OHg[4], OWg[4];
+    int step;
+};
+
+static int check_geom(const cai_conv_geom* g) {
+    CAI_CHECK_ARG(g, "conv: null geometry");
+    CAI_CHECK_ARG(g->batch > 0 && g->in_c > 0 && g->out_c > 0 && g->in_h > 0 && g->in_w > 0, "conv: bad sizes");
+    CAI_CHECK_ARG(g->kernel >= 1 && g->kernel <= 7 && g->stride >= 1 && g->stride <= 2 && g->pad >= 0,
+                  "conv: unsupported kernel %d stride %d pad %d", g->kernel, g->stride, g->pad);
+    int oh, ow;
+    if (g->transposed) {
+        oh = (g->in_h - 1) * g->stride - 2 * g->pad + g->kernel + g->output_padding;
+        ow = (g->in_w - 1) * g->stride - 2 * g->pad + g->kernel + g->output_padding;
+    } else {
+        CAI_CHECK_ARG(g->output_padding == 0, "conv: output_padding only for transposed");
+        oh = (g->in_h + 2 * g->pad - g->kernel) / g->stride + 1;
+        ow = (g->in_w + 2 * g->pad - g->kernel) / g->stride + 1;
+    }
+    CAI_CHECK_ARG(oh == g->out_h && ow == g->out_w, "conv: output size %dx%d != expected %dx%d", g->out_h, g->out_w, oh,
+                  ow);
+    return CAI_OK;
+}
+
+// direction 0 = forward, 1 = input gradient
+static Plan make_plan(const cai_conv_geom* g, int dtype, int direction) {
+    Plan P{};
+    const int VEC = dtype == CAI_BF16 ? 8 : 4;
+    const int BK = 128 / dtype_size(dtype);
+    const int k = g->kernel, s = g->stride, p = g->pad;
+    P.phase = (g->transposed != direction);
+    if (direction == 0) {
+        P.kin_c = g->in_c; P.kout_c = g->out_c;
+        P.in_h = g->in_h; P.in_w = g->in_w; P.out_h = g->out_h; P.out_w = g->out_w;
+    } else {
+        P.kin_c = g->out_c; P.kout_c = g->in_c;
+        P.in_h = g->out_h; P.in_w = g->out_w; P.out_h = g->in_h; P.out_w = g->in_w;
+    }
+    P.Cin_pad = round_up(P.kin_c, VEC);
+    P.Npad = round_up(P.kout_c, 16);
+    int kmax = 0;
+    if (!P.phase) {
+        P.nphase = 1;
+        P.ntaps[0] = k * k; P.ntx[0] = k; P.kh0[0] = P.kw0[0] = 0;
+        P.dy0[0] = P.dx0[0] = -p; P.oy0[0] = P.ox0[0] = 0;
+        P.OHg[0] = P.out_h; P.OWg[0] = P.out_w;
+        P.step = 1;
+        kmax = k * k * P.Cin_pad;
+    } else {
+        P.nphase = s * s;
+        P.step = s;
+        for (int py = 0; py < s; ++py)
+            for (int px = 0; px < s; ++px) {
+                const int ph = py * s + px;
+                const int kh0 = ((py + p) % s + s) % s, kw0 = ((px + p) % s + s) % s;
+                const int na = kh0 < k ? (k - kh0 + s - 1) / s : 0;
+                const int nc = kw0 < k ? (k - kw0 + s - 1) / s : 0;
+                P.kh0[ph] = kh0; P.kw0[ph] = kw0;
+                P.ntaps[ph] = na * nc; P.ntx[ph] = nc > 0 ? nc : 1;
+                P.dy0[ph] = (py + p - kh0) / s; P.dx0[ph] = (px + p - kw0) / s;
+                P.oy0[ph] = py; P.ox0[ph] = px;
+                P.OHg[ph] = P.out_h > py ? (P.out_h - py + s - 1) / s : 0;
+                P.OWg[ph] = P.out_w > px ? (P.out_w - px + s - 1) / s : 0;
+                kmax = std::max(kmax, na * nc * P.Cin_pad);
+            }
+    }
+    P.Kp = round_up(std::max(kmax, 1), BK);
+    return P;
+}
+
+template <typename T, typename C>
+static void launch_conv(const ConvArgs& a, int mmax, hipStream_t st) {
+    dim3 grid((mmax + C::BM - 1) / C::BM, (a.Cout + C::BN - 1) / C::BN, a.nphase);
+    hipLaunchKernelGGL((conv_gemm_kernel<T, C>), grid, dim3(NT), 0, st, a);
+}
+
+using CfgL = Cfg<128, 128, 2, 2>;
+using CfgW = Cfg<64, 192, 1, 4>;
+using CfgM = Cfg<128, 64, 2, 2>;
+using CfgS = Cfg<256, 16, 4, 1>;
+
+template <typename T>
+static void dispatch_conv(const ConvArgs& a, int mmax, hipStream_t st) {
+    const int C = a.Cout;
+    if (C <= 16)
+        launch_conv<T, CfgS>(a, mmax, st);
+    else if (C <= 64)
+        launch_conv<T, CfgM>(a, mmax, st);
+    else if (C % 128 != 0 && (C % 192 == 0 || C % 192 > 128 || (C > 128 && C <= 192)))
+        launch_conv<T, CfgW>(a, mmax, st);
+    else
+        launch_conv<T, CfgL>(a, mmax, st);
+}
+
+static int run_conv(const cai_conv_geom* g, int dtype, int direction, const void* x, int x_ld, int in_abs,
+                    const void* w, const float* bias, int act, float act_param, void* y, int y_dtype, int64_t ysb,
+                    int64_t ysc, int64_t ysy, int64_t ysx, const void* aux, int aux_ld, int mask_mode,
+                    float mask_param, void* stream, const char* name) {
+    int rc = check_geom(g);
+    if (rc) return rc;
+    CAI_CHECK_ARG(dtype == CAI_BF16 || dtype == CAI_F32, "%s: bad dtype", name);
+    CAI_CHECK_ARG(x && w && y, "%s: null pointer", name);
+    const Plan P = make_plan(g, dtype, direction);
+    const int VEC = dtype == CAI_BF16 ? 8 : 4;
+    CAI_CHECK_ARG(x_ld >= P.Cin_pad && x_ld % VEC == 0, "%s: input ld %d must be >= %d and a multiple of %d", name,
+                  x_ld, P.Cin_pad, VEC);
+    CAI_CHECK_ARG(((uintptr_t)x & 15) == 0, "%s: input not 16-byte aligned", name);
+    CAI_CHECK_ARG(!mask_mode || (aux && aux_ld >= P.kout_c), "%s: mask needs aux", name);
+    ConvArgs a{};
+    a.x = x; a.B = g->batch; a.IH = P.in_h; a.IW = P.in_w; a.x_ld = x_ld; a.Cin_pad = P.Cin_pad; a.in_abs = in_abs;
+    a.w = w; a.Kp = P.Kp; a.Npad = P.Npad; a.nphase = P.nphase;
+    a.tap_sy = P.phase ? -1 : 1; a.tap_sx = a.tap_sy;
+    a.row_stride = P.phase ? 1 : g->stride;
+    a.out_step = P.phase ? g->stride : 1;
+    a.out_h = P.out_h; a.out_w = P.out_w; a.Cout = P.kout_c;
+    a.y = y; a.y_dtype = y_dtype; a.ysb = ysb; a.ysc = ysc; a.ysy = ysy; a.ysx = ysx;
+    const int VO = y_dtype == CAI_BF16 ? 8 : 4;
+    a.y_vec = (ysc == 1 && ysx % VO == 0 && ysy % VO == 0 && ysb % VO == 0 && P.kout_c % VO == 0 &&
+               ((uintptr_t)y & 15) == 0);
+    a.bias = bias; a.act = act; a.act_param = act_param;
+    a.aux = aux; a.aux_ld = aux_ld; a.mask_mode = mask_mode; a.mask_param = mask_param;
+    int mmax = 0;
+    for (int ph = 0; ph < P.nphase; ++ph) {
+        PhaseDesc& d = a.ph[ph];
+        d.oy0 = P.oy0[ph]; d.ox0 = P.ox0[ph]; d.OHg = P.OHg[ph]; d.OWg = P.OWg[ph];
+        d.ntaps = P.ntaps[ph]; d.ntx = P.ntx[ph]; d.dy0 = P.dy0[ph]; d.dx0 = P.dx0[ph];
+        d.K = P.ntaps[ph] * P.Cin_pad;
+        d.w_off = (int64_t)ph * P.Npad * P.Kp;
+        mmax = std::max(mmax, g->batch * d.OHg * d.OWg);
+    }
+    if (mmax == 0) return CAI_OK;
+    if (dtype == CAI_BF16)
+        dispatch_conv<bf16>(a, mmax, as_stream(stream));
+    else
+        dispatch_conv<float>(a, mmax, as_stream(stream));
+    CAI_LAUNCH_CHECK(name);
+    return CAI_OK;
+}
+
+struct WgradPlan {
+    int Ng, Cq, Cq_pad, ncols, S;
+    int64_t M, split_len;
+    int nchunk;
+    int64_t chunk;
+    size_t ws_slab, ws_col;
+};
+
+static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype) {
+    WgradPlan W{};
+    const int VEC = dtype == CAI_BF16 ? 8 : 4;
+    if (!g->transposed) {
+        W.Ng = g->out_c; W.Cq = g->in_c;
+        W.M = (int64_t)g->batch * g->out_h * g->out_w;
+    } else {
+        W.Ng = g->in_c; W.Cq = g->out_c;
+        W.M = (int64_t)g->batch * g->in_h * g->in_w;
+    }
+    W.Cq_pad = round_up(W.Cq, VEC);
+    W.ncols = g->kernel * g->kernel * W.Cq_pad;
+    const int tiles = ((W.ncols + 127) / 128) * ((W.Ng + 127) / 128);
+    int64_t S = std::max<int64_t>(1, 640 / tiles);
+    const int64_t maxS = std::max<int64_t>(1, W.M / (32 * 16));   // >= 16 K-steps per split
+    S = std::min(S, maxS);
+    W.split_len = ((W.M + S - 1) / S + 31) / 32 * 32;
+    W.S = (int)((W.M + W.split_len - 1) / W.split_len);
+    W.ws_slab = (size_t)W.S * W.Ng * W.ncols * sizeof(float);
+    // bias grad: columns of the module output gradient
+    const int64_t npix_out = (int64_t)g->batch * g->out_h * g->out_w;
+    W.nchunk = (int)std::min<int64_t>(256, (npix_out + 255) / 256);
+    W.chunk = (npix_out + W.nchunk - 1) / W.nchunk;
+    W.ws_col = (size_t)W.nchunk * g->out_c * sizeof(float);
+    return W;
+}
+
+template <typename T>
+static void launch_colsum(const void* g, int64_t npix, int C, int ld, int nchunk, int64_t chunk, float* part,
+                          float* out, hipStream_t st) {
+    hipLaunchKernelGGL(colsum_stage1<T>, dim3((C + 63) / 64, nchunk), dim3(256), 0, st, reinterpret_cast<const T*>(g),
+                       npix, C, ld, chunk, part);
+    hipLaunchKernelGGL(colsum_stage2, dim3((C + 255) / 256), dim3(256), 0, st, part, nchunk, C, out);
+}
+
+}  // namespace cai
+
+using namespace cai;
+
+extern "C" {
+
+size_t cai_conv_packed_weight_bytes(const cai_conv_geom* g, int dtype, int direction) {
+    if (check_geom(g)) return 0;
+    const Plan P = make_plan(g, dtype, direction);
+    return (size_t)P.nphase * P.Npad * P.Kp * dtype_size(dtype);
+}
+
+int cai_conv_pack_weight(const cai_conv_geom* g, int dtype, int direction, const float* w, const float* mask,
+                         void* packed, void* stream) {
+    int rc = check_geom(g);
+    if (rc) return rc;
+    CAI_CHECK_ARG(direction == 0 || direction == 1, "pack_weight: bad direction");
+    CAI_CHECK_ARG(w && packed, "pack_weight: null pointer");
+    const Plan P = make_plan(g, dtype, direction);
+    PackArgs a{};
+    a.w = w; a.mask = mask; a.out = packed;
+    a.k = g->kernel;
+    // torch layout: Conv2d [out][in][k][k], ConvTranspose2d [in][out][k][k]
+    a.D1 = g->transposed ? g->out_c : g->in_c;
+    a.n_is_d0 = (g->transposed == direction);
+    a.Nreal = P.kout_c; a.Creal = P.kin_c; a.Cpad = P.Cin_pad; a.Npad = P.Npad; a.Kp = P.Kp;
+    a.nphase = P.nphase; a.step = P.step;
+    for (int ph = 0; ph < P.nphase; ++ph) {
+        a.ntaps[ph] = P.ntaps[ph]; a.ntx[ph] = P.ntx[ph]; a.kh0[ph] = P.kh0[ph]; a.kw0[ph] = P.kw0[ph];
+        a.off[ph] = (int64_t)ph * P.Npad * P.Kp;
+    }
+    const int64_t total = (int64_t)P.Npad * P.Kp;
+    const int blocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
+    if (dtype == CAI_BF16)
+        hipLaunchKernelGGL(pack_weight_kernel<bf16>, dim3(blocks, 1, P.nphase), dim3(256), 0, as_stream(stream), a);
+    else
+        hipLaunchKernelGGL(pack_weight_kernel<float>, dim3(blocks, 1, P.nphase), dim3(256), 0, as_stream(stream), a);
+    CAI_LAUNCH_CHECK("pack_weight");
+    return CAI_OK;
+}
+
+int cai_pack_nchw(const float* x, int32_t B, int32_t C, int32_t H, int32_t W, int dtype, void* out, int32_t ld,
+                  void* stream) {
+    CAI_CHECK_ARG(x && out && B > 0 && C > 0 && H > 0 && W > 0 && ld >= C && ld % 8 == 0, "pack_nchw: bad arguments");
+    const int64_t total = (int64_t)B * H * W * ld;
+    const int blocks = (int)std::min<int64_t>(8192, (total + 255) / 256);
+    if (dtype == CAI_BF16)
+        hipLaunchKernelGGL(pack_nchw_kernel<bf16>, dim3(blocks), dim3(256), 0, as_stream(stream), x, B, C, H * W,
+                           reinterpret_cast<bf16*>(out), ld);
+    else
+        hipLaunchKernelGGL(pack_nchw_kernel<float>, dim3(blocks), dim3(256), 0, as_stream(stream), x, B, C, H * W,
+                           reinterpret_cast<float*>(out), ld);
+    CAI_LAUNCH_CHECK("pack_nchw");
+    return CAI_OK;
+}
+
+int cai_conv_fwd(const cai_conv_geom* g, int dtype, const void* x, int32_t x_ld, int32_t in_abs, const void* packed_w,
+                 const float* bias, int32_t act, float act_param, void* y, int y_dtype, int64_t ysb, int64_t ysc,
+                 int64_t ysy, int64_t ysx, void* stream) {
+    return run_conv(g, dtype, 0, x, x_ld, in_abs, packed_w, bias, act, act_param, y, y_dtype, ysb, ysc, ysy, ysx,
+                    nullptr, 0, CAI_MASK_NONE, 0.f, stream, "conv_fwd");
+}
+
+int cai_conv_dgrad(const cai_conv_geom* g, int dtype, const void* dy, int32_t dy_ld, const void* packed_wt, void* dx,
+                   int32_t dx_ld, int32_t mask_mode, float mask_param, const void* aux, int32_t aux_ld,
+                   void* stream) {
+    int rc = check_geom(g);
+    if (rc) return rc;
+    const int64_t ld = dx_ld;
+    return run_conv(g, dtype, 1, dy, dy_ld, 0, packed_wt, nullptr, CAI_ACT_NONE, 0.f, dx, dtype,
+                    (int64_t)g->in_h * g->in_w * ld, 1, (int64_t)g->in_w * ld, ld, aux, aux_ld, mask_mode,
+                    mask_param, stream, "conv_dgrad");
+}
+
+size_t cai_conv_wgrad_workspace_bytes(const cai_conv_geom* g, int dtype) {
+    if (check_geom(g)) return 0;
+    const WgradPlan W = make_wgrad_plan(g, dtype);
+    return W.ws_slab + W.ws_col + 256;
+}
+
+int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_ld, int32_t in_abs, int32_t in_sq,
+                   const void* dy, int32_t dy_ld, float* dw, float* db, void* workspace, size_t ws_bytes,
+                   void* stream) {
+    int rc = check_geom(g);
+    if (rc) return rc;
+    CAI_CHECK_ARG(x && dy && dw, "conv_wgrad: null pointer");
+    const WgradPlan W = make_wgrad_plan(g, dtype);
+    CAI_CHECK_ARG(workspace && ws_bytes >= W.ws_slab + W.ws_col + 256, "conv_wgrad: workspace too small");
+    const int VEC = dtype == CAI_BF16 ? 8 : 4;
+    WgradArgs a{};
+    if (!g->transposed) {
+        a.g = dy; a.g_ld = dy_ld; a.x = x; a.x_ld = x_ld;
+        a.Hg = g->out_h; a.Wg = g->out_w; a.Hx = g->in_h; a.Wx = g->in_w;
+        a.in_abs = in_abs; a.in_sq = in_sq;
+    } else {
+        a.g = x; a.g_ld = x_ld; a.x = dy; a.x_ld = dy_ld;
+        a.Hg = g->in_h; a.Wg = g->in_w; a.Hx = g->out_h; a.Wx = g->out_w;
+        CAI_CHECK_ARG(!in_abs && !in_sq, "conv_wgrad: input transforms only for Conv2d");
+    }
+    CAI_CHECK_ARG(W.Ng % VEC == 0, "conv_wgrad: gradient-row channels %d must be a multiple of %d", W.Ng, VEC);
+    CAI_CHECK_ARG(a.g_ld % VEC == 0 && a.x_ld % VEC == 0 && a.x_ld >= W.Cq_pad && a.g_ld >= W.Ng,
+                  "conv_wgrad: bad leading dimensions");
+    a.Ng = W.Ng; a.Cq_pad = W.Cq_pad; a.B = g->batch;
+    a.k = g->kernel; a.s = g->stride; a.p = g->pad; a.ncols = W.ncols; a.M = W.M; a.split_len = W.split_len;
+    float* slab = reinterpret_cast<float*>(workspace);
+    a.ws = slab;
+    dim3 grid((W.ncols + 127) / 128, (W.Ng + 127) / 128, W.S);
+    hipStream_t st = as_stream(stream);
+    if (dtype == CAI_BF16)
+        hipLaunchKernelGGL(wgrad_kernel<bf16>, grid, dim3(NT), 0, st, a);
+    else
+        hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(NT), 0, st, a);
+    const int64_t tot = (int64_t)W.Ng * W.Cq * g->kernel * g->kernel;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)std::min<int64_t>(4096, (tot + 255) / 256)), dim3(256), 0,
+                       st, slab, W.S, W.Ng, W.ncols, W.Cq, W.Cq_pad, g->kernel, dw);
+    if (db) {
+        float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + W.ws_slab);
+        const int64_t npix = (int64_t)g->batch * g->out_h * g->out_w;
+        if (dtype == CAI_BF16)
+            launch_colsum<bf16>(dy, npix, g->out_c, dy_ld, W.nchunk, W.chunk, part, db, st);
+        else
+            launch_colsum<float>(dy, npix, g->out_c, dy_ld, W.nchunk, W.chunk, part, db, st);
+    }
+    CAI_LAUNCH_CHECK("conv_wgrad");
+    return CAI_OK;
+}
+
+}  // extern "C"
+
+// exported for gdn.hip (1x1 wgrad on u and x^2, column sums)
+namespace cai {
+int colsum_any(int dtype, const void* g, int64_t npix, int C, int ld, float* out, void* ws, size_t wsb,
+               hipStream_t st) {
+    const int nchunk = (int)std::min<int64_t>(256, (npix + 255) / 256);
+    const int64_t chunk = (npix + nchunk - 1) / nchunk;
+    CAI_CHECK_ARG(wsb >= (size_t)nchunk * C * sizeof(float), "colsum: workspace too small");
+    if (dtype == CAI_BF16)
+        launch_colsum<bf16>(g, npix, C, ld, nchunk, chunk, reinterpret_cast<float*>(ws), out, st);
+    else
+        launch_colsum<float>(g, npix, C, ld, nchunk, chunk, reinterpret_cast<float*>(ws), out, st);
+    return CAI_OK;
+}
+size_t colsum_ws_bytes(int64_t npix, int C) {
+    const int nchunk = (int)std::min<int64_t>(256, (npix + 255) / 256);
+    return (size_t)std::max(nchunk, 1) * C * sizeof(float);
+}
+}  // namespace cai

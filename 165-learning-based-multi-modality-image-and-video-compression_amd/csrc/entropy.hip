@@ -1,0 +1,620 @@
+// Entropy-model kernels: quantize, GaussianConditional and EntropyBottleneck
+// likelihoods (fwd + bwd), EB aux loss, RD-loss reductions.
+//
+// Reference semantics (paths under /root/reference/CompressAI/compressai):
+//   quantize ............ entropy_models/entropy_models.py:157-182 (torch.round = half-to-even -> rintf)
+//   GC likelihood ....... entropy_models.py:629-635, 692-731
+//   EB chain/likelihood . entropy_models.py:457-492, forward :495-540, loss :450-454
+//   LowerBound bwd rule . ops/bound_ops.py:40-42 (grad passes iff x >= bound or grad < 0)
+//
+// All element-wise kernels are HBM-bound, pixel-major: element (p, c) at
+// ptr[p*ld + c]; threads walk (p, c) in memory order so loads coalesce.
+#include "common.hpp"
+
+namespace cai {
+
+static constexpr float kNegInvSqrt2 = -0.70710678118654752440f;   // float(-(2**-0.5))
+static constexpr float kTwoOverSqrtPi = 1.12837916709551257390f;
+
+// ---------------------------------------------------------------------------
+// quantize
+// ---------------------------------------------------------------------------
+__global__ void quantize_kernel(int mode, int64_t n, int C, const void* __restrict__ x, int xdt, int xld,
+                                const float* __restrict__ means, int mld, int means_pc,
+                                const float* __restrict__ noise, int nld, void* __restrict__ out, int odt,
+                                int old) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t p = i / C;
+        const int c = (int)(i - p * C);
+        const float v = ld_any(x, xdt, p * xld + c);
+        if (mode == CAI_Q_NOISE) {
+            st_any(out, odt, p * old + c, v + noise[p * nld + c]);
+            continue;
+        }
+        float mu = 0.f;
+        if (means) mu = means_pc ? means[c] : means[p * mld + c];
+        float r = rintf(means ? v - mu : v);
+        if (mode == CAI_Q_SYMBOLS) {
+            reinterpret_cast<int32_t*>(out)[p * old + c] = (int32_t)r;
+        } else {
+            st_any(out, odt, p * old + c, means ? r + mu : r);
+        }
+    }
+}
+
+static inline int ew_grid(int64_t n, int nt = 256) {
+    int64_t b = (n + nt - 1) / nt;
+    if (b > 8192) b = 8192;
+    if (b < 1) b = 1;
+    return (int)b;
+}
+
+// ---------------------------------------------------------------------------
+// GaussianConditional
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float std_cum(float t) {   // 0.5 * erfc(-(2^-0.5) * t)
+    return 0.5f * erfcf(kNegInvSqrt2 * t);
+}
+// d/dt [0.5 erfc(c t)] following torch's erfc backward: -2/sqrt(pi) exp(-(ct)^2) * c * 0.5
+__device__ __forceinline__ float std_cum_grad(float t) {
+    const float a = kNegInvSqrt2 * t;
+    return 0.5f * (-kTwoOverSqrtPi * expf(-a * a)) * kNegInvSqrt2;
+}
+
+__global__ void gc_fwd_kernel(int mode, int64_t n, int C, const void* __restrict__ x, int xdt, int xld,
+                              const void* __restrict__ sc, int sld, const void* __restrict__ mu, int mld, int smdt,
+                              const float* __restrict__ noise, int nld, float sbound, float lbound,
+                              void* __restrict__ q, int qdt, int qld, float* __restrict__ lik, int lld) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t p = i / C;
+        const int c = (int)(i - p * C);
+        const float xv = ld_any(x, xdt, p * xld + c);
+        const float m = mu ? ld_any(mu, smdt, p * mld + c) : 0.f;
+        float qv;
+        if (mode == CAI_Q_NOISE)
+            qv = xv + noise[p * nld + c];
+        else
+            qv = mu ? rintf(xv - m) + m : rintf(xv);
+        if (q) st_any(q, qdt, p * qld + c, qv);
+        const float v = mu ? qv - m : qv;
+        const float s = fmaxf(ld_any(sc, smdt, p * sld + c), sbound);
+        const float av = fabsf(v);
+        const float up = std_cum((0.5f - av) / s);
+        const float lo = std_cum((-0.5f - av) / s);
+        lik[p * lld + c] = fmaxf(up - lo, lbound);
+    }
+}
+
+__global__ void gc_bwd_kernel(int mode, int64_t n, int C, const void* __restrict__ x, int xdt, int xld,
+                              const void* __restrict__ sc, int sld, const void* __restrict__ mu, int mld, int smdt,
+                              const float* __restrict__ noise, int nld, float sbound, float lbound,
+                              const float* __restrict__ glik, int glld, const void* __restrict__ gq, int gqdt,
+                              int gqld, void* __restrict__ dx, int dxld, void* __restrict__ ds, int dsld,
+                              void* __restrict__ dm, int dmld) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t p = i / C;
+        const int c = (int)(i - p * C);
+        const float xv = ld_any(x, xdt, p * xld + c);
+        const float m = mu ? ld_any(mu, smdt, p * mld + c) : 0.f;
+        const float qv = (mode == CAI_Q_NOISE) ? xv + noise[p * nld + c] : (mu ? rintf(xv - m) + m : rintf(xv));
+        const float v = mu ? qv - m : qv;
+        const float sraw = ld_any(sc, smdt, p * sld + c);
+        const float s = fmaxf(sraw, sbound);
+        const float av = fabsf(v);
+        const float tu = (0.5f - av) / s;
+        const float tl = (-0.5f - av) / s;
+        float g = glik ? glik[p * glld + c] : 0.f;
+        const float lraw = std_cum(tu) - std_cum(tl);
+        if (!(lraw >= lbound || g < 0.f)) g = 0.f;           // LowerBound(lik) backward
+        const float dtu = g * std_cum_grad(tu);
+        const float dtl = -g * std_cum_grad(tl);
+        // t = a / s : da = dt / s ; ds = -dt * a / (s*s)
+        const float dav = -(dtu + dtl) / s;
+        float dsv = -dtu * (0.5f - av) / (s * s) - dtl * (-0.5f - av) / (s * s);
+        if (!(sraw >= sbound || dsv < 0.f)) dsv = 0.f;      // LowerBound(scales) backward
+        const float sgn = (v > 0.f) ? 1.f : ((v < 0.f) ? -1.f : 0.f);
+        const float dv = dav * sgn;
+        const float gqv = gq ? ld_any(gq, gqdt, p * gqld + c) : 0.f;
+        if (mode == CAI_Q_NOISE) {
+            if (dx) st_any(dx, xdt, p * dxld + c, gqv + dv);
+            if (dm) st_any(dm, smdt, p * dmld + c, -dv);
+        } else {
+            if (dx) st_any(dx, xdt, p * dxld + c, 0.f);
+            if (dm) st_any(dm, smdt, p * dmld + c, (gqv + dv) - dv);
+        }
+        if (ds) st_any(ds, smdt, p * dsld + c, dsv);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// EntropyBottleneck: per-channel monotone MLP 1->3->3->3->3->1
+// ---------------------------------------------------------------------------
+// per-channel table: softplus'd matrices (3 + 9 + 9 + 9 + 3 = 33), biases
+// (3*4 + 1 = 13), tanh'd factors (12), median (1)
+constexpr int EB_SP = 0, EB_B = 33, EB_TF = 46, EB_MED = 58, EB_NP = 60;
+
+__device__ __forceinline__ float softplus_f(float v) {   // F.softplus(beta=1, threshold=20)
+    return v > 20.f ? v : log1pf(expf(v));
+}
+__device__ __forceinline__ float softplus_grad(float v) {   // torch softplus backward
+    if (v > 20.f) return 1.f;
+    const float z = expf(v);
+    return z / (z + 1.f);
+}
+__device__ __forceinline__ float sigmoid_f(float v) { return 1.f / (1.f + expf(-v)); }
+
+__device__ void eb_load_table(int c, const cai_eb_params& P, float* t) {
+    int o = 0;
+    // matrices (softplus)
+    for (int k = 0; k < 3; ++k) t[EB_SP + o++] = softplus_f(P.matrix[0][c * 3 + k]);
+    for (int l = 1; l < 4; ++l)
+        for (int k = 0; k < 9; ++k) t[EB_SP + o++] = softplus_f(P.matrix[l][c * 9 + k]);
+    for (int k = 0; k < 3; ++k) t[EB_SP + o++] = softplus_f(P.matrix[4][c * 3 + k]);
+    o = 0;
+    for (int l = 0; l < 4; ++l)
+        for (int k = 0; k < 3; ++k) t[EB_B + o++] = P.bias[l][c * 3 + k];
+    t[EB_B + 12] = P.bias[4][c];
+    o = 0;
+    for (int l = 0; l < 4; ++l)
+        for (int k = 0; k < 3; ++k) t[EB_TF + o++] = tanhf(P.factor[l][c * 3 + k]);
+    t[EB_MED] = P.quantiles[c * 3 + 1];
+}
+
+// forward of one chain; records pre-activations a[l][j] and outputs h[l][j]
+struct EbTrace {
+    float a[4][3];
+    float h[4][3];
+};
+
+__device__ __forceinline__ float eb_chain(float x, const float* t, EbTrace* tr) {
+    float h[3], hn[3];
+    // layer 0: [3,1]
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        float a = t[EB_SP + j] * x + t[EB_B + j];
+        if (tr) tr->a[0][j] = a;
+        h[j] = a + t[EB_TF + j] * tanhf(a);
+        if (tr) tr->h[0][j] = h[j];
+    }
+#pragma unroll
+    for (int l = 1; l < 4; ++l) {
+        const float* M = t + EB_SP + 3 + (l - 1) * 9;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            float a = M[j * 3 + 0] * h[0] + M[j * 3 + 1] * h[1] + M[j * 3 + 2] * h[2] + t[EB_B + l * 3 + j];
+            if (tr) tr->a[l][j] = a;
+            hn[j] = a + t[EB_TF + l * 3 + j] * tanhf(a);
+            if (tr) tr->h[l][j] = hn[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) h[j] = hn[j];
+    }
+    const float* M4 = t + EB_SP + 30;
+    return M4[0] * h[0] + M4[1] * h[1] + M4[2] * h[2] + t[EB_B + 12];
+}
+
+// backward of one chain with upstream gradient d; accumulates d(softplus'd
+// matrix), d(bias), d(tanh'd factor) into g[] (same index layout as the
+// table) and returns d input.
+__device__ __forceinline__ float eb_chain_bwd(float x, float d, const float* t, const EbTrace& tr, float* g) {
+    float dh[3];
+    g[EB_B + 12] += d;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        g[EB_SP + 30 + k] += d * tr.h[3][k];
+        dh[k] = d * t[EB_SP + 30 + k];
+    }
+#pragma unroll
+    for (int l = 3; l >= 0; --l) {
+        float da[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const float th = tanhf(tr.a[l][j]);
+            const float tf = t[EB_TF + l * 3 + j];
+            g[EB_TF + l * 3 + j] += dh[j] * th;
+            da[j] = dh[j] * (1.f + tf * (1.f - th * th));
+            g[EB_B + l * 3 + j] += da[j];
+        }
+        if (l == 0) {
+            float dx = 0.f;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                g[EB_SP + j] += da[j] * x;
+                dx += t[EB_SP + j] * da[j];
+            }
+            return dx;
+        }
+        const float* M = t + EB_SP + 3 + (l - 1) * 9;
+        float* gM = g + EB_SP + 3 + (l - 1) * 9;
+        float dp[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                gM[j * 3 + k] += da[j] * tr.h[l - 1][k];
+                dp[k] += M[j * 3 + k] * da[j];
+            }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) dh[k] = dp[k];
+    }
+    return 0.f;
+}
+
+// fwd: block = 256 threads = 32 channels x 8 pixel rows
+__global__ __launch_bounds__(256) void eb_fwd_kernel(int mode, int64_t npix, int C, cai_eb_params P,
+                                                      const void* __restrict__ x, int xdt, int xld,
+                                                      const float* __restrict__ noise, int nld, float lbound,
+                                                      void* __restrict__ q, int qdt, int qld,
+                                                      float* __restrict__ lik, int lld) {
+    __shared__ float tab[32][EB_NP];
+    const int cl = threadIdx.x & 31, pr = threadIdx.x >> 5;
+    const int c0 = blockIdx.x * 32;
+    for (int i = threadIdx.x; i < 32; i += blockDim.x)
+        if (c0 + i < C) eb_load_table(c0 + i, P, tab[i]);
+    __syncthreads();
+    const int c = c0 + cl;
+    if (c >= C) return;
+    const float* t = tab[cl];
+    for (int64_t p = blockIdx.y * 8 + pr; p < npix; p += (int64_t)gridDim.y * 8) {
+        const float xv = ld_any(x, xdt, p * xld + c);
+        float v;
+        if (mode == CAI_Q_NOISE)
+            v = xv + noise[p * nld + c];
+        else
+            v = rintf(xv - t[EB_MED]) + t[EB_MED];
+        if (q) st_any(q, qdt, p * qld + c, v);
+        const float lo = eb_chain(v - 0.5f, t, nullptr);
+        const float up = eb_chain(v + 0.5f, t, nullptr);
+        const float sum = lo + up;
+        const float sgn = -((sum > 0.f) ? 1.f : ((sum < 0.f) ? -1.f : 0.f));
+        const float l = fabsf(sigmoid_f(sgn * up) - sigmoid_f(sgn * lo));
+        lik[p * lld + c] = fmaxf(l, lbound);
+    }
+}
+
+// bwd: block = 256 threads = 8 channels x 32 pixel lanes; the 32 threads of a
+// channel sit in one half-wave so the per-channel parameter sums reduce with
+// shuffles in a fixed order (deterministic, no atomics).
+__global__ __launch_bounds__(256) void eb_bwd_kernel(int mode, int64_t npix, int C, cai_eb_params P,
+                                                       const void* __restrict__ x, int xdt, int xld,
+                                                       const float* __restrict__ noise, int nld, float lbound,
+                                                       const float* __restrict__ glik, int glld,
+                                                       const void* __restrict__ gq, int gqdt, int gqld,
+                                                       void* __restrict__ dx, int dxld, cai_eb_grads G) {
+    __shared__ float tab[8][EB_NP];
+    const int pl = threadIdx.x & 31, cl = threadIdx.x >> 5;
+    const int c0 = blockIdx.x * 8;
+    for (int i = threadIdx.x; i < 8; i += blockDim.x)
+        if (c0 + i < C) eb_load_table(c0 + i, P, tab[i]);
+    __syncthreads();
+    const int c = c0 + cl;
+    if (c >= C) return;   // whole half-waves exit together
+    const float* t = tab[cl];
+    float g[EB_NP];
+#pragma unroll
+    for (int k = 0; k < EB_NP; ++k) g[k] = 0.f;
+    for (int64_t p = pl; p < npix; p += 32) {
+        const float xv = ld_any(x, xdt, p * xld + c);
+        const float v = (mode == CAI_Q_NOISE) ? xv + noise[p * nld + c] : rintf(xv - t[EB_MED]) + t[EB_MED];
+        EbTrace tl, tu;
+        const float lo = eb_chain(v - 0.5f, t, &tl);
+        const float up = eb_chain(v + 0.5f, t, &tu);
+        const float sum = lo + up;
+        const float sgn = -((sum > 0.f) ? 1.f : ((sum < 0.f) ? -1.f : 0.f));
+        const float su = sigmoid_f(sgn * up), sl = sigmoid_f(sgn * lo);
+        const float D = su - sl;
+        float gl = glik ? glik[p * glld + c] : 0.f;
+        if (!(fabsf(D) >= lbound || gl < 0.f)) gl = 0.f;      // LowerBound(lik)
+        const float dD = gl * ((D > 0.f) ? 1.f : ((D < 0.f) ? -1.f : 0.f));   // abs
+        const float dup = dD * su * (1.f - su) * sgn;
+        const float dlo = -dD * sl * (1.f - sl) * sgn;
+        float dv = eb_chain_bwd(v + 0.5f, dup, t, tu, g) + eb_chain_bwd(v - 0.5f, dlo, t, tl, g);
+        const float gqv = gq ? ld_any(gq, gqdt, p * gqld + c) : 0.f;
+        if (mode == CAI_Q_NOISE) {
+            if (dx) st_any(dx, xdt, p * dxld + c, gqv + dv);
+        } else {
+            if (dx) st_any(dx, xdt, p * dxld + c, 0.f);
+            g[EB_MED] += gqv + dv;
+        }
+    }
+    // reduce each accumulator over the 32 lanes of this channel
+#pragma unroll
+    for (int k = 0; k < EB_NP; ++k) {
+        float v = g[k];
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        g[k] = v;
+    }
+    if (pl != 0) return;
+    // softplus / tanh chain rule and scatter to torch layout (all indices
+    // compile-time after unrolling so g[] stays in registers)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) G.matrix[0][c * 3 + k] = g[EB_SP + k] * softplus_grad(P.matrix[0][c * 3 + k]);
+#pragma unroll
+    for (int l = 1; l < 4; ++l)
+#pragma unroll
+        for (int k = 0; k < 9; ++k)
+            G.matrix[l][c * 9 + k] = g[EB_SP + 3 + (l - 1) * 9 + k] * softplus_grad(P.matrix[l][c * 9 + k]);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) G.matrix[4][c * 3 + k] = g[EB_SP + 30 + k] * softplus_grad(P.matrix[4][c * 3 + k]);
+#pragma unroll
+    for (int l = 0; l < 4; ++l)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) G.bias[l][c * 3 + k] = g[EB_B + l * 3 + k];
+    G.bias[4][c] = g[EB_B + 12];
+#pragma unroll
+    for (int l = 0; l < 4; ++l)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float th = t[EB_TF + l * 3 + k];
+            G.factor[l][c * 3 + k] = g[EB_TF + l * 3 + k] * (1.f - th * th);
+        }
+    if (G.quantiles) {
+        G.quantiles[c * 3 + 0] = 0.f;
+        G.quantiles[c * 3 + 1] = (mode == CAI_Q_NOISE) ? 0.f : g[EB_MED];
+        G.quantiles[c * 3 + 2] = 0.f;
+    }
+}
+
+// aux loss: one block, deterministic
+__global__ __launch_bounds__(1024) void eb_aux_kernel(int C, cai_eb_params P, const float* __restrict__ target,
+                                                       float* __restrict__ loss, const float* __restrict__ gloss,
+                                                       float* __restrict__ dq) {
+    __shared__ float red[16];
+    float acc = 0.f;
+    const float gs = gloss ? *gloss : 0.f;
+    for (int i = threadIdx.x; i < 3 * C; i += blockDim.x) {
+        const int c = i / 3, k = i - 3 * (i / 3);
+        float t[EB_NP];
+        eb_load_table(c, P, t);
+        const float qv = P.quantiles[c * 3 + k];
+        EbTrace tr;
+        const float f = eb_chain(qv, t, &tr);
+        const float diff = f - target[k];
+        acc += fabsf(diff);
+        if (dq) {
+            float gd[EB_NP];
+#pragma unroll
+            for (int j = 0; j < EB_NP; ++j) gd[j] = 0.f;
+            const float s = (diff > 0.f) ? 1.f : ((diff < 0.f) ? -1.f : 0.f);
+            dq[c * 3 + k] = eb_chain_bwd(qv, gs * s, t, tr, gd);
+        }
+    }
+    const float r = block_sum<1024>(acc, red);
+    if (threadIdx.x == 0 && loss) *loss = r;
+}
+
+// ---------------------------------------------------------------------------
+// reductions (two-stage, deterministic)
+// ---------------------------------------------------------------------------
+constexpr int RED_BLOCKS = 1024;
+
+template <int KIND>   // 0: sum log(a) over (p,c) with ld ; 1: sum (a-b)^2 contiguous ; 2: sum a^2 contiguous
+__global__ __launch_bounds__(256) void reduce_stage1(const float* __restrict__ a, const float* __restrict__ b,
+                                                      int64_t n, int C, int ld, float* __restrict__ part) {
+    __shared__ float red[4];
+    float acc = 0.f;
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        if (KIND == 0) {
+            const int64_t p = i / C;
+            acc += logf(a[p * ld + (i - p * C)]);
+        } else if (KIND == 1) {
+            const float d = a[i] - b[i];
+            acc += d * d;
+        } else {
+            acc += a[i] * a[i];
+        }
+    }
+    const float r = block_sum<256>(acc, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = r;
+}
+
+__global__ __launch_bounds__(256) void reduce_stage2(const float* __restrict__ part, int n, float* __restrict__ out) {
+    __shared__ float red[4];
+    float acc = 0.f;
+    for (int i = threadIdx.x; i < n; i += 256) acc += part[i];
+    const float r = block_sum<256>(acc, red);
+    if (threadIdx.x == 0) *out = r;
+}
+
+static int red_blocks(int64_t n) {
+    int64_t b = (n + 1023) / 1024;
+    if (b > RED_BLOCKS) b = RED_BLOCKS;
+    return b < 1 ? 1 : (int)b;
+}
+
+template <int KIND>
+static int run_reduce(const float* a, const float* b, int64_t n, int C, int ld, float* out, void* ws, size_t wsb,
+                      void* stream, const char* name) {
+    CAI_CHECK_ARG(n >= 0, "%s: negative size", name);
+    CAI_CHECK_ARG(ws && wsb >= cai_reduce_workspace_bytes(n), "%s: workspace too small", name);
+    const int nb = red_blocks(n);
+    float* part = reinterpret_cast<float*>(ws);
+    hipLaunchKernelGGL(reduce_stage1<KIND>, dim3(nb), dim3(256), 0, as_stream(stream), a, b, n, C, ld, part);
+    hipLaunchKernelGGL(reduce_stage2, dim3(1), dim3(256), 0, as_stream(stream), part, nb, out);
+    CAI_LAUNCH_CHECK(name);
+    return CAI_OK;
+}
+
+__global__ void log_bwd_kernel(const float* __restrict__ lik, int64_t n, int C, int ld, const float* __restrict__ scale,
+                               float coef, float* __restrict__ g) {
+    const float s = *scale * coef;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t p = i / C;
+        const int64_t o = p * ld + (i - p * C);
+        g[o] = s / lik[o];
+    }
+}
+
+__global__ void sqdiff_bwd_kernel(const float* __restrict__ a, const float* __restrict__ b, int64_t n,
+                                  const float* __restrict__ scale, float coef, float* __restrict__ ga) {
+    const float s = *scale * coef;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        ga[i] = s * (a[i] - b[i]);
+}
+
+__global__ void act_bwd_kernel(int mode, float prm, const void* __restrict__ y, int yld, const void* __restrict__ g,
+                               int gld, void* __restrict__ out, int old, int64_t n, int C, int dt) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t p = i / C;
+        const int c = (int)(i - p * C);
+        const float yv = ld_any(y, dt, p * yld + c);
+        const float gv = ld_any(g, dt, p * gld + c);
+        float m = 1.f;
+        if (mode == CAI_MASK_POS) m = yv > 0.f ? 1.f : 0.f;
+        else if (mode == CAI_MASK_LEAKY) m = yv > 0.f ? 1.f : prm;
+        else if (mode == CAI_MASK_SIGN) m = yv > 0.f ? 1.f : (yv < 0.f ? -1.f : 0.f);
+        st_any(out, dt, p * old + c, gv * m);
+    }
+}
+
+__global__ void cast_kernel(const void* __restrict__ x, int xdt, void* __restrict__ y, int ydt, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        st_any(y, ydt, i, ld_any(x, xdt, i));
+}
+
+}  // namespace cai
+
+using namespace cai;
+
+extern "C" {
+
+int cai_quantize(int mode, int64_t npix, int32_t C, const void* x, int x_dtype, int32_t x_ld, const float* means,
+                 int32_t means_ld, int32_t means_per_channel, const float* noise, int32_t noise_ld, void* out,
+                 int out_dtype, int32_t out_ld, void* stream) {
+    CAI_CHECK_ARG(mode == CAI_Q_NOISE || mode == CAI_Q_DEQUANTIZE || mode == CAI_Q_SYMBOLS,
+                  "quantize: invalid mode %d", mode);
+    CAI_CHECK_ARG(C > 0 && npix >= 0 && x_ld >= C && out_ld >= C, "quantize: bad shape");
+    CAI_CHECK_ARG(mode != CAI_Q_NOISE || noise, "quantize: noise mode needs a noise buffer");
+    const int64_t n = npix * C;
+    if (n == 0) return CAI_OK;
+    hipLaunchKernelGGL(quantize_kernel, dim3(ew_grid(n)), dim3(256), 0, as_stream(stream), mode, n, C, x, x_dtype,
+                       x_ld, means, means_ld, means_per_channel, noise, noise_ld, out, out_dtype, out_ld);
+    CAI_LAUNCH_CHECK("quantize");
+    return CAI_OK;
+}
+
+int cai_gc_fwd(int mode, int64_t npix, int32_t C, const void* x, int x_dtype, int32_t x_ld, const void* scales,
+               int32_t s_ld, const void* means, int32_t m_ld, int sm_dtype, const float* noise, int32_t noise_ld,
+               float scale_bound, float lik_bound, void* q, int q_dtype, int32_t q_ld, float* lik, int32_t lik_ld,
+               void* stream) {
+    CAI_CHECK_ARG(mode == CAI_Q_NOISE || mode == CAI_Q_DEQUANTIZE, "gc_fwd: invalid mode %d", mode);
+    CAI_CHECK_ARG(mode != CAI_Q_NOISE || noise, "gc_fwd: noise mode needs a noise buffer");
+    CAI_CHECK_ARG(C > 0 && npix >= 0 && lik, "gc_fwd: bad arguments");
+    const int64_t n = npix * C;
+    if (n == 0) return CAI_OK;
+    hipLaunchKernelGGL(gc_fwd_kernel, dim3(ew_grid(n)), dim3(256), 0, as_stream(stream), mode, n, C, x, x_dtype, x_ld,
+                       scales, s_ld, means, m_ld, sm_dtype, noise, noise_ld, scale_bound, lik_bound, q, q_dtype, q_ld,
+                       lik, lik_ld);
+    CAI_LAUNCH_CHECK("gc_fwd");
+    return CAI_OK;
+}
+
+int cai_gc_bwd(int mode, int64_t npix, int32_t C, const void* x, int x_dtype, int32_t x_ld, const void* scales,
+               int32_t s_ld, const void* means, int32_t m_ld, int sm_dtype, const float* noise, int32_t noise_ld,
+               float scale_bound, float lik_bound, const float* g_lik, int32_t gl_ld, const void* g_q, int gq_dtype,
+               int32_t gq_ld, void* dx, int32_t dx_ld, void* dscales, int32_t ds_ld, void* dmeans, int32_t dm_ld,
+               void* stream) {
+    CAI_CHECK_ARG(mode == CAI_Q_NOISE || mode == CAI_Q_DEQUANTIZE, "gc_bwd: invalid mode %d", mode);
+    CAI_CHECK_ARG(mode != CAI_Q_NOISE || noise, "gc_bwd: noise mode needs a noise buffer");
+    const int64_t n = npix * C;
+    if (n == 0) return CAI_OK;
+    hipLaunchKernelGGL(gc_bwd_kernel, dim3(ew_grid(n)), dim3(256), 0, as_stream(stream), mode, n, C, x, x_dtype, x_ld,
+                       scales, s_ld, means, m_ld, sm_dtype, noise, noise_ld, scale_bound, lik_bound, g_lik, gl_ld, g_q,
+                       gq_dtype, gq_ld, dx, dx_ld, dscales, ds_ld, dmeans, dm_ld);
+    CAI_LAUNCH_CHECK("gc_bwd");
+    return CAI_OK;
+}
+
+int cai_eb_fwd(int mode, int64_t npix, int32_t C, const cai_eb_params* prm, const void* x, int x_dtype, int32_t x_ld,
+               const float* noise, int32_t noise_ld, float lik_bound, void* q, int q_dtype, int32_t q_ld, float* lik,
+               int32_t lik_ld, void* stream) {
+    CAI_CHECK_ARG(prm, "eb_fwd: null params");
+    CAI_CHECK_ARG(mode == CAI_Q_NOISE || mode == CAI_Q_DEQUANTIZE, "eb_fwd: invalid mode %d", mode);
+    CAI_CHECK_ARG(mode != CAI_Q_NOISE || noise, "eb_fwd: noise mode needs a noise buffer");
+    if (npix * C == 0) return CAI_OK;
+    int64_t gy = (npix + 8 * 8 - 1) / (8 * 8);
+    if (gy > 1024) gy = 1024;
+    hipLaunchKernelGGL(eb_fwd_kernel, dim3((C + 31) / 32, (unsigned)gy), dim3(256), 0, as_stream(stream), mode, npix, C,
+                       *prm, x, x_dtype, x_ld, noise, noise_ld, lik_bound, q, q_dtype, q_ld, lik, lik_ld);
+    CAI_LAUNCH_CHECK("eb_fwd");
+    return CAI_OK;
+}
+
+int cai_eb_bwd(int mode, int64_t npix, int32_t C, const cai_eb_params* prm, const void* x, int x_dtype, int32_t x_ld,
+               const float* noise, int32_t noise_ld, float lik_bound, const float* g_lik, int32_t gl_ld,
+               const void* g_q, int gq_dtype, int32_t gq_ld, void* dx, int32_t dx_ld, const cai_eb_grads* grads,
+               void* stream) {
+    CAI_CHECK_ARG(prm && grads, "eb_bwd: null params/grads");
+    CAI_CHECK_ARG(mode == CAI_Q_NOISE || mode == CAI_Q_DEQUANTIZE, "eb_bwd: invalid mode %d", mode);
+    for (int i = 0; i < 5; ++i) CAI_CHECK_ARG(grads->matrix[i] && grads->bias[i], "eb_bwd: null grad");
+    for (int i = 0; i < 4; ++i) CAI_CHECK_ARG(grads->factor[i], "eb_bwd: null grad");
+    hipLaunchKernelGGL(eb_bwd_kernel, dim3((C + 7) / 8), dim3(256), 0, as_stream(stream), mode, npix, C, *prm, x,
+                       x_dtype, x_ld, noise, noise_ld, lik_bound, g_lik, gl_ld, g_q, gq_dtype, gq_ld, dx, dx_ld,
+                       *grads);
+    CAI_LAUNCH_CHECK("eb_bwd");
+    return CAI_OK;
+}
+
+int cai_eb_aux_loss(int32_t C, const cai_eb_params* prm, const float* target, float* loss, const float* g_loss,
+                    float* dquantiles, void* stream) {
+    CAI_CHECK_ARG(prm && target && C > 0, "eb_aux_loss: bad arguments");
+    CAI_CHECK_ARG(!dquantiles || g_loss, "eb_aux_loss: dquantiles needs g_loss");
+    hipLaunchKernelGGL(eb_aux_kernel, dim3(1), dim3(1024), 0, as_stream(stream), C, *prm, target, loss, g_loss,
+                       dquantiles);
+    CAI_LAUNCH_CHECK("eb_aux_loss");
+    return CAI_OK;
+}
+
+size_t cai_reduce_workspace_bytes(int64_t n) { return (size_t)red_blocks(n) * sizeof(float); }
+
+int cai_sum_log(const float* lik, int64_t npix, int32_t C, int32_t ld, float* out, void* workspace, size_t ws_bytes,
+                void* stream) {
+    CAI_CHECK_ARG(C > 0 && ld >= C, "sum_log: bad shape");
+    return run_reduce<0>(lik, nullptr, npix * C, C, ld, out, workspace, ws_bytes, stream, "sum_log");
+}
+
+int cai_sum_sqdiff(const float* a, const float* b, int64_t n, float* out, void* workspace, size_t ws_bytes,
+                   void* stream) {
+    return run_reduce<1>(a, b, n, 1, 1, out, workspace, ws_bytes, stream, "sum_sqdiff");
+}
+
+int cai_sqnorm(const float* g, int64_t n, float* out, void* workspace, size_t ws_bytes, void* stream) {
+    return run_reduce<2>(g, nullptr, n, 1, 1, out, workspace, ws_bytes, stream, "sqnorm");
+}
+
+int cai_log_bwd(const float* lik, int64_t npix, int32_t C, int32_t ld, const float* scale, float coef, float* g,
+                void* stream) {
+    const int64_t n = npix * C;
+    if (n == 0) return CAI_OK;
+    hipLaunchKernelGGL(log_bwd_kernel, dim3(ew_grid(n)), dim3(256), 0, as_stream(stream), lik, n, C, ld, scale, coef, g);
+    CAI_LAUNCH_CHECK("log_bwd");
+    return CAI_OK;
+}
+
+int cai_sqdiff_bwd(const float* a, const float* b, int64_t n, const float* scale, float coef, float* ga,
+                   void* stream) {
+    if (n == 0) return CAI_OK;
+    hipLaunchKernelGGL(sqdiff_bwd_kernel, dim3(ew_grid(n)), dim3(256), 0, as_stream(stream), a, b, n, scale, coef, ga);
+    CAI_LAUNCH_CHECK("sqdiff_bwd");
+    return CAI_OK;
+}
+
+int cai_act_bwd(int mask_mode, float param, const void* y, int32_t y_ld, const void* g, int32_t g_ld, void* out,
+                int32_t out_ld, int64_t npix, int32_t C, int dtype, void* stream) {
+    const int64_t n = npix * C;
+    if (n == 0) return CAI_OK;
+    hipLaunchKernelGGL(act_bwd_kernel, dim3(ew_grid(n)), dim3(256), 0, as_stream(stream), mask_mode, param, y, y_ld, g,
+                       g_ld, out, out_ld, n, C, dtype);
+    CAI_LAUNCH_CHECK("act_bwd");
+    return CAI_OK;
+}
+
+int cai_cast(const void* x, int x_dtype, void* y, int y_dtype, int64_t n, void* stream) {
+    if (n == 0) return CAI_OK;
+    hipLaunchKernelGGL(cast_kernel, dim3(ew_grid(n)), dim3(256), 0, as_stream(stream), x, x_dtype, y, y_dtype, n);
+    CAI_LAUNCH_CHECK("cast");
+    return CAI_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,463 @@
+// GDN / IGDN (compressai/layers/gdn.py:41-92) on CDNA4 MFMA.
+//
+//   beta  = max(beta_raw,  sqrt(beta_min + ped))^2 - ped      (ops/parametrizers.py:61-64)
+//   gamma = max(gamma_raw, sqrt(ped))^2 - ped                  (ped = reparam_offset^2)
+//   norm[p,i] = beta_i + sum_j gamma[i,j] x[p,j]^2             (F.conv2d(x**2, gamma, beta))
+//   out = x * rsqrt(norm)   (inverse: x * sqrt(norm))
+//
+// The C x C contraction is a small-K GEMM (K = C = 128/192): per 64-pixel tile
+// the x tile sits in LDS (rows padded by 16 B: conflict-free ds_read_b128),
+// x^2 is formed in registers on the way into v_mfma_f32_16x16x32_bf16 (or the
+// exact-fp32 16x16x4 path), the normalisation is fused into the epilogue and
+// the tile leaves through LDS as 16-byte stores.  HBM traffic per pixel is
+// the algorithmic minimum: read x once, write y once (fwd); read x, dy once,
+// write dx, u once (bwd).  The forward keeps its gamma fragments in registers
+// for the whole (persistent) block.
+//
+// Backward (per pixel, u_i = dLoss/dnorm_i):
+//   GDN : r = rsqrt(norm), u_i = -0.5 g_i x_i r_i^3, dx_j = g_j r_j + 2 x_j sum_i gamma[i,j] u_i
+//   IGDN: s = sqrt(norm),  u_i =  0.5 g_i x_i / s_i, dx_j = g_j s_j + 2 x_j sum_i gamma[i,j] u_i
+//   dgamma[i,j] = sum_p u_i x_j^2 ; dbeta_i = sum_p u_i   (cai_gdn_param_grad: split-K MFMA
+//   through the 1x1 wgrad kernel + fixed-order column sums), then the LowerBound rule.
+#include "common.hpp"
+
+#include <algorithm>
+
+namespace cai {
+
+int colsum_any(int dtype, const void* g, int64_t npix, int C, int ld, float* out, void* ws, size_t wsb, hipStream_t st);
+size_t colsum_ws_bytes(int64_t npix, int C);
+
+template <typename T>
+__device__ __forceinline__ f32x4 mma_sq(u32x4 a, u32x4 b, f32x4 c, bool square);
+template <>
+__device__ __forceinline__ f32x4 mma_sq<bf16>(u32x4 a, u32x4 b, f32x4 c, bool square) {
+    bf16x8 av = __builtin_bit_cast(bf16x8, a);
+    if (square) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float f = (float)av[e];
+            av[e] = (bf16)(f * f);
+        }
+    }
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+template <>
+__device__ __forceinline__ f32x4 mma_sq<float>(u32x4 a, u32x4 b, f32x4 c, bool square) {
+    f32x4 av = __builtin_bit_cast(f32x4, a);
+    if (square) av = av * av;
+    const f32x4 bv = __builtin_bit_cast(f32x4, b);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], bv[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1], bv[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(av[2], bv[2], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(av[3], bv[3], c, 0, 0, 0);
+    return c;
+}
+
+constexpr int GBM = 64;    // pixels per tile
+constexpr int GNT = 256;   // 4 waves, split over channels (1 x 4)
+
+template <typename T, int C>
+struct GdnGeo {
+    static constexpr int RB = C * (int)sizeof(T);   // bytes of one pixel row
+    static constexpr int RS = RB + 16;               // padded LDS row stride
+    static constexpr int KB = RB / 64;               // 64-byte K blocks per row
+    static constexpr int TN = C / 64;                // 16-col tiles per wave
+    static constexpr int TM = GBM / 16;
+    static constexpr int CHR = RB / 16;              // 16-byte chunks per row
+    static constexpr int TILE_CH = GBM * CHR;        // chunks per tile
+    static constexpr int CPT = (TILE_CH + GNT - 1) / GNT;
+    static constexpr int TILE_LDS = GBM * RS;
+};
+
+template <typename T, int C>
+struct TileRegs {
+    u32x4 v[GdnGeo<T, C>::CPT];
+};
+template <typename T, int C>
+struct BFrags {
+    u32x4 v[GdnGeo<T, C>::TN][GdnGeo<T, C>::KB];
+};
+template <typename T, int C>
+struct Acc {
+    f32x4 v[GdnGeo<T, C>::TM][GdnGeo<T, C>::TN];
+};
+
+// stage a [GBM][C] pixel-major tile (ld elements per pixel) into registers
+template <typename T, int C>
+__device__ __forceinline__ void tile_load(TileRegs<T, C>& R, const T* src, int ld, int64_t p0, int64_t npix) {
+    auto& r = R.v;
+    using G = GdnGeo<T, C>;
+#pragma unroll
+    for (int i = 0; i < G::CPT; ++i) {
+        const int id = i * GNT + threadIdx.x;
+        const int row = id / G::CHR, ch = id - (id / G::CHR) * G::CHR;
+        const int64_t p = p0 + row;
+        if (id < G::TILE_CH && p < npix)
+            r[i] = *reinterpret_cast<const u32x4*>(src + p * ld + ch * (16 / sizeof(T)));
+        else
+            r[i] = u32x4{0u, 0u, 0u, 0u};
+    }
+}
+template <typename T, int C>
+__device__ __forceinline__ void tile_to_lds(const TileRegs<T, C>& R, char* lds) {
+    using G = GdnGeo<T, C>;
+    const auto& r = R.v;
+#pragma unroll
+    for (int i = 0; i < G::CPT; ++i) {
+        const int id = i * GNT + threadIdx.x;
+        const int row = id / G::CHR, ch = id - (id / G::CHR) * G::CHR;
+        if (id < G::TILE_CH) *reinterpret_cast<u32x4*>(lds + row * G::RS + ch * 16) = r[i];
+    }
+}
+template <typename T, int C>
+__device__ __forceinline__ void lds_to_global(const char* lds, T* dst, int ld, int64_t p0, int64_t npix) {
+    using G = GdnGeo<T, C>;
+#pragma unroll
+    for (int i = 0; i < G::CPT; ++i) {
+        const int id = i * GNT + threadIdx.x;
+        const int row = id / G::CHR, ch = id - (id / G::CHR) * G::CHR;
+        const int64_t p = p0 + row;
+        if (id < G::TILE_CH && p < npix)
+            *reinterpret_cast<u32x4*>(dst + p * ld + ch * (16 / sizeof(T))) =
+                *reinterpret_cast<const u32x4*>(lds + row * G::RS + ch * 16);
+    }
+}
+
+// B fragments of a [C][C] row-major matrix for this wave's column slice
+template <typename T, int C>
+__device__ __forceinline__ void load_bfrag(BFrags<T, C>& FB, const T* mat, int wave) {
+    using G = GdnGeo<T, C>;
+    auto& fb = FB.v;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int tn = 0; tn < G::TN; ++tn) {
+        const int n = wave * (C / 4) + tn * 16 + (lane & 15);
+#pragma unroll
+        for (int kb = 0; kb < G::KB; ++kb)
+            fb[tn][kb] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(mat + (int64_t)n * C) + kb * 64 +
+                                                         16 * (lane >> 4));
+    }
+}
+
+template <typename T, int C>
+__device__ __forceinline__ void tile_gemm(Acc<T, C>& ACC, const char* lds, const BFrags<T, C>& FB, bool square) {
+    using G = GdnGeo<T, C>;
+    auto& acc = ACC.v;
+    const auto& fb = FB.v;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < G::TN; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < G::KB; ++kb) {
+        u32x4 fa[G::TM];
+#pragma unroll
+        for (int tm = 0; tm < G::TM; ++tm) {
+            const int row = tm * 16 + (lane & 15);
+            fa[tm] = *reinterpret_cast<const u32x4*>(lds + row * G::RS + kb * 64 + 16 * (lane >> 4));
+        }
+#pragma unroll
+        for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+            for (int tn = 0; tn < G::TN; ++tn) acc[tm][tn] = mma_sq<T>(fa[tm], fb[tn][kb], acc[tm][tn], square);
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ T* lds_elem(char* lds, int rs, int row, int col) {
+    return reinterpret_cast<T*>(lds + row * rs) + col;
+}
+
+template <typename T, int C>
+__global__ __launch_bounds__(GNT, sizeof(T) == 2 ? 2 : 1) void gdn_fwd_kernel(const T* __restrict__ x, int x_ld, int64_t npix,
+                                                         const T* __restrict__ gamma, const float* __restrict__ beta,
+                                                         int inverse, T* __restrict__ y, int y_ld) {
+    using G = GdnGeo<T, C>;
+    __shared__ __attribute__((aligned(16))) char lds[G::TILE_LDS];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    BFrags<T, C> fb;
+    load_bfrag<T, C>(fb, gamma, wave);
+    float bv[G::TN];
+#pragma unroll
+    for (int tn = 0; tn < G::TN; ++tn) bv[tn] = beta[wave * (C / 4) + tn * 16 + (lane & 15)];
+
+    const int64_t ntiles = (npix + GBM - 1) / GBM;
+    TileRegs<T, C> rx;
+    int64_t tile = blockIdx.x;
+    if (tile < ntiles) tile_load<T, C>(rx, x, x_ld, tile * GBM, npix);
+    for (; tile < ntiles; tile += gridDim.x) {
+        tile_to_lds<T, C>(rx, lds);
+        __syncthreads();
+        const int64_t nxt = tile + gridDim.x;
+        if (nxt < ntiles) tile_load<T, C>(rx, x, x_ld, nxt * GBM, npix);
+        Acc<T, C> A;
+        tile_gemm<T, C>(A, lds, fb, true);
+        auto& acc = A.v;
+        // normalise: out = x * rsqrt(norm)  (or sqrt)
+#pragma unroll
+        for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+            for (int tn = 0; tn < G::TN; ++tn) {
+                const int col = wave * (C / 4) + tn * 16 + (lane & 15);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = tm * 16 + (lane >> 4) * 4 + r;
+                    const float xv = to_f32(*lds_elem<T>(lds, G::RS, row, col));
+                    const float nv = acc[tm][tn][r] + bv[tn];
+                    acc[tm][tn][r] = xv * (inverse ? sqrtf(nv) : rsqrtf(nv));
+                }
+            }
+        __syncthreads();
+#pragma unroll
+        for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+            for (int tn = 0; tn < G::TN; ++tn) {
+                const int col = wave * (C / 4) + tn * 16 + (lane & 15);
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    *lds_elem<T>(lds, G::RS, tm * 16 + (lane >> 4) * 4 + r, col) = from_f32<T>(acc[tm][tn][r]);
+            }
+        __syncthreads();
+        lds_to_global<T, C>(lds, y, y_ld, tile * GBM, npix);
+        __syncthreads();
+    }
+}
+
+template <typename T, int C>
+__global__ __launch_bounds__(GNT, 1) void gdn_bwd_kernel(const T* __restrict__ x, int x_ld, const T* __restrict__ dy,
+                                                         int dy_ld, int64_t npix, const T* __restrict__ gamma_op,
+                                                         const float* __restrict__ beta, int inverse,
+                                                         T* __restrict__ dx, int dx_ld, T* __restrict__ u) {
+    using G = GdnGeo<T, C>;
+    __shared__ __attribute__((aligned(16))) char lds[3 * G::TILE_LDS];
+    char* Lx = lds;
+    char* Lg = lds + G::TILE_LDS;
+    char* Lu = lds + 2 * G::TILE_LDS;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const T* gammaT = gamma_op + (int64_t)C * C;
+    float bv[G::TN];
+#pragma unroll
+    for (int tn = 0; tn < G::TN; ++tn) bv[tn] = beta[wave * (C / 4) + tn * 16 + (lane & 15)];
+
+    const int64_t p0 = (int64_t)blockIdx.x * GBM;
+    {
+        TileRegs<T, C> r;
+        tile_load<T, C>(r, x, x_ld, p0, npix);
+        tile_to_lds<T, C>(r, Lx);
+        tile_load<T, C>(r, dy, dy_ld, p0, npix);
+        tile_to_lds<T, C>(r, Lg);
+    }
+    __syncthreads();
+    Acc<T, C> A;
+    auto& acc = A.v;
+    {
+        BFrags<T, C> fb;
+        load_bfrag<T, C>(fb, gamma_op, wave);
+        tile_gemm<T, C>(A, Lx, fb, true);
+    }
+    // u = dLoss/dnorm into LDS; t1 = g * r (or g * s) replaces g in LDS
+#pragma unroll
+    for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < G::TN; ++tn) {
+            const int col = wave * (C / 4) + tn * 16 + (lane & 15);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = tm * 16 + (lane >> 4) * 4 + r;
+                const float xv = to_f32(*lds_elem<T>(Lx, G::RS, row, col));
+                T* gp = lds_elem<T>(Lg, G::RS, row, col);
+                const float gv = to_f32(*gp);
+                const float nv = acc[tm][tn][r] + bv[tn];
+                float uv, t1;
+                if (inverse) {
+                    const float s = sqrtf(nv);
+                    t1 = gv * s;
+                    uv = 0.5f * gv * xv / s;
+                } else {
+                    const float rr = rsqrtf(nv);
+                    t1 = gv * rr;
+                    uv = -0.5f * gv * xv * rr * rr * rr;
+                }
+                *gp = from_f32<T>(t1);
+                *lds_elem<T>(Lu, G::RS, row, col) = from_f32<T>(uv);
+            }
+        }
+    __syncthreads();
+    lds_to_global<T, C>(Lu, u, C, p0, npix);
+    {
+        BFrags<T, C> fb;
+        load_bfrag<T, C>(fb, gammaT, wave);
+        tile_gemm<T, C>(A, Lu, fb, false);
+    }
+    // dx = t1 + 2 x (u gamma)  -> written over t1 in LDS
+#pragma unroll
+    for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < G::TN; ++tn) {
+            const int col = wave * (C / 4) + tn * 16 + (lane & 15);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = tm * 16 + (lane >> 4) * 4 + r;
+                const float xv = to_f32(*lds_elem<T>(Lx, G::RS, row, col));
+                T* gp = lds_elem<T>(Lg, G::RS, row, col);
+                *gp = from_f32<T>(to_f32(*gp) + 2.f * xv * acc[tm][tn][r]);
+            }
+        }
+    __syncthreads();
+    lds_to_global<T, C>(Lg, dx, dx_ld, p0, npix);
+}
+
+__global__ void gdn_reparam_kernel(const float* __restrict__ beta_raw, const float* __restrict__ gamma_raw, int C,
+                                   float bbound, float gbound, float ped, int dtype, float* __restrict__ beta,
+                                   void* __restrict__ gop) {
+    const int64_t CC = (int64_t)C * C;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < CC; i += (int64_t)gridDim.x * blockDim.x) {
+        const int r = (int)(i / C), c = (int)(i - (int64_t)r * C);
+        const float lb = fmaxf(gamma_raw[i], gbound);
+        const float v = lb * lb - ped;
+        st_any(gop, dtype, i, v);                        // gamma[i][j]
+        st_any(gop, dtype, CC + (int64_t)c * C + r, v);  // gamma^T
+        if (i < C) {
+            const float lbb = fmaxf(beta_raw[i], bbound);
+            beta[i] = lbb * lbb - ped;
+        }
+    }
+}
+
+// NonNegativeParametrizer / LowerBound backward: d raw = (raw >= bound || d < 0) ? d : 0, d = 2 lb dparam
+__global__ void gdn_reparam_bwd_kernel(const float* __restrict__ beta_raw, const float* __restrict__ gamma_raw,
+                                       const float* __restrict__ dbeta, const float* __restrict__ dgamma, int C,
+                                       float bbound, float gbound, float* __restrict__ dbeta_raw,
+                                       float* __restrict__ dgamma_raw) {
+    const int64_t CC = (int64_t)C * C;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < CC; i += (int64_t)gridDim.x * blockDim.x) {
+        const float gr = gamma_raw[i];
+        const float d = 2.f * fmaxf(gr, gbound) * dgamma[i];
+        dgamma_raw[i] = (gr >= gbound || d < 0.f) ? d : 0.f;
+        if (i < C) {
+            const float br = beta_raw[i];
+            const float db = 2.f * fmaxf(br, bbound) * dbeta[i];
+            dbeta_raw[i] = (br >= bbound || db < 0.f) ? db : 0.f;
+        }
+    }
+}
+
+template <typename T, int C>
+static void launch_gdn_fwd(const void* x, int x_ld, int64_t npix, const void* g, const float* b, int inv, void* y,
+                           int y_ld, hipStream_t st) {
+    const int64_t ntiles = (npix + GBM - 1) / GBM;
+    const int grid = (int)std::min<int64_t>(ntiles, 1024);
+    hipLaunchKernelGGL((gdn_fwd_kernel<T, C>), dim3(grid), dim3(GNT), 0, st, reinterpret_cast<const T*>(x), x_ld, npix,
+                       reinterpret_cast<const T*>(g), b, inv, reinterpret_cast<T*>(y), y_ld);
+}
+template <typename T, int C>
+static void launch_gdn_bwd(const void* x, int x_ld, const void* dy, int dy_ld, int64_t npix, const void* g,
+                           const float* b, int inv, void* dx, int dx_ld, void* u, hipStream_t st) {
+    const int64_t ntiles = (npix + GBM - 1) / GBM;
+    hipLaunchKernelGGL((gdn_bwd_kernel<T, C>), dim3((unsigned)ntiles), dim3(GNT), 0, st,
+                       reinterpret_cast<const T*>(x), x_ld, reinterpret_cast<const T*>(dy), dy_ld, npix,
+                       reinterpret_cast<const T*>(g), b, inv, reinterpret_cast<T*>(dx), dx_ld, reinterpret_cast<T*>(u));
+}
+
+#define GDN_DISPATCH(FN, ...)                                                  \
+    do {                                                                       \
+        if (dtype == CAI_BF16) {                                               \
+            switch (C) {                                                       \
+                case 64: FN<bf16, 64>(__VA_ARGS__); break;                     \
+                case 128: FN<bf16, 128>(__VA_ARGS__); break;                   \
+                case 192: FN<bf16, 192>(__VA_ARGS__); break;                   \
+            }                                                                  \
+        } else {                                                               \
+            switch (C) {                                                       \
+                case 64: FN<float, 64>(__VA_ARGS__); break;                    \
+                case 128: FN<float, 128>(__VA_ARGS__); break;                  \
+                case 192: FN<float, 192>(__VA_ARGS__); break;                  \
+            }                                                                  \
+        }                                                                      \
+    } while (0)
+
+static bool gdn_c_ok(int C) { return C == 64 || C == 128 || C == 192; }
+
+}  // namespace cai
+
+using namespace cai;
+
+extern "C" {
+
+int cai_gdn_reparam(const float* beta_raw, const float* gamma_raw, int32_t C, float beta_min, float reparam_offset,
+                    int dtype, float* beta, void* gamma_op, void* stream) {
+    CAI_CHECK_ARG(beta_raw && gamma_raw && beta && gamma_op && C > 0, "gdn_reparam: bad arguments");
+    const float ped = reparam_offset * reparam_offset;
+    const float bbound = sqrtf(beta_min + ped), gbound = sqrtf(0.f + ped);
+    const int64_t CC = (int64_t)C * C;
+    hipLaunchKernelGGL(gdn_reparam_kernel, dim3((unsigned)std::min<int64_t>(1024, (CC + 255) / 256)), dim3(256), 0,
+                       as_stream(stream), beta_raw, gamma_raw, C, bbound, gbound, ped, dtype, beta, gamma_op);
+    CAI_LAUNCH_CHECK("gdn_reparam");
+    return CAI_OK;
+}
+
+int cai_gdn_fwd(int dtype, const void* x, int32_t x_ld, int64_t npix, int32_t C, const void* gamma_op,
+                const float* beta, int32_t inverse, void* y, int32_t y_ld, void* stream) {
+    CAI_CHECK_ARG(gdn_c_ok(C), "gdn_fwd: unsupported channel count %d", C);
+    CAI_CHECK_ARG(x && gamma_op && beta && y && x_ld >= C && y_ld >= C, "gdn_fwd: bad arguments");
+    CAI_CHECK_ARG(x_ld % 8 == 0 && y_ld % 8 == 0, "gdn_fwd: ld must be a multiple of 8");
+    if (npix == 0) return CAI_OK;
+    GDN_DISPATCH(launch_gdn_fwd, x, x_ld, npix, gamma_op, beta, inverse, y, y_ld, as_stream(stream));
+    CAI_LAUNCH_CHECK("gdn_fwd");
+    return CAI_OK;
+}
+
+int cai_gdn_bwd(int dtype, const void* x, int32_t x_ld, const void* dy, int32_t dy_ld, int64_t npix, int32_t C,
+                const void* gamma_op, const float* beta, int32_t inverse, void* dx, int32_t dx_ld, void* u,
+                void* stream) {
+    CAI_CHECK_ARG(gdn_c_ok(C), "gdn_bwd: unsupported channel count %d", C);
+    CAI_CHECK_ARG(x && dy && gamma_op && beta && dx && u, "gdn_bwd: bad arguments");
+    CAI_CHECK_ARG(x_ld % 8 == 0 && dy_ld % 8 == 0 && dx_ld % 8 == 0 && x_ld >= C && dy_ld >= C && dx_ld >= C,
+                  "gdn_bwd: bad leading dimensions");
+    if (npix == 0) return CAI_OK;
+    GDN_DISPATCH(launch_gdn_bwd, x, x_ld, dy, dy_ld, npix, gamma_op, beta, inverse, dx, dx_ld, u, as_stream(stream));
+    CAI_LAUNCH_CHECK("gdn_bwd");
+    return CAI_OK;
+}
+
+static cai_conv_geom gdn_geom(int64_t npix, int C) {
+    cai_conv_geom g{};
+    g.batch = 1; g.in_c = C; g.out_c = C; g.in_h = (int)npix; g.in_w = 1; g.out_h = (int)npix; g.out_w = 1;
+    g.kernel = 1; g.stride = 1; g.pad = 0; g.output_padding = 0; g.transposed = 0;
+    return g;
+}
+
+size_t cai_gdn_param_grad_workspace_bytes(int64_t npix, int32_t C, int dtype) {
+    const cai_conv_geom g = gdn_geom(npix, C);
+    return cai_conv_wgrad_workspace_bytes(&g, dtype) + (size_t)C * C * 4 + (size_t)C * 4 + colsum_ws_bytes(npix, C) +
+           512;
+}
+
+int cai_gdn_param_grad(int dtype, const void* x, int32_t x_ld, const void* u, int64_t npix, int32_t C,
+                       const float* beta_raw, const float* gamma_raw, float beta_min, float reparam_offset,
+                       float* dbeta_raw, float* dgamma_raw, void* workspace, size_t ws_bytes, void* stream) {
+    CAI_CHECK_ARG(npix > 0 && npix < (1ll << 31), "gdn_param_grad: bad pixel count");
+    CAI_CHECK_ARG(ws_bytes >= cai_gdn_param_grad_workspace_bytes(npix, C, dtype), "gdn_param_grad: workspace too small");
+    const cai_conv_geom g = gdn_geom(npix, C);
+    const size_t wgb = cai_conv_wgrad_workspace_bytes(&g, dtype);
+    char* ws = reinterpret_cast<char*>(workspace);
+    float* dgamma = reinterpret_cast<float*>(ws + wgb);
+    float* dbeta = dgamma + (size_t)C * C;
+    char* cws = reinterpret_cast<char*>(dbeta + C);
+    // dgamma[i][j] = sum_p u[p][i] * x[p][j]^2   (G = u, X = x squared on load)
+    int rc = cai_conv_wgrad(&g, dtype, x, x_ld, 0, 1, u, C, dgamma, nullptr, ws, wgb, stream);
+    if (rc) return rc;
+    rc = colsum_any(dtype, u, npix, C, C, dbeta, cws, colsum_ws_bytes(npix, C), as_stream(stream));
+    if (rc) return rc;
+    const float ped = reparam_offset * reparam_offset;
+    const float bbound = sqrtf(beta_min + ped), gbound = sqrtf(ped);
+    const int64_t CC = (int64_t)C * C;
+    hipLaunchKernelGGL(gdn_reparam_bwd_kernel, dim3((unsigned)std::min<int64_t>(1024, (CC + 255) / 256)), dim3(256), 0,
+                       as_stream(stream), beta_raw, gamma_raw, dbeta, dgamma, C, bbound, gbound, dbeta_raw, dgamma_raw);
+    CAI_LAUNCH_CHECK("gdn_param_grad");
+    return CAI_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,253 @@
+/*
+ * libcai -- C ABI of the MI355X (gfx950) learned-compression hot path.
+ *
+ * Every entry point takes plain device pointers, sizes and a hipStream_t
+ * (passed as void*), allocates nothing persistent (scratch comes in as a
+ * caller-owned workspace), keeps no global mutable state and is reentrant:
+ * one host thread per device (DataParallel-style) or one process per GPU
+ * (DDP) may call it concurrently.  All launches go to the given stream, so a
+ * caller may capture them into a hipGraph.
+ *
+ * Return value: 0 (CAI_OK) on success, otherwise a CAI_E* code; a
+ * thread-local message is available from cai_last_error().
+ *
+ * Tensor convention ("pixel-major"): an activation of logical NCHW shape
+ * [B,C,H,W] is stored channels-last: element (p, c) with p = (b*H + y)*W + x
+ * lives at ptr[p*ld + c] (ld >= C: pixel stride in elements).  This is what a
+ * torch tensor in torch.channels_last memory format is; channel slices of a
+ * wider tensor (chunk(2, 1)) are expressed with ld > C and an offset pointer.
+ *
+ * Reference interfaces replaced (paths relative to /root/reference/CompressAI):
+ *   conv / deconv factories ........ compressai/models/utils.py:128-146 (nn.Conv2d / nn.ConvTranspose2d)
+ *   GDN / IGDN ...................... compressai/layers/gdn.py:41-92 (+ ops/parametrizers.py:47-64, ops/bound_ops.py:36-80)
+ *   EntropyModel.quantize ........... compressai/entropy_models/entropy_models.py:157-182
+ *   EntropyBottleneck ............... entropy_models.py:450-540 (_logits_cumulative :457-477, _likelihood :480-492, loss :450-454)
+ *   GaussianConditional ............. entropy_models.py:629-635,692-731
+ *   RateDistortionLoss .............. examples/train.py:59-82
+ *   Adam step + clip_grad_norm_ ..... examples/train.py:111-142,176-186 (torch.optim.Adam, torch.nn.utils.clip_grad_norm_)
+ */
+#ifndef CAI_H
+#define CAI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------- */
+#define CAI_OK 0
+#define CAI_EINVAL 1      /* bad argument / shape (python shim raises ValueError) */
+#define CAI_EDEVICE 2     /* HIP launch / runtime error (python shim raises RuntimeError) */
+#define CAI_EWORKSPACE 3  /* workspace too small */
+
+/* ---- element types ---------------------------------------------------- */
+#define CAI_F32 0
+#define CAI_BF16 1
+
+/* ---- epilogue activations / gradient masks ---------------------------- */
+#define CAI_ACT_NONE 0
+#define CAI_ACT_RELU 1
+#define CAI_ACT_LEAKY 2   /* LeakyReLU, negative_slope = act_param */
+
+#define CAI_MASK_NONE 0
+#define CAI_MASK_POS 1    /* dgrad epilogue: out *= (aux > 0)          (ReLU backward)      */
+#define CAI_MASK_LEAKY 2  /* dgrad epilogue: out *= aux > 0 ? 1 : slope (LeakyReLU backward) */
+#define CAI_MASK_SIGN 3   /* dgrad epilogue: out *= sign(aux)           (abs backward)       */
+
+/* ---- quantisation modes (entropy_models.py:157-182) -------------------- */
+#define CAI_Q_NOISE 0
+#define CAI_Q_DEQUANTIZE 1
+#define CAI_Q_SYMBOLS 2
+
+/* ---- misc ------------------------------------------------------------- */
+const char* cai_last_error(void);
+int cai_version(void);
+/* number of entry points exported below (checked by the loader test) */
+int cai_abi_count(void);
+
+/* =======================================================================
+ * Convolution (implicit GEMM on MFMA).  One geometry struct describes the
+ * *module*: an nn.Conv2d (transposed = 0) or nn.ConvTranspose2d
+ * (transposed = 1) with square kernel, symmetric padding and output_padding.
+ * Spatial sizes are those of the module's input (in_h, in_w) and output
+ * (out_h, out_w); the library checks them against the module formula.
+ * ======================================================================= */
+typedef struct cai_conv_geom {
+    int32_t batch;
+    int32_t in_c, in_h, in_w;
+    int32_t out_c, out_h, out_w;
+    int32_t kernel, stride, pad, output_padding;
+    int32_t transposed;
+} cai_conv_geom;
+
+/* Bytes of the packed-weight buffer for one direction (0 = forward,
+ * 1 = input-gradient) at element type dtype. */
+size_t cai_conv_packed_weight_bytes(const cai_conv_geom* g, int dtype, int direction);
+
+/* Repack the fp32 torch weight ([out,in,k,k] for Conv2d, [in,out,k,k] for
+ * ConvTranspose2d) into the per-phase MFMA layout for `direction`;
+ * mask (nullable, same shape as w) multiplies the weight (MaskedConv2d). */
+int cai_conv_pack_weight(const cai_conv_geom* g, int dtype, int direction,
+                         const float* w, const float* mask, void* packed, void* stream);
+
+/* NCHW (fp32, contiguous) -> pixel-major [B*H*W][ld] of dtype with zero
+ * padding of channels C..ld-1.  ld must be a multiple of 8. */
+int cai_pack_nchw(const float* x, int32_t B, int32_t C, int32_t H, int32_t W,
+                  int dtype, void* out, int32_t ld, void* stream);
+
+/* forward: y = act(conv(x) + bias).  x: pixel-major input with ld x_ld
+ * (x_ld >= in_c, multiple of 8 elements);  in_abs != 0 reads |x|.
+ * y is written at y_ptr[b*ysb + c*ysc + oy*ysy + ox*ysx] (element strides);
+ * y_dtype may differ from dtype (the operand type). */
+int cai_conv_fwd(const cai_conv_geom* g, int dtype,
+                 const void* x, int32_t x_ld, int32_t in_abs,
+                 const void* packed_w, const float* bias,
+                 int32_t act, float act_param,
+                 void* y, int y_dtype, int64_t ysb, int64_t ysc, int64_t ysy, int64_t ysx,
+                 void* stream);
+
+/* input gradient: dx = mask(aux) * conv_input_grad(dy).  dy pixel-major
+ * (ld dy_ld), dx pixel-major (ld dx_ld), aux pixel-major (ld aux_ld) or NULL. */
+int cai_conv_dgrad(const cai_conv_geom* g, int dtype,
+                   const void* dy, int32_t dy_ld, const void* packed_wt,
+                   void* dx, int32_t dx_ld,
+                   int32_t mask_mode, float mask_param, const void* aux, int32_t aux_ld,
+                   void* stream);
+
+/* weight / bias gradient (fp32, torch layout, overwritten, not accumulated).
+ * x: module input (pixel-major, ld x_ld, in_abs as in forward; in_sq != 0
+ * squares it), dy: output gradient (pixel-major, ld dy_ld).  db may be NULL. */
+size_t cai_conv_wgrad_workspace_bytes(const cai_conv_geom* g, int dtype);
+int cai_conv_wgrad(const cai_conv_geom* g, int dtype,
+                   const void* x, int32_t x_ld, int32_t in_abs, int32_t in_sq,
+                   const void* dy, int32_t dy_ld,
+                   float* dw, float* db, void* workspace, size_t ws_bytes, void* stream);
+
+/* =======================================================================
+ * GDN / IGDN (layers/gdn.py:41-92), C in {64,128,192}.
+ * ======================================================================= */
+/* beta = max(beta_raw, sqrt(beta_min + ped))^2 - ped ; gamma likewise with
+ * bound sqrt(ped); gamma_op is written in the operand dtype in both the
+ * [i][j] and the transposed [j][i] order (2*C*C elements). */
+int cai_gdn_reparam(const float* beta_raw, const float* gamma_raw, int32_t C,
+                    float beta_min, float reparam_offset, int dtype,
+                    float* beta, void* gamma_op, void* stream);
+int cai_gdn_fwd(int dtype, const void* x, int32_t x_ld, int64_t npix, int32_t C,
+                const void* gamma_op, const float* beta, int32_t inverse,
+                void* y, int32_t y_ld, void* stream);
+/* dx and u (= dLoss/dnorm, pixel-major [npix][C], operand dtype); dgamma and
+ * dbeta are produced afterwards by cai_gdn_param_grad. */
+int cai_gdn_bwd(int dtype, const void* x, int32_t x_ld, const void* dy, int32_t dy_ld,
+                int64_t npix, int32_t C, const void* gamma_op, const float* beta,
+                int32_t inverse, void* dx, int32_t dx_ld, void* u, void* stream);
+size_t cai_gdn_param_grad_workspace_bytes(int64_t npix, int32_t C, int dtype);
+/* dgamma_raw/dbeta_raw (fp32, overwritten) through the NonNegativeParametrizer
+ * / LowerBound backward rule (bound_ops.py:40-42). */
+int cai_gdn_param_grad(int dtype, const void* x, int32_t x_ld, const void* u, int64_t npix, int32_t C,
+                       const float* beta_raw, const float* gamma_raw, float beta_min, float reparam_offset,
+                       float* dbeta_raw, float* dgamma_raw, void* workspace, size_t ws_bytes, void* stream);
+
+/* =======================================================================
+ * Entropy models.  Element (p, c) of every operand at ptr[p*ld + c].
+ * ======================================================================= */
+/* quantize: NOISE  out = x + noise  (noise required, fp32 ld noise_ld)
+ *           DEQUANTIZE out = rint(x - means) + means  (means nullable)
+ *           SYMBOLS    out(int32) = (int)rint(x - means)
+ * x_dtype / out_dtype in {CAI_F32, CAI_BF16} (out int32 for SYMBOLS). */
+int cai_quantize(int mode, int64_t npix, int32_t C,
+                 const void* x, int x_dtype, int32_t x_ld,
+                 const float* means, int32_t means_ld, int32_t means_per_channel,
+                 const float* noise, int32_t noise_ld,
+                 void* out, int out_dtype, int32_t out_ld, void* stream);
+
+/* GaussianConditional forward: q = quantize(x) (NOISE or DEQUANTIZE),
+ * lik = max(Phi((0.5-|q-mu|)/s) - Phi((-0.5-|q-mu|)/s), lik_bound), s = max(scales, scale_bound).
+ * scales/means (means nullable) in dtype sm_dtype.  q may be NULL. */
+int cai_gc_fwd(int mode, int64_t npix, int32_t C,
+               const void* x, int x_dtype, int32_t x_ld,
+               const void* scales, int32_t s_ld, const void* means, int32_t m_ld, int sm_dtype,
+               const float* noise, int32_t noise_ld,
+               float scale_bound, float lik_bound,
+               void* q, int q_dtype, int32_t q_ld, float* lik, int32_t lik_ld, void* stream);
+/* backward: inputs the gradients wrt lik (fp32, nullable) and wrt q (nullable),
+ * outputs dx (x_dtype layout, nullable), dscales, dmeans (sm_dtype, nullable). */
+int cai_gc_bwd(int mode, int64_t npix, int32_t C,
+               const void* x, int x_dtype, int32_t x_ld,
+               const void* scales, int32_t s_ld, const void* means, int32_t m_ld, int sm_dtype,
+               const float* noise, int32_t noise_ld,
+               float scale_bound, float lik_bound,
+               const float* g_lik, int32_t gl_ld, const void* g_q, int gq_dtype, int32_t gq_ld,
+               void* dx, int32_t dx_ld, void* dscales, int32_t ds_ld, void* dmeans, int32_t dm_ld,
+               void* stream);
+
+/* EntropyBottleneck.  params: the 5 matrices, 5 biases, 4 factors and the
+ * quantiles, each fp32 contiguous torch tensors ([C,3,1],[C,3,3]x3,[C,1,3]; bias
+ * [C,w,1]; factor [C,3,1]; quantiles [C,1,3]). */
+typedef struct cai_eb_params {
+    const float* matrix[5];
+    const float* bias[5];
+    const float* factor[4];
+    const float* quantiles;
+} cai_eb_params;
+typedef struct cai_eb_grads {
+    float* matrix[5];
+    float* bias[5];
+    float* factor[4];
+    float* quantiles;   /* medians gradient in DEQUANTIZE mode (nullable) */
+} cai_eb_grads;
+
+int cai_eb_fwd(int mode, int64_t npix, int32_t C, const cai_eb_params* prm,
+               const void* x, int x_dtype, int32_t x_ld,
+               const float* noise, int32_t noise_ld, float lik_bound,
+               void* q, int q_dtype, int32_t q_ld, float* lik, int32_t lik_ld, void* stream);
+/* parameter gradients are overwritten (fp32, torch layout). */
+int cai_eb_bwd(int mode, int64_t npix, int32_t C, const cai_eb_params* prm,
+               const void* x, int x_dtype, int32_t x_ld,
+               const float* noise, int32_t noise_ld, float lik_bound,
+               const float* g_lik, int32_t gl_ld, const void* g_q, int gq_dtype, int32_t gq_ld,
+               void* dx, int32_t dx_ld, const cai_eb_grads* grads, void* stream);
+/* aux loss sum_c sum_k |F_c(quantiles[c,k]) - target[k]| -> *loss (fp32 scalar);
+ * if dquantiles != NULL also writes d loss / d quantiles scaled by *g_loss. */
+int cai_eb_aux_loss(int32_t C, const cai_eb_params* prm, const float* target,
+                    float* loss, const float* g_loss, float* dquantiles, void* stream);
+
+/* =======================================================================
+ * Rate-distortion loss reductions (examples/train.py:68-82).
+ * ======================================================================= */
+/* out[0] += sum(log(lik)) over n elements (fp32, contiguous or strided by ld over C). */
+int cai_sum_log(const float* lik, int64_t npix, int32_t C, int32_t ld, float* out, void* workspace,
+                size_t ws_bytes, void* stream);
+/* out[0] = sum((a-b)^2) over n contiguous fp32 elements */
+int cai_sum_sqdiff(const float* a, const float* b, int64_t n, float* out, void* workspace,
+                   size_t ws_bytes, void* stream);
+size_t cai_reduce_workspace_bytes(int64_t n);
+/* g[i] = (*scale) * coef / lik[i]  (bpp backward) */
+int cai_log_bwd(const float* lik, int64_t npix, int32_t C, int32_t ld, const float* scale, float coef,
+                float* g, void* stream);
+/* ga[i] = (*scale) * coef * (a[i] - b[i])   (mse backward) */
+int cai_sqdiff_bwd(const float* a, const float* b, int64_t n, const float* scale, float coef,
+                   float* ga, void* stream);
+
+/* =======================================================================
+ * Optimiser over flat fp32 buffers (torch.optim.Adam semantics).
+ * ======================================================================= */
+/* state[0] = sum(g^2) (fp32); workspace >= cai_reduce_workspace_bytes(n) */
+int cai_sqnorm(const float* g, int64_t n, float* out, void* workspace, size_t ws_bytes, void* stream);
+/* One Adam step on n parameters; grads are first scaled by
+ * min(1, max_norm / (sqrt(*sqnorm) + 1e-6)) when sqnorm != NULL (clip_grad_norm_).
+ * *step (fp32, device) is incremented by the kernel's first block before use. */
+int cai_adam(float* p, const float* g, float* m, float* v, int64_t n,
+             float lr, float beta1, float beta2, float eps,
+             float* step, const float* sqnorm, float max_norm, void* stream);
+
+/* elementwise helpers */
+int cai_act_bwd(int mask_mode, float param, const void* y, int32_t y_ld, const void* g, int32_t g_ld,
+                void* out, int32_t out_ld, int64_t npix, int32_t C, int dtype, void* stream);
+int cai_cast(const void* x, int x_dtype, void* y, int y_dtype, int64_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CAI_H */

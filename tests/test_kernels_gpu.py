@@ -1,0 +1,313 @@
+"""Per-kernel parity on the GPU: HIP path (through libcai) vs the CPU oracle /
+plain PyTorch fp32 CPU ops on identical seeded inputs.
+
+Tolerances (written here, per north_star): exact-fp32 mode (no autocast)
+relative max error <= 2e-4 for conv / GDN / likelihood values and gradients;
+bf16 mode (autocast) <= 3e-2 relative to the fp32 reference; quantisation
+(round-to-index) bit-exact.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn as nn
+
+import cai_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+FP32_TOL = 2e-4
+BF16_TOL = 3e-2
+
+
+def relerr(a, b):
+    a = a.detach().float().cpu()
+    b = b.detach().float().cpu()
+    den = b.abs().max().item()
+    return (a - b).abs().max().item() / (den if den > 0 else 1.0)
+
+
+def _autocast(bf16):
+    return torch.autocast("cuda", dtype=torch.bfloat16, enabled=bf16)
+
+
+CONV_CASES = [
+    # kind, B, cin, cout, H, W, k, s
+    ("conv", 2, 3, 128, 32, 32, 5, 2),
+    ("conv", 2, 128, 128, 16, 16, 5, 2),
+    ("conv", 2, 128, 192, 16, 16, 5, 2),
+    ("conv", 2, 192, 128, 8, 8, 3, 1),
+    ("conv", 3, 64, 40, 9, 7, 5, 2),
+    ("conv", 2, 384, 320, 6, 6, 1, 1),
+    ("deconv", 2, 192, 128, 8, 8, 5, 2),
+    ("deconv", 2, 128, 3, 16, 16, 5, 2),
+    ("deconv", 2, 128, 192, 5, 7, 5, 2),
+    ("deconv", 1, 96, 64, 6, 6, 3, 1),
+]
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+@pytest.mark.parametrize("case", CONV_CASES, ids=[f"{c[0]}{c[2]}-{c[3]}k{c[6]}s{c[7]}" for c in CONV_CASES])
+def test_conv_fwd_bwd(cuda, case, bf16):
+    from compressai.layers import Conv2d, ConvTranspose2d
+
+    kind, B, cin, cout, H, W, k, s = case
+    torch.manual_seed(0)
+    if kind == "conv":
+        ref = nn.Conv2d(cin, cout, k, stride=s, padding=k // 2)
+        mod = Conv2d(cin, cout, k, stride=s, padding=k // 2)
+    else:
+        ref = nn.ConvTranspose2d(cin, cout, k, stride=s, padding=k // 2, output_padding=s - 1)
+        mod = ConvTranspose2d(cin, cout, k, stride=s, padding=k // 2, output_padding=s - 1)
+    mod.load_state_dict(ref.state_dict())
+    mod = mod.to(cuda)
+    x = torch.randn(B, cin, H, W)
+    xr = x.clone().requires_grad_()
+    yr = ref(xr)
+    g = torch.randn_like(yr)
+    yr.backward(g)
+    xd = x.to(cuda).requires_grad_()
+    with _autocast(bf16):
+        y = mod(xd)
+    y.backward(g.to(cuda))
+    tol = BF16_TOL if bf16 else FP32_TOL
+    assert y.shape == yr.shape
+    assert relerr(y, yr) < tol
+    assert relerr(xd.grad, xr.grad) < tol
+    assert relerr(mod.weight.grad, ref.weight.grad) < tol
+    assert relerr(mod.bias.grad, ref.bias.grad) < tol
+
+
+@pytest.mark.parametrize("act", ["relu", "leaky"])
+def test_fused_conv_act_chain(cuda, act):
+    """conv -> act -> conv in a fused Sequential: epilogue act + dgrad-epilogue mask."""
+    from compressai.layers import Conv2d, Sequential
+
+    torch.manual_seed(1)
+    A = nn.ReLU if act == "relu" else nn.LeakyReLU
+    ref = nn.Sequential(nn.Conv2d(64, 64, 3, padding=1), A(), nn.Conv2d(64, 64, 5, stride=2, padding=2), A())
+    mod = Sequential(Conv2d(64, 64, 3, padding=1), A(), Conv2d(64, 64, 5, stride=2, padding=2), A())
+    mod.load_state_dict(ref.state_dict())
+    mod = mod.to(cuda)
+    x = torch.randn(2, 64, 12, 12)
+    xr = x.clone().requires_grad_()
+    yr = ref(xr)
+    g = torch.randn_like(yr)
+    yr.backward(g)
+    xd = x.to(cuda).requires_grad_()
+    y = mod(xd)
+    y.backward(g.to(cuda))
+    assert relerr(y, yr) < FP32_TOL
+    assert relerr(xd.grad, xr.grad) < FP32_TOL
+    for a, b in zip(mod.parameters(), ref.parameters()):
+        assert relerr(a.grad, b.grad) < FP32_TOL
+
+
+def test_abs_input_fusion(cuda):
+    """h_a(|y|): abs on the operand load, sign mask in the dgrad epilogue."""
+    from compressai.layers import Conv2d, Sequential
+
+    torch.manual_seed(2)
+    ref = nn.Sequential(nn.Conv2d(64, 32, 3, padding=1))
+    mod = Sequential(Conv2d(64, 32, 3, padding=1))
+    mod.load_state_dict(ref.state_dict())
+    mod = mod.to(cuda)
+    x = torch.randn(2, 64, 8, 8)
+    xr = x.clone().requires_grad_()
+    yr = ref(torch.abs(xr))
+    g = torch.randn_like(yr)
+    yr.backward(g)
+    xd = x.to(cuda).requires_grad_()
+    y = mod(xd, input_abs=True)
+    y.backward(g.to(cuda))
+    assert relerr(y, yr) < FP32_TOL
+    assert relerr(xd.grad, xr.grad) < FP32_TOL
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+@pytest.mark.parametrize("inverse", [False, True])
+@pytest.mark.parametrize("C", [64, 128, 192])
+def test_gdn(cuda, C, inverse, bf16):
+    from compressai.layers import GDN
+
+    torch.manual_seed(3)
+    ref = O.GDN(C, inverse=inverse)
+    with torch.no_grad():
+        ref.gamma.add_(0.02 * torch.rand(C, C))
+        ref.beta.add_(0.1 * torch.rand(C))
+    mod = GDN(C, inverse=inverse)
+    mod.load_state_dict(ref.state_dict())
+    mod = mod.to(cuda)
+    x = torch.randn(2, C, 9, 11)
+    xr = x.clone().requires_grad_()
+    yr = ref(xr)
+    g = torch.randn_like(yr)
+    yr.backward(g)
+    xd = x.to(cuda).contiguous(memory_format=torch.channels_last).requires_grad_()
+    with _autocast(bf16):
+        y = mod(xd)
+    y.backward(g.to(cuda))
+    tol = BF16_TOL if bf16 else FP32_TOL
+    assert relerr(y, yr) < tol
+    assert relerr(xd.grad, xr.grad) < tol
+    assert relerr(mod.gamma.grad, ref.gamma.grad) < tol * 5
+    assert relerr(mod.beta.grad, ref.beta.grad) < tol * 5
+
+
+def test_gdn_closed_form_at_init(cuda):
+    """tests/test_layers.py:134-160 KATs (GDN(64) instead of GDN(32): C in {64,128,192})."""
+    from compressai.layers import GDN
+
+    x = torch.rand(1, 64, 16, 16)
+    y = GDN(64).to(cuda)(x.to(cuda)).cpu()
+    assert torch.allclose(y, x / torch.sqrt(1 + 0.1 * x ** 2), atol=1e-6)
+    y = GDN(64, inverse=True).to(cuda)(x.to(cuda)).cpu()
+    assert torch.allclose(y, x * torch.sqrt(1 + 0.1 * x ** 2), atol=1e-6)
+
+
+def _noise_feed(tensors):
+    q = list(tensors)
+    return lambda x: q.pop(0)
+
+
+@pytest.mark.parametrize("with_means", [False, True])
+@pytest.mark.parametrize("training", [True, False])
+def test_gaussian_conditional(cuda, with_means, training):
+    from compressai.entropy_models import GaussianConditional, set_noise_source
+
+    torch.manual_seed(4)
+    shape = (2, 24, 7, 5)
+    x = torch.randn(shape) * 4
+    sc = torch.rand(shape) * 3
+    sc[0, 0] = 0.01       # exercises the scale lower bound
+    mu = torch.randn(shape) if with_means else None
+    noise = torch.empty(shape).uniform_(-0.5, 0.5)
+    ref = O.GaussianConditional(None).train(training)
+    xr, sr = x.clone().requires_grad_(), sc.clone().requires_grad_()
+    mr = mu.clone().requires_grad_() if with_means else None
+    with O.NoiseFeed([noise]):
+        qr, lr = ref(xr, sr, mr)
+    gq, gl = torch.randn(shape), torch.randn(shape)
+    (qr * gq).sum().backward(retain_graph=True)
+    (lr * gl).sum().backward()
+
+    mod = GaussianConditional(None).to(cuda).train(training)
+    xd = x.to(cuda).requires_grad_()
+    sd = sc.to(cuda).requires_grad_()
+    md = mu.to(cuda).requires_grad_() if with_means else None
+    set_noise_source(_noise_feed([noise]))
+    try:
+        q, lik = mod(xd, sd, md)
+    finally:
+        set_noise_source(None)
+    torch.autograd.backward([q, lik], [gq.to(cuda), gl.to(cuda)])
+    if training:
+        assert relerr(q, qr) < 1e-6
+    else:
+        assert torch.equal(q.cpu(), qr.detach())     # round-to-index: bit-exact
+    assert relerr(lik, lr) < FP32_TOL
+    assert relerr(xd.grad, xr.grad) < FP32_TOL
+    assert relerr(sd.grad, sr.grad) < FP32_TOL
+    if with_means:
+        assert relerr(md.grad, mr.grad) < FP32_TOL
+
+
+@pytest.mark.parametrize("training", [True, False])
+def test_entropy_bottleneck(cuda, training):
+    from compressai.entropy_models import EntropyBottleneck, set_noise_source
+
+    torch.manual_seed(5)
+    C = 40
+    ref = O.EntropyBottleneck(C).train(training)
+    with torch.no_grad():
+        for n, p in ref.named_parameters():
+            p.add_(0.1 * torch.randn_like(p))
+    mod = EntropyBottleneck(C)
+    mod.load_state_dict(ref.state_dict())
+    mod = mod.to(cuda).train(training)
+    shape = (3, C, 6, 5)
+    x = torch.randn(shape) * 3
+    noise = torch.empty(shape).uniform_(-0.5, 0.5)
+    xr = x.clone().requires_grad_()
+    with O.NoiseFeed([noise]):
+        qr, lr = ref(xr)
+    gq, gl = torch.randn(shape), torch.randn(shape)
+    torch.autograd.backward([qr, lr], [gq, gl])
+    xd = x.to(cuda).requires_grad_()
+    set_noise_source(_noise_feed([noise]))
+    try:
+        q, lik = mod(xd)
+    finally:
+        set_noise_source(None)
+    torch.autograd.backward([q, lik], [gq.to(cuda), gl.to(cuda)])
+    if training:
+        assert relerr(q, qr) < 1e-6
+    else:
+        assert torch.equal(q.cpu(), qr.detach())
+    assert relerr(lik, lr) < FP32_TOL
+    assert relerr(xd.grad, xr.grad) < FP32_TOL
+    for (n, a), b in zip(mod.named_parameters(), ref.parameters()):
+        if b.grad is None:
+            assert a.grad is None or a.grad.abs().max() == 0, n
+        else:
+            assert relerr(a.grad, b.grad) < 1e-3, n
+
+
+def test_entropy_bottleneck_aux_loss(cuda):
+    from compressai.entropy_models import EntropyBottleneck
+
+    torch.manual_seed(6)
+    ref = O.EntropyBottleneck(64)
+    with torch.no_grad():
+        ref.quantiles.add_(torch.randn_like(ref.quantiles))
+    mod = EntropyBottleneck(64)
+    mod.load_state_dict(ref.state_dict())
+    mod = mod.to(cuda)
+    lr = ref.loss()
+    lr.backward()
+    l = mod.loss()
+    l.backward()
+    assert l.dim() == 0
+    assert relerr(l, lr) < FP32_TOL
+    assert relerr(mod.quantiles.grad, ref.quantiles.grad) < FP32_TOL
+    assert mod._matrix0.grad is None
+
+
+def test_quantize_modes_bit_exact(cuda):
+    """tests/test_entropy_models.py:54-99 semantics on the HIP quantize kernel."""
+    from compressai.entropy_models import EntropyModel
+
+    em = EntropyModel()
+    x = (torch.rand(1, 3, 4, 4) * 8 - 4)
+    x[0, 0, 0, :] = torch.tensor([0.5, 1.5, -0.5, 2.5])   # half-to-even cases
+    means = torch.rand(1, 3, 4, 4)
+    xd, md = x.to(cuda), means.to(cuda)
+    assert torch.equal(em.quantize(xd, "symbols").cpu(), torch.round(x).int())
+    assert torch.equal(em.quantize(xd, "dequantize", md).cpu(), torch.round(x - means) + means)
+    y = em.quantize(xd, "noise").cpu()
+    assert ((y - x) <= 0.5).all() and ((y - x) >= -0.5).all() and (y != torch.round(x)).any()
+    with pytest.raises(ValueError):
+        em.quantize(xd, "toto")
+
+
+def test_rd_loss(cuda):
+    from compressai.losses import RateDistortionLoss
+
+    torch.manual_seed(7)
+    x = torch.rand(2, 3, 16, 16)
+    xh = torch.rand(2, 3, 16, 16)
+    ly = torch.rand(2, 12, 1, 1) * 0.9 + 0.05
+    lz = torch.rand(2, 8, 1, 1) * 0.9 + 0.05
+    out_r = {"x_hat": xh.clone().requires_grad_(), "likelihoods": {"y": ly.clone().requires_grad_(),
+                                                                    "z": lz.clone().requires_grad_()}}
+    cr = O.RateDistortionLoss(3)(out_r, x)
+    cr["loss"].backward()
+    out_d = {"x_hat": xh.to(cuda).requires_grad_(), "likelihoods": {"y": ly.to(cuda).requires_grad_(),
+                                                                     "z": lz.to(cuda).requires_grad_()}}
+    cd = RateDistortionLoss(3)(out_d, x.to(cuda))
+    cd["loss"].backward()
+    for k in ("loss", "mse_loss", "bpp_loss"):
+        assert abs(cd[k].item() - cr[k].item()) <= 1e-5 * max(1.0, abs(cr[k].item())), k
+    assert relerr(out_d["x_hat"].grad, out_r["x_hat"].grad) < 1e-5
+    assert relerr(out_d["likelihoods"]["y"].grad, out_r["likelihoods"]["y"].grad) < 1e-5
+    assert relerr(out_d["likelihoods"]["z"].grad, out_r["likelihoods"]["z"].grad) < 1e-5
