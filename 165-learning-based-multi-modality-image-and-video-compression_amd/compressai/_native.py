@@ -32,7 +32,8 @@ class EbParams(Structure):
 
 
 class EbGrads(Structure):
-    _fields_ = [("matrix", c_void_p * 5), ("bias", c_void_p * 5), ("factor", c_void_p * 4), ("quantiles", c_void_p)]
+    _fields_ = [("matrix", c_void_p * 5), ("bias", c_void_p * 5), ("factor", c_void_p * 4), ("quantiles", c_void_p),
+                ("accumulate", c_int32)]
 
 
 # name -> (restype, argtypes)
@@ -48,12 +49,12 @@ SIGNATURES = {
     "cai_conv_fwd": (_I, [_G, _I, _P, c_int32, c_int32, _P, _P, c_int32, _F, _P, _I, _I64, _I64, _I64, _I64, _P]),
     "cai_conv_dgrad": (_I, [_G, _I, _P, c_int32, _P, _P, c_int32, c_int32, _F, _P, c_int32, _P]),
     "cai_conv_wgrad_workspace_bytes": (_S, [_G, _I]),
-    "cai_conv_wgrad": (_I, [_G, _I, _P, c_int32, c_int32, c_int32, _P, c_int32, _P, _P, _P, _S, _P]),
+    "cai_conv_wgrad": (_I, [_G, _I, _P, c_int32, c_int32, c_int32, _P, c_int32, _P, _P, c_int32, _P, _S, _P]),
     "cai_gdn_reparam": (_I, [_P, _P, c_int32, _F, _F, _I, _P, _P, _P]),
     "cai_gdn_fwd": (_I, [_I, _P, c_int32, _I64, c_int32, _P, _P, c_int32, _P, c_int32, _P]),
     "cai_gdn_bwd": (_I, [_I, _P, c_int32, _P, c_int32, _I64, c_int32, _P, _P, c_int32, _P, c_int32, _P, _P]),
     "cai_gdn_param_grad_workspace_bytes": (_S, [_I64, c_int32, _I]),
-    "cai_gdn_param_grad": (_I, [_I, _P, c_int32, _P, _I64, c_int32, _P, _P, _F, _F, _P, _P, _P, _S, _P]),
+    "cai_gdn_param_grad": (_I, [_I, _P, c_int32, _P, _I64, c_int32, _P, _P, _F, _F, _P, _P, c_int32, _P, _S, _P]),
     "cai_quantize": (_I, [_I, _I64, c_int32, _P, _I, c_int32, _P, c_int32, c_int32, _P, c_int32, _P, _I, c_int32, _P]),
     "cai_gc_fwd": (_I, [_I, _I64, c_int32, _P, _I, c_int32, _P, c_int32, _P, c_int32, _I, _P, c_int32, _F, _F,
                         _P, _I, c_int32, _P, c_int32, _P]),
@@ -63,7 +64,7 @@ SIGNATURES = {
                         _P, c_int32, _P]),
     "cai_eb_bwd": (_I, [_I, _I64, c_int32, POINTER(EbParams), _P, _I, c_int32, _P, c_int32, _F, _P, c_int32, _P,
                         _I, c_int32, _P, c_int32, POINTER(EbGrads), _P]),
-    "cai_eb_aux_loss": (_I, [c_int32, POINTER(EbParams), _P, _P, _P, _P, _P]),
+    "cai_eb_aux_loss": (_I, [c_int32, POINTER(EbParams), _P, _P, _P, _P, c_int32, _P]),
     "cai_sum_log": (_I, [_P, _I64, c_int32, c_int32, _P, _P, _S, _P]),
     "cai_sum_sqdiff": (_I, [_P, _P, _I64, _P, _P, _S, _P]),
     "cai_reduce_workspace_bytes": (_S, [_I64]),

@@ -33,6 +33,15 @@ _VP = ctypes.c_void_p
 # small helpers
 # ---------------------------------------------------------------------------
 
+DIRECT_GRAD_ATTR = "_cai_direct_grad"
+
+
+def direct_grad(p) -> bool:
+    """True when p.grad is a live fp32 view the kernels may accumulate into (set by optim.FusedAdam)."""
+    return (p is not None and getattr(p, DIRECT_GRAD_ATTR, False) and p.grad is not None
+            and p.grad.dtype == torch.float32 and p.grad.is_contiguous())
+
+
 def _stream() -> _VP:
     return _VP(torch.cuda.current_stream().cuda_stream)
 
@@ -209,6 +218,7 @@ class ConvFn(torch.autograd.Function):
                          spec.act_param, _p(y), ydt, *ys, _stream())
         ctx.spec, ctx.geom, ctx.dt, ctx.xld = spec, g, dt, xld
         ctx.has_bias = bias is not None
+        ctx.params = (weight, bias)
         ctx.save_for_backward(xpm, weight, y if spec.act != ACT_NONE else None)
         return y
 
@@ -238,11 +248,18 @@ class ConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             nbytes = lib.cai_conv_wgrad_workspace_bytes(ctypes.byref(g), code)
             ws = torch.empty(nbytes, dtype=torch.uint8, device=gy.device)
-            dw = torch.empty(weight.shape, dtype=torch.float32, device=gy.device)
-            db = torch.empty(g.out_c, dtype=torch.float32, device=gy.device) if ctx.has_bias else None
+            wparam, bparam = ctx.params
+            direct = direct_grad(wparam) and (bparam is None or direct_grad(bparam))
+            if direct:   # accumulate straight into the optimizer's flat gradient buffer
+                dw, db = wparam.grad, (bparam.grad if bparam is not None else None)
+            else:
+                dw = torch.empty(weight.shape, dtype=torch.float32, device=gy.device)
+                db = torch.empty(g.out_c, dtype=torch.float32, device=gy.device) if ctx.has_bias else None
             lib.cai_conv_wgrad(ctypes.byref(g), code, _p(xpm), ctx.xld, int(spec.in_abs), 0, _p(gpm), gld, _p(dw),
-                               _p(db), _p(ws), nbytes, st)
-            if weight.dtype != torch.float32:
+                               _p(db), int(direct), _p(ws), nbytes, st)
+            if direct:
+                dw = db = None
+            elif weight.dtype != torch.float32:
                 dw = dw.to(weight.dtype)
         return dx, dw, db, None
 
@@ -270,6 +287,7 @@ class GdnFn(torch.autograd.Function):
         lib.cai_gdn_fwd(code, _p(xpm), xld, npix, C, _p(gop), _p(beta), int(inverse), _p(y), C, st)
         ctx.save_for_backward(xpm, br, gr, beta, gop)
         ctx.cfg = (dt, xld, int(inverse), float(beta_min), float(reparam_offset))
+        ctx.params = (beta_raw, gamma_raw)
         return y
 
     @staticmethod
@@ -286,10 +304,17 @@ class GdnFn(torch.autograd.Function):
         lib.cai_gdn_bwd(code, _p(xpm), xld, _p(gpm), gld, npix, C, _p(gop), _p(beta), inverse, _p(dx), C, _p(u), st)
         nbytes = lib.cai_gdn_param_grad_workspace_bytes(npix, C, code)
         ws = torch.empty(nbytes, dtype=torch.uint8, device=gy.device)
-        dbr = torch.empty(C, dtype=torch.float32, device=gy.device)
-        dgr = torch.empty((C, C), dtype=torch.float32, device=gy.device)
+        bp, gp = ctx.params
+        direct = direct_grad(bp) and direct_grad(gp)
+        if direct:
+            dbr, dgr = bp.grad, gp.grad
+        else:
+            dbr = torch.empty(C, dtype=torch.float32, device=gy.device)
+            dgr = torch.empty((C, C), dtype=torch.float32, device=gy.device)
         lib.cai_gdn_param_grad(code, _p(xpm), xld, _p(u), npix, C, _p(br), _p(gr), beta_min, off, _p(dbr), _p(dgr),
-                               _p(ws), nbytes, st)
+                               int(direct), _p(ws), nbytes, st)
+        if direct:
+            dbr = dgr = None
         return dx, dbr, dgr, None, None, None
 
 
@@ -366,6 +391,7 @@ class BottleneckFn(torch.autograd.Function):
                        _p(qbuf), dcode(x.dtype), C, _p(lbuf), C, _stream())
         ctx.save_for_backward(xr, nr, q_, *prm)
         ctx.cfg = (mode, lik_bound, xld, nld, npix, C, x.shape, x.dtype)
+        ctx.params = (quantiles,) + tuple(params)
         return q, lik
 
     @staticmethod
@@ -379,8 +405,12 @@ class BottleneckFn(torch.autograd.Function):
         if gq is not None:
             gq_r, gqld = as_rows(gq)[:2]
         dx, dxb = empty_rows_like(xshape, xdtype, xr.device)
-        grads = [torch.empty_like(p) for p in prm]
-        dq = torch.empty_like(q_)
+        direct = all(direct_grad(p) for p in ctx.params)
+        if direct:
+            dq, grads = ctx.params[0].grad, [p.grad for p in ctx.params[1:]]
+        else:
+            grads = [torch.empty_like(p) for p in prm]
+            dq = torch.empty_like(q_)
         G = EbGrads()
         for i in range(5):
             G.matrix[i] = grads[i].data_ptr()
@@ -388,10 +418,13 @@ class BottleneckFn(torch.autograd.Function):
         for i in range(4):
             G.factor[i] = grads[10 + i].data_ptr()
         G.quantiles = dq.data_ptr()
+        G.accumulate = int(direct)
         P = _eb_params(prm, q_)
         lib.cai_eb_bwd(mode, npix, C, ctypes.byref(P), _p(xr), dcode(xdtype), xld, _p(nr), nld, lb, _p(gl), glld,
                        _p(gq_r), dcode(gq_r.dtype) if gq_r is not None else F32, gqld, _p(dxb), C, ctypes.byref(G),
                        _stream())
+        if direct:
+            return (dx, None, None, None, None, *([None] * len(grads)))
         return (dx, dq, None, None, None, *grads)
 
 
@@ -407,8 +440,9 @@ class BottleneckAuxFn(torch.autograd.Function):
         t = target.float().contiguous()
         loss = torch.empty((), dtype=torch.float32, device=quantiles.device)
         P = _eb_params(prm, q_)
-        lib.cai_eb_aux_loss(C, ctypes.byref(P), _p(t), _p(loss), None, None, _stream())
+        lib.cai_eb_aux_loss(C, ctypes.byref(P), _p(t), _p(loss), None, None, 0, _stream())
         ctx.save_for_backward(q_, t, *prm)
+        ctx.qparam = quantiles
         return loss
 
     @staticmethod
@@ -416,10 +450,11 @@ class BottleneckAuxFn(torch.autograd.Function):
         q_, t, *prm = ctx.saved_tensors
         C = q_.shape[0]
         gl = g.float().contiguous().reshape(())
-        dq = torch.empty_like(q_)
+        direct = direct_grad(ctx.qparam)
+        dq = ctx.qparam.grad if direct else torch.empty_like(q_)
         P = _eb_params(prm, q_)
-        lib.cai_eb_aux_loss(C, ctypes.byref(P), _p(t), None, _p(gl), _p(dq), _stream())
-        return (dq, None, *([None] * len(prm)))
+        lib.cai_eb_aux_loss(C, ctypes.byref(P), _p(t), None, _p(gl), _p(dq), int(direct), _stream())
+        return (None if direct else dq, None, *([None] * len(prm)))
 
 
 # ---------------------------------------------------------------------------

@@ -98,6 +98,8 @@ class EntropyModel(nn.Module):
         self.entropy_coder = entropy_coder
         self.entropy_coder_precision = int(entropy_coder_precision)
         self.use_likelihood_bound = likelihood_bound > 0
+        # python-side copy: kernels take the bound by value (no .item() sync, graph-capturable)
+        self._lik_bound_value = float(likelihood_bound) if self.use_likelihood_bound else 0.0
         if self.use_likelihood_bound:
             self.likelihood_lower_bound = LowerBound(likelihood_bound)
         self.register_buffer("_offset", torch.IntTensor())
@@ -117,7 +119,7 @@ class EntropyModel(nn.Module):
         return self._cdf_length
 
     def _lik_bound(self) -> float:
-        return float(self.likelihood_lower_bound.bound.item()) if self.use_likelihood_bound else 0.0
+        return self._lik_bound_value
 
     def forward(self, *args: Any) -> Any:
         raise NotImplementedError()
@@ -214,6 +216,7 @@ class GaussianConditional(EntropyModel):
         if scale_bound is None or scale_bound <= 0:
             raise ValueError("Invalid parameters")
         self.lower_bound_scale = LowerBound(scale_bound)
+        self._scale_bound_value = float(scale_bound)
         self.register_buffer("scale_table",
                              torch.Tensor(tuple(float(s) for s in scale_table)) if scale_table else torch.Tensor())
         self.register_buffer("scale_bound", torch.Tensor([float(scale_bound)]))
@@ -229,12 +232,12 @@ class GaussianConditional(EntropyModel):
         if scales.shape != inputs.shape or (means is not None and means.shape != inputs.shape):
             raise ValueError("inputs, scales and means must have the same shape")
         noise = _draw_noise(inputs) if training else None
-        sb = float(self.lower_bound_scale.bound.item())
+        sb = self._scale_bound_value
         return GaussianFn.apply(inputs, scales, means, noise, Q_NOISE if training else Q_DEQUANTIZE, sb,
                                 self._lik_bound())
 
     def build_indexes(self, scales: torch.Tensor) -> torch.Tensor:
-        scales = torch.clamp_min(scales, float(self.lower_bound_scale.bound.item()))
+        scales = torch.clamp_min(scales, self._scale_bound_value)
         indexes = scales.new_full(scales.size(), len(self.scale_table) - 1).int()
         for s in self.scale_table[:-1]:
             indexes -= (scales <= s).int()

@@ -591,46 +591,99 @@ __global__ __launch_bounds__(NT, 2) void wgrad_kernel(const WgradArgs a) {
         }
 }
 
-// dw[n][q][kh][kw] = sum_s ws[s][n][(kh*k+kw)*Cq_pad + q]
+// dw[n][q][kh][kw] (+)= sum_s ws[s][n][(kh*k+kw)*Cq_pad + q]
+// Walks the slabs in their memory order (16-byte coalesced reads, split sums
+// in a fixed order: deterministic); the transposed writes are 1/S of the bytes.
 __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int S, int Ng, int ncols, int Cq, int Cq_pad, int k,
-                                    float* __restrict__ dw) {
-    const int64_t total = (int64_t)Ng * Cq * k * k;
+                                    float* __restrict__ dw, int accumulate) {
+    const int c4 = ncols >> 2;
+    const int64_t total = (int64_t)Ng * c4;
+    const int64_t slab = (int64_t)Ng * ncols;
+    const int kk = k * k;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        const int kk = k * k;
-        const int64_t nq = i / kk;
-        const int t = (int)(i - nq * kk);
-        const int n = (int)(nq / Cq), q = (int)(nq - (int64_t)n * Cq);
-        const int64_t col = (int64_t)t * Cq_pad + q;
-        float s = 0.f;
-        for (int sp = 0; sp < S; ++sp) s += ws[((int64_t)sp * Ng + n) * ncols + col];
-        dw[i] = s;
+        const int n = (int)(i / c4);
+        const int col = (int)(i - (int64_t)n * c4) * 4;
+        const f32x4* src = reinterpret_cast<const f32x4*>(ws + (int64_t)n * ncols + col);
+        f32x4 s0 = f32x4{0.f, 0.f, 0.f, 0.f}, s1 = s0;
+        int sp = 0;
+        for (; sp + 1 < S; sp += 2) {
+            s0 += src[(sp * slab) >> 2];
+            s1 += src[((sp + 1) * slab) >> 2];
+        }
+        if (sp < S) s0 += src[(sp * slab) >> 2];
+        s0 += s1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int cc = col + e;
+            const int t = cc / Cq_pad, q = cc - (cc / Cq_pad) * Cq_pad;
+            if (q >= Cq) continue;
+            float* d = dw + ((int64_t)n * Cq + q) * kk + t;
+            *d = accumulate ? *d + s0[e] : s0[e];
+        }
     }
 }
 
-// column sums: stage 1 partials[chunk][c], stage 2 fixed-order sum
+// Column sums of a pixel-major tensor (bias gradients, GDN dbeta).
+// stage 1: a block takes a pixel chunk and all channels: each thread owns one
+// 16-byte channel group and strides over rows (vector loads, fp32 sums), then
+// the rows reduce through LDS -> part[chunk][C].  stage 2: one block per 64
+// channels, 16 waves over the chunks, fixed-order tree: deterministic.
+constexpr int COLSUM_MAXC = 1024;
 template <typename T>
-__global__ void colsum_stage1(const T* __restrict__ g, int64_t npix, int C, int ld, int64_t chunk,
-                              float* __restrict__ part) {
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int r = threadIdx.x >> 6;   // 4 row lanes
-    __shared__ float red[4][64];
-    const int64_t pb = blockIdx.y * chunk;
+__global__ __launch_bounds__(256) void colsum_stage1(const T* __restrict__ g, int64_t npix, int C, int ld,
+                                                     int64_t chunk, float* __restrict__ part) {
+    constexpr int VEC = OpT<T>::VEC;
+    __shared__ float red[256 * VEC];
+    const int cpt = (C + VEC - 1) / VEC;      // channel groups per row
+    const int rows = 256 / cpt;               // rows in flight per pass
+    const int tid = threadIdx.x;
+    const int r = tid / cpt, cg = tid - (tid / cpt) * cpt;
+    const int64_t pb = blockIdx.x * chunk;
     int64_t pe = pb + chunk;
     if (pe > npix) pe = npix;
+    float s[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) s[e] = 0.f;
+    if (r < rows) {
+        for (int64_t p = pb + r; p < pe; p += rows) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(g + p * ld + cg * VEC);
+            if constexpr (VEC == 8) {
+                const bf16x8 h = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) s[e] += (float)h[e];
+            } else {
+                const f32x4 f = __builtin_bit_cast(f32x4, v);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) s[e] += f[e];
+            }
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) red[tid * VEC + e] = (r < rows) ? s[e] : 0.f;
+    __syncthreads();
+    for (int c = tid; c < C; c += 256) {
+        const int g0 = c / VEC, e = c - (c / VEC) * VEC;
+        float acc = 0.f;
+        for (int rr = 0; rr < rows; ++rr) acc += red[(rr * cpt + g0) * VEC + e];
+        part[(int64_t)blockIdx.x * C + c] = acc;
+    }
+}
+__global__ __launch_bounds__(1024) void colsum_stage2(const float* __restrict__ part, int nchunk, int C,
+                                                      float* __restrict__ out, int accumulate) {
+    __shared__ float red[16][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + lane;
     float s = 0.f;
     if (c < C)
-        for (int64_t p = pb + r; p < pe; p += 4) s += to_f32(g[p * ld + c]);
-    red[r][threadIdx.x & 63] = s;
+        for (int i = w; i < nchunk; i += 16) s += part[(int64_t)i * C + c];
+    red[w][lane] = s;
     __syncthreads();
-    if (r == 0 && c < C) part[(int64_t)blockIdx.y * C + c] = red[0][threadIdx.x] + red[1][threadIdx.x] +
-                                                             red[2][threadIdx.x] + red[3][threadIdx.x];
-}
-__global__ void colsum_stage2(const float* __restrict__ part, int nchunk, int C, float* __restrict__ out) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    float s = 0.f;
-    for (int i = 0; i < nchunk; ++i) s += part[(int64_t)i * C + c];
-    out[c] = s;
+    if (w == 0 && c < C) {
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) t += red[i][lane];
+        out[c] = accumulate ? out[c] + t : t;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -791,6 +844,10 @@ struct WgradPlan {
     size_t ws_slab, ws_col;
 };
 
+static int colsum_nchunk(int64_t npix) {
+    return (int)std::max<int64_t>(1, std::min<int64_t>(128, (npix + 511) / 512));
+}
+
 static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype) {
     WgradPlan W{};
     const int VEC = dtype == CAI_BF16 ? 8 : 4;
@@ -812,7 +869,7 @@ static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype) {
     W.ws_slab = (size_t)W.S * W.Ng * W.ncols * sizeof(float);
     // bias grad: columns of the module output gradient
     const int64_t npix_out = (int64_t)g->batch * g->out_h * g->out_w;
-    W.nchunk = (int)std::min<int64_t>(256, (npix_out + 255) / 256);
+    W.nchunk = colsum_nchunk(npix_out);
     W.chunk = (npix_out + W.nchunk - 1) / W.nchunk;
     W.ws_col = (size_t)W.nchunk * g->out_c * sizeof(float);
     return W;
@@ -820,10 +877,10 @@ static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype) {
 
 template <typename T>
 static void launch_colsum(const void* g, int64_t npix, int C, int ld, int nchunk, int64_t chunk, float* part,
-                          float* out, hipStream_t st) {
-    hipLaunchKernelGGL(colsum_stage1<T>, dim3((C + 63) / 64, nchunk), dim3(256), 0, st, reinterpret_cast<const T*>(g),
-                       npix, C, ld, chunk, part);
-    hipLaunchKernelGGL(colsum_stage2, dim3((C + 255) / 256), dim3(256), 0, st, part, nchunk, C, out);
+                          float* out, int accumulate, hipStream_t st) {
+    hipLaunchKernelGGL(colsum_stage1<T>, dim3(nchunk), dim3(256), 0, st, reinterpret_cast<const T*>(g), npix, C, ld,
+                       chunk, part);
+    hipLaunchKernelGGL(colsum_stage2, dim3((C + 63) / 64), dim3(1024), 0, st, part, nchunk, C, out, accumulate);
 }
 
 }  // namespace cai
@@ -907,8 +964,8 @@ size_t cai_conv_wgrad_workspace_bytes(const cai_conv_geom* g, int dtype) {
 }
 
 int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_ld, int32_t in_abs, int32_t in_sq,
-                   const void* dy, int32_t dy_ld, float* dw, float* db, void* workspace, size_t ws_bytes,
-                   void* stream) {
+                   const void* dy, int32_t dy_ld, float* dw, float* db, int32_t accumulate, void* workspace,
+                   size_t ws_bytes, void* stream) {
     int rc = check_geom(g);
     if (rc) return rc;
     CAI_CHECK_ARG(x && dy && dw, "conv_wgrad: null pointer");
@@ -928,6 +985,7 @@ int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_l
     CAI_CHECK_ARG(W.Ng % VEC == 0, "conv_wgrad: gradient-row channels %d must be a multiple of %d", W.Ng, VEC);
     CAI_CHECK_ARG(a.g_ld % VEC == 0 && a.x_ld % VEC == 0 && a.x_ld >= W.Cq_pad && a.g_ld >= W.Ng,
                   "conv_wgrad: bad leading dimensions");
+    CAI_CHECK_ARG(!db || (dy_ld % VEC == 0 && g->out_c <= COLSUM_MAXC), "conv_wgrad: bad bias-gradient layout");
     a.Ng = W.Ng; a.Cq_pad = W.Cq_pad; a.B = g->batch;
     a.k = g->kernel; a.s = g->stride; a.p = g->pad; a.ncols = W.ncols; a.M = W.M; a.split_len = W.split_len;
     float* slab = reinterpret_cast<float*>(workspace);
@@ -938,16 +996,16 @@ int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_l
         hipLaunchKernelGGL(wgrad_kernel<bf16>, grid, dim3(NT), 0, st, a);
     else
         hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(NT), 0, st, a);
-    const int64_t tot = (int64_t)W.Ng * W.Cq * g->kernel * g->kernel;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)std::min<int64_t>(4096, (tot + 255) / 256)), dim3(256), 0,
-                       st, slab, W.S, W.Ng, W.ncols, W.Cq, W.Cq_pad, g->kernel, dw);
+    const int64_t tot = (int64_t)W.Ng * (W.ncols / 4);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)std::min<int64_t>(8192, (tot + 255) / 256)), dim3(256), 0,
+                       st, slab, W.S, W.Ng, W.ncols, W.Cq, W.Cq_pad, g->kernel, dw, accumulate);
     if (db) {
         float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + W.ws_slab);
         const int64_t npix = (int64_t)g->batch * g->out_h * g->out_w;
         if (dtype == CAI_BF16)
-            launch_colsum<bf16>(dy, npix, g->out_c, dy_ld, W.nchunk, W.chunk, part, db, st);
+            launch_colsum<bf16>(dy, npix, g->out_c, dy_ld, W.nchunk, W.chunk, part, db, accumulate, st);
         else
-            launch_colsum<float>(dy, npix, g->out_c, dy_ld, W.nchunk, W.chunk, part, db, st);
+            launch_colsum<float>(dy, npix, g->out_c, dy_ld, W.nchunk, W.chunk, part, db, accumulate, st);
     }
     CAI_LAUNCH_CHECK("conv_wgrad");
     return CAI_OK;
@@ -957,19 +1015,17 @@ int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_l
 
 // exported for gdn.hip (1x1 wgrad on u and x^2, column sums)
 namespace cai {
-int colsum_any(int dtype, const void* g, int64_t npix, int C, int ld, float* out, void* ws, size_t wsb,
-               hipStream_t st) {
-    const int nchunk = (int)std::min<int64_t>(256, (npix + 255) / 256);
+int colsum_any(int dtype, const void* g, int64_t npix, int C, int ld, float* out, int accumulate, void* ws,
+               size_t wsb, hipStream_t st) {
+    const int nchunk = colsum_nchunk(npix);
     const int64_t chunk = (npix + nchunk - 1) / nchunk;
     CAI_CHECK_ARG(wsb >= (size_t)nchunk * C * sizeof(float), "colsum: workspace too small");
+    CAI_CHECK_ARG(C <= COLSUM_MAXC && ld % (dtype == CAI_BF16 ? 8 : 4) == 0, "colsum: bad layout");
     if (dtype == CAI_BF16)
-        launch_colsum<bf16>(g, npix, C, ld, nchunk, chunk, reinterpret_cast<float*>(ws), out, st);
+        launch_colsum<bf16>(g, npix, C, ld, nchunk, chunk, reinterpret_cast<float*>(ws), out, accumulate, st);
     else
-        launch_colsum<float>(g, npix, C, ld, nchunk, chunk, reinterpret_cast<float*>(ws), out, st);
+        launch_colsum<float>(g, npix, C, ld, nchunk, chunk, reinterpret_cast<float*>(ws), out, accumulate, st);
     return CAI_OK;
 }
-size_t colsum_ws_bytes(int64_t npix, int C) {
-    const int nchunk = (int)std::min<int64_t>(256, (npix + 255) / 256);
-    return (size_t)std::max(nchunk, 1) * C * sizeof(float);
-}
+size_t colsum_ws_bytes(int64_t npix, int C) { return (size_t)colsum_nchunk(npix) * C * sizeof(float); }
 }  // namespace cai

@@ -326,40 +326,41 @@ __global__ __launch_bounds__(256) void eb_bwd_kernel(int mode, int64_t npix, int
         g[k] = v;
     }
     if (pl != 0) return;
+#define EB_PUT(dst, val) ((dst) = G.accumulate ? (dst) + (val) : (val))
     // softplus / tanh chain rule and scatter to torch layout (all indices
     // compile-time after unrolling so g[] stays in registers)
 #pragma unroll
-    for (int k = 0; k < 3; ++k) G.matrix[0][c * 3 + k] = g[EB_SP + k] * softplus_grad(P.matrix[0][c * 3 + k]);
+    for (int k = 0; k < 3; ++k) EB_PUT(G.matrix[0][c * 3 + k], g[EB_SP + k] * softplus_grad(P.matrix[0][c * 3 + k]));
 #pragma unroll
     for (int l = 1; l < 4; ++l)
 #pragma unroll
         for (int k = 0; k < 9; ++k)
-            G.matrix[l][c * 9 + k] = g[EB_SP + 3 + (l - 1) * 9 + k] * softplus_grad(P.matrix[l][c * 9 + k]);
+            EB_PUT(G.matrix[l][c * 9 + k], g[EB_SP + 3 + (l - 1) * 9 + k] * softplus_grad(P.matrix[l][c * 9 + k]));
 #pragma unroll
-    for (int k = 0; k < 3; ++k) G.matrix[4][c * 3 + k] = g[EB_SP + 30 + k] * softplus_grad(P.matrix[4][c * 3 + k]);
+    for (int k = 0; k < 3; ++k) EB_PUT(G.matrix[4][c * 3 + k], g[EB_SP + 30 + k] * softplus_grad(P.matrix[4][c * 3 + k]));
 #pragma unroll
     for (int l = 0; l < 4; ++l)
 #pragma unroll
-        for (int k = 0; k < 3; ++k) G.bias[l][c * 3 + k] = g[EB_B + l * 3 + k];
-    G.bias[4][c] = g[EB_B + 12];
+        for (int k = 0; k < 3; ++k) EB_PUT(G.bias[l][c * 3 + k], g[EB_B + l * 3 + k]);
+    EB_PUT(G.bias[4][c], g[EB_B + 12]);
 #pragma unroll
     for (int l = 0; l < 4; ++l)
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const float th = t[EB_TF + l * 3 + k];
-            G.factor[l][c * 3 + k] = g[EB_TF + l * 3 + k] * (1.f - th * th);
+            EB_PUT(G.factor[l][c * 3 + k], g[EB_TF + l * 3 + k] * (1.f - th * th));
         }
     if (G.quantiles) {
-        G.quantiles[c * 3 + 0] = 0.f;
-        G.quantiles[c * 3 + 1] = (mode == CAI_Q_NOISE) ? 0.f : g[EB_MED];
-        G.quantiles[c * 3 + 2] = 0.f;
+        EB_PUT(G.quantiles[c * 3 + 0], 0.f);
+        EB_PUT(G.quantiles[c * 3 + 1], (mode == CAI_Q_NOISE) ? 0.f : g[EB_MED]);
+        EB_PUT(G.quantiles[c * 3 + 2], 0.f);
     }
 }
 
 // aux loss: one block, deterministic
 __global__ __launch_bounds__(1024) void eb_aux_kernel(int C, cai_eb_params P, const float* __restrict__ target,
                                                        float* __restrict__ loss, const float* __restrict__ gloss,
-                                                       float* __restrict__ dq) {
+                                                       float* __restrict__ dq, int accumulate) {
     __shared__ float red[16];
     float acc = 0.f;
     const float gs = gloss ? *gloss : 0.f;
@@ -377,7 +378,8 @@ __global__ __launch_bounds__(1024) void eb_aux_kernel(int C, cai_eb_params P, co
 #pragma unroll
             for (int j = 0; j < EB_NP; ++j) gd[j] = 0.f;
             const float s = (diff > 0.f) ? 1.f : ((diff < 0.f) ? -1.f : 0.f);
-            dq[c * 3 + k] = eb_chain_bwd(qv, gs * s, t, tr, gd);
+            const float v = eb_chain_bwd(qv, gs * s, t, tr, gd);
+            dq[c * 3 + k] = accumulate ? dq[c * 3 + k] + v : v;
         }
     }
     const float r = block_sum<1024>(acc, red);
@@ -557,11 +559,11 @@ int cai_eb_bwd(int mode, int64_t npix, int32_t C, const cai_eb_params* prm, cons
 }
 
 int cai_eb_aux_loss(int32_t C, const cai_eb_params* prm, const float* target, float* loss, const float* g_loss,
-                    float* dquantiles, void* stream) {
+                    float* dquantiles, int32_t accumulate, void* stream) {
     CAI_CHECK_ARG(prm && target && C > 0, "eb_aux_loss: bad arguments");
     CAI_CHECK_ARG(!dquantiles || g_loss, "eb_aux_loss: dquantiles needs g_loss");
     hipLaunchKernelGGL(eb_aux_kernel, dim3(1), dim3(1024), 0, as_stream(stream), C, *prm, target, loss, g_loss,
-                       dquantiles);
+                       dquantiles, accumulate);
     CAI_LAUNCH_CHECK("eb_aux_loss");
     return CAI_OK;
 }

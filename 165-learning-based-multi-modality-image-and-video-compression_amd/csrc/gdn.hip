@@ -25,7 +25,8 @@
 
 namespace cai {
 
-int colsum_any(int dtype, const void* g, int64_t npix, int C, int ld, float* out, void* ws, size_t wsb, hipStream_t st);
+int colsum_any(int dtype, const void* g, int64_t npix, int C, int ld, float* out, int accumulate, void* ws, size_t wsb,
+               hipStream_t st);
 size_t colsum_ws_bytes(int64_t npix, int C);
 
 template <typename T>
@@ -62,8 +63,14 @@ struct GdnGeo {
     static constexpr int RB = C * (int)sizeof(T);   // bytes of one pixel row
     static constexpr int RS = RB + 16;               // padded LDS row stride
     static constexpr int KB = RB / 64;               // 64-byte K blocks per row
-    static constexpr int TN = C / 64;                // 16-col tiles per wave
-    static constexpr int TM = GBM / 16;
+    // 4 waves split WM (pixels) x WN (channels); every wave owns >= one 16-col tile
+    static constexpr int WN = (C % 64 == 0) ? 4 : ((C % 32 == 0) ? 2 : 1);
+    static constexpr int WM = 4 / WN;
+    static constexpr int NW = C / WN;                // channels per wave
+    static constexpr int TN = NW / 16;               // 16-col tiles per wave
+    static constexpr int TM = GBM / (16 * WM);       // 16-row tiles per wave
+    __device__ static int col0(int wave) { return (wave % WN) * NW; }
+    __device__ static int row0(int wave) { return (wave / WN) * (GBM / WM); }
     static constexpr int CHR = RB / 16;              // 16-byte chunks per row
     static constexpr int TILE_CH = GBM * CHR;        // chunks per tile
     static constexpr int CPT = (TILE_CH + GNT - 1) / GNT;
@@ -132,7 +139,7 @@ __device__ __forceinline__ void load_bfrag(BFrags<T, C>& FB, const T* mat, int w
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int tn = 0; tn < G::TN; ++tn) {
-        const int n = wave * (C / 4) + tn * 16 + (lane & 15);
+        const int n = G::col0(wave) + tn * 16 + (lane & 15);
 #pragma unroll
         for (int kb = 0; kb < G::KB; ++kb)
             fb[tn][kb] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(mat + (int64_t)n * C) + kb * 64 +
@@ -141,7 +148,8 @@ __device__ __forceinline__ void load_bfrag(BFrags<T, C>& FB, const T* mat, int w
 }
 
 template <typename T, int C>
-__device__ __forceinline__ void tile_gemm(Acc<T, C>& ACC, const char* lds, const BFrags<T, C>& FB, bool square) {
+__device__ __forceinline__ void tile_gemm(Acc<T, C>& ACC, const char* lds, const BFrags<T, C>& FB, bool square,
+                                          int wave) {
     using G = GdnGeo<T, C>;
     auto& acc = ACC.v;
     const auto& fb = FB.v;
@@ -155,7 +163,7 @@ __device__ __forceinline__ void tile_gemm(Acc<T, C>& ACC, const char* lds, const
         u32x4 fa[G::TM];
 #pragma unroll
         for (int tm = 0; tm < G::TM; ++tm) {
-            const int row = tm * 16 + (lane & 15);
+            const int row = G::row0(wave) + tm * 16 + (lane & 15);
             fa[tm] = *reinterpret_cast<const u32x4*>(lds + row * G::RS + kb * 64 + 16 * (lane >> 4));
         }
 #pragma unroll
@@ -181,7 +189,7 @@ __global__ __launch_bounds__(GNT, sizeof(T) == 2 ? 2 : 1) void gdn_fwd_kernel(co
     load_bfrag<T, C>(fb, gamma, wave);
     float bv[G::TN];
 #pragma unroll
-    for (int tn = 0; tn < G::TN; ++tn) bv[tn] = beta[wave * (C / 4) + tn * 16 + (lane & 15)];
+    for (int tn = 0; tn < G::TN; ++tn) bv[tn] = beta[G::col0(wave) + tn * 16 + (lane & 15)];
 
     const int64_t ntiles = (npix + GBM - 1) / GBM;
     TileRegs<T, C> rx;
@@ -193,17 +201,17 @@ __global__ __launch_bounds__(GNT, sizeof(T) == 2 ? 2 : 1) void gdn_fwd_kernel(co
         const int64_t nxt = tile + gridDim.x;
         if (nxt < ntiles) tile_load<T, C>(rx, x, x_ld, nxt * GBM, npix);
         Acc<T, C> A;
-        tile_gemm<T, C>(A, lds, fb, true);
+        tile_gemm<T, C>(A, lds, fb, true, wave);
         auto& acc = A.v;
         // normalise: out = x * rsqrt(norm)  (or sqrt)
 #pragma unroll
         for (int tm = 0; tm < G::TM; ++tm)
 #pragma unroll
             for (int tn = 0; tn < G::TN; ++tn) {
-                const int col = wave * (C / 4) + tn * 16 + (lane & 15);
+                const int col = G::col0(wave) + tn * 16 + (lane & 15);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int row = tm * 16 + (lane >> 4) * 4 + r;
+                    const int row = G::row0(wave) + tm * 16 + (lane >> 4) * 4 + r;
                     const float xv = to_f32(*lds_elem<T>(lds, G::RS, row, col));
                     const float nv = acc[tm][tn][r] + bv[tn];
                     acc[tm][tn][r] = xv * (inverse ? sqrtf(nv) : rsqrtf(nv));
@@ -214,10 +222,10 @@ __global__ __launch_bounds__(GNT, sizeof(T) == 2 ? 2 : 1) void gdn_fwd_kernel(co
         for (int tm = 0; tm < G::TM; ++tm)
 #pragma unroll
             for (int tn = 0; tn < G::TN; ++tn) {
-                const int col = wave * (C / 4) + tn * 16 + (lane & 15);
+                const int col = G::col0(wave) + tn * 16 + (lane & 15);
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    *lds_elem<T>(lds, G::RS, tm * 16 + (lane >> 4) * 4 + r, col) = from_f32<T>(acc[tm][tn][r]);
+                    *lds_elem<T>(lds, G::RS, G::row0(wave) + tm * 16 + (lane >> 4) * 4 + r, col) = from_f32<T>(acc[tm][tn][r]);
             }
         __syncthreads();
         lds_to_global<T, C>(lds, y, y_ld, tile * GBM, npix);
@@ -239,7 +247,7 @@ __global__ __launch_bounds__(GNT, 1) void gdn_bwd_kernel(const T* __restrict__ x
     const T* gammaT = gamma_op + (int64_t)C * C;
     float bv[G::TN];
 #pragma unroll
-    for (int tn = 0; tn < G::TN; ++tn) bv[tn] = beta[wave * (C / 4) + tn * 16 + (lane & 15)];
+    for (int tn = 0; tn < G::TN; ++tn) bv[tn] = beta[G::col0(wave) + tn * 16 + (lane & 15)];
 
     const int64_t p0 = (int64_t)blockIdx.x * GBM;
     {
@@ -255,17 +263,17 @@ __global__ __launch_bounds__(GNT, 1) void gdn_bwd_kernel(const T* __restrict__ x
     {
         BFrags<T, C> fb;
         load_bfrag<T, C>(fb, gamma_op, wave);
-        tile_gemm<T, C>(A, Lx, fb, true);
+        tile_gemm<T, C>(A, Lx, fb, true, wave);
     }
     // u = dLoss/dnorm into LDS; t1 = g * r (or g * s) replaces g in LDS
 #pragma unroll
     for (int tm = 0; tm < G::TM; ++tm)
 #pragma unroll
         for (int tn = 0; tn < G::TN; ++tn) {
-            const int col = wave * (C / 4) + tn * 16 + (lane & 15);
+            const int col = G::col0(wave) + tn * 16 + (lane & 15);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int row = tm * 16 + (lane >> 4) * 4 + r;
+                const int row = G::row0(wave) + tm * 16 + (lane >> 4) * 4 + r;
                 const float xv = to_f32(*lds_elem<T>(Lx, G::RS, row, col));
                 T* gp = lds_elem<T>(Lg, G::RS, row, col);
                 const float gv = to_f32(*gp);
@@ -289,17 +297,17 @@ __global__ __launch_bounds__(GNT, 1) void gdn_bwd_kernel(const T* __restrict__ x
     {
         BFrags<T, C> fb;
         load_bfrag<T, C>(fb, gammaT, wave);
-        tile_gemm<T, C>(A, Lu, fb, false);
+        tile_gemm<T, C>(A, Lu, fb, false, wave);
     }
     // dx = t1 + 2 x (u gamma)  -> written over t1 in LDS
 #pragma unroll
     for (int tm = 0; tm < G::TM; ++tm)
 #pragma unroll
         for (int tn = 0; tn < G::TN; ++tn) {
-            const int col = wave * (C / 4) + tn * 16 + (lane & 15);
+            const int col = G::col0(wave) + tn * 16 + (lane & 15);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int row = tm * 16 + (lane >> 4) * 4 + r;
+                const int row = G::row0(wave) + tm * 16 + (lane >> 4) * 4 + r;
                 const float xv = to_f32(*lds_elem<T>(Lx, G::RS, row, col));
                 T* gp = lds_elem<T>(Lg, G::RS, row, col);
                 *gp = from_f32<T>(to_f32(*gp) + 2.f * xv * acc[tm][tn][r]);
@@ -330,16 +338,18 @@ __global__ void gdn_reparam_kernel(const float* __restrict__ beta_raw, const flo
 __global__ void gdn_reparam_bwd_kernel(const float* __restrict__ beta_raw, const float* __restrict__ gamma_raw,
                                        const float* __restrict__ dbeta, const float* __restrict__ dgamma, int C,
                                        float bbound, float gbound, float* __restrict__ dbeta_raw,
-                                       float* __restrict__ dgamma_raw) {
+                                       float* __restrict__ dgamma_raw, int accumulate) {
     const int64_t CC = (int64_t)C * C;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < CC; i += (int64_t)gridDim.x * blockDim.x) {
         const float gr = gamma_raw[i];
         const float d = 2.f * fmaxf(gr, gbound) * dgamma[i];
-        dgamma_raw[i] = (gr >= gbound || d < 0.f) ? d : 0.f;
+        const float vg = (gr >= gbound || d < 0.f) ? d : 0.f;
+        dgamma_raw[i] = accumulate ? dgamma_raw[i] + vg : vg;
         if (i < C) {
             const float br = beta_raw[i];
             const float db = 2.f * fmaxf(br, bbound) * dbeta[i];
-            dbeta_raw[i] = (br >= bbound || db < 0.f) ? db : 0.f;
+            const float vb = (br >= bbound || db < 0.f) ? db : 0.f;
+            dbeta_raw[i] = accumulate ? dbeta_raw[i] + vb : vb;
         }
     }
 }
@@ -365,20 +375,24 @@ static void launch_gdn_bwd(const void* x, int x_ld, const void* dy, int dy_ld, i
     do {                                                                       \
         if (dtype == CAI_BF16) {                                               \
             switch (C) {                                                       \
+                case 32: FN<bf16, 32>(__VA_ARGS__); break;                     \
                 case 64: FN<bf16, 64>(__VA_ARGS__); break;                     \
+                case 96: FN<bf16, 96>(__VA_ARGS__); break;                     \
                 case 128: FN<bf16, 128>(__VA_ARGS__); break;                   \
                 case 192: FN<bf16, 192>(__VA_ARGS__); break;                   \
             }                                                                  \
         } else {                                                               \
             switch (C) {                                                       \
+                case 32: FN<float, 32>(__VA_ARGS__); break;                    \
                 case 64: FN<float, 64>(__VA_ARGS__); break;                    \
+                case 96: FN<float, 96>(__VA_ARGS__); break;                    \
                 case 128: FN<float, 128>(__VA_ARGS__); break;                  \
                 case 192: FN<float, 192>(__VA_ARGS__); break;                  \
             }                                                                  \
         }                                                                      \
     } while (0)
 
-static bool gdn_c_ok(int C) { return C == 64 || C == 128 || C == 192; }
+static bool gdn_c_ok(int C) { return C == 32 || C == 64 || C == 96 || C == 128 || C == 192; }
 
 }  // namespace cai
 
@@ -437,7 +451,8 @@ size_t cai_gdn_param_grad_workspace_bytes(int64_t npix, int32_t C, int dtype) {
 
 int cai_gdn_param_grad(int dtype, const void* x, int32_t x_ld, const void* u, int64_t npix, int32_t C,
                        const float* beta_raw, const float* gamma_raw, float beta_min, float reparam_offset,
-                       float* dbeta_raw, float* dgamma_raw, void* workspace, size_t ws_bytes, void* stream) {
+                       float* dbeta_raw, float* dgamma_raw, int32_t accumulate, void* workspace, size_t ws_bytes,
+                       void* stream) {
     CAI_CHECK_ARG(npix > 0 && npix < (1ll << 31), "gdn_param_grad: bad pixel count");
     CAI_CHECK_ARG(ws_bytes >= cai_gdn_param_grad_workspace_bytes(npix, C, dtype), "gdn_param_grad: workspace too small");
     const cai_conv_geom g = gdn_geom(npix, C);
@@ -447,15 +462,16 @@ int cai_gdn_param_grad(int dtype, const void* x, int32_t x_ld, const void* u, in
     float* dbeta = dgamma + (size_t)C * C;
     char* cws = reinterpret_cast<char*>(dbeta + C);
     // dgamma[i][j] = sum_p u[p][i] * x[p][j]^2   (G = u, X = x squared on load)
-    int rc = cai_conv_wgrad(&g, dtype, x, x_ld, 0, 1, u, C, dgamma, nullptr, ws, wgb, stream);
+    int rc = cai_conv_wgrad(&g, dtype, x, x_ld, 0, 1, u, C, dgamma, nullptr, 0, ws, wgb, stream);
     if (rc) return rc;
-    rc = colsum_any(dtype, u, npix, C, C, dbeta, cws, colsum_ws_bytes(npix, C), as_stream(stream));
+    rc = colsum_any(dtype, u, npix, C, C, dbeta, 0, cws, colsum_ws_bytes(npix, C), as_stream(stream));
     if (rc) return rc;
     const float ped = reparam_offset * reparam_offset;
     const float bbound = sqrtf(beta_min + ped), gbound = sqrtf(ped);
     const int64_t CC = (int64_t)C * C;
     hipLaunchKernelGGL(gdn_reparam_bwd_kernel, dim3((unsigned)std::min<int64_t>(1024, (CC + 255) / 256)), dim3(256), 0,
-                       as_stream(stream), beta_raw, gamma_raw, dbeta, dgamma, C, bbound, gbound, dbeta_raw, dgamma_raw);
+                       as_stream(stream), beta_raw, gamma_raw, dbeta, dgamma, C, bbound, gbound, dbeta_raw, dgamma_raw,
+                       accumulate);
     CAI_LAUNCH_CHECK("gdn_param_grad");
     return CAI_OK;
 }

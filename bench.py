@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""Headline benchmark: 256x256 patches/s of one RD-loss training step.
+
+Workload (BASELINE.json configs[1]): bmshj2018-hyperprior (ScaleHyperprior,
+quality 1 -> N=128, M=192), bf16 autocast, 16 synthetic U[0,1) 256x256 RGB
+patches per GPU, one step = forward + RD loss + backward + clip_grad_norm(1.0)
++ Adam (main) + aux-loss backward + Adam (aux), i.e. examples/train.py:155-186.
+Inputs live in HBM before the timed region; the whole step is replayed from
+HIP graphs.  Multi-GPU: one process per GPU (torchrun), per-patch data
+parallelism, one RCCL all-reduce (average) of the flat gradient per step;
+per-GPU batch is fixed (weak scaling) and `value` is the whole-job rate.
+
+Also reported:
+  roofline     -- the dominant kernel timed live with HIP events on its own
+                  stream, algorithmic FLOPs / average launch time vs the bf16
+                  dense MFMA peak (2.5 PFLOP/s);
+  cpu_baseline -- the CPU oracle (op-for-op restatement of the reference path,
+                  fp32) timed on this host on a bounded sample (rank 0, N=1).
+"""
+import argparse
+import ctypes
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "165-learning-based-multi-modality-image-and-video-compression_amd")
+for _p in (PKG, os.path.join(ROOT, "oracle")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=16, help="patches per GPU")
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--model", default="bmshj2018-hyperprior")
+    ap.add_argument("--quality", type=int, default=1)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-batch", type=int, default=2)
+    return ap.parse_args()
+
+
+def dominant_kernel_roofline(B, size, reps=20):
+    """g_a[2]: Conv2d(128,128,k5,s2,p2) at (size/2)^2 -> (size/4)^2, bf16 implicit GEMM."""
+    from compressai._native import BF16, ConvGeom, lib
+    from compressai._ops import _pack_weight, _p
+
+    H = size // 2
+    OH = H // 2
+    g = ConvGeom(B, 128, H, H, 128, OH, OH, 5, 2, 2, 0, 0)
+    dev = torch.device("cuda")
+    x = torch.randn(B, H, H, 128, device=dev).to(torch.bfloat16)
+    w = torch.randn(128, 128, 5, 5, device=dev) * 0.02
+    b = torch.zeros(128, device=dev)
+    y = torch.empty(B, OH, OH, 128, device=dev, dtype=torch.bfloat16)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        from compressai import _ops
+        wp = _pack_weight(g, torch.bfloat16, 0, w)
+        st = ctypes.c_void_p(s.cuda_stream)
+
+        def launch():
+            lib.cai_conv_fwd(ctypes.byref(g), BF16, _p(x), 128, 0, _p(wp), _p(b), 0, 0.0, _p(y), BF16,
+                             OH * OH * 128, 1, OH * 128, 128, st)
+        for _ in range(3):
+            launch()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            launch()
+        e1.record(s)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    flops = 2.0 * (B * OH * OH) * 128 * (25 * 128)
+    tflops = flops / (ms * 1e-3) / 1e12
+    return {"kernel": "conv_gemm_kernel<bf16,128x128> (g_a[2] fwd: Conv2d 128->128 k5 s2, %dx%d->%dx%d, B=%d)"
+                      % (H, H, OH, OH, B),
+            "bound": "mfma", "achieved": round(tflops, 2), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tflops / BF16_PEAK_TFLOPS, 4), "traffic": None, "avg_launch_ms": round(ms, 4),
+            "algorithmic_flop_per_launch": flops}
+
+
+def cpu_baseline(model_name, quality, batch, size, seconds):
+    import cai_oracle as O
+
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    net = O.build(model_name, quality)
+    opt, aux_opt = O.configure_optimizers(net)
+    crit = O.RateDistortionLoss(quality)
+    x = torch.rand(batch, 3, size, size, generator=torch.Generator().manual_seed(0))
+    O.train_step(net, crit, x, opt, aux_opt)           # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        O.train_step(net, crit, x, opt, aux_opt)
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds or n >= 50:
+            break
+    return {"value": round(n * batch / dt, 4), "unit": "patches/s", "cores": threads, "kind": "port",
+            "sample": f"oracle {model_name} q{quality} fp32 train step (fwd+bwd+clip+Adam+aux), batch {batch} "
+                      f"@ {size}x{size}, {n} timed steps after 1 warm-up, torch CPU threads={threads}"}
+
+
+def main():
+    args = parse()
+    from compressai.distributed import allreduce_mean_, broadcast_parameters_, init_from_env
+    from compressai.losses import RateDistortionLoss
+    from compressai.optim import configure_optimizers
+    from compressai.zoo import image_models
+
+    rank, world = init_from_env()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    torch.manual_seed(0)
+    net = image_models[args.model](args.quality).to(dev).train()
+    broadcast_parameters_(net)
+    opt, aux_opt = configure_optimizers(net)
+    criterion = RateDistortionLoss(args.quality)
+    x = torch.rand(args.batch, 3, args.size, args.size, generator=torch.Generator().manual_seed(1234 + rank)).to(dev)
+    state = {}
+
+    def fwd_bwd():
+        opt.zero_grad()
+        aux_opt.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = net(x)
+            crit = criterion(out, x)
+        crit["loss"].backward()
+        state["loss"] = crit["loss"].detach()
+
+    def opt_part():
+        opt.step(max_norm=1.0)
+        aux = net.aux_loss()
+        aux.backward()
+        aux_opt.step()
+
+    def eager_step():
+        fwd_bwd()
+        allreduce_mean_(opt.flat_grad)
+        opt_part()
+
+    step = eager_step
+    if not args.no_graph:
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                eager_step()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        gA, gB = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gA):
+            fwd_bwd()
+        with torch.cuda.graph(gB, pool=gA.pool()):
+            opt_part()
+
+        def step():
+            gA.replay()
+            allreduce_mean_(opt.flat_grad)
+            gB.replay()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    dt = dt.item()
+    loss = float(state["loss"].item())
+    if not math.isfinite(loss):
+        raise RuntimeError(f"non-finite loss {loss}")
+
+    roof = dominant_kernel_roofline(args.batch, args.size) if rank == 0 else None
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(args.model, args.quality, args.cpu_batch, args.size, args.cpu_seconds)
+    if rank == 0:
+        value = world * args.batch * args.steps / dt
+        line = {
+            "metric": METRIC, "value": round(value, 3), "unit": "patches/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic U[0,1) 256x256 RGB patches, random-init weights",
+            "config": {"workload": f"{args.model} q{args.quality} RD-loss training step "
+                                   f"(fwd+bwd+clip+Adam+aux), HIP-graph replay",
+                       "model": args.model, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
+                       "seq_len": None, "patch": args.size, "parallelism": f"dp{world}"},
+            "final_loss": round(loss, 5),
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        if cpu:
+            line["gpu_over_cpu"] = round(value / cpu["value"], 1)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

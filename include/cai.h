@@ -116,17 +116,20 @@ int cai_conv_dgrad(const cai_conv_geom* g, int dtype,
                    int32_t mask_mode, float mask_param, const void* aux, int32_t aux_ld,
                    void* stream);
 
-/* weight / bias gradient (fp32, torch layout, overwritten, not accumulated).
+/* weight / bias gradient (fp32, torch layout; overwritten, or added to the
+ * existing values when accumulate != 0 -- the .grad += semantics of autograd,
+ * used to write straight into an optimizer's flat gradient buffer).
  * x: module input (pixel-major, ld x_ld, in_abs as in forward; in_sq != 0
  * squares it), dy: output gradient (pixel-major, ld dy_ld).  db may be NULL. */
 size_t cai_conv_wgrad_workspace_bytes(const cai_conv_geom* g, int dtype);
 int cai_conv_wgrad(const cai_conv_geom* g, int dtype,
                    const void* x, int32_t x_ld, int32_t in_abs, int32_t in_sq,
                    const void* dy, int32_t dy_ld,
-                   float* dw, float* db, void* workspace, size_t ws_bytes, void* stream);
+                   float* dw, float* db, int32_t accumulate,
+                   void* workspace, size_t ws_bytes, void* stream);
 
 /* =======================================================================
- * GDN / IGDN (layers/gdn.py:41-92), C in {64,128,192}.
+ * GDN / IGDN (layers/gdn.py:41-92), C in {32,64,96,128,192}.
  * ======================================================================= */
 /* beta = max(beta_raw, sqrt(beta_min + ped))^2 - ped ; gamma likewise with
  * bound sqrt(ped); gamma_op is written in the operand dtype in both the
@@ -143,11 +146,12 @@ int cai_gdn_bwd(int dtype, const void* x, int32_t x_ld, const void* dy, int32_t 
                 int64_t npix, int32_t C, const void* gamma_op, const float* beta,
                 int32_t inverse, void* dx, int32_t dx_ld, void* u, void* stream);
 size_t cai_gdn_param_grad_workspace_bytes(int64_t npix, int32_t C, int dtype);
-/* dgamma_raw/dbeta_raw (fp32, overwritten) through the NonNegativeParametrizer
- * / LowerBound backward rule (bound_ops.py:40-42). */
+/* dgamma_raw/dbeta_raw (fp32; overwritten or, accumulate != 0, added) through
+ * the NonNegativeParametrizer / LowerBound backward rule (bound_ops.py:40-42). */
 int cai_gdn_param_grad(int dtype, const void* x, int32_t x_ld, const void* u, int64_t npix, int32_t C,
                        const float* beta_raw, const float* gamma_raw, float beta_min, float reparam_offset,
-                       float* dbeta_raw, float* dgamma_raw, void* workspace, size_t ws_bytes, void* stream);
+                       float* dbeta_raw, float* dgamma_raw, int32_t accumulate,
+                       void* workspace, size_t ws_bytes, void* stream);
 
 /* =======================================================================
  * Entropy models.  Element (p, c) of every operand at ptr[p*ld + c].
@@ -196,13 +200,14 @@ typedef struct cai_eb_grads {
     float* bias[5];
     float* factor[4];
     float* quantiles;   /* medians gradient in DEQUANTIZE mode (nullable) */
+    int32_t accumulate; /* 0: overwrite, 1: add to the existing values */
 } cai_eb_grads;
 
 int cai_eb_fwd(int mode, int64_t npix, int32_t C, const cai_eb_params* prm,
                const void* x, int x_dtype, int32_t x_ld,
                const float* noise, int32_t noise_ld, float lik_bound,
                void* q, int q_dtype, int32_t q_ld, float* lik, int32_t lik_ld, void* stream);
-/* parameter gradients are overwritten (fp32, torch layout). */
+/* parameter gradients (fp32, torch layout) per grads->accumulate. */
 int cai_eb_bwd(int mode, int64_t npix, int32_t C, const cai_eb_params* prm,
                const void* x, int x_dtype, int32_t x_ld,
                const float* noise, int32_t noise_ld, float lik_bound,
@@ -211,7 +216,7 @@ int cai_eb_bwd(int mode, int64_t npix, int32_t C, const cai_eb_params* prm,
 /* aux loss sum_c sum_k |F_c(quantiles[c,k]) - target[k]| -> *loss (fp32 scalar);
  * if dquantiles != NULL also writes d loss / d quantiles scaled by *g_loss. */
 int cai_eb_aux_loss(int32_t C, const cai_eb_params* prm, const float* target,
-                    float* loss, const float* g_loss, float* dquantiles, void* stream);
+                    float* loss, const float* g_loss, float* dquantiles, int32_t accumulate, void* stream);
 
 /* =======================================================================
  * Rate-distortion loss reductions (examples/train.py:68-82).

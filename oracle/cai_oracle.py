@@ -56,8 +56,12 @@ class NoiseFeed:
 
     active: Optional["NoiseFeed"] = None
 
-    def __init__(self, tensors: Sequence[torch.Tensor]):
+    def __init__(self, tensors: Sequence[torch.Tensor] = (), record: Optional[torch.Generator] = None):
+        # record: when the queue is empty, draw from this generator and keep the
+        # draws in .drawn so the identical sequence can be replayed elsewhere
         self._q = list(tensors)
+        self.record = record
+        self.drawn: List[torch.Tensor] = []
 
     def __enter__(self):
         NoiseFeed.active = self
@@ -67,6 +71,10 @@ class NoiseFeed:
         NoiseFeed.active = None
 
     def pop(self, shape) -> torch.Tensor:
+        if not self._q and self.record is not None:
+            t = torch.empty(tuple(shape)).uniform_(-0.5, 0.5, generator=self.record)
+            self.drawn.append(t)
+            return t
         t = self._q.pop(0)
         if tuple(t.shape) != tuple(shape):
             raise ValueError(f"injected noise shape {tuple(t.shape)} != {tuple(shape)}")

@@ -126,7 +126,7 @@ def test_abs_input_fusion(cuda):
 
 @pytest.mark.parametrize("bf16", [False, True])
 @pytest.mark.parametrize("inverse", [False, True])
-@pytest.mark.parametrize("C", [64, 128, 192])
+@pytest.mark.parametrize("C", [32, 64, 96, 128, 192])
 def test_gdn(cuda, C, inverse, bf16):
     from compressai.layers import GDN
 
