@@ -194,6 +194,13 @@ def _pack_weight(g: ConvGeom, dtype, direction: int, weight: torch.Tensor) -> to
     return wp
 
 
+def _conv_ws(g: ConvGeom, dtype, direction: int, device):
+    nbytes = lib.cai_conv_workspace_bytes(ctypes.byref(g), dcode(dtype), direction)
+    if nbytes == 0:
+        return None, 0
+    return torch.empty(nbytes, dtype=torch.uint8, device=device), nbytes
+
+
 class ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, spec: ConvSpec):
@@ -214,8 +221,9 @@ class ConvFn(torch.autograd.Function):
             y = empty_pm(B, cout, g.out_h, g.out_w, dt, x.device)
             ys = (g.out_h * g.out_w * cout, 1, g.out_w * cout, cout)
             ydt = dcode(dt)
+        ws, wsb = _conv_ws(g, dt, 0, x.device)
         lib.cai_conv_fwd(ctypes.byref(g), dcode(dt), _p(xpm), xld, int(spec.in_abs), _p(wp), _p(b), spec.act,
-                         spec.act_param, _p(y), ydt, *ys, _stream())
+                         spec.act_param, _p(y), ydt, *ys, _p(ws), wsb, _stream())
         ctx.spec, ctx.geom, ctx.dt, ctx.xld = spec, g, dt, xld
         ctx.has_bias = bias is not None
         ctx.params = (weight, bias)
@@ -243,8 +251,9 @@ class ConvFn(torch.autograd.Function):
             ldx = (g.in_c + vec - 1) // vec * vec
             dx = empty_pm(g.batch, g.in_c, g.in_h, g.in_w, dt, gy.device, ld=ldx)
             aux = xpm if spec.in_mask != MASK_NONE else None
+            ws, wsb = _conv_ws(g, dt, 1, gy.device)
             lib.cai_conv_dgrad(ctypes.byref(g), code, _p(gpm), gld, _p(wt), _p(dx), ldx, spec.in_mask,
-                               spec.in_mask_param, _p(aux), ctx.xld if aux is not None else 0, st)
+                               spec.in_mask_param, _p(aux), ctx.xld if aux is not None else 0, _p(ws), wsb, st)
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             nbytes = lib.cai_conv_wgrad_workspace_bytes(ctypes.byref(g), code)
             ws = torch.empty(nbytes, dtype=torch.uint8, device=gy.device)

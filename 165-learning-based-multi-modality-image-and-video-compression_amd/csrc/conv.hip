@@ -65,6 +65,9 @@ struct ConvArgs {
     const void* aux;
     int aux_ld, mask_mode;
     float mask_param;
+    int ksplit;              // K splits per phase (grid.z = nphase * ksplit)
+    float* ws;               // split-K partials [nphase*ksplit][ws_rows][ws_ld] fp32
+    int ws_rows, ws_ld;
     PhaseDesc ph[4];
 };
 
@@ -147,6 +150,53 @@ struct U4 {
     u32x4 v[N];
 };
 
+// output-mapping helpers shared by the fused epilogue and the split-K reduce
+template <typename T>
+__device__ __forceinline__ void out_pixel(const ConvArgs& a, const PhaseDesc& P, int plane, int m, int& b, int& oy,
+                                          int& ox) {
+    b = m / plane;
+    const int r = m - b * plane;
+    const int j = r / P.OWg;
+    oy = P.oy0 + a.out_step * j;
+    ox = P.ox0 + a.out_step * (r - j * P.OWg);
+}
+
+template <typename T>
+__device__ __forceinline__ void store_out_chunk(const ConvArgs& a, const PhaseDesc& P, int plane, int m, int n,
+                                                float (&v)[8], int VO) {
+    int b, oy, ox;
+    out_pixel<T>(a, P, plane, m, b, oy, ox);
+    if (a.mask_mode) {
+        const T* AUX = reinterpret_cast<const T*>(a.aux);
+        const int64_t pa = (((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.aux_ld + n;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            if (e < VO) v[e] *= mask_val(a.mask_mode, to_f32(AUX[pa + e]), a.mask_param);
+    }
+    const int64_t off = (int64_t)b * a.ysb + (int64_t)oy * a.ysy + (int64_t)ox * a.ysx + n;
+    if (a.y_dtype == CAI_BF16) {
+        bf16x8 h;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) h[e] = (bf16)v[e];
+        *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(a.y) + off) = h;
+    } else {
+        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.y) + off) = f32x4{v[0], v[1], v[2], v[3]};
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void store_out_scalar(const ConvArgs& a, const PhaseDesc& P, int plane, int m, int n,
+                                                 float v) {
+    int b, oy, ox;
+    out_pixel<T>(a, P, plane, m, b, oy, ox);
+    if (a.mask_mode) {
+        const T* AUX = reinterpret_cast<const T*>(a.aux);
+        v *= mask_val(a.mask_mode, to_f32(AUX[(((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.aux_ld + n]),
+                      a.mask_param);
+    }
+    st_any(a.y, a.y_dtype, (int64_t)b * a.ysb + (int64_t)n * a.ysc + (int64_t)oy * a.ysy + (int64_t)ox * a.ysx, v);
+}
+
 template <typename T, typename C>
 __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(const ConvArgs a) {
     constexpr int BM = C::BM, BN = C::BN, WM = C::WM, WN = C::WN;
@@ -160,10 +210,11 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(const ConvArgs a) {
     using SM = ConvSmem<T, C>;
     __shared__ __attribute__((aligned(16))) char smem[SM::BYTES];
 
-    // select the phase descriptor with uniform branches (a dynamic index into
-    // the by-value kernarg struct would be copied to scratch)
-    const int z = blockIdx.z;
-    const PhaseDesc P = z == 0 ? a.ph[0] : (z == 1 ? a.ph[1] : (z == 2 ? a.ph[2] : a.ph[3]));
+    // grid.z = phase * ksplit + split.  The phase descriptor is selected with
+    // uniform branches (a dynamic index into the by-value kernarg struct would
+    // be copied to scratch).
+    const int ph = blockIdx.z / a.ksplit, split = blockIdx.z - ph * a.ksplit;
+    const PhaseDesc P = ph == 0 ? a.ph[0] : (ph == 1 ? a.ph[1] : (ph == 2 ? a.ph[2] : a.ph[3]));
     const int plane = P.OHg * P.OWg;
     const int Mph = a.B * plane;
     const int m0 = blockIdx.x * BM;
@@ -192,7 +243,6 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(const ConvArgs a) {
         }
     }
     const gptr<T> X = to_global<T>(a.x);
-    // B chunks: row = id/8 of the tile, slot = id%8 == tid%8 (NT multiple of 8)
     const gptr<T> W = to_global<T>(a.w) + P.w_off + slot * VEC;
     int woff[B_CH];
     bool wok[B_CH];
@@ -202,14 +252,20 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(const ConvArgs a) {
         wok[i] = row < BN && n0 + row < a.Npad;
         woff[i] = wok[i] ? (n0 + row) * a.Kp : 0;
     }
-    const int nk = (P.K + BK - 1) / BK;
+    // K-tile range of this split
+    const int nk_all = (P.K + BK - 1) / BK;
+    const int per = (nk_all + a.ksplit - 1) / a.ksplit;
+    const int kt0 = split * per;
+    const int kt1 = min(nk_all, kt0 + per);
+    const int nk = max(0, kt1 - kt0);
     const u32x4 zero = u32x4{0u, 0u, 0u, 0u};
-    U4<A_CH> ra;
-    U4<B_CH> rw;
+    U4<A_CH> ra0, ra1;
+    U4<B_CH> rw0, rw1;
 
-#define CONV_LOAD_TILE(KT)                                                                                   \
+#define CONV_LOAD_TILE(KT, RA, RW)                                                                           \
     {                                                                                                        \
-        const int k_ = (KT) * BK + slot * VEC;                                                               \
+        const int kg_ = kt0 + (KT);                                                                          \
+        const int k_ = kg_ * BK + slot * VEC;                                                                \
         const int t_ = k_ / a.Cin_pad;                                                                       \
         const int ci_ = k_ - t_ * a.Cin_pad;                                                                 \
         const int ty_ = t_ / P.ntx;                                                                          \
@@ -222,26 +278,47 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(const ConvArgs a) {
             const int64_t off = ok ? ((int64_t)(rbase[i] + iy) * a.IW + ix) * a.x_ld + ci_ : 0;             \
             u32x4 v = *reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(X + off);            \
             if (a.in_abs) v = abs_chunk(v, sizeof(T));                                                       \
-            ra.v[i] = ok ? v : zero;                                                                         \
+            RA.v[i] = ok ? v : zero;                                                                         \
         }                                                                                                    \
         _Pragma("unroll") for (int i = 0; i < B_CH; ++i) {                                                   \
-            const u32x4 v = *reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(               \
-                W + woff[i] + (KT) * BK);                                                                    \
-            rw.v[i] = wok[i] ? v : zero;                                                                     \
+            const u32x4 v = *reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(              \
+                W + woff[i] + kg_ * BK);                                                                     \
+            RW.v[i] = wok[i] ? v : zero;                                                                     \
         }                                                                                                    \
     }
 
-#define CONV_STORE_TILE(BUF)                                                                                 \
+#define CONV_STORE_TILE(BUF, RA, RW)                                                                         \
     {                                                                                                        \
         char* As_ = smem + (BUF) * (BM + BN) * 128;                                                          \
         char* Bs_ = As_ + BM * 128;                                                                          \
         _Pragma("unroll") for (int i = 0; i < A_CH; ++i) {                                                   \
             const int row = i * (NT / 8) + (tid >> 3);                                                       \
-            *reinterpret_cast<u32x4*>(As_ + row * 128 + swz(row, slot) * 16) = ra.v[i];                      \
+            *reinterpret_cast<u32x4*>(As_ + row * 128 + swz(row, slot) * 16) = RA.v[i];                      \
         }                                                                                                    \
         _Pragma("unroll") for (int i = 0; i < B_CH; ++i) {                                                   \
             const int row = (i * NT + tid) >> 3;                                                             \
-            if (row < BN) *reinterpret_cast<u32x4*>(Bs_ + row * 128 + swz(row, slot) * 16) = rw.v[i];        \
+            if (row < BN) *reinterpret_cast<u32x4*>(Bs_ + row * 128 + swz(row, slot) * 16) = RW.v[i];        \
+        }                                                                                                    \
+    }
+
+#define CONV_COMPUTE(BUF)                                                                                    \
+    {                                                                                                        \
+        const char* As = smem + (BUF) * (BM + BN) * 128;                                                     \
+        const char* Bs = As + BM * 128;                                                                      \
+        _Pragma("unroll") for (int c = 0; c < 2; ++c) {                                                      \
+            const int ls = c * 4 + (lane >> 4);                                                              \
+            u32x4 fa[TM], fb[TN];                                                                            \
+            _Pragma("unroll") for (int tm = 0; tm < TM; ++tm) {                                              \
+                const int row = wm * WTM + tm * 16 + (lane & 15);                                            \
+                fa[tm] = *reinterpret_cast<const u32x4*>(As + row * 128 + swz(row, ls) * 16);                \
+            }                                                                                                \
+            _Pragma("unroll") for (int tn = 0; tn < TN; ++tn) {                                              \
+                const int row = wn * WTN + tn * 16 + (lane & 15);                                            \
+                fb[tn] = *reinterpret_cast<const u32x4*>(Bs + row * 128 + swz(row, ls) * 16);                \
+            }                                                                                                \
+            _Pragma("unroll") for (int tm = 0; tm < TM; ++tm)                                                \
+                _Pragma("unroll") for (int tn = 0; tn < TN; ++tn)                                            \
+                    acc[tm][tn] = mma16<T>(fa[tm], fb[tn], acc[tm][tn]);                                     \
         }                                                                                                    \
     }
 
@@ -251,44 +328,55 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(const ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    CONV_LOAD_TILE(0);
-    CONV_STORE_TILE(0);
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-        const bool more = kt + 1 < nk;
-        if (more) CONV_LOAD_TILE(kt + 1);
-        {
-            const char* As = smem + (kt & 1) * (BM + BN) * 128;
-            const char* Bs = As + BM * 128;
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                const int ls = c * 4 + (lane >> 4);
-                u32x4 fa[TM], fb[TN];
-#pragma unroll
-                for (int tm = 0; tm < TM; ++tm) {
-                    const int row = wm * WTM + tm * 16 + (lane & 15);
-                    fa[tm] = *reinterpret_cast<const u32x4*>(As + row * 128 + swz(row, ls) * 16);
-                }
-#pragma unroll
-                for (int tn = 0; tn < TN; ++tn) {
-                    const int row = wn * WTN + tn * 16 + (lane & 15);
-                    fb[tn] = *reinterpret_cast<const u32x4*>(Bs + row * 128 + swz(row, ls) * 16);
-                }
-#pragma unroll
-                for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-                    for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mma16<T>(fa[tm], fb[tn], acc[tm][tn]);
-            }
-        }
-        if (more) CONV_STORE_TILE((kt + 1) & 1);
+    // 2-deep register prefetch: tile t+2 is in flight while tile t is
+    // computed and tile t+1 is written to the other LDS buffer.
+    if (nk > 0) {
+        CONV_LOAD_TILE(0, ra0, rw0);
+        CONV_STORE_TILE(0, ra0, rw0);
+        if (nk > 1) CONV_LOAD_TILE(1, ra1, rw1);
         __syncthreads();
+        for (int kt = 0; kt < nk; kt += 2) {
+            if (kt + 2 < nk) CONV_LOAD_TILE(kt + 2, ra0, rw0);
+            CONV_COMPUTE(0);
+            if (kt + 1 < nk) CONV_STORE_TILE(1, ra1, rw1);
+            __syncthreads();
+            if (kt + 1 >= nk) break;
+            if (kt + 3 < nk) CONV_LOAD_TILE(kt + 3, ra1, rw1);
+            CONV_COMPUTE(1);
+            if (kt + 2 < nk) CONV_STORE_TILE(0, ra0, rw0);
+            __syncthreads();
+        }
     }
 #undef CONV_LOAD_TILE
 #undef CONV_STORE_TILE
+#undef CONV_COMPUTE
 
-    // ---- epilogue: acc (+bias, act) -> LDS fp32 [BM][BN+4] ----
     float* E = reinterpret_cast<float*>(smem);
     constexpr int ES = SM::EPI_STRIDE;
+    if (a.ksplit > 1) {
+        // ---- split-K: raw fp32 partial tile -> ws[z][m][n] (bias/act/mask in the reduce) ----
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                const int col = wn * WTN + tn * 16 + (lane & 15);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) E[(wm * WTM + tm * 16 + (lane >> 4) * 4 + r) * ES + col] = acc[tm][tn][r];
+            }
+        __syncthreads();
+        float* dst = a.ws + (int64_t)blockIdx.z * a.ws_rows * a.ws_ld;
+        constexpr int cpr = BN / 4;
+        for (int id = tid; id < BM * cpr; id += NT) {
+            const int row = id / cpr, cc = id - (id / cpr) * cpr;
+            const int m = m0 + row, n = n0 + cc * 4;
+            if (m >= Mph || n >= a.ws_ld) continue;
+            *reinterpret_cast<f32x4*>(dst + (int64_t)m * a.ws_ld + n) =
+                *reinterpret_cast<const f32x4*>(E + row * ES + cc * 4);
+        }
+        return;
+    }
+
+    // ---- epilogue: acc (+bias, act) -> LDS fp32 [BM][BN+4] -> 16-byte stores ----
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
@@ -303,56 +391,68 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(const ConvArgs a) {
             }
         }
     __syncthreads();
-
-    const T* AUX = reinterpret_cast<const T*>(a.aux);
     if (a.y_vec) {
-        const bool obf = a.y_dtype == CAI_BF16;
-        const int VO = obf ? 8 : 4;
+        const int VO = a.y_dtype == CAI_BF16 ? 8 : 4;
         const int cpr = BN / VO;
         for (int id = tid; id < BM * cpr; id += NT) {
             const int row = id / cpr, cc = id - (id / cpr) * cpr;
             const int m = m0 + row, n = n0 + cc * VO;
             if (m >= Mph || n >= a.Cout) continue;
-            const int b = m / plane;
-            const int r = m - b * plane;
-            const int j = r / P.OWg;
-            const int oy = P.oy0 + a.out_step * j, ox = P.ox0 + a.out_step * (r - j * P.OWg);
+            float v[8];
             const f32x4 lo = *reinterpret_cast<const f32x4*>(E + row * ES + cc * VO);
             f32x4 hi = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (obf) hi = *reinterpret_cast<const f32x4*>(E + row * ES + cc * VO + 4);
-            float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            if (a.mask_mode) {
-                const int64_t pa = (((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.aux_ld + n;
-#pragma unroll
-                for (int e = 0; e < 8; ++e)
-                    if (e < VO) v[e] *= mask_val(a.mask_mode, to_f32(AUX[pa + e]), a.mask_param);
-            }
-            const int64_t off = (int64_t)b * a.ysb + (int64_t)oy * a.ysy + (int64_t)ox * a.ysx + n;
-            if (obf) {
-                bf16x8 h;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) h[e] = (bf16)v[e];
-                *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(a.y) + off) = h;
-            } else {
-                *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.y) + off) = f32x4{v[0], v[1], v[2], v[3]};
-            }
+            if (VO == 8) hi = *reinterpret_cast<const f32x4*>(E + row * ES + cc * VO + 4);
+            v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+            v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+            store_out_chunk<T>(a, P, plane, m, n, v, VO);
         }
     } else {
         for (int id = tid; id < BM * BN; id += NT) {
             const int col = id / BM, row = id - (id / BM) * BM;
             const int m = m0 + row, n = n0 + col;
             if (m >= Mph || n >= a.Cout) continue;
-            const int b = m / plane;
-            const int r = m - b * plane;
-            const int j = r / P.OWg;
-            const int oy = P.oy0 + a.out_step * j, ox = P.ox0 + a.out_step * (r - j * P.OWg);
-            float v = E[row * ES + col];
-            if (a.mask_mode) {
-                const int64_t pa = (((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.aux_ld + n;
-                v *= mask_val(a.mask_mode, to_f32(AUX[pa]), a.mask_param);
+            store_out_scalar<T>(a, P, plane, m, n, E[row * ES + col]);
+        }
+    }
+}
+
+// split-K reduce: out = epilogue(sum_s ws[ph*S + s][m][n]) in a fixed order
+template <typename T>
+__global__ __launch_bounds__(256) void conv_splitk_reduce_kernel(const ConvArgs a) {
+    const int ph = blockIdx.y;
+    const PhaseDesc P = ph == 0 ? a.ph[0] : (ph == 1 ? a.ph[1] : (ph == 2 ? a.ph[2] : a.ph[3]));
+    const int plane = P.OHg * P.OWg;
+    const int Mph = a.B * plane;
+    const int VO = (a.y_vec && a.y_dtype == CAI_BF16) ? 8 : 4;
+    const int cpr = (a.Cout + VO - 1) / VO;
+    const int64_t total = (int64_t)Mph * cpr;
+    const int64_t slab = (int64_t)a.ws_rows * a.ws_ld;
+    for (int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; id < total;
+         id += (int64_t)gridDim.x * blockDim.x) {
+        const int m = (int)(id / cpr);
+        const int n = (int)(id - (int64_t)m * cpr) * VO;
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        const float* src = a.ws + ((int64_t)ph * a.ksplit) * slab + (int64_t)m * a.ws_ld + n;
+        for (int s = 0; s < a.ksplit; ++s) {
+            const f32x4 lo = *reinterpret_cast<const f32x4*>(src + s * slab);
+            v[0] += lo[0]; v[1] += lo[1]; v[2] += lo[2]; v[3] += lo[3];
+            if (VO == 8) {
+                const f32x4 hi = *reinterpret_cast<const f32x4*>(src + s * slab + 4);
+                v[4] += hi[0]; v[5] += hi[1]; v[6] += hi[2]; v[7] += hi[3];
             }
-            st_any(a.y, a.y_dtype, (int64_t)b * a.ysb + (int64_t)n * a.ysc + (int64_t)oy * a.ysy + (int64_t)ox * a.ysx,
-                   v);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int nn = n + e;
+            const float bv = (a.bias && nn < a.Cout) ? a.bias[nn] : 0.f;
+            v[e] = apply_act(v[e] + bv, a.act, a.act_param);
+        }
+        if (a.y_vec) {
+            store_out_chunk<T>(a, P, plane, m, n, v, VO);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (n + e < a.Cout) store_out_scalar<T>(a, P, plane, m, n + e, v[e]);
         }
     }
 }
@@ -419,7 +519,18 @@ struct WgradArgs {
     int64_t M;
     int64_t split_len;
     float* ws;
+    int ctiles, rtiles, nsub, grp_len;
 };
+
+constexpr int WG_CHUNK = 1024;   // pixels per L2-resident wgrad chunk (multiple of 64)
+
+// bijective XCD remap (cdna_hip_programming.md T1): physical workgroup id ->
+// logical id such that logical ids [x*q, (x+1)*q) run on one XCD
+__device__ __forceinline__ int xcd_remap(int wgid, int nwg) {
+    const int xcd = wgid & 7, idx = wgid >> 3;
+    const int q = nwg >> 3, r = nwg & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
 
 // LDS byte offset of 16-byte slot `slot` of row `row` in a [32][256 B] bf16 image
 // read by ds_read_b64_tr_b16 (rows 8g+q of a half-wave land on distinct slots)
@@ -437,7 +548,7 @@ __device__ __forceinline__ s16x4 ds_tr16(const char* base, int byte_off) {
 template <typename T>
 __global__ __launch_bounds__(NT, 2) void wgrad_kernel(const WgradArgs a) {
     constexpr int VEC = OpT<T>::VEC;
-    constexpr int BKP = 32;                       // pixels per K-step
+    constexpr int BKP = sizeof(T) == 2 ? 64 : 32;  // pixels per K-step
     constexpr int ROWB = 128 * (int)sizeof(T);    // bytes per LDS row (128 channels)
     constexpr int CPR = ROWB / 16;                // 16-byte chunks per row
     constexpr int CH = BKP * CPR / NT;            // chunks per thread per operand
@@ -446,19 +557,37 @@ __global__ __launch_bounds__(NT, 2) void wgrad_kernel(const WgradArgs a) {
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid >> 1, wn = wid & 1;
-    const int c0 = blockIdx.x * 128;   // column tile (tap, q)
-    const int r0 = blockIdx.y * 128;   // row tile (G channel)
-    const int64_t mbeg = (int64_t)blockIdx.z * a.split_len;
-    int64_t mend = mbeg + a.split_len;
-    if (mend > a.M) mend = a.M;
-    if (mbeg >= mend) {
+    // Pixel partition (speed only -- any placement is correct): workgroups
+    // b and b+8 share an XCD, so group g = b % 8 owns pixel range g of 8; its
+    // workgroups (all tap/channel tiles x nsub) walk that range in 1024-pixel
+    // chunks, sub k taking chunks k, k+nsub, ...  The tiles working on one
+    // chunk gather the same pixels at about the same time from one L2.
+    const int grp = (int)(blockIdx.x & 7);
+    const int w = (int)(blockIdx.x >> 3);
+    const int ctile = w % a.ctiles;
+    const int rtile = (w / a.ctiles) % a.rtiles;
+    const int sub = w / (a.ctiles * a.rtiles);
+    const int split = grp * a.nsub + sub;
+    const int c0 = ctile * 128;        // column tile (tap, q)
+    const int r0 = rtile * 128;        // row tile (G channel)
+    // pixel indices fit in 32 bits (M < 2^31 is checked on the host)
+    const int gbeg = min((int)a.M, grp * a.grp_len);
+    const int gend = min((int)a.M, gbeg + a.grp_len);
+    const int nchunk = (gend - gbeg + WG_CHUNK - 1) / WG_CHUNK;
+    int nsteps = 0;   // 64-pixel steps of this workgroup
+    for (int c = sub; c < nchunk; c += a.nsub)
+        nsteps += (min(gend, gbeg + (c + 1) * WG_CHUNK) - (gbeg + c * WG_CHUNK) + BKP - 1) / BKP;
+    if (nsteps == 0) {
         // empty split: still write zeros so the reduce reads defined data
         for (int id = tid; id < 128 * 128; id += NT) {
             const int rr = r0 + id / 128, cc = c0 + (id & 127);
-            if (rr < a.Ng && cc < a.ncols) a.ws[((int64_t)blockIdx.z * a.Ng + rr) * a.ncols + cc] = 0.f;
+            if (rr < a.Ng && cc < a.ncols) a.ws[((int64_t)split * a.Ng + rr) * a.ncols + cc] = 0.f;
         }
         return;
     }
+    constexpr int SPC = WG_CHUNK / BKP;   // steps per chunk
+    // first pixel of step st (this sub's chunks in order; the last chunk may be short)
+    auto step_base = [&](int st) { return gbeg + (sub + (st / SPC) * a.nsub) * WG_CHUNK + (st % SPC) * BKP; };
 
     // this thread's fixed chunk column
     const int cc = tid % CPR;
@@ -469,51 +598,44 @@ __global__ __launch_bounds__(NT, 2) void wgrad_kernel(const WgradArgs a) {
     const bool xvalid = xcol < a.ncols;
     const bool gvalid = gcol < a.Ng;
     const int plane = a.Hg * a.Wg;
-
-    const T* G = reinterpret_cast<const T*>(a.g);
-    const T* X = reinterpret_cast<const T*>(a.x);
-    u32x4 rg[CH], rx[CH];
+    const gptr<T> G = to_global<T>(a.g);
+    const gptr<T> X = to_global<T>(a.x);
     const u32x4 zero = u32x4{0u, 0u, 0u, 0u};
+    U4<CH> rg0, rx0;
 
-    auto load = [&](int64_t mb) {
-#pragma unroll
-        for (int i = 0; i < CH; ++i) {
-            const int row = i * (NT / CPR) + tid / CPR;
-            const int64_t m = mb + row;
-            rg[i] = zero;
-            rx[i] = zero;
-            if (m < mend) {
-                if (gvalid) rg[i] = *reinterpret_cast<const u32x4*>(G + m * a.g_ld + gcol);
-                if (xvalid) {
-                    const int b = (int)(m / plane);
-                    const int r = (int)(m - (int64_t)b * plane);
-                    const int j = r / a.Wg;
-                    const int iy = j * a.s - a.p + xkh, ix = (r - j * a.Wg) * a.s - a.p + xkw;
-                    if ((unsigned)iy < (unsigned)a.Hx && (unsigned)ix < (unsigned)a.Wx) {
-                        u32x4 v = *reinterpret_cast<const u32x4*>(X + (((int64_t)b * a.Hx + iy) * a.Wx + ix) * a.x_ld + xq);
-                        if (a.in_abs) v = abs_chunk(v, sizeof(T));
-                        if (a.in_sq) v = sq_chunk<T>(v);
-                        rx[i] = v;
-                    }
-                }
-            }
-        }
-    };
-    auto store = [&](int buf) {
-        char* Gs = smem + buf * 2 * OPB;
-        char* Xs = Gs + OPB;
-#pragma unroll
-        for (int i = 0; i < CH; ++i) {
-            const int row = i * (NT / CPR) + tid / CPR;
-            int off;
-            if constexpr (sizeof(T) == 2)
-                off = trswz(row, cc);
-            else
-                off = row * ROWB + cc * 16;
-            *reinterpret_cast<u32x4*>(Gs + off) = rg[i];
-            *reinterpret_cast<u32x4*>(Xs + off) = rx[i];
-        }
-    };
+#define WG_LOAD(MB, RG, RX)                                                                                  \
+    {                                                                                                        \
+        _Pragma("unroll") for (int i = 0; i < CH; ++i) {                                                     \
+            const int row = i * (NT / CPR) + tid / CPR;                                                      \
+            const int m = (MB) + row;                                                                        \
+            const bool mok = m < gend && (m - gbeg) / WG_CHUNK == ((MB) - gbeg) / WG_CHUNK;                  \
+            const int mm = mok ? m : gbeg;                                                                   \
+            const u32x4 gv = *reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(              \
+                G + (int64_t)mm * a.g_ld + (gvalid ? gcol : 0));                                             \
+            RG.v[i] = (mok && gvalid) ? gv : zero;                                                           \
+            const int b = mm / plane;                                                                        \
+            const int r = mm - b * plane;                                                                    \
+            const int j = r / a.Wg;                                                                          \
+            const int iy = j * a.s - a.p + xkh, ix = (r - j * a.Wg) * a.s - a.p + xkw;                       \
+            const bool ok = mok && xvalid && (unsigned)iy < (unsigned)a.Hx && (unsigned)ix < (unsigned)a.Wx; \
+            const int64_t off = ok ? (((int64_t)b * a.Hx + iy) * a.Wx + ix) * a.x_ld + xq : 0;               \
+            u32x4 v = *reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(X + off);            \
+            if (a.in_abs) v = abs_chunk(v, sizeof(T));                                                       \
+            if (a.in_sq) v = sq_chunk<T>(v);                                                                 \
+            RX.v[i] = ok ? v : zero;                                                                         \
+        }                                                                                                    \
+    }
+#define WG_STORE(BUF, RG, RX)                                                                                \
+    {                                                                                                        \
+        char* Gs_ = smem + (BUF) * 2 * OPB;                                                                  \
+        char* Xs_ = Gs_ + OPB;                                                                               \
+        _Pragma("unroll") for (int i = 0; i < CH; ++i) {                                                     \
+            const int row = i * (NT / CPR) + tid / CPR;                                                      \
+            const int off = (sizeof(T) == 2) ? trswz(row, cc) : row * ROWB + cc * 16;                        \
+            *reinterpret_cast<u32x4*>(Gs_ + off) = RG.v[i];                                                  \
+            *reinterpret_cast<u32x4*>(Xs_ + off) = RX.v[i];                                                  \
+        }                                                                                                    \
+    }
 
     f32x4 acc[4][4];
 #pragma unroll
@@ -521,62 +643,66 @@ __global__ __launch_bounds__(NT, 2) void wgrad_kernel(const WgradArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    auto compute = [&](int buf) {
-        const char* Gs = smem + buf * 2 * OPB;
-        const char* Xs = Gs + OPB;
-        if constexpr (sizeof(T) == 2) {
-            const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p4 = i16 & 3;
-            u32x4 fa[4], fb[4];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int colA = wm * 64 + t * 16 + 4 * p4;   // element column (G channel within tile)
-                const int colB = wn * 64 + t * 16 + 4 * p4;
-                s16x4 a0 = ds_tr16(Gs, trswz(8 * g + q, colA >> 3) + ((colA & 7) << 1));
-                s16x4 a1 = ds_tr16(Gs, trswz(8 * g + 4 + q, colA >> 3) + ((colA & 7) << 1));
-                s16x4 b0 = ds_tr16(Xs, trswz(8 * g + q, colB >> 3) + ((colB & 7) << 1));
-                s16x4 b1 = ds_tr16(Xs, trswz(8 * g + 4 + q, colB >> 3) + ((colB & 7) << 1));
-                s16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-                s16x8 bv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
-                fa[t] = __builtin_bit_cast(u32x4, av);
-                fb[t] = __builtin_bit_cast(u32x4, bv);
-            }
-#pragma unroll
-            for (int tm = 0; tm < 4; ++tm)
-#pragma unroll
-                for (int tn = 0; tn < 4; ++tn) acc[tm][tn] = mma16<bf16>(fa[tm], fb[tn], acc[tm][tn]);
-        } else {
-            const float* Gf = reinterpret_cast<const float*>(Gs);
-            const float* Xf = reinterpret_cast<const float*>(Xs);
-#pragma unroll
-            for (int ks = 0; ks < BKP / 4; ++ks) {
-                const int row = ks * 4 + (lane >> 4);
-                float fa[4], fb[4];
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    fa[t] = Gf[row * 128 + wm * 64 + t * 16 + (lane & 15)];
-                    fb[t] = Xf[row * 128 + wn * 64 + t * 16 + (lane & 15)];
-                }
-#pragma unroll
-                for (int tm = 0; tm < 4; ++tm)
-#pragma unroll
-                    for (int tn = 0; tn < 4; ++tn)
-                        acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[tm], fb[tn], acc[tm][tn], 0, 0, 0);
-            }
-        }
-    };
-
-    const int nsteps = (int)((mend - mbeg + BKP - 1) / BKP);
-    load(mbeg);
-    store(0);
-    __syncthreads();
-    for (int st = 0; st < nsteps; ++st) {
-        if (st + 1 < nsteps) load(mbeg + (int64_t)(st + 1) * BKP);
-        compute(st & 1);
-        if (st + 1 < nsteps) store((st + 1) & 1);
-        __syncthreads();
+#define WG_COMPUTE(BUF)                                                                                      \
+    {                                                                                                        \
+        const char* Gs = smem + (BUF) * 2 * OPB;                                                             \
+        const char* Xs = Gs + OPB;                                                                           \
+        if constexpr (sizeof(T) == 2) {                                                                      \
+            const int g_ = lane >> 4, i16 = lane & 15, q_ = i16 >> 2, p4 = i16 & 3;                          \
+            _Pragma("unroll") for (int ks = 0; ks < BKP / 32; ++ks) {                                        \
+                const int r0_ = 32 * ks + 8 * g_ + q_;                                                       \
+                u32x4 fb[4];                                                                                 \
+                _Pragma("unroll") for (int t = 0; t < 4; ++t) {                                              \
+                    const int colB = wn * 64 + t * 16 + 4 * p4;                                              \
+                    s16x4 b0 = ds_tr16(Xs, trswz(r0_, colB >> 3) + ((colB & 7) << 1));                      \
+                    s16x4 b1 = ds_tr16(Xs, trswz(r0_ + 4, colB >> 3) + ((colB & 7) << 1));                  \
+                    s16x8 bv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};                     \
+                    fb[t] = __builtin_bit_cast(u32x4, bv);                                                   \
+                }                                                                                            \
+                _Pragma("unroll") for (int tm = 0; tm < 4; ++tm) {                                           \
+                    const int colA = wm * 64 + tm * 16 + 4 * p4;                                             \
+                    s16x4 a0 = ds_tr16(Gs, trswz(r0_, colA >> 3) + ((colA & 7) << 1));                      \
+                    s16x4 a1 = ds_tr16(Gs, trswz(r0_ + 4, colA >> 3) + ((colA & 7) << 1));                  \
+                    s16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};                     \
+                    const u32x4 fa = __builtin_bit_cast(u32x4, av);                                          \
+                    _Pragma("unroll") for (int tn = 0; tn < 4; ++tn)                                         \
+                        acc[tm][tn] = mma16<bf16>(fa, fb[tn], acc[tm][tn]);                                  \
+                }                                                                                            \
+            }                                                                                                \
+        } else {                                                                                             \
+            const float* Gf = reinterpret_cast<const float*>(Gs);                                            \
+            const float* Xf = reinterpret_cast<const float*>(Xs);                                           \
+            _Pragma("unroll") for (int ks = 0; ks < BKP / 4; ++ks) {                                         \
+                const int row = ks * 4 + (lane >> 4);                                                        \
+                float fa[4], fb[4];                                                                          \
+                _Pragma("unroll") for (int t = 0; t < 4; ++t) {                                              \
+                    fa[t] = Gf[row * 128 + wm * 64 + t * 16 + (lane & 15)];                                  \
+                    fb[t] = Xf[row * 128 + wn * 64 + t * 16 + (lane & 15)];                                  \
+                }                                                                                            \
+                _Pragma("unroll") for (int tm = 0; tm < 4; ++tm)                                             \
+                    _Pragma("unroll") for (int tn = 0; tn < 4; ++tn)                                         \
+                        acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[tm], fb[tn], acc[tm][tn], 0, 0, 0); \
+            }                                                                                                \
+        }                                                                                                    \
     }
 
-    float* out = a.ws + (int64_t)blockIdx.z * a.Ng * a.ncols;
+    // one register set in flight: tile st+1 loads while tile st is computed
+    // (64-pixel steps keep 32 MFMAs per wave between barriers)
+    WG_LOAD(step_base(0), rg0, rx0);
+    WG_STORE(0, rg0, rx0);
+    __syncthreads();
+    for (int st = 0; st < nsteps; ++st) {
+        const bool more = st + 1 < nsteps;
+        if (more) WG_LOAD(step_base(st + 1), rg0, rx0);
+        WG_COMPUTE(st & 1);
+        if (more) WG_STORE((st + 1) & 1, rg0, rx0);
+        __syncthreads();
+    }
+#undef WG_LOAD
+#undef WG_STORE
+#undef WG_COMPUTE
+
+    float* out = a.ws + (int64_t)split * a.Ng * a.ncols;
 #pragma unroll
     for (int tm = 0; tm < 4; ++tm)
 #pragma unroll
@@ -592,34 +718,38 @@ __global__ __launch_bounds__(NT, 2) void wgrad_kernel(const WgradArgs a) {
 }
 
 // dw[n][q][kh][kw] (+)= sum_s ws[s][n][(kh*k+kw)*Cq_pad + q]
-// Walks the slabs in their memory order (16-byte coalesced reads, split sums
-// in a fixed order: deterministic); the transposed writes are 1/S of the bytes.
-__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int S, int Ng, int ncols, int Cq, int Cq_pad, int k,
-                                    float* __restrict__ dw, int accumulate) {
+// Block = 16 float4 column groups x 16 split groups: reads walk the slabs in
+// memory order (256-byte runs), the 16 split partials meet in LDS in a fixed
+// order (deterministic); the transposed writes are 1/S of the bytes.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int S, int Ng, int ncols,
+                                                           int Cq, int Cq_pad, int k, float* __restrict__ dw,
+                                                           int accumulate) {
+    __shared__ f32x4 red[16][16];
     const int c4 = ncols >> 2;
     const int64_t total = (int64_t)Ng * c4;
-    const int64_t slab = (int64_t)Ng * ncols;
-    const int kk = k * k;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        const int n = (int)(i / c4);
-        const int col = (int)(i - (int64_t)n * c4) * 4;
-        const f32x4* src = reinterpret_cast<const f32x4*>(ws + (int64_t)n * ncols + col);
-        f32x4 s0 = f32x4{0.f, 0.f, 0.f, 0.f}, s1 = s0;
-        int sp = 0;
-        for (; sp + 1 < S; sp += 2) {
-            s0 += src[(sp * slab) >> 2];
-            s1 += src[((sp + 1) * slab) >> 2];
-        }
-        if (sp < S) s0 += src[(sp * slab) >> 2];
-        s0 += s1;
+    const int64_t slab4 = ((int64_t)Ng * ncols) >> 2;
+    const int cg = threadIdx.x & 15, sg = threadIdx.x >> 4;
+    const int64_t i = (int64_t)blockIdx.x * 16 + cg;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (i < total) {
+        const f32x4* src = reinterpret_cast<const f32x4*>(ws) + i;
+        for (int sp = sg; sp < S; sp += 16) acc += src[sp * slab4];
+    }
+    red[sg][cg] = acc;
+    __syncthreads();
+    if (sg != 0 || i >= total) return;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int cc = col + e;
-            const int t = cc / Cq_pad, q = cc - (cc / Cq_pad) * Cq_pad;
-            if (q >= Cq) continue;
-            float* d = dw + ((int64_t)n * Cq + q) * kk + t;
-            *d = accumulate ? *d + s0[e] : s0[e];
-        }
+    for (int j = 1; j < 16; ++j) acc += red[j][cg];
+    const int n = (int)(i / c4);
+    const int col = (int)(i - (int64_t)n * c4) * 4;
+    const int kk = k * k;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int cc = col + e;
+        const int t = cc / Cq_pad, q = cc - (cc / Cq_pad) * Cq_pad;
+        if (q >= Cq) continue;
+        float* d = dw + ((int64_t)n * Cq + q) * kk + t;
+        *d = accumulate ? *d + acc[e] : acc[e];
     }
 }
 
@@ -665,25 +795,18 @@ __global__ __launch_bounds__(256) void colsum_stage1(const T* __restrict__ g, in
         const int g0 = c / VEC, e = c - (c / VEC) * VEC;
         float acc = 0.f;
         for (int rr = 0; rr < rows; ++rr) acc += red[(rr * cpt + g0) * VEC + e];
-        part[(int64_t)blockIdx.x * C + c] = acc;
+        part[(int64_t)c * gridDim.x + blockIdx.x] = acc;
     }
 }
-__global__ __launch_bounds__(1024) void colsum_stage2(const float* __restrict__ part, int nchunk, int C,
-                                                      float* __restrict__ out, int accumulate) {
-    __shared__ float red[16][64];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int c = blockIdx.x * 64 + lane;
+__global__ __launch_bounds__(256) void colsum_stage2(const float* __restrict__ part, int nchunk, int C,
+                                                     float* __restrict__ out, int accumulate) {
+    const int lane = threadIdx.x & 63;
+    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= C) return;
     float s = 0.f;
-    if (c < C)
-        for (int i = w; i < nchunk; i += 16) s += part[(int64_t)i * C + c];
-    red[w][lane] = s;
-    __syncthreads();
-    if (w == 0 && c < C) {
-        float t = 0.f;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) t += red[i][lane];
-        out[c] = accumulate ? out[c] + t : t;
-    }
+    for (int i = lane; i < nchunk; i += 64) s += part[(int64_t)c * nchunk + i];
+    s = wave_sum(s);
+    if (lane == 0) out[c] = accumulate ? out[c] + s : s;
 }
 
 // ---------------------------------------------------------------------------
@@ -767,44 +890,93 @@ static Plan make_plan(const cai_conv_geom* g, int dtype, int direction) {
     return P;
 }
 
-template <typename T, typename C>
-static void launch_conv(const ConvArgs& a, int mmax, hipStream_t st) {
-    dim3 grid((mmax + C::BM - 1) / C::BM, (a.Cout + C::BN - 1) / C::BN, a.nphase);
-    hipLaunchKernelGGL((conv_gemm_kernel<T, C>), grid, dim3(NT), 0, st, a);
-}
-
 using CfgL = Cfg<128, 128, 2, 2>;
 using CfgW = Cfg<64, 192, 1, 4>;
 using CfgM = Cfg<128, 64, 2, 2>;
 using CfgS = Cfg<256, 16, 4, 1>;
 
+enum { CFG_L, CFG_W, CFG_M, CFG_S };
+
+static int pick_cfg(int C, int& BM, int& BN) {
+    int id;
+    if (C <= 16) id = CFG_S;
+    else if (C <= 64) id = CFG_M;
+    else if (C % 128 != 0 && (C % 192 == 0 || C % 192 > 128 || (C > 128 && C <= 192))) id = CFG_W;
+    else id = CFG_L;
+    static const int bm[] = {128, 64, 128, 256}, bn[] = {128, 192, 64, 16};
+    BM = bm[id];
+    BN = bn[id];
+    return id;
+}
+
+// Launch geometry of one conv call: tiles, split-K factor and its workspace.
+struct ConvLaunch {
+    int cfg, BM, BN, mtiles, ntiles, mmax, ksplit, ws_ld;
+    size_t ws_bytes;
+};
+
+static ConvLaunch conv_launch(const cai_conv_geom* g, int dtype, int direction) {
+    const Plan P = make_plan(g, dtype, direction);
+    ConvLaunch L{};
+    L.cfg = pick_cfg(P.kout_c, L.BM, L.BN);
+    int kmax = 0;
+    for (int ph = 0; ph < P.nphase; ++ph) {
+        L.mmax = std::max(L.mmax, g->batch * P.OHg[ph] * P.OWg[ph]);
+        kmax = std::max(kmax, P.ntaps[ph] * P.Cin_pad);
+    }
+    L.mtiles = (L.mmax + L.BM - 1) / L.BM;
+    L.ntiles = (P.kout_c + L.BN - 1) / L.BN;
+    const int tiles = L.mtiles * L.ntiles * P.nphase;
+    const int nk = (kmax + 128 / dtype_size(dtype) - 1) / (128 / dtype_size(dtype));
+    // split K when the tile grid cannot fill the 256 CUs (small spatial layers);
+    // each split keeps >= 4 K-tiles so the 2-deep prefetch still has work to hide
+    int ks = 1;
+    if (tiles < 256) ks = std::min({(512 + tiles - 1) / tiles, std::max(1, nk / 4), 16});
+    L.ksplit = std::max(1, ks);
+    L.ws_ld = L.ntiles * L.BN;
+    L.ws_bytes = L.ksplit > 1 ? (size_t)P.nphase * L.ksplit * L.mmax * L.ws_ld * sizeof(float) : 0;
+    return L;
+}
+
+template <typename T, typename C>
+static void launch_conv(const ConvArgs& a, const ConvLaunch& L, hipStream_t st) {
+    dim3 grid(L.mtiles, L.ntiles, a.nphase * a.ksplit);
+    hipLaunchKernelGGL((conv_gemm_kernel<T, C>), grid, dim3(NT), 0, st, a);
+    if (a.ksplit > 1) {
+        const int VO = (a.y_vec && a.y_dtype == CAI_BF16) ? 8 : 4;
+        const int64_t total = (int64_t)L.mmax * ((a.Cout + VO - 1) / VO);
+        const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, (total + 255) / 256));
+        hipLaunchKernelGGL((conv_splitk_reduce_kernel<T>), dim3(gx, a.nphase), dim3(256), 0, st, a);
+    }
+}
+
 template <typename T>
-static void dispatch_conv(const ConvArgs& a, int mmax, hipStream_t st) {
-    const int C = a.Cout;
-    if (C <= 16)
-        launch_conv<T, CfgS>(a, mmax, st);
-    else if (C <= 64)
-        launch_conv<T, CfgM>(a, mmax, st);
-    else if (C % 128 != 0 && (C % 192 == 0 || C % 192 > 128 || (C > 128 && C <= 192)))
-        launch_conv<T, CfgW>(a, mmax, st);
-    else
-        launch_conv<T, CfgL>(a, mmax, st);
+static void dispatch_conv(const ConvArgs& a, const ConvLaunch& L, hipStream_t st) {
+    switch (L.cfg) {
+        case CFG_S: launch_conv<T, CfgS>(a, L, st); break;
+        case CFG_M: launch_conv<T, CfgM>(a, L, st); break;
+        case CFG_W: launch_conv<T, CfgW>(a, L, st); break;
+        default: launch_conv<T, CfgL>(a, L, st); break;
+    }
 }
 
 static int run_conv(const cai_conv_geom* g, int dtype, int direction, const void* x, int x_ld, int in_abs,
                     const void* w, const float* bias, int act, float act_param, void* y, int y_dtype, int64_t ysb,
                     int64_t ysc, int64_t ysy, int64_t ysx, const void* aux, int aux_ld, int mask_mode,
-                    float mask_param, void* stream, const char* name) {
+                    float mask_param, void* workspace, size_t ws_bytes, void* stream, const char* name) {
     int rc = check_geom(g);
     if (rc) return rc;
     CAI_CHECK_ARG(dtype == CAI_BF16 || dtype == CAI_F32, "%s: bad dtype", name);
     CAI_CHECK_ARG(x && w && y, "%s: null pointer", name);
     const Plan P = make_plan(g, dtype, direction);
+    const ConvLaunch L = conv_launch(g, dtype, direction);
     const int VEC = dtype == CAI_BF16 ? 8 : 4;
     CAI_CHECK_ARG(x_ld >= P.Cin_pad && x_ld % VEC == 0, "%s: input ld %d must be >= %d and a multiple of %d", name,
                   x_ld, P.Cin_pad, VEC);
     CAI_CHECK_ARG(((uintptr_t)x & 15) == 0, "%s: input not 16-byte aligned", name);
     CAI_CHECK_ARG(!mask_mode || (aux && aux_ld >= P.kout_c), "%s: mask needs aux", name);
+    CAI_CHECK_ARG(L.ws_bytes == 0 || (workspace && ws_bytes >= L.ws_bytes && ((uintptr_t)workspace & 15) == 0),
+                  "%s: workspace of %zu bytes required", name, L.ws_bytes);
     ConvArgs a{};
     a.x = x; a.B = g->batch; a.IH = P.in_h; a.IW = P.in_w; a.x_ld = x_ld; a.Cin_pad = P.Cin_pad; a.in_abs = in_abs;
     a.w = w; a.Kp = P.Kp; a.Npad = P.Npad; a.nphase = P.nphase;
@@ -818,26 +990,25 @@ static int run_conv(const cai_conv_geom* g, int dtype, int direction, const void
                ((uintptr_t)y & 15) == 0);
     a.bias = bias; a.act = act; a.act_param = act_param;
     a.aux = aux; a.aux_ld = aux_ld; a.mask_mode = mask_mode; a.mask_param = mask_param;
-    int mmax = 0;
+    a.ksplit = L.ksplit; a.ws = reinterpret_cast<float*>(workspace); a.ws_rows = L.mmax; a.ws_ld = L.ws_ld;
     for (int ph = 0; ph < P.nphase; ++ph) {
         PhaseDesc& d = a.ph[ph];
         d.oy0 = P.oy0[ph]; d.ox0 = P.ox0[ph]; d.OHg = P.OHg[ph]; d.OWg = P.OWg[ph];
         d.ntaps = P.ntaps[ph]; d.ntx = P.ntx[ph]; d.dy0 = P.dy0[ph]; d.dx0 = P.dx0[ph];
         d.K = P.ntaps[ph] * P.Cin_pad;
         d.w_off = (int64_t)ph * P.Npad * P.Kp;
-        mmax = std::max(mmax, g->batch * d.OHg * d.OWg);
     }
-    if (mmax == 0) return CAI_OK;
+    if (L.mmax == 0) return CAI_OK;
     if (dtype == CAI_BF16)
-        dispatch_conv<bf16>(a, mmax, as_stream(stream));
+        dispatch_conv<bf16>(a, L, as_stream(stream));
     else
-        dispatch_conv<float>(a, mmax, as_stream(stream));
+        dispatch_conv<float>(a, L, as_stream(stream));
     CAI_LAUNCH_CHECK(name);
     return CAI_OK;
 }
 
 struct WgradPlan {
-    int Ng, Cq, Cq_pad, ncols, S;
+    int Ng, Cq, Cq_pad, ncols, S, nsub, grp_len;
     int64_t M, split_len;
     int nchunk;
     int64_t chunk;
@@ -845,7 +1016,7 @@ struct WgradPlan {
 };
 
 static int colsum_nchunk(int64_t npix) {
-    return (int)std::max<int64_t>(1, std::min<int64_t>(128, (npix + 511) / 512));
+    return (int)std::max<int64_t>(1, std::min<int64_t>(1024, (npix + 255) / 256));
 }
 
 static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype) {
@@ -861,11 +1032,15 @@ static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype) {
     W.Cq_pad = round_up(W.Cq, VEC);
     W.ncols = g->kernel * g->kernel * W.Cq_pad;
     const int tiles = ((W.ncols + 127) / 128) * ((W.Ng + 127) / 128);
-    int64_t S = std::max<int64_t>(1, 640 / tiles);
-    const int64_t maxS = std::max<int64_t>(1, W.M / (32 * 16));   // >= 16 K-steps per split
-    S = std::min(S, maxS);
-    W.split_len = ((W.M + S - 1) / S + 31) / 32 * 32;
-    W.S = (int)((W.M + W.split_len - 1) / W.split_len);
+    // 8 pixel groups (one per XCD) x nsub workgroups per tile and group:
+    // >= ~512 workgroups, >= 8 steps of 64 pixels per workgroup
+    const int64_t per_grp = (W.M + 7) / 8;
+    int nsub = std::max(1, (512 + 8 * tiles - 1) / (8 * tiles));
+    nsub = (int)std::max<int64_t>(1, std::min<int64_t>(nsub, per_grp / 512));
+    W.nsub = nsub;
+    W.grp_len = (int)((per_grp + 63) / 64 * 64);
+    W.S = 8 * nsub;
+    W.split_len = 0;
     W.ws_slab = (size_t)W.S * W.Ng * W.ncols * sizeof(float);
     // bias grad: columns of the module output gradient
     const int64_t npix_out = (int64_t)g->batch * g->out_h * g->out_w;
@@ -880,7 +1055,7 @@ static void launch_colsum(const void* g, int64_t npix, int C, int ld, int nchunk
                           float* out, int accumulate, hipStream_t st) {
     hipLaunchKernelGGL(colsum_stage1<T>, dim3(nchunk), dim3(256), 0, st, reinterpret_cast<const T*>(g), npix, C, ld,
                        chunk, part);
-    hipLaunchKernelGGL(colsum_stage2, dim3((C + 63) / 64), dim3(1024), 0, st, part, nchunk, C, out, accumulate);
+    hipLaunchKernelGGL(colsum_stage2, dim3((C + 3) / 4), dim3(256), 0, st, part, nchunk, C, out, accumulate);
 }
 
 }  // namespace cai
@@ -939,22 +1114,27 @@ int cai_pack_nchw(const float* x, int32_t B, int32_t C, int32_t H, int32_t W, in
     return CAI_OK;
 }
 
+size_t cai_conv_workspace_bytes(const cai_conv_geom* g, int dtype, int direction) {
+    if (check_geom(g)) return 0;
+    return conv_launch(g, dtype, direction).ws_bytes;
+}
+
 int cai_conv_fwd(const cai_conv_geom* g, int dtype, const void* x, int32_t x_ld, int32_t in_abs, const void* packed_w,
                  const float* bias, int32_t act, float act_param, void* y, int y_dtype, int64_t ysb, int64_t ysc,
-                 int64_t ysy, int64_t ysx, void* stream) {
+                 int64_t ysy, int64_t ysx, void* workspace, size_t ws_bytes, void* stream) {
     return run_conv(g, dtype, 0, x, x_ld, in_abs, packed_w, bias, act, act_param, y, y_dtype, ysb, ysc, ysy, ysx,
-                    nullptr, 0, CAI_MASK_NONE, 0.f, stream, "conv_fwd");
+                    nullptr, 0, CAI_MASK_NONE, 0.f, workspace, ws_bytes, stream, "conv_fwd");
 }
 
 int cai_conv_dgrad(const cai_conv_geom* g, int dtype, const void* dy, int32_t dy_ld, const void* packed_wt, void* dx,
                    int32_t dx_ld, int32_t mask_mode, float mask_param, const void* aux, int32_t aux_ld,
-                   void* stream) {
+                   void* workspace, size_t ws_bytes, void* stream) {
     int rc = check_geom(g);
     if (rc) return rc;
     const int64_t ld = dx_ld;
     return run_conv(g, dtype, 1, dy, dy_ld, 0, packed_wt, nullptr, CAI_ACT_NONE, 0.f, dx, dtype,
                     (int64_t)g->in_h * g->in_w * ld, 1, (int64_t)g->in_w * ld, ld, aux, aux_ld, mask_mode,
-                    mask_param, stream, "conv_dgrad");
+                    mask_param, workspace, ws_bytes, stream, "conv_dgrad");
 }
 
 size_t cai_conv_wgrad_workspace_bytes(const cai_conv_geom* g, int dtype) {
@@ -983,6 +1163,7 @@ int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_l
         CAI_CHECK_ARG(!in_abs && !in_sq, "conv_wgrad: input transforms only for Conv2d");
     }
     CAI_CHECK_ARG(W.Ng % VEC == 0, "conv_wgrad: gradient-row channels %d must be a multiple of %d", W.Ng, VEC);
+    CAI_CHECK_ARG(W.M < (1ll << 31), "conv_wgrad: too many pixels");
     CAI_CHECK_ARG(a.g_ld % VEC == 0 && a.x_ld % VEC == 0 && a.x_ld >= W.Cq_pad && a.g_ld >= W.Ng,
                   "conv_wgrad: bad leading dimensions");
     CAI_CHECK_ARG(!db || (dy_ld % VEC == 0 && g->out_c <= COLSUM_MAXC), "conv_wgrad: bad bias-gradient layout");
@@ -990,14 +1171,18 @@ int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_l
     a.k = g->kernel; a.s = g->stride; a.p = g->pad; a.ncols = W.ncols; a.M = W.M; a.split_len = W.split_len;
     float* slab = reinterpret_cast<float*>(workspace);
     a.ws = slab;
-    dim3 grid((W.ncols + 127) / 128, (W.Ng + 127) / 128, W.S);
+    a.ctiles = (W.ncols + 127) / 128;
+    a.rtiles = (W.Ng + 127) / 128;
+    a.nsub = W.nsub;
+    a.grp_len = W.grp_len;
+    dim3 grid(8 * a.ctiles * a.rtiles * a.nsub);
     hipStream_t st = as_stream(stream);
     if (dtype == CAI_BF16)
         hipLaunchKernelGGL(wgrad_kernel<bf16>, grid, dim3(NT), 0, st, a);
     else
         hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(NT), 0, st, a);
     const int64_t tot = (int64_t)W.Ng * (W.ncols / 4);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)std::min<int64_t>(8192, (tot + 255) / 256)), dim3(256), 0,
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((tot + 15) / 16)), dim3(256), 0,
                        st, slab, W.S, W.Ng, W.ncols, W.Cq, W.Cq_pad, g->kernel, dw, accumulate);
     if (db) {
         float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + W.ws_slab);

@@ -75,7 +75,7 @@ def dominant_kernel_roofline(B, size, reps=20):
 
         def launch():
             lib.cai_conv_fwd(ctypes.byref(g), BF16, _p(x), 128, 0, _p(wp), _p(b), 0, 0.0, _p(y), BF16,
-                             OH * OH * 128, 1, OH * 128, 128, st)
+                             OH * OH * 128, 1, OH * 128, 128, None, 0, st)
         for _ in range(3):
             launch()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -97,6 +97,11 @@ int cai_conv_pack_weight(const cai_conv_geom* g, int dtype, int direction,
 int cai_pack_nchw(const float* x, int32_t B, int32_t C, int32_t H, int32_t W,
                   int dtype, void* out, int32_t ld, void* stream);
 
+/* Scratch for split-K (small spatial layers whose tile grid cannot fill the
+ * GPU split the reduction dimension over workgroups and reduce the fp32
+ * partials in a fixed order); 0 when the call does not split. */
+size_t cai_conv_workspace_bytes(const cai_conv_geom* g, int dtype, int direction);
+
 /* forward: y = act(conv(x) + bias).  x: pixel-major input with ld x_ld
  * (x_ld >= in_c, multiple of 8 elements);  in_abs != 0 reads |x|.
  * y is written at y_ptr[b*ysb + c*ysc + oy*ysy + ox*ysx] (element strides);
@@ -106,7 +111,7 @@ int cai_conv_fwd(const cai_conv_geom* g, int dtype,
                  const void* packed_w, const float* bias,
                  int32_t act, float act_param,
                  void* y, int y_dtype, int64_t ysb, int64_t ysc, int64_t ysy, int64_t ysx,
-                 void* stream);
+                 void* workspace, size_t ws_bytes, void* stream);
 
 /* input gradient: dx = mask(aux) * conv_input_grad(dy).  dy pixel-major
  * (ld dy_ld), dx pixel-major (ld dx_ld), aux pixel-major (ld aux_ld) or NULL. */
@@ -114,7 +119,7 @@ int cai_conv_dgrad(const cai_conv_geom* g, int dtype,
                    const void* dy, int32_t dy_ld, const void* packed_wt,
                    void* dx, int32_t dx_ld,
                    int32_t mask_mode, float mask_param, const void* aux, int32_t aux_ld,
-                   void* stream);
+                   void* workspace, size_t ws_bytes, void* stream);
 
 /* weight / bias gradient (fp32, torch layout; overwritten, or added to the
  * existing values when accumulate != 0 -- the .grad += semantics of autograd,

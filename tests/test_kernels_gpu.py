@@ -43,6 +43,9 @@ CONV_CASES = [
     ("deconv", 2, 128, 3, 16, 16, 5, 2),
     ("deconv", 2, 128, 192, 5, 7, 5, 2),
     ("deconv", 1, 96, 64, 6, 6, 3, 1),
+    # large pixel counts: several 1024-pixel chunks per XCD group in wgrad
+    ("conv", 4, 64, 64, 160, 150, 5, 2),
+    ("deconv", 3, 64, 32, 70, 90, 5, 2),
 ]
 
 
