@@ -201,6 +201,45 @@ def _conv_ws(g: ConvGeom, dtype, direction: int, device):
     return torch.empty(nbytes, dtype=torch.uint8, device=device), nbytes
 
 
+def _small_deconv(spec: ConvSpec, g: ConvGeom, xld: int, dtype) -> bool:
+    """Few-output-channel ConvTranspose2d (x_hat layer): csrc/deconv_small.hip."""
+    return (spec.transposed and spec.out_nchw32 and g.out_c <= 16 and spec.act == ACT_NONE and not spec.in_abs
+            and spec.in_mask == MASK_NONE and g.in_c % 8 == 0 and xld % 8 == 0
+            and lib.cai_deconv_small_workspace_bytes(ctypes.byref(g), dcode(dtype)) > 0)
+
+
+def _small_ws(g: ConvGeom, dtype, device):
+    nbytes = lib.cai_deconv_small_workspace_bytes(ctypes.byref(g), dcode(dtype))
+    return torch.empty(nbytes, dtype=torch.uint8, device=device), nbytes
+
+
+def _small_deconv_bwd(ctx, xpm, weight, gy):
+    g, dt = ctx.geom, ctx.dt
+    gy = gy.float().contiguous()
+    dx = dw = db = None
+    if ctx.needs_input_grad[0]:
+        ldx = (g.in_c + _vec(dt) - 1) // _vec(dt) * _vec(dt)
+        dx = empty_pm(g.batch, g.in_c, g.in_h, g.in_w, dt, gy.device, ld=ldx)
+    want_w = ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2])
+    wparam, bparam = ctx.params
+    direct = want_w and direct_grad(wparam) and (bparam is None or direct_grad(bparam))
+    if want_w:
+        if direct:
+            dw, db = wparam.grad, (bparam.grad if bparam is not None else None)
+        else:
+            dw = torch.empty(weight.shape, dtype=torch.float32, device=gy.device)
+            db = torch.empty(g.out_c, dtype=torch.float32, device=gy.device) if ctx.has_bias else None
+    ws, wsb = _small_ws(g, dt, gy.device)
+    lib.cai_deconv_small_bwd(ctypes.byref(g), dcode(dt), _p(xpm), ctx.xld, _p(weight.detach().float().contiguous()),
+                             _p(gy), _p(dx), ldx if dx is not None else 0, _p(dw), _p(db), int(direct), _p(ws), wsb,
+                             _stream())
+    if direct:
+        dw = db = None
+    elif dw is not None and weight.dtype != torch.float32:
+        dw = dw.to(weight.dtype)
+    return dx, dw, db, None
+
+
 class ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, spec: ConvSpec):
@@ -211,7 +250,6 @@ class ConvFn(torch.autograd.Function):
         cout = weight.shape[1] if spec.transposed else weight.shape[0]
         g = conv_geom(spec, B, cin, H, W, cout)
         xpm, xld = to_pm(x, dt, vec)
-        wp = _pack_weight(g, dt, 0, weight)
         b = bias.detach().float().contiguous() if bias is not None else None
         if spec.out_nchw32:
             y = torch.empty((B, cout, g.out_h, g.out_w), dtype=torch.float32, device=x.device)
@@ -221,9 +259,16 @@ class ConvFn(torch.autograd.Function):
             y = empty_pm(B, cout, g.out_h, g.out_w, dt, x.device)
             ys = (g.out_h * g.out_w * cout, 1, g.out_w * cout, cout)
             ydt = dcode(dt)
-        ws, wsb = _conv_ws(g, dt, 0, x.device)
-        lib.cai_conv_fwd(ctypes.byref(g), dcode(dt), _p(xpm), xld, int(spec.in_abs), _p(wp), _p(b), spec.act,
-                         spec.act_param, _p(y), ydt, *ys, _p(ws), wsb, _stream())
+        ctx.small = _small_deconv(spec, g, xld, dt)
+        if ctx.small:   # few output channels: per-input-pixel GEMM + col2im (csrc/deconv_small.hip)
+            ws, wsb = _small_ws(g, dt, x.device)
+            lib.cai_deconv_small_fwd(ctypes.byref(g), dcode(dt), _p(xpm), xld, _p(weight.detach().float().contiguous()),
+                                     _p(b), _p(y), _p(ws), wsb, _stream())
+        else:
+            wp = _pack_weight(g, dt, 0, weight)
+            ws, wsb = _conv_ws(g, dt, 0, x.device)
+            lib.cai_conv_fwd(ctypes.byref(g), dcode(dt), _p(xpm), xld, int(spec.in_abs), _p(wp), _p(b), spec.act,
+                             spec.act_param, _p(y), ydt, *ys, _p(ws), wsb, _stream())
         ctx.spec, ctx.geom, ctx.dt, ctx.xld = spec, g, dt, xld
         ctx.has_bias = bias is not None
         ctx.params = (weight, bias)
@@ -237,6 +282,8 @@ class ConvFn(torch.autograd.Function):
         vec = _vec(dt)
         code = dcode(dt)
         st = _stream()
+        if ctx.small:
+            return _small_deconv_bwd(ctx, xpm, weight, gy)
         gpm, gld = to_pm(gy, dt, vec)
         if spec.act != ACT_NONE and not spec.act_bwd_downstream:
             mode = 1 if spec.act == 1 else 2

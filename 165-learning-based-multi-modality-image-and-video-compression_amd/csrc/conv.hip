@@ -25,15 +25,12 @@
 // reduce: deterministic).  Both operands arrive [pixel][channel]; bf16 MFMA
 // fragments are read with ds_read_b64_tr_b16 (hardware transpose).
 #include "common.hpp"
+#include "mfma.hpp"
 
 #include <algorithm>
 #include <vector>
 
 namespace cai {
-
-template <typename T> struct OpT;
-template <> struct OpT<bf16> { static constexpr int VEC = 8; };
-template <> struct OpT<float> { static constexpr int VEC = 4; };
 
 constexpr int NT = 256;
 
@@ -71,46 +68,6 @@ struct ConvArgs {
     PhaseDesc ph[4];
 };
 
-__device__ __forceinline__ u32x4 abs_chunk(u32x4 v, int elem_bytes) {
-    const unsigned m = elem_bytes == 2 ? 0x7FFF7FFFu : 0x7FFFFFFFu;
-    v.x &= m; v.y &= m; v.z &= m; v.w &= m;
-    return v;
-}
-
-template <typename T>
-__device__ __forceinline__ u32x4 sq_chunk(u32x4 v);
-template <> __device__ __forceinline__ u32x4 sq_chunk<bf16>(u32x4 v) {
-    bf16x8 h = __builtin_bit_cast(bf16x8, v);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const float f = (float)h[e];
-        h[e] = (bf16)(f * f);
-    }
-    return __builtin_bit_cast(u32x4, h);
-}
-template <> __device__ __forceinline__ u32x4 sq_chunk<float>(u32x4 v) {
-    f32x4 h = __builtin_bit_cast(f32x4, v);
-    h = h * h;
-    return __builtin_bit_cast(u32x4, h);
-}
-
-template <typename T>
-__device__ __forceinline__ f32x4 mma16(u32x4 a, u32x4 b, f32x4 c);
-template <> __device__ __forceinline__ f32x4 mma16<bf16>(u32x4 a, u32x4 b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
-                                                   0, 0);
-}
-template <> __device__ __forceinline__ f32x4 mma16<float>(u32x4 a, u32x4 b, f32x4 c) {
-    // the four k-values of a 16-byte slot go to four MFMAs; A and B use the
-    // same permutation of k so the sum is unchanged
-    const f32x4 av = __builtin_bit_cast(f32x4, a), bv = __builtin_bit_cast(f32x4, b);
-    c = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], bv[0], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1], bv[1], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x4f32(av[2], bv[2], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x4f32(av[3], bv[3], c, 0, 0, 0);
-    return c;
-}
-
 __device__ __forceinline__ int swz(int row, int slot) { return slot ^ ((row >> 1) & 7); }
 
 __device__ __forceinline__ float apply_act(float v, int act, float prm) {
@@ -137,13 +94,6 @@ struct ConvSmem {
     static constexpr int EPI = C::BM * EPI_STRIDE * 4;
     static constexpr int BYTES = PIPE > EPI ? PIPE : EPI;
 };
-
-template <typename T>
-using gptr = const T __attribute__((address_space(1)))*;
-template <typename T>
-__device__ __forceinline__ gptr<T> to_global(const void* p) {
-    return (gptr<T>)(reinterpret_cast<uintptr_t>(p));
-}
 
 template <int N>
 struct U4 {
@@ -519,10 +469,10 @@ struct WgradArgs {
     int64_t M;
     int64_t split_len;
     float* ws;
-    int ctiles, rtiles, nsub, grp_len;
+    int ctiles, rtiles, nsub, grp_len, chunk;
 };
 
-constexpr int WG_CHUNK = 1024;   // pixels per L2-resident wgrad chunk (multiple of 64)
+constexpr int WG_CHUNK = 1024;   // max pixels per L2-resident wgrad chunk (multiple of 64)
 
 // bijective XCD remap (cdna_hip_programming.md T1): physical workgroup id ->
 // logical id such that logical ids [x*q, (x+1)*q) run on one XCD
@@ -573,10 +523,11 @@ __global__ __launch_bounds__(NT, 2) void wgrad_kernel(const WgradArgs a) {
     // pixel indices fit in 32 bits (M < 2^31 is checked on the host)
     const int gbeg = min((int)a.M, grp * a.grp_len);
     const int gend = min((int)a.M, gbeg + a.grp_len);
-    const int nchunk = (gend - gbeg + WG_CHUNK - 1) / WG_CHUNK;
+    const int CHK = a.chunk;
+    const int nchunk = (gend - gbeg + CHK - 1) / CHK;
     int nsteps = 0;   // 64-pixel steps of this workgroup
     for (int c = sub; c < nchunk; c += a.nsub)
-        nsteps += (min(gend, gbeg + (c + 1) * WG_CHUNK) - (gbeg + c * WG_CHUNK) + BKP - 1) / BKP;
+        nsteps += (min(gend, gbeg + (c + 1) * CHK) - (gbeg + c * CHK) + BKP - 1) / BKP;
     if (nsteps == 0) {
         // empty split: still write zeros so the reduce reads defined data
         for (int id = tid; id < 128 * 128; id += NT) {
@@ -585,9 +536,9 @@ __global__ __launch_bounds__(NT, 2) void wgrad_kernel(const WgradArgs a) {
         }
         return;
     }
-    constexpr int SPC = WG_CHUNK / BKP;   // steps per chunk
+    const int SPC = CHK / BKP;   // steps per chunk
     // first pixel of step st (this sub's chunks in order; the last chunk may be short)
-    auto step_base = [&](int st) { return gbeg + (sub + (st / SPC) * a.nsub) * WG_CHUNK + (st % SPC) * BKP; };
+    auto step_base = [&](int st) { return gbeg + (sub + (st / SPC) * a.nsub) * CHK + (st % SPC) * BKP; };
 
     // this thread's fixed chunk column
     const int cc = tid % CPR;
@@ -608,7 +559,7 @@ __global__ __launch_bounds__(NT, 2) void wgrad_kernel(const WgradArgs a) {
         _Pragma("unroll") for (int i = 0; i < CH; ++i) {                                                     \
             const int row = i * (NT / CPR) + tid / CPR;                                                      \
             const int m = (MB) + row;                                                                        \
-            const bool mok = m < gend && (m - gbeg) / WG_CHUNK == ((MB) - gbeg) / WG_CHUNK;                  \
+            const bool mok = m < gend && (m - gbeg) / CHK == ((MB) - gbeg) / CHK;                            \
             const int mm = mok ? m : gbeg;                                                                   \
             const u32x4 gv = *reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(              \
                 G + (int64_t)mm * a.g_ld + (gvalid ? gcol : 0));                                             \
@@ -1008,7 +959,7 @@ static int run_conv(const cai_conv_geom* g, int dtype, int direction, const void
 }
 
 struct WgradPlan {
-    int Ng, Cq, Cq_pad, ncols, S, nsub, grp_len;
+    int Ng, Cq, Cq_pad, ncols, S, nsub, grp_len, px_chunk;
     int64_t M, split_len;
     int nchunk;
     int64_t chunk;
@@ -1036,8 +987,10 @@ static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype) {
     // >= ~512 workgroups, >= 8 steps of 64 pixels per workgroup
     const int64_t per_grp = (W.M + 7) / 8;
     int nsub = std::max(1, (512 + 8 * tiles - 1) / (8 * tiles));
-    nsub = (int)std::max<int64_t>(1, std::min<int64_t>(nsub, per_grp / 512));
+    nsub = (int)std::max<int64_t>(1, std::min<int64_t>(nsub, per_grp / 256));
     W.nsub = nsub;
+    // chunk: at most WG_CHUNK, small enough that every sub gets one
+    W.px_chunk = (int)std::min<int64_t>(WG_CHUNK, ((per_grp + nsub - 1) / nsub + 63) / 64 * 64);
     W.grp_len = (int)((per_grp + 63) / 64 * 64);
     W.S = 8 * nsub;
     W.split_len = 0;
@@ -1175,6 +1128,7 @@ int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_l
     a.rtiles = (W.Ng + 127) / 128;
     a.nsub = W.nsub;
     a.grp_len = W.grp_len;
+    a.chunk = W.px_chunk;
     dim3 grid(8 * a.ctiles * a.rtiles * a.nsub);
     hipStream_t st = as_stream(stream);
     if (dtype == CAI_BF16)

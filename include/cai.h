@@ -133,6 +133,20 @@ int cai_conv_wgrad(const cai_conv_geom* g, int dtype,
                    float* dw, float* db, int32_t accumulate,
                    void* workspace, size_t ws_bytes, void* stream);
 
+/* ConvTranspose2d with out_c <= 16 (the synthesis transform's last layer,
+ * models/utils.py:138-146, e.g. deconv(N, 3)): forward as one dense GEMM per
+ * input pixel (N = k*k*out_c columns) + col2im, backward as im2col + two 1x1
+ * GEMMs.  w / dw: torch layout [in_c][out_c][k][k] fp32 (dw overwritten or
+ * accumulated); y / dy: fp32 NCHW contiguous (x_hat); x / dx pixel-major. */
+size_t cai_deconv_small_workspace_bytes(const cai_conv_geom* g, int dtype);
+int cai_deconv_small_fwd(const cai_conv_geom* g, int dtype, const void* x, int32_t x_ld,
+                         const float* w, const float* bias, float* y,
+                         void* workspace, size_t ws_bytes, void* stream);
+int cai_deconv_small_bwd(const cai_conv_geom* g, int dtype, const void* x, int32_t x_ld,
+                         const float* w, const float* dy, void* dx, int32_t dx_ld,
+                         float* dw, float* db, int32_t accumulate,
+                         void* workspace, size_t ws_bytes, void* stream);
+
 /* =======================================================================
  * GDN / IGDN (layers/gdn.py:41-92), C in {32,64,96,128,192}.
  * ======================================================================= */

@@ -46,6 +46,10 @@ CONV_CASES = [
     # large pixel counts: several 1024-pixel chunks per XCD group in wgrad
     ("conv", 4, 64, 64, 160, 150, 5, 2),
     ("deconv", 3, 64, 32, 70, 90, 5, 2),
+    # few output channels: per-input-pixel GEMM + col2im path (deconv_small.hip)
+    ("deconv", 2, 192, 3, 33, 20, 5, 2),
+    ("deconv", 2, 64, 1, 12, 12, 3, 1),
+    ("deconv", 2, 128, 3, 64, 64, 5, 2),
 ]
 
 
