@@ -147,6 +147,78 @@ __device__ __forceinline__ void store_out_scalar(const ConvArgs& a, const PhaseD
     st_any(a.y, a.y_dtype, (int64_t)b * a.ysb + (int64_t)n * a.ysc + (int64_t)oy * a.ysy + (int64_t)ox * a.ysx, v);
 }
 
+// Epilogue shared by the conv kernels: the wave accumulators go through LDS as
+// fp32 [BM][BN+4]; split-K writes the raw partial tile to ws[z][m][n] (bias /
+// act / mask applied by the reduce), otherwise bias + act (+ mask) and 16-byte
+// stores.  `E` must hold BM*(BN+4) floats and may alias the operand stages.
+template <typename T, int BM, int BN, int WM, int WN, int NTH>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const PhaseDesc& P, int plane, int Mph, int m0,
+                                              int n0, float* E, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16]) {
+    constexpr int WTM = BM / WM, WTN = BN / WN;
+    constexpr int TM = WTM / 16, TN = WTN / 16;
+    constexpr int ES = BN + 4;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    if (a.ksplit > 1) {
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                const int col = wn * WTN + tn * 16 + (lane & 15);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) E[(wm * WTM + tm * 16 + (lane >> 4) * 4 + r) * ES + col] = acc[tm][tn][r];
+            }
+        __syncthreads();
+        float* dst = a.ws + (int64_t)blockIdx.z * a.ws_rows * a.ws_ld;
+        constexpr int cpr = BN / 4;
+        for (int id = tid; id < BM * cpr; id += NTH) {
+            const int row = id / cpr, cc = id - (id / cpr) * cpr;
+            const int m = m0 + row, n = n0 + cc * 4;
+            if (m >= Mph || n >= a.ws_ld) continue;
+            *reinterpret_cast<f32x4*>(dst + (int64_t)m * a.ws_ld + n) =
+                *reinterpret_cast<const f32x4*>(E + row * ES + cc * 4);
+        }
+        return;
+    }
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int col = wn * WTN + tn * 16 + (lane & 15);
+            const int n = n0 + col;
+            const float bv = (a.bias && n < a.Cout) ? a.bias[n] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = wm * WTM + tm * 16 + (lane >> 4) * 4 + r;
+                E[row * ES + col] = apply_act(acc[tm][tn][r] + bv, a.act, a.act_param);
+            }
+        }
+    __syncthreads();
+    if (a.y_vec) {
+        const int VO = a.y_dtype == CAI_BF16 ? 8 : 4;
+        const int cpr = BN / VO;
+        for (int id = tid; id < BM * cpr; id += NTH) {
+            const int row = id / cpr, cc = id - (id / cpr) * cpr;
+            const int m = m0 + row, n = n0 + cc * VO;
+            if (m >= Mph || n >= a.Cout) continue;
+            float v[8];
+            const f32x4 lo = *reinterpret_cast<const f32x4*>(E + row * ES + cc * VO);
+            f32x4 hi = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (VO == 8) hi = *reinterpret_cast<const f32x4*>(E + row * ES + cc * VO + 4);
+            v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+            v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+            store_out_chunk<T>(a, P, plane, m, n, v, VO);
+        }
+    } else {
+        for (int id = tid; id < BM * BN; id += NTH) {
+            const int col = id / BM, row = id - (id / BM) * BM;
+            const int m = m0 + row, n = n0 + col;
+            if (m >= Mph || n >= a.Cout) continue;
+            store_out_scalar<T>(a, P, plane, m, n, E[row * ES + col]);
+        }
+    }
+}
+
 template <typename T, typename C>
 __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(const ConvArgs a) {
     constexpr int BM = C::BM, BN = C::BN, WM = C::WM, WN = C::WN;
@@ -301,69 +373,157 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(const ConvArgs a) {
 #undef CONV_STORE_TILE
 #undef CONV_COMPUTE
 
-    float* E = reinterpret_cast<float*>(smem);
-    constexpr int ES = SM::EPI_STRIDE;
-    if (a.ksplit > 1) {
-        // ---- split-K: raw fp32 partial tile -> ws[z][m][n] (bias/act/mask in the reduce) ----
+    conv_epilogue<T, BM, BN, WM, WN, NT>(a, P, plane, Mph, m0, n0, reinterpret_cast<float*>(smem), acc);
+}
+
+// ---------------------------------------------------------------------------
+// bf16 implicit GEMM with LDS-DMA staging (global_load_lds_dwordx4) and a
+// 3-stage ring: tile kt+2 streams into LDS while tile kt is multiplied, one
+// raw barrier per K-tile behind a counted vmcnt (cdna_hip_programming.md §5
+// "Pipelining across barriers").  512 threads = 8 waves.  Requires
+// Cin_pad % 64 == 0 so every 64-channel K-tile lies inside one tap: the tap's
+// (dy, dx) shift is uniform per tile and the per-lane gather is one add + a
+// bounds test.  Padding taps read a zero page.  The LDS image is lane-linear
+// (DMA), so the XOR swizzle that keeps the fragment reads conflict-free is
+// applied to the per-lane SOURCE slot (both-sides rule).
+// ---------------------------------------------------------------------------
+__device__ __attribute__((aligned(64))) unsigned cai_zero_page[64];
+
+template <int BM_, int BN_, int WM_, int WN_>
+struct Cfg2 {
+    static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+    static constexpr int NTH = 512, STAGES = 3;
+    static constexpr int STAGE = (BM + BN) * 128;
+    static constexpr int EPI = BM * (BN + 4) * 4;
+    static constexpr int BYTES = (STAGES * STAGE > EPI) ? STAGES * STAGE : EPI;
+};
+
+typedef const void __attribute__((address_space(1)))* gvoid_ptr;
+typedef void __attribute__((address_space(3)))* lvoid_ptr;
+
+__device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
+    __builtin_amdgcn_global_load_lds((gvoid_ptr)(reinterpret_cast<uintptr_t>(g)),
+                                     (lvoid_ptr)(reinterpret_cast<uintptr_t>(lds_wave_base)), 16, 0, 0);
+}
+
+template <typename C>
+__global__ __launch_bounds__(512, 1) void conv_glds_kernel(const ConvArgs a) {
+    constexpr int BM = C::BM, BN = C::BN, WM = C::WM, WN = C::WN;
+    constexpr int WTM = BM / WM, WTN = BN / WN;
+    constexpr int TM = WTM / 16, TN = WTN / 16;
+    constexpr int AG = BM / 64, BG = BN / 64;     // DMA instructions per thread per K-tile
+    constexpr int G = AG + BG;
+    static_assert(WM * WN == 8 && BM % 64 == 0 && BN % 64 == 0, "bad tile");
+    __shared__ __attribute__((aligned(16))) char smem[C::BYTES];
+
+    const int ph = blockIdx.z / a.ksplit, split = blockIdx.z - ph * a.ksplit;
+    const PhaseDesc P = ph == 0 ? a.ph[0] : (ph == 1 ? a.ph[1] : (ph == 2 ? a.ph[2] : a.ph[3]));
+    const int plane = P.OHg * P.OWg;
+    const int Mph = a.B * plane;
+    const int m0 = blockIdx.x * BM;
+    if (m0 >= Mph) return;
+    const int n0 = blockIdx.y * BN;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+
+    // this thread's DMA rows: i*64 + wid*8 + lane/8; all share one logical slot
+    const int rsub = wid * 8 + (lane >> 3);
+    const int ls = (lane & 7) ^ ((rsub >> 1) & 7);
+    const char* X = reinterpret_cast<const char*>(a.x);
+    const int ld_b = a.x_ld * 2;                 // bytes per pixel row
+    int abase[AG], ay[AG], ax[AG];
 #pragma unroll
-        for (int tm = 0; tm < TM; ++tm)
+    for (int i = 0; i < AG; ++i) {
+        const int m = m0 + i * 64 + rsub;
+        if (m < Mph) {
+            const int b = m / plane;
+            const int r = m - b * plane;
+            const int j = r / P.OWg;
+            ay[i] = j * a.row_stride;
+            ax[i] = (r - j * P.OWg) * a.row_stride;
+            abase[i] = ((b * a.IH + ay[i]) * a.IW + ax[i]) * ld_b + ls * 16;
+        } else {
+            ay[i] = -(1 << 28);
+            ax[i] = 0;
+            abase[i] = 0;
+        }
+    }
+    const char* Wb = reinterpret_cast<const char*>(a.w) + P.w_off * 2 + ls * 16;
+    int boff[BG];
+#pragma unroll
+    for (int i = 0; i < BG; ++i) {
+        const int row = n0 + i * 64 + rsub;
+        boff[i] = row < a.Npad ? row * a.Kp * 2 : -1;
+    }
+    const int nk_all = P.K / 64;
+    const int per = (nk_all + a.ksplit - 1) / a.ksplit;
+    const int kt0 = split * per;
+    const int nk = max(0, min(nk_all, kt0 + per) - kt0);
+
+    auto issue = [&](int kt, int stage) {
+        const int kg = kt0 + kt;
+        const int t = (kg * 64) / a.Cin_pad;
+        const int ci0 = kg * 64 - t * a.Cin_pad;
+        const int ty = t / P.ntx;
+        const int dy = P.dy0 + a.tap_sy * ty, dx = P.dx0 + a.tap_sx * (t - ty * P.ntx);
+        const int delta = (dy * a.IW + dx) * ld_b + ci0 * 2;
+        char* sbase = smem + stage * C::STAGE + wid * 8 * 128;
+#pragma unroll
+        for (int i = 0; i < AG; ++i) {
+            const int iy = ay[i] + dy, ix = ax[i] + dx;
+            const bool ok = (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW;
+            const void* src = ok ? (const void*)(X + abase[i] + delta) : (const void*)cai_zero_page;
+            glds16(src, sbase + i * 64 * 128);
+        }
+#pragma unroll
+        for (int i = 0; i < BG; ++i) {
+            const void* src = boff[i] >= 0 ? (const void*)(Wb + boff[i] + kg * 128) : (const void*)cai_zero_page;
+            glds16(src, sbase + BM * 128 + i * 64 * 128);
+        }
+    };
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    if (nk > 0) issue(0, 0);
+    if (nk > 1) issue(1, 1);
+    for (int kt = 0; kt < nk; ++kt) {
+        if (kt + 1 < nk)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (kt + 2 < nk) issue(kt + 2, (kt + 2) % 3);
+        const char* As = smem + (kt % 3) * C::STAGE;
+        const char* Bs = As + BM * 128;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int lsr = c * 4 + (lane >> 4);
+            u32x4 fa[TM], fb[TN];
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm) {
+                const int row = wm * WTM + tm * 16 + (lane & 15);
+                fa[tm] = *reinterpret_cast<const u32x4*>(As + row * 128 + swz(row, lsr) * 16);
+            }
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn) {
-                const int col = wn * WTN + tn * 16 + (lane & 15);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) E[(wm * WTM + tm * 16 + (lane >> 4) * 4 + r) * ES + col] = acc[tm][tn][r];
+                const int row = wn * WTN + tn * 16 + (lane & 15);
+                fb[tn] = *reinterpret_cast<const u32x4*>(Bs + row * 128 + swz(row, lsr) * 16);
             }
-        __syncthreads();
-        float* dst = a.ws + (int64_t)blockIdx.z * a.ws_rows * a.ws_ld;
-        constexpr int cpr = BN / 4;
-        for (int id = tid; id < BM * cpr; id += NT) {
-            const int row = id / cpr, cc = id - (id / cpr) * cpr;
-            const int m = m0 + row, n = n0 + cc * 4;
-            if (m >= Mph || n >= a.ws_ld) continue;
-            *reinterpret_cast<f32x4*>(dst + (int64_t)m * a.ws_ld + n) =
-                *reinterpret_cast<const f32x4*>(E + row * ES + cc * 4);
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mma16<bf16>(fa[tm], fb[tn], acc[tm][tn]);
         }
-        return;
+        __builtin_amdgcn_sched_barrier(0);
     }
-
-    // ---- epilogue: acc (+bias, act) -> LDS fp32 [BM][BN+4] -> 16-byte stores ----
-#pragma unroll
-    for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn) {
-            const int col = wn * WTN + tn * 16 + (lane & 15);
-            const int n = n0 + col;
-            const float bv = (a.bias && n < a.Cout) ? a.bias[n] : 0.f;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = wm * WTM + tm * 16 + (lane >> 4) * 4 + r;
-                E[row * ES + col] = apply_act(acc[tm][tn][r] + bv, a.act, a.act_param);
-            }
-        }
     __syncthreads();
-    if (a.y_vec) {
-        const int VO = a.y_dtype == CAI_BF16 ? 8 : 4;
-        const int cpr = BN / VO;
-        for (int id = tid; id < BM * cpr; id += NT) {
-            const int row = id / cpr, cc = id - (id / cpr) * cpr;
-            const int m = m0 + row, n = n0 + cc * VO;
-            if (m >= Mph || n >= a.Cout) continue;
-            float v[8];
-            const f32x4 lo = *reinterpret_cast<const f32x4*>(E + row * ES + cc * VO);
-            f32x4 hi = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (VO == 8) hi = *reinterpret_cast<const f32x4*>(E + row * ES + cc * VO + 4);
-            v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
-            v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
-            store_out_chunk<T>(a, P, plane, m, n, v, VO);
-        }
-    } else {
-        for (int id = tid; id < BM * BN; id += NT) {
-            const int col = id / BM, row = id - (id / BM) * BM;
-            const int m = m0 + row, n = n0 + col;
-            if (m >= Mph || n >= a.Cout) continue;
-            store_out_scalar<T>(a, P, plane, m, n, E[row * ES + col]);
-        }
-    }
+    conv_epilogue<bf16, BM, BN, WM, WN, 512>(a, P, plane, Mph, m0, n0, reinterpret_cast<float*>(smem), acc);
 }
 
 // split-K reduce: out = epilogue(sum_s ws[ph*S + s][m][n]) in a fixed order
@@ -470,6 +630,8 @@ struct WgradArgs {
     int64_t split_len;
     float* ws;
     int ctiles, rtiles, nsub, grp_len, chunk;
+    int nsplit;        // glds kernel: pixel splits (split_len pixels each)
+    float* bws;        // glds kernel: per-split bias partials [nsplit][Ng] (NULL: none)
 };
 
 constexpr int WG_CHUNK = 1024;   // max pixels per L2-resident wgrad chunk (multiple of 64)
@@ -672,11 +834,216 @@ __global__ __launch_bounds__(NT, 2) void wgrad_kernel(const WgradArgs a) {
 // Block = 16 float4 column groups x 16 split groups: reads walk the slabs in
 // memory order (256-byte runs), the 16 split partials meet in LDS in a fixed
 // order (deterministic); the transposed writes are 1/S of the bytes.
+// ---------------------------------------------------------------------------
+// bf16 wgrad with LDS-DMA staging: block tile 128 G-channels (rows n) x 256
+// (tap, q) columns, 64-pixel K-steps, 3-stage ring, 8 waves (2 x 4, each
+// 64 x 64).  The G tile [64 px][128 ch] and the two X half-tiles
+// [64 px][128 cols] are 256-byte-row images filled lane-linearly by
+// global_load_lds (4 rows per wave-instruction); the tr-read swizzle trswz()
+// goes on the per-lane source slot.  A lane's column chunk (tap, q) is fixed
+// for the whole launch, so its X gather is one bounds test per pixel row.
+// Block b works on pixel split (xcd-remapped index / tiles): the tiles of one
+// pixel range share an XCD's L2.
+// ---------------------------------------------------------------------------
+enum { WG_ABS = 1, WG_SQ = 2, WG_BIAS = 4 };
+
+template <int CT, int FLAGS>
+__global__ __launch_bounds__(512, 1) void wgrad_glds_kernel(const WgradArgs a) {
+    constexpr int OPB = 64 * 256;                 // one [64][256 B] image
+    constexpr int NX = CT / 128;                  // X images (128 columns each)
+    constexpr int STAGE = (1 + NX) * OPB;         // G, X_0 [, X_1]
+    constexpr int WCOL = CT / 4;                  // columns per wave
+    constexpr int TN = WCOL / 16;
+    constexpr int G = 2 * (1 + NX);               // DMA instructions per thread per step
+    __shared__ __attribute__((aligned(16))) char smem[3 * STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wr = wid >> 2, wc = wid & 3;        // 2 (rows) x 4 (cols) waves
+    const int ntile = a.ctiles * a.rtiles;
+    const int L = xcd_remap((int)blockIdx.x, (int)gridDim.x);
+    const int split = L / ntile;
+    const int tl = L - split * ntile;
+    const int ctile = tl % a.ctiles, rtile = tl / a.ctiles;
+    const int c0 = ctile * CT, r0 = rtile * 128;
+    const int pbeg = min((int)a.M, (int)(split * a.split_len));
+    const int pend = min((int)a.M, (int)(pbeg + a.split_len));
+    const int nsteps = (pend - pbeg + 63) / 64;
+    float* out = a.ws + (int64_t)split * a.Ng * a.ncols;
+
+    // DMA rows of this lane: (i*8 + wid)*4 + lane/16 for i = 0, 1; the source
+    // slot is the physical slot lane%16 XOR the tr-read swizzle of that row
+    const int prow0 = wid * 4 + (lane >> 4);      // i = 0; i = 1 adds 32
+    const int sl = (lane & 15) ^ ((((lane >> 4) & 3) << 1) | (((wid >> 1) & 1) << 3));
+    const char* Gp = reinterpret_cast<const char*>(a.g);
+    const char* Xp = reinterpret_cast<const char*>(a.x);
+    const int gch = r0 + sl * 8;
+    const bool gvalid = gch < a.Ng;
+    int xoff[NX], xkh[NX], xkw[NX];
+    bool xvalid[NX];
+#pragma unroll
+    for (int h = 0; h < NX; ++h) {
+        const int col = c0 + h * 128 + sl * 8;
+        xvalid[h] = col < a.ncols;
+        const int t = xvalid[h] ? col / a.Cq_pad : 0;
+        const int q = xvalid[h] ? col - t * a.Cq_pad : 0;
+        xkh[h] = t / a.k;
+        xkw[h] = t - xkh[h] * a.k;
+        xoff[h] = q * 2;
+    }
+    const int plane = a.Hg * a.Wg;
+
+    auto issue = [&](int st, int stage) {
+        char* sb = smem + stage * STAGE + wid * 4 * 256;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int m = pbeg + st * 64 + prow0 + i * 32;
+            const bool mok = m < pend;
+            const void* gs = (mok && gvalid) ? (const void*)(Gp + ((int64_t)m * a.g_ld + gch) * 2)
+                                             : (const void*)cai_zero_page;
+            glds16(gs, sb + i * 32 * 256);
+            const int b = m / plane;
+            const int r = m - b * plane;
+            const int j = r / a.Wg;
+            const int yb = j * a.s - a.p, xb = (r - j * a.Wg) * a.s - a.p;
+#pragma unroll
+            for (int h = 0; h < NX; ++h) {
+                const int iy = yb + xkh[h], ix = xb + xkw[h];
+                const bool ok = mok && xvalid[h] && (unsigned)iy < (unsigned)a.Hx && (unsigned)ix < (unsigned)a.Wx;
+                const void* xs = ok ? (const void*)(Xp + (((int64_t)b * a.Hx + iy) * a.Wx + ix) * a.x_ld * 2 + xoff[h])
+                                    : (const void*)cai_zero_page;
+                glds16(xs, sb + (1 + h) * OPB + i * 32 * 256);
+            }
+        }
+    };
+
+    f32x4 acc[4][TN];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int g_ = lane >> 4, i16 = lane & 15, q_ = i16 >> 2, p4 = i16 & 3;
+    // bias gradient (column sums of G) from the A fragments: the wc == 0 waves
+    // of the ctile-0 blocks hold every G value of the tile exactly once
+    // (the four column waves of a row pair share the A fragments: wave wc sums tm == wc)
+    const bool do_bias = (FLAGS & WG_BIAS) && ctile == 0;
+    float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+    const int wcol = wc * WCOL;
+    const int ximg = 1 + wcol / 128, xcb = wcol % 128;
+    if (nsteps > 0) issue(0, 0);
+    if (nsteps > 1) issue(1, 1);
+    for (int st = 0; st < nsteps; ++st) {
+        if (st + 1 < nsteps)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (st + 2 < nsteps) issue(st + 2, (st + 2) % 3);
+        const char* Gs = smem + (st % 3) * STAGE;
+        const char* Xs = Gs + OPB * ximg;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int rr = 32 * ks + 8 * g_ + q_;
+            u32x4 fb[TN];
+#pragma unroll
+            for (int t = 0; t < TN; ++t) {
+                const int colB = xcb + t * 16 + 4 * p4;
+                s16x4 b0 = ds_tr16(Xs, trswz(rr, colB >> 3) + ((colB & 7) << 1));
+                s16x4 b1 = ds_tr16(Xs, trswz(rr + 4, colB >> 3) + ((colB & 7) << 1));
+                s16x8 bv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+                fb[t] = __builtin_bit_cast(u32x4, bv);
+                if constexpr ((FLAGS & WG_ABS) != 0) fb[t] = abs_chunk(fb[t], 2);
+                if constexpr ((FLAGS & WG_SQ) != 0) fb[t] = sq_chunk<bf16>(fb[t]);
+            }
+#pragma unroll
+            for (int tm = 0; tm < 4; ++tm) {
+                const int colA = wr * 64 + tm * 16 + 4 * p4;
+                s16x4 a0 = ds_tr16(Gs, trswz(rr, colA >> 3) + ((colA & 7) << 1));
+                s16x4 a1 = ds_tr16(Gs, trswz(rr + 4, colA >> 3) + ((colA & 7) << 1));
+                s16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+                const u32x4 fa = __builtin_bit_cast(u32x4, av);
+                if constexpr ((FLAGS & WG_BIAS) != 0) {
+                    if (do_bias && tm == wc) {
+                        const bf16x8 h = __builtin_bit_cast(bf16x8, fa);
+                        float sacc = 0.f;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) sacc += (float)h[e];
+                        bsum[tm] += sacc;
+                    }
+                }
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mma16<bf16>(fa, fb[tn], acc[tm][tn]);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr ((FLAGS & WG_BIAS) != 0) {
+        if (do_bias) {
+            // an A fragment lane holds channel (lane & 15) of its 16-row group
+            // over 8 pixels (8 * (lane >> 4)): fold the four pixel groups
+            float v = bsum[0] + bsum[1] + bsum[2] + bsum[3];   // only bsum[wc] is non-zero
+            v += __shfl_xor(v, 16);
+            v += __shfl_xor(v, 32);
+            const int n = r0 + wr * 64 + wc * 16 + lane;
+            if (lane < 16 && n < a.Ng) a.bws[(int64_t)split * a.Ng + n] = v;
+        }
+    }
+#pragma unroll
+    for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int col = c0 + wcol + tn * 16 + (lane & 15);
+            if (col >= a.ncols) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = r0 + wr * 64 + tm * 16 + (lane >> 4) * 4 + r;
+                if (row < a.Ng) out[(int64_t)row * a.ncols + col] = acc[tm][tn][r];
+            }
+        }
+}
+
+template <int CT>
+static void launch_wgrad_glds(const WgradArgs& a, int nblocks, int in_abs, int in_sq, bool bias, hipStream_t st) {
+    const int f = (in_abs ? WG_ABS : 0) | (in_sq ? WG_SQ : 0) | (bias ? WG_BIAS : 0);
+    switch (f) {
+        case 0: hipLaunchKernelGGL((wgrad_glds_kernel<CT, 0>), dim3(nblocks), dim3(512), 0, st, a); break;
+        case WG_ABS: hipLaunchKernelGGL((wgrad_glds_kernel<CT, WG_ABS>), dim3(nblocks), dim3(512), 0, st, a); break;
+        case WG_SQ: hipLaunchKernelGGL((wgrad_glds_kernel<CT, WG_SQ>), dim3(nblocks), dim3(512), 0, st, a); break;
+        case WG_BIAS: hipLaunchKernelGGL((wgrad_glds_kernel<CT, WG_BIAS>), dim3(nblocks), dim3(512), 0, st, a); break;
+        case WG_ABS | WG_BIAS:
+            hipLaunchKernelGGL((wgrad_glds_kernel<CT, WG_ABS | WG_BIAS>), dim3(nblocks), dim3(512), 0, st, a);
+            break;
+        default:   // WG_SQ | WG_BIAS (GDN), WG_ABS | WG_SQ never requested
+            hipLaunchKernelGGL((wgrad_glds_kernel<CT, WG_SQ | WG_BIAS>), dim3(nblocks), dim3(512), 0, st, a);
+            break;
+    }
+}
+
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int S, int Ng, int ncols,
                                                            int Cq, int Cq_pad, int k, float* __restrict__ dw,
-                                                           int accumulate) {
+                                                           int accumulate, const float* __restrict__ bws,
+                                                           float* __restrict__ db) {
     __shared__ f32x4 red[16][16];
     const int c4 = ncols >> 2;
+    const int wblocks = (int)(((int64_t)Ng * c4 + 15) / 16);
+    if ((int)blockIdx.x >= wblocks) {
+        // trailing blocks: bias partials [S][Ng] -> db, 16 channels per block,
+        // 16 split groups summed in a fixed order
+        __shared__ float bred[16][16];
+        const int cgb = threadIdx.x & 15, sgb = threadIdx.x >> 4;
+        const int n = ((int)blockIdx.x - wblocks) * 16 + cgb;
+        float v = 0.f;
+        if (n < Ng)
+            for (int sp = sgb; sp < S; sp += 16) v += bws[(int64_t)sp * Ng + n];
+        bred[sgb][cgb] = v;
+        __syncthreads();
+        if (sgb == 0 && n < Ng) {
+            for (int j = 1; j < 16; ++j) v += bred[j][cgb];
+            db[n] = accumulate ? db[n] + v : v;
+        }
+        return;
+    }
     const int64_t total = (int64_t)Ng * c4;
     const int64_t slab4 = ((int64_t)Ng * ncols) >> 2;
     const int cg = threadIdx.x & 15, sg = threadIdx.x >> 4;
@@ -860,16 +1227,40 @@ static int pick_cfg(int C, int& BM, int& BN) {
     return id;
 }
 
+using CfgG1 = Cfg2<256, 128, 4, 2>;
+using CfgG2 = Cfg2<128, 192, 2, 4>;
+using CfgG3 = Cfg2<256, 64, 4, 2>;
+using CfgG4 = Cfg2<128, 128, 2, 4>;
+enum { CFG_G1 = 10, CFG_G2, CFG_G3, CFG_G4 };
+
+static int pick_cfg_glds(int C, int nphase, int& BM, int& BN) {
+    if (C <= 64) { BM = 256; BN = 64; return CFG_G3; }
+    // phase mode: the s*s phases carry different tap counts (9/6/6/4 for k5 s2);
+    // half-height tiles give the dispatcher enough blocks to balance them
+    (void)nphase;
+    if (C % 128 != 0 && (C % 192 == 0 || C % 192 > 128 || (C > 128 && C <= 192))) { BM = 128; BN = 192; return CFG_G2; }
+    BM = 256; BN = 128;
+    return CFG_G1;
+}
+
+// the LDS-DMA kernel needs bf16 operands read as stored (no |x| on load) and
+// 64-channel K-tiles inside one tap
+static bool glds_eligible(const Plan& P, int dtype, int in_abs) {
+    return dtype == CAI_BF16 && !in_abs && P.Cin_pad % 64 == 0;
+}
+
 // Launch geometry of one conv call: tiles, split-K factor and its workspace.
 struct ConvLaunch {
     int cfg, BM, BN, mtiles, ntiles, mmax, ksplit, ws_ld;
+    bool glds;
     size_t ws_bytes;
 };
 
-static ConvLaunch conv_launch(const cai_conv_geom* g, int dtype, int direction) {
+static ConvLaunch conv_launch(const cai_conv_geom* g, int dtype, int direction, int in_abs) {
     const Plan P = make_plan(g, dtype, direction);
     ConvLaunch L{};
-    L.cfg = pick_cfg(P.kout_c, L.BM, L.BN);
+    L.glds = glds_eligible(P, dtype, in_abs);
+    L.cfg = L.glds ? pick_cfg_glds(P.kout_c, P.nphase, L.BM, L.BN) : pick_cfg(P.kout_c, L.BM, L.BN);
     int kmax = 0;
     for (int ph = 0; ph < P.nphase; ++ph) {
         L.mmax = std::max(L.mmax, g->batch * P.OHg[ph] * P.OWg[ph]);
@@ -882,7 +1273,8 @@ static ConvLaunch conv_launch(const cai_conv_geom* g, int dtype, int direction) 
     // split K when the tile grid cannot fill the 256 CUs (small spatial layers);
     // each split keeps >= 4 K-tiles so the 2-deep prefetch still has work to hide
     int ks = 1;
-    if (tiles < 256) ks = std::min({(512 + tiles - 1) / tiles, std::max(1, nk / 4), 16});
+    const int target = L.glds ? 256 : 512;    // one 512-thread block per CU vs two 256-thread ones
+    if (tiles < 256) ks = std::min({(target + tiles - 1) / tiles, std::max(1, nk / 4), 16});
     L.ksplit = std::max(1, ks);
     L.ws_ld = L.ntiles * L.BN;
     L.ws_bytes = L.ksplit > 1 ? (size_t)P.nphase * L.ksplit * L.mmax * L.ws_ld * sizeof(float) : 0;
@@ -901,8 +1293,29 @@ static void launch_conv(const ConvArgs& a, const ConvLaunch& L, hipStream_t st) 
     }
 }
 
+template <typename C>
+static void launch_conv_glds(const ConvArgs& a, const ConvLaunch& L, hipStream_t st) {
+    dim3 grid(L.mtiles, L.ntiles, a.nphase * a.ksplit);
+    hipLaunchKernelGGL((conv_glds_kernel<C>), grid, dim3(512), 0, st, a);
+    if (a.ksplit > 1) {
+        const int VO = (a.y_vec && a.y_dtype == CAI_BF16) ? 8 : 4;
+        const int64_t total = (int64_t)L.mmax * ((a.Cout + VO - 1) / VO);
+        const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, (total + 255) / 256));
+        hipLaunchKernelGGL((conv_splitk_reduce_kernel<bf16>), dim3(gx, a.nphase), dim3(256), 0, st, a);
+    }
+}
+
 template <typename T>
 static void dispatch_conv(const ConvArgs& a, const ConvLaunch& L, hipStream_t st) {
+    if constexpr (sizeof(T) == 2) {
+        switch (L.cfg) {
+            case CFG_G1: launch_conv_glds<CfgG1>(a, L, st); return;
+            case CFG_G2: launch_conv_glds<CfgG2>(a, L, st); return;
+            case CFG_G3: launch_conv_glds<CfgG3>(a, L, st); return;
+            case CFG_G4: launch_conv_glds<CfgG4>(a, L, st); return;
+            default: break;
+        }
+    }
     switch (L.cfg) {
         case CFG_S: launch_conv<T, CfgS>(a, L, st); break;
         case CFG_M: launch_conv<T, CfgM>(a, L, st); break;
@@ -920,11 +1333,13 @@ static int run_conv(const cai_conv_geom* g, int dtype, int direction, const void
     CAI_CHECK_ARG(dtype == CAI_BF16 || dtype == CAI_F32, "%s: bad dtype", name);
     CAI_CHECK_ARG(x && w && y, "%s: null pointer", name);
     const Plan P = make_plan(g, dtype, direction);
-    const ConvLaunch L = conv_launch(g, dtype, direction);
+    const ConvLaunch L = conv_launch(g, dtype, direction, in_abs);
     const int VEC = dtype == CAI_BF16 ? 8 : 4;
     CAI_CHECK_ARG(x_ld >= P.Cin_pad && x_ld % VEC == 0, "%s: input ld %d must be >= %d and a multiple of %d", name,
                   x_ld, P.Cin_pad, VEC);
     CAI_CHECK_ARG(((uintptr_t)x & 15) == 0, "%s: input not 16-byte aligned", name);
+    CAI_CHECK_ARG((int64_t)g->batch * P.in_h * P.in_w * x_ld * dtype_size(dtype) < (1ll << 31),
+                  "%s: input larger than 2 GiB", name);
     CAI_CHECK_ARG(!mask_mode || (aux && aux_ld >= P.kout_c), "%s: mask needs aux", name);
     CAI_CHECK_ARG(L.ws_bytes == 0 || (workspace && ws_bytes >= L.ws_bytes && ((uintptr_t)workspace & 15) == 0),
                   "%s: workspace of %zu bytes required", name, L.ws_bytes);
@@ -959,6 +1374,10 @@ static int run_conv(const cai_conv_geom* g, int dtype, int direction, const void
 }
 
 struct WgradPlan {
+    bool glds, fused_bias;
+    int ct;
+    size_t ws_bias;
+    int tiles;
     int Ng, Cq, Cq_pad, ncols, S, nsub, grp_len, px_chunk;
     int64_t M, split_len;
     int nchunk;
@@ -970,8 +1389,9 @@ static int colsum_nchunk(int64_t npix) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(1024, (npix + 255) / 256));
 }
 
-static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype) {
+static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype, bool glds) {
     WgradPlan W{};
+    W.glds = glds && dtype == CAI_BF16;
     const int VEC = dtype == CAI_BF16 ? 8 : 4;
     if (!g->transposed) {
         W.Ng = g->out_c; W.Cq = g->in_c;
@@ -994,7 +1414,18 @@ static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype) {
     W.grp_len = (int)((per_grp + 63) / 64 * 64);
     W.S = 8 * nsub;
     W.split_len = 0;
+    if (W.glds) {
+        // one 512-thread block per CU: ~256 blocks of (256-col tile, pixel split)
+        W.ct = W.ncols <= 128 ? 128 : 256;      // 1x1 layers (GDN, small deconv): half-width tile
+        W.tiles = ((W.ncols + W.ct - 1) / W.ct) * ((W.Ng + 127) / 128);
+        int S = std::max(1, 256 / W.tiles);
+        S = (int)std::max<int64_t>(1, std::min<int64_t>(S, W.M / 256));
+        W.split_len = ((W.M + S - 1) / S + 63) / 64 * 64;
+        W.S = (int)((W.M + W.split_len - 1) / W.split_len);
+    }
     W.ws_slab = (size_t)W.S * W.Ng * W.ncols * sizeof(float);
+    W.fused_bias = W.glds && !g->transposed;
+    W.ws_bias = W.fused_bias ? ((size_t)W.S * W.Ng * sizeof(float) + 255) / 256 * 256 : 0;
     // bias grad: columns of the module output gradient
     const int64_t npix_out = (int64_t)g->batch * g->out_h * g->out_w;
     W.nchunk = colsum_nchunk(npix_out);
@@ -1069,7 +1500,8 @@ int cai_pack_nchw(const float* x, int32_t B, int32_t C, int32_t H, int32_t W, in
 
 size_t cai_conv_workspace_bytes(const cai_conv_geom* g, int dtype, int direction) {
     if (check_geom(g)) return 0;
-    return conv_launch(g, dtype, direction).ws_bytes;
+    // the kernel choice may depend on in_abs (not known here): cover both
+    return std::max(conv_launch(g, dtype, direction, 0).ws_bytes, conv_launch(g, dtype, direction, 1).ws_bytes);
 }
 
 int cai_conv_fwd(const cai_conv_geom* g, int dtype, const void* x, int32_t x_ld, int32_t in_abs, const void* packed_w,
@@ -1092,8 +1524,8 @@ int cai_conv_dgrad(const cai_conv_geom* g, int dtype, const void* dy, int32_t dy
 
 size_t cai_conv_wgrad_workspace_bytes(const cai_conv_geom* g, int dtype) {
     if (check_geom(g)) return 0;
-    const WgradPlan W = make_wgrad_plan(g, dtype);
-    return W.ws_slab + W.ws_col + 256;
+    const WgradPlan W0 = make_wgrad_plan(g, dtype, false), W1 = make_wgrad_plan(g, dtype, true);
+    return std::max(W0.ws_slab + W0.ws_col, W1.ws_slab + W1.ws_bias + W1.ws_col) + 256;
 }
 
 int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_ld, int32_t in_abs, int32_t in_sq,
@@ -1102,8 +1534,8 @@ int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_l
     int rc = check_geom(g);
     if (rc) return rc;
     CAI_CHECK_ARG(x && dy && dw, "conv_wgrad: null pointer");
-    const WgradPlan W = make_wgrad_plan(g, dtype);
-    CAI_CHECK_ARG(workspace && ws_bytes >= W.ws_slab + W.ws_col + 256, "conv_wgrad: workspace too small");
+    const WgradPlan W = make_wgrad_plan(g, dtype, true);
+    CAI_CHECK_ARG(workspace && ws_bytes >= W.ws_slab + W.ws_bias + W.ws_col + 256, "conv_wgrad: workspace too small");
     const int VEC = dtype == CAI_BF16 ? 8 : 4;
     WgradArgs a{};
     if (!g->transposed) {
@@ -1129,17 +1561,30 @@ int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_l
     a.nsub = W.nsub;
     a.grp_len = W.grp_len;
     a.chunk = W.px_chunk;
-    dim3 grid(8 * a.ctiles * a.rtiles * a.nsub);
     hipStream_t st = as_stream(stream);
-    if (dtype == CAI_BF16)
-        hipLaunchKernelGGL(wgrad_kernel<bf16>, grid, dim3(NT), 0, st, a);
-    else
-        hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(NT), 0, st, a);
+    float* bws = nullptr;
+    if (W.glds) {
+        a.ctiles = (W.ncols + W.ct - 1) / W.ct;
+        a.split_len = W.split_len;
+        a.nsplit = W.S;
+        if (W.fused_bias && db) bws = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + W.ws_slab);
+        a.bws = bws;
+        if (W.ct == 256)
+            launch_wgrad_glds<256>(a, W.S * W.tiles, in_abs, in_sq, bws != nullptr, st);
+        else
+            launch_wgrad_glds<128>(a, W.S * W.tiles, in_abs, in_sq, bws != nullptr, st);
+    } else {
+        dim3 grid(8 * a.ctiles * a.rtiles * a.nsub);
+        if (dtype == CAI_BF16)
+            hipLaunchKernelGGL(wgrad_kernel<bf16>, grid, dim3(NT), 0, st, a);
+        else
+            hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(NT), 0, st, a);
+    }
     const int64_t tot = (int64_t)W.Ng * (W.ncols / 4);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((tot + 15) / 16)), dim3(256), 0,
-                       st, slab, W.S, W.Ng, W.ncols, W.Cq, W.Cq_pad, g->kernel, dw, accumulate);
-    if (db) {
-        float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + W.ws_slab);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((tot + 15) / 16) + (bws ? (W.Ng + 15) / 16 : 0)), dim3(256), 0,
+                       st, slab, W.S, W.Ng, W.ncols, W.Cq, W.Cq_pad, g->kernel, dw, accumulate, bws, db);
+    if (db && !bws) {
+        float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + W.ws_slab + W.ws_bias);
         const int64_t npix = (int64_t)g->batch * g->out_h * g->out_w;
         if (dtype == CAI_BF16)
             launch_colsum<bf16>(dy, npix, g->out_c, dy_ld, W.nchunk, W.chunk, part, db, accumulate, st);

@@ -71,7 +71,7 @@ static SmallPlan small_plan(const cai_conv_geom* g, int dtype) {
 
 static size_t rows_gemm_lds(int nti, int kp, int es) { return (size_t)nti * 16 * (kp * es + 16); }
 static size_t col2im_lds(const SmallPlan& L, int es) { return (size_t)L.c2i_r * L.c2i_c * L.Np * es; }
-static size_t im2col_lds(const SmallPlan& L) { return (size_t)L.Cout * L.i2c_r * L.i2c_c * 4; }
+static size_t im2col_lds(const SmallPlan& L) { return (size_t)L.Cout * L.i2c_r * L.i2c_c * 4 + (size_t)L.Np * 4; }
 
 __device__ __forceinline__ int floordiv(int a, int s) { return a >= 0 ? a / s : -((-a + s - 1) / s); }
 
@@ -116,10 +116,13 @@ __global__ __launch_bounds__(256) void rows_gemm_kernel(const T* __restrict__ A,
     __syncthreads();
     const int lane = tid & 63, wave = tid >> 6;
     const int pl = lane & 15, kq = lane >> 4;
-    const int m0 = (blockIdx.x * 4 + wave) * (PT * 16);
-    if (m0 >= M) return;
     const gptr<T> Ag = to_global<T>(A);
     const u32x4 zero = u32x4{0u, 0u, 0u, 0u};
+    const int ntiles = (M + 64 * PT - 1) / (64 * PT);
+    // grid-stride over 64*PT-row tiles: the LDS weight copy is amortised
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int m0 = (tile * 4 + wave) * (PT * 16);
+    if (m0 >= M) continue;
     f32x4 acc[NTI][PT];
 #pragma unroll
     for (int i = 0; i < NTI; ++i)
@@ -167,6 +170,7 @@ __global__ __launch_bounds__(256) void rows_gemm_kernel(const T* __restrict__ A,
             }
         }
     }
+    }
 }
 
 template <typename T, int NTI>
@@ -175,8 +179,11 @@ static void launch_rows_gemm_nt(const T* A, int lda, int M, int K, const T* Bw, 
     constexpr int PT = NTI <= 4 ? 4 : (NTI <= 8 ? 2 : 1);
     const int rows_per_block = 4 * PT * 16;
     const size_t lds = rows_gemm_lds(NTI, Kp, (int)sizeof(T));
-    hipLaunchKernelGGL((rows_gemm_kernel<T, NTI, PT>), dim3((M + rows_per_block - 1) / rows_per_block), dim3(256),
-                       lds, st, A, lda, M, K, Bw, Kp, C, ldc, N);
+    const int ntiles = (M + rows_per_block - 1) / rows_per_block;
+    // ~4 workgroups per CU resident, each walking several row tiles
+    const int grid = std::min(ntiles, 1024);
+    hipLaunchKernelGGL((rows_gemm_kernel<T, NTI, PT>), dim3(grid), dim3(256), lds, st, A, lda, M, K, Bw, Kp, C, ldc,
+                       N);
 }
 
 template <typename T>
@@ -264,25 +271,31 @@ __global__ __launch_bounds__(256) void im2col_kernel(const float* __restrict__ d
         const int oy = oy_lo + r, ox = ox_lo + cc;
         S[i] = (oy >= 0 && oy < OH && ox >= 0 && ox < OW) ? src[((int64_t)c * OH + oy) * OW + ox] : 0.f;
     }
+    // column n -> window offset (c*R + kh)*Cc + kw, or -1 for the pad columns
+    int* off = reinterpret_cast<int*>(sm + (size_t)Cout * R * Cc * 4);
+    const int kk = k * k;
+    for (int n = tid; n < Np; n += 256) {
+        int o = -1;
+        if (n < kk * Cout) {
+            const int t = n / Cout, c = n - (n / Cout) * Cout;
+            const int kh = t / k, kw = t - (t / k) * k;
+            o = (c * R + kh) * Cc + kw;
+        }
+        off[n] = o;
+    }
     __syncthreads();
     const int nch = Np / 8;
-    const int kk = k * k;
     for (int i = tid; i < I2C_TH * I2C_TW * nch; i += 256) {
         const int pix = i / nch, ch = i - (i / nch) * nch;
         const int ly = pix / I2C_TW, lx = pix - (pix / I2C_TW) * I2C_TW;
         const int iy = iy0 + ly, ix = ix0 + lx;
         if (iy >= H || ix >= W) continue;
+        const int base = ly * s * Cc + lx * s;
         float v[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-            const int n = ch * 8 + e;
-            float x = 0.f;
-            if (n < kk * Cout) {
-                const int t = n / Cout, c = n - (n / Cout) * Cout;
-                const int kh = t / k, kw = t - (t / k) * k;
-                x = S[(c * R + ly * s + kh) * Cc + lx * s + kw];
-            }
-            v[e] = x;
+            const int o = off[ch * 8 + e];
+            v[e] = o >= 0 ? S[base + o] : 0.f;
         }
         T* dst = Q + (((int64_t)b * H + iy) * W + ix) * Np + ch * 8;
         if constexpr (sizeof(T) == 2) {

@@ -462,9 +462,9 @@ int cai_gdn_param_grad(int dtype, const void* x, int32_t x_ld, const void* u, in
     float* dbeta = dgamma + (size_t)C * C;
     char* cws = reinterpret_cast<char*>(dbeta + C);
     // dgamma[i][j] = sum_p u[p][i] * x[p][j]^2   (G = u, X = x squared on load)
-    int rc = cai_conv_wgrad(&g, dtype, x, x_ld, 0, 1, u, C, dgamma, nullptr, 0, ws, wgb, stream);
-    if (rc) return rc;
-    rc = colsum_any(dtype, u, npix, C, C, dbeta, 0, cws, colsum_ws_bytes(npix, C), as_stream(stream));
+    // dbeta[i]     = sum_p u[p][i]                (the same call's bias gradient)
+    (void)cws;
+    int rc = cai_conv_wgrad(&g, dtype, x, x_ld, 0, 1, u, C, dgamma, dbeta, 0, ws, wgb, stream);
     if (rc) return rc;
     const float ped = reparam_offset * reparam_offset;
     const float bbound = sqrtf(beta_min + ped), gbound = sqrtf(ped);
