@@ -86,10 +86,17 @@ class FusedAdam:
         self.exp_avg_sq.copy_(sd["exp_avg_sq"])
 
 
-def configure_optimizers(net, lr: float = 1e-4, aux_lr: float = 1e-3):
-    """train.py:111-142: main Adam on all but `.quantiles`, aux Adam on `.quantiles` (sorted by name)."""
+def parameter_groups(net):
+    """train.py:115-124: names of the main (all but `.quantiles`) and aux (`.quantiles`) parameters, sorted."""
     named = dict(net.named_parameters())
     main = sorted(n for n, p in named.items() if not n.endswith(".quantiles") and p.requires_grad)
     aux = sorted(n for n, p in named.items() if n.endswith(".quantiles") and p.requires_grad)
     assert len(set(main) & set(aux)) == 0 and len(set(main) | set(aux)) == len(named)
+    return main, aux
+
+
+def configure_optimizers(net, lr: float = 1e-4, aux_lr: float = 1e-3):
+    """train.py:111-142: main Adam on all but `.quantiles`, aux Adam on `.quantiles` (sorted by name)."""
+    named = dict(net.named_parameters())
+    main, aux = parameter_groups(net)
     return FusedAdam((named[n] for n in main), lr=lr), FusedAdam((named[n] for n in aux), lr=aux_lr)

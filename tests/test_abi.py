@@ -1,0 +1,87 @@
+"""The C-ABI boundary (include/cai.h <-> lib/libcai.so <-> compressai._native), on CPU.
+
+No kernel is launched: the library is loaded, every symbol the header declares
+must be exported and bound, and argument validation (which runs before any
+device work) must reject bad calls with CAI_EINVAL and a message, the way the
+reference's pybind layer turns std::domain_error into ValueError
+(cpp_exts/ops/ops.cpp:46-64).
+"""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "cai.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(cai_[a-z0-9_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def native():
+    from compressai import _native
+
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("libcai.so not built")
+    _native.lib.load()
+    return _native
+
+
+def test_every_declared_symbol_is_exported(native):
+    raw = ctypes.CDLL(native.LIB_PATH)
+    missing = [f for f in declared_functions() if not hasattr(raw, f)]
+    assert not missing, missing
+
+
+def test_binding_table_matches_header(native):
+    decl = set(declared_functions())
+    bound = set(native.SIGNATURES)
+    assert decl == bound, (sorted(decl - bound), sorted(bound - decl))
+    assert native.lib.cai_abi_count() == len(decl)
+    assert native.lib.cai_version() >= 1
+
+
+def test_invalid_geometry_is_einval_with_message(native):
+    lib = native.lib.load()
+    g = native.ConvGeom(2, 16, 8, 8, 16, 7, 7, 5, 2, 2, 0, 0)   # 8x8 k5 s2 p2 -> 4x4, not 7x7
+    rc = lib.cai_conv_fwd(ctypes.byref(g), native.BF16, None, 16, 0, None, None, 0, 0.0, None, native.BF16,
+                          0, 0, 0, 0, None, 0, None)
+    assert rc == native.CAI_EINVAL
+    assert b"output size" in lib.cai_last_error()
+    assert lib.cai_conv_packed_weight_bytes(None, native.BF16, 0) == 0
+
+
+def test_python_shim_raises_valueerror(native):
+    g = native.ConvGeom(2, 16, 8, 8, 16, 4, 4, 9, 2, 2, 0, 0)   # kernel 9 unsupported
+    with pytest.raises(ValueError, match="unsupported kernel"):
+        native.lib.cai_conv_fwd(ctypes.byref(g), native.BF16, None, 16, 0, None, None, 0, 0.0, None, native.BF16,
+                                0, 0, 0, 0, None, 0, None)
+
+
+def test_small_deconv_gate(native):
+    lib = native.lib.load()
+    ok = native.ConvGeom(2, 128, 16, 16, 3, 32, 32, 5, 2, 2, 1, 1)
+    wide = native.ConvGeom(2, 128, 16, 16, 32, 32, 32, 5, 2, 2, 1, 1)
+    assert lib.cai_deconv_small_workspace_bytes(ctypes.byref(ok), native.BF16) > 0
+    assert lib.cai_deconv_small_workspace_bytes(ctypes.byref(wide), native.BF16) == 0
+
+
+def test_gdn_channel_counts_validated(native):
+    with pytest.raises(ValueError):
+        native.lib.cai_gdn_fwd(native.BF16, None, 48, 16, 48, None, None, 0, None, 48, None)
+
+
+def test_product_path_has_no_cpu_fallback():
+    """A CPU tensor must be refused, not silently computed by torch."""
+    import torch
+
+    from compressai.layers import Conv2d
+
+    m = Conv2d(8, 8, 3, padding=1)
+    with pytest.raises((RuntimeError, ValueError)):
+        m(torch.zeros(1, 8, 8, 8))

@@ -1,0 +1,165 @@
+"""Golden fixtures (tests/golden/*.npz, written by tests/golden/make_golden.py).
+
+CPU: the oracle still reproduces the frozen vectors (guards the restatement
+against drift, e.g. across torch versions).
+GPU: the HIP path reproduces them in exact-fp32 mode: outputs within 1e-4
+relative (north_star: PSNR/bpp within 1e-4), quantised values bit-exact in
+eval mode, gradients within 2e-3 relative (fp32 summation order differs).
+"""
+import math
+import os
+import sys
+
+import pytest
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+import make_golden as MG  # noqa: E402
+
+
+def relerr(a, b):
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    assert a.shape == b.shape, (a.shape, b.shape)
+    if b.numel() == 0:
+        return 0.0
+    d = b.abs().max().item()
+    return (a - b).abs().max().item() / (d if d > 0 else 1.0)
+
+
+@pytest.mark.parametrize("name", sorted(MG.GENERATORS))
+def test_oracle_reproduces_fixture(name):
+    torch.set_num_threads(1)
+    gold = MG.load(name)
+    fresh = {k: v.detach() for k, v in MG.GENERATORS[name]().items()}
+    assert set(gold) == set(fresh)
+    for k, v in gold.items():
+        assert relerr(fresh[k], v) < 1e-5, k
+
+
+# --------------------------------------------------------------------------- GPU
+
+
+def _noise(queue):
+    from compressai.entropy_models import set_noise_source
+
+    q = list(queue)
+    set_noise_source(lambda t: q.pop(0))
+    return q
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("training", [True, False])
+def test_gaussian_conditional_vs_fixture(cuda, training):
+    from compressai.entropy_models import GaussianConditional, set_noise_source
+
+    G = MG.load("gaussian_conditional")
+    gc = GaussianConditional(None).to(cuda)
+    xx, ss, mm = (G[k].to(cuda).requires_grad_() for k in ("x", "scales", "means"))
+    _noise([G["noise"].to(cuda)])
+    try:
+        q, lik = gc(xx, ss, mm, training=training)
+    finally:
+        set_noise_source(None)
+    ((q * G["gq"].to(cuda)).sum() + (lik * G["glik"].to(cuda)).sum()).backward()
+    tag = "train" if training else "eval"
+    if training:
+        assert relerr(q, G[f"{tag}_q"]) < 1e-6
+    else:
+        assert torch.equal(q.cpu(), G[f"{tag}_q"])      # round-to-index step bit-exact
+    assert relerr(lik, G[f"{tag}_lik"]) < 1e-4
+    for k, t in (("dx", xx), ("dscales", ss), ("dmeans", mm)):
+        assert relerr(t.grad, G[f"{tag}_{k}"]) < 2e-3, k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("training", [True, False])
+def test_entropy_bottleneck_vs_fixture(cuda, training):
+    from compressai.entropy_models import EntropyBottleneck, set_noise_source
+
+    G = MG.load("entropy_bottleneck")
+    eb = EntropyBottleneck(8)
+    eb.load_state_dict({k[6:]: v for k, v in G.items() if k.startswith("param.")})
+    eb = eb.to(cuda)
+    xx = G["x"].to(cuda).requires_grad_()
+    _noise([G["noise"].to(cuda)])
+    try:
+        q, lik = eb(xx, training=training)
+    finally:
+        set_noise_source(None)
+    ((q * G["gq"].to(cuda)).sum() + (lik * G["glik"].to(cuda)).sum()).backward()
+    tag = "train" if training else "eval"
+    if not training:
+        assert torch.equal(q.cpu(), G[f"{tag}_q"])
+    assert relerr(lik, G[f"{tag}_lik"]) < 1e-4
+    assert relerr(xx.grad, G[f"{tag}_dx"]) < 2e-3
+    named = dict(eb.named_parameters())
+    for k, v in G.items():
+        if k.startswith(f"{tag}_grad."):
+            assert relerr(named[k[len(tag) + 6:]].grad, v) < 2e-3, k
+    eb.zero_grad()
+    aux = eb.loss()
+    aux.backward()
+    assert relerr(aux.reshape(1), G["aux_loss"]) < 1e-5
+    assert relerr(eb.quantiles.grad, G["aux_dquantiles"]) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("inverse", [False, True])
+def test_gdn_vs_fixture(cuda, inverse):
+    from compressai.layers import GDN
+
+    G = MG.load("gdn")
+    tag = "igdn" if inverse else "gdn"
+    m = GDN(32, inverse=inverse)
+    with torch.no_grad():
+        m.beta.copy_(G[f"{tag}_beta"])
+        m.gamma.copy_(G[f"{tag}_gamma"])
+    m = m.to(cuda)
+    xx = G["x"].to(cuda).requires_grad_()
+    y = m(xx)
+    (y * G["gy"].to(cuda)).sum().backward()
+    assert relerr(y, G[f"{tag}_y"]) < 1e-4
+    assert relerr(xx.grad, G[f"{tag}_dx"]) < 2e-3
+    assert relerr(m.beta.grad, G[f"{tag}_dbeta"]) < 2e-3
+    assert relerr(m.gamma.grad, G[f"{tag}_dgamma"]) < 2e-3
+
+
+@pytest.mark.gpu
+def test_scale_hyperprior_vs_fixture(cuda):
+    from compressai.entropy_models import set_noise_source
+    from compressai.losses import RateDistortionLoss
+    from compressai.models import ScaleHyperprior
+
+    G = MG.load("scale_hyperprior")
+    net = ScaleHyperprior(32, 48)
+    net.load_state_dict({k[6:]: v for k, v in G.items() if k.startswith("param.")})
+    net = net.to(cuda)
+    x = G["x"].to(cuda)
+    noise = [G[f"noise{i}"].to(cuda) for i in range(sum(k.startswith("noise") for k in G))]
+    left = _noise(noise)
+    try:
+        out = net(x)
+    finally:
+        set_noise_source(None)
+    assert not left
+    crit = RateDistortionLoss(3)(out, x)
+    crit["loss"].backward()
+    assert relerr(out["x_hat"], G["x_hat"]) < 1e-4
+    assert relerr(out["likelihoods"]["y"], G["lik_y"]) < 1e-4
+    assert relerr(out["likelihoods"]["z"], G["lik_z"]) < 1e-4
+    for k in ("loss", "bpp_loss", "mse_loss"):
+        assert abs(crit[k].item() - G[k].item()) <= 1e-4 * max(1.0, abs(G[k].item())), k
+    named = dict(net.named_parameters())
+    for k, v in G.items():
+        if k.startswith("grad."):
+            assert relerr(named[k[5:]].grad, v) < 2e-3, k
+    net.eval()
+    with torch.no_grad():
+        ev = net(x)
+    npix = x.shape[0] * x.shape[2] * x.shape[3]
+    bpp = sum(torch.log(l).sum().item() for l in ev["likelihoods"].values()) / (-math.log(2) * npix)
+    mse = torch.mean((ev["x_hat"].clamp(0, 1) - x) ** 2).item()
+    psnr = -10 * math.log10(mse)
+    assert abs(bpp - G["eval_bpp"].item()) <= 1e-4 * max(1.0, G["eval_bpp"].item())
+    assert abs(psnr - G["eval_psnr"].item()) <= 1e-4 * G["eval_psnr"].item()
