@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-batch", type=int, default=2)
+    ap.add_argument("--roofline-only", action="store_true",
+                    help="only launch the roofline kernel --steps times (for rocprofv3 --pmc passes)")
     return ap.parse_args()
 
 
@@ -87,11 +89,26 @@ def dominant_kernel_roofline(B, size, reps=20):
     ms = e0.elapsed_time(e1) / reps
     flops = 2.0 * (B * OH * OH) * 128 * (25 * 128)
     tflops = flops / (ms * 1e-3) / 1e12
-    return {"kernel": "conv_gemm_kernel<bf16,128x128> (g_a[2] fwd: Conv2d 128->128 k5 s2, %dx%d->%dx%d, B=%d)"
-                      % (H, H, OH, OH, B),
-            "bound": "mfma", "achieved": round(tflops, 2), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(tflops / BF16_PEAK_TFLOPS, 4), "traffic": None, "avg_launch_ms": round(ms, 4),
-            "algorithmic_flop_per_launch": flops}
+    name = ("conv_glds_kernel<256x128> (g_a[2] fwd: Conv2d 128->128 k5 s2, %dx%d->%dx%d, B=%d)"
+            % (H, H, OH, OH, B))
+    return {"kernel": name, "bound": "mfma", "achieved": round(tflops, 2), "peak": BF16_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(tflops / BF16_PEAK_TFLOPS, 4), "traffic": pmc_traffic(B, size),
+            "avg_launch_ms": round(ms, 4), "algorithmic_flop_per_launch": flops,
+            "algorithmic_bytes_per_launch": B * H * H * 128 * 2 + 128 * 128 * 25 * 2 + B * OH * OH * 128 * 2}
+
+
+def pmc_traffic(B, size):
+    """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC passes
+    (profiles/pmc_traffic.json, written by tools/pmc_summary.py: 2 x FETCH_SIZE + WRITE_SIZE,
+    MI355X_MICROARCH.md 'HBM'); null when no measurement for this workload is committed."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        rec = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    if rec.get("batch") != B or rec.get("size") != size:
+        return None
+    return rec.get("hbm_bytes_per_launch")
 
 
 def cpu_baseline(model_name, quality, batch, size, seconds):
@@ -124,6 +141,10 @@ def main():
     from compressai.optim import configure_optimizers
     from compressai.zoo import image_models
 
+    if args.roofline_only:
+        torch.cuda.set_device(0)
+        print(json.dumps(dominant_kernel_roofline(args.batch, args.size, reps=args.steps)))
+        return
     rank, world = init_from_env()
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
