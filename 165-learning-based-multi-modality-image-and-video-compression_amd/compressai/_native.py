@@ -55,6 +55,12 @@ SIGNATURES = {
     "cai_deconv_small_workspace_bytes": (_S, [_G, _I]),
     "cai_deconv_small_fwd": (_I, [_G, _I, _P, c_int32, _P, _P, _P, _P, _S, _P]),
     "cai_deconv_small_bwd": (_I, [_G, _I, _P, c_int32, _P, _P, _P, c_int32, _P, _P, c_int32, _P, _S, _P]),
+    "cai_add_act": (_I, [_I, _P, c_int32, _P, c_int32, _P, c_int32, _I64, c_int32, c_int32, _F, _P]),
+    "cai_act": (_I, [_I, _P, c_int32, _P, c_int32, _I64, c_int32, c_int32, _F, _P]),
+    "cai_gate_fwd": (_I, [_I, _P, _P, _P, _P, c_int32, _I64, c_int32, _P]),
+    "cai_gate_bwd": (_I, [_I, _P, _P, _P, c_int32, _P, _P, c_int32, _I64, c_int32, _P]),
+    "cai_pixel_shuffle": (_I, [_I, _P, POINTER(c_int64), _P, POINTER(c_int64), c_int32, c_int32, c_int32, c_int32,
+                               c_int32, c_int32, _P]),
     "cai_gdn_reparam": (_I, [_P, _P, c_int32, _F, _F, _I, _P, _P, _P]),
     "cai_gdn_fwd": (_I, [_I, _P, c_int32, _I64, c_int32, _P, _P, c_int32, _P, c_int32, _P]),
     "cai_gdn_bwd": (_I, [_I, _P, c_int32, _P, c_int32, _I64, c_int32, _P, _P, c_int32, _P, c_int32, _P, _P]),

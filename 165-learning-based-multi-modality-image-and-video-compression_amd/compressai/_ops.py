@@ -24,7 +24,8 @@ from typing import Optional, Sequence, Tuple
 
 import torch
 
-from ._native import (ACT_NONE, BF16, F32, MASK_NONE, Q_DEQUANTIZE, Q_NOISE, ConvGeom, EbGrads, EbParams, lib)
+from ._native import (ACT_LEAKY, ACT_NONE, ACT_RELU, BF16, F32, MASK_LEAKY, MASK_NONE, MASK_POS, Q_DEQUANTIZE, Q_NOISE,
+                      ConvGeom, EbGrads, EbParams, lib)
 
 _VP = ctypes.c_void_p
 
@@ -565,3 +566,151 @@ class RdLossFn(torch.autograd.Function):
             lib.cai_log_bwd(_p(lr), lp, C, ld, _p(gbt), bpp_coef, _p(dbuf), st)
             dliks.append(d)
         return (dxh.view(xshape), None, None, None, *dliks)
+
+
+# ---------------------------------------------------------------------------
+# pointwise glue of the residual / attention / sub-pixel blocks
+# (layers/layers.py:81-244) -- csrc/elementwise.hip
+# ---------------------------------------------------------------------------
+
+def _out_pm_like(t: torch.Tensor, dtype) -> Tuple[torch.Tensor, int]:
+    B, C, H, W = t.shape
+    ld = (C + _vec(dtype) - 1) // _vec(dtype) * _vec(dtype)
+    return empty_pm(B, C, H, W, dtype, t.device, ld=ld), ld
+
+
+_MASK_OF_ACT = {ACT_RELU: MASK_POS, ACT_LEAKY: MASK_LEAKY}
+
+
+def _act_grad(g, y, ld_y, act, prm, dtype):
+    """g * act'(pre) from the activated output y (y > 0 <=> pre > 0 for ReLU / LeakyReLU)."""
+    gp, gld = to_pm(g, dtype, _vec(dtype))
+    if act == ACT_NONE:
+        return gp
+    out, old = _out_pm_like(g, dtype)
+    B, C, H, W = g.shape
+    lib.cai_act_bwd(_MASK_OF_ACT[act], prm, _p(y), ld_y, _p(gp), gld, _p(out), old, B * H * W, C, dcode(dtype),
+                    _stream())
+    return out
+
+
+class AddActFn(torch.autograd.Function):
+    """y = act(a + b): the residual `out += identity` (+ the trailing ReLU of ResidualUnit)."""
+
+    @staticmethod
+    def forward(ctx, a, b, act: int, prm: float):
+        _check_cuda(a, b)
+        if a.shape != b.shape:
+            raise ValueError(f"residual add: shape mismatch {tuple(a.shape)} vs {tuple(b.shape)}")
+        dt = compute_dtype()
+        vec = _vec(dt)
+        ap, ald = to_pm(a, dt, vec)
+        bp, bld = to_pm(b, dt, vec)
+        y, yld = _out_pm_like(a, dt)
+        B, C, H, W = a.shape
+        lib.cai_add_act(dcode(dt), _p(ap), ald, _p(bp), bld, _p(y), yld, B * H * W, C, act, prm, _stream())
+        ctx.cfg = (act, prm, dt, yld)
+        ctx.save_for_backward(y if act != ACT_NONE else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (y,) = ctx.saved_tensors
+        act, prm, dt, yld = ctx.cfg
+        d = _act_grad(g, y, yld, act, prm, dt)
+        return d, d, None, None
+
+
+class ActFn(torch.autograd.Function):
+    """Standalone ReLU / LeakyReLU (when no conv epilogue can absorb it)."""
+
+    @staticmethod
+    def forward(ctx, x, act: int, prm: float):
+        _check_cuda(x)
+        dt = compute_dtype()
+        xp, xld = to_pm(x, dt, _vec(dt))
+        y, yld = _out_pm_like(x, dt)
+        B, C, H, W = x.shape
+        lib.cai_act(dcode(dt), _p(xp), xld, _p(y), yld, B * H * W, C, act, prm, _stream())
+        ctx.cfg = (act, prm, dt, yld)
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (y,) = ctx.saved_tensors
+        act, prm, dt, yld = ctx.cfg
+        return _act_grad(g, y, yld, act, prm, dt), None, None
+
+
+class GateFn(torch.autograd.Function):
+    """AttentionBlock (layers.py:238-243): y = a * sigmoid(b) + x."""
+
+    @staticmethod
+    def forward(ctx, a, b, x):
+        _check_cuda(a, b, x)
+        dt = compute_dtype()
+        B, C, H, W = a.shape
+        ld = (C + _vec(dt) - 1) // _vec(dt) * _vec(dt)
+
+        def same(t):   # the kernel takes one ld for a, b, x, y
+            tp, tld = to_pm(t, dt, _vec(dt))
+            if tld != ld:
+                tp2 = empty_pm(B, C, H, W, dt, t.device, ld=ld)
+                tp2.copy_(tp)
+                tp = tp2
+            return tp
+        ap, bp, xp = same(a), same(b), same(x)
+        y = empty_pm(B, C, H, W, dt, a.device, ld=ld)
+        lib.cai_gate_fwd(dcode(dt), _p(ap), _p(bp), _p(xp), _p(y), ld, B * H * W, C, _stream())
+        ctx.cfg = (dt, ld)
+        ctx.save_for_backward(ap, bp)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        ap, bp = ctx.saved_tensors
+        dt, ld = ctx.cfg
+        B, C, H, W = ap.shape
+        gp, gld = to_pm(g, dt, _vec(dt))
+        da = empty_pm(B, C, H, W, dt, g.device, ld=ld)
+        db = empty_pm(B, C, H, W, dt, g.device, ld=ld)
+        lib.cai_gate_bwd(dcode(dt), _p(ap), _p(bp), _p(gp), gld, _p(da), _p(db), ld, B * H * W, C, _stream())
+        return da, db, g
+
+
+def _bhwc_strides(t: torch.Tensor):
+    s = t.stride()
+    return (ctypes.c_int64 * 4)(s[0], s[2], s[3], s[1])
+
+
+class PixelShuffleFn(torch.autograd.Function):
+    """nn.PixelShuffle(r) (subpel_conv3x3, layers.py:86-91) on any layout; pixel-major stays pixel-major."""
+
+    @staticmethod
+    def forward(ctx, x, r: int):
+        _check_cuda(x)
+        B, Cr, H, W = x.shape
+        if Cr % (r * r):
+            raise ValueError(f"pixel_shuffle: {Cr} channels not divisible by r^2 = {r * r}")
+        C = Cr // (r * r)
+        dt = x.dtype
+        if dt not in (torch.float32, torch.bfloat16):
+            raise ValueError("pixel_shuffle: fp32 / bf16 only")
+        pm = pixel_major_ld(x) is not None and C % _vec(dt) == 0
+        y = empty_pm(B, C, H * r, W * r, dt, x.device) if pm else torch.empty((B, C, H * r, W * r), dtype=dt,
+                                                                              device=x.device)
+        lib.cai_pixel_shuffle(dcode(dt), _p(x), _bhwc_strides(x), _p(y), _bhwc_strides(y), B, H, W, C, r, 0,
+                              _stream())
+        ctx.cfg = (r, dt, tuple(x.shape), pixel_major_ld(x) is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        r, dt, xshape, x_pm = ctx.cfg
+        B, Cr, H, W = xshape
+        g = g.to(dt)
+        dx = empty_pm(B, Cr, H, W, dt, g.device) if x_pm else torch.empty(xshape, dtype=dt, device=g.device)
+        lib.cai_pixel_shuffle(dcode(dt), _p(g), _bhwc_strides(g), _p(dx), _bhwc_strides(dx), B, H, W, Cr // (r * r),
+                              r, 1, _stream())
+        return dx, None

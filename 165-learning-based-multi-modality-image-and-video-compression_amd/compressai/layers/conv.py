@@ -17,7 +17,7 @@ import torch
 import torch.nn as nn
 
 from .._native import ACT_LEAKY, ACT_NONE, ACT_RELU, MASK_LEAKY, MASK_NONE, MASK_POS, MASK_SIGN
-from .._ops import ConvFn, ConvSpec
+from .._ops import ActFn, ConvFn, ConvSpec, PixelShuffleFn
 
 
 def _square(v, name):
@@ -62,35 +62,75 @@ class ConvTranspose2d(_ConvMixin, nn.ConvTranspose2d):
 _CONVS = (Conv2d, ConvTranspose2d)
 
 
-class Sequential(nn.Sequential):
-    """nn.Sequential with conv+activation epilogue fusion (see module docstring)."""
+def _act_of(m):
+    if isinstance(m, nn.ReLU):
+        return ACT_RELU, 0.0
+    if isinstance(m, nn.LeakyReLU):
+        return ACT_LEAKY, float(m.negative_slope)
+    return ACT_NONE, 0.0
 
-    def forward(self, x, input_abs: bool = False):
+
+class PixelShuffle(nn.PixelShuffle):
+    """nn.PixelShuffle on the HIP permutation kernel (pixel-major in -> pixel-major out)."""
+
+    def forward(self, x):
+        return PixelShuffleFn.apply(x, int(self.upscale_factor))
+
+
+def _is_subpel(m):
+    """Sequential(conv, PixelShuffle) as built by subpel_conv3x3 (layers.py:86-91)."""
+    return (isinstance(m, Sequential) and len(m) == 2 and isinstance(m[0], _CONVS)
+            and isinstance(m[1], nn.PixelShuffle))
+
+
+class Sequential(nn.Sequential):
+    """nn.Sequential with conv+activation epilogue fusion (see module docstring).
+
+    A sub-pixel block (conv, PixelShuffle) counts as a conv: an activation after
+    it runs in the conv epilogue (the permutation commutes with it), and its
+    backward mask in the next conv's dgrad epilogue, whose aux input is the
+    shuffled activation.  ``act`` applies a trailing activation requested by an
+    enclosing Sequential."""
+
+    def forward(self, x, input_abs: bool = False, act: int = ACT_NONE, act_param: float = 0.0,
+                in_mask: int = MASK_NONE, in_mask_param: float = 0.0, act_bwd_downstream: bool = False):
         mods = list(self)
         n = len(mods)
         i = 0
-        pending = (MASK_SIGN, 0.0) if input_abs else (MASK_NONE, 0.0)
+        pending = (MASK_SIGN, 0.0) if input_abs else (in_mask, in_mask_param)
         first = True
         while i < n:
             m = mods[i]
-            if isinstance(m, _CONVS):
-                act, prm, skip = ACT_NONE, 0.0, 0
-                nxt = mods[i + 1] if i + 1 < n else None
-                if isinstance(nxt, nn.ReLU):
-                    act, skip = ACT_RELU, 1
-                elif isinstance(nxt, nn.LeakyReLU):
-                    act, prm, skip = ACT_LEAKY, float(nxt.negative_slope), 1
+            convlike = isinstance(m, _CONVS) or _is_subpel(m)
+            if convlike:
+                a, prm = _act_of(mods[i + 1]) if i + 1 < n else (ACT_NONE, 0.0)
+                skip = 1 if a != ACT_NONE else 0
+                # last producer: only permutations (PixelShuffle) follow it
+                last = all(isinstance(mm, nn.PixelShuffle) for mm in mods[i + 1 + skip:])
+                if last and a == ACT_NONE and act != ACT_NONE:
+                    a, prm = act, act_param           # the enclosing Sequential's activation
                 after = mods[i + 1 + skip] if i + 1 + skip < n else None
-                downstream = act != ACT_NONE and isinstance(after, _CONVS)
-                x = m.run(x, act=act, act_param=prm, in_abs=(input_abs and first), in_mask=pending[0],
-                          in_mask_param=pending[1], act_bwd_downstream=downstream)
-                pending = ((MASK_POS if act == ACT_RELU else MASK_LEAKY), prm) if downstream else (MASK_NONE, 0.0)
+                if last:
+                    downstream = a != ACT_NONE and act_bwd_downstream
+                else:
+                    downstream = a != ACT_NONE and (isinstance(after, _CONVS) or _is_subpel(after))
+                kw = dict(act=a, act_param=prm, in_mask=pending[0], in_mask_param=pending[1],
+                          act_bwd_downstream=downstream)
+                if isinstance(m, _CONVS):
+                    x = m.run(x, in_abs=(input_abs and first), **kw)
+                else:
+                    x = m(x, input_abs=(input_abs and first), **kw)
+                pending = ((MASK_POS if a == ACT_RELU else MASK_LEAKY), prm) if downstream else (MASK_NONE, 0.0)
                 i += 1 + skip
             else:
                 if input_abs and first:
                     x = torch.abs(x)
-                x = m(x)
+                a, prm = _act_of(m)
+                x = ActFn.apply(x, a, prm) if a != ACT_NONE else m(x)
                 pending = (MASK_NONE, 0.0)
                 i += 1
             first = False
+        if act != ACT_NONE and not (n and (isinstance(mods[-1], _CONVS) or _is_subpel(mods[-1])
+                                           or isinstance(mods[-1], nn.PixelShuffle))):
+            x = ActFn.apply(x, act, act_param)
         return x

@@ -1,17 +1,31 @@
-"""Layer zoo (reference: compressai/layers/layers.py:40-296).
+"""Layer zoo (reference: compressai/layers/layers.py:40-244).
 
 MaskedConv2d follows layers.py:52-78: the weight is masked in place before
 every call (so gradients reach masked taps exactly as in the reference), then
 the conv runs on the HIP implicit-GEMM kernel.
+
+The residual / attention blocks of the cheng2020 models (layers.py:97-244)
+keep the reference's module tree (so state_dict keys match: ``conv1``,
+``conv2``, ``gdn``, ``skip``, ``subpel_conv.0``, ``upsample.0``,
+``conv_a.0.conv.2`` ...).  Their forward passes chain the HIP convs with the
+activation in the conv epilogue and its backward mask in the next conv's
+dgrad epilogue; the residual add (+ trailing ReLU), the attention gate and
+the pixel shuffle run on the elementwise kernels (csrc/elementwise.hip).
 """
 from typing import Any
 
 import torch
 import torch.nn as nn
 
-from .conv import Conv2d, ConvTranspose2d
+from .._native import ACT_LEAKY, ACT_NONE, ACT_RELU, MASK_LEAKY
+from .._ops import AddActFn, GateFn
+from .conv import Conv2d, ConvTranspose2d, PixelShuffle, Sequential
+from .gdn import GDN
 
-__all__ = ["MaskedConv2d", "conv1x1", "conv3x3"]
+__all__ = ["MaskedConv2d", "conv1x1", "conv3x3", "subpel_conv3x3", "PixelShuffle", "ResidualBlockWithStride",
+           "ResidualBlockUpsample", "ResidualBlock", "AttentionBlock"]
+
+_SLOPE = 0.01   # nn.LeakyReLU() default negative_slope
 
 
 class MaskedConv2d(Conv2d):
@@ -35,3 +49,90 @@ def conv3x3(in_ch: int, out_ch: int, stride: int = 1) -> nn.Module:
 
 def conv1x1(in_ch: int, out_ch: int, stride: int = 1) -> nn.Module:
     return Conv2d(in_ch, out_ch, kernel_size=1, stride=stride)
+
+
+def subpel_conv3x3(in_ch: int, out_ch: int, r: int = 1) -> nn.Module:
+    """layers.py:86-91: conv3x3 to out_ch*r^2 channels, then PixelShuffle(r)."""
+    return Sequential(Conv2d(in_ch, out_ch * r ** 2, kernel_size=3, padding=1), PixelShuffle(r))
+
+
+class ResidualBlockWithStride(nn.Module):
+    """layers.py:97-129: conv3x3(s) -> LeakyReLU -> conv3x3 -> GDN, + skip (conv1x1(s) or identity)."""
+
+    def __init__(self, in_ch: int, out_ch: int, stride: int = 2):
+        super().__init__()
+        self.conv1 = conv3x3(in_ch, out_ch, stride=stride)
+        self.leaky_relu = nn.LeakyReLU(inplace=True)
+        self.conv2 = conv3x3(out_ch, out_ch)
+        self.gdn = GDN(out_ch)
+        self.skip = conv1x1(in_ch, out_ch, stride=stride) if (stride != 1 or in_ch != out_ch) else None
+
+    def forward(self, x):
+        out = self.conv1.run(x, act=ACT_LEAKY, act_param=_SLOPE, act_bwd_downstream=True)
+        out = self.conv2.run(out, in_mask=MASK_LEAKY, in_mask_param=_SLOPE)
+        out = self.gdn(out)
+        identity = self.skip(x) if self.skip is not None else x
+        return AddActFn.apply(out, identity, ACT_NONE, 0.0)
+
+
+class ResidualBlockUpsample(nn.Module):
+    """layers.py:132-159: subpel_conv3x3 -> LeakyReLU -> conv3x3 -> IGDN, + subpel_conv3x3(x)."""
+
+    def __init__(self, in_ch: int, out_ch: int, upsample: int = 2):
+        super().__init__()
+        self.subpel_conv = subpel_conv3x3(in_ch, out_ch, upsample)
+        self.leaky_relu = nn.LeakyReLU(inplace=True)
+        self.conv = conv3x3(out_ch, out_ch)
+        self.igdn = GDN(out_ch, inverse=True)
+        self.upsample = subpel_conv3x3(in_ch, out_ch, upsample)
+
+    def forward(self, x):
+        out = self.subpel_conv(x, act=ACT_LEAKY, act_param=_SLOPE, act_bwd_downstream=True)
+        out = self.conv.run(out, in_mask=MASK_LEAKY, in_mask_param=_SLOPE)
+        out = self.igdn(out)
+        identity = self.upsample(x)
+        return AddActFn.apply(out, identity, ACT_NONE, 0.0)
+
+
+class ResidualBlock(nn.Module):
+    """layers.py:162-193: conv3x3 -> LeakyReLU -> conv3x3 -> LeakyReLU, + skip (conv1x1 or identity)."""
+
+    def __init__(self, in_ch: int, out_ch: int):
+        super().__init__()
+        self.conv1 = conv3x3(in_ch, out_ch)
+        self.leaky_relu = nn.LeakyReLU(inplace=True)
+        self.conv2 = conv3x3(out_ch, out_ch)
+        self.skip = conv1x1(in_ch, out_ch) if in_ch != out_ch else None
+
+    def forward(self, x):
+        out = self.conv1.run(x, act=ACT_LEAKY, act_param=_SLOPE, act_bwd_downstream=True)
+        out = self.conv2.run(out, act=ACT_LEAKY, act_param=_SLOPE, in_mask=MASK_LEAKY, in_mask_param=_SLOPE)
+        identity = self.skip(x) if self.skip is not None else x
+        return AddActFn.apply(out, identity, ACT_NONE, 0.0)
+
+
+class ResidualUnit(nn.Module):
+    """AttentionBlock's inner unit (layers.py:211-226): relu(conv1x1 -> ReLU -> conv3x3 -> ReLU -> conv1x1 + x)."""
+
+    def __init__(self, N: int):
+        super().__init__()
+        self.conv = Sequential(conv1x1(N, N // 2), nn.ReLU(inplace=True), conv3x3(N // 2, N // 2),
+                               nn.ReLU(inplace=True), conv1x1(N // 2, N))
+        self.relu = nn.ReLU(inplace=True)
+
+    def forward(self, x):
+        return AddActFn.apply(self.conv(x), x, ACT_RELU, 0.0)
+
+
+class AttentionBlock(nn.Module):
+    """layers.py:196-244: x + conv_a(x) * sigmoid(conv_b(x))."""
+
+    def __init__(self, N: int):
+        super().__init__()
+        self.conv_a = Sequential(ResidualUnit(N), ResidualUnit(N), ResidualUnit(N))
+        self.conv_b = Sequential(ResidualUnit(N), ResidualUnit(N), ResidualUnit(N), conv1x1(N, N))
+
+    def forward(self, x):
+        a = self.conv_a(x)
+        b = self.conv_b(x)
+        return GateFn.apply(a, b, x)

@@ -1,0 +1,246 @@
+// Pointwise glue of the residual / attention / sub-pixel blocks
+// (compressai/layers/layers.py:81-244: ResidualBlockWithStride,
+// ResidualBlockUpsample, ResidualBlock, AttentionBlock, subpel_conv3x3) on
+// pixel-major activations.  All kernels move 16-byte chunks (8 bf16 / 4 fp32)
+// when the channel count allows it, and are HBM-bound by construction:
+//   add_act      y = act(a + b)                       12 B/elem (bf16: 6)
+//   act          y = act(x)                           (used when no conv epilogue can take it)
+//   gate fwd     y = a * sigmoid(b) + x               AttentionBlock.forward, layers.py:236-243
+//   gate bwd     da = g * s(b), db = g * a * s(b)(1 - s(b))
+//   pixel shuffle / its inverse (torch.nn.PixelShuffle channel order c*r^2 + i*r + j)
+#include "common.hpp"
+
+#include <algorithm>
+
+namespace cai {
+
+__device__ __forceinline__ float act_f(float v, int act, float prm) {
+    if (act == CAI_ACT_RELU) return v > 0.f ? v : 0.f;
+    if (act == CAI_ACT_LEAKY) return v > 0.f ? v : v * prm;
+    return v;
+}
+
+template <typename T>
+struct Vec;
+template <>
+struct Vec<bf16> {
+    static constexpr int N = 8;
+    typedef bf16x8 V;
+};
+template <>
+struct Vec<float> {
+    static constexpr int N = 4;
+    typedef f32x4 V;
+};
+
+// one thread per (pixel, chunk of N channels); `vec` chunks when C % N == 0
+template <typename T>
+__global__ void add_act_kernel(const T* __restrict__ a, int ald, const T* __restrict__ b, int bld, T* __restrict__ y,
+                               int yld, int npix, int C, int act, float prm) {
+    constexpr int N = Vec<T>::N;
+    const int nch = (C + N - 1) / N;
+    const int64_t total = (int64_t)npix * nch;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int p = (int)(i / nch), c0 = (int)(i - (int64_t)p * nch) * N;
+        if (c0 + N <= C) {
+            const typename Vec<T>::V va = *reinterpret_cast<const typename Vec<T>::V*>(a + (int64_t)p * ald + c0);
+            const typename Vec<T>::V vb = *reinterpret_cast<const typename Vec<T>::V*>(b + (int64_t)p * bld + c0);
+            typename Vec<T>::V vy;
+#pragma unroll
+            for (int e = 0; e < N; ++e) vy[e] = from_f32<T>(act_f(to_f32(va[e]) + to_f32(vb[e]), act, prm));
+            *reinterpret_cast<typename Vec<T>::V*>(y + (int64_t)p * yld + c0) = vy;
+        } else {
+            for (int c = c0; c < C; ++c)
+                y[(int64_t)p * yld + c] =
+                    from_f32<T>(act_f(to_f32(a[(int64_t)p * ald + c]) + to_f32(b[(int64_t)p * bld + c]), act, prm));
+        }
+    }
+}
+
+template <typename T>
+__global__ void act_kernel(const T* __restrict__ x, int xld, T* __restrict__ y, int yld, int npix, int C, int act,
+                           float prm) {
+    constexpr int N = Vec<T>::N;
+    const int nch = (C + N - 1) / N;
+    const int64_t total = (int64_t)npix * nch;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int p = (int)(i / nch), c0 = (int)(i - (int64_t)p * nch) * N;
+        if (c0 + N <= C) {
+            const typename Vec<T>::V vx = *reinterpret_cast<const typename Vec<T>::V*>(x + (int64_t)p * xld + c0);
+            typename Vec<T>::V vy;
+#pragma unroll
+            for (int e = 0; e < N; ++e) vy[e] = from_f32<T>(act_f(to_f32(vx[e]), act, prm));
+            *reinterpret_cast<typename Vec<T>::V*>(y + (int64_t)p * yld + c0) = vy;
+        } else {
+            for (int c = c0; c < C; ++c) y[(int64_t)p * yld + c] = from_f32<T>(act_f(to_f32(x[(int64_t)p * xld + c]), act, prm));
+        }
+    }
+}
+
+__device__ __forceinline__ float sigmoidf_(float v) { return 1.f / (1.f + __expf(-v)); }
+
+// y = a * sigmoid(b) + x
+template <typename T>
+__global__ void gate_fwd_kernel(const T* __restrict__ a, const T* __restrict__ b, const T* __restrict__ x,
+                                T* __restrict__ y, int ld, int npix, int C) {
+    const int64_t total = (int64_t)npix * C;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int p = (int)(i / C), c = (int)(i - (int64_t)p * C);
+        const int64_t o = (int64_t)p * ld + c;
+        y[o] = from_f32<T>(to_f32(a[o]) * sigmoidf_(to_f32(b[o])) + to_f32(x[o]));
+    }
+}
+
+template <typename T>
+__global__ void gate_bwd_kernel(const T* __restrict__ a, const T* __restrict__ b, const T* __restrict__ g, int gld,
+                                T* __restrict__ da, T* __restrict__ db, int ld, int npix, int C) {
+    const int64_t total = (int64_t)npix * C;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int p = (int)(i / C), c = (int)(i - (int64_t)p * C);
+        const int64_t o = (int64_t)p * ld + c;
+        const float s = sigmoidf_(to_f32(b[o]));
+        const float gv = to_f32(g[(int64_t)p * gld + c]);
+        da[o] = from_f32<T>(gv * s);
+        db[o] = from_f32<T>(gv * to_f32(a[o]) * s * (1.f - s));
+    }
+}
+
+// Pixel shuffle between x [B][H][W][C*r*r] (channel n = c*r*r + i*r + j) and
+// y [B][H*r][W*r][C], both given by element strides (b, row, col, channel) so
+// either side may be pixel-major or NCHW.  inverse = 0: y <- x; 1: x <- y.
+struct ShuffleArgs {
+    const void* src;
+    void* dst;
+    int64_t xs[4], ys[4];
+    int B, H, W, C, r, inverse;
+};
+
+template <typename T>
+__global__ void pixel_shuffle_kernel(const ShuffleArgs s) {
+    const int OH = s.H * s.r, OW = s.W * s.r;
+    const int64_t total = (int64_t)s.B * OH * OW * s.C;
+    const T* src = reinterpret_cast<const T*>(s.src);
+    T* dst = reinterpret_cast<T*>(s.dst);
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        // y-major order: channel fastest (coalesced on the pixel-major side)
+        const int c = (int)(i % s.C);
+        int64_t r = i / s.C;
+        const int ox = (int)(r % OW);
+        r /= OW;
+        const int oy = (int)(r % OH);
+        const int b = (int)(r / OH);
+        const int h = oy / s.r, ii = oy - h * s.r, w = ox / s.r, jj = ox - w * s.r;
+        const int n = (c * s.r + ii) * s.r + jj;
+        const int64_t xo = b * s.xs[0] + h * s.xs[1] + w * s.xs[2] + n * s.xs[3];
+        const int64_t yo = b * s.ys[0] + oy * s.ys[1] + ox * s.ys[2] + c * s.ys[3];
+        if (s.inverse)
+            dst[xo] = src[yo];
+        else
+            dst[yo] = src[xo];
+    }
+}
+
+static int ew_grid2(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(16384, (n + 255) / 256)); }
+
+}  // namespace cai
+
+using namespace cai;
+
+extern "C" {
+
+int cai_add_act(int dtype, const void* a, int32_t a_ld, const void* b, int32_t b_ld, void* y, int32_t y_ld,
+                int64_t npix, int32_t C, int32_t act, float act_param, void* stream) {
+    CAI_CHECK_ARG(dtype == CAI_BF16 || dtype == CAI_F32, "add_act: bad dtype");
+    CAI_CHECK_ARG(a && b && y && a_ld >= C && b_ld >= C && y_ld >= C, "add_act: bad arguments");
+    CAI_CHECK_ARG(npix < (1ll << 31), "add_act: too many pixels");
+    const int N = dtype == CAI_BF16 ? 8 : 4;
+    CAI_CHECK_ARG(a_ld % N == 0 && b_ld % N == 0 && y_ld % N == 0, "add_act: ld must be a multiple of %d", N);
+    const int64_t n = npix * ((C + N - 1) / N);
+    if (n == 0) return CAI_OK;
+    hipStream_t st = as_stream(stream);
+    if (dtype == CAI_BF16)
+        hipLaunchKernelGGL(add_act_kernel<bf16>, dim3(ew_grid2(n)), dim3(256), 0, st, (const bf16*)a, a_ld,
+                           (const bf16*)b, b_ld, (bf16*)y, y_ld, (int)npix, C, act, act_param);
+    else
+        hipLaunchKernelGGL(add_act_kernel<float>, dim3(ew_grid2(n)), dim3(256), 0, st, (const float*)a, a_ld,
+                           (const float*)b, b_ld, (float*)y, y_ld, (int)npix, C, act, act_param);
+    CAI_LAUNCH_CHECK("add_act");
+    return CAI_OK;
+}
+
+int cai_act(int dtype, const void* x, int32_t x_ld, void* y, int32_t y_ld, int64_t npix, int32_t C, int32_t act,
+            float act_param, void* stream) {
+    CAI_CHECK_ARG(dtype == CAI_BF16 || dtype == CAI_F32, "act: bad dtype");
+    CAI_CHECK_ARG(x && y && x_ld >= C && y_ld >= C && npix < (1ll << 31), "act: bad arguments");
+    const int N = dtype == CAI_BF16 ? 8 : 4;
+    CAI_CHECK_ARG(x_ld % N == 0 && y_ld % N == 0, "act: ld must be a multiple of %d", N);
+    const int64_t n = npix * ((C + N - 1) / N);
+    if (n == 0) return CAI_OK;
+    hipStream_t st = as_stream(stream);
+    if (dtype == CAI_BF16)
+        hipLaunchKernelGGL(act_kernel<bf16>, dim3(ew_grid2(n)), dim3(256), 0, st, (const bf16*)x, x_ld, (bf16*)y, y_ld,
+                           (int)npix, C, act, act_param);
+    else
+        hipLaunchKernelGGL(act_kernel<float>, dim3(ew_grid2(n)), dim3(256), 0, st, (const float*)x, x_ld, (float*)y,
+                           y_ld, (int)npix, C, act, act_param);
+    CAI_LAUNCH_CHECK("act");
+    return CAI_OK;
+}
+
+int cai_gate_fwd(int dtype, const void* a, const void* b, const void* x, void* y, int32_t ld, int64_t npix, int32_t C,
+                 void* stream) {
+    CAI_CHECK_ARG(dtype == CAI_BF16 || dtype == CAI_F32, "gate_fwd: bad dtype");
+    CAI_CHECK_ARG(a && b && x && y && ld >= C && npix < (1ll << 31), "gate_fwd: bad arguments");
+    const int64_t n = npix * C;
+    if (n == 0) return CAI_OK;
+    hipStream_t st = as_stream(stream);
+    if (dtype == CAI_BF16)
+        hipLaunchKernelGGL(gate_fwd_kernel<bf16>, dim3(ew_grid2(n)), dim3(256), 0, st, (const bf16*)a, (const bf16*)b,
+                           (const bf16*)x, (bf16*)y, ld, (int)npix, C);
+    else
+        hipLaunchKernelGGL(gate_fwd_kernel<float>, dim3(ew_grid2(n)), dim3(256), 0, st, (const float*)a,
+                           (const float*)b, (const float*)x, (float*)y, ld, (int)npix, C);
+    CAI_LAUNCH_CHECK("gate_fwd");
+    return CAI_OK;
+}
+
+int cai_gate_bwd(int dtype, const void* a, const void* b, const void* g, int32_t g_ld, void* da, void* db, int32_t ld,
+                 int64_t npix, int32_t C, void* stream) {
+    CAI_CHECK_ARG(dtype == CAI_BF16 || dtype == CAI_F32, "gate_bwd: bad dtype");
+    CAI_CHECK_ARG(a && b && g && da && db && ld >= C && g_ld >= C && npix < (1ll << 31), "gate_bwd: bad arguments");
+    const int64_t n = npix * C;
+    if (n == 0) return CAI_OK;
+    hipStream_t st = as_stream(stream);
+    if (dtype == CAI_BF16)
+        hipLaunchKernelGGL(gate_bwd_kernel<bf16>, dim3(ew_grid2(n)), dim3(256), 0, st, (const bf16*)a, (const bf16*)b,
+                           (const bf16*)g, g_ld, (bf16*)da, (bf16*)db, ld, (int)npix, C);
+    else
+        hipLaunchKernelGGL(gate_bwd_kernel<float>, dim3(ew_grid2(n)), dim3(256), 0, st, (const float*)a,
+                           (const float*)b, (const float*)g, g_ld, (float*)da, (float*)db, ld, (int)npix, C);
+    CAI_LAUNCH_CHECK("gate_bwd");
+    return CAI_OK;
+}
+
+int cai_pixel_shuffle(int dtype, const void* src, const int64_t* src_strides, void* dst, const int64_t* dst_strides,
+                      int32_t B, int32_t H, int32_t W, int32_t C, int32_t r, int32_t inverse, void* stream) {
+    CAI_CHECK_ARG(dtype == CAI_BF16 || dtype == CAI_F32, "pixel_shuffle: bad dtype");
+    CAI_CHECK_ARG(src && dst && src_strides && dst_strides && r >= 1 && B > 0 && H > 0 && W > 0 && C > 0,
+                  "pixel_shuffle: bad arguments");
+    ShuffleArgs s{};
+    s.src = src; s.dst = dst;
+    // strides are given for the (source, destination) tensors; map them to x / y
+    const int64_t* xs = inverse ? dst_strides : src_strides;
+    const int64_t* ys = inverse ? src_strides : dst_strides;
+    for (int i = 0; i < 4; ++i) { s.xs[i] = xs[i]; s.ys[i] = ys[i]; }
+    s.B = B; s.H = H; s.W = W; s.C = C; s.r = r; s.inverse = inverse;
+    const int64_t n = (int64_t)B * H * r * W * r * C;
+    hipStream_t st = as_stream(stream);
+    if (dtype == CAI_BF16)
+        hipLaunchKernelGGL(pixel_shuffle_kernel<bf16>, dim3(ew_grid2(n)), dim3(256), 0, st, s);
+    else
+        hipLaunchKernelGGL(pixel_shuffle_kernel<float>, dim3(ew_grid2(n)), dim3(256), 0, st, s);
+    CAI_LAUNCH_CHECK("pixel_shuffle");
+    return CAI_OK;
+}
+
+}  // extern "C"

@@ -148,6 +148,30 @@ int cai_deconv_small_bwd(const cai_conv_geom* g, int dtype, const void* x, int32
                          void* workspace, size_t ws_bytes, void* stream);
 
 /* =======================================================================
+ * Pointwise glue of the residual / attention / sub-pixel blocks
+ * (layers/layers.py:81-244), pixel-major, ld a multiple of 8 (bf16) / 4 (fp32).
+ * ======================================================================= */
+/* y = act(a + b): `out += identity` (layers.py:124,177) with the trailing
+ * ReLU of AttentionBlock's ResidualUnit (layers.py:222-226) folded in. */
+int cai_add_act(int dtype, const void* a, int32_t a_ld, const void* b, int32_t b_ld, void* y, int32_t y_ld,
+                int64_t npix, int32_t C, int32_t act, float act_param, void* stream);
+/* y = act(x) for a ReLU / LeakyReLU that no conv epilogue can absorb. */
+int cai_act(int dtype, const void* x, int32_t x_ld, void* y, int32_t y_ld, int64_t npix, int32_t C, int32_t act,
+            float act_param, void* stream);
+/* AttentionBlock gate (layers.py:238-243): y = a * sigmoid(b) + x;
+ * backward da = g * s(b), db = g * a * s(b) * (1 - s(b)) (dx = g). */
+int cai_gate_fwd(int dtype, const void* a, const void* b, const void* x, void* y, int32_t ld, int64_t npix, int32_t C,
+                 void* stream);
+int cai_gate_bwd(int dtype, const void* a, const void* b, const void* g, int32_t g_ld, void* da, void* db, int32_t ld,
+                 int64_t npix, int32_t C, void* stream);
+/* nn.PixelShuffle(r) of subpel_conv3x3 (layers.py:86-91) between
+ * x[B][H][W][C*r*r] and y[B][H*r][W*r][C], each side described by element
+ * strides {batch, row, column, channel}; inverse != 0 maps y back to x
+ * (the backward).  src/dst strides describe the source/destination. */
+int cai_pixel_shuffle(int dtype, const void* src, const int64_t* src_strides, void* dst, const int64_t* dst_strides,
+                      int32_t B, int32_t H, int32_t W, int32_t C, int32_t r, int32_t inverse, void* stream);
+
+/* =======================================================================
  * GDN / IGDN (layers/gdn.py:41-92), C in {32,64,96,128,192}.
  * ======================================================================= */
 /* beta = max(beta_raw, sqrt(beta_min + ped))^2 - ped ; gamma likewise with

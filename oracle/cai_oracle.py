@@ -509,6 +509,140 @@ class JointAutoregressiveHierarchicalPriors(MeanScaleHyperprior):
 
 
 # --------------------------------------------------------------------------
+# cheng2020 building blocks (layers/layers.py:81-244) and models
+# (models/waseda.py:48-158)
+# --------------------------------------------------------------------------
+
+
+def conv3x3(cin, cout, stride=1):
+    """layers.py:81-83."""
+    return nn.Conv2d(cin, cout, kernel_size=3, stride=stride, padding=1)
+
+
+def conv1x1(cin, cout, stride=1):
+    """layers.py:94-96."""
+    return nn.Conv2d(cin, cout, kernel_size=1, stride=stride)
+
+
+def subpel_conv3x3(cin, cout, r=1):
+    """layers.py:86-91: conv to cout*r^2 channels + PixelShuffle(r)."""
+    return nn.Sequential(nn.Conv2d(cin, cout * r * r, kernel_size=3, padding=1), nn.PixelShuffle(r))
+
+
+class ResidualBlockWithStride(nn.Module):
+    """layers.py:97-129."""
+
+    def __init__(self, cin, cout, stride=2):
+        super().__init__()
+        self.conv1 = conv3x3(cin, cout, stride=stride)
+        self.leaky_relu = nn.LeakyReLU(inplace=True)
+        self.conv2 = conv3x3(cout, cout)
+        self.gdn = GDN(cout)
+        self.skip = conv1x1(cin, cout, stride=stride) if (stride != 1 or cin != cout) else None
+
+    def forward(self, x):
+        out = self.gdn(self.conv2(self.leaky_relu(self.conv1(x))))
+        identity = self.skip(x) if self.skip is not None else x
+        return out + identity
+
+
+class ResidualBlockUpsample(nn.Module):
+    """layers.py:132-159."""
+
+    def __init__(self, cin, cout, upsample=2):
+        super().__init__()
+        self.subpel_conv = subpel_conv3x3(cin, cout, upsample)
+        self.leaky_relu = nn.LeakyReLU(inplace=True)
+        self.conv = conv3x3(cout, cout)
+        self.igdn = GDN(cout, inverse=True)
+        self.upsample = subpel_conv3x3(cin, cout, upsample)
+
+    def forward(self, x):
+        out = self.igdn(self.conv(self.leaky_relu(self.subpel_conv(x))))
+        return out + self.upsample(x)
+
+
+class ResidualBlock(nn.Module):
+    """layers.py:162-193."""
+
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.conv1 = conv3x3(cin, cout)
+        self.leaky_relu = nn.LeakyReLU(inplace=True)
+        self.conv2 = conv3x3(cout, cout)
+        self.skip = conv1x1(cin, cout) if cin != cout else None
+
+    def forward(self, x):
+        out = self.leaky_relu(self.conv2(self.leaky_relu(self.conv1(x))))
+        identity = self.skip(x) if self.skip is not None else x
+        return out + identity
+
+
+class ResidualUnit(nn.Module):
+    """layers.py:211-226 (defined inside AttentionBlock.__init__ in the reference)."""
+
+    def __init__(self, N):
+        super().__init__()
+        self.conv = nn.Sequential(conv1x1(N, N // 2), nn.ReLU(inplace=True), conv3x3(N // 2, N // 2),
+                                  nn.ReLU(inplace=True), conv1x1(N // 2, N))
+        self.relu = nn.ReLU(inplace=True)
+
+    def forward(self, x):
+        return self.relu(self.conv(x) + x)
+
+
+class AttentionBlock(nn.Module):
+    """layers.py:196-244."""
+
+    def __init__(self, N):
+        super().__init__()
+        self.conv_a = nn.Sequential(ResidualUnit(N), ResidualUnit(N), ResidualUnit(N))
+        self.conv_b = nn.Sequential(ResidualUnit(N), ResidualUnit(N), ResidualUnit(N), conv1x1(N, N))
+
+    def forward(self, x):
+        return self.conv_a(x) * torch.sigmoid(self.conv_b(x)) + x
+
+
+class Cheng2020Anchor(JointAutoregressiveHierarchicalPriors):
+    """waseda.py:48-123: residual analysis/synthesis, 3x3 hyper transforms, sub-pixel upsampling."""
+
+    def __init__(self, N=192, channel=3, **kwargs):
+        super().__init__(N=N, M=N, **kwargs)
+        self.g_a = nn.Sequential(
+            ResidualBlockWithStride(channel, N, stride=2), ResidualBlock(N, N),
+            ResidualBlockWithStride(N, N, stride=2), ResidualBlock(N, N),
+            ResidualBlockWithStride(N, N, stride=2), ResidualBlock(N, N), conv3x3(N, N, stride=2))
+        self.h_a = nn.Sequential(
+            conv3x3(N, N), nn.LeakyReLU(inplace=True), conv3x3(N, N), nn.LeakyReLU(inplace=True),
+            conv3x3(N, N, stride=2), nn.LeakyReLU(inplace=True), conv3x3(N, N), nn.LeakyReLU(inplace=True),
+            conv3x3(N, N, stride=2))
+        self.h_s = nn.Sequential(
+            conv3x3(N, N), nn.LeakyReLU(inplace=True), subpel_conv3x3(N, N, 2), nn.LeakyReLU(inplace=True),
+            conv3x3(N, N * 3 // 2), nn.LeakyReLU(inplace=True), subpel_conv3x3(N * 3 // 2, N * 3 // 2, 2),
+            nn.LeakyReLU(inplace=True), conv3x3(N * 3 // 2, N * 2))
+        self.g_s = nn.Sequential(
+            ResidualBlock(N, N), ResidualBlockUpsample(N, N, 2), ResidualBlock(N, N),
+            ResidualBlockUpsample(N, N, 2), ResidualBlock(N, N), ResidualBlockUpsample(N, N, 2),
+            ResidualBlock(N, N), subpel_conv3x3(N, channel, 2))
+
+
+class Cheng2020Attention(Cheng2020Anchor):
+    """waseda.py:126-158: Anchor + attention blocks in g_a / g_s."""
+
+    def __init__(self, N=192, channel=3, **kwargs):
+        super().__init__(N=N, **kwargs)
+        self.g_a = nn.Sequential(
+            ResidualBlockWithStride(channel, N, stride=2), ResidualBlock(N, N),
+            ResidualBlockWithStride(N, N, stride=2), AttentionBlock(N), ResidualBlock(N, N),
+            ResidualBlockWithStride(N, N, stride=2), ResidualBlock(N, N), conv3x3(N, N, stride=2),
+            AttentionBlock(N))
+        self.g_s = nn.Sequential(
+            AttentionBlock(N), ResidualBlock(N, N), ResidualBlockUpsample(N, N, 2), ResidualBlock(N, N),
+            ResidualBlockUpsample(N, N, 2), AttentionBlock(N), ResidualBlock(N, N),
+            ResidualBlockUpsample(N, N, 2), ResidualBlock(N, N), subpel_conv3x3(N, channel, 2))
+
+
+# --------------------------------------------------------------------------
 # L7 caller: RD loss, optimizer split, one training step (examples/train.py)
 # --------------------------------------------------------------------------
 
@@ -566,12 +700,16 @@ CFGS = {
     "bmshj2018-hyperprior": {q: ((128, 192) if q <= 5 else (192, 320)) for q in range(1, 9)},
     "mbt2018-mean": {q: ((128, 192) if q <= 4 else (192, 320)) for q in range(1, 9)},
     "mbt2018": {q: ((192, 192) if q <= 4 else (192, 320)) for q in range(1, 9)},
+    "cheng2020-anchor": {q: ((128,) if q <= 3 else (192,)) for q in range(1, 7)},
+    "cheng2020-attn": {q: ((128,) if q <= 3 else (192,)) for q in range(1, 7)},
 }
 ARCHS = {
     "bmshj2018-factorized": FactorizedPrior,
     "bmshj2018-hyperprior": ScaleHyperprior,
     "mbt2018-mean": MeanScaleHyperprior,
     "mbt2018": JointAutoregressiveHierarchicalPriors,
+    "cheng2020-anchor": Cheng2020Anchor,
+    "cheng2020-attn": Cheng2020Attention,
 }
 
 

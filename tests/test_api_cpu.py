@@ -8,7 +8,8 @@ import torch
 
 import cai_oracle as O
 
-ARCHS = ["bmshj2018-factorized", "bmshj2018-hyperprior", "mbt2018-mean", "mbt2018"]
+ARCHS = ["bmshj2018-factorized", "bmshj2018-hyperprior", "mbt2018-mean", "mbt2018", "cheng2020-anchor",
+         "cheng2020-attn"]
 
 
 @pytest.mark.parametrize("name", ARCHS)
@@ -31,10 +32,13 @@ def test_zoo_and_model_classes():
 
     assert set(image_models) == set(ARCHS)
     for cls in ("FactorizedPrior", "ScaleHyperprior", "MeanScaleHyperprior", "JointAutoregressiveHierarchicalPriors",
-                "CompressionModel"):
+                "CompressionModel", "Cheng2020Anchor", "Cheng2020Attention"):
         assert hasattr(models, cls)
     assert cfgs["bmshj2018-hyperprior"][1] == (128, 192)
     assert cfgs["bmshj2018-hyperprior"][8] == (192, 320)
+    assert cfgs["cheng2020-attn"][6] == (192,)
+    with pytest.raises(ValueError):
+        image_models["cheng2020-attn"](7)
     with pytest.raises(ValueError):
         image_models["bmshj2018-hyperprior"](9)
     with pytest.raises(ValueError):
@@ -80,3 +84,11 @@ def test_rd_loss_lambda_table():
     from compressai.losses import RateDistortionLoss
 
     assert [RateDistortionLoss(q).lmbda[q] for q in range(7)] == [256, 512, 1024, 2048, 4096, 8192, 10240]
+
+
+def test_cheng2020_attn_q6_parameter_count():
+    """cheng2020-attn q6 has 29.63 M parameters."""
+    from compressai.zoo import image_models
+
+    n = sum(p.numel() for p in image_models["cheng2020-attn"](6).parameters())
+    assert abs(n - 29.63e6) < 0.01e6

@@ -11,6 +11,7 @@ import math
 import pytest
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 import cai_oracle as O
 
@@ -50,6 +51,12 @@ CONV_CASES = [
     ("deconv", 2, 192, 3, 33, 20, 5, 2),
     ("deconv", 2, 64, 1, 12, 12, 3, 1),
     ("deconv", 2, 128, 3, 64, 64, 5, 2),
+    # cheng2020 shapes: 3x3 stride 2 (RGB and feature inputs), 1x1 stride 2 skips, 3x3 to r^2*C sub-pixel convs
+    ("conv", 2, 3, 64, 32, 32, 3, 2),
+    ("conv", 2, 64, 64, 17, 15, 3, 2),
+    ("conv", 2, 64, 128, 16, 16, 1, 2),
+    ("conv", 2, 64, 256, 8, 8, 3, 1),
+    ("conv", 2, 64, 12, 8, 8, 3, 1),
 ]
 
 
@@ -318,3 +325,70 @@ def test_rd_loss(cuda):
     assert relerr(out_d["x_hat"].grad, out_r["x_hat"].grad) < 1e-5
     assert relerr(out_d["likelihoods"]["y"].grad, out_r["likelihoods"]["y"].grad) < 1e-5
     assert relerr(out_d["likelihoods"]["z"].grad, out_r["likelihoods"]["z"].grad) < 1e-5
+
+
+# --------------------------------------------------------------------------- cheng2020 blocks
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+@pytest.mark.parametrize("pm", [True, False])
+def test_pixel_shuffle(cuda, bf16, pm):
+    from compressai._ops import PixelShuffleFn, empty_pm
+
+    torch.manual_seed(3)
+    dt = torch.bfloat16 if bf16 else torch.float32
+    x = torch.randn(2, 64, 5, 7).to(dt)
+    g = torch.randn(2, 16, 10, 14).to(dt)
+    if pm:
+        xd = empty_pm(2, 64, 5, 7, dt, cuda)
+        xd.copy_(x)
+    else:
+        xd = x.to(cuda).contiguous()
+    xd.requires_grad_()
+    y = PixelShuffleFn.apply(xd, 2)
+    y.backward(g.to(cuda))
+    assert torch.equal(y.cpu(), F.pixel_shuffle(x, 2))
+    assert torch.equal(xd.grad.cpu(), F.pixel_unshuffle(g, 2))
+
+
+def _block_pair(kind, cuda):
+    import compressai.layers as L
+
+    torch.manual_seed(4)
+    ctor = {
+        "rbws3": (lambda M: M.ResidualBlockWithStride(3, 32, 2)),
+        "rbws": (lambda M: M.ResidualBlockWithStride(32, 32, 2)),
+        "rb": (lambda M: M.ResidualBlock(32, 32)),
+        "rbskip": (lambda M: M.ResidualBlock(32, 64)),
+        "rbup": (lambda M: M.ResidualBlockUpsample(32, 32, 2)),
+        "attn": (lambda M: M.AttentionBlock(32)),
+        "subpel": (lambda M: M.subpel_conv3x3(32, 3, 2)),
+    }[kind]
+    ref = ctor(O)
+    mod = ctor(L)
+    mod.load_state_dict(ref.state_dict())
+    cin = 3 if kind == "rbws3" else 32
+    return ref, mod.to(cuda), cin
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+@pytest.mark.parametrize("kind", ["rbws3", "rbws", "rb", "rbskip", "rbup", "attn", "subpel"])
+def test_cheng2020_blocks(cuda, kind, bf16):
+    ref, mod, cin = _block_pair(kind, cuda)
+    x = torch.randn(2, cin, 16, 12, generator=torch.Generator().manual_seed(5))
+    xr = x.clone().requires_grad_()
+    yr = ref(xr)
+    g = torch.randn(yr.shape, generator=torch.Generator().manual_seed(6))
+    yr.backward(g)
+    xd = x.to(cuda).requires_grad_()
+    with _autocast(bf16):
+        y = mod(xd)
+    y.backward(g.to(cuda))
+    tol = 3e-2 if bf16 else 1e-4
+    gtol = 5e-2 if bf16 else 2e-3
+    assert y.shape == yr.shape
+    assert relerr(y, yr) < tol
+    assert relerr(xd.grad, xr.grad) < gtol
+    pr = dict(ref.named_parameters())
+    for n, p in mod.named_parameters():
+        assert relerr(p.grad, pr[n].grad) < gtol, n

@@ -14,15 +14,17 @@ import cai_oracle as O
 
 pytestmark = pytest.mark.gpu
 
-MODELS = ["bmshj2018-factorized", "bmshj2018-hyperprior", "mbt2018-mean", "mbt2018"]
+MODELS = ["bmshj2018-factorized", "bmshj2018-hyperprior", "mbt2018-mean", "mbt2018", "cheng2020-anchor",
+          "cheng2020-attn"]
 
 
 def _pair(name, N, M, dev):
     from compressai.zoo import model_architectures
 
     torch.manual_seed(0)
-    ref = O.ARCHS[name](N, M)
-    net = model_architectures[name](N, M)
+    args = (N,) if name.startswith("cheng2020") else (N, M)
+    ref = O.ARCHS[name](*args)
+    net = model_architectures[name](*args)
     net.load_state_dict(ref.state_dict())
     return ref, net.to(dev)
 
