@@ -1547,10 +1547,12 @@ int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_l
         a.Hg = g->in_h; a.Wg = g->in_w; a.Hx = g->out_h; a.Wx = g->out_w;
         CAI_CHECK_ARG(!in_abs && !in_sq, "conv_wgrad: input transforms only for Conv2d");
     }
-    CAI_CHECK_ARG(W.Ng % VEC == 0, "conv_wgrad: gradient-row channels %d must be a multiple of %d", W.Ng, VEC);
+    // gradient rows are read in VEC-channel chunks: rows past Ng (inside g_ld) only
+    // feed output rows that are never stored
     CAI_CHECK_ARG(W.M < (1ll << 31), "conv_wgrad: too many pixels");
-    CAI_CHECK_ARG(a.g_ld % VEC == 0 && a.x_ld % VEC == 0 && a.x_ld >= W.Cq_pad && a.g_ld >= W.Ng,
-                  "conv_wgrad: bad leading dimensions");
+    CAI_CHECK_ARG(a.g_ld % VEC == 0 && a.x_ld % VEC == 0 && a.x_ld >= W.Cq_pad && a.g_ld >= round_up(W.Ng, VEC),
+                  "conv_wgrad: bad leading dimensions (g_ld %d for %d rows, x_ld %d for %d columns)", a.g_ld, W.Ng,
+                  a.x_ld, W.Cq_pad);
     CAI_CHECK_ARG(!db || (dy_ld % VEC == 0 && g->out_c <= COLSUM_MAXC), "conv_wgrad: bad bias-gradient layout");
     a.Ng = W.Ng; a.Cq_pad = W.Cq_pad; a.B = g->batch;
     a.k = g->kernel; a.s = g->stride; a.p = g->pad; a.ncols = W.ncols; a.M = W.M; a.split_len = W.split_len;

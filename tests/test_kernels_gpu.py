@@ -384,11 +384,15 @@ def test_cheng2020_blocks(cuda, kind, bf16):
     with _autocast(bf16):
         y = mod(xd)
     y.backward(g.to(cuda))
+    # fp32 mode: parity bar.  bf16 mode: closeness only -- weight gradients of the
+    # first conv pass through two bf16 dgrads and LeakyReLU masks taken from bf16
+    # activations (sign flips of near-zero values), so they get a wider bound.
     tol = 3e-2 if bf16 else 1e-4
     gtol = 5e-2 if bf16 else 2e-3
+    wtol = 0.15 if bf16 else 2e-3
     assert y.shape == yr.shape
     assert relerr(y, yr) < tol
     assert relerr(xd.grad, xr.grad) < gtol
     pr = dict(ref.named_parameters())
     for n, p in mod.named_parameters():
-        assert relerr(p.grad, pr[n].grad) < gtol, n
+        assert relerr(p.grad, pr[n].grad) < wtol, n
