@@ -1076,16 +1076,18 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 // 16-byte channel group and strides over rows (vector loads, fp32 sums), then
 // the rows reduce through LDS -> part[chunk][C].  stage 2: one block per 64
 // channels, 16 waves over the chunks, fixed-order tree: deterministic.
-constexpr int COLSUM_MAXC = 1024;
+constexpr int COLSUM_MAXC = 1 << 16;
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_stage1(const T* __restrict__ g, int64_t npix, int C, int ld,
                                                      int64_t chunk, float* __restrict__ part) {
     constexpr int VEC = OpT<T>::VEC;
     __shared__ float red[256 * VEC];
-    const int cpt = (C + VEC - 1) / VEC;      // channel groups per row
+    // blockIdx.y picks a slice of <= 256 channel groups (any C)
+    const int cg0 = blockIdx.y * 256;
+    const int cpt = min(256, (C + VEC - 1) / VEC - cg0);   // channel groups of this slice
     const int rows = 256 / cpt;               // rows in flight per pass
     const int tid = threadIdx.x;
-    const int r = tid / cpt, cg = tid - (tid / cpt) * cpt;
+    const int r = tid / cpt, cg = cg0 + tid - (tid / cpt) * cpt;
     const int64_t pb = blockIdx.x * chunk;
     int64_t pe = pb + chunk;
     if (pe > npix) pe = npix;
@@ -1109,8 +1111,10 @@ __global__ __launch_bounds__(256) void colsum_stage1(const T* __restrict__ g, in
 #pragma unroll
     for (int e = 0; e < VEC; ++e) red[tid * VEC + e] = (r < rows) ? s[e] : 0.f;
     __syncthreads();
-    for (int c = tid; c < C; c += 256) {
-        const int g0 = c / VEC, e = c - (c / VEC) * VEC;
+    for (int cl = tid; cl < cpt * VEC; cl += 256) {
+        const int c = cg0 * VEC + cl;
+        if (c >= C) break;
+        const int g0 = cl / VEC, e = cl - (cl / VEC) * VEC;
         float acc = 0.f;
         for (int rr = 0; rr < rows; ++rr) acc += red[(rr * cpt + g0) * VEC + e];
         part[(int64_t)c * gridDim.x + blockIdx.x] = acc;
@@ -1437,7 +1441,8 @@ static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype, bool glds) {
 template <typename T>
 static void launch_colsum(const void* g, int64_t npix, int C, int ld, int nchunk, int64_t chunk, float* part,
                           float* out, int accumulate, hipStream_t st) {
-    hipLaunchKernelGGL(colsum_stage1<T>, dim3(nchunk), dim3(256), 0, st, reinterpret_cast<const T*>(g), npix, C, ld,
+    const int nslice = ((C + OpT<T>::VEC - 1) / OpT<T>::VEC + 255) / 256;
+    hipLaunchKernelGGL(colsum_stage1<T>, dim3(nchunk, nslice), dim3(256), 0, st, reinterpret_cast<const T*>(g), npix, C, ld,
                        chunk, part);
     hipLaunchKernelGGL(colsum_stage2, dim3((C + 3) / 4), dim3(256), 0, st, part, nchunk, C, out, accumulate);
 }

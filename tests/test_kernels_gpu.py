@@ -57,6 +57,7 @@ CONV_CASES = [
     ("conv", 2, 64, 128, 16, 16, 1, 2),
     ("conv", 2, 64, 256, 8, 8, 3, 1),
     ("conv", 2, 64, 12, 8, 8, 3, 1),
+    ("conv", 1, 64, 1152, 4, 4, 3, 1),    # cheng2020 q6 h_s sub-pixel conv: > 1024 bias channels
 ]
 
 
