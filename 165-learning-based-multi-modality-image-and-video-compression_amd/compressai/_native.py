@@ -45,6 +45,9 @@ SIGNATURES = {
     "cai_abi_count": (c_int, []),
     "cai_conv_packed_weight_bytes": (_S, [_G, _I, _I]),
     "cai_conv_pack_weight": (_I, [_G, _I, _I, _P, _P, _P, _P]),
+    "cai_conv_pack_desc_bytes": (_S, []),
+    "cai_conv_pack_describe": (_I, [_G, _I, _I, _P, _P, _P, _P]),
+    "cai_conv_pack_many": (_I, [_P, c_int32, _I, _I64, _P]),
     "cai_pack_nchw": (_I, [_P, c_int32, c_int32, c_int32, c_int32, _I, _P, c_int32, _P]),
     "cai_conv_workspace_bytes": (_S, [_G, _I, _I]),
     "cai_conv_fwd": (_I, [_G, _I, _P, c_int32, c_int32, _P, _P, c_int32, _F, _P, _I, _I64, _I64, _I64, _I64,

@@ -202,6 +202,12 @@ def _conv_ws(g: ConvGeom, dtype, direction: int, device):
     return torch.empty(nbytes, dtype=torch.uint8, device=device), nbytes
 
 
+def _prepack_active():
+    from ._prepack import active
+
+    return active()
+
+
 def _small_deconv(spec: ConvSpec, g: ConvGeom, xld: int, dtype) -> bool:
     """Few-output-channel ConvTranspose2d (x_hat layer): csrc/deconv_small.hip."""
     return (spec.transposed and spec.out_nchw32 and g.out_c <= 16 and spec.act == ACT_NONE and not spec.in_abs
@@ -266,7 +272,11 @@ class ConvFn(torch.autograd.Function):
             lib.cai_deconv_small_fwd(ctypes.byref(g), dcode(dt), _p(xpm), xld, _p(weight.detach().float().contiguous()),
                                      _p(b), _p(y), _p(ws), wsb, _stream())
         else:
-            wp = _pack_weight(g, dt, 0, weight)
+            packer = _prepack_active()
+            wp = packer.lookup(weight, dt, 0) if packer is not None else None
+            ctx.wt_packed = packer.lookup(weight, dt, 1) if packer is not None else None
+            if wp is None:
+                wp = _pack_weight(g, dt, 0, weight)
             ws, wsb = _conv_ws(g, dt, 0, x.device)
             lib.cai_conv_fwd(ctypes.byref(g), dcode(dt), _p(xpm), xld, int(spec.in_abs), _p(wp), _p(b), spec.act,
                              spec.act_param, _p(y), ydt, *ys, _p(ws), wsb, _stream())
@@ -295,7 +305,7 @@ class ConvFn(torch.autograd.Function):
             gpm, gld = out, g.out_c
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            wt = _pack_weight(g, dt, 1, weight)
+            wt = ctx.wt_packed if getattr(ctx, "wt_packed", None) is not None else _pack_weight(g, dt, 1, weight)
             ldx = (g.in_c + vec - 1) // vec * vec
             dx = empty_pm(g.batch, g.in_c, g.in_h, g.in_w, dt, gy.device, ld=ldx)
             aux = xpm if spec.in_mask != MASK_NONE else None

@@ -45,6 +45,14 @@ class CompressionModel(nn.Module):
     def forward(self, *args):
         raise NotImplementedError()
 
+    def __call__(self, *args, **kwargs):
+        # all conv weights are packed to the MFMA layout in one launch per forward
+        # (compressai/_prepack.py); the reference has no counterpart (stock convs)
+        from .._prepack import prepacked_forward
+
+        with prepacked_forward(self):
+            return super().__call__(*args, **kwargs)
+
     def update(self, force=False):
         updated = False
         for m in self.children():

@@ -583,8 +583,7 @@ struct PackArgs {
 };
 
 template <typename T>
-__global__ void pack_weight_kernel(const PackArgs a) {
-    const int ph = blockIdx.z;
+__device__ __forceinline__ void pack_weight_body(const PackArgs& a, int ph) {
     const int64_t total = (int64_t)a.Npad * a.Kp;
     T* out = reinterpret_cast<T*>(a.out) + a.off[ph];
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -602,6 +601,19 @@ __global__ void pack_weight_kernel(const PackArgs a) {
         }
         out[i] = from_f32<T>(v);
     }
+}
+
+template <typename T>
+__global__ void pack_weight_kernel(const PackArgs a) {
+    pack_weight_body<T>(a, blockIdx.z);
+}
+
+// all the convs of a model in one launch: grid.y = descriptor, grid.z = phase
+template <typename T>
+__global__ void pack_many_kernel(const PackArgs* __restrict__ descs) {
+    const PackArgs a = descs[blockIdx.y];
+    if ((int)blockIdx.z >= a.nphase) return;
+    pack_weight_body<T>(a, blockIdx.z);
 }
 
 template <typename T>
@@ -1459,14 +1471,15 @@ size_t cai_conv_packed_weight_bytes(const cai_conv_geom* g, int dtype, int direc
     return (size_t)P.nphase * P.Npad * P.Kp * dtype_size(dtype);
 }
 
-int cai_conv_pack_weight(const cai_conv_geom* g, int dtype, int direction, const float* w, const float* mask,
-                         void* packed, void* stream) {
+static int fill_pack_args(const cai_conv_geom* g, int dtype, int direction, const float* w, const float* mask,
+                          void* packed, PackArgs& a) {
     int rc = check_geom(g);
     if (rc) return rc;
     CAI_CHECK_ARG(direction == 0 || direction == 1, "pack_weight: bad direction");
+    CAI_CHECK_ARG(dtype == CAI_BF16 || dtype == CAI_F32, "pack_weight: bad dtype");
     CAI_CHECK_ARG(w && packed, "pack_weight: null pointer");
     const Plan P = make_plan(g, dtype, direction);
-    PackArgs a{};
+    a = PackArgs{};
     a.w = w; a.mask = mask; a.out = packed;
     a.k = g->kernel;
     // torch layout: Conv2d [out][in][k][k], ConvTranspose2d [in][out][k][k]
@@ -1478,13 +1491,47 @@ int cai_conv_pack_weight(const cai_conv_geom* g, int dtype, int direction, const
         a.ntaps[ph] = P.ntaps[ph]; a.ntx[ph] = P.ntx[ph]; a.kh0[ph] = P.kh0[ph]; a.kw0[ph] = P.kw0[ph];
         a.off[ph] = (int64_t)ph * P.Npad * P.Kp;
     }
-    const int64_t total = (int64_t)P.Npad * P.Kp;
+    return CAI_OK;
+}
+
+int cai_conv_pack_weight(const cai_conv_geom* g, int dtype, int direction, const float* w, const float* mask,
+                         void* packed, void* stream) {
+    PackArgs a;
+    const int rc = fill_pack_args(g, dtype, direction, w, mask, packed, a);
+    if (rc) return rc;
+    const int64_t total = (int64_t)a.Npad * a.Kp;
     const int blocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
     if (dtype == CAI_BF16)
-        hipLaunchKernelGGL(pack_weight_kernel<bf16>, dim3(blocks, 1, P.nphase), dim3(256), 0, as_stream(stream), a);
+        hipLaunchKernelGGL(pack_weight_kernel<bf16>, dim3(blocks, 1, a.nphase), dim3(256), 0, as_stream(stream), a);
     else
-        hipLaunchKernelGGL(pack_weight_kernel<float>, dim3(blocks, 1, P.nphase), dim3(256), 0, as_stream(stream), a);
+        hipLaunchKernelGGL(pack_weight_kernel<float>, dim3(blocks, 1, a.nphase), dim3(256), 0, as_stream(stream), a);
     CAI_LAUNCH_CHECK("pack_weight");
+    return CAI_OK;
+}
+
+size_t cai_conv_pack_desc_bytes(void) { return sizeof(PackArgs); }
+
+int cai_conv_pack_describe(const cai_conv_geom* g, int dtype, int direction, const float* w, const float* mask,
+                           void* packed, void* desc) {
+    CAI_CHECK_ARG(desc, "pack_describe: null descriptor");
+    PackArgs a;
+    const int rc = fill_pack_args(g, dtype, direction, w, mask, packed, a);
+    if (rc) return rc;
+    memcpy(desc, &a, sizeof(a));
+    return CAI_OK;
+}
+
+int cai_conv_pack_many(const void* descs, int32_t n, int dtype, int64_t max_elems, void* stream) {
+    CAI_CHECK_ARG(descs && n > 0 && n <= 65535 && max_elems > 0, "pack_many: bad arguments");
+    CAI_CHECK_ARG(dtype == CAI_BF16 || dtype == CAI_F32, "pack_many: bad dtype");
+    CAI_CHECK_ARG(((uintptr_t)descs & 7) == 0, "pack_many: descriptor table not 8-byte aligned");
+    const int blocks = (int)std::min<int64_t>(512, (max_elems + 255) / 256);
+    const PackArgs* d = reinterpret_cast<const PackArgs*>(descs);
+    if (dtype == CAI_BF16)
+        hipLaunchKernelGGL(pack_many_kernel<bf16>, dim3(blocks, n, 4), dim3(256), 0, as_stream(stream), d);
+    else
+        hipLaunchKernelGGL(pack_many_kernel<float>, dim3(blocks, n, 4), dim3(256), 0, as_stream(stream), d);
+    CAI_LAUNCH_CHECK("pack_many");
     return CAI_OK;
 }
 

@@ -92,6 +92,16 @@ size_t cai_conv_packed_weight_bytes(const cai_conv_geom* g, int dtype, int direc
 int cai_conv_pack_weight(const cai_conv_geom* g, int dtype, int direction,
                          const float* w, const float* mask, void* packed, void* stream);
 
+/* Batched packing (one launch per step for all convs of a model): the host
+ * fills a cai_conv_pack_desc_bytes()-sized descriptor per (conv, direction)
+ * with cai_conv_pack_describe() (pointers captured, nothing launched), copies
+ * the table to device memory once, and each step calls cai_conv_pack_many()
+ * on it.  max_elems = the largest packed-buffer element count in the table. */
+size_t cai_conv_pack_desc_bytes(void);
+int cai_conv_pack_describe(const cai_conv_geom* g, int dtype, int direction, const float* w, const float* mask,
+                           void* packed, void* desc);
+int cai_conv_pack_many(const void* descs, int32_t n, int dtype, int64_t max_elems, void* stream);
+
 /* NCHW (fp32, contiguous) -> pixel-major [B*H*W][ld] of dtype with zero
  * padding of channels C..ld-1.  ld must be a multiple of 8. */
 int cai_pack_nchw(const float* x, int32_t B, int32_t C, int32_t H, int32_t W,
