@@ -47,6 +47,7 @@ SIGNATURES = {
     "cai_conv_pack_weight": (_I, [_G, _I, _I, _P, _P, _P, _P]),
     "cai_conv_pack_desc_bytes": (_S, []),
     "cai_conv_pack_describe": (_I, [_G, _I, _I, _P, _P, _P, _P]),
+    "cai_conv_pack_finalize": (_I64, [_P, c_int32]),
     "cai_conv_pack_many": (_I, [_P, c_int32, _I, _I64, _P]),
     "cai_pack_nchw": (_I, [_P, c_int32, c_int32, c_int32, c_int32, _I, _P, c_int32, _P]),
     "cai_conv_workspace_bytes": (_S, [_G, _I, _I]),

@@ -53,8 +53,7 @@ class Prepacker:
     def _build(self, dtype):
         dev = next(self.model.parameters()).device
         dsz = lib.cai_conv_pack_desc_bytes()
-        descs, table, buffers, max_elems = [], {}, [], 1
-        es = 2 if dtype == torch.bfloat16 else 4
+        descs, table, buffers = [], {}, []
         for m, mask in self._convs():
             spec = m._spec()
             g = conv_geom(spec, 1, m.in_channels, 16, 16, m.out_channels)   # packing ignores spatial size
@@ -70,12 +69,13 @@ class Prepacker:
                 descs.append(d.raw)
                 buffers.append(buf)
                 table[(w.data_ptr(), direction)] = buf
-                max_elems = max(max_elems, nbytes // es)
         if not descs:
             return None
-        blob = torch.frombuffer(bytearray(b"".join(descs)), dtype=torch.uint8).to(dev)
+        host = ctypes.create_string_buffer(b"".join(descs), len(descs) * dsz)
+        total = lib.cai_conv_pack_finalize(host, len(descs))
+        blob = torch.frombuffer(bytearray(host.raw), dtype=torch.uint8).to(dev)
         return {"sig": self._signature(), "table": table, "buffers": buffers, "descs": blob, "n": len(descs),
-                "max": max_elems}
+                "total": total}
 
     # -------------------------------------------------------------------- use
     def refresh(self):
@@ -87,7 +87,7 @@ class Prepacker:
             if plan is None:
                 return None
             self._plans[dtype] = plan
-        lib.cai_conv_pack_many(_p(plan["descs"]), plan["n"], dcode(dtype), plan["max"], _stream())
+        lib.cai_conv_pack_many(_p(plan["descs"]), plan["n"], dcode(dtype), plan["total"], _stream())
         return plan
 
     def lookup(self, weight: torch.Tensor, dtype, direction: int) -> Optional[torch.Tensor]:

@@ -580,6 +580,8 @@ struct PackArgs {
     int nphase;
     int ntaps[4], ntx[4], kh0[4], kw0[4], step;   // step = tap stride inside the kernel (s for phase, 1 for gather)
     int64_t off[4];
+    int64_t item_begin;    // pack_many: first global 8-element item of this descriptor
+    int items_pp;          // pack_many: 8-element items per phase (Npad * Kp / 8)
 };
 
 template <typename T>
@@ -608,12 +610,56 @@ __global__ void pack_weight_kernel(const PackArgs a) {
     pack_weight_body<T>(a, blockIdx.z);
 }
 
-// all the convs of a model in one launch: grid.y = descriptor, grid.z = phase
+// all the convs of a model in one launch: one flat space of 8-element items
+// over (descriptor, phase, row, k); a thread finds its descriptor by binary
+// search on item_begin, then writes 8 consecutive packed elements (16 B bf16)
 template <typename T>
-__global__ void pack_many_kernel(const PackArgs* __restrict__ descs) {
-    const PackArgs a = descs[blockIdx.y];
-    if ((int)blockIdx.z >= a.nphase) return;
-    pack_weight_body<T>(a, blockIdx.z);
+__global__ __launch_bounds__(256) void pack_many_kernel(const PackArgs* __restrict__ descs, int n, int64_t total) {
+    for (int64_t gi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; gi < total;
+         gi += (int64_t)gridDim.x * blockDim.x) {
+        int lo = 0, hi = n - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (descs[mid].item_begin <= gi) lo = mid; else hi = mid - 1;
+        }
+        const PackArgs& a = descs[lo];
+        const int local = (int)(gi - a.item_begin);
+        const int ph = local / a.items_pp;
+        const int e0 = (local - ph * a.items_pp) * 8;
+        const int nrow = e0 / a.Kp;
+        const int kk0 = e0 - nrow * a.Kp;
+        int t = kk0 / a.Cpad, c = kk0 - t * a.Cpad;
+        const int ntaps = ph == 0 ? a.ntaps[0] : (ph == 1 ? a.ntaps[1] : (ph == 2 ? a.ntaps[2] : a.ntaps[3]));
+        const int ntx = ph == 0 ? a.ntx[0] : (ph == 1 ? a.ntx[1] : (ph == 2 ? a.ntx[2] : a.ntx[3]));
+        const int kh0 = ph == 0 ? a.kh0[0] : (ph == 1 ? a.kh0[1] : (ph == 2 ? a.kh0[2] : a.kh0[3]));
+        const int kw0 = ph == 0 ? a.kw0[0] : (ph == 1 ? a.kw0[1] : (ph == 2 ? a.kw0[2] : a.kw0[3]));
+        const int64_t off = ph == 0 ? a.off[0] : (ph == 1 ? a.off[1] : (ph == 2 ? a.off[2] : a.off[3]));
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            float x = 0.f;
+            if (nrow < a.Nreal && c < a.Creal && t < ntaps) {
+                const int ty = t / ntx;
+                const int kh = kh0 + a.step * ty, kw = kw0 + a.step * (t - ty * ntx);
+                const int d0 = a.n_is_d0 ? nrow : c, d1 = a.n_is_d0 ? c : nrow;
+                const int64_t src = (((int64_t)d0 * a.D1 + d1) * a.k + kh) * a.k + kw;
+                x = a.w[src];
+                if (a.mask) x *= a.mask[src];
+            }
+            v[e] = x;
+            if (++c == a.Cpad) { c = 0; ++t; }
+        }
+        T* out = reinterpret_cast<T*>(a.out) + off + e0;
+        if constexpr (sizeof(T) == 2) {
+            bf16x8 h;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) h[e] = (bf16)v[e];
+            *reinterpret_cast<bf16x8*>(out) = h;
+        } else {
+            *reinterpret_cast<f32x4*>(out) = f32x4{v[0], v[1], v[2], v[3]};
+            *reinterpret_cast<f32x4*>(out + 4) = f32x4{v[4], v[5], v[6], v[7]};
+        }
+    }
 }
 
 template <typename T>
@@ -1521,16 +1567,28 @@ int cai_conv_pack_describe(const cai_conv_geom* g, int dtype, int direction, con
     return CAI_OK;
 }
 
-int cai_conv_pack_many(const void* descs, int32_t n, int dtype, int64_t max_elems, void* stream) {
-    CAI_CHECK_ARG(descs && n > 0 && n <= 65535 && max_elems > 0, "pack_many: bad arguments");
+int64_t cai_conv_pack_finalize(void* descs, int32_t n) {
+    if (!descs || n <= 0) return -1;
+    PackArgs* d = reinterpret_cast<PackArgs*>(descs);
+    int64_t begin = 0;
+    for (int i = 0; i < n; ++i) {
+        d[i].items_pp = (int)((int64_t)d[i].Npad * d[i].Kp / 8);
+        d[i].item_begin = begin;
+        begin += (int64_t)d[i].items_pp * d[i].nphase;
+    }
+    return begin;
+}
+
+int cai_conv_pack_many(const void* descs, int32_t n, int dtype, int64_t total_items, void* stream) {
+    CAI_CHECK_ARG(descs && n > 0 && total_items > 0, "pack_many: bad arguments");
     CAI_CHECK_ARG(dtype == CAI_BF16 || dtype == CAI_F32, "pack_many: bad dtype");
     CAI_CHECK_ARG(((uintptr_t)descs & 7) == 0, "pack_many: descriptor table not 8-byte aligned");
-    const int blocks = (int)std::min<int64_t>(512, (max_elems + 255) / 256);
+    const int blocks = (int)std::min<int64_t>(4096, (total_items + 255) / 256);
     const PackArgs* d = reinterpret_cast<const PackArgs*>(descs);
     if (dtype == CAI_BF16)
-        hipLaunchKernelGGL(pack_many_kernel<bf16>, dim3(blocks, n, 4), dim3(256), 0, as_stream(stream), d);
+        hipLaunchKernelGGL(pack_many_kernel<bf16>, dim3(blocks), dim3(256), 0, as_stream(stream), d, n, total_items);
     else
-        hipLaunchKernelGGL(pack_many_kernel<float>, dim3(blocks, n, 4), dim3(256), 0, as_stream(stream), d);
+        hipLaunchKernelGGL(pack_many_kernel<float>, dim3(blocks), dim3(256), 0, as_stream(stream), d, n, total_items);
     CAI_LAUNCH_CHECK("pack_many");
     return CAI_OK;
 }

@@ -96,11 +96,14 @@ int cai_conv_pack_weight(const cai_conv_geom* g, int dtype, int direction,
  * fills a cai_conv_pack_desc_bytes()-sized descriptor per (conv, direction)
  * with cai_conv_pack_describe() (pointers captured, nothing launched), copies
  * the table to device memory once, and each step calls cai_conv_pack_many()
- * on it.  max_elems = the largest packed-buffer element count in the table. */
+ * on it. */
 size_t cai_conv_pack_desc_bytes(void);
 int cai_conv_pack_describe(const cai_conv_geom* g, int dtype, int direction, const float* w, const float* mask,
                            void* packed, void* desc);
-int cai_conv_pack_many(const void* descs, int32_t n, int dtype, int64_t max_elems, void* stream);
+/* host side, once: number the 8-element work items of a contiguous table of n
+ * descriptors; returns the total item count (total_items of pack_many). */
+int64_t cai_conv_pack_finalize(void* descs, int32_t n);
+int cai_conv_pack_many(const void* descs, int32_t n, int dtype, int64_t total_items, void* stream);
 
 /* NCHW (fp32, contiguous) -> pixel-major [B*H*W][ld] of dtype with zero
  * padding of channels C..ld-1.  ld must be a multiple of 8. */
