@@ -27,6 +27,13 @@ class ConvGeom(Structure):
         "kernel", "stride", "pad", "output_padding", "transposed")]
 
 
+class WindowAttn(Structure):
+    _fields_ = [("q", c_void_p), ("q_ld", c_int32), ("kv", c_void_p), ("kv_ld", c_int32), ("bias_table", c_void_p),
+                ("rel_index", c_void_p), ("mask", c_void_p), ("B", c_int32), ("Hr", c_int32), ("Wr", c_int32),
+                ("heads", c_int32), ("head_dim", c_int32), ("window", c_int32), ("shift", c_int32),
+                ("scale", c_float)]
+
+
 class EbParams(Structure):
     _fields_ = [("matrix", c_void_p * 5), ("bias", c_void_p * 5), ("factor", c_void_p * 4), ("quantiles", c_void_p)]
 
@@ -65,6 +72,18 @@ SIGNATURES = {
     "cai_gate_bwd": (_I, [_I, _P, _P, _P, c_int32, _P, _P, c_int32, _I64, c_int32, _P]),
     "cai_pixel_shuffle": (_I, [_I, _P, POINTER(c_int64), _P, POINTER(c_int64), c_int32, c_int32, c_int32, c_int32,
                                c_int32, c_int32, _P]),
+    "cai_layernorm_fwd": (_I, [_I, _P, c_int32, _I64, c_int32, _P, _P, _F, _P, c_int32, _P, _P, _P]),
+    "cai_layernorm_bwd_workspace_bytes": (_S, [_I64, c_int32]),
+    "cai_layernorm_bwd": (_I, [_I, _P, c_int32, _P, c_int32, _I64, c_int32, _P, _P, _P, _P, c_int32, _P, _P, c_int32,
+                               _P, _S, _P]),
+    "cai_gelu_fwd": (_I, [_I, _P, c_int32, _P, c_int32, _I64, c_int32, _P]),
+    "cai_gelu_bwd": (_I, [_I, _P, c_int32, _P, c_int32, _P, c_int32, _I64, c_int32, _P]),
+    "cai_window_attn_fwd": (_I, [_I, POINTER(WindowAttn), _P, c_int32, _P]),
+    "cai_window_attn_bwd_workspace_bytes": (_S, [POINTER(WindowAttn)]),
+    "cai_window_attn_bwd": (_I, [_I, POINTER(WindowAttn), _P, c_int32, _P, c_int32, _P, c_int32, _P, c_int32, _P, _S,
+                                 _P]),
+    "cai_channel_mean": (_I, [_I, _P, c_int32, _P, c_int32, c_int32, _I64, c_int32, _P, _F, _P]),
+    "cai_channel_affine": (_I, [_I, _P, c_int32, _P, _P, _F, _P, c_int32, c_int32, _I64, c_int32, _P]),
     "cai_gdn_reparam": (_I, [_P, _P, c_int32, _F, _F, _I, _P, _P, _P]),
     "cai_gdn_fwd": (_I, [_I, _P, c_int32, _I64, c_int32, _P, _P, c_int32, _P, c_int32, _P]),
     "cai_gdn_bwd": (_I, [_I, _P, c_int32, _P, c_int32, _I64, c_int32, _P, _P, c_int32, _P, c_int32, _P, _P]),

@@ -724,3 +724,212 @@ class PixelShuffleFn(torch.autograd.Function):
         lib.cai_pixel_shuffle(dcode(dt), _p(g), _bhwc_strides(g), _p(dx), _bhwc_strides(dx), B, H, W, Cr // (r * r),
                               r, 1, _stream())
         return dx, None
+
+
+# ---------------------------------------------------------------------------
+# multi-modal codec alignment modules (models/master.py) -- csrc/swin.hip.
+# Token sequences (B, L, C) are held as pixel-major [B, C, Hr, Wr] tensors:
+# row b*L + l, exactly the reference's flattened token order.
+# ---------------------------------------------------------------------------
+
+class CatFn(torch.autograd.Function):
+    """torch.cat(tensors, dim=1) into one pixel-major buffer (HIP copies); grads are channel views."""
+
+    @staticmethod
+    def forward(ctx, *ts):
+        _check_cuda(*ts)
+        dt = compute_dtype()
+        vec = _vec(dt)
+        B, _, H, W = ts[0].shape
+        cs = [t.shape[1] for t in ts]
+        if any(c % vec for c in cs[:-1]):
+            raise ValueError("cat: leading channel counts must be multiples of the vector width")
+        total = sum(cs)
+        ld = (total + vec - 1) // vec * vec
+        out = empty_pm(B, total, H, W, dt, ts[0].device, ld=ld)
+        off = 0
+        for t, c in zip(ts, cs):
+            tp, tld = to_pm(t, dt, vec)
+            dst = _VP(out.data_ptr() + off * out.element_size())
+            lib.cai_act(dcode(dt), _p(tp), tld, dst, ld, B * H * W, c, ACT_NONE, 0.0, _stream())
+            off += c
+        ctx.cs = cs
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        outs, off = [], 0
+        for c in ctx.cs:
+            outs.append(g[:, off:off + c])
+            off += c
+        return tuple(outs)
+
+
+class LayerNormFn(torch.autograd.Function):
+    """nn.LayerNorm(C) over the channel dim of pixel-major tokens."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps: float):
+        _check_cuda(x, weight, bias)
+        dt = compute_dtype()
+        B, C, H, W = x.shape
+        xp, xld = to_pm(x, dt, _vec(dt))
+        y, yld = _out_pm_like(x, dt)
+        n = B * H * W
+        mean = torch.empty(n, dtype=torch.float32, device=x.device)
+        rstd = torch.empty(n, dtype=torch.float32, device=x.device)
+        w = weight.detach().float().contiguous()
+        lib.cai_layernorm_fwd(dcode(dt), _p(xp), xld, n, C, _p(w), _p(bias.detach().float().contiguous()), eps,
+                              _p(y), yld, _p(mean), _p(rstd), _stream())
+        ctx.save_for_backward(xp, w, mean, rstd)
+        ctx.cfg = (dt, xld)
+        ctx.params = (weight, bias)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        xp, w, mean, rstd = ctx.saved_tensors
+        dt, xld = ctx.cfg
+        B, C, H, W = xp.shape
+        n = B * H * W
+        gp, gld = to_pm(g, dt, _vec(dt))
+        dx, dxld = _out_pm_like(xp, dt)
+        wparam, bparam = ctx.params
+        direct = direct_grad(wparam) and direct_grad(bparam)
+        dw = wparam.grad if direct else torch.empty(C, dtype=torch.float32, device=g.device)
+        db = bparam.grad if direct else torch.empty(C, dtype=torch.float32, device=g.device)
+        nb = lib.cai_layernorm_bwd_workspace_bytes(n, C)
+        ws = torch.empty(nb, dtype=torch.uint8, device=g.device)
+        lib.cai_layernorm_bwd(dcode(dt), _p(xp), xld, _p(gp), gld, n, C, _p(w), _p(mean), _p(rstd), _p(dx), dxld,
+                              _p(dw), _p(db), int(direct), _p(ws), nb, _stream())
+        if direct:
+            return dx, None, None, None
+        return dx, dw, db, None
+
+
+class GeluFn(torch.autograd.Function):
+    """nn.GELU() (exact erf form)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        _check_cuda(x)
+        dt = compute_dtype()
+        B, C, H, W = x.shape
+        xp, xld = to_pm(x, dt, _vec(dt))
+        y, yld = _out_pm_like(x, dt)
+        lib.cai_gelu_fwd(dcode(dt), _p(xp), xld, _p(y), yld, B * H * W, C, _stream())
+        ctx.save_for_backward(xp)
+        ctx.cfg = (dt, xld)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (xp,) = ctx.saved_tensors
+        dt, xld = ctx.cfg
+        B, C, H, W = xp.shape
+        gp, gld = to_pm(g, dt, _vec(dt))
+        dx, dxld = _out_pm_like(xp, dt)
+        lib.cai_gelu_bwd(dcode(dt), _p(xp), xld, _p(gp), gld, _p(dx), dxld, B * H * W, C, _stream())
+        return dx
+
+
+class WindowAttnFn(torch.autograd.Function):
+    """WindowAttention core (master.py:534-566, before proj) with the block's shift / partition folded in."""
+
+    @staticmethod
+    def forward(ctx, q, kv, table, rel_index, mask, cfg):
+        _check_cuda(q, kv, table)
+        dt = compute_dtype()
+        (Hr, Wr, heads, window, shift, scale) = cfg
+        B, C, H, W = q.shape
+        if H * W != Hr * Wr:
+            raise ValueError(f"window attention: {H * W} tokens for a {Hr}x{Wr} resolution")
+        qp, qld = to_pm(q, dt, _vec(dt))
+        kp, kld = to_pm(kv, dt, _vec(dt))
+        tb = table.detach().float().contiguous()
+        P = _attn_desc(qp, qld, kp, kld, tb, rel_index, mask, B, Hr, Wr, heads, window, shift, scale)
+        out, old = _out_pm_like(q, dt)
+        lib.cai_window_attn_fwd(dcode(dt), ctypes.byref(P), _p(out), old, _stream())
+        ctx.save_for_backward(qp, kp, tb)
+        ctx.cfg = (dt, qld, kld, rel_index, mask, B, Hr, Wr, heads, window, shift, scale)
+        ctx.tparam = table
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        qp, kp, tb = ctx.saved_tensors
+        dt, qld, kld, rel_index, mask, B, Hr, Wr, heads, window, shift, scale = ctx.cfg
+        P = _attn_desc(qp, qld, kp, kld, tb, rel_index, mask, B, Hr, Wr, heads, window, shift, scale)
+        gp, gld = to_pm(g, dt, _vec(dt))
+        dq, dqld = _out_pm_like(qp, dt)
+        dkv, dkvld = _out_pm_like(kp, dt)
+        direct = direct_grad(ctx.tparam)
+        dtab = ctx.tparam.grad if direct else torch.empty(tb.shape, dtype=torch.float32, device=g.device)
+        nb = lib.cai_window_attn_bwd_workspace_bytes(ctypes.byref(P))
+        ws = torch.empty(nb, dtype=torch.uint8, device=g.device)
+        lib.cai_window_attn_bwd(dcode(dt), ctypes.byref(P), _p(gp), gld, _p(dq), dqld, _p(dkv), dkvld, _p(dtab),
+                                int(direct), _p(ws), nb, _stream())
+        return dq, dkv, (None if direct else dtab), None, None, None
+
+
+def _attn_desc(qp, qld, kp, kld, tb, rel_index, mask, B, Hr, Wr, heads, window, shift, scale):
+    from ._native import WindowAttn
+
+    return WindowAttn(_VP(qp.data_ptr()), qld, _VP(kp.data_ptr()), kld, _VP(tb.data_ptr()),
+                      _VP(rel_index.data_ptr()), _VP(mask.data_ptr()) if mask is not None else None, B, Hr, Wr,
+                      heads, qp.shape[1] // heads, window, shift, scale)
+
+
+class ChannelMeanFn(torch.autograd.Function):
+    """nn.AdaptiveAvgPool2d(1) of a pixel-major map -> [B, C, 1, 1] fp32."""
+
+    @staticmethod
+    def forward(ctx, x):
+        _check_cuda(x)
+        dt = compute_dtype()
+        B, C, H, W = x.shape
+        xp, xld = to_pm(x, dt, _vec(dt))
+        out = torch.empty((B, C, 1, 1), dtype=torch.float32, device=x.device)
+        lib.cai_channel_mean(dcode(dt), _p(xp), xld, None, 0, B, H * W, C, _p(out), 1.0 / (H * W), _stream())
+        ctx.cfg = (dt, tuple(x.shape))
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        dt, (B, C, H, W) = ctx.cfg
+        gb = g.float().contiguous()
+        dx = empty_pm(B, C, H, W, dt, g.device, ld=(C + _vec(dt) - 1) // _vec(dt) * _vec(dt))
+        lib.cai_channel_affine(dcode(dt), None, 0, None, _p(gb), 1.0 / (H * W), _p(dx), pixel_major_ld(dx), B, H * W,
+                               C, _stream())
+        return dx
+
+
+class ChannelAffineFn(torch.autograd.Function):
+    """gamma * x + beta with per-(image, channel) gamma / beta [B, C, 1, 1] (Channel_aligner output)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta):
+        _check_cuda(x, gamma, beta)
+        dt = compute_dtype()
+        B, C, H, W = x.shape
+        xp, xld = to_pm(x, dt, _vec(dt))
+        ga, be = gamma.float().contiguous(), beta.float().contiguous()
+        y, yld = _out_pm_like(x, dt)
+        lib.cai_channel_affine(dcode(dt), _p(xp), xld, _p(ga), _p(be), 1.0, _p(y), yld, B, H * W, C, _stream())
+        ctx.save_for_backward(xp, ga)
+        ctx.cfg = (dt, xld)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        xp, ga = ctx.saved_tensors
+        dt, xld = ctx.cfg
+        B, C, H, W = xp.shape
+        gp, gld = to_pm(g, dt, _vec(dt))
+        dx, dxld = _out_pm_like(xp, dt)
+        lib.cai_channel_affine(dcode(dt), _p(gp), gld, _p(ga), None, 0.0, _p(dx), dxld, B, H * W, C, _stream())
+        dgamma = torch.empty((B, C, 1, 1), dtype=torch.float32, device=g.device)
+        dbeta = torch.empty((B, C, 1, 1), dtype=torch.float32, device=g.device)
+        lib.cai_channel_mean(dcode(dt), _p(gp), gld, _p(xp), xld, B, H * W, C, _p(dgamma), 1.0, _stream())
+        lib.cai_channel_mean(dcode(dt), _p(gp), gld, None, 0, B, H * W, C, _p(dbeta), 1.0, _stream())
+        return dx, dgamma, dbeta

@@ -185,6 +185,55 @@ int cai_pixel_shuffle(int dtype, const void* src, const int64_t* src_strides, vo
                       int32_t B, int32_t H, int32_t W, int32_t C, int32_t r, int32_t inverse, void* stream);
 
 /* =======================================================================
+ * Multi-modal codec alignment modules (models/master.py): LayerNorm, GELU,
+ * shifted-window cross attention, Channel_aligner pooling + affine.
+ * Tokens are pixel-major rows (row = b*L + l, l = r*Wr + c).
+ * ======================================================================= */
+/* nn.LayerNorm over C (SwinTransformerBlock.norm1/norm2, master.py:603-606).
+ * mean / rstd (fp32, one per token) are saved for the backward. */
+int cai_layernorm_fwd(int dtype, const void* x, int32_t x_ld, int64_t ntok, int32_t C, const float* w, const float* b,
+                      float eps, void* y, int32_t y_ld, float* mean, float* rstd, void* stream);
+size_t cai_layernorm_bwd_workspace_bytes(int64_t ntok, int32_t C);
+int cai_layernorm_bwd(int dtype, const void* x, int32_t x_ld, const void* dy, int32_t dy_ld, int64_t ntok, int32_t C,
+                      const float* w, const float* mean, const float* rstd, void* dx, int32_t dx_ld, float* dw,
+                      float* db, int32_t accumulate, void* workspace, size_t ws_bytes, void* stream);
+/* exact (erf) GELU of Mlp.act (master.py:465-482). */
+int cai_gelu_fwd(int dtype, const void* x, int32_t x_ld, void* y, int32_t y_ld, int64_t ntok, int32_t C, void* stream);
+int cai_gelu_bwd(int dtype, const void* x, int32_t x_ld, const void* g, int32_t g_ld, void* dx, int32_t dx_ld,
+                 int64_t ntok, int32_t C, void* stream);
+
+/* WindowAttention.forward (master.py:534-568) with SwinTransformerBlock's
+ * cyclic shift and window partition / reverse (master.py:665-695) folded into
+ * the token addressing: q = qkv1(x) rows, kv = qkv2(guided) rows (k = columns
+ * [0, C), v = [C, 2C), C = heads*head_dim); output rows in token order (before
+ * the proj Linear).  window 4, head_dim 32 are built. */
+typedef struct cai_window_attn {
+    const void* q;
+    int32_t q_ld;
+    const void* kv;
+    int32_t kv_ld;
+    const float* bias_table;   /* relative_position_bias_table [(2w-1)^2][heads] */
+    const int32_t* rel_index;  /* relative_position_index [w*w][w*w] */
+    const float* mask;         /* attn_mask [nW][w*w][w*w] or NULL */
+    int32_t B, Hr, Wr;         /* token grid (input_resolution) */
+    int32_t heads, head_dim, window, shift;
+    float scale;
+} cai_window_attn;
+int cai_window_attn_fwd(int dtype, const cai_window_attn* p, void* out, int32_t out_ld, void* stream);
+size_t cai_window_attn_bwd_workspace_bytes(const cai_window_attn* p);
+int cai_window_attn_bwd(int dtype, const cai_window_attn* p, const void* dout, int32_t dout_ld, void* dq,
+                        int32_t dq_ld, void* dkv, int32_t dkv_ld, float* dbias_table, int32_t accumulate,
+                        void* workspace, size_t ws_bytes, void* stream);
+
+/* Channel_aligner (master.py:179-210): out[b][c] = scale * sum_p x[b,p,c] (* x2[b,p,c])
+ * (AdaptiveAvgPool2d(1) with scale = 1/HW; with x2, the gamma gradient);
+ * y = gamma[b][c] * x + beta_scale * beta[b][c] (gamma / beta nullable). */
+int cai_channel_mean(int dtype, const void* x, int32_t x_ld, const void* x2, int32_t x2_ld, int32_t B, int64_t HW,
+                     int32_t C, float* out, float scale, void* stream);
+int cai_channel_affine(int dtype, const void* x, int32_t x_ld, const float* gamma, const float* beta, float beta_scale,
+                       void* y, int32_t y_ld, int32_t B, int64_t HW, int32_t C, void* stream);
+
+/* =======================================================================
  * GDN / IGDN (layers/gdn.py:41-92), C in {32,64,96,128,192}.
  * ======================================================================= */
 /* beta = max(beta_raw, sqrt(beta_min + ped))^2 - ped ; gamma likewise with

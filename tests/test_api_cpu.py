@@ -92,3 +92,27 @@ def test_cheng2020_attn_q6_parameter_count():
 
     n = sum(p.numel() for p in image_models["cheng2020-attn"](6).parameters())
     assert abs(n - 29.63e6) < 0.01e6
+
+
+@pytest.mark.parametrize("channel", [1, 3])
+def test_master_guided_state_dict_parity(channel):
+    """models/master.py: Master_compresser / Guided_compresser module trees and keys."""
+    import cai_oracle_master as OM
+    from compressai.models import Guided_compresser, Master_compresser
+
+    torch.manual_seed(0)
+    for ref, net in ((OM.Master_compresser(width=64, height=64, channel=channel),
+                      Master_compresser(width=64, height=64, channel=channel)),
+                     (OM.Guided_compresser(channel=channel), Guided_compresser(channel=channel))):
+        a = {k: tuple(v.shape) for k, v in ref.state_dict().items()}
+        b = {k: tuple(v.shape) for k, v in net.state_dict().items()}
+        assert a == b
+        net.load_state_dict(ref.state_dict())
+
+
+def test_master_paper_config_parameter_count():
+    """Master (IR master, 512x640) 26.8 M parameters incl. the unused g_s of its base class."""
+    from compressai.models import Master_compresser
+
+    n = sum(p.numel() for p in Master_compresser(width=512, height=640, channel=1).parameters())
+    assert 26e6 < n < 29e6
