@@ -1,0 +1,20 @@
+#!/bin/bash
+# GPU-box routine: stall / LDS / L2 counters of the bench's roofline kernel,
+# one rocprofv3 --pmc pass per counter group (no tracing domains with --pmc).
+# usage (via gpurun): bash tools/pmc_diag.sh <tag> [bench args...]
+tag=$1; shift
+out=$GRAFT_REPO_ROOT/gpurun_out
+mkdir -p $out
+cd /tmp && export TMPDIR=/tmp
+timeout -s KILL 60 rocprofv3 -L > $out/pmc_list_$tag.txt 2>&1
+i=0
+for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVES" \
+           "SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE" \
+           "TCC_HIT_sum TCC_MISS_sum GRBM_COUNT"; do
+  i=$((i+1))
+  timeout -s KILL 90 rocprofv3 --pmc $grp -d $out/pmcd_${tag}_$i -o run --output-format csv -- \
+      python3 $GRAFT_REPO_ROOT/bench.py --roofline-only --steps 20 "$@" > $out/pmcd_${tag}_$i.log 2>&1
+  rc=$?
+  echo "group $i rc=$rc" >> $out/pmcd_${tag}.status
+  if [ $rc -ge 124 ]; then exit $rc; fi   # killed / timed out: start nothing more
+done
