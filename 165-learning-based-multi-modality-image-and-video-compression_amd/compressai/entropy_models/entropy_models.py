@@ -9,8 +9,13 @@ and backward of the likelihood path are single fused kernels
 training-mode noise is U(-1/2, 1/2) drawn with torch's generator exactly like
 the reference (``empty_like(x).uniform_(-0.5, 0.5)``), consumed by the kernel.
 
-The bitstream side (update / compress / decompress, C++ in the reference)
-is not on the hot path and is not provided in this round.
+The bitstream side follows the reference too:
+update() evaluates the pmfs with the reference's torch expressions on the
+module's device and quantizes them to CDF tables in libcai_coder.so
+(cai_pmf_to_quantized_cdf_rows); compress() takes its integer symbols from
+the quantize kernel (SYMBOLS mode) and codes one rANS stream per image on
+host threads (cai_rans_encode_batch), byte-identical to compressai.ans;
+decompress() decodes them (cai_rans_decode_batch) and dequantizes.
 """
 from __future__ import annotations
 
@@ -21,6 +26,9 @@ import numpy as np
 import torch
 import torch.nn as nn
 
+import scipy.stats
+
+from .. import _coder
 from .._native import F32, Q_DEQUANTIZE, Q_NOISE, Q_SYMBOLS, lib
 from .._ops import BottleneckAuxFn, BottleneckFn, GaussianFn, _check_cuda, _p, _stream, as_rows, dcode, empty_rows_like
 from ..ops import LowerBound
@@ -141,6 +149,81 @@ class EntropyModel(nn.Module):
             return out
         return inputs.type(dtype)
 
+    # ---- bitstream side (entropy_models.py:206-327) --------------------------
+
+    def _pmf_to_cdf(self, pmf, tail_mass, pmf_length, max_length):
+        """entropy_models.py:206-214: row i = quantized CDF of [pmf[i, :pmf_length[i]], tail_mass[i]]
+        in a zero-filled [rows, max_length + 2] int32 table (libcai_coder.so, rows on host threads)."""
+        lengths = pmf_length.detach().reshape(-1).to("cpu", torch.int64).numpy()
+        rows = lengths.size
+        p = pmf.detach().float().reshape(rows, -1).cpu().numpy()
+        tail = tail_mass.detach().float().reshape(rows, -1)[:, 0].cpu().numpy()
+        table = np.zeros((rows, max_length + 1), dtype=np.float32)
+        keep = np.arange(p.shape[1])[None, :] < lengths[:, None]
+        table[:, :p.shape[1]] = np.where(keep, p, 0.0)
+        table[np.arange(rows), lengths] = tail
+        cdf = _coder.pmf_to_quantized_cdf_rows(table, lengths + 1, self.entropy_coder_precision, max_length + 2)
+        return torch.from_numpy(cdf).to(pmf.device)
+
+    def _check_cdf_size(self):
+        if self._quantized_cdf.numel() == 0:
+            raise ValueError("Uninitialized CDFs. Run update() first")
+        if len(self._quantized_cdf.size()) != 2:
+            raise ValueError(f"Invalid CDF size {self._quantized_cdf.size()}")
+
+    def _check_offsets_size(self):
+        if self._offset.numel() == 0:
+            raise ValueError("Uninitialized offsets. Run update() first")
+        if len(self._offset.size()) != 1:
+            raise ValueError(f"Invalid offsets size {self._offset.size()}")
+
+    def _check_cdf_length(self):
+        if self._cdf_length.numel() == 0:
+            raise ValueError("Uninitialized CDF lengths. Run update() first")
+        if len(self._cdf_length.size()) != 1:
+            raise ValueError(f"Invalid offsets size {self._cdf_length.size()}")
+
+    def _tables(self) -> "_coder.Tables":
+        return _coder.Tables(self._quantized_cdf.cpu().numpy(), self._cdf_length.reshape(-1).cpu().numpy(),
+                             self._offset.reshape(-1).cpu().numpy())
+
+    def compress(self, inputs, indexes, means=None):
+        """entropy_models.py:237-270: one rANS string per batch element."""
+        if len(inputs.size()) < 2:
+            raise ValueError("Invalid `inputs` size. Expected a tensor with at least 2 dimensions.")
+        if inputs.size() != indexes.size():
+            raise ValueError("`inputs` and `indexes` should have the same size.")
+        self._check_cdf_size()
+        self._check_cdf_length()
+        self._check_offsets_size()
+        symbols = self.quantize(inputs, "symbols", means)
+        B = symbols.size(0)
+        sym = symbols.reshape(B, -1).cpu().numpy()
+        idx = indexes.reshape(B, -1).int().cpu().numpy()
+        return _coder.encode_streams(sym, idx, self._tables(), B)
+
+    def decompress(self, strings, indexes, dtype: torch.dtype = torch.float, means: torch.Tensor = None):
+        """entropy_models.py:272-327."""
+        if not isinstance(strings, (tuple, list)):
+            raise ValueError("Invalid `strings` parameter type.")
+        if not len(strings) == indexes.size(0):
+            raise ValueError("Invalid strings or indexes parameters")
+        if len(indexes.size()) < 2:
+            raise ValueError("Invalid `indexes` size. Expected a tensor with at least 2 dimensions.")
+        self._check_cdf_size()
+        self._check_cdf_length()
+        self._check_offsets_size()
+        if means is not None:
+            if means.size()[:2] != indexes.size()[:2]:
+                raise ValueError("Invalid means or indexes parameters")
+            if means.size() != indexes.size():
+                for i in range(2, len(indexes.size())):
+                    if means.size(i) != 1:
+                        raise ValueError("Invalid means parameters")
+        vals = _coder.decode_streams(strings, indexes.reshape(len(strings), -1).int().cpu().numpy(), self._tables())
+        outputs = torch.from_numpy(vals).to(self._quantized_cdf.device).reshape(indexes.size())
+        return self.dequantize(outputs, means, dtype)
+
 
 class EntropyBottleneck(EntropyModel):
     _offset: torch.Tensor
@@ -196,8 +279,67 @@ class EntropyBottleneck(EntropyModel):
         view_dims[1] = -1
         return torch.arange(size[1]).view(*view_dims).int().repeat(size[0], 1, *size[2:])
 
+    @staticmethod
+    def _extend_ndims(tensor, n):
+        return tensor.reshape(-1, *([1] * n)) if n > 0 else tensor.reshape(-1)
+
+    def _logits_cumulative(self, inputs: torch.Tensor, stop_gradient: bool) -> torch.Tensor:
+        """entropy_models.py:457-477 in torch ops, for update() only (the training / eval
+        forward runs the fused cai_eb_* kernels)."""
+        logits = inputs
+        for i in range(len(self.filters) + 1):
+            matrix = getattr(self, f"_matrix{i:d}")
+            bias = getattr(self, f"_bias{i:d}")
+            if stop_gradient:
+                matrix, bias = matrix.detach(), bias.detach()
+            logits = torch.matmul(torch.nn.functional.softplus(matrix), logits) + bias
+            if i < len(self.filters):
+                factor = getattr(self, f"_factor{i:d}")
+                if stop_gradient:
+                    factor = factor.detach()
+                logits = logits + torch.tanh(factor) * torch.tanh(logits)
+        return logits
+
+    @torch.no_grad()
     def update(self, force: bool = False) -> bool:
-        raise NotImplementedError("CDF tables / rANS coding are not part of this round (SURVEY.md 8f-2/3)")
+        """entropy_models.py:396-441."""
+        if self._offset.numel() > 0 and not force:
+            return False
+        medians = self.quantiles[:, 0, 1]
+        minima = torch.clamp(torch.ceil(medians - self.quantiles[:, 0, 0]).int(), min=0)
+        maxima = torch.clamp(torch.ceil(self.quantiles[:, 0, 2] - medians).int(), min=0)
+        self._offset = -minima
+        pmf_start = medians - minima
+        pmf_length = maxima + minima + 1
+        max_length = int(pmf_length.max().item())
+        samples = torch.arange(max_length, device=pmf_start.device)
+        samples = samples[None, :] + pmf_start[:, None, None]
+        half = float(0.5)
+        lower = self._logits_cumulative(samples - half, stop_gradient=True)
+        upper = self._logits_cumulative(samples + half, stop_gradient=True)
+        sign = -torch.sign(lower + upper)
+        pmf = torch.abs(torch.sigmoid(sign * upper) - torch.sigmoid(sign * lower))[:, 0, :]
+        tail_mass = torch.sigmoid(lower[:, 0, :1]) + torch.sigmoid(-upper[:, 0, -1:])
+        self._quantized_cdf = self._pmf_to_cdf(pmf, tail_mass, pmf_length, max_length)
+        self._cdf_length = pmf_length + 2
+        return True
+
+    def compress(self, x):
+        """entropy_models.py:559-567."""
+        indexes = self._build_indexes(x.size()).to(x.device)
+        medians = self._get_medians().detach()
+        spatial_dims = len(x.size()) - 2
+        medians = self._extend_ndims(medians, spatial_dims)
+        medians = medians.expand(x.size(0), *([-1] * (spatial_dims + 1)))
+        return super().compress(x, indexes, medians)
+
+    def decompress(self, strings, size):
+        """entropy_models.py:569-574."""
+        output_size = (len(strings), self._quantized_cdf.size(0), *size)
+        indexes = self._build_indexes(output_size).to(self._quantized_cdf.device)
+        medians = self._extend_ndims(self._get_medians().detach(), len(size))
+        medians = medians.expand(len(strings), *([-1] * (len(size) + 1)))
+        return super().decompress(strings, indexes, medians.dtype, medians)
 
 
 class GaussianConditional(EntropyModel):
@@ -243,5 +385,40 @@ class GaussianConditional(EntropyModel):
             indexes -= (scales <= s).int()
         return indexes
 
+    @staticmethod
+    def _standardized_cumulative(inputs: torch.Tensor) -> torch.Tensor:
+        """entropy_models.py:629-635 (update() only; the likelihood kernels use the same erfc form)."""
+        half = float(0.5)
+        const = float(-(2 ** -0.5))
+        return half * torch.erfc(const * inputs)
+
+    @staticmethod
+    def _standardized_quantile(quantile):
+        return scipy.stats.norm.ppf(quantile)
+
     def update_scale_table(self, scale_table, force=False):
-        raise NotImplementedError("CDF tables / rANS coding are not part of this round (SURVEY.md 8f-2/3)")
+        """entropy_models.py:643-652."""
+        if self._offset.numel() > 0 and not force:
+            return False
+        device = self.scale_table.device
+        self.scale_table = self._prepare_scale_table(scale_table).to(device)
+        self.update()
+        return True
+
+    @torch.no_grad()
+    def update(self):
+        """entropy_models.py:655-678 (without the reference's debug prints, :680-689)."""
+        multiplier = -self._standardized_quantile(self.tail_mass / 2)
+        pmf_center = torch.ceil(self.scale_table * multiplier).int()
+        pmf_length = 2 * pmf_center + 1
+        max_length = int(torch.max(pmf_length).item())
+        device = pmf_center.device
+        samples = torch.abs(torch.arange(max_length, device=device).int() - pmf_center[:, None]).float()
+        samples_scale = self.scale_table.unsqueeze(1).float()
+        upper = self._standardized_cumulative((0.5 - samples) / samples_scale)
+        lower = self._standardized_cumulative((-0.5 - samples) / samples_scale)
+        pmf = upper - lower
+        tail_mass = 2 * lower[:, :1]
+        self._quantized_cdf = self._pmf_to_cdf(pmf, tail_mass, pmf_length, max_length)
+        self._offset = -pmf_center
+        self._cdf_length = pmf_length + 2

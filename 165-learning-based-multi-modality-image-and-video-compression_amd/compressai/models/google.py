@@ -8,15 +8,26 @@ MI355X-motivated differences that leave the arithmetic unchanged:
     operand load (and its backward sign mask inside that conv's dgrad);
   * conv -> ReLU/LeakyReLU pairs run fused (layers.Sequential);
 and without the reference's debug prints (google.py:287-288).
+
+compress / decompress (google.py:195-204, 325-344, 393-416, 526-692) follow
+the reference: transforms on the HIP kernels (fp32 outside autocast, so the
+encoder and decoder reproduce each other's scales exactly), symbols from the
+quantize kernel, rANS strings from libcai_coder.so.  The autoregressive
+models' serial per-latent-pixel loop runs the masked 5x5 context conv and
+the 1x1 entropy-parameter stack on the same kernels, one pixel at a time.
 """
 import math
 import warnings
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from ..entropy_models import EntropyBottleneck, GaussianConditional
 from ..layers import GDN, MaskedConv2d, Sequential
+from .._ops import CatFn, ConvFn, ConvSpec
+from .._prepack import prepacked_forward
+from ..ans import BufferedRansEncoder, RansDecoder
 from ..layers.conv import Conv2d
 from .utils import conv, deconv, update_registered_buffers
 
@@ -99,6 +110,23 @@ class FactorizedPrior(CompressionModel):
         net.load_state_dict(state_dict)
         return net
 
+    @torch.no_grad()
+    def compress(self, x):
+        """google.py:195-198."""
+        with prepacked_forward(self):
+            y = self.g_a(x)
+            y_strings = self.entropy_bottleneck.compress(y)
+        return {"strings": [y_strings], "shape": y.size()[-2:]}
+
+    @torch.no_grad()
+    def decompress(self, strings, shape):
+        """google.py:200-204."""
+        assert isinstance(strings, list) and len(strings) == 1
+        with prepacked_forward(self):
+            y_hat = self.entropy_bottleneck.decompress(strings[0], shape)
+            x_hat = self.g_s(y_hat).clamp_(0, 1)
+        return {"x_hat": x_hat}
+
 
 class ScaleHyperprior(CompressionModel):
     def __init__(self, N, M, channel=3, **kwargs):
@@ -144,6 +172,31 @@ class ScaleHyperprior(CompressionModel):
         updated |= super().update(force=force)
         return updated
 
+    @torch.no_grad()
+    def compress(self, x):
+        """google.py:325-335."""
+        with prepacked_forward(self):
+            y = self.g_a(x)
+            z = self.h_a(y, input_abs=True)
+            z_strings = self.entropy_bottleneck.compress(z)
+            z_hat = self.entropy_bottleneck.decompress(z_strings, z.size()[-2:])
+            scales_hat = self.h_s(z_hat)
+            indexes = self.gaussian_conditional.build_indexes(scales_hat)
+            y_strings = self.gaussian_conditional.compress(y, indexes)
+        return {"strings": [y_strings, z_strings], "shape": z.size()[-2:]}
+
+    @torch.no_grad()
+    def decompress(self, strings, shape):
+        """google.py:337-344."""
+        assert isinstance(strings, list) and len(strings) == 2
+        with prepacked_forward(self):
+            z_hat = self.entropy_bottleneck.decompress(strings[1], shape)
+            scales_hat = self.h_s(z_hat)
+            indexes = self.gaussian_conditional.build_indexes(scales_hat)
+            y_hat = self.gaussian_conditional.decompress(strings[0], indexes, z_hat.dtype)
+            x_hat = self.g_s(y_hat).clamp_(0, 1)
+        return {"x_hat": x_hat}
+
 
 class MeanScaleHyperprior(ScaleHyperprior):
     def __init__(self, N, M, channel=3, **kwargs):
@@ -161,6 +214,31 @@ class MeanScaleHyperprior(ScaleHyperprior):
         y_hat, y_likelihoods = self.gaussian_conditional(y, scales_hat, means=means_hat)
         x_hat = self.g_s(y_hat)
         return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods, "z": z_likelihoods}}
+
+    @torch.no_grad()
+    def compress(self, x):
+        """google.py:393-404."""
+        with prepacked_forward(self):
+            y = self.g_a(x)
+            z = self.h_a(y)
+            z_strings = self.entropy_bottleneck.compress(z)
+            z_hat = self.entropy_bottleneck.decompress(z_strings, z.size()[-2:])
+            scales_hat, means_hat = self.h_s(z_hat).chunk(2, 1)
+            indexes = self.gaussian_conditional.build_indexes(scales_hat)
+            y_strings = self.gaussian_conditional.compress(y, indexes, means=means_hat)
+        return {"strings": [y_strings, z_strings], "shape": z.size()[-2:]}
+
+    @torch.no_grad()
+    def decompress(self, strings, shape):
+        """google.py:406-416."""
+        assert isinstance(strings, list) and len(strings) == 2
+        with prepacked_forward(self):
+            z_hat = self.entropy_bottleneck.decompress(strings[1], shape)
+            scales_hat, means_hat = self.h_s(z_hat).chunk(2, 1)
+            indexes = self.gaussian_conditional.build_indexes(scales_hat)
+            y_hat = self.gaussian_conditional.decompress(strings[0], indexes, means=means_hat)
+            x_hat = self.g_s(y_hat).clamp_(0, 1)
+        return {"x_hat": x_hat}
 
 
 class JointAutoregressiveHierarchicalPriors(MeanScaleHyperprior):
@@ -184,3 +262,100 @@ class JointAutoregressiveHierarchicalPriors(MeanScaleHyperprior):
         _, y_likelihoods = self.gaussian_conditional(y, scales_hat, means=means_hat)
         x_hat = self.g_s(y_hat)
         return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods, "z": z_likelihoods}}
+
+    # ---- serial autoregressive coding (google.py:526-692) -------------------
+
+    _AR_SPEC = None
+
+    def _ar_params(self, y_crop, p):
+        """Entropy parameters of the centre pixel of a 5x5 crop: masked context conv
+        (valid, no padding) + the 1x1 stack (google.py:580-592 / 671-681)."""
+        if JointAutoregressiveHierarchicalPriors._AR_SPEC is None:
+            JointAutoregressiveHierarchicalPriors._AR_SPEC = ConvSpec(5, 1, 0)
+        cp = self.context_prediction
+        ctx_p = ConvFn.apply(y_crop, cp.weight, cp.bias, JointAutoregressiveHierarchicalPriors._AR_SPEC)
+        return self.entropy_parameters(CatFn.apply(p, ctx_p)).chunk(2, 1)
+
+    def _gc_tables(self):
+        gc = self.gaussian_conditional
+        return gc._quantized_cdf.tolist(), gc._cdf_length.tolist(), gc._offset.tolist()
+
+    @torch.no_grad()
+    def compress(self, x):
+        if next(self.parameters()).device != torch.device("cpu"):
+            warnings.warn("Inference on GPU is not recommended for the autoregressive models (the entropy coder is "
+                          "run sequentially on CPU).")
+        cp = self.context_prediction
+        cp.weight.data *= cp.mask          # MaskedConv2d semantics (layers.py:75-78)
+        with prepacked_forward(self):
+            y = self.g_a(x)
+            z = self.h_a(y)
+            z_strings = self.entropy_bottleneck.compress(z)
+            z_hat = self.entropy_bottleneck.decompress(z_strings, z.size()[-2:])
+            params = self.h_s(z_hat)
+            s, kernel_size = 4, 5
+            padding = (kernel_size - 1) // 2
+            y_height, y_width = z_hat.size(2) * s, z_hat.size(3) * s
+            y_hat = F.pad(y.float(), (padding, padding, padding, padding))
+            y_strings = [self._compress_ar(y_hat[i:i + 1], params[i:i + 1], y_height, y_width, kernel_size, padding)
+                         for i in range(y.size(0))]
+        return {"strings": [y_strings, z_strings], "shape": z.size()[-2:]}
+
+    def _compress_ar(self, y_hat, params, height, width, kernel_size, padding):
+        """google.py:565-608."""
+        cdf, cdf_lengths, offsets = self._gc_tables()
+        encoder = BufferedRansEncoder()
+        symbols_list, indexes_list = [], []
+        gc = self.gaussian_conditional
+        for h in range(height):
+            for w in range(width):
+                y_crop = y_hat[:, :, h:h + kernel_size, w:w + kernel_size]
+                p = params[:, :, h:h + 1, w:w + 1]
+                scales_hat, means_hat = self._ar_params(y_crop, p)
+                indexes = gc.build_indexes(scales_hat)
+                y_c = y_crop[:, :, padding:padding + 1, padding:padding + 1]
+                y_q = gc.quantize(y_c, "symbols", means_hat)
+                y_hat[:, :, h + padding:h + padding + 1, w + padding:w + padding + 1] = y_q.float() + means_hat.float()
+                symbols_list.extend(y_q.reshape(-1).tolist())
+                indexes_list.extend(indexes.reshape(-1).tolist())
+        encoder.encode_with_indexes(symbols_list, indexes_list, cdf, cdf_lengths, offsets)
+        return encoder.flush()
+
+    @torch.no_grad()
+    def decompress(self, strings, shape):
+        assert isinstance(strings, list) and len(strings) == 2
+        if next(self.parameters()).device != torch.device("cpu"):
+            warnings.warn("Inference on GPU is not recommended for the autoregressive models (the entropy coder is "
+                          "run sequentially on CPU).")
+        cp = self.context_prediction
+        cp.weight.data *= cp.mask
+        with prepacked_forward(self):
+            z_hat = self.entropy_bottleneck.decompress(strings[1], shape)
+            params = self.h_s(z_hat)
+            s, kernel_size = 4, 5
+            padding = (kernel_size - 1) // 2
+            y_height, y_width = z_hat.size(2) * s, z_hat.size(3) * s
+            y_hat = torch.zeros((z_hat.size(0), self.M, y_height + 2 * padding, y_width + 2 * padding),
+                                device=z_hat.device)
+            for i, y_string in enumerate(strings[0]):
+                self._decompress_ar(y_string, y_hat[i:i + 1], params[i:i + 1], y_height, y_width, kernel_size, padding)
+            y_hat = F.pad(y_hat, (-padding, -padding, -padding, -padding))
+            x_hat = self.g_s(y_hat).clamp_(0, 1)
+        return {"x_hat": x_hat}
+
+    def _decompress_ar(self, y_string, y_hat, params, height, width, kernel_size, padding):
+        """google.py:654-692."""
+        cdf, cdf_lengths, offsets = self._gc_tables()
+        decoder = RansDecoder()
+        decoder.set_stream(y_string)
+        gc = self.gaussian_conditional
+        for h in range(height):
+            for w in range(width):
+                y_crop = y_hat[:, :, h:h + kernel_size, w:w + kernel_size]
+                p = params[:, :, h:h + 1, w:w + 1]
+                scales_hat, means_hat = self._ar_params(y_crop, p)
+                indexes = gc.build_indexes(scales_hat)
+                rv = decoder.decode_stream(indexes.reshape(-1).tolist(), cdf, cdf_lengths, offsets)
+                rv = torch.tensor(rv, dtype=torch.float32, device=y_hat.device).reshape(1, -1, 1, 1)
+                rv = gc.dequantize(rv, means_hat.float())
+                y_hat[:, :, h + padding:h + padding + 1, w + padding:w + padding + 1] = rv

@@ -1,4 +1,6 @@
 """Model zoo (reference: compressai/zoo/__init__.py:30-56)."""
+from .pretrained import load_pretrained
+from .pretrained import load_pretrained as load_state_dict
 from .image import (bmshj2018_factorized, bmshj2018_hyperprior, cfgs, cheng2020_anchor, cheng2020_attn, mbt2018,
                     mbt2018_mean, model_architectures)
 
@@ -13,4 +15,4 @@ image_models = {
 
 models = dict(image_models)
 
-__all__ = ["image_models", "models", "cfgs", "model_architectures"]
+__all__ = ["image_models", "models", "cfgs", "model_architectures", "load_state_dict", "load_pretrained"]

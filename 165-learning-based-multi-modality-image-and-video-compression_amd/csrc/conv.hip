@@ -1221,6 +1221,7 @@ static int check_geom(const cai_conv_geom* g) {
     }
     CAI_CHECK_ARG(oh == g->out_h && ow == g->out_w, "conv: output size %dx%d != expected %dx%d", g->out_h, g->out_w, oh,
                   ow);
+    CAI_CHECK_ARG(oh > 0 && ow > 0, "conv: empty output (%dx%d): input smaller than the kernel", oh, ow);
     return CAI_OK;
 }
 

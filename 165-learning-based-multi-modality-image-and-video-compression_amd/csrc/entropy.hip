@@ -143,21 +143,55 @@ __device__ __forceinline__ float softplus_grad(float v) {   // torch softplus ba
 }
 __device__ __forceinline__ float sigmoid_f(float v) { return 1.f / (1.f + expf(-v)); }
 
-__device__ void eb_load_table(int c, const cai_eb_params& P, float* t) {
-    int o = 0;
-    // matrices (softplus)
-    for (int k = 0; k < 3; ++k) t[EB_SP + o++] = softplus_f(P.matrix[0][c * 3 + k]);
-    for (int l = 1; l < 4; ++l)
-        for (int k = 0; k < 9; ++k) t[EB_SP + o++] = softplus_f(P.matrix[l][c * 9 + k]);
-    for (int k = 0; k < 3; ++k) t[EB_SP + o++] = softplus_f(P.matrix[4][c * 3 + k]);
-    o = 0;
-    for (int l = 0; l < 4; ++l)
-        for (int k = 0; k < 3; ++k) t[EB_B + o++] = P.bias[l][c * 3 + k];
-    t[EB_B + 12] = P.bias[4][c];
-    o = 0;
-    for (int l = 0; l < 4; ++l)
-        for (int k = 0; k < 3; ++k) t[EB_TF + o++] = tanhf(P.factor[l][c * 3 + k]);
-    t[EB_MED] = P.quantiles[c * 3 + 1];
+// Address of the raw parameter behind element k of channel c's table (layout
+// above; k < EB_NP, always a valid address -- the pad slot reads the median).
+__device__ __forceinline__ const float* eb_raw_ptr(int c, int k, const cai_eb_params& P) {
+    if (k < 3) return P.matrix[0] + c * 3 + k;
+    if (k < 30) {
+        const int l = (k - 3) / 9, j = (k - 3) - 9 * ((k - 3) / 9);
+        return (l == 0 ? P.matrix[1] : (l == 1 ? P.matrix[2] : P.matrix[3])) + c * 9 + j;
+    }
+    if (k < 33) return P.matrix[4] + c * 3 + (k - 30);
+    if (k < 45) {
+        const int l = (k - 33) / 3, j = (k - 33) - 3 * ((k - 33) / 3);
+        return (l == 0 ? P.bias[0] : (l == 1 ? P.bias[1] : (l == 2 ? P.bias[2] : P.bias[3]))) + c * 3 + j;
+    }
+    if (k == 45) return P.bias[4] + c;
+    if (k < 58) {
+        const int l = (k - 46) / 3, j = (k - 46) - 3 * ((k - 46) / 3);
+        return (l == 0 ? P.factor[0] : (l == 1 ? P.factor[1] : (l == 2 ? P.factor[2] : P.factor[3]))) + c * 3 + j;
+    }
+    return P.quantiles + c * 3 + 1;
+}
+__device__ __forceinline__ float eb_xform(int k, float v) {
+    if (k < EB_B) return softplus_f(v);
+    if (k >= EB_TF && k < EB_MED) return tanhf(v);
+    return k <= EB_MED ? v : 0.f;
+}
+
+// Tables of channels [c0, c0 + nch) into tab[nch][EB_NP] (LDS); caller syncs.
+// Filled cooperatively in two passes: every thread first issues all of its
+// PT loads (unconditional, from clamped valid addresses, so they are in
+// flight together), then transforms them -- one global-load latency per
+// block instead of one per parameter.  PT >= nch * EB_NP / blockDim.x.
+template <int PT>
+__device__ __forceinline__ void eb_fill_tables(int c0, int nch, int C, const cai_eb_params& P, float* tab) {
+    const int n = nch * EB_NP;
+    float raw[PT];
+#pragma unroll
+    for (int r = 0; r < PT; ++r) {
+        const int i = min((int)(threadIdx.x + r * blockDim.x), n - 1);
+        const int cl = i / EB_NP, k = i - cl * EB_NP;
+        raw[r] = *eb_raw_ptr(min(c0 + cl, C - 1), k, P);
+    }
+#pragma unroll
+    for (int r = 0; r < PT; ++r) {
+        const int i = threadIdx.x + r * blockDim.x;
+        if (i < n) {
+            const int cl = i / EB_NP, k = i - cl * EB_NP;
+            tab[i] = (c0 + cl < C) ? eb_xform(k, raw[r]) : 0.f;
+        }
+    }
 }
 
 // forward of one chain; records pre-activations a[l][j] and outputs h[l][j]
@@ -249,8 +283,7 @@ __global__ __launch_bounds__(256) void eb_fwd_kernel(int mode, int64_t npix, int
     __shared__ float tab[32][EB_NP];
     const int cl = threadIdx.x & 31, pr = threadIdx.x >> 5;
     const int c0 = blockIdx.x * 32;
-    for (int i = threadIdx.x; i < 32; i += blockDim.x)
-        if (c0 + i < C) eb_load_table(c0 + i, P, tab[i]);
+    eb_fill_tables<(32 * EB_NP + 255) / 256>(c0, 32, C, P, &tab[0][0]);
     __syncthreads();
     const int c = c0 + cl;
     if (c >= C) return;
@@ -272,28 +305,26 @@ __global__ __launch_bounds__(256) void eb_fwd_kernel(int mode, int64_t npix, int
     }
 }
 
-// bwd: block = 256 threads = 8 channels x 32 pixel lanes; the 32 threads of a
-// channel sit in one half-wave so the per-channel parameter sums reduce with
-// shuffles in a fixed order (deterministic, no atomics).
+// bwd: one channel per block; its pixels spread over the 256 threads (one
+// chain pair per thread and pass), then the 60 per-channel parameter sums
+// reduce in a fixed order -- lanes by xor-shuffles, the 4 waves through LDS
+// (deterministic, no atomics).
 __global__ __launch_bounds__(256) void eb_bwd_kernel(int mode, int64_t npix, int C, cai_eb_params P,
                                                        const void* __restrict__ x, int xdt, int xld,
                                                        const float* __restrict__ noise, int nld, float lbound,
                                                        const float* __restrict__ glik, int glld,
                                                        const void* __restrict__ gq, int gqdt, int gqld,
                                                        void* __restrict__ dx, int dxld, cai_eb_grads G) {
-    __shared__ float tab[8][EB_NP];
-    const int pl = threadIdx.x & 31, cl = threadIdx.x >> 5;
-    const int c0 = blockIdx.x * 8;
-    for (int i = threadIdx.x; i < 8; i += blockDim.x)
-        if (c0 + i < C) eb_load_table(c0 + i, P, tab[i]);
+    __shared__ float tab[EB_NP];
+    __shared__ float red[4][EB_NP];
+    const int c = blockIdx.x;
+    eb_fill_tables<1>(c, 1, C, P, tab);
     __syncthreads();
-    const int c = c0 + cl;
-    if (c >= C) return;   // whole half-waves exit together
-    const float* t = tab[cl];
+    const float* t = tab;
     float g[EB_NP];
 #pragma unroll
     for (int k = 0; k < EB_NP; ++k) g[k] = 0.f;
-    for (int64_t p = pl; p < npix; p += 32) {
+    for (int64_t p = threadIdx.x; p < npix; p += 256) {
         const float xv = ld_any(x, xdt, p * xld + c);
         const float v = (mode == CAI_Q_NOISE) ? xv + noise[p * nld + c] : rintf(xv - t[EB_MED]) + t[EB_MED];
         EbTrace tl, tu;
@@ -317,15 +348,17 @@ __global__ __launch_bounds__(256) void eb_bwd_kernel(int mode, int64_t npix, int
             g[EB_MED] += gqv + dv;
         }
     }
-    // reduce each accumulator over the 32 lanes of this channel
+    // reduce each accumulator: 64 lanes by shuffles, then the 4 waves in order
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
     for (int k = 0; k < EB_NP; ++k) {
-        float v = g[k];
-#pragma unroll
-        for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        g[k] = v;
+        const float v = wave_sum(g[k]);
+        if (lane == 0) red[w][k] = v;
     }
-    if (pl != 0) return;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+#pragma unroll
+    for (int k = 0; k < EB_NP; ++k) g[k] = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
 #define EB_PUT(dst, val) ((dst) = G.accumulate ? (dst) + (val) : (val))
     // softplus / tanh chain rule and scatter to torch layout (all indices
     // compile-time after unrolling so g[] stays in registers)
@@ -357,30 +390,39 @@ __global__ __launch_bounds__(256) void eb_bwd_kernel(int mode, int64_t npix, int
     }
 }
 
-// aux loss: one block, deterministic
+// aux loss: one block, deterministic.  Channels in chunks of 320: the chunk's
+// tables are filled cooperatively into LDS, then one thread per (channel, k).
+constexpr int EB_AUX_CH = 320;   // every zoo EntropyBottleneck (C <= 320) in one pass
 __global__ __launch_bounds__(1024) void eb_aux_kernel(int C, cai_eb_params P, const float* __restrict__ target,
                                                        float* __restrict__ loss, const float* __restrict__ gloss,
                                                        float* __restrict__ dq, int accumulate) {
     __shared__ float red[16];
+    __shared__ float tab[EB_AUX_CH * EB_NP];
     float acc = 0.f;
     const float gs = gloss ? *gloss : 0.f;
-    for (int i = threadIdx.x; i < 3 * C; i += blockDim.x) {
-        const int c = i / 3, k = i - 3 * (i / 3);
-        float t[EB_NP];
-        eb_load_table(c, P, t);
-        const float qv = P.quantiles[c * 3 + k];
-        EbTrace tr;
-        const float f = eb_chain(qv, t, &tr);
-        const float diff = f - target[k];
-        acc += fabsf(diff);
-        if (dq) {
-            float gd[EB_NP];
+    for (int c0 = 0; c0 < C; c0 += EB_AUX_CH) {
+        const int nch = min(EB_AUX_CH, C - c0);
+        eb_fill_tables<(EB_AUX_CH * EB_NP + 1023) / 1024>(c0, nch, C, P, tab);
+        __syncthreads();
+        const int i = threadIdx.x;
+        if (i < 3 * nch) {
+            const int cl = i / 3, k = i - 3 * (i / 3), c = c0 + cl;
+            const float* t = tab + cl * EB_NP;
+            const float qv = P.quantiles[c * 3 + k];
+            EbTrace tr;
+            const float f = eb_chain(qv, t, &tr);
+            const float diff = f - target[k];
+            acc += fabsf(diff);
+            if (dq) {
+                float gd[EB_NP];
 #pragma unroll
-            for (int j = 0; j < EB_NP; ++j) gd[j] = 0.f;
-            const float s = (diff > 0.f) ? 1.f : ((diff < 0.f) ? -1.f : 0.f);
-            const float v = eb_chain_bwd(qv, gs * s, t, tr, gd);
-            dq[c * 3 + k] = accumulate ? dq[c * 3 + k] + v : v;
+                for (int j = 0; j < EB_NP; ++j) gd[j] = 0.f;
+                const float sg = (diff > 0.f) ? 1.f : ((diff < 0.f) ? -1.f : 0.f);
+                const float v = eb_chain_bwd(qv, gs * sg, t, tr, gd);
+                dq[c * 3 + k] = accumulate ? dq[c * 3 + k] + v : v;
+            }
         }
+        __syncthreads();
     }
     const float r = block_sum<1024>(acc, red);
     if (threadIdx.x == 0 && loss) *loss = r;
@@ -535,7 +577,7 @@ int cai_eb_fwd(int mode, int64_t npix, int32_t C, const cai_eb_params* prm, cons
     CAI_CHECK_ARG(mode == CAI_Q_NOISE || mode == CAI_Q_DEQUANTIZE, "eb_fwd: invalid mode %d", mode);
     CAI_CHECK_ARG(mode != CAI_Q_NOISE || noise, "eb_fwd: noise mode needs a noise buffer");
     if (npix * C == 0) return CAI_OK;
-    int64_t gy = (npix + 8 * 8 - 1) / (8 * 8);
+    int64_t gy = (npix + 7) / 8;   // one pixel row per thread and pass
     if (gy > 1024) gy = 1024;
     hipLaunchKernelGGL(eb_fwd_kernel, dim3((C + 31) / 32, (unsigned)gy), dim3(256), 0, as_stream(stream), mode, npix, C,
                        *prm, x, x_dtype, x_ld, noise, noise_ld, lik_bound, q, q_dtype, q_ld, lik, lik_ld);
@@ -551,7 +593,7 @@ int cai_eb_bwd(int mode, int64_t npix, int32_t C, const cai_eb_params* prm, cons
     CAI_CHECK_ARG(mode == CAI_Q_NOISE || mode == CAI_Q_DEQUANTIZE, "eb_bwd: invalid mode %d", mode);
     for (int i = 0; i < 5; ++i) CAI_CHECK_ARG(grads->matrix[i] && grads->bias[i], "eb_bwd: null grad");
     for (int i = 0; i < 4; ++i) CAI_CHECK_ARG(grads->factor[i], "eb_bwd: null grad");
-    hipLaunchKernelGGL(eb_bwd_kernel, dim3((C + 7) / 8), dim3(256), 0, as_stream(stream), mode, npix, C, *prm, x,
+    hipLaunchKernelGGL(eb_bwd_kernel, dim3(C), dim3(256), 0, as_stream(stream), mode, npix, C, *prm, x,
                        x_dtype, x_ld, noise, noise_ld, lik_bound, g_lik, gl_ld, g_q, gq_dtype, gq_ld, dx, dx_ld,
                        *grads);
     CAI_LAUNCH_CHECK("eb_bwd");

@@ -85,3 +85,13 @@ def test_product_path_has_no_cpu_fallback():
     m = Conv2d(8, 8, 3, padding=1)
     with pytest.raises((RuntimeError, ValueError)):
         m(torch.zeros(1, 8, 8, 8))
+
+
+def test_empty_conv_output_is_einval(native):
+    """A kernel larger than its (padded) input is rejected before any launch sizing."""
+    lib = native.lib.load()
+    g = native.ConvGeom(1, 16, 3, 3, 16, -1, -1, 5, 1, 0, 0, 0)
+    assert lib.cai_conv_workspace_bytes(ctypes.byref(g), native.BF16, 0) == 0
+    with pytest.raises(ValueError, match="empty output"):
+        native.lib.cai_conv_fwd(ctypes.byref(g), native.BF16, None, 16, 0, None, None, 0, 0.0, None, native.BF16,
+                                0, 0, 0, 0, None, 0, None)

@@ -172,3 +172,53 @@ def test_invalid_arguments_raise(coder):
         ans.RansDecoder().decode_with_indexes(s[:5], [0] * 100, cdfs, [3], [0])   # not a whole word
     with pytest.raises(ValueError):
         ans.RansDecoder().decode_with_indexes(s[:8], [0] * 100, cdfs, [3], [0])   # truncated
+
+
+def test_update_tables_cpu_exact(coder):
+    """EntropyBottleneck / GaussianConditional.update() (entropy_models.py:396-441, 655-678) on CPU
+    parameters: the pmfs are the reference's torch expressions, so the tables equal the oracle's
+    pure-Python quantization of the same pmfs exactly."""
+    import torch
+
+    import cai_oracle as OR
+    from compressai.entropy_models import EntropyBottleneck, GaussianConditional
+    from compressai.models import get_scale_table
+
+    torch.manual_seed(2)
+    ref = OR.EntropyBottleneck(16)
+    with torch.no_grad():
+        ref.quantiles.add_(torch.randn(16, 1, 3))
+    eb = EntropyBottleneck(16)
+    eb.load_state_dict(ref.state_dict(), strict=False)
+    assert eb.update() and not eb.update() and eb.update(force=True)
+    with torch.no_grad():
+        q = ref.quantiles
+        med = q[:, 0, 1]
+        mn = torch.clamp(torch.ceil(med - q[:, 0, 0]).int(), min=0)
+        mx = torch.clamp(torch.ceil(q[:, 0, 2] - med).int(), min=0)
+        length = mn + mx + 1
+        samples = torch.arange(int(length.max()))[None, :] + (med - mn)[:, None, None]
+        lo = ref._logits_cumulative(samples - 0.5, stop_gradient=True)
+        up = ref._logits_cumulative(samples + 0.5, stop_gradient=True)
+        sg = -torch.sign(lo + up)
+        pmf = torch.abs(torch.sigmoid(sg * up) - torch.sigmoid(sg * lo))[:, 0, :]
+        tail = torch.sigmoid(lo[:, 0, :1]) + torch.sigmoid(-up[:, 0, -1:])
+    assert torch.equal(eb._offset, -mn) and torch.equal(eb._cdf_length, length + 2)
+    for i, n in enumerate(length.tolist()):
+        c = O.pmf_to_quantized_cdf(pmf[i, :n].tolist() + [float(tail[i, 0])], 16)
+        assert eb._quantized_cdf[i, :len(c)].tolist() == c
+        assert not eb._quantized_cdf[i, len(c):].any()
+
+    gc = GaussianConditional(None)
+    assert gc.update_scale_table(get_scale_table())
+    st = get_scale_table().float()
+    center = torch.ceil(st * float(-__import__("scipy.stats").stats.norm.ppf(1e-9 / 2))).int()
+    assert torch.equal(gc._offset, -center)
+    samples = torch.abs(torch.arange(int((2 * center + 1).max())).int() - center[:, None]).float()
+    upper = 0.5 * torch.erfc(float(-(2 ** -0.5)) * ((0.5 - samples) / st[:, None]))
+    lower = 0.5 * torch.erfc(float(-(2 ** -0.5)) * ((-0.5 - samples) / st[:, None]))
+    pmf = upper - lower
+    for i in (0, 9, 33, 63):
+        n = int(2 * center[i] + 1)
+        c = O.pmf_to_quantized_cdf(pmf[i, :n].tolist() + [float(2 * lower[i, 0])], 16)
+        assert gc._quantized_cdf[i, :len(c)].tolist() == c

@@ -1,0 +1,164 @@
+"""Bitstream path on the GPU models: update() CDF tables, compress / decompress round trips.
+
+Reference behaviour pinned here:
+  * EntropyBottleneck compress -> decompress == round(x) for 2-D .. 5-D inputs
+    (tests/test_entropy_models.py:258-283);
+  * update() tables within 2 of an independent computation (the reference's own
+    tolerance, tests/test_entropy_models.py:382-398) -- here the oracle's CPU
+    restatement of update() (entropy_models.py:396-441, 655-678) quantized by the
+    pure-Python pmf_to_quantized_cdf;
+  * decompress(compress(x)) reproduces the eval-mode forward's reconstruction
+    (the decoder sees exactly the encoder's y_hat), and the real rate stays near
+    the estimated one (eval_model/__main__t.py:137-138 vs :195-200).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import cai_coder_oracle as OC
+import cai_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_eb_tables(eb_ref):
+    """CPU restatement of EntropyBottleneck.update (entropy_models.py:396-441)."""
+    with torch.no_grad():
+        q = eb_ref.quantiles
+        medians = q[:, 0, 1]
+        minima = torch.clamp(torch.ceil(medians - q[:, 0, 0]).int(), min=0)
+        maxima = torch.clamp(torch.ceil(q[:, 0, 2] - medians).int(), min=0)
+        pmf_start = medians - minima
+        pmf_length = maxima + minima + 1
+        L = int(pmf_length.max())
+        samples = torch.arange(L)[None, :] + pmf_start[:, None, None]
+        lower = eb_ref._logits_cumulative(samples - 0.5, stop_gradient=True)
+        upper = eb_ref._logits_cumulative(samples + 0.5, stop_gradient=True)
+        sign = -torch.sign(lower + upper)
+        pmf = torch.abs(torch.sigmoid(sign * upper) - torch.sigmoid(sign * lower))[:, 0, :]
+        tail = torch.sigmoid(lower[:, 0, :1]) + torch.sigmoid(-upper[:, 0, -1:])
+    cdf = np.zeros((len(pmf_length), L + 2), dtype=np.int64)
+    for i, n in enumerate(pmf_length.tolist()):
+        c = OC.pmf_to_quantized_cdf(pmf[i, :n].tolist() + [float(tail[i, 0])], 16)
+        cdf[i, :len(c)] = c
+    return cdf, (-minima).numpy(), (pmf_length + 2).numpy()
+
+
+@pytest.mark.parametrize("dims", [0, 1, 2, 3])
+def test_eb_compression_nd(cuda, dims):
+    from compressai.entropy_models import EntropyBottleneck
+
+    torch.manual_seed(0)
+    eb = EntropyBottleneck(128).to(cuda)
+    eb.update()
+    x = torch.rand(2, 128, *([4] * dims), generator=torch.Generator().manual_seed(dims)).to(cuda) * 6 - 3
+    s = eb.compress(x)
+    assert len(s) == 2 and all(isinstance(b, bytes) for b in s)
+    x2 = eb.decompress(s, x.size()[2:])
+    assert torch.equal(torch.round(x), x2)
+
+
+def test_eb_tables_match_oracle(cuda):
+    from compressai.entropy_models import EntropyBottleneck
+
+    torch.manual_seed(1)
+    ref = O.EntropyBottleneck(64)
+    with torch.no_grad():
+        ref.quantiles.copy_(torch.tensor([-4.3, 0.2, 5.1]).repeat(64, 1, 1) + torch.randn(64, 1, 3) * 0.5)
+    eb = EntropyBottleneck(64)
+    eb.load_state_dict(ref.state_dict(), strict=False)
+    eb = eb.to(cuda)
+    assert eb.update(force=True)
+    assert not eb.update()
+    cdf, off, length = _oracle_eb_tables(ref)
+    assert np.array_equal(eb._offset.cpu().numpy(), off)
+    assert np.array_equal(eb._cdf_length.cpu().numpy(), length)
+    assert np.abs(eb._quantized_cdf.cpu().numpy().astype(np.int64) - cdf).max() <= 2
+
+
+def test_gc_tables_match_oracle(cuda):
+    from compressai.entropy_models import GaussianConditional
+    from compressai.models import get_scale_table
+
+    gc = GaussianConditional(None).to(cuda)
+    table = get_scale_table()
+    assert gc.update_scale_table(table)
+    assert not gc.update_scale_table(table)
+    # entropy_models.py:655-678 on the CPU, quantized by the oracle
+    mult = 6.109410204869  # -norm.ppf(1e-9 / 2)
+    st = table.float()
+    center = torch.ceil(st * mult).int()
+    assert torch.equal(gc._offset.cpu(), -center)
+    length = 2 * center + 1
+    assert torch.equal(gc._cdf_length.cpu(), length + 2)
+    L = int(length.max())
+    samples = torch.abs(torch.arange(L).int() - center[:, None]).float()
+    upper = 0.5 * torch.erfc(-(2 ** -0.5) * (0.5 - samples) / st[:, None])
+    lower = 0.5 * torch.erfc(-(2 ** -0.5) * (-0.5 - samples) / st[:, None])
+    pmf = upper - lower
+    tab = gc._quantized_cdf.cpu().numpy()
+    for i in (0, 1, 17, 40, 63):
+        n = int(length[i])
+        c = OC.pmf_to_quantized_cdf(pmf[i, :n].tolist() + [float(2 * lower[i, 0])], 16)
+        assert np.abs(tab[i, :len(c)].astype(np.int64) - np.array(c)).max() <= 2
+
+
+def _bits(strings):
+    return sum(len(b) for s in strings for b in (s if isinstance(s, list) else [s])) * 8
+
+
+@pytest.mark.parametrize("name", ["FactorizedPrior", "ScaleHyperprior", "MeanScaleHyperprior"])
+def test_model_round_trip(cuda, name):
+    import compressai.models as M
+
+    torch.manual_seed(3)
+    net = getattr(M, name)(32, 48).to(cuda).eval()
+    net.update()
+    x = torch.rand(2, 3, 128, 128, generator=torch.Generator().manual_seed(4)).to(cuda)
+    with torch.no_grad():
+        out = net(x)
+    enc = net.compress(x)
+    dec = net.decompress(enc["strings"], enc["shape"])
+    # the decoder rebuilds exactly the eval forward's y_hat
+    assert (dec["x_hat"] - out["x_hat"].clamp(0, 1)).abs().max().item() < 1e-5
+    est = sum(torch.log(l).sum().item() for l in out["likelihoods"].values()) / -math.log(2)
+    real = _bits(enc["strings"])
+    nstr = sum(len(s) for s in enc["strings"])
+    assert 0.9 * est <= real <= 1.1 * est + 64 * nstr, (real, est)
+
+
+def test_autoregressive_round_trip(cuda):
+    """JointAutoregressiveHierarchicalPriors: serial context coding; the decoder's y_hat
+    equals the encoder's (google.py:565-692)."""
+    import torch.nn.functional as F
+
+    from compressai.models import JointAutoregressiveHierarchicalPriors
+
+    torch.manual_seed(5)
+    net = JointAutoregressiveHierarchicalPriors(32, 48).to(cuda).eval()
+    net.update()
+    x = torch.rand(1, 3, 64, 64, generator=torch.Generator().manual_seed(6)).to(cuda)
+    with pytest.warns(UserWarning):
+        enc = net.compress(x)
+    with pytest.warns(UserWarning):
+        dec = net.decompress(enc["strings"], enc["shape"])
+    assert dec["x_hat"].shape == x.shape and torch.isfinite(dec["x_hat"]).all()
+    with pytest.warns(UserWarning):
+        enc2 = net.compress(x)
+    assert enc2["strings"] == enc["strings"]          # deterministic kernels
+    # encoder-side y_hat, rebuilt with the same loop, vs the decoder's
+    from compressai._prepack import prepacked_forward
+
+    with torch.no_grad(), prepacked_forward(net):
+        y = net.g_a(x)
+        z_hat = net.entropy_bottleneck.decompress(enc["strings"][1], enc["shape"])
+        params = net.h_s(z_hat)
+        y_enc = F.pad(y.float(), (2, 2, 2, 2))
+        H, W = y.shape[2], y.shape[3]
+        s = net._compress_ar(y_enc, params, H, W, 5, 2)
+        assert s == enc["strings"][0][0]
+        y_dec = torch.zeros_like(y_enc)
+        net._decompress_ar(s, y_dec, params, H, W, 5, 2)
+    assert torch.equal(y_enc[:, :, 2:-2, 2:-2], y_dec[:, :, 2:-2, 2:-2])
