@@ -89,6 +89,9 @@ SIGNATURES = {
     "cai_gdn_bwd": (_I, [_I, _P, c_int32, _P, c_int32, _I64, c_int32, _P, _P, c_int32, _P, c_int32, _P, _P]),
     "cai_gdn_param_grad_workspace_bytes": (_S, [_I64, c_int32, _I]),
     "cai_gdn_param_grad": (_I, [_I, _P, c_int32, _P, _I64, c_int32, _P, _P, _F, _F, _P, _P, c_int32, _P, _S, _P]),
+    "cai_gdn_backward_workspace_bytes": (_S, [_I64, c_int32, _I]),
+    "cai_gdn_backward": (_I, [_I, _P, c_int32, _P, c_int32, _I64, c_int32, _P, _P, c_int32, _P, c_int32, _P, _P, _F, _F,
+                              _P, _P, c_int32, _P, _S, _P]),
     "cai_quantize": (_I, [_I, _I64, c_int32, _P, _I, c_int32, _P, c_int32, c_int32, _P, c_int32, _P, _I, c_int32, _P]),
     "cai_gc_fwd": (_I, [_I, _I64, c_int32, _P, _I, c_int32, _P, c_int32, _P, c_int32, _I, _P, c_int32, _F, _F,
                         _P, _I, c_int32, _P, c_int32, _P]),

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from typing import Optional, Sequence, Tuple
 
 import torch
@@ -28,6 +29,7 @@ from ._native import (ACT_LEAKY, ACT_NONE, ACT_RELU, BF16, F32, MASK_LEAKY, MASK
                       ConvGeom, EbGrads, EbParams, lib)
 
 _VP = ctypes.c_void_p
+_GDN_TWO_PASS = os.environ.get("CAI_GDN_TWO_PASS", "0") == "1"
 
 
 # ---------------------------------------------------------------------------
@@ -367,9 +369,7 @@ class GdnFn(torch.autograd.Function):
         st = _stream()
         gpm, gld = to_pm(gy, dt, 8)
         dx = empty_pm(B, C, H, W, dt, gy.device)
-        u = torch.empty(npix * C, dtype=dt, device=gy.device)
-        lib.cai_gdn_bwd(code, _p(xpm), xld, _p(gpm), gld, npix, C, _p(gop), _p(beta), inverse, _p(dx), C, _p(u), st)
-        nbytes = lib.cai_gdn_param_grad_workspace_bytes(npix, C, code)
+        nbytes = lib.cai_gdn_backward_workspace_bytes(npix, C, code)
         ws = torch.empty(nbytes, dtype=torch.uint8, device=gy.device)
         bp, gp = ctx.params
         direct = direct_grad(bp) and direct_grad(gp)
@@ -378,8 +378,18 @@ class GdnFn(torch.autograd.Function):
         else:
             dbr = torch.empty(C, dtype=torch.float32, device=gy.device)
             dgr = torch.empty((C, C), dtype=torch.float32, device=gy.device)
-        lib.cai_gdn_param_grad(code, _p(xpm), xld, _p(u), npix, C, _p(br), _p(gr), beta_min, off, _p(dbr), _p(dgr),
-                               int(direct), _p(ws), nbytes, st)
+        if _GDN_TWO_PASS:   # A/B knob: the two-kernel path (dx + u, then the split-K parameter gradient)
+            u = torch.empty(npix * C, dtype=dt, device=gy.device)
+            lib.cai_gdn_bwd(code, _p(xpm), xld, _p(gpm), gld, npix, C, _p(gop), _p(beta), inverse, _p(dx), C, _p(u),
+                            st)
+            nb2 = lib.cai_gdn_param_grad_workspace_bytes(npix, C, code)
+            ws2 = torch.empty(nb2, dtype=torch.uint8, device=gy.device)
+            lib.cai_gdn_param_grad(code, _p(xpm), xld, _p(u), npix, C, _p(br), _p(gr), beta_min, off, _p(dbr),
+                                   _p(dgr), int(direct), _p(ws2), nb2, st)
+        else:
+            # dx and the parameter gradients in one call (fused pass for bf16, C in {64, 128})
+            lib.cai_gdn_backward(code, _p(xpm), xld, _p(gpm), gld, npix, C, _p(gop), _p(beta), inverse, _p(dx), C,
+                                 _p(br), _p(gr), beta_min, off, _p(dbr), _p(dgr), int(direct), _p(ws), nbytes, st)
         if direct:
             dbr = dgr = None
         return dx, dbr, dgr, None, None, None

@@ -20,6 +20,7 @@
 //   dgamma[i,j] = sum_p u_i x_j^2 ; dbeta_i = sum_p u_i   (cai_gdn_param_grad: split-K MFMA
 //   through the 1x1 wgrad kernel + fixed-order column sums), then the LowerBound rule.
 #include "common.hpp"
+#include "mfma.hpp"
 
 #include <algorithm>
 
@@ -28,6 +29,10 @@ namespace cai {
 int colsum_any(int dtype, const void* g, int64_t npix, int C, int ld, float* out, int accumulate, void* ws, size_t wsb,
                hipStream_t st);
 size_t colsum_ws_bytes(int64_t npix, int C);
+
+__device__ __forceinline__ s16x4 ds_tr16(const char* base, int byte_off) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + byte_off));
+}
 
 template <typename T>
 __device__ __forceinline__ f32x4 mma_sq(u32x4 a, u32x4 b, f32x4 c, bool square);
@@ -56,6 +61,15 @@ __device__ __forceinline__ f32x4 mma_sq<float>(u32x4 a, u32x4 b, f32x4 c, bool s
 }
 
 constexpr int GBM = 64;    // pixels per tile
+
+// Workgroup barrier for LDS hand-offs that leaves global loads in flight:
+// __syncthreads() also waits for every outstanding vector-memory operation,
+// which would drain the next tile's register prefetch at each barrier.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+}
 constexpr int GNT = 256;   // 4 waves, split over channels (1 x 4)
 
 template <typename T, int C>
@@ -197,7 +211,7 @@ __global__ __launch_bounds__(GNT, sizeof(T) == 2 ? 2 : 1) void gdn_fwd_kernel(co
     if (tile < ntiles) tile_load<T, C>(rx, x, x_ld, tile * GBM, npix);
     for (; tile < ntiles; tile += gridDim.x) {
         tile_to_lds<T, C>(rx, lds);
-        __syncthreads();
+        lds_barrier();
         const int64_t nxt = tile + gridDim.x;
         if (nxt < ntiles) tile_load<T, C>(rx, x, x_ld, nxt * GBM, npix);
         Acc<T, C> A;
@@ -217,7 +231,7 @@ __global__ __launch_bounds__(GNT, sizeof(T) == 2 ? 2 : 1) void gdn_fwd_kernel(co
                     acc[tm][tn][r] = xv * (inverse ? sqrtf(nv) : rsqrtf(nv));
                 }
             }
-        __syncthreads();
+        lds_barrier();
 #pragma unroll
         for (int tm = 0; tm < G::TM; ++tm)
 #pragma unroll
@@ -227,9 +241,9 @@ __global__ __launch_bounds__(GNT, sizeof(T) == 2 ? 2 : 1) void gdn_fwd_kernel(co
                 for (int r = 0; r < 4; ++r)
                     *lds_elem<T>(lds, G::RS, G::row0(wave) + tm * 16 + (lane >> 4) * 4 + r, col) = from_f32<T>(acc[tm][tn][r]);
             }
-        __syncthreads();
+        lds_barrier();
         lds_to_global<T, C>(lds, y, y_ld, tile * GBM, npix);
-        __syncthreads();
+        lds_barrier();
     }
 }
 
@@ -315,6 +329,289 @@ __global__ __launch_bounds__(GNT, 1) void gdn_bwd_kernel(const T* __restrict__ x
         }
     __syncthreads();
     lds_to_global<T, C>(Lg, dx, dx_ld, p0, npix);
+}
+
+// ---------------------------------------------------------------------------
+// Fused backward (bf16, C in {64, 128}): dx AND the parameter gradients in one
+// pass over x and dy.  Per 64-pixel tile (persistent blocks, next tile's x / dy
+// prefetched into registers while this one is computed):
+//   norm = x^2 gamma^T + beta          (MFMA, gamma fragments held in registers)
+//   u, t1 = g*r (g*s)                  (fp32, u kept as a bf16 LDS tile)
+//   dx = t1 + 2 x (u gamma)            (MFMA, gamma^T fragments in registers)
+//   dgamma += u^T x^2                  (MFMA with the pixels as K: operands are
+//                                       columns of the [pixel][channel] tiles,
+//                                       read with ds_read_b64_tr_b16)
+//   dbeta  += column sums of u (fp32)
+// Each block leaves its fp32 dgamma / dbeta partial in the workspace; a
+// fixed-order reduce over blocks applies the LowerBound / reparametrization
+// rule (deterministic).  HBM traffic per pixel: read x, dy, write dx (6C B)
+// -- the two-kernel path also writes and re-reads u and re-reads x (+6C B)
+// and runs a separate split-K weight-gradient GEMM.
+// ---------------------------------------------------------------------------
+constexpr int FNT = 512;   // 8 waves
+
+template <int C>
+struct FusedGeo {
+    static constexpr int RS = 2 * C + 16;           // padded LDS row (bf16)
+    static constexpr int KB = C / 32;               // 32-deep K blocks over channels
+    static constexpr int NB = C / 16;               // 16-channel blocks
+    static constexpr int WN = NB < 8 ? NB : 8;      // waves across channels (pixel GEMMs)
+    static constexpr int WM = 8 / WN;               // waves across pixels
+    static constexpr int TM = GBM / (16 * WM);      // 16-pixel blocks per wave
+    static constexpr int WJ = 8 / NB;               // waves sharing one dgamma column block
+    static constexpr int TI = NB / WJ;              // dgamma row blocks per wave
+    static constexpr int CPT = GBM * (2 * C / 16) / FNT;   // 16-byte chunks per thread per tile
+    static constexpr int TILE = GBM * RS;
+    static_assert(WM * WN == 8 && TM >= 1 && CPT >= 1 && WJ * NB == 8, "unsupported C");
+};
+
+template <int C>
+__device__ __forceinline__ void ftile_load(u32x4 (&r)[FusedGeo<C>::CPT], const bf16* src, int ld, int64_t p0,
+                                           int64_t npix) {
+    using G = FusedGeo<C>;
+    constexpr int CHR = 2 * C / 16;
+#pragma unroll
+    for (int i = 0; i < G::CPT; ++i) {
+        const int id = i * FNT + threadIdx.x;
+        const int row = id / CHR, ch = id - (id / CHR) * CHR;
+        const int64_t p = min(p0 + row, npix - 1);   // clamped: every load is issued (rows >= npix unused)
+        r[i] = *reinterpret_cast<const u32x4*>(src + p * ld + ch * 8);
+    }
+}
+template <int C>
+__device__ __forceinline__ void ftile_to_lds(const u32x4 (&r)[FusedGeo<C>::CPT], char* lds, int64_t p0, int64_t npix) {
+    using G = FusedGeo<C>;
+    constexpr int CHR = 2 * C / 16;
+#pragma unroll
+    for (int i = 0; i < G::CPT; ++i) {
+        const int id = i * FNT + threadIdx.x;
+        const int row = id / CHR, ch = id - (id / CHR) * CHR;
+        // rows past the end are zero: they contribute nothing to dgamma / dbeta
+        *reinterpret_cast<u32x4*>(lds + row * G::RS + ch * 16) = (p0 + row < npix) ? r[i] : u32x4{0u, 0u, 0u, 0u};
+    }
+}
+
+template <int C>
+__device__ __forceinline__ void lds_to_global_rows(const char* lds, bf16* dst, int ld, int64_t p0, int64_t npix) {
+    using G = FusedGeo<C>;
+    constexpr int CHR = 2 * C / 16;
+#pragma unroll
+    for (int i = 0; i < G::CPT; ++i) {
+        const int id = i * FNT + threadIdx.x;
+        const int row = id / CHR, ch = id - (id / CHR) * CHR;
+        if (p0 + row < npix)
+            *reinterpret_cast<u32x4*>(dst + (p0 + row) * ld + ch * 8) =
+                *reinterpret_cast<const u32x4*>(lds + row * G::RS + ch * 16);
+    }
+}
+
+template <int C>
+__global__ __launch_bounds__(FNT, 1) void gdn_bwd_fused_kernel(const bf16* __restrict__ x, int x_ld,
+                                                               const bf16* __restrict__ dy, int dy_ld, int64_t npix,
+                                                               const bf16* __restrict__ gamma_op,
+                                                               const float* __restrict__ beta, int inverse,
+                                                               bf16* __restrict__ dx, int dx_ld,
+                                                               float* __restrict__ part) {
+    using G = FusedGeo<C>;
+    __shared__ __attribute__((aligned(16))) char lds[3 * G::TILE];
+    char* Lx = lds;
+    char* Lg = lds + G::TILE;
+    char* Lu = lds + 2 * G::TILE;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wn = wave % G::WN, wm = wave / G::WN;
+    const int n0 = wn * 16, r0 = wm * (GBM / G::WM);
+    const int g_ = lane >> 4, i16 = lane & 15, q_ = i16 >> 2, p4 = i16 & 3;
+    // dgamma tiling: column block jb, row blocks [ib0, ib0 + TI)
+    const int jb = wave % G::NB, ib0 = (wave / G::NB) * G::TI;
+    const bf16* gammaT = gamma_op + (int64_t)C * C;
+
+    // gamma / gamma^T B fragments of this wave's 16 channels
+    u32x4 fb[G::KB], fbT[G::KB];
+#pragma unroll
+    for (int kb = 0; kb < G::KB; ++kb) {
+        const int n = n0 + i16;
+        fb[kb] = *reinterpret_cast<const u32x4*>(gamma_op + (int64_t)n * C + kb * 32 + 8 * g_);
+        fbT[kb] = *reinterpret_cast<const u32x4*>(gammaT + (int64_t)n * C + kb * 32 + 8 * g_);
+    }
+    const float bv = beta[n0 + i16];
+    f32x4 dg[G::TI];
+#pragma unroll
+    for (int t = 0; t < G::TI; ++t) dg[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float dbeta = 0.f;
+
+    // two tiles in flight: registers set A holds tile t + 2*stride while set B
+    // waits with t + stride (the loop body alternates A / B, unrolled by hand)
+    const int64_t ntiles = (npix + GBM - 1) / GBM;
+    const int64_t stride = gridDim.x;
+    u32x4 rxa[G::CPT], rga[G::CPT], rxb[G::CPT], rgb[G::CPT];
+    int64_t tile = blockIdx.x;
+    if (tile < ntiles) {
+        ftile_load<C>(rxa, x, x_ld, tile * GBM, npix);
+        ftile_load<C>(rga, dy, dy_ld, tile * GBM, npix);
+    }
+    if (tile + stride < ntiles) {
+        ftile_load<C>(rxb, x, x_ld, (tile + stride) * GBM, npix);
+        ftile_load<C>(rgb, dy, dy_ld, (tile + stride) * GBM, npix);
+    }
+    for (int parity = 0; tile < ntiles; tile += stride, parity ^= 1) {
+        const int64_t p0 = tile * GBM;
+        lds_barrier();                       // previous tile's dx store has read Lg
+        const int64_t nxt = tile + 2 * stride;
+        if (parity == 0) {
+            ftile_to_lds<C>(rxa, Lx, p0, npix);
+            ftile_to_lds<C>(rga, Lg, p0, npix);
+            if (nxt < ntiles) {
+                ftile_load<C>(rxa, x, x_ld, nxt * GBM, npix);
+                ftile_load<C>(rga, dy, dy_ld, nxt * GBM, npix);
+            }
+        } else {
+            ftile_to_lds<C>(rxb, Lx, p0, npix);
+            ftile_to_lds<C>(rgb, Lg, p0, npix);
+            if (nxt < ntiles) {
+                ftile_load<C>(rxb, x, x_ld, nxt * GBM, npix);
+                ftile_load<C>(rgb, dy, dy_ld, nxt * GBM, npix);
+            }
+        }
+        lds_barrier();
+        // ---- norm = x^2 gamma^T (+ beta) ----
+        f32x4 acc[G::TM];
+#pragma unroll
+        for (int tm = 0; tm < G::TM; ++tm) acc[tm] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kb = 0; kb < G::KB; ++kb)
+#pragma unroll
+            for (int tm = 0; tm < G::TM; ++tm) {
+                const int row = r0 + tm * 16 + i16;
+                const u32x4 a = *reinterpret_cast<const u32x4*>(Lx + row * G::RS + kb * 64 + 16 * g_);
+                acc[tm] = mma_sq<bf16>(a, fb[kb], acc[tm], true);
+            }
+        // ---- u, t1 (thread-owned elements: row (lane>>4)*4 + r, column n0 + i16) ----
+#pragma unroll
+        for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = r0 + tm * 16 + g_ * 4 + r;
+                const float xv = (float)*lds_elem<bf16>(Lx, G::RS, row, n0 + i16);
+                bf16* gp = lds_elem<bf16>(Lg, G::RS, row, n0 + i16);
+                const float gv = (float)*gp;
+                const float nv = acc[tm][r] + bv;
+                float uv, t1;
+                if (inverse) {
+                    const float sq = sqrtf(nv);
+                    t1 = gv * sq;
+                    uv = 0.5f * gv * xv / sq;
+                } else {
+                    const float rr = rsqrtf(nv);
+                    t1 = gv * rr;
+                    uv = -0.5f * gv * xv * rr * rr * rr;
+                }
+                if (p0 + row >= npix) uv = 0.f;
+                dbeta += uv;
+                *gp = (bf16)t1;
+                *lds_elem<bf16>(Lu, G::RS, row, n0 + i16) = (bf16)uv;
+            }
+        lds_barrier();
+        // ---- dgamma += u^T x^2 (K = the tile's 64 pixels; column reads by hardware transpose) ----
+#pragma unroll
+        for (int ks = 0; ks < GBM / 32; ++ks) {
+            const int rr = 32 * ks + 8 * g_ + q_;
+            const int colB = jb * 16 + 4 * p4;
+            const s16x4 b0 = ds_tr16(Lx, rr * G::RS + colB * 2);
+            const s16x4 b1 = ds_tr16(Lx, (rr + 4) * G::RS + colB * 2);
+            const s16x8 bvv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+            const u32x4 fbx = sq_chunk<bf16>(__builtin_bit_cast(u32x4, bvv));
+#pragma unroll
+            for (int t = 0; t < G::TI; ++t) {
+                const int colA = (ib0 + t) * 16 + 4 * p4;
+                const s16x4 a0 = ds_tr16(Lu, rr * G::RS + colA * 2);
+                const s16x4 a1 = ds_tr16(Lu, (rr + 4) * G::RS + colA * 2);
+                const s16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+                dg[t] = mma16<bf16>(__builtin_bit_cast(u32x4, av), fbx, dg[t]);
+            }
+        }
+        // ---- dx = t1 + 2 x (u gamma) ----
+#pragma unroll
+        for (int tm = 0; tm < G::TM; ++tm) acc[tm] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kb = 0; kb < G::KB; ++kb)
+#pragma unroll
+            for (int tm = 0; tm < G::TM; ++tm) {
+                const int row = r0 + tm * 16 + i16;
+                const u32x4 a = *reinterpret_cast<const u32x4*>(Lu + row * G::RS + kb * 64 + 16 * g_);
+                acc[tm] = mma16<bf16>(a, fbT[kb], acc[tm]);
+            }
+#pragma unroll
+        for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = r0 + tm * 16 + g_ * 4 + r;
+                const float xv = (float)*lds_elem<bf16>(Lx, G::RS, row, n0 + i16);
+                bf16* gp = lds_elem<bf16>(Lg, G::RS, row, n0 + i16);
+                *gp = (bf16)((float)*gp + 2.f * xv * acc[tm][r]);
+            }
+        lds_barrier();
+        lds_to_global_rows<C>(Lg, dx, dx_ld, p0, npix);
+    }
+    // ---- partials: dbeta (lanes of one column: xor 16, 32; waves of one column block via LDS) ----
+    dbeta += __shfl_xor(dbeta, 16, 64);
+    dbeta += __shfl_xor(dbeta, 32, 64);
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(lds);
+    if (lane < 16) red[wm * C + n0 + lane] = dbeta;
+    __syncthreads();
+    float* pb = part + (int64_t)blockIdx.x * (C * C + C);
+    for (int c = threadIdx.x; c < C; c += FNT) {
+        float v = 0.f;
+        for (int m = 0; m < G::WM; ++m) v += red[m * C + c];
+        pb[C * C + c] = v;
+    }
+#pragma unroll
+    for (int t = 0; t < G::TI; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = (ib0 + t) * 16 + g_ * 4 + r, j = jb * 16 + i16;
+            pb[(int64_t)i * C + j] = dg[t][r];
+        }
+}
+
+// sum the per-block partials in a fixed order, then the NonNegativeParametrizer /
+// LowerBound backward rule (as gdn_reparam_bwd_kernel).  256 threads = 16
+// element columns x 16 partial-block groups; groups combine through LDS in
+// a fixed tree (deterministic).
+__global__ __launch_bounds__(256) void gdn_fused_reduce_kernel(const float* __restrict__ part, int nblk, int C,
+                                                               const float* __restrict__ beta_raw,
+                                                               const float* __restrict__ gamma_raw, float bbound,
+                                                               float gbound, float* __restrict__ dbeta_raw,
+                                                               float* __restrict__ dgamma_raw, int accumulate) {
+    __shared__ float red[16][17];
+    const int64_t CC = (int64_t)C * C, stride = CC + C;
+    const int cg = threadIdx.x & 15, bg = threadIdx.x >> 4;
+    const int64_t i = (int64_t)blockIdx.x * 16 + cg;
+    float v = 0.f;
+    if (i < CC + C)
+        for (int b = bg; b < nblk; b += 16) v += part[b * stride + i];
+    red[bg][cg] = v;
+    __syncthreads();
+    if (bg != 0 || i >= CC + C) return;
+#pragma unroll
+    for (int j = 1; j < 16; ++j) v += red[j][cg];
+    if (i < CC) {
+        const float gr = gamma_raw[i];
+        const float d = 2.f * fmaxf(gr, gbound) * v;
+        const float vg = (gr >= gbound || d < 0.f) ? d : 0.f;
+        dgamma_raw[i] = accumulate ? dgamma_raw[i] + vg : vg;
+    } else {
+        const int64_t c = i - CC;
+        const float br = beta_raw[c];
+        const float db = 2.f * fmaxf(br, bbound) * v;
+        const float vb = (br >= bbound || db < 0.f) ? db : 0.f;
+        dbeta_raw[c] = accumulate ? dbeta_raw[c] + vb : vb;
+    }
+}
+
+static int fused_blocks(int64_t npix) {
+    const int64_t tiles = (npix + GBM - 1) / GBM;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(256, tiles));
 }
 
 __global__ void gdn_reparam_kernel(const float* __restrict__ beta_raw, const float* __restrict__ gamma_raw, int C,
@@ -473,6 +770,61 @@ int cai_gdn_param_grad(int dtype, const void* x, int32_t x_ld, const void* u, in
                        as_stream(stream), beta_raw, gamma_raw, dbeta, dgamma, C, bbound, gbound, dbeta_raw, dgamma_raw,
                        accumulate);
     CAI_LAUNCH_CHECK("gdn_param_grad");
+    return CAI_OK;
+}
+
+
+static bool fused_ok(int dtype, int C) { return dtype == CAI_BF16 && (C == 64 || C == 128); }
+
+size_t cai_gdn_backward_workspace_bytes(int64_t npix, int32_t C, int dtype) {
+    if (npix <= 0 || !gdn_c_ok(C)) return 0;
+    if (fused_ok(dtype, C)) return (size_t)fused_blocks(npix) * ((size_t)C * C + C) * sizeof(float);
+    const size_t ub = ((size_t)npix * C * dtype_size(dtype) + 255) / 256 * 256;
+    return ub + cai_gdn_param_grad_workspace_bytes(npix, C, dtype);
+}
+
+int cai_gdn_backward(int dtype, const void* x, int32_t x_ld, const void* dy, int32_t dy_ld, int64_t npix, int32_t C,
+                     const void* gamma_op, const float* beta, int32_t inverse, void* dx, int32_t dx_ld,
+                     const float* beta_raw, const float* gamma_raw, float beta_min, float reparam_offset,
+                     float* dbeta_raw, float* dgamma_raw, int32_t accumulate, void* workspace, size_t ws_bytes,
+                     void* stream) {
+    CAI_CHECK_ARG(gdn_c_ok(C), "gdn_backward: unsupported channel count %d", C);
+    CAI_CHECK_ARG(x && dy && gamma_op && beta && dx && beta_raw && gamma_raw && dbeta_raw && dgamma_raw,
+                  "gdn_backward: null pointer");
+    CAI_CHECK_ARG(x_ld % 8 == 0 && dy_ld % 8 == 0 && dx_ld % 8 == 0 && x_ld >= C && dy_ld >= C && dx_ld >= C,
+                  "gdn_backward: bad leading dimensions");
+    CAI_CHECK_ARG(npix > 0 && npix < (1ll << 31), "gdn_backward: bad pixel count");
+    CAI_CHECK_ARG(workspace && ws_bytes >= cai_gdn_backward_workspace_bytes(npix, C, dtype) &&
+                      ((uintptr_t)workspace & 255) == 0,
+                  "gdn_backward: workspace of %zu bytes (256-byte aligned) required",
+                  cai_gdn_backward_workspace_bytes(npix, C, dtype));
+    hipStream_t st = as_stream(stream);
+    if (!fused_ok(dtype, C)) {
+        // two-kernel path: dx + u, then the split-K parameter gradient
+        const size_t ub = ((size_t)npix * C * dtype_size(dtype) + 255) / 256 * 256;
+        char* ws = reinterpret_cast<char*>(workspace);
+        int rc = cai_gdn_bwd(dtype, x, x_ld, dy, dy_ld, npix, C, gamma_op, beta, inverse, dx, dx_ld, ws, stream);
+        if (rc) return rc;
+        return cai_gdn_param_grad(dtype, x, x_ld, ws, npix, C, beta_raw, gamma_raw, beta_min, reparam_offset,
+                                  dbeta_raw, dgamma_raw, accumulate, ws + ub, ws_bytes - ub, stream);
+    }
+    const int nblk = fused_blocks(npix);
+    float* part = reinterpret_cast<float*>(workspace);
+    auto launch = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(nblk), dim3(FNT), 0, st, reinterpret_cast<const bf16*>(x), x_ld,
+                           reinterpret_cast<const bf16*>(dy), dy_ld, npix, reinterpret_cast<const bf16*>(gamma_op),
+                           beta, inverse, reinterpret_cast<bf16*>(dx), dx_ld, part);
+    };
+    if (C == 128)
+        launch(gdn_bwd_fused_kernel<128>);
+    else
+        launch(gdn_bwd_fused_kernel<64>);
+    const float ped = reparam_offset * reparam_offset;
+    const float bbound = sqrtf(beta_min + ped), gbound = sqrtf(ped);
+    const int64_t n = (int64_t)C * C + C;
+    hipLaunchKernelGGL(gdn_fused_reduce_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0,
+                       st, part, nblk, C, beta_raw, gamma_raw, bbound, gbound, dbeta_raw, dgamma_raw, accumulate);
+    CAI_LAUNCH_CHECK("gdn_backward");
     return CAI_OK;
 }
 

@@ -258,6 +258,18 @@ int cai_gdn_param_grad(int dtype, const void* x, int32_t x_ld, const void* u, in
                        float* dbeta_raw, float* dgamma_raw, int32_t accumulate,
                        void* workspace, size_t ws_bytes, void* stream);
 
+/* The whole GDN / IGDN backward in one call: dx plus dgamma_raw / dbeta_raw
+ * (overwritten, or added with accumulate != 0).  bf16 with C in {64, 128}
+ * runs one fused pass over x and dy (dgamma as an MFMA with the pixels as K,
+ * per-block partials reduced in a fixed order); other cases run cai_gdn_bwd +
+ * cai_gdn_param_grad.  workspace: 256-byte aligned. */
+size_t cai_gdn_backward_workspace_bytes(int64_t npix, int32_t C, int dtype);
+int cai_gdn_backward(int dtype, const void* x, int32_t x_ld, const void* dy, int32_t dy_ld, int64_t npix, int32_t C,
+                     const void* gamma_op, const float* beta, int32_t inverse, void* dx, int32_t dx_ld,
+                     const float* beta_raw, const float* gamma_raw, float beta_min, float reparam_offset,
+                     float* dbeta_raw, float* dgamma_raw, int32_t accumulate, void* workspace, size_t ws_bytes,
+                     void* stream);
+
 /* =======================================================================
  * Entropy models.  Element (p, c) of every operand at ptr[p*ld + c].
  * ======================================================================= */

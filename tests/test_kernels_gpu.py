@@ -169,6 +169,68 @@ def test_gdn(cuda, C, inverse, bf16):
     assert relerr(mod.beta.grad, ref.beta.grad) < tol * 5
 
 
+@pytest.mark.parametrize("inverse", [False, True])
+@pytest.mark.parametrize("C", [64, 128])
+def test_gdn_fused_backward_many_blocks(cuda, C, inverse):
+    """bf16 fused backward (cai_gdn_backward: dx + per-block dgamma/dbeta partials, fixed-order
+    reduce) over many tiles and blocks, against the fp32 oracle; and equal (to bf16 rounding of u)
+    to the two-kernel path it replaces."""
+    from compressai import _native
+    from compressai._ops import _p
+    from compressai.layers import GDN
+
+    torch.manual_seed(11)
+    ref = O.GDN(C, inverse=inverse)
+    with torch.no_grad():
+        ref.gamma.add_(0.02 * torch.rand(C, C))
+        ref.beta.add_(0.1 * torch.rand(C))
+    mod = GDN(C, inverse=inverse)
+    mod.load_state_dict(ref.state_dict())
+    mod = mod.to(cuda)
+    x = torch.randn(3, C, 40, 37)          # 4440 pixels: 70 tiles, ragged last tile, 8 blocks
+    xr = x.clone().requires_grad_()
+    yr = ref(xr)
+    g = torch.randn_like(yr)
+    yr.backward(g)
+    xd = x.to(cuda).contiguous(memory_format=torch.channels_last).requires_grad_()
+    with _autocast(True):
+        y = mod(xd)
+    y.backward(g.to(cuda))
+    assert relerr(xd.grad, xr.grad) < BF16_TOL
+    assert relerr(mod.gamma.grad, ref.gamma.grad) < BF16_TOL
+    assert relerr(mod.beta.grad, ref.beta.grad) < BF16_TOL
+    # the two-kernel path on the same bf16 operands
+    lib = _native.lib
+    npix = x.shape[0] * x.shape[2] * x.shape[3]
+    xb = x.to(cuda).permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    gb = g.to(cuda).permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    br, gr = mod.beta.detach().float().contiguous(), mod.gamma.detach().float().contiguous()
+    beta = torch.empty(C, device=cuda)
+    gop = torch.empty(2 * C * C, dtype=torch.bfloat16, device=cuda)
+    st = torch.cuda.current_stream().cuda_stream
+    lib.cai_gdn_reparam(_p(br), _p(gr), C, 1e-6, 2 ** -18, _native.BF16, _p(beta), _p(gop), st)
+    outs = []
+    for fused in (True, False):
+        dx = torch.empty_like(xb)
+        dbr, dgr = torch.empty(C, device=cuda), torch.empty(C, C, device=cuda)
+        if fused:
+            nb = lib.cai_gdn_backward_workspace_bytes(npix, C, _native.BF16)
+            ws = torch.empty(nb, dtype=torch.uint8, device=cuda)
+            lib.cai_gdn_backward(_native.BF16, _p(xb), C, _p(gb), C, npix, C, _p(gop), _p(beta), int(inverse), _p(dx),
+                                 C, _p(br), _p(gr), 1e-6, 2 ** -18, _p(dbr), _p(dgr), 0, _p(ws), nb, st)
+        else:
+            u = torch.empty(npix * C, dtype=torch.bfloat16, device=cuda)
+            lib.cai_gdn_bwd(_native.BF16, _p(xb), C, _p(gb), C, npix, C, _p(gop), _p(beta), int(inverse), _p(dx), C,
+                            _p(u), st)
+            nb = lib.cai_gdn_param_grad_workspace_bytes(npix, C, _native.BF16)
+            ws = torch.empty(nb, dtype=torch.uint8, device=cuda)
+            lib.cai_gdn_param_grad(_native.BF16, _p(xb), C, _p(u), npix, C, _p(br), _p(gr), 1e-6, 2 ** -18, _p(dbr),
+                                   _p(dgr), 0, _p(ws), nb, st)
+        outs.append((dx.float(), dbr, dgr))
+    for a, b in zip(outs[0], outs[1]):
+        assert relerr(a, b) < 1e-2
+
+
 def test_gdn_closed_form_at_init(cuda):
     """tests/test_layers.py:134-160 KATs (GDN(64) instead of GDN(32): C in {64,128,192})."""
     from compressai.layers import GDN
