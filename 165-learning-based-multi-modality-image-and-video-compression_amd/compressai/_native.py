@@ -82,7 +82,8 @@ SIGNATURES = {
     "cai_window_attn_bwd_workspace_bytes": (_S, [POINTER(WindowAttn)]),
     "cai_window_attn_bwd": (_I, [_I, POINTER(WindowAttn), _P, c_int32, _P, c_int32, _P, c_int32, _P, c_int32, _P, _S,
                                  _P]),
-    "cai_channel_mean": (_I, [_I, _P, c_int32, _P, c_int32, c_int32, _I64, c_int32, _P, _F, _P]),
+    "cai_channel_mean_workspace_bytes": (_S, [c_int32, _I64, c_int32]),
+    "cai_channel_mean": (_I, [_I, _P, c_int32, _P, c_int32, c_int32, _I64, c_int32, _P, _F, _P, _S, _P]),
     "cai_channel_affine": (_I, [_I, _P, c_int32, _P, _P, _F, _P, c_int32, c_int32, _I64, c_int32, _P]),
     "cai_gdn_reparam": (_I, [_P, _P, c_int32, _F, _F, _I, _P, _P, _P]),
     "cai_gdn_fwd": (_I, [_I, _P, c_int32, _I64, c_int32, _P, _P, c_int32, _P, c_int32, _P]),

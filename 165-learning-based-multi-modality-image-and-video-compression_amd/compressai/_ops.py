@@ -890,6 +890,11 @@ def _attn_desc(qp, qld, kp, kld, tb, rel_index, mask, B, Hr, Wr, heads, window, 
                       heads, qp.shape[1] // heads, window, shift, scale)
 
 
+def _mean_ws(B, HW, C, device):
+    nb = lib.cai_channel_mean_workspace_bytes(B, HW, C)
+    return torch.empty(max(nb, 16), dtype=torch.uint8, device=device), nb
+
+
 class ChannelMeanFn(torch.autograd.Function):
     """nn.AdaptiveAvgPool2d(1) of a pixel-major map -> [B, C, 1, 1] fp32."""
 
@@ -900,7 +905,9 @@ class ChannelMeanFn(torch.autograd.Function):
         B, C, H, W = x.shape
         xp, xld = to_pm(x, dt, _vec(dt))
         out = torch.empty((B, C, 1, 1), dtype=torch.float32, device=x.device)
-        lib.cai_channel_mean(dcode(dt), _p(xp), xld, None, 0, B, H * W, C, _p(out), 1.0 / (H * W), _stream())
+        ws, nb = _mean_ws(B, H * W, C, x.device)
+        lib.cai_channel_mean(dcode(dt), _p(xp), xld, None, 0, B, H * W, C, _p(out), 1.0 / (H * W), _p(ws), nb,
+                             _stream())
         ctx.cfg = (dt, tuple(x.shape))
         return out
 
@@ -940,6 +947,7 @@ class ChannelAffineFn(torch.autograd.Function):
         lib.cai_channel_affine(dcode(dt), _p(gp), gld, _p(ga), None, 0.0, _p(dx), dxld, B, H * W, C, _stream())
         dgamma = torch.empty((B, C, 1, 1), dtype=torch.float32, device=g.device)
         dbeta = torch.empty((B, C, 1, 1), dtype=torch.float32, device=g.device)
-        lib.cai_channel_mean(dcode(dt), _p(gp), gld, _p(xp), xld, B, H * W, C, _p(dgamma), 1.0, _stream())
-        lib.cai_channel_mean(dcode(dt), _p(gp), gld, None, 0, B, H * W, C, _p(dbeta), 1.0, _stream())
+        ws, nb = _mean_ws(B, H * W, C, g.device)
+        lib.cai_channel_mean(dcode(dt), _p(gp), gld, _p(xp), xld, B, H * W, C, _p(dgamma), 1.0, _p(ws), nb, _stream())
+        lib.cai_channel_mean(dcode(dt), _p(gp), gld, None, 0, B, H * W, C, _p(dbeta), 1.0, _p(ws), nb, _stream())
         return dx, dgamma, dbeta

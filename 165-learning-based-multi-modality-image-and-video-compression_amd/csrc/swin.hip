@@ -346,47 +346,118 @@ __global__ __launch_bounds__(256) void window_attn_bwd_kernel(const AttnArgs a) 
     for (int k = threadIdx.x; k < a.heads * WN * WN; k += 256) a.dbias_part[(int64_t)blockIdx.x * a.heads * WN * WN + k] = acc[k];
 }
 
-// dtable[idx[i][j]][h] (+)= sum_blocks part[blk][h][i][j], fixed order
-__global__ void attn_bias_grad_reduce(const float* __restrict__ part, int nblk, int heads,
-                                      const int* __restrict__ rel_index, int table_rows, float* __restrict__ dtable,
-                                      int accumulate) {
-    // one thread per table entry (row r, head h): sum over (i, j) with idx == r
+// dtable[idx[i][j]][h] (+)= sum_blocks part[blk][h][i][j], in a fixed order and
+// in three stages, so that every stage has plenty of threads:
+//   1. part[blk][e] -> part2[split][e]   (e = h*WN*WN + ij: coalesced rows, a block range per split)
+//   2. part2[split][e] -> tot[e]
+//   3. dtable[r][h] = sum over ij with rel_index[ij] == r of tot[h][ij]
+constexpr int ATTN_SPLITS = 64;
+__global__ __launch_bounds__(256) void attn_bias_sum_splits(const float* __restrict__ part, int nblk, int E,
+                                                            float* __restrict__ part2) {
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= E) return;
+    const int per = (nblk + ATTN_SPLITS - 1) / ATTN_SPLITS;
+    const int b0 = blockIdx.y * per, b1 = min(nblk, b0 + per);
+    float s = 0.f;
+    for (int blk = b0; blk < b1; ++blk) s += part[(int64_t)blk * E + e];
+    part2[blockIdx.y * E + e] = s;
+}
+__global__ __launch_bounds__(256) void attn_bias_sum_total(const float* __restrict__ part2, int E,
+                                                           float* __restrict__ tot) {
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= E) return;
+    float s = 0.f;
+    for (int sp = 0; sp < ATTN_SPLITS; ++sp) s += part2[sp * E + e];
+    tot[e] = s;
+}
+__global__ void attn_bias_grad_reduce(const float* __restrict__ tot, int heads, const int* __restrict__ rel_index,
+                                      int table_rows, float* __restrict__ dtable, int accumulate) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= table_rows * heads) return;
     const int r = e / heads, h = e - (e / heads) * heads;
     float s = 0.f;
-    for (int ij = 0; ij < WN * WN; ++ij) {
-        if (rel_index[ij] != r) continue;
-        for (int blk = 0; blk < nblk; ++blk) s += part[((int64_t)blk * heads + h) * WN * WN + ij];
-    }
+    for (int ij = 0; ij < WN * WN; ++ij)
+        if (rel_index[ij] == r) s += tot[h * WN * WN + ij];
     dtable[e] = accumulate ? dtable[e] + s : s;
 }
 
 // --------------------------------------------------------------------------
 // Channel aligner: per-(image, channel) means, y = gamma[b][c] * x + beta[b][c]
 // --------------------------------------------------------------------------
-// mean[b][c] = (1/HW) sum_p x[b][p][c]: block per (b, 64-channel slice)
+// out[b][c] = scale * sum_p x[b][p][c] (* x2[b][p][c]), two stages, fixed order.
+// Stage 1: block (chunk, b) sums a pixel chunk of image b for every channel:
+// thread = (16-byte channel group, pixel row), rows in flight = 256 / groups.
 template <typename T>
-__global__ __launch_bounds__(256) void channel_mean_kernel(const T* __restrict__ x, int xld, int HW, int C,
-                                                           const T* __restrict__ x2, int x2ld,
-                                                           float* __restrict__ out, float scale) {
-    // optional second operand: out = scale * sum x * x2 (the affine's gamma gradient)
-    __shared__ float red[4][64];
-    const int b = blockIdx.y, c = blockIdx.x * 64 + (threadIdx.x & 63), wv = threadIdx.x >> 6;
-    float s = 0.f;
-    if (c < C) {
-        const T* base = x + (int64_t)b * HW * xld + c;
-        const T* base2 = x2 ? x2 + (int64_t)b * HW * x2ld + c : nullptr;
-        for (int p = wv; p < HW; p += 4) {
-            float v = ldf(base, (int64_t)p * xld);
-            if (base2) v *= ldf(base2, (int64_t)p * x2ld);
-            s += v;
+__global__ __launch_bounds__(256) void channel_mean_stage1(const T* __restrict__ x, int xld,
+                                                           const T* __restrict__ x2, int x2ld, int HW, int C,
+                                                           int chunk, float* __restrict__ part) {
+    constexpr int VEC = 16 / sizeof(T);
+    __shared__ float red[256 * VEC];
+    const int ngrp = (C + VEC - 1) / VEC;
+    const int rows = 256 / ngrp;
+    const int tid = threadIdx.x, r = tid / ngrp, grp = tid - (tid / ngrp) * ngrp;
+    const int b = blockIdx.y;
+    const int64_t pb = (int64_t)blockIdx.x * chunk, pe = min((int64_t)HW, pb + chunk);
+    float s[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) s[e] = 0.f;
+    if (r < rows) {
+        const T* xb = x + (int64_t)b * HW * xld + grp * VEC;
+        const T* x2b = x2 ? x2 + (int64_t)b * HW * x2ld + grp * VEC : nullptr;
+        for (int64_t p = pb + r; p < pe; p += rows) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(xb + p * xld);
+            float f[VEC];
+            if constexpr (VEC == 8) {
+                const bf16x8 h = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) f[e] = (float)h[e];
+            } else {
+                const f32x4 h = __builtin_bit_cast(f32x4, v);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) f[e] = h[e];
+            }
+            if (x2b) {
+                const u32x4 v2 = *reinterpret_cast<const u32x4*>(x2b + p * x2ld);
+                if constexpr (VEC == 8) {
+                    const bf16x8 h = __builtin_bit_cast(bf16x8, v2);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) f[e] *= (float)h[e];
+                } else {
+                    const f32x4 h = __builtin_bit_cast(f32x4, v2);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) f[e] *= h[e];
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) s[e] += f[e];
         }
     }
-    red[wv][threadIdx.x & 63] = s;
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) red[tid * VEC + e] = (r < rows) ? s[e] : 0.f;
     __syncthreads();
-    if (wv == 0 && c < C) out[(int64_t)b * C + c] = (red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
-                                                     red[3][threadIdx.x]) * scale;
+    for (int c = tid; c < C; c += 256) {
+        const int g0 = c / VEC, e = c - g0 * VEC;
+        float acc = 0.f;
+        for (int rr = 0; rr < rows; ++rr) acc += red[(rr * ngrp + g0) * VEC + e];
+        part[((int64_t)b * gridDim.x + blockIdx.x) * C + c] = acc;
+    }
+}
+// stage 2: one wave per (b, c): the chunk partials, fixed xor tree
+__global__ __launch_bounds__(256) void channel_mean_stage2(const float* __restrict__ part, int nchunk, int B, int C,
+                                                           float* __restrict__ out, float scale) {
+    const int lane = threadIdx.x & 63;
+    const int o = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (o >= B * C) return;
+    const int b = o / C, c = o - (o / C) * C;
+    float s = 0.f;
+    for (int i = lane; i < nchunk; i += 64) s += part[((int64_t)b * nchunk + i) * C + c];
+    s = wave_sum(s);
+    if (lane == 0) out[o] = s * scale;
+}
+
+static int mean_chunk(int B, int64_t HW) {
+    const int64_t target = std::max(1, 1024 / B);                 // ~1024 stage-1 blocks in all
+    return (int)std::max<int64_t>(256, (HW + target - 1) / target);
 }
 
 template <typename T>
@@ -521,7 +592,8 @@ int cai_window_attn_fwd(int dtype, const cai_window_attn* p, void* out, int32_t 
 
 size_t cai_window_attn_bwd_workspace_bytes(const cai_window_attn* p) {
     if (check_attn(p)) return 0;
-    return (size_t)attn_blocks(p) * p->heads * WN * WN * sizeof(float);
+    // per-block partials, ATTN_SPLITS split sums, the totals
+    return ((size_t)attn_blocks(p) + ATTN_SPLITS + 1) * p->heads * WN * WN * sizeof(float);
 }
 
 int cai_window_attn_bwd(int dtype, const cai_window_attn* p, const void* dout, int32_t dout_ld, void* dq,
@@ -539,19 +611,41 @@ int cai_window_attn_bwd(int dtype, const cai_window_attn* p, const void* dout, i
     hipStream_t st = as_stream(stream);
     DISPATCH_T(dtype, hipLaunchKernelGGL(window_attn_bwd_kernel<T>, dim3(nblk), dim3(256), 0, st, a));
     const int rows = (2 * WS - 1) * (2 * WS - 1);
-    hipLaunchKernelGGL(attn_bias_grad_reduce, dim3((rows * p->heads + 63) / 64), dim3(64), 0, st, a.dbias_part, nblk,
-                       p->heads, p->rel_index, rows, dbias_table, accumulate);
+    const int E = p->heads * WN * WN;
+    float* part2 = a.dbias_part + (int64_t)nblk * E;
+    float* tot = part2 + (int64_t)ATTN_SPLITS * E;
+    hipLaunchKernelGGL(attn_bias_sum_splits, dim3((E + 255) / 256, ATTN_SPLITS), dim3(256), 0, st, a.dbias_part, nblk,
+                       E, part2);
+    hipLaunchKernelGGL(attn_bias_sum_total, dim3((E + 255) / 256), dim3(256), 0, st, part2, E, tot);
+    hipLaunchKernelGGL(attn_bias_grad_reduce, dim3((rows * p->heads + 63) / 64), dim3(64), 0, st, tot, p->heads,
+                       p->rel_index, rows, dbias_table, accumulate);
     CAI_LAUNCH_CHECK("window_attn_bwd");
     return CAI_OK;
 }
 
+size_t cai_channel_mean_workspace_bytes(int32_t B, int64_t HW, int32_t C) {
+    if (B <= 0 || HW <= 0 || C <= 0) return 0;
+    const int64_t nchunk = (HW + mean_chunk(B, HW) - 1) / mean_chunk(B, HW);
+    return (size_t)B * nchunk * C * sizeof(float);
+}
+
 int cai_channel_mean(int dtype, const void* x, int32_t x_ld, const void* x2, int32_t x2_ld, int32_t B, int64_t HW,
-                     int32_t C, float* out, float scale, void* stream) {
+                     int32_t C, float* out, float scale, void* workspace, size_t ws_bytes, void* stream) {
     CAI_CHECK_ARG(dtype == CAI_BF16 || dtype == CAI_F32, "channel_mean: bad dtype");
     CAI_CHECK_ARG(x && out && B > 0 && HW > 0 && HW < (1ll << 31) && C > 0, "channel_mean: bad arguments");
-    DISPATCH_T(dtype, hipLaunchKernelGGL(channel_mean_kernel<T>, dim3((C + 63) / 64, B), dim3(256), 0,
-                                         as_stream(stream), (const T*)x, x_ld, (int)HW, C, (const T*)x2, x2_ld, out,
-                                         scale));
+    const int vec = dtype == CAI_BF16 ? 8 : 4;
+    CAI_CHECK_ARG(C <= 256 * vec && x_ld % vec == 0 && ((uintptr_t)x & 15) == 0 &&
+                      (!x2 || (x2_ld % vec == 0 && ((uintptr_t)x2 & 15) == 0)),
+                  "channel_mean: operands must be 16-byte aligned with ld %% %d == 0 and C <= %d", vec, 256 * vec);
+    CAI_CHECK_ARG(workspace && ws_bytes >= cai_channel_mean_workspace_bytes(B, HW, C),
+                  "channel_mean: workspace of %zu bytes required", cai_channel_mean_workspace_bytes(B, HW, C));
+    const int chunk = mean_chunk(B, HW);
+    const int nchunk = (int)((HW + chunk - 1) / chunk);
+    float* part = reinterpret_cast<float*>(workspace);
+    hipStream_t st = as_stream(stream);
+    DISPATCH_T(dtype, hipLaunchKernelGGL(channel_mean_stage1<T>, dim3(nchunk, B), dim3(256), 0, st, (const T*)x, x_ld,
+                                         (const T*)x2, x2_ld, (int)HW, C, chunk, part));
+    hipLaunchKernelGGL(channel_mean_stage2, dim3((B * C + 3) / 4), dim3(256), 0, st, part, nchunk, B, C, out, scale);
     CAI_LAUNCH_CHECK("channel_mean");
     return CAI_OK;
 }

@@ -36,6 +36,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+MM_IR = (512, 640)          # FLIR IR frame (ResearchReport.pdf 4.2; image_rgbt_rgb.py:133-141)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -44,9 +45,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=16, help="patches per GPU")
+    ap.add_argument("--batch", type=int, default=None, help="patches (pairs) per GPU; default 16 (2 for multimodal)")
     ap.add_argument("--size", type=int, default=256)
-    ap.add_argument("--model", default="bmshj2018-hyperprior")
+    ap.add_argument("--model", default="bmshj2018-hyperprior",
+                    help="a zoo name, or 'multimodal' (BASELINE configs[4]: Master_compresser on IR 512x640 "
+                         "guided by Guided_compresser on RGB 1024x1280, train.py:208-274)")
     ap.add_argument("--quality", type=int, default=1)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
@@ -58,17 +61,26 @@ def parse():
 
 def dominant_kernel_roofline(B, size, reps=20):
     """g_a[2]: Conv2d(128,128,k5,s2,p2) at (size/2)^2 -> (size/4)^2, bf16 implicit GEMM."""
+    H = size // 2
+    r = conv_roofline(B, 128, H, H, 128, 5, 2, reps)
+    r["kernel"] = ("conv_glds_kernel<256x128> (g_a[2] fwd: Conv2d 128->128 k5 s2, %dx%d->%dx%d, B=%d)"
+                   % (H, H, H // 2, H // 2, B))
+    r["traffic"] = pmc_traffic(B, size)
+    return r
+
+
+def conv_roofline(B, C, H, W, N, k, stride, reps=20):
+    """One bf16 Conv2d(C, N, k, s, k//2) launch on its own stream, HIP-event timed."""
     from compressai._native import BF16, ConvGeom, lib
     from compressai._ops import _pack_weight, _p
 
-    H = size // 2
-    OH = H // 2
-    g = ConvGeom(B, 128, H, H, 128, OH, OH, 5, 2, 2, 0, 0)
+    OH, OW = (H + 2 * (k // 2) - k) // stride + 1, (W + 2 * (k // 2) - k) // stride + 1
+    g = ConvGeom(B, C, H, W, N, OH, OW, k, stride, k // 2, 0, 0)
     dev = torch.device("cuda")
-    x = torch.randn(B, H, H, 128, device=dev).to(torch.bfloat16)
-    w = torch.randn(128, 128, 5, 5, device=dev) * 0.02
-    b = torch.zeros(128, device=dev)
-    y = torch.empty(B, OH, OH, 128, device=dev, dtype=torch.bfloat16)
+    x = torch.randn(B, H, W, C, device=dev).to(torch.bfloat16)
+    w = torch.randn(N, C, k, k, device=dev) * 0.02
+    b = torch.zeros(N, device=dev)
+    y = torch.empty(B, OH, OW, N, device=dev, dtype=torch.bfloat16)
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
         from compressai import _ops
@@ -78,8 +90,8 @@ def dominant_kernel_roofline(B, size, reps=20):
         ws = torch.empty(max(nws, 16), dtype=torch.uint8, device=dev)   # split-K scratch at small batch
 
         def launch():
-            lib.cai_conv_fwd(ctypes.byref(g), BF16, _p(x), 128, 0, _p(wp), _p(b), 0, 0.0, _p(y), BF16,
-                             OH * OH * 128, 1, OH * 128, 128, _p(ws), nws, st)
+            lib.cai_conv_fwd(ctypes.byref(g), BF16, _p(x), C, 0, _p(wp), _p(b), 0, 0.0, _p(y), BF16,
+                             OH * OW * N, 1, OW * N, N, _p(ws), nws, st)
         for _ in range(3):
             launch()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -89,14 +101,13 @@ def dominant_kernel_roofline(B, size, reps=20):
         e1.record(s)
     e1.synchronize()
     ms = e0.elapsed_time(e1) / reps
-    flops = 2.0 * (B * OH * OH) * 128 * (25 * 128)
+    flops = 2.0 * (B * OH * OW) * N * (k * k * C)
     tflops = flops / (ms * 1e-3) / 1e12
-    name = ("conv_glds_kernel<256x128> (g_a[2] fwd: Conv2d 128->128 k5 s2, %dx%d->%dx%d, B=%d)"
-            % (H, H, OH, OH, B))
+    name = "conv (Conv2d %d->%d k%d s%d, %dx%d->%dx%d, B=%d)" % (C, N, k, stride, H, W, OH, OW, B)
     return {"kernel": name, "bound": "mfma", "achieved": round(tflops, 2), "peak": BF16_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(tflops / BF16_PEAK_TFLOPS, 4), "traffic": pmc_traffic(B, size),
+            "unit": "TFLOP/s", "frac": round(tflops / BF16_PEAK_TFLOPS, 4), "traffic": None,
             "avg_launch_ms": round(ms, 4), "algorithmic_flop_per_launch": flops,
-            "algorithmic_bytes_per_launch": B * H * H * 128 * 2 + 128 * 128 * 25 * 2 + B * OH * OH * 128 * 2}
+            "algorithmic_bytes_per_launch": B * H * W * C * 2 + N * C * k * k * 2 + B * OH * OW * N * 2}
 
 
 def pmc_traffic(B, size):
@@ -138,6 +149,8 @@ def cpu_baseline(model_name, quality, batch, size, seconds):
 
 def main():
     args = parse()
+    if args.batch is None:
+        args.batch = 2 if args.model == "multimodal" else 16
     from compressai.distributed import allreduce_mean_, broadcast_parameters_, init_from_env
     from compressai.losses import RateDistortionLoss
     from compressai.optim import configure_optimizers
@@ -152,18 +165,35 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     torch.manual_seed(0)
-    net = image_models[args.model](args.quality).to(dev).train()
+    multimodal = args.model == "multimodal"
+    gen = torch.Generator().manual_seed(1234 + rank)
+    if multimodal:
+        # train.py:208-246 / 379-382: IR master (channel 1, 512x640) guided by RGB (1024x1280);
+        # the Guided codec runs under no_grad in training mode, in fp32 like the reference
+        from compressai.models import Guided_compresser, Master_compresser
+
+        H, W = MM_IR
+        net = Master_compresser(width=H, height=W, channel=1).to(dev).train()
+        net_g = Guided_compresser(channel=3).to(dev).train()
+        broadcast_parameters_(net_g)
+        x = torch.rand(args.batch, 1, H, W, generator=gen).to(dev)
+        guide = torch.rand(args.batch, 3, 2 * H, 2 * W, generator=gen).to(dev)
+    else:
+        net = image_models[args.model](args.quality).to(dev).train()
+        x = torch.rand(args.batch, 3, args.size, args.size, generator=gen).to(dev)
     broadcast_parameters_(net)
     opt, aux_opt = configure_optimizers(net)
     criterion = RateDistortionLoss(args.quality)
-    x = torch.rand(args.batch, 3, args.size, args.size, generator=torch.Generator().manual_seed(1234 + rank)).to(dev)
     state = {}
 
     def fwd_bwd():
         opt.zero_grad()
         aux_opt.zero_grad()
+        if multimodal:
+            with torch.no_grad():
+                hidden = net_g(guide)["hidden"]
         with torch.autocast("cuda", dtype=torch.bfloat16):
-            out = net(x)
+            out = net(x, guide, hidden) if multimodal else net(x)
             crit = criterion(out, x)
         crit["loss"].backward()
         state["loss"] = crit["loss"].detach()
@@ -218,21 +248,31 @@ def main():
     if not math.isfinite(loss):
         raise RuntimeError(f"non-finite loss {loss}")
 
-    roof = dominant_kernel_roofline(args.batch, args.size) if rank == 0 else None
+    roof = None
+    if rank == 0:
+        # multimodal: Channel_aligner conv2 (256->256 k3 at 512x640), ~70 % of its FLOPs
+        roof = (conv_roofline(args.batch, 256, MM_IR[0], MM_IR[1], 256, 3, 1) if multimodal
+                else dominant_kernel_roofline(args.batch, args.size))
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+    if rank == 0 and world == 1 and args.cpu_seconds > 0 and not multimodal:
         cpu = cpu_baseline(args.model, args.quality, args.cpu_batch, args.size, args.cpu_seconds)
     if rank == 0:
         value = world * args.batch * args.steps / dt
+        unit = "IR+RGB pairs/s" if multimodal else "patches/s"
+        workload = ("multimodal paired codec: Master_compresser(IR 1x%dx%d) + Guided_compresser(RGB 3x%dx%d, "
+                    "no_grad fp32) RD-loss training step (fwd+bwd+clip+Adam+aux), HIP-graph replay"
+                    % (MM_IR[0], MM_IR[1], 2 * MM_IR[0], 2 * MM_IR[1]) if multimodal else
+                    f"{args.model} q{args.quality} RD-loss training step (fwd+bwd+clip+Adam+aux), HIP-graph replay")
         line = {
-            "metric": METRIC, "value": round(value, 3), "unit": "patches/s", "n_gpus": world,
+            "metric": METRIC, "value": round(value, 3), "unit": unit, "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-            "data": "synthetic U[0,1) 256x256 RGB patches, random-init weights",
-            "config": {"workload": f"{args.model} q{args.quality} RD-loss training step "
-                                   f"(fwd+bwd+clip+Adam+aux), HIP-graph replay",
+            "data": ("synthetic U[0,1) IR/RGB frame pairs, random-init weights" if multimodal else
+                     "synthetic U[0,1) 256x256 RGB patches, random-init weights"),
+            "config": {"workload": workload,
                        "model": args.model, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
-                       "seq_len": None, "patch": args.size, "parallelism": f"dp{world}"},
+                       "seq_len": None, "patch": list(MM_IR) if multimodal else args.size,
+                       "parallelism": f"dp{world}"},
             "final_loss": round(loss, 5),
             "roofline": roof, "cpu_baseline": cpu,
         }

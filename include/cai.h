@@ -226,10 +226,12 @@ int cai_window_attn_bwd(int dtype, const cai_window_attn* p, const void* dout, i
                         void* workspace, size_t ws_bytes, void* stream);
 
 /* Channel_aligner (master.py:179-210): out[b][c] = scale * sum_p x[b,p,c] (* x2[b,p,c])
- * (AdaptiveAvgPool2d(1) with scale = 1/HW; with x2, the gamma gradient);
+ * (AdaptiveAvgPool2d(1) with scale = 1/HW; with x2, the gamma gradient): pixel chunks in parallel, then
+ * a fixed-order sum of the chunk partials (workspace: cai_channel_mean_workspace_bytes);
  * y = gamma[b][c] * x + beta_scale * beta[b][c] (gamma / beta nullable). */
+size_t cai_channel_mean_workspace_bytes(int32_t B, int64_t HW, int32_t C);
 int cai_channel_mean(int dtype, const void* x, int32_t x_ld, const void* x2, int32_t x2_ld, int32_t B, int64_t HW,
-                     int32_t C, float* out, float scale, void* stream);
+                     int32_t C, float* out, float scale, void* workspace, size_t ws_bytes, void* stream);
 int cai_channel_affine(int dtype, const void* x, int32_t x_ld, const float* gamma, const float* beta, float beta_scale,
                        void* y, int32_t y_ld, int32_t B, int64_t HW, int32_t C, void* stream);
 
