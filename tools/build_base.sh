@@ -1,0 +1,14 @@
+#!/bin/bash
+# Build lib/libcai_base.so from the last commit (HEAD) for an A/B against the
+# working tree's lib/libcai.so (tools/gpu_ab.sh).  Uncommitted changes are
+# stashed around the build and restored.
+set -e
+cd "$(dirname "$0")/.."
+CSRC=165-learning-based-multi-modality-image-and-video-compression_amd/csrc
+LIB=165-learning-based-multi-modality-image-and-video-compression_amd/lib
+stashed=0
+if ! git diff --quiet -- $CSRC include; then git stash push -q -- $CSRC include; stashed=1; fi
+make -C $CSRC -j8 OUT=../lib/libcai_base.so BUILD=build_base > /tmp/build_base.log 2>&1 || { [ $stashed = 1 ] && git stash pop -q; exit 1; }
+if [ $stashed = 1 ]; then git stash pop -q; fi
+make -C $CSRC -j8 > /tmp/build_new.log 2>&1
+ls -la $LIB
