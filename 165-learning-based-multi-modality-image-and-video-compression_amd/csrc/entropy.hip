@@ -274,6 +274,27 @@ __device__ __forceinline__ float eb_chain_bwd(float x, float d, const float* t, 
     return 0.f;
 }
 
+// d input of one chain (no parameter gradients): the aux loss's quantiles grad
+__device__ __forceinline__ float eb_chain_dx(float d, const float* t, const EbTrace& tr) {
+    float dh[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) dh[k] = d * t[EB_SP + 30 + k];
+#pragma unroll
+    for (int l = 3; l >= 0; --l) {
+        float da[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const float th = tanhf(tr.a[l][j]);
+            da[j] = dh[j] * (1.f + t[EB_TF + l * 3 + j] * (1.f - th * th));
+        }
+        if (l == 0) return t[EB_SP + 0] * da[0] + t[EB_SP + 1] * da[1] + t[EB_SP + 2] * da[2];
+        const float* M = t + EB_SP + 3 + (l - 1) * 9;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) dh[k] = M[0 * 3 + k] * da[0] + M[1 * 3 + k] * da[1] + M[2 * 3 + k] * da[2];
+    }
+    return 0.f;
+}
+
 // fwd: block = 256 threads = 32 channels x 8 pixel rows
 __global__ __launch_bounds__(256) void eb_fwd_kernel(int mode, int64_t npix, int C, cai_eb_params P,
                                                       const void* __restrict__ x, int xdt, int xld,
@@ -356,43 +377,46 @@ __global__ __launch_bounds__(256) void eb_bwd_kernel(int mode, int64_t npix, int
         if (lane == 0) red[w][k] = v;
     }
     __syncthreads();
-    if (threadIdx.x != 0) return;
-#pragma unroll
-    for (int k = 0; k < EB_NP; ++k) g[k] = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
-#define EB_PUT(dst, val) ((dst) = G.accumulate ? (dst) + (val) : (val))
-    // softplus / tanh chain rule and scatter to torch layout (all indices
-    // compile-time after unrolling so g[] stays in registers)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) EB_PUT(G.matrix[0][c * 3 + k], g[EB_SP + k] * softplus_grad(P.matrix[0][c * 3 + k]));
-#pragma unroll
-    for (int l = 1; l < 4; ++l)
-#pragma unroll
-        for (int k = 0; k < 9; ++k)
-            EB_PUT(G.matrix[l][c * 9 + k], g[EB_SP + 3 + (l - 1) * 9 + k] * softplus_grad(P.matrix[l][c * 9 + k]));
-#pragma unroll
-    for (int k = 0; k < 3; ++k) EB_PUT(G.matrix[4][c * 3 + k], g[EB_SP + 30 + k] * softplus_grad(P.matrix[4][c * 3 + k]));
-#pragma unroll
-    for (int l = 0; l < 4; ++l)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) EB_PUT(G.bias[l][c * 3 + k], g[EB_B + l * 3 + k]);
-    EB_PUT(G.bias[4][c], g[EB_B + 12]);
-#pragma unroll
-    for (int l = 0; l < 4; ++l)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const float th = t[EB_TF + l * 3 + k];
-            EB_PUT(G.factor[l][c * 3 + k], g[EB_TF + l * 3 + k] * (1.f - th * th));
-        }
-    if (G.quantiles) {
-        EB_PUT(G.quantiles[c * 3 + 0], 0.f);
-        EB_PUT(G.quantiles[c * 3 + 1], (mode == CAI_Q_NOISE) ? 0.f : g[EB_MED]);
-        EB_PUT(G.quantiles[c * 3 + 2], 0.f);
+    // one thread per table element: chain rule through softplus / tanh and the
+    // store to torch layout (independent loads and stores across threads)
+    const int k = threadIdx.x;
+    if (k >= EB_NP || k == 59) return;
+    const float v = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
+    float* dst;
+    float val;
+    if (k < EB_B) {                                   // matrices: d softplus(raw) = sigmoid(raw)
+        const float* raw = eb_raw_ptr(c, k, P);
+        val = v * softplus_grad(*raw);
+        const int64_t off = raw - (k < 3 ? P.matrix[0] : (k < 12 ? P.matrix[1] : (k < 21 ? P.matrix[2] :
+                                   (k < 30 ? P.matrix[3] : P.matrix[4]))));
+        float* base = k < 3 ? G.matrix[0] : (k < 12 ? G.matrix[1] : (k < 21 ? G.matrix[2] :
+                      (k < 30 ? G.matrix[3] : G.matrix[4])));
+        dst = base + off;
+    } else if (k < EB_TF) {                           // biases
+        const int kb = k - EB_B;
+        const int l = kb / 3, j = kb - 3 * (kb / 3);
+        val = v;
+        dst = kb == 12 ? G.bias[4] + c
+                       : (l == 0 ? G.bias[0] : (l == 1 ? G.bias[1] : (l == 2 ? G.bias[2] : G.bias[3]))) + c * 3 + j;
+    } else if (k < EB_MED) {                          // factors: d tanh(raw) = 1 - tanh^2
+        const int kf = k - EB_TF;
+        const int l = kf / 3, j = kf - 3 * (kf / 3);
+        const float th = t[k];
+        val = v * (1.f - th * th);
+        dst = (l == 0 ? G.factor[0] : (l == 1 ? G.factor[1] : (l == 2 ? G.factor[2] : G.factor[3]))) + c * 3 + j;
+    } else {                                          // k == EB_MED: the medians (quantiles[:, :, 1])
+        if (!G.quantiles) return;
+        G.quantiles[c * 3 + 0] = G.accumulate ? G.quantiles[c * 3 + 0] : 0.f;
+        G.quantiles[c * 3 + 2] = G.accumulate ? G.quantiles[c * 3 + 2] : 0.f;
+        val = (mode == CAI_Q_NOISE) ? 0.f : v;
+        dst = G.quantiles + c * 3 + 1;
     }
+    *dst = G.accumulate ? *dst + val : val;
 }
 
-// aux loss: one block, deterministic.  Channels in chunks of 320: the chunk's
+// aux loss: one block, deterministic.  Channels in chunks of 128: the chunk's
 // tables are filled cooperatively into LDS, then one thread per (channel, k).
-constexpr int EB_AUX_CH = 320;   // every zoo EntropyBottleneck (C <= 320) in one pass
+constexpr int EB_AUX_CH = 128;   // PT = 8 loads per thread: no register spill at 1024 threads
 __global__ __launch_bounds__(1024) void eb_aux_kernel(int C, cai_eb_params P, const float* __restrict__ target,
                                                        float* __restrict__ loss, const float* __restrict__ gloss,
                                                        float* __restrict__ dq, int accumulate) {
@@ -414,11 +438,8 @@ __global__ __launch_bounds__(1024) void eb_aux_kernel(int C, cai_eb_params P, co
             const float diff = f - target[k];
             acc += fabsf(diff);
             if (dq) {
-                float gd[EB_NP];
-#pragma unroll
-                for (int j = 0; j < EB_NP; ++j) gd[j] = 0.f;
                 const float sg = (diff > 0.f) ? 1.f : ((diff < 0.f) ? -1.f : 0.f);
-                const float v = eb_chain_bwd(qv, gs * sg, t, tr, gd);
+                const float v = eb_chain_dx(gs * sg, t, tr);
                 dq[c * 3 + k] = accumulate ? dq[c * 3 + k] + v : v;
             }
         }
