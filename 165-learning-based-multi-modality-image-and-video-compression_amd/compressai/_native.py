@@ -38,6 +38,15 @@ class EbParams(Structure):
     _fields_ = [("matrix", c_void_p * 5), ("bias", c_void_p * 5), ("factor", c_void_p * 4), ("quantiles", c_void_p)]
 
 
+class RdInputs(Structure):
+    _fields_ = [("lik", c_void_p * 4), ("lik_n", c_int64 * 4), ("nlik", c_int32), ("x_hat", c_void_p),
+                ("target", c_void_p), ("n", c_int64)]
+
+
+class RdGrads(Structure):
+    _fields_ = [("dlik", c_void_p * 4)]
+
+
 class EbGrads(Structure):
     _fields_ = [("matrix", c_void_p * 5), ("bias", c_void_p * 5), ("factor", c_void_p * 4), ("quantiles", c_void_p),
                 ("accumulate", c_int32)]
@@ -103,6 +112,9 @@ SIGNATURES = {
     "cai_eb_bwd": (_I, [_I, _I64, c_int32, POINTER(EbParams), _P, _I, c_int32, _P, c_int32, _F, _P, c_int32, _P,
                         _I, c_int32, _P, c_int32, POINTER(EbGrads), _P]),
     "cai_eb_aux_loss": (_I, [c_int32, POINTER(EbParams), _P, _P, _P, _P, c_int32, _P]),
+    "cai_rd_loss_workspace_bytes": (_S, []),
+    "cai_rd_loss_fwd": (_I, [POINTER(RdInputs), _F, _F, _P, _P, _S, _P]),
+    "cai_rd_loss_bwd": (_I, [POINTER(RdInputs), _F, _F, _P, _P, _P, _P, POINTER(RdGrads), _P]),
     "cai_sum_log": (_I, [_P, _I64, c_int32, c_int32, _P, _P, _S, _P]),
     "cai_sum_sqdiff": (_I, [_P, _P, _I64, _P, _P, _S, _P]),
     "cai_reduce_workspace_bytes": (_S, [_I64]),
@@ -127,20 +139,25 @@ class _Lib:
                     " (there is no CPU fallback)")
             lib = ctypes.CDLL(LIB_PATH)
             for name, (res, args) in SIGNATURES.items():
-                fn = getattr(lib, name)
-                fn.restype = res
-                fn.argtypes = args
+                # an older library missing a newer entry point still serves the
+                # others (A/B benches); calling the missing one raises
+                fn = getattr(lib, name, None)
+                if fn is not None:
+                    fn.restype, fn.argtypes = res, args
             self._lib = lib
         return self._lib
 
+    def _bound(self, name):
+        return getattr(self.load(), name)
+
     def __getattr__(self, name):
-        fn = getattr(self.load(), name)
+        fn = self._bound(name)
 
         if fn.restype is c_int and name not in ("cai_version", "cai_abi_count"):
             def call(*args):
                 rc = fn(*args)
                 if rc != CAI_OK:
-                    msg = self.load().cai_last_error().decode(errors="replace")
+                    msg = self._bound("cai_last_error")().decode(errors="replace")
                     if rc in (CAI_EINVAL, CAI_EWORKSPACE):
                         raise ValueError(f"{name}: {msg}")
                     raise RuntimeError(f"{name}: {msg}")

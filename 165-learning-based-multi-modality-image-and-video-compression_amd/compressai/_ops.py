@@ -26,10 +26,11 @@ from typing import Optional, Sequence, Tuple
 import torch
 
 from ._native import (ACT_LEAKY, ACT_NONE, ACT_RELU, BF16, F32, MASK_LEAKY, MASK_NONE, MASK_POS, Q_DEQUANTIZE, Q_NOISE,
-                      ConvGeom, EbGrads, EbParams, lib)
+                      ConvGeom, EbGrads, EbParams, RdGrads, RdInputs, lib)
 
 _VP = ctypes.c_void_p
-_GDN_TWO_PASS = os.environ.get("CAI_GDN_TWO_PASS", "0") == "1"
+_GDN_TWO_PASS = os.environ.get("CAI_GDN_TWO_PASS", "0") == "1"   # A/B knobs (tools/gpu_ab.sh)
+_RD_UNFUSED = os.environ.get("CAI_RD_UNFUSED", "0") == "1"
 
 
 # ---------------------------------------------------------------------------
@@ -538,7 +539,9 @@ class BottleneckAuxFn(torch.autograd.Function):
 # rate-distortion loss (examples/train.py:68-82)
 # ---------------------------------------------------------------------------
 
-class RdLossFn(torch.autograd.Function):
+class RdLossFnUnfused(torch.autograd.Function):
+    """The per-tensor reduction path (cai_sum_log / cai_sum_sqdiff + torch scalar ops): A/B reference."""
+
     @staticmethod
     def forward(ctx, x_hat, target, lmbda: float, npix: int, *liks):
         _check_cuda(x_hat, target, *liks)
@@ -581,11 +584,74 @@ class RdLossFn(torch.autograd.Function):
         dliks = []
         for lr, (ld, lp, C), shp in zip(lrs, meta, lshapes):
             d, dbuf = empty_rows_like(shp, torch.float32, xh.device)
-            if ld != C:
-                raise ValueError("likelihood tensors must be dense pixel-major")
             lib.cai_log_bwd(_p(lr), lp, C, ld, _p(gbt), bpp_coef, _p(dbuf), st)
             dliks.append(d)
         return (dxh.view(xshape), None, None, None, *dliks)
+
+
+class RdLossFn(torch.autograd.Function):
+    """RateDistortionLoss (examples/train.py:68-82): forward in two launches (cai_rd_loss_fwd), backward in
+    one (cai_rd_loss_bwd); the upstream gradients stay on the device."""
+
+    @staticmethod
+    def forward(ctx, x_hat, target, lmbda: float, npix: int, *liks):
+        _check_cuda(x_hat, target, *liks)
+        if not 1 <= len(liks) <= 4:
+            raise ValueError("RD loss takes 1 to 4 likelihood tensors")
+        xh = x_hat.float().contiguous()
+        tg = target.float().contiguous()
+        if xh.shape != tg.shape:
+            raise ValueError(f"x_hat {tuple(xh.shape)} and target {tuple(tg.shape)} differ")
+        lbufs = []
+        for l in liks:
+            r, ld, lp, C = as_rows(l.float())
+            if ld != C:
+                r = r.contiguous() if r.is_contiguous() else l.float().contiguous()
+            lbufs.append(r)
+        bpp_coef = 1.0 / (-math.log(2) * npix)
+        desc = RdInputs()
+        for i, r in enumerate(lbufs):
+            desc.lik[i] = r.data_ptr()
+            desc.lik_n[i] = r.numel()
+        desc.nlik, desc.x_hat, desc.target, desc.n = len(lbufs), xh.data_ptr(), tg.data_ptr(), xh.numel()
+        out = torch.empty(3, dtype=torch.float32, device=xh.device)
+        ws = torch.empty(lib.cai_rd_loss_workspace_bytes(), dtype=torch.uint8, device=xh.device)
+        lib.cai_rd_loss_fwd(ctypes.byref(desc), float(lmbda), bpp_coef, _p(out), _p(ws), ws.numel(), _stream())
+        ctx.save_for_backward(xh, tg, *lbufs)
+        ctx.cfg = (float(lmbda), bpp_coef, [l.shape for l in liks], x_hat.shape)
+        return out[0], out[1], out[2]
+
+    @staticmethod
+    def backward(ctx, gl, gm, gb):
+        xh, tg, *lbufs = ctx.saved_tensors
+        lmbda, bpp_coef, lshapes, xshape = ctx.cfg
+        desc = RdInputs()
+        grads = RdGrads()
+        dliks = []
+        for i, (r, shp) in enumerate(zip(lbufs, lshapes)):
+            desc.lik[i] = r.data_ptr()
+            desc.lik_n[i] = r.numel()
+            d = torch.empty_like(r)
+            grads.dlik[i] = d.data_ptr()
+            dliks.append(d)
+        desc.nlik, desc.x_hat, desc.target, desc.n = len(lbufs), xh.data_ptr(), tg.data_ptr(), xh.numel()
+        dxh = torch.empty_like(xh)
+        g = [None if t is None else t.float().contiguous() for t in (gl, gm, gb)]
+        lib.cai_rd_loss_bwd(ctypes.byref(desc), lmbda, bpp_coef, _p(g[0]), _p(g[1]), _p(g[2]), _p(dxh),
+                            ctypes.byref(grads), _stream())
+        # each likelihood gradient in the layout of its buffer, viewed with the logical shape
+        outs = []
+        for d, r, shp in zip(dliks, lbufs, lshapes):
+            outs.append(_like_logical(d, r, shp))
+        return (dxh.view(xshape), None, None, None, *outs)
+
+
+def _like_logical(d: torch.Tensor, buf: torch.Tensor, shape) -> torch.Tensor:
+    """d has buf's memory layout; return it as a tensor of the likelihood's logical shape."""
+    if tuple(buf.shape) == tuple(shape):
+        return d.as_strided(buf.shape, buf.stride())
+    # as_rows moved the channel dim last: [B, *spatial, C] -> logical [B, C, *spatial]
+    return d.movedim(-1, 1)
 
 
 # ---------------------------------------------------------------------------

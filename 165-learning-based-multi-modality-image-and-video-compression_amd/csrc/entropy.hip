@@ -11,6 +11,8 @@
 // ptr[p*ld + c]; threads walk (p, c) in memory order so loads coalesce.
 #include "common.hpp"
 
+#include <algorithm>
+
 namespace cai {
 
 static constexpr float kNegInvSqrt2 = -0.70710678118654752440f;   // float(-(2**-0.5))
@@ -631,6 +633,70 @@ int cai_eb_aux_loss(int32_t C, const cai_eb_params* prm, const float* target, fl
     return CAI_OK;
 }
 
+
+// ---------------------------------------------------------------------------
+// RD loss in two launches (examples/train.py:68-82): stage 1 sums log(lik) of
+// every likelihood tensor and (x_hat - x)^2 as one grid (grid.y = segment),
+// stage 2 (one block) folds the per-block partials in a fixed order and
+// forms {loss, mse, bpp}.  The backward is one elementwise launch over all
+// segments with the upstream scalars read on the device.
+// ---------------------------------------------------------------------------
+constexpr int RD_BLOCKS = 256;
+
+__global__ __launch_bounds__(256) void rd_stage1(cai_rd_inputs in, float* __restrict__ part) {
+    __shared__ float red[4];
+    const int seg = blockIdx.y;
+    const bool sq = seg == in.nlik;
+    const float* a = sq ? in.x_hat : (seg == 0 ? in.lik[0] : (seg == 1 ? in.lik[1] : (seg == 2 ? in.lik[2] : in.lik[3])));
+    const int64_t n = sq ? in.n : (seg == 0 ? in.lik_n[0] : (seg == 1 ? in.lik_n[1] : (seg == 2 ? in.lik_n[2] : in.lik_n[3])));
+    float acc = 0.f;
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        if (sq) {
+            const float d = a[i] - in.target[i];
+            acc += d * d;
+        } else {
+            acc += logf(a[i]);
+        }
+    }
+    const float r = block_sum<256>(acc, red);
+    if (threadIdx.x == 0) part[seg * RD_BLOCKS + blockIdx.x] = r;
+}
+
+__global__ __launch_bounds__(256) void rd_stage2(const float* __restrict__ part, int nlik, float lmbda, float bpp_coef,
+                                                 float inv_n, float* __restrict__ out) {
+    __shared__ float red[4];
+    float bpp = 0.f, sse = 0.f;
+    for (int seg = 0; seg <= nlik; ++seg) {
+        const float v = block_sum<256>(part[seg * RD_BLOCKS + threadIdx.x], red);
+        if (seg < nlik) bpp += v; else sse = v;
+    }
+    if (threadIdx.x == 0) {
+        const float b = bpp * bpp_coef, m = sse * inv_n;
+        out[0] = lmbda * m + b;
+        out[1] = m;
+        out[2] = b;
+    }
+}
+
+__global__ __launch_bounds__(256) void rd_bwd_kernel(cai_rd_inputs in, float lmbda, float bpp_coef,
+                                                     const float* __restrict__ g_loss, const float* __restrict__ g_mse,
+                                                     const float* __restrict__ g_bpp, float* __restrict__ dxh,
+                                                     cai_rd_grads out) {
+    const int seg = blockIdx.y;
+    const float gl = g_loss ? *g_loss : 0.f;
+    if (seg == in.nlik) {   // d loss / d x_hat = (g_mse + lmbda g_loss) * 2 (x_hat - x) / n
+        const float k = ((g_mse ? *g_mse : 0.f) + lmbda * gl) * (2.f / (float)in.n);
+        for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < in.n; i += (int64_t)gridDim.x * 256)
+            dxh[i] = k * (in.x_hat[i] - in.target[i]);
+        return;
+    }
+    const float* l = seg == 0 ? in.lik[0] : (seg == 1 ? in.lik[1] : (seg == 2 ? in.lik[2] : in.lik[3]));
+    float* d = seg == 0 ? out.dlik[0] : (seg == 1 ? out.dlik[1] : (seg == 2 ? out.dlik[2] : out.dlik[3]));
+    const int64_t n = seg == 0 ? in.lik_n[0] : (seg == 1 ? in.lik_n[1] : (seg == 2 ? in.lik_n[2] : in.lik_n[3]));
+    const float k = ((g_bpp ? *g_bpp : 0.f) + gl) * bpp_coef;   // d bpp / d lik = coef / lik
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) d[i] = k / l[i];
+}
+
 size_t cai_reduce_workspace_bytes(int64_t n) { return (size_t)red_blocks(n) * sizeof(float); }
 
 int cai_sum_log(const float* lik, int64_t npix, int32_t C, int32_t ld, float* out, void* workspace, size_t ws_bytes,
@@ -679,6 +745,43 @@ int cai_cast(const void* x, int x_dtype, void* y, int y_dtype, int64_t n, void* 
     if (n == 0) return CAI_OK;
     hipLaunchKernelGGL(cast_kernel, dim3(ew_grid(n)), dim3(256), 0, as_stream(stream), x, x_dtype, y, y_dtype, n);
     CAI_LAUNCH_CHECK("cast");
+    return CAI_OK;
+}
+
+
+static int check_rd(const cai_rd_inputs* in) {
+    CAI_CHECK_ARG(in && in->nlik >= 1 && in->nlik <= 4 && in->x_hat && in->target && in->n > 0, "rd_loss: bad inputs");
+    for (int i = 0; i < in->nlik; ++i) CAI_CHECK_ARG(in->lik[i] && in->lik_n[i] > 0, "rd_loss: bad likelihood %d", i);
+    return CAI_OK;
+}
+
+size_t cai_rd_loss_workspace_bytes(void) { return (size_t)5 * RD_BLOCKS * sizeof(float); }
+
+int cai_rd_loss_fwd(const cai_rd_inputs* in, float lmbda, float bpp_coef, float* out, void* workspace,
+                    size_t ws_bytes, void* stream) {
+    int rc = check_rd(in);
+    if (rc) return rc;
+    CAI_CHECK_ARG(out && workspace && ws_bytes >= cai_rd_loss_workspace_bytes(), "rd_loss_fwd: bad output/workspace");
+    float* part = reinterpret_cast<float*>(workspace);
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(rd_stage1, dim3(RD_BLOCKS, in->nlik + 1), dim3(256), 0, st, *in, part);
+    hipLaunchKernelGGL(rd_stage2, dim3(1), dim3(256), 0, st, part, in->nlik, lmbda, bpp_coef, 1.f / (float)in->n, out);
+    CAI_LAUNCH_CHECK("rd_loss_fwd");
+    return CAI_OK;
+}
+
+int cai_rd_loss_bwd(const cai_rd_inputs* in, float lmbda, float bpp_coef, const float* g_loss, const float* g_mse,
+                    const float* g_bpp, float* dx_hat, const cai_rd_grads* grads, void* stream) {
+    int rc = check_rd(in);
+    if (rc) return rc;
+    CAI_CHECK_ARG(dx_hat && grads, "rd_loss_bwd: null output");
+    for (int i = 0; i < in->nlik; ++i) CAI_CHECK_ARG(grads->dlik[i], "rd_loss_bwd: null dlik[%d]", i);
+    int64_t mx = in->n;
+    for (int i = 0; i < in->nlik; ++i) mx = std::max(mx, in->lik_n[i]);
+    const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, (mx + 255) / 256));
+    hipLaunchKernelGGL(rd_bwd_kernel, dim3(gx, in->nlik + 1), dim3(256), 0, as_stream(stream), *in, lmbda, bpp_coef,
+                       g_loss, g_mse, g_bpp, dx_hat, *grads);
+    CAI_LAUNCH_CHECK("rd_loss_bwd");
     return CAI_OK;
 }
 

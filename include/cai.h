@@ -340,6 +340,28 @@ int cai_eb_aux_loss(int32_t C, const cai_eb_params* prm, const float* target,
 /* =======================================================================
  * Rate-distortion loss reductions (examples/train.py:68-82).
  * ======================================================================= */
+/* The whole RD loss in two launches: out[3] = {loss, mse, bpp} with
+ * bpp = bpp_coef * sum_k sum(log lik_k), mse = mean((x_hat - target)^2),
+ * loss = lmbda * mse + bpp (fixed-order reductions).  Tensors are dense fp32
+ * (likelihoods in any layout: the sums are order-independent per element). */
+typedef struct cai_rd_inputs {
+    const float* lik[4];
+    int64_t lik_n[4];
+    int32_t nlik;
+    const float* x_hat;
+    const float* target;
+    int64_t n;
+} cai_rd_inputs;
+typedef struct cai_rd_grads {
+    float* dlik[4];
+} cai_rd_grads;
+size_t cai_rd_loss_workspace_bytes(void);
+int cai_rd_loss_fwd(const cai_rd_inputs* in, float lmbda, float bpp_coef, float* out, void* workspace,
+                    size_t ws_bytes, void* stream);
+/* one launch: dx_hat = (g_mse + lmbda g_loss) 2 (x_hat - target) / n, dlik_k = (g_bpp + g_loss) bpp_coef / lik_k;
+ * the upstream gradients are device scalars (nullable = 0). */
+int cai_rd_loss_bwd(const cai_rd_inputs* in, float lmbda, float bpp_coef, const float* g_loss, const float* g_mse,
+                    const float* g_bpp, float* dx_hat, const cai_rd_grads* grads, void* stream);
 /* out[0] += sum(log(lik)) over n elements (fp32, contiguous or strided by ld over C). */
 int cai_sum_log(const float* lik, int64_t npix, int32_t C, int32_t ld, float* out, void* workspace,
                 size_t ws_bytes, void* stream);
