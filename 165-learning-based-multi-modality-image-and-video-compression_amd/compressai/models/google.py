@@ -241,65 +241,56 @@ class MeanScaleHyperprior(ScaleHyperprior):
         return {"x_hat": x_hat}
 
 
-class JointAutoregressiveHierarchicalPriors(MeanScaleHyperprior):
-    def __init__(self, N=192, M=192, channel=3, **kwargs):
-        super().__init__(N=N, M=M, channel=channel, **kwargs)
-        self.entropy_parameters = Sequential(
-            Conv2d(M * 12 // 3, M * 10 // 3, 1), nn.LeakyReLU(inplace=True),
-            Conv2d(M * 10 // 3, M * 8 // 3, 1), nn.LeakyReLU(inplace=True),
-            Conv2d(M * 8 // 3, M * 6 // 3, 1))
-        self.context_prediction = MaskedConv2d(M, 2 * M, kernel_size=5, padding=2, stride=1)
-
-    def forward(self, x):
-        y = self.g_a(x)
-        z = self.h_a(y)
-        z_hat, z_likelihoods = self.entropy_bottleneck(z)
-        params = self.h_s(z_hat)
-        y_hat = self.gaussian_conditional.quantize(y, "noise" if self.training else "dequantize")
-        ctx_params = self.context_prediction(y_hat)
-        gaussian_params = self.entropy_parameters(torch.cat((params, ctx_params), dim=1))
-        scales_hat, means_hat = gaussian_params.chunk(2, 1)
-        _, y_likelihoods = self.gaussian_conditional(y, scales_hat, means=means_hat)
-        x_hat = self.g_s(y_hat)
-        return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods, "z": z_likelihoods}}
-
-    # ---- serial autoregressive coding (google.py:526-692) -------------------
+class _ARCoding:
+    """Serial autoregressive entropy coding of the context models (google.py:565-608, 654-692), shared by
+    JointAutoregressiveHierarchicalPriors and the multi-modal Guided / Master codecs (master.py:993-1147,
+    1337-1464): per latent pixel, the masked 5x5 context conv (valid, on a crop) and the 1x1
+    entropy-parameter stack run on the HIP kernels, fp32, so encoder and decoder agree exactly."""
 
     _AR_SPEC = None
 
     def _ar_params(self, y_crop, p):
         """Entropy parameters of the centre pixel of a 5x5 crop: masked context conv
         (valid, no padding) + the 1x1 stack (google.py:580-592 / 671-681)."""
-        if JointAutoregressiveHierarchicalPriors._AR_SPEC is None:
-            JointAutoregressiveHierarchicalPriors._AR_SPEC = ConvSpec(5, 1, 0)
+        if _ARCoding._AR_SPEC is None:
+            _ARCoding._AR_SPEC = ConvSpec(5, 1, 0)
         cp = self.context_prediction
-        ctx_p = ConvFn.apply(y_crop, cp.weight, cp.bias, JointAutoregressiveHierarchicalPriors._AR_SPEC)
+        ctx_p = ConvFn.apply(y_crop, cp.weight, cp.bias, _ARCoding._AR_SPEC)
         return self.entropy_parameters(CatFn.apply(p, ctx_p)).chunk(2, 1)
 
     def _gc_tables(self):
         gc = self.gaussian_conditional
         return gc._quantized_cdf.tolist(), gc._cdf_length.tolist(), gc._offset.tolist()
 
-    @torch.no_grad()
-    def compress(self, x):
-        if next(self.parameters()).device != torch.device("cpu"):
+    @staticmethod
+    def _warn_gpu(model):
+        if next(model.parameters()).device != torch.device("cpu"):
             warnings.warn("Inference on GPU is not recommended for the autoregressive models (the entropy coder is "
                           "run sequentially on CPU).")
+
+    def _ar_encode_all(self, y, params):
+        """y_strings of a batch (google.py:542-561)."""
         cp = self.context_prediction
         cp.weight.data *= cp.mask          # MaskedConv2d semantics (layers.py:75-78)
-        with prepacked_forward(self):
-            y = self.g_a(x)
-            z = self.h_a(y)
-            z_strings = self.entropy_bottleneck.compress(z)
-            z_hat = self.entropy_bottleneck.decompress(z_strings, z.size()[-2:])
-            params = self.h_s(z_hat)
-            s, kernel_size = 4, 5
-            padding = (kernel_size - 1) // 2
-            y_height, y_width = z_hat.size(2) * s, z_hat.size(3) * s
-            y_hat = F.pad(y.float(), (padding, padding, padding, padding))
-            y_strings = [self._compress_ar(y_hat[i:i + 1], params[i:i + 1], y_height, y_width, kernel_size, padding)
-                         for i in range(y.size(0))]
-        return {"strings": [y_strings, z_strings], "shape": z.size()[-2:]}
+        kernel_size = 5
+        padding = (kernel_size - 1) // 2
+        y_height, y_width = params.size(2), params.size(3)
+        y_hat = F.pad(y.float(), (padding, padding, padding, padding))
+        return [self._compress_ar(y_hat[i:i + 1], params[i:i + 1], y_height, y_width, kernel_size, padding)
+                for i in range(y.size(0))]
+
+    def _ar_decode_all(self, y_strings, params):
+        """y_hat of a batch (google.py:622-650)."""
+        cp = self.context_prediction
+        cp.weight.data *= cp.mask
+        kernel_size = 5
+        padding = (kernel_size - 1) // 2
+        y_height, y_width = params.size(2), params.size(3)
+        y_hat = torch.zeros((params.size(0), self.M, y_height + 2 * padding, y_width + 2 * padding),
+                            device=params.device)
+        for i, y_string in enumerate(y_strings):
+            self._decompress_ar(y_string, y_hat[i:i + 1], params[i:i + 1], y_height, y_width, kernel_size, padding)
+        return F.pad(y_hat, (-padding, -padding, -padding, -padding))
 
     def _compress_ar(self, y_hat, params, height, width, kernel_size, padding):
         """google.py:565-608."""
@@ -321,28 +312,6 @@ class JointAutoregressiveHierarchicalPriors(MeanScaleHyperprior):
         encoder.encode_with_indexes(symbols_list, indexes_list, cdf, cdf_lengths, offsets)
         return encoder.flush()
 
-    @torch.no_grad()
-    def decompress(self, strings, shape):
-        assert isinstance(strings, list) and len(strings) == 2
-        if next(self.parameters()).device != torch.device("cpu"):
-            warnings.warn("Inference on GPU is not recommended for the autoregressive models (the entropy coder is "
-                          "run sequentially on CPU).")
-        cp = self.context_prediction
-        cp.weight.data *= cp.mask
-        with prepacked_forward(self):
-            z_hat = self.entropy_bottleneck.decompress(strings[1], shape)
-            params = self.h_s(z_hat)
-            s, kernel_size = 4, 5
-            padding = (kernel_size - 1) // 2
-            y_height, y_width = z_hat.size(2) * s, z_hat.size(3) * s
-            y_hat = torch.zeros((z_hat.size(0), self.M, y_height + 2 * padding, y_width + 2 * padding),
-                                device=z_hat.device)
-            for i, y_string in enumerate(strings[0]):
-                self._decompress_ar(y_string, y_hat[i:i + 1], params[i:i + 1], y_height, y_width, kernel_size, padding)
-            y_hat = F.pad(y_hat, (-padding, -padding, -padding, -padding))
-            x_hat = self.g_s(y_hat).clamp_(0, 1)
-        return {"x_hat": x_hat}
-
     def _decompress_ar(self, y_string, y_hat, params, height, width, kernel_size, padding):
         """google.py:654-692."""
         cdf, cdf_lengths, offsets = self._gc_tables()
@@ -359,3 +328,51 @@ class JointAutoregressiveHierarchicalPriors(MeanScaleHyperprior):
                 rv = torch.tensor(rv, dtype=torch.float32, device=y_hat.device).reshape(1, -1, 1, 1)
                 rv = gc.dequantize(rv, means_hat.float())
                 y_hat[:, :, h + padding:h + padding + 1, w + padding:w + padding + 1] = rv
+
+
+class JointAutoregressiveHierarchicalPriors(_ARCoding, MeanScaleHyperprior):
+    def __init__(self, N=192, M=192, channel=3, **kwargs):
+        super().__init__(N=N, M=M, channel=channel, **kwargs)
+        self.entropy_parameters = Sequential(
+            Conv2d(M * 12 // 3, M * 10 // 3, 1), nn.LeakyReLU(inplace=True),
+            Conv2d(M * 10 // 3, M * 8 // 3, 1), nn.LeakyReLU(inplace=True),
+            Conv2d(M * 8 // 3, M * 6 // 3, 1))
+        self.context_prediction = MaskedConv2d(M, 2 * M, kernel_size=5, padding=2, stride=1)
+
+    def forward(self, x):
+        y = self.g_a(x)
+        z = self.h_a(y)
+        z_hat, z_likelihoods = self.entropy_bottleneck(z)
+        params = self.h_s(z_hat)
+        y_hat = self.gaussian_conditional.quantize(y, "noise" if self.training else "dequantize")
+        ctx_params = self.context_prediction(y_hat)
+        gaussian_params = self.entropy_parameters(torch.cat((params, ctx_params), dim=1))
+        scales_hat, means_hat = gaussian_params.chunk(2, 1)
+        _, y_likelihoods = self.gaussian_conditional(y, scales_hat, means=means_hat)
+        x_hat = self.g_s(y_hat)
+        return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods, "z": z_likelihoods}}
+
+    @torch.no_grad()
+    def compress(self, x):
+        """google.py:526-563."""
+        self._warn_gpu(self)
+        with prepacked_forward(self):
+            y = self.g_a(x)
+            z = self.h_a(y)
+            z_strings = self.entropy_bottleneck.compress(z)
+            z_hat = self.entropy_bottleneck.decompress(z_strings, z.size()[-2:])
+            params = self.h_s(z_hat)
+            y_strings = self._ar_encode_all(y, params)
+        return {"strings": [y_strings, z_strings], "shape": z.size()[-2:]}
+
+    @torch.no_grad()
+    def decompress(self, strings, shape):
+        """google.py:610-652."""
+        assert isinstance(strings, list) and len(strings) == 2
+        self._warn_gpu(self)
+        with prepacked_forward(self):
+            z_hat = self.entropy_bottleneck.decompress(strings[1], shape)
+            params = self.h_s(z_hat)
+            y_hat = self._ar_decode_all(strings[0], params)
+            x_hat = self.g_s(y_hat).clamp_(0, 1)
+        return {"x_hat": x_hat}

@@ -24,7 +24,8 @@ from .._ops import (AddActFn, CatFn, ChannelAffineFn, ChannelMeanFn, ConvFn, Con
 from ..entropy_models import GaussianConditional
 from ..layers import GDN, MaskedConv2d, ResidualBlock, Sequential
 from ..layers.conv import Conv2d, ConvTranspose2d
-from .google import MeanScaleHyperprior
+from .._prepack import prepacked_forward
+from .google import MeanScaleHyperprior, _ARCoding
 
 __all__ = ["Master_compresser", "Guided_compresser", "Spatial_aligner", "Channel_aligner", "SwinTransformerBlock",
            "WindowAttention", "Feature_encoder", "Feature_decoder", "Master_decoder", "Encoder1", "Decoder1"]
@@ -373,7 +374,7 @@ def _entropy(model, y):
     return y_hat, y_lik, z_lik
 
 
-class Master_compresser(MeanScaleHyperprior):
+class Master_compresser(_ARCoding, MeanScaleHyperprior):
     """master.py:837-951: net(x, guided_hat, guided_hidden) -> {"x_hat", "likelihoods"}."""
 
     def __init__(self, width=256, height=256, channel=3, N=192, M=192):
@@ -399,6 +400,36 @@ class Master_compresser(MeanScaleHyperprior):
         res = self.decoder(y_hat, guided_hidden)
         out = self.fdecoder(CatFn.apply(res["x_feature_hat"], guided_align))
         return {"x_hat": out, "likelihoods": {"y": y_lik, "z": z_lik}}
+
+    @torch.no_grad()
+    def compress(self, x, guided_hat):
+        """master.py:953-991: the channel-aligner's beta / gamma travel as side information."""
+        with prepacked_forward(self):
+            x_feature = self.fencoder1(x)
+            guided_feature = self.fencoder2(guided_hat)
+            guided_align, beta, gamma = self.ch_aligner(x_feature, guided_feature)
+            y = self.g_a(CatFn.apply(x_feature, guided_align))
+            z = self.h_a(y)
+            z_strings = self.entropy_bottleneck.compress(z)
+            z_hat = self.entropy_bottleneck.decompress(z_strings, z.size()[-2:])
+            params = self.h_s(z_hat)
+            y_strings = self._ar_encode_all(y, params)
+        return {"strings": [y_strings, z_strings], "shape": z.size()[-2:], "gamma": gamma, "beta": beta}
+
+    @torch.no_grad()
+    def decompress(self, out_net, out_net_guided):
+        """master.py:1054-1107: the guide's decoded image and synthesis activations condition the decoder."""
+        strings, shape, beta, gamma = out_net["strings"], out_net["shape"], out_net["beta"], out_net["gamma"]
+        assert isinstance(strings, list) and len(strings) == 2
+        self._warn_gpu(self)
+        with prepacked_forward(self):
+            guided_align = ChannelAffineFn.apply(self.fencoder2(out_net_guided["x_hat"]), gamma, beta)
+            z_hat = self.entropy_bottleneck.decompress(strings[1], shape)
+            params = self.h_s(z_hat)
+            y_hat = self._ar_decode_all(strings[0], params)
+            res = self.decoder(y_hat, out_net_guided["hidden"])
+            x_hat = self.fdecoder(CatFn.apply(res["x_feature_hat"], guided_align)).clamp_(0, 1)
+        return {"x_hat": x_hat}
 
 
 class Encoder1(nn.Module):
@@ -441,7 +472,7 @@ class Decoder1(nn.Module):
         return self.g_s_conv4(g3), g1, g2, g3
 
 
-class Guided_compresser(MeanScaleHyperprior):
+class Guided_compresser(_ARCoding, MeanScaleHyperprior):
     """master.py:1215-1295: net(x) -> {"x_hat", "likelihoods", "hidden": {ga1..3, gs1..3}}."""
 
     def __init__(self, N=192, M=192, channel=1, first_stride=2, **kwargs):
@@ -461,3 +492,29 @@ class Guided_compresser(MeanScaleHyperprior):
         x1_hat, gs1, gs2, gs3 = self.dec1(y1_hat)
         return {"x_hat": x1_hat, "likelihoods": {"y": y_lik, "z": z_lik},
                 "hidden": {"ga1": ga1, "ga2": ga2, "ga3": ga3, "gs1": gs1, "gs2": gs2, "gs3": gs3}}
+
+    @torch.no_grad()
+    def compress(self, x):
+        """master.py:1297-1335."""
+        self._warn_gpu(self)
+        with prepacked_forward(self):
+            y, ga1, ga2, ga3 = self.enc1(x)
+            z = self.h_a(y)
+            z_strings = self.entropy_bottleneck.compress(z)
+            z_hat = self.entropy_bottleneck.decompress(z_strings, z.size()[-2:])
+            params = self.h_s(z_hat)
+            y_strings = self._ar_encode_all(y, params)
+        return {"strings": [y_strings, z_strings], "shape": z.size()[-2:],
+                "hidden": {"ga1": ga1, "ga2": ga2, "ga3": ga3}}
+
+    @torch.no_grad()
+    def decompress(self, strings, shape):
+        """master.py:1381-1424: the reconstruction and the synthesis activations the Master codec needs."""
+        assert isinstance(strings, list) and len(strings) == 2
+        self._warn_gpu(self)
+        with prepacked_forward(self):
+            z_hat = self.entropy_bottleneck.decompress(strings[1], shape)
+            params = self.h_s(z_hat)
+            y_hat = self._ar_decode_all(strings[0], params)
+            x_hat, gs1, gs2, gs3 = self.dec1(y_hat)
+        return {"x_hat": x_hat.clamp(0, 1), "hidden": {"gs1": gs1, "gs2": gs2, "gs3": gs3}}

@@ -150,6 +150,31 @@ def inference_entropy_estimation_rgbt(model, model_guided, x: torch.Tensor, guid
             "encoding_time": elapsed / 2.0, "decoding_time": elapsed / 2.0}
 
 
+@torch.no_grad()
+def inference_rgbt(model, model_guided, x: torch.Tensor, guided: torch.Tensor) -> Dict[str, float]:
+    """Paired real coding (__main__rgbt.py:99-150): the guide is coded first; the Master codec is
+    conditioned on the decoded guide.  bpp counts the master's strings plus its 64 beta + 64 gamma
+    fp32 side values (:142)."""
+    if x.dim() == 3:
+        x, guided = x.unsqueeze(0), guided.unsqueeze(0)
+    _sync(x)
+    start = time.time()
+    out_net_r = model_guided.compress(guided)
+    out_dec_r = model_guided.decompress(out_net_r["strings"], out_net_r["shape"])
+    out_net = model.compress(x, out_dec_r["x_hat"])
+    _sync(x)
+    enc_time = time.time() - start
+    start = time.time()
+    out_dec = model.decompress(out_net, out_dec_r)
+    _sync(x)
+    dec_time = time.time() - start
+    num_pixels = x.size(0) * x.size(2) * x.size(3)
+    bpp = (sum(len(s[0]) for s in out_net["strings"]) * 8.0 + 64 * 2 * 4 * 8) / num_pixels
+    msssim = ms_ssim(x, out_dec["x_hat"], data_range=1.0).item() if min(x.shape[-2:]) > 160 else float("nan")
+    return {"psnr": psnr(x, out_dec["x_hat"]), "ms-ssim": msssim, "bpp": bpp, "encoding_time": enc_time,
+            "decoding_time": dec_time}
+
+
 def _state_dict_from(path: str) -> Dict[str, torch.Tensor]:
     ckpt = torch.load(path, map_location="cpu", weights_only=True)
     if isinstance(ckpt, dict) and "state_dict" in ckpt:
@@ -187,13 +212,15 @@ def eval_model(model, filepaths, entropy_estimation=True, half=False) -> Dict[st
     return {k: v / len(filepaths) for k, v in metrics.items()}
 
 
-def eval_model_rgbt(model, model_guided, pairs, half=False) -> Dict[str, float]:
-    """__main__rgbt.py:193-219 (entropy estimation)."""
+def eval_model_rgbt(model, model_guided, pairs, entropy_estimation=True, half=False) -> Dict[str, float]:
+    """__main__rgbt.py:193-219."""
     device = next(model.parameters()).device
     metrics = defaultdict(float)
     for fx, fg in pairs:
         x, g = read_image(fx).to(device), read_image(fg).to(device)
-        for k, v in inference_entropy_estimation_rgbt(model, model_guided, x, g, half).items():
+        rv = (inference_entropy_estimation_rgbt(model, model_guided, x, g, half) if entropy_estimation
+              else inference_rgbt(model, model_guided, x, g))
+        for k, v in rv.items():
             metrics[k] += v
     return {k: v / len(pairs) for k, v in metrics.items()}
 
@@ -255,7 +282,11 @@ def main(argv):
             model = load_checkpoint(args.architecture, run, args.channel, width=w, height=h).to(device)
             gch = args.guided_channel or (3 if args.channel == 1 else 1)
             model_g = load_checkpoint("Guided_compresser", args.guided_checkpoint, gch).to(device)
-            metrics = eval_model_rgbt(model, model_g, list(zip(filepaths, gfiles)), args.half)
+            if not args.entropy_estimation:
+                model.update()
+                model_g.update()
+            metrics = eval_model_rgbt(model, model_g, list(zip(filepaths, gfiles)), args.entropy_estimation,
+                                      args.half)
         else:
             model = load_checkpoint(args.architecture, run, args.channel).to(device)
             if not args.entropy_estimation:
@@ -265,7 +296,7 @@ def main(argv):
             results[k].append(v)
     if args.verbose:
         sys.stderr.write("\n")
-    description = "entropy estimation" if (args.entropy_estimation or paired) else args.entropy_coder
+    description = "entropy estimation" if args.entropy_estimation else args.entropy_coder
     output = {"name": args.architecture, "description": f"Inference ({description})", "results": results}
     if args.output:
         with open(args.output, "a") as f:

@@ -162,3 +162,44 @@ def test_autoregressive_round_trip(cuda):
         y_dec = torch.zeros_like(y_enc)
         net._decompress_ar(s, y_dec, params, H, W, 5, 2)
     assert torch.equal(y_enc[:, :, 2:-2, 2:-2], y_dec[:, :, 2:-2, 2:-2])
+
+
+def test_multimodal_round_trip(cuda):
+    """Guided_compresser / Master_compresser compress -> decompress (master.py:953-1147, 1297-1464): the
+    decoder rebuilds exactly the encoder-side reconstruction (same y_hat, same aligned guide)."""
+    import torch.nn.functional as F
+
+    from compressai._ops import CatFn, ChannelAffineFn
+    from compressai._prepack import prepacked_forward
+    from compressai.models import Guided_compresser, Master_compresser
+
+    torch.manual_seed(7)
+    g = Guided_compresser(channel=3).to(cuda).eval()
+    m = Master_compresser(width=64, height=64, channel=1).to(cuda).eval()
+    g.update()
+    m.update()
+    x = torch.rand(1, 1, 64, 64, generator=torch.Generator().manual_seed(8)).to(cuda)
+    rgb = torch.rand(1, 3, 128, 128, generator=torch.Generator().manual_seed(9)).to(cuda)
+    with pytest.warns(UserWarning):
+        enc_g = g.compress(rgb)
+    with pytest.warns(UserWarning):
+        dec_g = g.decompress(enc_g["strings"], enc_g["shape"])
+    assert dec_g["x_hat"].shape == rgb.shape and set(dec_g["hidden"]) == {"gs1", "gs2", "gs3"}
+    enc_m = m.compress(x, dec_g["x_hat"])
+    assert enc_m["gamma"].shape == (1, 64, 1, 1) and enc_m["beta"].shape == (1, 64, 1, 1)
+    with pytest.warns(UserWarning):
+        dec_m = m.decompress(enc_m, dec_g)
+    # encoder-side reconstruction
+    with torch.no_grad(), prepacked_forward(m):
+        xf = m.fencoder1(x)
+        ga, beta, gamma = m.ch_aligner(xf, m.fencoder2(dec_g["x_hat"]))
+        y = m.g_a(CatFn.apply(xf, ga))
+        z_hat = m.entropy_bottleneck.decompress(enc_m["strings"][1], enc_m["shape"])
+        params = m.h_s(z_hat)
+        y_enc = F.pad(y.float(), (2, 2, 2, 2))
+        s = m._compress_ar(y_enc, params, y.shape[2], y.shape[3], 5, 2)
+        assert s == enc_m["strings"][0][0]
+        res = m.decoder(y_enc[:, :, 2:-2, 2:-2].contiguous(), dec_g["hidden"])
+        ga2 = ChannelAffineFn.apply(m.fencoder2(dec_g["x_hat"]), gamma, beta)
+        x_rec = m.fdecoder(CatFn.apply(res["x_feature_hat"], ga2)).clamp_(0, 1)
+    assert torch.equal(dec_m["x_hat"], x_rec)

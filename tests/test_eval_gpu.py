@@ -83,3 +83,31 @@ def test_real_coding_rate_tracks_estimate(cuda, tmp_path):
     # strings carry a few bytes of rANS state per image and model: 0.9x .. 1.1x + overhead
     assert 0.9 * e["bpp"][0] <= r["bpp"][0] <= 1.1 * e["bpp"][0] + 0.05, (r["bpp"], e["bpp"])
     assert 0.0 < r["ms-ssim"][0] <= 1.0
+
+
+def test_paired_eval_real_coding(cuda, tmp_path):
+    """Paired (IR master + RGB guide) evaluation, __main__rgbt.py:99-178: real coding's rate tracks the
+    entropy estimate plus the 64 beta + 64 gamma fp32 side values (:142); PSNR of real coding equals the
+    estimate's within quantization-of-means noise."""
+    from PIL import Image
+
+    from compressai.models import Guided_compresser, Master_compresser
+    from compressai.utils.eval_model.__main__ import main
+
+    torch.manual_seed(2)
+    m, g = Master_compresser(width=64, height=64, channel=1), Guided_compresser(channel=3)
+    torch.save(m.state_dict(), tmp_path / "m.pth")
+    torch.save(g.state_dict(), tmp_path / "g.pth")
+    _, rgb_paths = _write_images(tmp_path, [(128, 128), (128, 128)], seed=3)
+    ird = tmp_path / "ir"
+    ird.mkdir()
+    for i, p in enumerate(rgb_paths):
+        Image.open(p).convert("L").resize((64, 64)).save(ird / f"ir{i}.png")
+    args = ["checkpoint", str(ird), "-a", "Master_compresser", "-p", str(tmp_path / "m.pth"), "-ch", "1",
+            "--guided-dataset", str(tmp_path / "imgs"), "--guided-checkpoint", str(tmp_path / "g.pth"), "--cuda"]
+    est = main(args + ["--entropy-estimation"])["results"]
+    with pytest.warns(UserWarning):
+        real = main(args)["results"]
+    side = 64 * 2 * 4 * 8 / (64 * 64)
+    assert 0.9 * est["bpp"][0] + side <= real["bpp"][0] <= 1.1 * est["bpp"][0] + side + 0.05, (real, est)
+    assert math.isfinite(real["psnr"][0]) and real["encoding_time"][0] > 0
