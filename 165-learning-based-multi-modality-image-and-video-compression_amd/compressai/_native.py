@@ -75,6 +75,12 @@ SIGNATURES = {
     "cai_deconv_small_workspace_bytes": (_S, [_G, _I]),
     "cai_deconv_small_fwd": (_I, [_G, _I, _P, c_int32, _P, _P, _P, _P, _S, _P]),
     "cai_deconv_small_bwd": (_I, [_G, _I, _P, c_int32, _P, _P, _P, c_int32, _P, _P, c_int32, _P, _S, _P]),
+    "cai_edge_supported": (_I, [_G, _I]),
+    "cai_edge_workspace_bytes": (_S, [_G, _I]),
+    "cai_edge_conv_fwd": (_I, [_G, _P, _P, _P, _P, c_int32, _P]),
+    "cai_edge_deconv_fwd": (_I, [_G, _P, c_int32, _P, _P, _P, _P]),
+    "cai_edge_deconv_dgrad": (_I, [_G, _P, _P, _P, c_int32, _P]),
+    "cai_edge_wgrad": (_I, [_G, _P, _P, c_int32, _P, _P, c_int32, _P, _S, _P]),
     "cai_add_act": (_I, [_I, _P, c_int32, _P, c_int32, _P, c_int32, _I64, c_int32, c_int32, _F, _P]),
     "cai_act": (_I, [_I, _P, c_int32, _P, c_int32, _I64, c_int32, c_int32, _F, _P]),
     "cai_gate_fwd": (_I, [_I, _P, _P, _P, _P, c_int32, _I64, c_int32, _P]),
@@ -153,7 +159,7 @@ class _Lib:
     def __getattr__(self, name):
         fn = self._bound(name)
 
-        if fn.restype is c_int and name not in ("cai_version", "cai_abi_count"):
+        if fn.restype is c_int and name not in ("cai_version", "cai_abi_count", "cai_edge_supported"):
             def call(*args):
                 rc = fn(*args)
                 if rc != CAI_OK:

@@ -31,6 +31,7 @@ from ._native import (ACT_LEAKY, ACT_NONE, ACT_RELU, BF16, F32, MASK_LEAKY, MASK
 _VP = ctypes.c_void_p
 _GDN_TWO_PASS = os.environ.get("CAI_GDN_TWO_PASS", "0") == "1"   # A/B knobs (tools/gpu_ab.sh)
 _RD_UNFUSED = os.environ.get("CAI_RD_UNFUSED", "0") == "1"
+_EDGE_OFF = os.environ.get("CAI_EDGE_OFF", "0") == "1"
 
 
 # ---------------------------------------------------------------------------
@@ -250,6 +251,55 @@ def _small_deconv_bwd(ctx, xpm, weight, gy):
     return dx, dw, db, None
 
 
+def edge_eligible(k: int, s: int, p: int, cin: int, cout: int, transposed: bool) -> bool:
+    """Static part of the edge-layer test (csrc/edge.hip): stride-2 image-side conv / deconv."""
+    img_c = cout if transposed else cin
+    return s == 2 and k % 2 == 1 and k <= 5 and p == k // 2 and 1 <= img_c <= 3
+
+
+def _edge_mode(ctx, spec: ConvSpec, g: ConvGeom, dt) -> int:
+    """1: analysis first conv (NCHW fp32 image in); 2: synthesis last deconv (NCHW fp32 image out);
+    0: the general implicit-GEMM path."""
+    if (_EDGE_OFF or dt != torch.bfloat16 or spec.act != ACT_NONE or spec.in_abs or spec.in_mask != MASK_NONE
+            or not lib.cai_edge_supported(ctypes.byref(g), dcode(dt))):
+        return 0
+    if spec.transposed:
+        return 2 if spec.out_nchw32 else 0
+    return 0 if (spec.out_nchw32 or ctx.needs_input_grad[0]) else 1
+
+
+def _edge_bwd(ctx, xs, weight, gy):
+    g, dt = ctx.geom, ctx.dt
+    st = _stream()
+    w32 = weight.detach().float().contiguous()
+    dx = dw = db = None
+    if ctx.edge == 1:      # image = x, feature side = dy
+        img = xs
+        feat, fld = to_pm(gy, dt, 8)
+    else:                  # image = dy, feature side = x
+        img = gy.float().contiguous()
+        feat, fld = xs, ctx.xld
+        if ctx.needs_input_grad[0]:
+            ldx = (g.in_c + 7) // 8 * 8
+            dx = empty_pm(g.batch, g.in_c, g.in_h, g.in_w, dt, gy.device, ld=ldx)
+            lib.cai_edge_deconv_dgrad(ctypes.byref(g), _p(img), _p(w32), _p(dx), ldx, st)
+    if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+        wparam, bparam = ctx.params
+        direct = direct_grad(wparam) and (bparam is None or direct_grad(bparam))
+        if direct:
+            dwt, dbt = wparam.grad, (bparam.grad if bparam is not None else None)
+        else:
+            dwt = torch.empty(weight.shape, dtype=torch.float32, device=gy.device)
+            dbt = torch.empty(g.out_c, dtype=torch.float32, device=gy.device) if ctx.has_bias else None
+        nbytes = lib.cai_edge_workspace_bytes(ctypes.byref(g), dcode(dt))
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=gy.device)
+        lib.cai_edge_wgrad(ctypes.byref(g), _p(img), _p(feat), fld, _p(dwt), _p(dbt), int(direct), _p(ws), nbytes, st)
+        if not direct:
+            dw = dwt if weight.dtype == torch.float32 else dwt.to(weight.dtype)
+            db = dbt
+    return dx, dw, db, None
+
+
 class ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, spec: ConvSpec):
@@ -259,8 +309,28 @@ class ConvFn(torch.autograd.Function):
         B, cin, H, W = x.shape
         cout = weight.shape[1] if spec.transposed else weight.shape[0]
         g = conv_geom(spec, B, cin, H, W, cout)
-        xpm, xld = to_pm(x, dt, vec)
         b = bias.detach().float().contiguous() if bias is not None else None
+        ctx.spec, ctx.geom, ctx.dt = spec, g, dt
+        ctx.has_bias = bias is not None
+        ctx.params = (weight, bias)
+        ctx.edge = _edge_mode(ctx, spec, g, dt)
+        ctx.small = False
+        if ctx.edge == 1:   # space-to-depth first layer: reads the NCHW fp32 image directly
+            x32 = x.detach().float().contiguous()
+            y = empty_pm(B, cout, g.out_h, g.out_w, dt, x.device)
+            lib.cai_edge_conv_fwd(ctypes.byref(g), _p(x32), _p(weight.detach().float().contiguous()), _p(b), _p(y),
+                                  cout, _stream())
+            ctx.xld = 0
+            ctx.save_for_backward(x32, weight, None)
+            return y
+        xpm, xld = to_pm(x, dt, vec)
+        if ctx.edge == 2:   # depth-to-space last layer: writes the NCHW fp32 image directly
+            y = torch.empty((B, cout, g.out_h, g.out_w), dtype=torch.float32, device=x.device)
+            lib.cai_edge_deconv_fwd(ctypes.byref(g), _p(xpm), xld, _p(weight.detach().float().contiguous()), _p(b),
+                                    _p(y), _stream())
+            ctx.xld = xld
+            ctx.save_for_backward(xpm, weight, None)
+            return y
         if spec.out_nchw32:
             y = torch.empty((B, cout, g.out_h, g.out_w), dtype=torch.float32, device=x.device)
             ys = (cout * g.out_h * g.out_w, g.out_h * g.out_w, g.out_w, 1)
@@ -283,9 +353,7 @@ class ConvFn(torch.autograd.Function):
             ws, wsb = _conv_ws(g, dt, 0, x.device)
             lib.cai_conv_fwd(ctypes.byref(g), dcode(dt), _p(xpm), xld, int(spec.in_abs), _p(wp), _p(b), spec.act,
                              spec.act_param, _p(y), ydt, *ys, _p(ws), wsb, _stream())
-        ctx.spec, ctx.geom, ctx.dt, ctx.xld = spec, g, dt, xld
-        ctx.has_bias = bias is not None
-        ctx.params = (weight, bias)
+        ctx.xld = xld
         ctx.save_for_backward(xpm, weight, y if spec.act != ACT_NONE else None)
         return y
 
@@ -296,6 +364,8 @@ class ConvFn(torch.autograd.Function):
         vec = _vec(dt)
         code = dcode(dt)
         st = _stream()
+        if ctx.edge:
+            return _edge_bwd(ctx, xpm, weight, gy)
         if ctx.small:
             return _small_deconv_bwd(ctx, xpm, weight, gy)
         gpm, gld = to_pm(gy, dt, vec)

@@ -19,7 +19,7 @@ from typing import Dict, Optional, Tuple
 import torch
 
 from ._native import ConvGeom, lib
-from ._ops import _p, _stream, compute_dtype, conv_geom, dcode
+from ._ops import _p, _stream, compute_dtype, conv_geom, dcode, edge_eligible
 
 _active = threading.local()
 
@@ -44,6 +44,9 @@ class Prepacker:
             transposed = isinstance(m, torch.nn.ConvTranspose2d)
             if transposed and m.out_channels <= 16:
                 continue   # few-channel deconv path packs its own per-pixel GEMM weights
+            spec = m._spec()
+            if edge_eligible(spec.k, spec.s, spec.p, m.in_channels, m.out_channels, transposed):
+                continue   # csrc/edge.hip gathers its weights from the fp32 tensor itself
             mask = m.mask if isinstance(m, MaskedConv2d) else None
             yield m, mask
 

@@ -1,0 +1,839 @@
+// The stride-2 "edge" layers of the transforms through the space-to-depth view.
+//
+//   analysis first layer   Conv2d(C, N, k, stride 2, pad k/2)                models/utils.py conv()
+//   synthesis last layer   ConvTranspose2d(N, C, k, stride 2, pad k/2, op 1) models/utils.py deconv()
+//   (google.py:96-112 / 145-170 and every model built on them), C <= 3 image channels, k odd <= 5.
+//
+// Viewing the image as a grid of 2x2 superpixels (S: 4C channels at half resolution, read straight
+// from the NCHW fp32 tensor) turns both layers into a 3x3 stride-1 convolution between S and the
+// pixel-major bf16 feature map P on the same Hs x Ws grid:
+//   conv fwd     P[p][n]   = sum_t sum_ch S[p + off(t)][ch] W1[t][ch][n]            (edge_s2d_kernel)
+//   deconv dgrad dX[p][n]  = same form, W1'[t][ch][n] = W2[8 - t][n][ch]            (edge_s2d_kernel)
+//   deconv fwd   S[q][c16] = sum_t sum_ci P[q + off(t)][ci] W2[t][ci][c16]          (edge_d2s_kernel)
+//   wgrads       G[t][ch][n] = sum_p S[p + off(t)][ch] P[p][n]                       (edge_wgrad_kernel)
+//                conv: dW1 = G (+ bias grad from a constant-1 channel); deconv: dW2[t] = G[8 - t]^T
+// with W1[t=(dy,dx)][(py,px,ci)][n] = W[n][ci][2dy+py+k/2][2dx+px+k/2] and
+// W2[t][ci][(py,px,co)] = W[ci][co][py-2dy+k/2][px-2dx+k/2] (zero where the tap falls outside k x k).
+//
+// This replaces, for these layers, the image-side pack + 16x-padded implicit GEMM (first layer) and the
+// per-pixel GEMM + col2im / im2col pipeline of deconv_small.hip (last layer): every kernel reads its
+// HBM operands once, coalesced, stages the 3-row halo in LDS and runs v_mfma_f32_16x16x32_bf16 with
+// the weights gathered from the fp32 torch tensors into registers once per (persistent) block.  The
+// weight-gradient partials are reduced in a fixed order (no float atomics) straight into the torch
+// layout of dW / db.
+#include "common.hpp"
+#include "mfma.hpp"
+
+#include <algorithm>
+
+namespace cai {
+namespace {
+
+constexpr int TB = 64;            // superpixel columns per tile
+constexpr int TBH = TB + 2;       // plus the 3x3 halo
+constexpr int SROW = TBH * 32;    // bytes of one staged superpixel row (16 bf16 channels)
+constexpr int NT = 256;           // threads of the s2d / wgrad kernels
+constexpr int ONES = 12;          // constant-1 superpixel channel (bias gradient of the conv)
+
+struct EdgeArgs {
+    const float* img;     // NCHW fp32 [B, C, 2Hs, 2Ws] (x of the conv, dy of the deconv)
+    const bf16* feat;     // pixel-major bf16 [B, Hs, Ws, N] (dy of the conv, x of the deconv)
+    int feat_ld;
+    const float* w;       // torch weight: conv [N][C][k][k], deconv [N][C][k][k] (in, out)
+    const float* bias;
+    bf16* out_feat;       // s2d output, pixel-major
+    int out_ld;
+    float* out_img;       // d2s output, NCHW fp32
+    float* part;          // wgrad partials [units][9*16*N + 16]
+    int B, C, Hs, Ws, N, k, p;
+    int mode;             // 0: conv weights, 1: deconv weights
+    int ncb;              // column blocks of TB superpixels
+    int rch;              // rows per work unit (d2s / wgrad)
+    int units;
+    bf16* sbf;            // packed superpixels [B][Hs][Ws][16] bf16 (wgrad DMA path)
+    float* cs_part;       // per-pack-block fp32 column sums of the image side [npack][16]
+    int npack, prow;      // pack blocks, superpixel rows per pack block
+};
+
+__device__ __attribute__((aligned(64))) unsigned edge_zero_page[64];
+
+typedef const void __attribute__((address_space(1)))* gvoid_ptr;
+typedef void __attribute__((address_space(3)))* lvoid_ptr;
+
+__device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
+    __builtin_amdgcn_global_load_lds((gvoid_ptr)(reinterpret_cast<uintptr_t>(g)),
+                                     (lvoid_ptr)(reinterpret_cast<uintptr_t>(lds_wave_base)), 16, 0, 0);
+}
+
+// LDS byte offset of 16-byte slot `slot` of row `row` in a [rows][256 B] bf16 image read by
+// ds_read_b64_tr_b16 (the rows 8g+q of a half-wave land on distinct slots)
+__device__ __forceinline__ int trswz(int row, int slot) {
+    return row * 256 + ((slot ^ (((row & 3) << 1) | (((row >> 3) & 1) << 3))) << 4);
+}
+
+__device__ __forceinline__ s16x4 ds_tr16(const char* base, int byte_off) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + byte_off));
+}
+__device__ __forceinline__ u32x4 tr_frag(const char* base, int off0, int off4) {
+    const s16x4 a = ds_tr16(base, off0), b = ds_tr16(base, off4);
+    const s16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    return __builtin_bit_cast(u32x4, v);
+}
+
+// The weight fragments are gathered from a copy of the fp32 torch weight in LDS (wl), loaded once per
+// block with coalesced reads: a per-lane gather straight from global memory costs ~80 dependent
+// L2 round trips per lane.
+__device__ __forceinline__ void load_w_lds(const EdgeArgs& A, float* wl, int nthreads) {
+    const int nw = A.N * A.C * A.k * A.k;
+    for (int i = threadIdx.x; i < nw; i += nthreads) wl[i] = A.w[i];
+    __syncthreads();
+}
+
+// W2[t][ci][c16] of a ConvTranspose2d weight [N][C][k][k], c16 = (py*2+px)*C + co
+template <int C>
+__device__ __forceinline__ float w_d2s(const EdgeArgs& A, const float* wl, int t, int ci, int c16) {
+    const int sp = c16 / C, co = c16 - sp * C;
+    const int ky = (sp >> 1) - 2 * (t / 3 - 1) + A.p, kx = (sp & 1) - 2 * (t % 3 - 1) + A.p;
+    const bool ok = t <= 8 && c16 < 4 * C && ky >= 0 && ky < A.k && kx >= 0 && kx < A.k;
+    return ok ? wl[((ci * C + co) * A.k + ky) * A.k + kx] : 0.f;
+}
+
+// W1[t][ch][n]: the conv's weight (mode 0) or the deconv's input-gradient weight (mode 1)
+template <int C>
+__device__ __forceinline__ float w_s2d(const EdgeArgs& A, const float* wl, int t, int ch, int n) {
+    if (A.mode == 1) return w_d2s<C>(A, wl, 8 - t, n, ch);
+    const int sp = ch / C, ci = ch - sp * C;
+    const int ky = 2 * (t / 3 - 1) + (sp >> 1) + A.p, kx = 2 * (t % 3 - 1) + (sp & 1) + A.p;
+    const bool ok = t <= 8 && ch < 4 * C && ky >= 0 && ky < A.k && kx >= 0 && kx < A.k;
+    return ok ? wl[((n * C + ci) * A.k + ky) * A.k + kx] : 0.f;
+}
+
+// Ss[dyi][j][16] <- superpixel (a - 1 + dyi, b0 - 1 + j) of image n as bf16, channel (py*2+px)*C + ci,
+// channel ONES = 1, zero outside the image.  want_cs: the centre row's fp32 values are added to the
+// calling thread's cs[] (each superpixel column of the tile is owned by one fixed thread).
+template <int C>
+__device__ __forceinline__ void stage_s(const EdgeArgs& A, int n, int a, int b0, char* Ss, float (&cs)[12],
+                                        bool want_cs) {
+    const int it = threadIdx.x;
+    if (it >= 3 * TBH) return;
+    const int dyi = it / TBH, j = it - dyi * TBH;
+    const int sa = a - 1 + dyi, sb = b0 - 1 + j;
+    float v[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) v[e] = 0.f;
+    v[ONES] = 1.f;
+    if (sa >= 0 && sa < A.Hs && sb >= 0 && sb < A.Ws) {
+        const int64_t W2 = 2 * (int64_t)A.Ws;
+#pragma unroll
+        for (int ci = 0; ci < C; ++ci) {
+            const float* base = A.img + ((int64_t)(n * C + ci) * (2 * A.Hs) + 2 * sa) * W2 + 2 * sb;
+            const float2 q0 = *reinterpret_cast<const float2*>(base);
+            const float2 q1 = *reinterpret_cast<const float2*>(base + W2);
+            v[0 * C + ci] = q0.x;
+            v[1 * C + ci] = q0.y;
+            v[2 * C + ci] = q1.x;
+            v[3 * C + ci] = q1.y;
+        }
+    }
+    if (want_cs && dyi == 1 && j >= 1 && j <= TB) {
+#pragma unroll
+        for (int e = 0; e < 4 * C; ++e) cs[e] += v[e];
+    }
+    bf16x8 lo, hi;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        lo[e] = (bf16)v[e];
+        hi[e] = (bf16)v[8 + e];
+    }
+    *reinterpret_cast<u32x4*>(Ss + dyi * SROW + j * 32) = __builtin_bit_cast(u32x4, lo);
+    *reinterpret_cast<u32x4*>(Ss + dyi * SROW + j * 32 + 16) = __builtin_bit_cast(u32x4, hi);
+}
+
+// ---------------------------------------------------------------------------
+// S (image side) -> P (feature side): conv forward, deconv input gradient.
+// Tile = 64 superpixels of one row x all N channels; wave w owns the n-tiles [w*NPW, (w+1)*NPW).
+// K = 9 taps x 16 channels in 5 k-steps of two taps (the 10th tap is zero).
+// ---------------------------------------------------------------------------
+template <int C, int NPW>
+__global__ __launch_bounds__(NT) void edge_s2d_kernel(const EdgeArgs A) {
+    constexpr int N = 64 * NPW, RS = N * 2 + 16;
+    constexpr int WB = N * C * 25 * 4, TILEB = 3 * SROW + TB * RS;
+    __shared__ __attribute__((aligned(16))) char smem[WB > TILEB ? WB : TILEB];
+    char* Ss = smem;
+    char* Ls = smem + 3 * SROW;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g_ = lane >> 4, i16 = lane & 15;
+
+    load_w_lds(A, reinterpret_cast<float*>(smem), NT);
+    u32x4 bw[5][NPW];
+    float bias[NPW];
+#pragma unroll
+    for (int j = 0; j < NPW; ++j) {
+        const int n = (wave * NPW + j) * 16 + i16;
+        bias[j] = (A.mode == 0 && A.bias) ? A.bias[n] : 0.f;
+#pragma unroll
+        for (int ks = 0; ks < 5; ++ks) {
+            const int t = 2 * ks + (g_ >> 1), ch0 = 8 * (g_ & 1);
+            bf16x8 f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] = (bf16)w_s2d<C>(A, reinterpret_cast<const float*>(smem), t, ch0 + e, n);
+            bw[ks][j] = __builtin_bit_cast(u32x4, f);
+        }
+    }
+    float cs_unused[12];
+    const int64_t ntiles = (int64_t)A.B * A.Hs * A.ncb;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int cb = (int)(tile % A.ncb);
+        const int64_t rest = tile / A.ncb;
+        const int a = (int)(rest % A.Hs), n = (int)(rest / A.Hs);
+        const int b0 = cb * TB;
+        __syncthreads();   // the previous tile's readers of Ss / Ls are done
+        stage_s<C>(A, n, a, b0, Ss, cs_unused, false);
+        __syncthreads();
+        f32x4 acc[4][NPW];
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int j = 0; j < NPW; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 5; ++ks) {
+            const int t = 2 * ks + (g_ >> 1);
+            const int tt = t < 9 ? t : 4;
+            const int off = (tt / 3) * SROW + (tt % 3) * 32 + 16 * (g_ & 1);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                u32x4 av = *reinterpret_cast<const u32x4*>(Ss + off + (16 * m + i16) * 32);
+                if (t > 8) av = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int j = 0; j < NPW; ++j) acc[m][j] = mma16<bf16>(av, bw[ks][j], acc[m][j]);
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int j = 0; j < NPW; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int px = 16 * m + 4 * g_ + r, col = (wave * NPW + j) * 16 + i16;
+                    *reinterpret_cast<bf16*>(Ls + px * RS + col * 2) = (bf16)(acc[m][j][r] + bias[j]);
+                }
+        __syncthreads();
+        const int npx = min(TB, A.Ws - b0);
+        bf16* dst = A.out_feat + ((int64_t)n * A.Hs + a) * A.Ws * A.out_ld;
+        for (int c = threadIdx.x; c < TB * (N / 8); c += NT) {
+            const int px = c / (N / 8), part = c - px * (N / 8);
+            if (px < npx)
+                *reinterpret_cast<u32x4*>(dst + (int64_t)(b0 + px) * A.out_ld + part * 8) =
+                    *reinterpret_cast<const u32x4*>(Ls + px * RS + part * 16);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// P (feature side) -> S (image side): deconv forward.  NW = N / 32 waves; wave w owns input channels
+// [32w, 32w + 32) (one k-step per tap, its 9 weight fragments in registers).  A unit streams the
+// feature rows a0 - 1 .. a1 of a 64-superpixel column block through LDS; each staged 16-pixel fragment
+// feeds the three output rows it touches (dy = -1, 0, 1) from three rotating accumulator slots, and
+// output row r - 1 is complete once row r has been consumed: its per-wave partials meet in LDS, are
+// summed in wave order, biased and written as 2 x 128 contiguous fp32 per channel.
+// ---------------------------------------------------------------------------
+template <int C, int NW, int U>
+__device__ __forceinline__ void d2s_row(const EdgeArgs& A, int n, int b0, int a0, int a1, int rr, char* Px,
+                                        float* red, const u32x4 (&bw)[9], f32x4 (&acc)[3][4]) {
+    constexpr int N = 32 * NW, RS = N * 2 + 16, NTH = NW * 64;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g_ = lane >> 4, i16 = lane & 15;
+    const int r = a0 - 1 + rr;
+    const bool live = r >= 0 && r < A.Hs;
+    __syncthreads();   // readers of Px / red from the previous row are done
+    if (live) {
+        const bf16* src = A.feat + ((int64_t)n * A.Hs + r) * A.Ws * A.feat_ld;
+        for (int c = threadIdx.x; c < TBH * (N / 8); c += NTH) {
+            const int j = c / (N / 8), part = c - j * (N / 8);
+            const int sb = b0 - 1 + j;
+            u32x4 v = u32x4{0u, 0u, 0u, 0u};
+            if (sb >= 0 && sb < A.Ws) v = *reinterpret_cast<const u32x4*>(src + (int64_t)sb * A.feat_ld + part * 8);
+            *reinterpret_cast<u32x4*>(Px + j * RS + part * 16) = v;
+        }
+    }
+    __syncthreads();
+    if (live) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int dxi = 0; dxi < 3; ++dxi) {
+                const u32x4 av =
+                    *reinterpret_cast<const u32x4*>(Px + (16 * m + i16 + dxi) * RS + (32 * wave + 8 * g_) * 2);
+                // feature row r feeds output row r - dy: dy = -1 -> slot U+1, 0 -> U, +1 -> U-1 (mod 3)
+                acc[(U + 1) % 3][m] = mma16<bf16>(av, bw[0 + dxi], acc[(U + 1) % 3][m]);
+                acc[U % 3][m] = mma16<bf16>(av, bw[3 + dxi], acc[U % 3][m]);
+                acc[(U + 2) % 3][m] = mma16<bf16>(av, bw[6 + dxi], acc[(U + 2) % 3][m]);
+            }
+    }
+    constexpr int SL = (U + 2) % 3;   // output row r - 1
+    const int a = r - 1;
+    if (a >= a0 && a < a1) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) red[(wave * TB + 16 * m + 4 * g_ + q) * 16 + i16] = acc[SL][m][q];
+        __syncthreads();
+        const int64_t W2 = 2 * (int64_t)A.Ws;
+        const int xw = min(2 * TB, (int)(W2 - 2 * b0));
+        for (int idx = threadIdx.x; idx < C * 2 * 2 * TB; idx += NTH) {
+            const int co = idx / (4 * TB), rem = idx - co * (4 * TB);
+            const int py = rem / (2 * TB), x = rem - py * (2 * TB);
+            const int c16 = (py * 2 + (x & 1)) * C + co;
+            float s = A.bias ? A.bias[co] : 0.f;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) s += red[(w * TB + (x >> 1)) * 16 + c16];
+            if (x < xw) A.out_img[((int64_t)(n * C + co) * (2 * A.Hs) + 2 * a + py) * W2 + 2 * b0 + x] = s;
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) acc[SL][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+template <int C, int NW>
+__global__ __launch_bounds__(NW * 64) void edge_d2s_kernel(const EdgeArgs A) {
+    constexpr int N = 32 * NW, RS = N * 2 + 16;
+    constexpr int WB = N * C * 25 * 4, TILEB = TBH * RS + NW * TB * 16 * 4;
+    __shared__ __attribute__((aligned(16))) char smem[WB > TILEB ? WB : TILEB];
+    char* Px = smem;
+    float* red = reinterpret_cast<float*>(smem + TBH * RS);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g_ = lane >> 4, i16 = lane & 15;
+    load_w_lds(A, reinterpret_cast<float*>(smem), NW * 64);
+    u32x4 bw[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+        bf16x8 f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            f[e] = (bf16)w_d2s<C>(A, reinterpret_cast<const float*>(smem), t, 32 * wave + 8 * g_ + e, i16);
+        bw[t] = __builtin_bit_cast(u32x4, f);
+    }
+    const int nch = (A.Hs + A.rch - 1) / A.rch;
+    for (int unit = blockIdx.x; unit < A.units; unit += gridDim.x) {
+        const int cb = unit % A.ncb, rest = unit / A.ncb;
+        const int ch = rest % nch, n = rest / nch;
+        const int a0 = ch * A.rch, a1 = min(a0 + A.rch, A.Hs);
+        const int b0 = cb * TB;
+        f32x4 acc[3][4];
+#pragma unroll
+        for (int s = 0; s < 3; ++s)
+#pragma unroll
+            for (int m = 0; m < 4; ++m) acc[s][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int nrows = a1 - a0 + 2;   // feature rows a0 - 1 .. a1
+        for (int i = 0; i < nrows; i += 3) {
+            d2s_row<C, NW, 0>(A, n, b0, a0, a1, i, Px, red, bw, acc);
+            if (i + 1 < nrows) d2s_row<C, NW, 1>(A, n, b0, a0, a1, i + 1, Px, red, bw, acc);
+            if (i + 2 < nrows) d2s_row<C, NW, 2>(A, n, b0, a0, a1, i + 2, Px, red, bw, acc);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Weight gradient: G[t][ch][n] = sum_p S[p + off(t)][ch] P[p][n] over a unit of rows (all columns),
+// K = pixels: both operands come out of pixel-major LDS tiles by ds_read_b64_tr_b16.  Wave w owns
+// n-tiles [w*NPW, (w+1)*NPW) and all 9 taps (36*NPW accumulator registers).  The partial of a unit
+// and the fp32 column sums of the image side (the deconv's bias gradient) go to the workspace.
+// ---------------------------------------------------------------------------
+template <int C, int NPW>
+__global__ __launch_bounds__(NT) void edge_wgrad_kernel(const EdgeArgs A) {
+    constexpr int N = 64 * NPW, RS = N * 2 + 16;
+    __shared__ __attribute__((aligned(16))) char Ss[3 * SROW];
+    __shared__ __attribute__((aligned(16))) char Pf[TB * RS];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g_ = lane >> 4, i16 = lane & 15, q_ = i16 >> 2, p4 = i16 & 3;
+    f32x4 acc[9][NPW];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int j = 0; j < NPW; ++j) acc[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float cs[12];
+#pragma unroll
+    for (int e = 0; e < 12; ++e) cs[e] = 0.f;
+
+    const int nch = (A.Hs + A.rch - 1) / A.rch;
+    const int unit = blockIdx.x;
+    const int ch = unit % nch, n = unit / nch;
+    const int a0 = ch * A.rch, a1 = min(a0 + A.rch, A.Hs);
+    for (int a = a0; a < a1; ++a)
+        for (int cb = 0; cb < A.ncb; ++cb) {
+            const int b0 = cb * TB;
+            __syncthreads();
+            stage_s<C>(A, n, a, b0, Ss, cs, true);
+            const bf16* src = A.feat + ((int64_t)n * A.Hs + a) * A.Ws * A.feat_ld;
+            for (int c = threadIdx.x; c < TB * (N / 8); c += NT) {
+                const int px = c / (N / 8), part = c - px * (N / 8);
+                u32x4 v = u32x4{0u, 0u, 0u, 0u};
+                if (b0 + px < A.Ws)
+                    v = *reinterpret_cast<const u32x4*>(src + (int64_t)(b0 + px) * A.feat_ld + part * 8);
+                *reinterpret_cast<u32x4*>(Pf + px * RS + part * 16) = v;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int ks = 0; ks < TB / 32; ++ks) {
+                const int rr = 32 * ks + 8 * g_ + q_;
+                u32x4 bv[NPW];
+#pragma unroll
+                for (int j = 0; j < NPW; ++j) {
+                    const int col = (wave * NPW + j) * 16 + 4 * p4;
+                    bv[j] = tr_frag(Pf, rr * RS + col * 2, (rr + 4) * RS + col * 2);
+                }
+#pragma unroll
+                for (int t = 0; t < 9; ++t) {
+                    const char* base = Ss + (t / 3) * SROW + (t % 3) * 32;
+                    const u32x4 av = tr_frag(base, rr * 32 + 8 * p4, (rr + 4) * 32 + 8 * p4);
+#pragma unroll
+                    for (int j = 0; j < NPW; ++j) acc[t][j] = mma16<bf16>(av, bv[j], acc[t][j]);
+                }
+            }
+        }
+    const int O = 9 * 16 * N + 16;
+    float* P = A.part + (int64_t)unit * O;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int j = 0; j < NPW; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) P[(t * 16 + 4 * g_ + q) * N + (wave * NPW + j) * 16 + i16] = acc[t][j][q];
+    // image-side column sums: the centre-row owners are threads TBH + 1 .. TBH + TB
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(Pf);
+    const int own = threadIdx.x - (TBH + 1);
+    if (own >= 0 && own < TB)
+#pragma unroll
+        for (int e = 0; e < 12; ++e) red[own * 12 + e] = cs[e];
+    __syncthreads();
+    if (threadIdx.x < 16) {
+        float s = 0.f;
+        if (threadIdx.x < 4 * C)
+            for (int i = 0; i < TB; ++i) s += red[i * 12 + threadIdx.x];
+        P[9 * 16 * N + threadIdx.x] = s;
+    }
+}
+
+// Image side -> packed bf16 superpixels S[B][Hs][Ws][16] (the constant-1 channel set), and the fp32
+// column sums of the image side per pack block (the deconv's bias gradient), fixed thread/row order.
+template <int C>
+__global__ __launch_bounds__(256) void edge_pack_s_kernel(const EdgeArgs A) {
+    float cs[12];
+#pragma unroll
+    for (int e = 0; e < 12; ++e) cs[e] = 0.f;
+    const int64_t rows = (int64_t)A.B * A.Hs;
+    const int64_t r0 = (int64_t)blockIdx.x * A.prow, r1 = min(rows, r0 + A.prow);
+    const int64_t W2 = 2 * (int64_t)A.Ws;
+    for (int64_t row = r0; row < r1; ++row) {
+        const int n = (int)(row / A.Hs), a = (int)(row - (int64_t)n * A.Hs);
+        for (int sb = threadIdx.x; sb < A.Ws; sb += 256) {
+            float v[16];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) v[e] = 0.f;
+            v[ONES] = 1.f;
+#pragma unroll
+            for (int ci = 0; ci < C; ++ci) {
+                const float* base = A.img + ((int64_t)(n * C + ci) * (2 * A.Hs) + 2 * a) * W2 + 2 * sb;
+                const float2 q0 = *reinterpret_cast<const float2*>(base);
+                const float2 q1 = *reinterpret_cast<const float2*>(base + W2);
+                v[0 * C + ci] = q0.x;
+                v[1 * C + ci] = q0.y;
+                v[2 * C + ci] = q1.x;
+                v[3 * C + ci] = q1.y;
+            }
+#pragma unroll
+            for (int e = 0; e < 4 * C; ++e) cs[e] += v[e];
+            bf16x8 lo, hi;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                lo[e] = (bf16)v[e];
+                hi[e] = (bf16)v[8 + e];
+            }
+            bf16* dst = A.sbf + (row * A.Ws + sb) * 16;
+            *reinterpret_cast<u32x4*>(dst) = __builtin_bit_cast(u32x4, lo);
+            *reinterpret_cast<u32x4*>(dst + 8) = __builtin_bit_cast(u32x4, hi);
+        }
+    }
+    __shared__ float red[256 * 12];
+#pragma unroll
+    for (int e = 0; e < 12; ++e) red[threadIdx.x * 12 + e] = cs[e];
+    __syncthreads();
+    if (threadIdx.x < 16) {
+        float s = 0.f;
+        if (threadIdx.x < 4 * C)
+            for (int i = 0; i < 256; ++i) s += red[i * 12 + threadIdx.x];
+        A.cs_part[blockIdx.x * 16 + threadIdx.x] = s;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Weight gradient, N = 128, LDS-DMA staging: one step = one superpixel row a x 128 columns; the
+// feature tile [128 px][256 B] (tr-read swizzled) and the three packed superpixel rows a-1..a+1
+// [3][132][32 B] arrive by global_load_lds into a 3-stage ring (12 DMA instructions per wave and
+// step behind a counted vmcnt), so two steps are in flight while one is consumed.  Wave w owns the
+// n-tiles 2w, 2w+1 and all 9 taps: per 32-pixel k-step 2 + 9 fragments feed 18 MFMAs.
+// ---------------------------------------------------------------------------
+constexpr int WTB = 128;                  // columns per step
+constexpr int WPB = WTB * 256;            // feature image bytes
+constexpr int WSR = 132 * 32;             // one packed superpixel row (130 used)
+constexpr int WSB = 16 * 1024;            // S region: 3 rows, padded to 16 DMA instructions
+constexpr int WSTAGE = WPB + WSB;
+constexpr int WG = 12;                    // DMA instructions per wave and step
+
+__global__ __launch_bounds__(NT, 1) void edge_wgrad_dma_kernel(const EdgeArgs A) {
+    __shared__ __attribute__((aligned(16))) char smem[3 * WSTAGE];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g_ = lane >> 4, i16 = lane & 15, q_ = i16 >> 2, p4 = i16 & 3;
+    const int ncb = (A.Ws + WTB - 1) / WTB;
+    const int nch = (A.Hs + A.rch - 1) / A.rch;
+    const int unit = blockIdx.x;
+    const int ch = unit % nch, n = unit / nch;
+    const int a0 = ch * A.rch, a1 = min(a0 + A.rch, A.Hs);
+    const int nsteps = (a1 - a0) * ncb;
+    const char* Pg = reinterpret_cast<const char*>(A.feat);
+    const char* Sg = reinterpret_cast<const char*>(A.sbf);
+
+    auto issue = [&](int st, int stage) {
+        const int a = a0 + st / ncb, b0 = (st % ncb) * WTB;
+        char* base = smem + stage * WSTAGE;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {            // feature tile: 32 instructions, 8 per wave
+            const int k = i * 4 + wave;
+            const int row = k * 4 + (lane >> 4);
+            const int sl = (lane & 15) ^ ((((lane >> 4) & 3) << 1) | (((k >> 1) & 1) << 3));
+            const int px = b0 + row;
+            const void* src = px < A.Ws
+                                  ? (const void*)(Pg + ((((int64_t)n * A.Hs + a) * A.Ws + px) * A.feat_ld + sl * 8) * 2)
+                                  : (const void*)edge_zero_page;
+            glds16(src, base + k * 1024);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {            // superpixel rows: 16 instructions, 4 per wave
+            const int k = i * 4 + wave;
+            const int off = k * 1024 + lane * 16;
+            const void* src = (const void*)edge_zero_page;
+            if (off < 3 * WSR) {
+                const int sr = off / WSR, rem = off - sr * WSR;
+                const int sa = a - 1 + sr, sb = b0 - 1 + rem / 32;
+                if (sa >= 0 && sa < A.Hs && sb >= 0 && sb < A.Ws && rem / 32 < WTB + 2)
+                    src = (const void*)(Sg + ((((int64_t)n * A.Hs + sa) * A.Ws + sb) * 16) * 2 + (rem & 31));
+            }
+            glds16(src, base + WPB + k * 1024);
+        }
+    };
+
+    f32x4 acc[9][2];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (nsteps > 0) issue(0, 0);
+    if (nsteps > 1) issue(1, 1);
+    for (int st = 0; st < nsteps; ++st) {
+        if (st + 1 < nsteps)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WG) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (st + 2 < nsteps) issue(st + 2, (st + 2) % 3);
+        const char* Pst = smem + (st % 3) * WSTAGE;
+        const char* Sst = Pst + WPB;
+#pragma unroll
+        for (int ks = 0; ks < WTB / 32; ++ks) {
+            const int rr = 32 * ks + 8 * g_ + q_;
+            u32x4 bv[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int col = (wave * 2 + j) * 16 + 4 * p4;
+                bv[j] = tr_frag(Pst, trswz(rr, col >> 3) + ((col & 7) << 1),
+                                trswz(rr + 4, col >> 3) + ((col & 7) << 1));
+            }
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const char* sbase = Sst + (t / 3) * WSR + (t % 3) * 32;
+                const u32x4 av = tr_frag(sbase, rr * 32 + 8 * p4, (rr + 4) * 32 + 8 * p4);
+                acc[t][0] = mma16<bf16>(av, bv[0], acc[t][0]);
+                acc[t][1] = mma16<bf16>(av, bv[1], acc[t][1]);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    const int O = 9 * 16 * 128 + 16;
+    float* P = A.part + (int64_t)unit * O;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) P[(t * 16 + 4 * g_ + q) * 128 + (wave * 2 + j) * 16 + i16] = acc[t][j][q];
+}
+
+// Fixed-order sum of the unit partials, scattered into the torch layout of dW (every element of dW /
+// db has exactly one source in G).  Block = 16 outputs x 16 unit groups; the image-side column sums
+// (16 outputs after G) come from cs_src[count][stride].
+template <int C>
+__global__ __launch_bounds__(256) void edge_wgrad_reduce_kernel(const EdgeArgs A, const float* __restrict__ cs_src,
+                                                                int cs_count, int cs_stride, float* __restrict__ dw,
+                                                                float* __restrict__ db, int accumulate) {
+    const int G = 9 * 16 * A.N, O = G + 16;
+    const int l = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    const int o = blockIdx.x * 16 + l;
+    const float* src;
+    int cnt;
+    int64_t stride;
+    if (o < G) {
+        src = A.part + o;
+        cnt = A.units;
+        stride = O;
+    } else {
+        src = cs_src + (o - G);
+        cnt = cs_count;
+        stride = cs_stride;
+    }
+    float s = 0.f;
+    int u = grp;
+    for (; u + 16 * 7 < cnt; u += 16 * 8) {
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = src[(int64_t)(u + 16 * i) * stride];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s += v[i];
+    }
+    for (; u < cnt; u += 16) s += src[(int64_t)u * stride];
+    __shared__ float red[16][16];
+    __shared__ float tot[16];
+    red[grp][l] = s;
+    __syncthreads();
+    if (grp == 0) {
+        float v = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v += red[i][l];
+        tot[l] = v;
+    }
+    __syncthreads();
+    if (grp != 0) return;
+    s = tot[l];
+    if (o >= G) {   // G is a multiple of 16: this block holds exactly the 16 column sums
+        const int co = o - G;
+        if (A.mode == 1 && db && co < C) {
+            float v = 0.f;
+#pragma unroll
+            for (int sp = 0; sp < 4; ++sp) v += tot[sp * C + co];
+            db[co] = accumulate ? db[co] + v : v;
+        }
+        return;
+    }
+    const int nn = o % A.N, tc = o / A.N, t = tc / 16, chn = tc % 16;
+    int dst = -1;
+    if (A.mode == 0) {
+        if (chn == ONES) {
+            if (t == 4 && db) db[nn] = accumulate ? db[nn] + s : s;
+            return;
+        }
+        if (chn >= 4 * C) return;
+        const int sp = chn / C, ci = chn - sp * C;
+        const int ky = 2 * (t / 3 - 1) + (sp >> 1) + A.p, kx = 2 * (t % 3 - 1) + (sp & 1) + A.p;
+        if (ky >= 0 && ky < A.k && kx >= 0 && kx < A.k) dst = ((nn * C + ci) * A.k + ky) * A.k + kx;
+    } else {
+        if (chn >= 4 * C) return;
+        const int sp = chn / C, co = chn - sp * C, tf = 8 - t;
+        const int ky = (sp >> 1) - 2 * (tf / 3 - 1) + A.p, kx = (sp & 1) - 2 * (tf % 3 - 1) + A.p;
+        if (ky >= 0 && ky < A.k && kx >= 0 && kx < A.k) dst = ((nn * C + co) * A.k + ky) * A.k + kx;
+    }
+    if (dst >= 0) dw[dst] = accumulate ? dw[dst] + s : s;
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+bool edge_geo(const cai_conv_geom* g, int dtype, EdgeArgs& A) {
+    if (!g || dtype != CAI_BF16 || g->batch < 1 || g->stride != 2 || g->kernel % 2 == 0 || g->kernel > 5 ||
+        g->pad != g->kernel / 2)
+        return false;
+    A = EdgeArgs{};
+    A.B = g->batch;
+    A.k = g->kernel;
+    A.p = g->pad;
+    if (!g->transposed) {
+        if (g->output_padding != 0 || g->in_h != 2 * g->out_h || g->in_w != 2 * g->out_w) return false;
+        A.C = g->in_c;
+        A.N = g->out_c;
+        A.Hs = g->out_h;
+        A.Ws = g->out_w;
+        A.mode = 0;
+    } else {
+        if (g->out_h != 2 * g->in_h || g->out_w != 2 * g->in_w) return false;
+        A.C = g->out_c;
+        A.N = g->in_c;
+        A.Hs = g->in_h;
+        A.Ws = g->in_w;
+        A.mode = 1;
+    }
+    if (A.C < 1 || A.C > 3 || (A.N != 128 && A.N != 192) || A.Hs < 1 || A.Ws < 1) return false;
+    A.ncb = (A.Ws + TB - 1) / TB;
+    return true;
+}
+
+int wgrad_units(const EdgeArgs& A, int* rch) {
+    const int64_t rows = (int64_t)A.B * A.Hs;
+    const int r = (int)std::max<int64_t>(1, (rows + 255) / 256);
+    *rch = r;
+    return A.B * ((A.Hs + r - 1) / r);
+}
+
+// workspace of the wgrad: [unit partials][packed superpixels (N = 128)][pack column sums]
+struct WgradWs {
+    size_t off_sbf, off_cs, total;
+    int npack, prow;
+};
+WgradWs wgrad_ws(const EdgeArgs& A) {
+    WgradWs W{};
+    int rch;
+    const int units = wgrad_units(A, &rch);
+    const int64_t rows = (int64_t)A.B * A.Hs;
+    W.prow = (int)std::max<int64_t>(1, (rows + 255) / 256);
+    W.npack = (int)((rows + W.prow - 1) / W.prow);
+    auto up = [](size_t v) { return (v + 255) / 256 * 256; };
+    W.off_sbf = up((size_t)units * (9 * 16 * A.N + 16) * sizeof(float));
+    W.off_cs = W.off_sbf + (A.N == 128 ? up((size_t)rows * A.Ws * 32) : 0);
+    W.total = W.off_cs + up((size_t)W.npack * 16 * sizeof(float));
+    return W;
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+template <int C>
+void launch_s2d(const EdgeArgs& A, hipStream_t st) {
+    const int64_t tiles = (int64_t)A.B * A.Hs * A.ncb;
+    const int grid = (int)std::min<int64_t>(tiles, 1024);
+    if (A.N == 128)
+        edge_s2d_kernel<C, 2><<<grid, NT, 0, st>>>(A);
+    else
+        edge_s2d_kernel<C, 3><<<grid, NT, 0, st>>>(A);
+}
+
+template <int C>
+void launch_d2s(EdgeArgs A, hipStream_t st) {
+    int rch = 8;
+    auto units = [&](int r) { return A.B * A.ncb * ((A.Hs + r - 1) / r); };
+    while (rch > 2 && units(rch) < 1024) rch /= 2;
+    A.rch = rch;
+    A.units = units(rch);
+    const int grid = std::min(A.units, 2048);
+    if (A.N == 128)
+        edge_d2s_kernel<C, 4><<<grid, 256, 0, st>>>(A);
+    else
+        edge_d2s_kernel<C, 6><<<grid, 384, 0, st>>>(A);
+}
+
+template <int C>
+void launch_wgrad(EdgeArgs A, char* ws, float* dw, float* db, int accumulate, hipStream_t st) {
+    const int O = 9 * 16 * A.N + 16;
+    if (A.N == 128) {   // packed superpixels + LDS-DMA ring
+        const WgradWs W = wgrad_ws(A);
+        A.sbf = reinterpret_cast<bf16*>(ws + W.off_sbf);
+        A.cs_part = reinterpret_cast<float*>(ws + W.off_cs);
+        A.npack = W.npack;
+        A.prow = W.prow;
+        edge_pack_s_kernel<C><<<W.npack, 256, 0, st>>>(A);
+        edge_wgrad_dma_kernel<<<A.units, NT, 0, st>>>(A);
+        edge_wgrad_reduce_kernel<C><<<O / 16, 256, 0, st>>>(A, A.cs_part, W.npack, 16, dw, db, accumulate);
+    } else {
+        edge_wgrad_kernel<C, 3><<<A.units, NT, 0, st>>>(A);
+        edge_wgrad_reduce_kernel<C><<<O / 16, 256, 0, st>>>(A, A.part + 9 * 16 * A.N, A.units, O, dw, db, accumulate);
+    }
+}
+
+#define EDGE_BY_C(fn, ...)                  \
+    switch (A.C) {                          \
+        case 1: fn<1>(__VA_ARGS__); break;  \
+        case 2: fn<2>(__VA_ARGS__); break;  \
+        default: fn<3>(__VA_ARGS__); break; \
+    }
+
+}  // namespace
+}  // namespace cai
+
+using namespace cai;
+
+extern "C" {
+
+int cai_edge_supported(const cai_conv_geom* g, int dtype) {
+    EdgeArgs A;
+    return edge_geo(g, dtype, A) ? 1 : 0;
+}
+
+size_t cai_edge_workspace_bytes(const cai_conv_geom* g, int dtype) {
+    EdgeArgs A;
+    if (!edge_geo(g, dtype, A)) return 0;
+    return wgrad_ws(A).total;
+}
+
+int cai_edge_conv_fwd(const cai_conv_geom* g, const float* x, const float* w, const float* bias, void* y,
+                      int32_t y_ld, void* stream) {
+    EdgeArgs A;
+    CAI_CHECK_ARG(g && !g->transposed && edge_geo(g, CAI_BF16, A), "edge_conv_fwd: unsupported geometry");
+    CAI_CHECK_ARG(x && w && y && aligned16(y) && ((uintptr_t)x & 7) == 0, "edge_conv_fwd: null or misaligned pointer");
+    CAI_CHECK_ARG(y_ld >= A.N && y_ld % 8 == 0, "edge_conv_fwd: y_ld %d", y_ld);
+    A.img = x;
+    A.w = w;
+    A.bias = bias;
+    A.out_feat = static_cast<bf16*>(y);
+    A.out_ld = y_ld;
+    EDGE_BY_C(launch_s2d, A, as_stream(stream));
+    CAI_LAUNCH_CHECK("edge_conv_fwd");
+    return CAI_OK;
+}
+
+int cai_edge_deconv_fwd(const cai_conv_geom* g, const void* x, int32_t x_ld, const float* w, const float* bias,
+                        float* y, void* stream) {
+    EdgeArgs A;
+    CAI_CHECK_ARG(g && g->transposed && edge_geo(g, CAI_BF16, A), "edge_deconv_fwd: unsupported geometry");
+    CAI_CHECK_ARG(x && w && y && aligned16(x), "edge_deconv_fwd: null or misaligned pointer");
+    CAI_CHECK_ARG(x_ld >= A.N && x_ld % 8 == 0, "edge_deconv_fwd: x_ld %d", x_ld);
+    A.feat = static_cast<const bf16*>(x);
+    A.feat_ld = x_ld;
+    A.w = w;
+    A.bias = bias;
+    A.out_img = y;
+    EDGE_BY_C(launch_d2s, A, as_stream(stream));
+    CAI_LAUNCH_CHECK("edge_deconv_fwd");
+    return CAI_OK;
+}
+
+int cai_edge_deconv_dgrad(const cai_conv_geom* g, const float* dy, const float* w, void* dx, int32_t dx_ld,
+                          void* stream) {
+    EdgeArgs A;
+    CAI_CHECK_ARG(g && g->transposed && edge_geo(g, CAI_BF16, A), "edge_deconv_dgrad: unsupported geometry");
+    CAI_CHECK_ARG(dy && w && dx && aligned16(dx) && ((uintptr_t)dy & 7) == 0,
+                  "edge_deconv_dgrad: null or misaligned pointer");
+    CAI_CHECK_ARG(dx_ld >= A.N && dx_ld % 8 == 0, "edge_deconv_dgrad: dx_ld %d", dx_ld);
+    A.img = dy;
+    A.w = w;
+    A.out_feat = static_cast<bf16*>(dx);
+    A.out_ld = dx_ld;
+    EDGE_BY_C(launch_s2d, A, as_stream(stream));
+    CAI_LAUNCH_CHECK("edge_deconv_dgrad");
+    return CAI_OK;
+}
+
+int cai_edge_wgrad(const cai_conv_geom* g, const float* img, const void* feat, int32_t feat_ld, float* dw, float* db,
+                   int32_t accumulate, void* workspace, size_t ws_bytes, void* stream) {
+    EdgeArgs A;
+    CAI_CHECK_ARG(edge_geo(g, CAI_BF16, A), "edge_wgrad: unsupported geometry");
+    CAI_CHECK_ARG(img && feat && dw && aligned16(feat) && ((uintptr_t)img & 7) == 0,
+                  "edge_wgrad: null or misaligned pointer");
+    CAI_CHECK_ARG(feat_ld >= A.N && feat_ld % 8 == 0, "edge_wgrad: feat_ld %d", feat_ld);
+    CAI_CHECK_ARG(workspace && ws_bytes >= cai_edge_workspace_bytes(g, CAI_BF16), "edge_wgrad: workspace too small");
+    A.img = img;
+    A.feat = static_cast<const bf16*>(feat);
+    A.feat_ld = feat_ld;
+    A.part = static_cast<float*>(workspace);
+    A.units = wgrad_units(A, &A.rch);
+    EDGE_BY_C(launch_wgrad, A, static_cast<char*>(workspace), dw, db, accumulate, as_stream(stream));
+    CAI_LAUNCH_CHECK("edge_wgrad");
+    return CAI_OK;
+}
+
+}  // extern "C"

@@ -161,6 +161,32 @@ int cai_deconv_small_bwd(const cai_conv_geom* g, int dtype, const void* x, int32
                          void* workspace, size_t ws_bytes, void* stream);
 
 /* =======================================================================
+ * Stride-2 edge layers through the space-to-depth view (csrc/edge.hip):
+ * the analysis transform's first Conv2d(C, N, k, 2, k/2) and the synthesis
+ * transform's last ConvTranspose2d(N, C, k, 2, k/2, output_padding 1)
+ * (models/utils.py:21-38, google.py:96-112 / 145-170), C <= 3, k odd <= 5,
+ * N in {128, 192}, bf16 compute.  The image side is NCHW fp32
+ * [B, C, 2Hs, 2Ws], the feature side pixel-major bf16 [B, Hs, Ws, N] (ld).
+ * ======================================================================= */
+/* 1 when the edge path takes this geometry and dtype, else 0. */
+int cai_edge_supported(const cai_conv_geom* g, int dtype);
+/* Workspace of cai_edge_wgrad (0 when unsupported). */
+size_t cai_edge_workspace_bytes(const cai_conv_geom* g, int dtype);
+/* Conv forward: y = conv(x) + bias, x NCHW fp32, y pixel-major bf16. */
+int cai_edge_conv_fwd(const cai_conv_geom* g, const float* x, const float* w, const float* bias, void* y,
+                      int32_t y_ld, void* stream);
+/* ConvTranspose forward: y (NCHW fp32) = deconv(x) + bias, x pixel-major bf16. */
+int cai_edge_deconv_fwd(const cai_conv_geom* g, const void* x, int32_t x_ld, const float* w, const float* bias,
+                        float* y, void* stream);
+/* ConvTranspose input gradient: dx (pixel-major bf16) from dy (NCHW fp32). */
+int cai_edge_deconv_dgrad(const cai_conv_geom* g, const float* dy, const float* w, void* dx, int32_t dx_ld,
+                          void* stream);
+/* Weight / bias gradients of either layer into the torch layouts (accumulate: +=).
+ * conv: img = x, feat = dy; deconv: img = dy, feat = x.  Fixed-order reduction. */
+int cai_edge_wgrad(const cai_conv_geom* g, const float* img, const void* feat, int32_t feat_ld, float* dw, float* db,
+                   int32_t accumulate, void* workspace, size_t ws_bytes, void* stream);
+
+/* =======================================================================
  * Pointwise glue of the residual / attention / sub-pixel blocks
  * (layers/layers.py:81-244), pixel-major, ld a multiple of 8 (bf16) / 4 (fp32).
  * ======================================================================= */

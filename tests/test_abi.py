@@ -95,3 +95,26 @@ def test_empty_conv_output_is_einval(native):
     with pytest.raises(ValueError, match="empty output"):
         native.lib.cai_conv_fwd(ctypes.byref(g), native.BF16, None, 16, 0, None, None, 0, 0.0, None, native.BF16,
                                 0, 0, 0, 0, None, 0, None)
+
+
+def test_edge_gate(native):
+    """csrc/edge.hip takes stride-2, k odd <= 5, pad k/2 image-side layers with <= 3 image channels,
+    128/192 feature channels, bf16 only."""
+    lib = native.lib.load()
+    G = native.ConvGeom
+    yes = [G(2, 3, 256, 256, 128, 128, 128, 5, 2, 2, 0, 0), G(2, 128, 16, 16, 3, 32, 32, 5, 2, 2, 1, 1),
+           G(1, 1, 64, 64, 192, 32, 32, 3, 2, 1, 0, 0), G(1, 192, 8, 9, 2, 16, 18, 3, 2, 1, 1, 1)]
+    no = [G(2, 4, 64, 64, 128, 32, 32, 5, 2, 2, 0, 0),     # 4 image channels
+          G(2, 3, 64, 64, 64, 32, 32, 5, 2, 2, 0, 0),      # 64 feature channels
+          G(2, 3, 63, 64, 128, 32, 32, 5, 2, 2, 0, 0),     # odd image height
+          G(2, 128, 16, 16, 3, 16, 16, 5, 1, 2, 0, 1),     # stride 1
+          G(2, 3, 64, 64, 128, 32, 32, 4, 2, 1, 0, 0)]     # even kernel
+    for g in yes:
+        assert lib.cai_edge_supported(ctypes.byref(g), native.BF16) == 1
+        assert lib.cai_edge_workspace_bytes(ctypes.byref(g), native.BF16) > 0
+        assert lib.cai_edge_supported(ctypes.byref(g), native.F32) == 0
+    for g in no:
+        assert lib.cai_edge_supported(ctypes.byref(g), native.BF16) == 0
+        assert lib.cai_edge_workspace_bytes(ctypes.byref(g), native.BF16) == 0
+    with pytest.raises(ValueError, match="unsupported geometry"):
+        native.lib.cai_edge_conv_fwd(ctypes.byref(no[0]), None, None, None, None, 128, None)
