@@ -77,6 +77,9 @@ SIGNATURES = {
     "cai_deconv_small_bwd": (_I, [_G, _I, _P, c_int32, _P, _P, _P, c_int32, _P, _P, c_int32, _P, _S, _P]),
     "cai_edge_supported": (_I, [_G, _I]),
     "cai_edge_workspace_bytes": (_S, [_G, _I]),
+    "cai_edge_frag_bytes": (_S, [_G, _I, _I]),
+    "cai_edge_pack_weights": (_I, [_G, _I, _I, _P, _P, _P]),
+    "cai_edge_pack_describe": (_I, [_G, _I, _I, _P, _P, _P]),
     "cai_edge_conv_fwd": (_I, [_G, _P, _P, _P, _P, c_int32, _P]),
     "cai_edge_deconv_fwd": (_I, [_G, _P, c_int32, _P, _P, _P, _P]),
     "cai_edge_deconv_dgrad": (_I, [_G, _P, _P, _P, c_int32, _P]),

@@ -268,10 +268,22 @@ def _edge_mode(ctx, spec: ConvSpec, g: ConvGeom, dt) -> int:
     return 0 if (spec.out_nchw32 or ctx.needs_input_grad[0]) else 1
 
 
+def _edge_frag(g: ConvGeom, dt, direction: int, weight: torch.Tensor) -> torch.Tensor:
+    """Packed MFMA weight fragments of an edge layer: the model's prepacked copy while its forward is
+    active (cai_conv_pack_many), else packed here (one small launch)."""
+    packer = _prepack_active()
+    frag = packer.lookup(weight, dt, ("edge", direction)) if packer is not None else None
+    if frag is None:
+        nbytes = lib.cai_edge_frag_bytes(ctypes.byref(g), dcode(dt), direction)
+        frag = torch.empty(nbytes, dtype=torch.uint8, device=weight.device)
+        lib.cai_edge_pack_weights(ctypes.byref(g), dcode(dt), direction, _p(weight.detach().float().contiguous()),
+                                  _p(frag), _stream())
+    return frag
+
+
 def _edge_bwd(ctx, xs, weight, gy):
     g, dt = ctx.geom, ctx.dt
     st = _stream()
-    w32 = weight.detach().float().contiguous()
     dx = dw = db = None
     if ctx.edge == 1:      # image = x, feature side = dy
         img = xs
@@ -282,7 +294,8 @@ def _edge_bwd(ctx, xs, weight, gy):
         if ctx.needs_input_grad[0]:
             ldx = (g.in_c + 7) // 8 * 8
             dx = empty_pm(g.batch, g.in_c, g.in_h, g.in_w, dt, gy.device, ld=ldx)
-            lib.cai_edge_deconv_dgrad(ctypes.byref(g), _p(img), _p(w32), _p(dx), ldx, st)
+            frag = ctx.frag_bwd if ctx.frag_bwd is not None else _edge_frag(g, dt, 1, weight)
+            lib.cai_edge_deconv_dgrad(ctypes.byref(g), _p(img), _p(frag), _p(dx), ldx, st)
     if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
         wparam, bparam = ctx.params
         direct = direct_grad(wparam) and (bparam is None or direct_grad(bparam))
@@ -318,16 +331,18 @@ class ConvFn(torch.autograd.Function):
         if ctx.edge == 1:   # space-to-depth first layer: reads the NCHW fp32 image directly
             x32 = x.detach().float().contiguous()
             y = empty_pm(B, cout, g.out_h, g.out_w, dt, x.device)
-            lib.cai_edge_conv_fwd(ctypes.byref(g), _p(x32), _p(weight.detach().float().contiguous()), _p(b), _p(y),
-                                  cout, _stream())
+            lib.cai_edge_conv_fwd(ctypes.byref(g), _p(x32), _p(_edge_frag(g, dt, 0, weight)), _p(b), _p(y), cout,
+                                  _stream())
             ctx.xld = 0
             ctx.save_for_backward(x32, weight, None)
             return y
         xpm, xld = to_pm(x, dt, vec)
         if ctx.edge == 2:   # depth-to-space last layer: writes the NCHW fp32 image directly
             y = torch.empty((B, cout, g.out_h, g.out_w), dtype=torch.float32, device=x.device)
-            lib.cai_edge_deconv_fwd(ctypes.byref(g), _p(xpm), xld, _p(weight.detach().float().contiguous()), _p(b),
-                                    _p(y), _stream())
+            lib.cai_edge_deconv_fwd(ctypes.byref(g), _p(xpm), xld, _p(_edge_frag(g, dt, 0, weight)), _p(b), _p(y),
+                                    _stream())
+            packer = _prepack_active()   # the input-gradient fragments of this step's weights
+            ctx.frag_bwd = packer.lookup(weight, dt, ("edge", 1)) if packer is not None else None
             ctx.xld = xld
             ctx.save_for_backward(xpm, weight, None)
             return y

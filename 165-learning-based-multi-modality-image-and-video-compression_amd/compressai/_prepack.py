@@ -42,11 +42,10 @@ class Prepacker:
             if not isinstance(m, _ConvMixin):
                 continue
             transposed = isinstance(m, torch.nn.ConvTranspose2d)
-            if transposed and m.out_channels <= 16:
-                continue   # few-channel deconv path packs its own per-pixel GEMM weights
             spec = m._spec()
-            if edge_eligible(spec.k, spec.s, spec.p, m.in_channels, m.out_channels, transposed):
-                continue   # csrc/edge.hip gathers its weights from the fp32 tensor itself
+            if transposed and m.out_channels <= 16 and not edge_eligible(spec.k, spec.s, spec.p, m.in_channels,
+                                                                         m.out_channels, transposed):
+                continue   # few-channel deconv path packs its own per-pixel GEMM weights
             mask = m.mask if isinstance(m, MaskedConv2d) else None
             yield m, mask
 
@@ -63,6 +62,22 @@ class Prepacker:
             w = m.weight.detach()
             if w.dtype != torch.float32 or not w.is_contiguous():
                 return None   # packing reads the fp32 master weights in place
+            if edge_eligible(spec.k, spec.s, spec.p, m.in_channels, m.out_channels, spec.transposed):
+                # csrc/edge.hip MFMA fragments (bf16 only): forward, and the deconv's input gradient
+                if dtype != torch.bfloat16:
+                    continue
+                ge = conv_geom(spec, 1, m.in_channels, 32, 32, m.out_channels)
+                for direction in ((0, 1) if spec.transposed else (0,)):
+                    nbytes = lib.cai_edge_frag_bytes(ctypes.byref(ge), dcode(dtype), direction)
+                    if nbytes == 0:
+                        break
+                    buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+                    d = ctypes.create_string_buffer(dsz)
+                    lib.cai_edge_pack_describe(ctypes.byref(ge), dcode(dtype), direction, _p(w), _p(buf), d)
+                    descs.append(d.raw)
+                    buffers.append(buf)
+                    table[(w.data_ptr(), ("edge", direction))] = buf
+                continue
             for direction in (0, 1):
                 nbytes = lib.cai_conv_packed_weight_bytes(ctypes.byref(g), dcode(dtype), direction)
                 buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)

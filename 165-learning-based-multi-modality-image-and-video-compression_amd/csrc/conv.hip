@@ -25,6 +25,7 @@
 // reduce: deterministic).  Both operands arrive [pixel][channel]; bf16 MFMA
 // fragments are read with ds_read_b64_tr_b16 (hardware transpose).
 #include "common.hpp"
+#include "edge_frag.hpp"
 #include "mfma.hpp"
 
 #include <algorithm>
@@ -582,6 +583,8 @@ struct PackArgs {
     int64_t off[4];
     int64_t item_begin;    // pack_many: first global 8-element item of this descriptor
     int items_pp;          // pack_many: 8-element items per phase (Npad * Kp / 8)
+    int edge;              // 1: edge-layer MFMA fragments (edge_frag.hpp), one item per fragment
+    EdgeFragSpec es;
 };
 
 template <typename T>
@@ -624,6 +627,17 @@ __global__ __launch_bounds__(256) void pack_many_kernel(const PackArgs* __restri
         }
         const PackArgs& a = descs[lo];
         const int local = (int)(gi - a.item_begin);
+        if constexpr (sizeof(T) == 2) {
+            if (a.edge) {
+                float v[8];
+                edge_frag_values(a.w, a.es.C, a.es.N, a.es.k, a.es.p, a.es.emode, local, v);
+                bf16x8 h;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) h[e] = (bf16)v[e];
+                *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(a.out) + (int64_t)local * 8) = h;
+                continue;
+            }
+        }
         const int ph = local / a.items_pp;
         const int e0 = (local - ph * a.items_pp) * 8;
         const int nrow = e0 / a.Kp;
@@ -1564,6 +1578,20 @@ int cai_conv_pack_describe(const cai_conv_geom* g, int dtype, int direction, con
     PackArgs a;
     const int rc = fill_pack_args(g, dtype, direction, w, mask, packed, a);
     if (rc) return rc;
+    memcpy(desc, &a, sizeof(a));
+    return CAI_OK;
+}
+
+int cai_edge_pack_describe(const cai_conv_geom* g, int dtype, int direction, const float* w, void* frag, void* desc) {
+    CAI_CHECK_ARG(desc && w && frag, "edge_pack_describe: null pointer");
+    PackArgs a{};
+    CAI_CHECK_ARG(edge_frag_spec(g, dtype, direction, a.es), "edge_pack_describe: unsupported geometry / direction");
+    a.w = w;
+    a.out = frag;
+    a.edge = 1;
+    a.nphase = 1;
+    a.Npad = a.es.nfrag * 8;   // finalize: items_pp = Npad * Kp / 8 = one item per fragment
+    a.Kp = 1;
     memcpy(desc, &a, sizeof(a));
     return CAI_OK;
 }

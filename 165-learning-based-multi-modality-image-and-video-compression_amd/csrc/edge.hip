@@ -22,6 +22,7 @@
 // weight-gradient partials are reduced in a fixed order (no float atomics) straight into the torch
 // layout of dW / db.
 #include "common.hpp"
+#include "edge_frag.hpp"
 #include "mfma.hpp"
 
 #include <algorithm>
@@ -39,7 +40,7 @@ struct EdgeArgs {
     const float* img;     // NCHW fp32 [B, C, 2Hs, 2Ws] (x of the conv, dy of the deconv)
     const bf16* feat;     // pixel-major bf16 [B, Hs, Ws, N] (dy of the conv, x of the deconv)
     int feat_ld;
-    const float* w;       // torch weight: conv [N][C][k][k], deconv [N][C][k][k] (in, out)
+    const u32x4* frag;    // packed weight fragments (edge_frag.hpp)
     const float* bias;
     bf16* out_feat;       // s2d output, pixel-major
     int out_ld;
@@ -71,6 +72,13 @@ __device__ __forceinline__ int trswz(int row, int slot) {
     return row * 256 + ((slot ^ (((row & 3) << 1) | (((row >> 3) & 1) << 3))) << 4);
 }
 
+// bijective XCD remap: logical ids [x*q, (x+1)*q) run on XCD x (dispatch is round-robin over 8 XCDs)
+__device__ __forceinline__ int xcd_remap_e(int wgid, int nwg) {
+    const int xcd = wgid & 7, idx = wgid >> 3;
+    const int q = nwg >> 3, r = nwg & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
 __device__ __forceinline__ s16x4 ds_tr16(const char* base, int byte_off) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + byte_off));
 }
@@ -78,34 +86,6 @@ __device__ __forceinline__ u32x4 tr_frag(const char* base, int off0, int off4) {
     const s16x4 a = ds_tr16(base, off0), b = ds_tr16(base, off4);
     const s16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
     return __builtin_bit_cast(u32x4, v);
-}
-
-// The weight fragments are gathered from a copy of the fp32 torch weight in LDS (wl), loaded once per
-// block with coalesced reads: a per-lane gather straight from global memory costs ~80 dependent
-// L2 round trips per lane.
-__device__ __forceinline__ void load_w_lds(const EdgeArgs& A, float* wl, int nthreads) {
-    const int nw = A.N * A.C * A.k * A.k;
-    for (int i = threadIdx.x; i < nw; i += nthreads) wl[i] = A.w[i];
-    __syncthreads();
-}
-
-// W2[t][ci][c16] of a ConvTranspose2d weight [N][C][k][k], c16 = (py*2+px)*C + co
-template <int C>
-__device__ __forceinline__ float w_d2s(const EdgeArgs& A, const float* wl, int t, int ci, int c16) {
-    const int sp = c16 / C, co = c16 - sp * C;
-    const int ky = (sp >> 1) - 2 * (t / 3 - 1) + A.p, kx = (sp & 1) - 2 * (t % 3 - 1) + A.p;
-    const bool ok = t <= 8 && c16 < 4 * C && ky >= 0 && ky < A.k && kx >= 0 && kx < A.k;
-    return ok ? wl[((ci * C + co) * A.k + ky) * A.k + kx] : 0.f;
-}
-
-// W1[t][ch][n]: the conv's weight (mode 0) or the deconv's input-gradient weight (mode 1)
-template <int C>
-__device__ __forceinline__ float w_s2d(const EdgeArgs& A, const float* wl, int t, int ch, int n) {
-    if (A.mode == 1) return w_d2s<C>(A, wl, 8 - t, n, ch);
-    const int sp = ch / C, ci = ch - sp * C;
-    const int ky = 2 * (t / 3 - 1) + (sp >> 1) + A.p, kx = 2 * (t % 3 - 1) + (sp & 1) + A.p;
-    const bool ok = t <= 8 && ch < 4 * C && ky >= 0 && ky < A.k && kx >= 0 && kx < A.k;
-    return ok ? wl[((n * C + ci) * A.k + ky) * A.k + kx] : 0.f;
 }
 
 // Ss[dyi][j][16] <- superpixel (a - 1 + dyi, b0 - 1 + j) of image n as bf16, channel (py*2+px)*C + ci,
@@ -149,6 +129,58 @@ __device__ __forceinline__ void stage_s(const EdgeArgs& A, int n, int a, int b0,
     *reinterpret_cast<u32x4*>(Ss + dyi * SROW + j * 32 + 16) = __builtin_bit_cast(u32x4, hi);
 }
 
+// stage_s split in two for software pipelining: the loads of the next tile (branch-free, clamped
+// addresses) are in flight while the current tile is computed.
+template <int C>
+struct SPre {
+    float2 q[2 * C];
+    bool ok;
+};
+
+template <int C>
+__device__ __forceinline__ void s_load(const EdgeArgs& A, int n, int a, int b0, SPre<C>& L) {
+    const int it = min((int)threadIdx.x, 3 * TBH - 1);
+    const int dyi = it / TBH, j = it - dyi * TBH;
+    const int sa = a - 1 + dyi, sb = b0 - 1 + j;
+    L.ok = threadIdx.x < 3 * TBH && sa >= 0 && sa < A.Hs && sb >= 0 && sb < A.Ws;
+    const int64_t W2 = 2 * (int64_t)A.Ws;
+#pragma unroll
+    for (int ci = 0; ci < C; ++ci) {
+        const float* base =
+            L.ok ? A.img + ((int64_t)(n * C + ci) * (2 * A.Hs) + 2 * sa) * W2 + 2 * sb : A.img;
+        L.q[2 * ci] = *reinterpret_cast<const float2*>(base);
+        L.q[2 * ci + 1] = *reinterpret_cast<const float2*>(base + (L.ok ? W2 : 0));
+    }
+}
+
+template <int C>
+__device__ __forceinline__ void s_store(const SPre<C>& L, char* Ss) {
+    const int it = threadIdx.x;
+    if (it >= 3 * TBH) return;
+    const int dyi = it / TBH, j = it - dyi * TBH;
+    float v[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) v[e] = 0.f;
+    v[ONES] = 1.f;
+    if (L.ok) {
+#pragma unroll
+        for (int ci = 0; ci < C; ++ci) {
+            v[0 * C + ci] = L.q[2 * ci].x;
+            v[1 * C + ci] = L.q[2 * ci].y;
+            v[2 * C + ci] = L.q[2 * ci + 1].x;
+            v[3 * C + ci] = L.q[2 * ci + 1].y;
+        }
+    }
+    bf16x8 lo, hi;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        lo[e] = (bf16)v[e];
+        hi[e] = (bf16)v[8 + e];
+    }
+    *reinterpret_cast<u32x4*>(Ss + dyi * SROW + j * 32) = __builtin_bit_cast(u32x4, lo);
+    *reinterpret_cast<u32x4*>(Ss + dyi * SROW + j * 32 + 16) = __builtin_bit_cast(u32x4, hi);
+}
+
 // ---------------------------------------------------------------------------
 // S (image side) -> P (feature side): conv forward, deconv input gradient.
 // Tile = 64 superpixels of one row x all N channels; wave w owns the n-tiles [w*NPW, (w+1)*NPW).
@@ -156,76 +188,66 @@ __device__ __forceinline__ void stage_s(const EdgeArgs& A, int n, int a, int b0,
 // ---------------------------------------------------------------------------
 template <int C, int NPW>
 __global__ __launch_bounds__(NT) void edge_s2d_kernel(const EdgeArgs A) {
-    constexpr int N = 64 * NPW, RS = N * 2 + 16;
-    constexpr int WB = N * C * 25 * 4, TILEB = 3 * SROW + TB * RS;
-    __shared__ __attribute__((aligned(16))) char smem[WB > TILEB ? WB : TILEB];
-    char* Ss = smem;
-    char* Ls = smem + 3 * SROW;
+    constexpr int N = 64 * NPW, RS = N * 2 + 16, NTL = N / 16;
+    __shared__ __attribute__((aligned(16))) char Ss[3 * SROW];
+    __shared__ __attribute__((aligned(16))) char Ls[TB * RS];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g_ = lane >> 4, i16 = lane & 15;
-
-    load_w_lds(A, reinterpret_cast<float*>(smem), NT);
+    // one tile per block (the neighbouring rows of a tile share an XCD's L2)
+    const int tile = xcd_remap_e((int)blockIdx.x, (int)gridDim.x);
+    const int cb = tile % A.ncb, rest = tile / A.ncb;
+    const int a = rest % A.Hs, n = rest / A.Hs;
+    const int b0 = cb * TB;
+    SPre<C> pre;
+    s_load<C>(A, n, a, b0, pre);
     u32x4 bw[5][NPW];
     float bias[NPW];
 #pragma unroll
     for (int j = 0; j < NPW; ++j) {
-        const int n = (wave * NPW + j) * 16 + i16;
-        bias[j] = (A.mode == 0 && A.bias) ? A.bias[n] : 0.f;
+        const int nt = wave * NPW + j;
+        bias[j] = A.bias ? A.bias[nt * 16 + i16] : 0.f;
 #pragma unroll
-        for (int ks = 0; ks < 5; ++ks) {
-            const int t = 2 * ks + (g_ >> 1), ch0 = 8 * (g_ & 1);
-            bf16x8 f;
+        for (int ks = 0; ks < 5; ++ks) bw[ks][j] = A.frag[(ks * NTL + nt) * 64 + lane];
+    }
+    s_store<C>(pre, Ss);
+    __syncthreads();
+    f32x4 acc[4][NPW];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) f[e] = (bf16)w_s2d<C>(A, reinterpret_cast<const float*>(smem), t, ch0 + e, n);
-            bw[ks][j] = __builtin_bit_cast(u32x4, f);
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int j = 0; j < NPW; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 5; ++ks) {
+        const int t = 2 * ks + (g_ >> 1);
+        const int tt = t < 9 ? t : 4;
+        const int off = (tt / 3) * SROW + (tt % 3) * 32 + 16 * (g_ & 1);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            u32x4 av = *reinterpret_cast<const u32x4*>(Ss + off + (16 * m + i16) * 32);
+            if (t > 8) av = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int j = 0; j < NPW; ++j) acc[m][j] = mma16<bf16>(av, bw[ks][j], acc[m][j]);
         }
     }
-    float cs_unused[12];
-    const int64_t ntiles = (int64_t)A.B * A.Hs * A.ncb;
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int cb = (int)(tile % A.ncb);
-        const int64_t rest = tile / A.ncb;
-        const int a = (int)(rest % A.Hs), n = (int)(rest / A.Hs);
-        const int b0 = cb * TB;
-        __syncthreads();   // the previous tile's readers of Ss / Ls are done
-        stage_s<C>(A, n, a, b0, Ss, cs_unused, false);
-        __syncthreads();
-        f32x4 acc[4][NPW];
 #pragma unroll
-        for (int m = 0; m < 4; ++m)
+    for (int m = 0; m < 4; ++m)
 #pragma unroll
-            for (int j = 0; j < NPW; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < NPW; ++j)
 #pragma unroll
-        for (int ks = 0; ks < 5; ++ks) {
-            const int t = 2 * ks + (g_ >> 1);
-            const int tt = t < 9 ? t : 4;
-            const int off = (tt / 3) * SROW + (tt % 3) * 32 + 16 * (g_ & 1);
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                u32x4 av = *reinterpret_cast<const u32x4*>(Ss + off + (16 * m + i16) * 32);
-                if (t > 8) av = u32x4{0u, 0u, 0u, 0u};
-#pragma unroll
-                for (int j = 0; j < NPW; ++j) acc[m][j] = mma16<bf16>(av, bw[ks][j], acc[m][j]);
+            for (int r = 0; r < 4; ++r) {
+                const int px = 16 * m + 4 * g_ + r, col = (wave * NPW + j) * 16 + i16;
+                *reinterpret_cast<bf16*>(Ls + px * RS + col * 2) = (bf16)(acc[m][j][r] + bias[j]);
             }
-        }
+    __syncthreads();
+    const int npx = min(TB, A.Ws - b0);
+    bf16* dst = A.out_feat + ((int64_t)n * A.Hs + a) * A.Ws * A.out_ld;
 #pragma unroll
-        for (int m = 0; m < 4; ++m)
-#pragma unroll
-            for (int j = 0; j < NPW; ++j)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int px = 16 * m + 4 * g_ + r, col = (wave * NPW + j) * 16 + i16;
-                    *reinterpret_cast<bf16*>(Ls + px * RS + col * 2) = (bf16)(acc[m][j][r] + bias[j]);
-                }
-        __syncthreads();
-        const int npx = min(TB, A.Ws - b0);
-        bf16* dst = A.out_feat + ((int64_t)n * A.Hs + a) * A.Ws * A.out_ld;
-        for (int c = threadIdx.x; c < TB * (N / 8); c += NT) {
-            const int px = c / (N / 8), part = c - px * (N / 8);
-            if (px < npx)
-                *reinterpret_cast<u32x4*>(dst + (int64_t)(b0 + px) * A.out_ld + part * 8) =
-                    *reinterpret_cast<const u32x4*>(Ls + px * RS + part * 16);
-        }
+    for (int i = 0; i < TB * (N / 8) / NT; ++i) {
+        const int c = threadIdx.x + i * NT;
+        const int px = c / (N / 8), part = c - px * (N / 8);
+        if (px < npx)
+            *reinterpret_cast<u32x4*>(dst + (int64_t)(b0 + px) * A.out_ld + part * 8) =
+                *reinterpret_cast<const u32x4*>(Ls + px * RS + part * 16);
     }
 }
 
@@ -237,26 +259,53 @@ __global__ __launch_bounds__(NT) void edge_s2d_kernel(const EdgeArgs A) {
 // output row r - 1 is complete once row r has been consumed: its per-wave partials meet in LDS, are
 // summed in wave order, biased and written as 2 x 128 contiguous fp32 per channel.
 // ---------------------------------------------------------------------------
+// one feature row (64 + 2 halo superpixels x N channels) in registers: KP 16-byte chunks per thread
+template <int NW>
+struct RowPre {
+    static constexpr int N = 32 * NW, NTH = NW * 64, CH = TBH * (N / 8), KP = (CH + NTH - 1) / NTH;
+    u32x4 v[KP];
+    unsigned ok;   // bit i: chunk i is inside the image (zero otherwise), applied when stored
+};
+
+template <int NW>
+__device__ __forceinline__ void row_load(const EdgeArgs& A, int n, int r, int b0, RowPre<NW>& P) {
+    using R = RowPre<NW>;
+    const bool live = r >= 0 && r < A.Hs;
+    const bf16* src = A.feat + ((int64_t)n * A.Hs + (live ? r : 0)) * A.Ws * A.feat_ld;
+    P.ok = 0u;
+#pragma unroll
+    for (int i = 0; i < R::KP; ++i) {
+        const int c = threadIdx.x + i * R::NTH;
+        const int j = c / (R::N / 8), part = c - j * (R::N / 8);
+        const int sb = b0 - 1 + j;
+        const bool ok = live && c < R::CH && sb >= 0 && sb < A.Ws;
+        P.v[i] = *reinterpret_cast<const u32x4*>(src + (ok ? (int64_t)sb * A.feat_ld + part * 8 : 0));
+        P.ok |= (ok ? 1u : 0u) << i;
+    }
+}
+
 template <int C, int NW, int U>
 __device__ __forceinline__ void d2s_row(const EdgeArgs& A, int n, int b0, int a0, int a1, int rr, char* Px,
-                                        float* red, const u32x4 (&bw)[9], f32x4 (&acc)[3][4]) {
+                                        float* red, const u32x4 (&bw)[9], f32x4 (&acc)[3][4], RowPre<NW>& pre,
+                                        const float (&bC)[3]) {
     constexpr int N = 32 * NW, RS = N * 2 + 16, NTH = NW * 64;
+    using R = RowPre<NW>;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g_ = lane >> 4, i16 = lane & 15;
     const int r = a0 - 1 + rr;
     const bool live = r >= 0 && r < A.Hs;
     __syncthreads();   // readers of Px / red from the previous row are done
-    if (live) {
-        const bf16* src = A.feat + ((int64_t)n * A.Hs + r) * A.Ws * A.feat_ld;
-        for (int c = threadIdx.x; c < TBH * (N / 8); c += NTH) {
+#pragma unroll
+    for (int i = 0; i < R::KP; ++i) {
+        const int c = threadIdx.x + i * NTH;
+        if (c < R::CH) {
             const int j = c / (N / 8), part = c - j * (N / 8);
-            const int sb = b0 - 1 + j;
-            u32x4 v = u32x4{0u, 0u, 0u, 0u};
-            if (sb >= 0 && sb < A.Ws) v = *reinterpret_cast<const u32x4*>(src + (int64_t)sb * A.feat_ld + part * 8);
-            *reinterpret_cast<u32x4*>(Px + j * RS + part * 16) = v;
+            *reinterpret_cast<u32x4*>(Px + j * RS + part * 16) =
+                ((pre.ok >> i) & 1u) ? pre.v[i] : u32x4{0u, 0u, 0u, 0u};
         }
     }
     __syncthreads();
+    if (r + 1 <= a1) row_load<NW>(A, n, r + 1, b0, pre);   // next row in flight during this one
     if (live) {
 #pragma unroll
         for (int m = 0; m < 4; ++m)
@@ -280,15 +329,16 @@ __device__ __forceinline__ void d2s_row(const EdgeArgs& A, int n, int b0, int a0
         __syncthreads();
         const int64_t W2 = 2 * (int64_t)A.Ws;
         const int xw = min(2 * TB, (int)(W2 - 2 * b0));
-        for (int idx = threadIdx.x; idx < C * 2 * 2 * TB; idx += NTH) {
-            const int co = idx / (4 * TB), rem = idx - co * (4 * TB);
-            const int py = rem / (2 * TB), x = rem - py * (2 * TB);
-            const int c16 = (py * 2 + (x & 1)) * C + co;
-            float s = A.bias ? A.bias[co] : 0.f;
 #pragma unroll
-            for (int w = 0; w < NW; ++w) s += red[(w * TB + (x >> 1)) * 16 + c16];
-            if (x < xw) A.out_img[((int64_t)(n * C + co) * (2 * A.Hs) + 2 * a + py) * W2 + 2 * b0 + x] = s;
-        }
+        for (int co = 0; co < C; ++co)
+            for (int rem = threadIdx.x; rem < 4 * TB; rem += NTH) {
+                const int py = rem / (2 * TB), x = rem - py * (2 * TB);
+                const int c16 = (py * 2 + (x & 1)) * C + co;
+                float s = bC[co];
+#pragma unroll
+                for (int w = 0; w < NW; ++w) s += red[(w * TB + (x >> 1)) * 16 + c16];
+                if (x < xw) A.out_img[((int64_t)(n * C + co) * (2 * A.Hs) + 2 * a + py) * W2 + 2 * b0 + x] = s;
+            }
     }
 #pragma unroll
     for (int m = 0; m < 4; ++m) acc[SL][m] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -297,22 +347,16 @@ __device__ __forceinline__ void d2s_row(const EdgeArgs& A, int n, int b0, int a0
 template <int C, int NW>
 __global__ __launch_bounds__(NW * 64) void edge_d2s_kernel(const EdgeArgs A) {
     constexpr int N = 32 * NW, RS = N * 2 + 16;
-    constexpr int WB = N * C * 25 * 4, TILEB = TBH * RS + NW * TB * 16 * 4;
-    __shared__ __attribute__((aligned(16))) char smem[WB > TILEB ? WB : TILEB];
+    __shared__ __attribute__((aligned(16))) char smem[TBH * RS + NW * TB * 16 * 4];
     char* Px = smem;
     float* red = reinterpret_cast<float*>(smem + TBH * RS);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int g_ = lane >> 4, i16 = lane & 15;
-    load_w_lds(A, reinterpret_cast<float*>(smem), NW * 64);
+    float bC[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) bC[c] = (c < C && A.bias) ? A.bias[c] : 0.f;
     u32x4 bw[9];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-        bf16x8 f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-            f[e] = (bf16)w_d2s<C>(A, reinterpret_cast<const float*>(smem), t, 32 * wave + 8 * g_ + e, i16);
-        bw[t] = __builtin_bit_cast(u32x4, f);
-    }
+    for (int t = 0; t < 9; ++t) bw[t] = A.frag[(t * NW + wave) * 64 + lane];
     const int nch = (A.Hs + A.rch - 1) / A.rch;
     for (int unit = blockIdx.x; unit < A.units; unit += gridDim.x) {
         const int cb = unit % A.ncb, rest = unit / A.ncb;
@@ -325,10 +369,12 @@ __global__ __launch_bounds__(NW * 64) void edge_d2s_kernel(const EdgeArgs A) {
 #pragma unroll
             for (int m = 0; m < 4; ++m) acc[s][m] = f32x4{0.f, 0.f, 0.f, 0.f};
         const int nrows = a1 - a0 + 2;   // feature rows a0 - 1 .. a1
+        RowPre<NW> pre;
+        row_load<NW>(A, n, a0 - 1, b0, pre);
         for (int i = 0; i < nrows; i += 3) {
-            d2s_row<C, NW, 0>(A, n, b0, a0, a1, i, Px, red, bw, acc);
-            if (i + 1 < nrows) d2s_row<C, NW, 1>(A, n, b0, a0, a1, i + 1, Px, red, bw, acc);
-            if (i + 2 < nrows) d2s_row<C, NW, 2>(A, n, b0, a0, a1, i + 2, Px, red, bw, acc);
+            d2s_row<C, NW, 0>(A, n, b0, a0, a1, i, Px, red, bw, acc, pre, bC);
+            if (i + 1 < nrows) d2s_row<C, NW, 1>(A, n, b0, a0, a1, i + 1, Px, red, bw, acc, pre, bC);
+            if (i + 2 < nrows) d2s_row<C, NW, 2>(A, n, b0, a0, a1, i + 2, Px, red, bw, acc, pre, bC);
         }
     }
 }
@@ -705,12 +751,11 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 
 
 template <int C>
 void launch_s2d(const EdgeArgs& A, hipStream_t st) {
-    const int64_t tiles = (int64_t)A.B * A.Hs * A.ncb;
-    const int grid = (int)std::min<int64_t>(tiles, 1024);
+    const int tiles = A.B * A.Hs * A.ncb;
     if (A.N == 128)
-        edge_s2d_kernel<C, 2><<<grid, NT, 0, st>>>(A);
+        edge_s2d_kernel<C, 2><<<tiles, NT, 0, st>>>(A);
     else
-        edge_s2d_kernel<C, 3><<<grid, NT, 0, st>>>(A);
+        edge_s2d_kernel<C, 3><<<tiles, NT, 0, st>>>(A);
 }
 
 template <int C>
@@ -745,6 +790,18 @@ void launch_wgrad(EdgeArgs A, char* ws, float* dw, float* db, int accumulate, hi
     }
 }
 
+__global__ __launch_bounds__(256) void edge_pack_frag_kernel(const float* __restrict__ w, EdgeFragSpec s,
+                                                             u32x4* __restrict__ out) {
+    const int f = blockIdx.x * 256 + threadIdx.x;
+    if (f >= s.nfrag) return;
+    float v[8];
+    edge_frag_values(w, s.C, s.N, s.k, s.p, s.emode, f, v);
+    bf16x8 h;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) h[e] = (bf16)v[e];
+    out[f] = __builtin_bit_cast(u32x4, h);
+}
+
 #define EDGE_BY_C(fn, ...)                  \
     switch (A.C) {                          \
         case 1: fn<1>(__VA_ARGS__); break;  \
@@ -753,6 +810,20 @@ void launch_wgrad(EdgeArgs A, char* ws, float* dw, float* db, int accumulate, hi
     }
 
 }  // namespace
+
+// direction 0: the forward (s2d for the conv, d2s for the deconv); 1: the deconv's input gradient
+bool edge_frag_spec(const cai_conv_geom* g, int dtype, int direction, EdgeFragSpec& s) {
+    EdgeArgs A;
+    if (!edge_geo(g, dtype, A) || direction < 0 || direction > 1 || (direction == 1 && A.mode == 0)) return false;
+    s.C = A.C;
+    s.N = A.N;
+    s.k = A.k;
+    s.p = A.p;
+    s.emode = A.mode == 0 ? 0 : (direction == 0 ? 2 : 1);
+    s.nfrag = s.emode == 2 ? 9 * (A.N / 32) * 64 : 5 * (A.N / 16) * 64;
+    return true;
+}
+
 }  // namespace cai
 
 using namespace cai;
@@ -770,14 +841,30 @@ size_t cai_edge_workspace_bytes(const cai_conv_geom* g, int dtype) {
     return wgrad_ws(A).total;
 }
 
-int cai_edge_conv_fwd(const cai_conv_geom* g, const float* x, const float* w, const float* bias, void* y,
+size_t cai_edge_frag_bytes(const cai_conv_geom* g, int dtype, int direction) {
+    EdgeFragSpec s;
+    return edge_frag_spec(g, dtype, direction, s) ? (size_t)s.nfrag * 16 : 0;
+}
+
+int cai_edge_pack_weights(const cai_conv_geom* g, int dtype, int direction, const float* w, void* frag,
+                          void* stream) {
+    EdgeFragSpec s;
+    CAI_CHECK_ARG(edge_frag_spec(g, dtype, direction, s), "edge_pack_weights: unsupported geometry / direction");
+    CAI_CHECK_ARG(w && frag && aligned16(frag), "edge_pack_weights: null or misaligned pointer");
+    edge_pack_frag_kernel<<<(s.nfrag + 255) / 256, 256, 0, as_stream(stream)>>>(w, s, static_cast<u32x4*>(frag));
+    CAI_LAUNCH_CHECK("edge_pack_weights");
+    return CAI_OK;
+}
+
+int cai_edge_conv_fwd(const cai_conv_geom* g, const float* x, const void* frag, const float* bias, void* y,
                       int32_t y_ld, void* stream) {
     EdgeArgs A;
     CAI_CHECK_ARG(g && !g->transposed && edge_geo(g, CAI_BF16, A), "edge_conv_fwd: unsupported geometry");
-    CAI_CHECK_ARG(x && w && y && aligned16(y) && ((uintptr_t)x & 7) == 0, "edge_conv_fwd: null or misaligned pointer");
+    CAI_CHECK_ARG(x && frag && y && aligned16(y) && aligned16(frag) && ((uintptr_t)x & 7) == 0,
+                  "edge_conv_fwd: null or misaligned pointer");
     CAI_CHECK_ARG(y_ld >= A.N && y_ld % 8 == 0, "edge_conv_fwd: y_ld %d", y_ld);
     A.img = x;
-    A.w = w;
+    A.frag = static_cast<const u32x4*>(frag);
     A.bias = bias;
     A.out_feat = static_cast<bf16*>(y);
     A.out_ld = y_ld;
@@ -786,15 +873,15 @@ int cai_edge_conv_fwd(const cai_conv_geom* g, const float* x, const float* w, co
     return CAI_OK;
 }
 
-int cai_edge_deconv_fwd(const cai_conv_geom* g, const void* x, int32_t x_ld, const float* w, const float* bias,
+int cai_edge_deconv_fwd(const cai_conv_geom* g, const void* x, int32_t x_ld, const void* frag, const float* bias,
                         float* y, void* stream) {
     EdgeArgs A;
     CAI_CHECK_ARG(g && g->transposed && edge_geo(g, CAI_BF16, A), "edge_deconv_fwd: unsupported geometry");
-    CAI_CHECK_ARG(x && w && y && aligned16(x), "edge_deconv_fwd: null or misaligned pointer");
+    CAI_CHECK_ARG(x && frag && y && aligned16(x) && aligned16(frag), "edge_deconv_fwd: null or misaligned pointer");
     CAI_CHECK_ARG(x_ld >= A.N && x_ld % 8 == 0, "edge_deconv_fwd: x_ld %d", x_ld);
     A.feat = static_cast<const bf16*>(x);
     A.feat_ld = x_ld;
-    A.w = w;
+    A.frag = static_cast<const u32x4*>(frag);
     A.bias = bias;
     A.out_img = y;
     EDGE_BY_C(launch_d2s, A, as_stream(stream));
@@ -802,15 +889,15 @@ int cai_edge_deconv_fwd(const cai_conv_geom* g, const void* x, int32_t x_ld, con
     return CAI_OK;
 }
 
-int cai_edge_deconv_dgrad(const cai_conv_geom* g, const float* dy, const float* w, void* dx, int32_t dx_ld,
+int cai_edge_deconv_dgrad(const cai_conv_geom* g, const float* dy, const void* frag, void* dx, int32_t dx_ld,
                           void* stream) {
     EdgeArgs A;
     CAI_CHECK_ARG(g && g->transposed && edge_geo(g, CAI_BF16, A), "edge_deconv_dgrad: unsupported geometry");
-    CAI_CHECK_ARG(dy && w && dx && aligned16(dx) && ((uintptr_t)dy & 7) == 0,
+    CAI_CHECK_ARG(dy && frag && dx && aligned16(dx) && aligned16(frag) && ((uintptr_t)dy & 7) == 0,
                   "edge_deconv_dgrad: null or misaligned pointer");
     CAI_CHECK_ARG(dx_ld >= A.N && dx_ld % 8 == 0, "edge_deconv_dgrad: dx_ld %d", dx_ld);
     A.img = dy;
-    A.w = w;
+    A.frag = static_cast<const u32x4*>(frag);
     A.out_feat = static_cast<bf16*>(dx);
     A.out_ld = dx_ld;
     EDGE_BY_C(launch_s2d, A, as_stream(stream));

@@ -172,14 +172,23 @@ int cai_deconv_small_bwd(const cai_conv_geom* g, int dtype, const void* x, int32
 int cai_edge_supported(const cai_conv_geom* g, int dtype);
 /* Workspace of cai_edge_wgrad (0 when unsupported). */
 size_t cai_edge_workspace_bytes(const cai_conv_geom* g, int dtype);
+/* Packed bf16 MFMA weight fragments of one direction (0: forward, 1: the
+ * deconv's input gradient) from the fp32 torch weight; bytes 0 = unsupported.
+ * cai_edge_pack_describe fills a cai_conv_pack_many descriptor instead (the
+ * per-model one-launch packer). */
+size_t cai_edge_frag_bytes(const cai_conv_geom* g, int dtype, int direction);
+int cai_edge_pack_weights(const cai_conv_geom* g, int dtype, int direction, const float* w, void* frag,
+                          void* stream);
+int cai_edge_pack_describe(const cai_conv_geom* g, int dtype, int direction, const float* w, void* frag,
+                           void* desc);
 /* Conv forward: y = conv(x) + bias, x NCHW fp32, y pixel-major bf16. */
-int cai_edge_conv_fwd(const cai_conv_geom* g, const float* x, const float* w, const float* bias, void* y,
+int cai_edge_conv_fwd(const cai_conv_geom* g, const float* x, const void* frag, const float* bias, void* y,
                       int32_t y_ld, void* stream);
 /* ConvTranspose forward: y (NCHW fp32) = deconv(x) + bias, x pixel-major bf16. */
-int cai_edge_deconv_fwd(const cai_conv_geom* g, const void* x, int32_t x_ld, const float* w, const float* bias,
+int cai_edge_deconv_fwd(const cai_conv_geom* g, const void* x, int32_t x_ld, const void* frag, const float* bias,
                         float* y, void* stream);
 /* ConvTranspose input gradient: dx (pixel-major bf16) from dy (NCHW fp32). */
-int cai_edge_deconv_dgrad(const cai_conv_geom* g, const float* dy, const float* w, void* dx, int32_t dx_ld,
+int cai_edge_deconv_dgrad(const cai_conv_geom* g, const float* dy, const void* frag, void* dx, int32_t dx_ld,
                           void* stream);
 /* Weight / bias gradients of either layer into the torch layouts (accumulate: +=).
  * conv: img = x, feat = dy; deconv: img = dy, feat = x.  Fixed-order reduction. */
