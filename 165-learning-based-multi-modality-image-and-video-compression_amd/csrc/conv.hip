@@ -544,7 +544,22 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce_kernel(const ConvArgs 
         const int n = (int)(id - (int64_t)m * cpr) * VO;
         float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         const float* src = a.ws + ((int64_t)ph * a.ksplit) * slab + (int64_t)m * a.ws_ld + n;
-        for (int s = 0; s < a.ksplit; ++s) {
+        // split order fixed; loads in batches of 4 independent requests
+        int s = 0;
+        for (; s + 4 <= a.ksplit; s += 4) {
+            f32x4 lo[4], hi[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                lo[j] = *reinterpret_cast<const f32x4*>(src + (s + j) * slab);
+                hi[j] = VO == 8 ? *reinterpret_cast<const f32x4*>(src + (s + j) * slab + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                v[0] += lo[j][0]; v[1] += lo[j][1]; v[2] += lo[j][2]; v[3] += lo[j][3];
+                v[4] += hi[j][0]; v[5] += hi[j][1]; v[6] += hi[j][2]; v[7] += hi[j][3];
+            }
+        }
+        for (; s < a.ksplit; ++s) {
             const f32x4 lo = *reinterpret_cast<const f32x4*>(src + s * slab);
             v[0] += lo[0]; v[1] += lo[1]; v[2] += lo[2]; v[3] += lo[3];
             if (VO == 8) {
@@ -1096,40 +1111,42 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
                                                            int Cq, int Cq_pad, int k, float* __restrict__ dw,
                                                            int accumulate, const float* __restrict__ bws,
                                                            float* __restrict__ db) {
-    __shared__ f32x4 red[16][16];
+    // one thread per 16-byte column chunk summing its S split partials in split order; the loads go out
+    // in batches of 8 independent requests (the partials stream from HBM once)
     const int c4 = ncols >> 2;
-    const int wblocks = (int)(((int64_t)Ng * c4 + 15) / 16);
+    const int64_t total = (int64_t)Ng * c4;
+    const int wblocks = (int)((total + 255) / 256);
     if ((int)blockIdx.x >= wblocks) {
-        // trailing blocks: bias partials [S][Ng] -> db, 16 channels per block,
-        // 16 split groups summed in a fixed order
-        __shared__ float bred[16][16];
-        const int cgb = threadIdx.x & 15, sgb = threadIdx.x >> 4;
-        const int n = ((int)blockIdx.x - wblocks) * 16 + cgb;
+        // trailing blocks: bias partials [S][Ng] -> db, one thread per channel
+        const int n = ((int)blockIdx.x - wblocks) * 256 + threadIdx.x;
+        if (n >= Ng) return;
         float v = 0.f;
-        if (n < Ng)
-            for (int sp = sgb; sp < S; sp += 16) v += bws[(int64_t)sp * Ng + n];
-        bred[sgb][cgb] = v;
-        __syncthreads();
-        if (sgb == 0 && n < Ng) {
-            for (int j = 1; j < 16; ++j) v += bred[j][cgb];
-            db[n] = accumulate ? db[n] + v : v;
+        int sp = 0;
+        for (; sp + 8 <= S; sp += 8) {
+            float b[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) b[j] = bws[(int64_t)(sp + j) * Ng + n];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v += b[j];
         }
+        for (; sp < S; ++sp) v += bws[(int64_t)sp * Ng + n];
+        db[n] = accumulate ? db[n] + v : v;
         return;
     }
-    const int64_t total = (int64_t)Ng * c4;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= total) return;
     const int64_t slab4 = ((int64_t)Ng * ncols) >> 2;
-    const int cg = threadIdx.x & 15, sg = threadIdx.x >> 4;
-    const int64_t i = (int64_t)blockIdx.x * 16 + cg;
+    const f32x4* src = reinterpret_cast<const f32x4*>(ws) + i;
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (i < total) {
-        const f32x4* src = reinterpret_cast<const f32x4*>(ws) + i;
-        for (int sp = sg; sp < S; sp += 16) acc += src[sp * slab4];
-    }
-    red[sg][cg] = acc;
-    __syncthreads();
-    if (sg != 0 || i >= total) return;
+    int sp = 0;
+    for (; sp + 8 <= S; sp += 8) {
+        f32x4 v[8];
 #pragma unroll
-    for (int j = 1; j < 16; ++j) acc += red[j][cg];
+        for (int j = 0; j < 8; ++j) v[j] = src[(int64_t)(sp + j) * slab4];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc += v[j];
+    }
+    for (; sp < S; ++sp) acc += src[(int64_t)sp * slab4];
     const int n = (int)(i / c4);
     const int col = (int)(i - (int64_t)n * c4) * 4;
     const int kk = k * k;
@@ -1722,7 +1739,7 @@ int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_l
             hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(NT), 0, st, a);
     }
     const int64_t tot = (int64_t)W.Ng * (W.ncols / 4);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((tot + 15) / 16) + (bws ? (W.Ng + 15) / 16 : 0)), dim3(256), 0,
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((tot + 255) / 256) + (bws ? (W.Ng + 255) / 256 : 0)), dim3(256), 0,
                        st, slab, W.S, W.Ng, W.ncols, W.Cq, W.Cq_pad, g->kernel, dw, accumulate, bws, db);
     if (db && !bws) {
         float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + W.ws_slab + W.ws_bias);
