@@ -486,14 +486,24 @@ __global__ __launch_bounds__(FNT, 1) void gdn_bwd_fused_kernel(const bf16* __res
                 acc[tm] = mma_sq<bf16>(a, fb[kb], acc[tm], true);
             }
         // ---- u, t1 (thread-owned elements: row (lane>>4)*4 + r, column n0 + i16) ----
+        // all LDS reads first: Lx / Lg / Lu share one array, so a read after a store would be
+        // issued (and waited for) one element at a time
+        float xr[G::TM][4], gr[G::TM][4];
 #pragma unroll
         for (int tm = 0; tm < G::TM; ++tm)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = r0 + tm * 16 + g_ * 4 + r;
-                const float xv = (float)*lds_elem<bf16>(Lx, G::RS, row, n0 + i16);
-                bf16* gp = lds_elem<bf16>(Lg, G::RS, row, n0 + i16);
-                const float gv = (float)*gp;
+                xr[tm][r] = (float)*lds_elem<bf16>(Lx, G::RS, row, n0 + i16);
+                gr[tm][r] = (float)*lds_elem<bf16>(Lg, G::RS, row, n0 + i16);
+            }
+#pragma unroll
+        for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = r0 + tm * 16 + g_ * 4 + r;
+                const float xv = xr[tm][r];
+                const float gv = gr[tm][r];
                 const float nv = acc[tm][r] + bv;
                 float uv, t1;
                 if (inverse) {
@@ -507,7 +517,7 @@ __global__ __launch_bounds__(FNT, 1) void gdn_bwd_fused_kernel(const bf16* __res
                 }
                 if (p0 + row >= npix) uv = 0.f;
                 dbeta += uv;
-                *gp = (bf16)t1;
+                gr[tm][r] = (float)(bf16)t1;   // t1 stays in registers for the dx phase
                 *lds_elem<bf16>(Lu, G::RS, row, n0 + i16) = (bf16)uv;
             }
         lds_barrier();
@@ -540,14 +550,13 @@ __global__ __launch_bounds__(FNT, 1) void gdn_bwd_fused_kernel(const bf16* __res
                 const u32x4 a = *reinterpret_cast<const u32x4*>(Lu + row * G::RS + kb * 64 + 16 * g_);
                 acc[tm] = mma16<bf16>(a, fbT[kb], acc[tm]);
             }
+        // dx = t1 + 2 x (u gamma): x and t1 are still in registers (xr, gr)
 #pragma unroll
         for (int tm = 0; tm < G::TM; ++tm)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = r0 + tm * 16 + g_ * 4 + r;
-                const float xv = (float)*lds_elem<bf16>(Lx, G::RS, row, n0 + i16);
-                bf16* gp = lds_elem<bf16>(Lg, G::RS, row, n0 + i16);
-                *gp = (bf16)((float)*gp + 2.f * xv * acc[tm][r]);
+                *lds_elem<bf16>(Lg, G::RS, row, n0 + i16) = (bf16)(gr[tm][r] + 2.f * xr[tm][r] * acc[tm][r]);
             }
         lds_barrier();
         lds_to_global_rows<C>(Lg, dx, dx_ld, p0, npix);
