@@ -197,7 +197,8 @@ __global__ __launch_bounds__(GNT, sizeof(T) == 2 ? 2 : 1) void gdn_fwd_kernel(co
                                                          const T* __restrict__ gamma, const float* __restrict__ beta,
                                                          int inverse, T* __restrict__ y, int y_ld) {
     using G = GdnGeo<T, C>;
-    __shared__ __attribute__((aligned(16))) char lds[G::TILE_LDS];
+    __shared__ __attribute__((aligned(16))) char lds[2 * G::TILE_LDS];
+    char* lsq = lds + G::TILE_LDS;   // x^2, squared once per tile (not by each wave that reads it)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     BFrags<T, C> fb;
     load_bfrag<T, C>(fb, gamma, wave);
@@ -211,11 +212,17 @@ __global__ __launch_bounds__(GNT, sizeof(T) == 2 ? 2 : 1) void gdn_fwd_kernel(co
     if (tile < ntiles) tile_load<T, C>(rx, x, x_ld, tile * GBM, npix);
     for (; tile < ntiles; tile += gridDim.x) {
         tile_to_lds<T, C>(rx, lds);
+        {
+            TileRegs<T, C> sq;
+#pragma unroll
+            for (int i = 0; i < G::CPT; ++i) sq.v[i] = sq_chunk<T>(rx.v[i]);
+            tile_to_lds<T, C>(sq, lsq);
+        }
         lds_barrier();
         const int64_t nxt = tile + gridDim.x;
         if (nxt < ntiles) tile_load<T, C>(rx, x, x_ld, nxt * GBM, npix);
         Acc<T, C> A;
-        tile_gemm<T, C>(A, lds, fb, true, wave);
+        tile_gemm<T, C>(A, lsq, fb, false, wave);
         auto& acc = A.v;
         // normalise: out = x * rsqrt(norm)  (or sqrt)
 #pragma unroll
@@ -391,6 +398,23 @@ __device__ __forceinline__ void ftile_to_lds(const u32x4 (&r)[FusedGeo<C>::CPT],
     }
 }
 
+// x tile and its elementwise square (bf16-rounded, as the MFMA operand): squared once per tile here
+// instead of by each of the 8 waves that read it as a GEMM operand
+template <int C>
+__device__ __forceinline__ void ftile_to_lds_sq(const u32x4 (&r)[FusedGeo<C>::CPT], char* lds, char* lds_sq,
+                                                int64_t p0, int64_t npix) {
+    using G = FusedGeo<C>;
+    constexpr int CHR = 2 * C / 16;
+#pragma unroll
+    for (int i = 0; i < G::CPT; ++i) {
+        const int id = i * FNT + threadIdx.x;
+        const int row = id / CHR, ch = id - (id / CHR) * CHR;
+        const u32x4 v = (p0 + row < npix) ? r[i] : u32x4{0u, 0u, 0u, 0u};
+        *reinterpret_cast<u32x4*>(lds + row * G::RS + ch * 16) = v;
+        *reinterpret_cast<u32x4*>(lds_sq + row * G::RS + ch * 16) = sq_chunk<bf16>(v);
+    }
+}
+
 template <int C>
 __device__ __forceinline__ void lds_to_global_rows(const char* lds, bf16* dst, int ld, int64_t p0, int64_t npix) {
     using G = FusedGeo<C>;
@@ -413,10 +437,11 @@ __global__ __launch_bounds__(FNT, 1) void gdn_bwd_fused_kernel(const bf16* __res
                                                                bf16* __restrict__ dx, int dx_ld,
                                                                float* __restrict__ part) {
     using G = FusedGeo<C>;
-    __shared__ __attribute__((aligned(16))) char lds[3 * G::TILE];
+    __shared__ __attribute__((aligned(16))) char lds[4 * G::TILE];
     char* Lx = lds;
     char* Lg = lds + G::TILE;
     char* Lu = lds + 2 * G::TILE;
+    char* Lq = lds + 3 * G::TILE;   // x^2
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wn = wave % G::WN, wm = wave / G::WN;
     const int n0 = wn * 16, r0 = wm * (GBM / G::WM);
@@ -458,14 +483,14 @@ __global__ __launch_bounds__(FNT, 1) void gdn_bwd_fused_kernel(const bf16* __res
         lds_barrier();                       // previous tile's dx store has read Lg
         const int64_t nxt = tile + 2 * stride;
         if (parity == 0) {
-            ftile_to_lds<C>(rxa, Lx, p0, npix);
+            ftile_to_lds_sq<C>(rxa, Lx, Lq, p0, npix);
             ftile_to_lds<C>(rga, Lg, p0, npix);
             if (nxt < ntiles) {
                 ftile_load<C>(rxa, x, x_ld, nxt * GBM, npix);
                 ftile_load<C>(rga, dy, dy_ld, nxt * GBM, npix);
             }
         } else {
-            ftile_to_lds<C>(rxb, Lx, p0, npix);
+            ftile_to_lds_sq<C>(rxb, Lx, Lq, p0, npix);
             ftile_to_lds<C>(rgb, Lg, p0, npix);
             if (nxt < ntiles) {
                 ftile_load<C>(rxb, x, x_ld, nxt * GBM, npix);
@@ -482,8 +507,8 @@ __global__ __launch_bounds__(FNT, 1) void gdn_bwd_fused_kernel(const bf16* __res
 #pragma unroll
             for (int tm = 0; tm < G::TM; ++tm) {
                 const int row = r0 + tm * 16 + i16;
-                const u32x4 a = *reinterpret_cast<const u32x4*>(Lx + row * G::RS + kb * 64 + 16 * g_);
-                acc[tm] = mma_sq<bf16>(a, fb[kb], acc[tm], true);
+                const u32x4 a = *reinterpret_cast<const u32x4*>(Lq + row * G::RS + kb * 64 + 16 * g_);
+                acc[tm] = mma16<bf16>(a, fb[kb], acc[tm]);
             }
         // ---- u, t1 (thread-owned elements: row (lane>>4)*4 + r, column n0 + i16) ----
         // all LDS reads first: Lx / Lg / Lu share one array, so a read after a store would be
@@ -526,10 +551,10 @@ __global__ __launch_bounds__(FNT, 1) void gdn_bwd_fused_kernel(const bf16* __res
         for (int ks = 0; ks < GBM / 32; ++ks) {
             const int rr = 32 * ks + 8 * g_ + q_;
             const int colB = jb * 16 + 4 * p4;
-            const s16x4 b0 = ds_tr16(Lx, rr * G::RS + colB * 2);
-            const s16x4 b1 = ds_tr16(Lx, (rr + 4) * G::RS + colB * 2);
+            const s16x4 b0 = ds_tr16(Lq, rr * G::RS + colB * 2);
+            const s16x4 b1 = ds_tr16(Lq, (rr + 4) * G::RS + colB * 2);
             const s16x8 bvv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
-            const u32x4 fbx = sq_chunk<bf16>(__builtin_bit_cast(u32x4, bvv));
+            const u32x4 fbx = __builtin_bit_cast(u32x4, bvv);
 #pragma unroll
             for (int t = 0; t < G::TI; ++t) {
                 const int colA = (ib0 + t) * 16 + 4 * p4;
