@@ -235,7 +235,8 @@ __global__ __launch_bounds__(GNT, sizeof(T) == 2 ? 2 : 1) void gdn_fwd_kernel(co
                     const int row = G::row0(wave) + tm * 16 + (lane >> 4) * 4 + r;
                     const float xv = to_f32(*lds_elem<T>(lds, G::RS, row, col));
                     const float nv = acc[tm][tn][r] + bv[tn];
-                    acc[tm][tn][r] = xv * (inverse ? sqrtf(nv) : rsqrtf(nv));
+                    const float rs = rsqrtf(nv);
+                    acc[tm][tn][r] = xv * (inverse ? nv * rs : rs);
                 }
             }
         lds_barrier();
@@ -429,7 +430,7 @@ __device__ __forceinline__ void lds_to_global_rows(const char* lds, bf16* dst, i
     }
 }
 
-template <int C>
+template <int C, bool INV>
 __global__ __launch_bounds__(FNT, 1) void gdn_bwd_fused_kernel(const bf16* __restrict__ x, int x_ld,
                                                                const bf16* __restrict__ dy, int dy_ld, int64_t npix,
                                                                const bf16* __restrict__ gamma_op,
@@ -498,6 +499,7 @@ __global__ __launch_bounds__(FNT, 1) void gdn_bwd_fused_kernel(const bf16* __res
             }
         }
         lds_barrier();
+        const int nvalid = (int)min((int64_t)GBM, npix - p0);
         // ---- norm = x^2 gamma^T (+ beta) ----
         f32x4 acc[G::TM];
 #pragma unroll
@@ -530,17 +532,17 @@ __global__ __launch_bounds__(FNT, 1) void gdn_bwd_fused_kernel(const bf16* __res
                 const float xv = xr[tm][r];
                 const float gv = gr[tm][r];
                 const float nv = acc[tm][r] + bv;
+                // one v_rsq per element for both forms (no IEEE divide / sqrt sequences)
+                const float rs = rsqrtf(nv);
                 float uv, t1;
-                if (inverse) {
-                    const float sq = sqrtf(nv);
-                    t1 = gv * sq;
-                    uv = 0.5f * gv * xv / sq;
+                if constexpr (INV) {
+                    t1 = gv * nv * rs;                 // g sqrt(norm)
+                    uv = 0.5f * gv * xv * rs;          // g x / (2 sqrt(norm))
                 } else {
-                    const float rr = rsqrtf(nv);
-                    t1 = gv * rr;
-                    uv = -0.5f * gv * xv * rr * rr * rr;
+                    t1 = gv * rs;
+                    uv = -0.5f * gv * xv * rs * rs * rs;
                 }
-                if (p0 + row >= npix) uv = 0.f;
+                if (row >= nvalid) uv = 0.f;
                 dbeta += uv;
                 gr[tm][r] = (float)(bf16)t1;   // t1 stays in registers for the dx phase
                 *lds_elem<bf16>(Lu, G::RS, row, n0 + i16) = (bf16)uv;
@@ -850,9 +852,9 @@ int cai_gdn_backward(int dtype, const void* x, int32_t x_ld, const void* dy, int
                            beta, inverse, reinterpret_cast<bf16*>(dx), dx_ld, part);
     };
     if (C == 128)
-        launch(gdn_bwd_fused_kernel<128>);
+        inverse ? launch(gdn_bwd_fused_kernel<128, true>) : launch(gdn_bwd_fused_kernel<128, false>);
     else
-        launch(gdn_bwd_fused_kernel<64>);
+        inverse ? launch(gdn_bwd_fused_kernel<64, true>) : launch(gdn_bwd_fused_kernel<64, false>);
     const float ped = reparam_offset * reparam_offset;
     const float bbound = sqrtf(beta_min + ped), gbound = sqrtf(ped);
     const int64_t n = (int64_t)C * C + C;
