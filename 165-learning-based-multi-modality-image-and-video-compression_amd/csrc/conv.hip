@@ -974,9 +974,22 @@ __global__ __launch_bounds__(512, 1) void wgrad_glds_kernel(const WgradArgs a) {
         const int q = xvalid[h] ? col - t * a.Cq_pad : 0;
         xkh[h] = t / a.k;
         xkw[h] = t - xkh[h] * a.k;
-        xoff[h] = q * 2;
+        // byte offset of this lane's tap / channel slot from the tap-(0,0) pixel of its row
+        xoff[h] = ((xkh[h] * a.Wx + xkw[h]) * a.x_ld + q) * 2;
     }
     const int plane = a.Hg * a.Wg;
+    // pixel coordinates (image, row, column) of this thread's two DMA rows for the next step to issue:
+    // steps are issued in order and advance the pixel index by 64, so the coordinates advance by
+    // carries instead of two integer divisions per row and step
+    int cb[2], cj[2], cx[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int m = pbeg + prow0 + i * 32;
+        cb[i] = m / plane;
+        const int r = m - cb[i] * plane;
+        cj[i] = r / a.Wg;
+        cx[i] = r - cj[i] * a.Wg;
+    }
 
     auto issue = [&](int st, int stage) {
         char* sb = smem + stage * STAGE + wid * 4 * 256;
@@ -987,16 +1000,23 @@ __global__ __launch_bounds__(512, 1) void wgrad_glds_kernel(const WgradArgs a) {
             const void* gs = (mok && gvalid) ? (const void*)(Gp + ((int64_t)m * a.g_ld + gch) * 2)
                                              : (const void*)cai_zero_page;
             glds16(gs, sb + i * 32 * 256);
-            const int b = m / plane;
-            const int r = m - b * plane;
-            const int j = r / a.Wg;
-            const int yb = j * a.s - a.p, xb = (r - j * a.Wg) * a.s - a.p;
+            const int b = cb[i], j = cj[i];
+            const int yb = j * a.s - a.p, xb = cx[i] * a.s - a.p;
+            cx[i] += 64;
+            while (cx[i] >= a.Wg) {
+                cx[i] -= a.Wg;
+                if (++cj[i] == a.Hg) {
+                    cj[i] = 0;
+                    ++cb[i];
+                }
+            }
+            // tap-(0,0) pixel of this row (may lie in the padding; only in-range taps are read)
+            const char* xrow = Xp + (((int64_t)b * a.Hx + yb) * a.Wx + xb) * a.x_ld * 2;
 #pragma unroll
             for (int h = 0; h < NX; ++h) {
                 const int iy = yb + xkh[h], ix = xb + xkw[h];
                 const bool ok = mok && xvalid[h] && (unsigned)iy < (unsigned)a.Hx && (unsigned)ix < (unsigned)a.Wx;
-                const void* xs = ok ? (const void*)(Xp + (((int64_t)b * a.Hx + iy) * a.Wx + ix) * a.x_ld * 2 + xoff[h])
-                                    : (const void*)cai_zero_page;
+                const void* xs = ok ? (const void*)(xrow + xoff[h]) : (const void*)cai_zero_page;
                 glds16(xs, sb + (1 + h) * OPB + i * 32 * 256);
             }
         }

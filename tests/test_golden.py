@@ -33,8 +33,10 @@ def test_oracle_reproduces_fixture(name):
     gold = MG.load(name)
     fresh = {k: v.detach() for k, v in MG.GENERATORS[name]().items()}
     assert set(gold) == set(fresh)
+    # 5e-5: torch's CPU kernels pick vector code paths by host ISA, so fp32 sums of the same
+    # restatement differ in the last bits between hosts (1.3e-5 seen on a GPU box's host)
     for k, v in gold.items():
-        assert relerr(fresh[k], v) < 1e-5, k
+        assert relerr(fresh[k], v) < 5e-5, k
 
 
 # --------------------------------------------------------------------------- GPU
