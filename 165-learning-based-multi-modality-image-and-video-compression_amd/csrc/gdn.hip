@@ -624,8 +624,18 @@ __global__ __launch_bounds__(256) void gdn_fused_reduce_kernel(const float* __re
     const int cg = threadIdx.x & 15, bg = threadIdx.x >> 4;
     const int64_t i = (int64_t)blockIdx.x * 16 + cg;
     float v = 0.f;
-    if (i < CC + C)
-        for (int b = bg; b < nblk; b += 16) v += part[b * stride + i];
+    if (i < CC + C) {
+        // fixed block order; loads issued 8 at a time (independent requests in flight)
+        int b = bg;
+        for (; b + 16 * 7 < nblk; b += 16 * 8) {
+            float t[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) t[j] = part[(int64_t)(b + 16 * j) * stride + i];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v += t[j];
+        }
+        for (; b < nblk; b += 16) v += part[(int64_t)b * stride + i];
+    }
     red[bg][cg] = v;
     __syncthreads();
     if (bg != 0 || i >= CC + C) return;
