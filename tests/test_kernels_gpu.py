@@ -473,3 +473,33 @@ def test_cheng2020_blocks(cuda, kind, bf16):
     wm = max(v for k, v in mine.items() if k not in ("y", "dx"))
     wt = max(v for k, v in theirs.items() if k not in ("y", "dx"))
     assert wm <= 2 * wt + 1e-2, (wm, wt)
+
+
+@pytest.mark.parametrize("kind", ["deconv_fwd", "conv_dgrad"])
+def test_multiphase_conv(cuda, kind):
+    """Full-size s^2-phase GEMMs (the C2 g_s[2] forward / g_a[1] input gradient shape, B=14): four phases of
+    224 row tiles each on the LDS-DMA kernel.  Reference: torch fp32 on the GPU over the same bf16-rounded
+    operands; relative max error <= 1e-2."""
+    from compressai.layers import Conv2d, ConvTranspose2d
+
+    torch.manual_seed(3)
+    B = 14
+    if kind == "deconv_fwd":
+        mod = ConvTranspose2d(128, 128, 5, stride=2, padding=2, output_padding=1).to(cuda)
+        x = torch.randn(B, 128, 64, 64, device=cuda)
+        with _autocast(True):
+            y = mod(x)
+        ref = F.conv_transpose2d(x.bfloat16().float(), mod.weight.bfloat16().float(), mod.bias, stride=2, padding=2,
+                                 output_padding=1)
+        assert relerr(y, ref) < 1e-2
+    else:
+        mod = Conv2d(128, 128, 5, stride=2, padding=2).to(cuda)
+        x = torch.randn(B, 128, 128, 128, device=cuda).requires_grad_()
+        g = torch.randn(B, 128, 64, 64, device=cuda)
+        with _autocast(True):
+            y = mod(x)
+        y.backward(g)
+        xr = x.detach().bfloat16().float().requires_grad_()
+        yr = F.conv2d(xr, mod.weight.detach().bfloat16().float(), mod.bias.detach(), stride=2, padding=2)
+        yr.backward(g.bfloat16().float())
+        assert relerr(x.grad, xr.grad) < 1e-2
