@@ -203,3 +203,40 @@ def test_multimodal_round_trip(cuda):
         ga2 = ChannelAffineFn.apply(m.fencoder2(dec_g["x_hat"]), gamma, beta)
         x_rec = m.fdecoder(CatFn.apply(res["x_feature_hat"], ga2)).clamp_(0, 1)
     assert torch.equal(dec_m["x_hat"], x_rec)
+
+
+def test_codec_rgbt_file_round_trip(cuda, tmp_path):
+    """codec_rgbt.py encode_image / decode_image through the container file: the Master stream decodes to the
+    same image as the in-memory decompress; bpp is the file size over the master's pixels."""
+    import warnings
+
+    from compressai.models import Guided_compresser, Master_compresser
+    from compressai.utils.codec_rgbt import decode_image, encode_image
+    from compressai.zoo import bmshj2018_hyperprior
+
+    torch.manual_seed(11)
+    g = Guided_compresser(channel=3).to(cuda).eval()
+    m = Master_compresser(width=64, height=64, channel=1).to(cuda).eval()
+    g.update()
+    m.update()
+    x = torch.rand(1, 1, 64, 64, generator=torch.Generator().manual_seed(12)).to(cuda)
+    rgb = torch.rand(1, 3, 128, 128, generator=torch.Generator().manual_seed(13)).to(cuda)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        path = tmp_path / "m.bin"
+        r = encode_image(x, [g, m], str(path), "Master_compresser", "mse", 3, guided=rgb)
+        assert r["bpp"] == path.stat().st_size * 8.0 / (64 * 64)
+        hdr, x_hat = decode_image(str(path), [g, m], guided=rgb)
+        assert hdr == ("Master_compresser", "mse", 3, (64, 64), 8)
+        dec_g = g.decompress(*(lambda e: (e["strings"], e["shape"]))(g.compress(rgb)))
+        ref = m.decompress(m.compress(x, dec_g["x_hat"]), dec_g)["x_hat"]
+        assert torch.equal(x_hat, ref)
+
+        net = bmshj2018_hyperprior(1, channel=3).to(cuda).eval()
+        net.update()
+        path = tmp_path / "h.bin"
+        encode_image(rgb, net, str(path), "bmshj2018-hyperprior", "mse", 1)
+        hdr, x_hat = decode_image(str(path), net)
+        enc = net.compress(rgb)
+        assert hdr.model == "bmshj2018-hyperprior"
+        assert torch.equal(x_hat, net.decompress(enc["strings"], enc["shape"])["x_hat"])

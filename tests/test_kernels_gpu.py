@@ -58,22 +58,28 @@ CONV_CASES = [
     ("conv", 2, 64, 256, 8, 8, 3, 1),
     ("conv", 2, 64, 12, 8, 8, 3, 1),
     ("conv", 1, 64, 1152, 4, 4, 3, 1),    # cheng2020 q6 h_s sub-pixel conv: > 1024 bias channels
+    # Spatial_aligner patch embedding / recovery (master.py:708-724): kernel = stride = 2, no padding
+    ("conv", 2, 64, 96, 32, 24, 2, 2, 0, 0),
+    ("conv", 2, 3, 96, 16, 16, 2, 2, 0, 0),
+    ("deconv", 2, 96, 64, 16, 12, 2, 2, 0, 0),
+    ("deconv", 2, 96, 3, 8, 8, 2, 2, 0, 0),
 ]
 
 
 @pytest.mark.parametrize("bf16", [False, True])
-@pytest.mark.parametrize("case", CONV_CASES, ids=[f"{c[0]}{c[2]}-{c[3]}k{c[6]}s{c[7]}" for c in CONV_CASES])
+@pytest.mark.parametrize("case", CONV_CASES, ids=[f"{c[0]}{c[2]}-{c[3]}k{c[6]}s{c[7]}" + (f"p{c[8]}" if len(c) > 8 else "") for c in CONV_CASES])
 def test_conv_fwd_bwd(cuda, case, bf16):
     from compressai.layers import Conv2d, ConvTranspose2d
 
-    kind, B, cin, cout, H, W, k, s = case
+    kind, B, cin, cout, H, W, k, s = case[:8]
+    pad, op = case[8:] if len(case) > 8 else (k // 2, s - 1)
     torch.manual_seed(0)
     if kind == "conv":
-        ref = nn.Conv2d(cin, cout, k, stride=s, padding=k // 2)
-        mod = Conv2d(cin, cout, k, stride=s, padding=k // 2)
+        ref = nn.Conv2d(cin, cout, k, stride=s, padding=pad)
+        mod = Conv2d(cin, cout, k, stride=s, padding=pad)
     else:
-        ref = nn.ConvTranspose2d(cin, cout, k, stride=s, padding=k // 2, output_padding=s - 1)
-        mod = ConvTranspose2d(cin, cout, k, stride=s, padding=k // 2, output_padding=s - 1)
+        ref = nn.ConvTranspose2d(cin, cout, k, stride=s, padding=pad, output_padding=op)
+        mod = ConvTranspose2d(cin, cout, k, stride=s, padding=pad, output_padding=op)
     mod.load_state_dict(ref.state_dict())
     mod = mod.to(cuda)
     x = torch.randn(B, cin, H, W)
