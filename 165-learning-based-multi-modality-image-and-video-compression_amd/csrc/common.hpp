@@ -95,4 +95,16 @@ __device__ __forceinline__ float block_sum(float v, float* smem) {
     return r;
 }
 
+// ---------------------------------------------------------------------------
+// counted waits as compiler builtins (gfx9 s_waitcnt encoding: vmcnt[3:0] + [15:14], expcnt[6:4],
+// lgkmcnt[11:8]).  Unlike inline asm these are visible to the waitcnt pass, which otherwise falls
+// back to lgkmcnt(0) before every later LDS-fragment use.
+// ---------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt");
+    __builtin_amdgcn_s_waitcnt(0x0F70 | (N & 15) | ((N >> 4) << 14));
+}
+__device__ __forceinline__ void wait_lgkmcnt0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
+
 }  // namespace cai

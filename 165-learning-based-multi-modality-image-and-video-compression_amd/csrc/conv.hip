@@ -152,9 +152,10 @@ __device__ __forceinline__ void store_out_scalar(const ConvArgs& a, const PhaseD
 // fp32 [BM][BN+4]; split-K writes the raw partial tile to ws[z][m][n] (bias /
 // act / mask applied by the reduce), otherwise bias + act (+ mask) and 16-byte
 // stores.  `E` must hold BM*(BN+4) floats and may alias the operand stages.
-template <typename T, int BM, int BN, int WM, int WN, int NTH>
-__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const PhaseDesc& P, int plane, int Mph, int m0,
-                                              int n0, float* E, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16]) {
+// rowm(row): the GEMM row m of tile row `row`, or -1 outside the phase
+template <typename T, int BM, int BN, int WM, int WN, int NTH, class RowMap>
+__device__ __forceinline__ void conv_epilogue_rows(const ConvArgs& a, const PhaseDesc& P, int plane, int n0, float* E,
+                                                   const f32x4 (&acc)[BM / WM / 16][BN / WN / 16], RowMap rowm) {
     constexpr int WTM = BM / WM, WTN = BN / WN;
     constexpr int TM = WTM / 16, TN = WTN / 16;
     constexpr int ES = BN + 4;
@@ -174,8 +175,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const PhaseDesc
         constexpr int cpr = BN / 4;
         for (int id = tid; id < BM * cpr; id += NTH) {
             const int row = id / cpr, cc = id - (id / cpr) * cpr;
-            const int m = m0 + row, n = n0 + cc * 4;
-            if (m >= Mph || n >= a.ws_ld) continue;
+            const int m = rowm(row), n = n0 + cc * 4;
+            if (m < 0 || n >= a.ws_ld) continue;
             *reinterpret_cast<f32x4*>(dst + (int64_t)m * a.ws_ld + n) =
                 *reinterpret_cast<const f32x4*>(E + row * ES + cc * 4);
         }
@@ -200,8 +201,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const PhaseDesc
         const int cpr = BN / VO;
         for (int id = tid; id < BM * cpr; id += NTH) {
             const int row = id / cpr, cc = id - (id / cpr) * cpr;
-            const int m = m0 + row, n = n0 + cc * VO;
-            if (m >= Mph || n >= a.Cout) continue;
+            const int m = rowm(row), n = n0 + cc * VO;
+            if (m < 0 || n >= a.Cout) continue;
             float v[8];
             const f32x4 lo = *reinterpret_cast<const f32x4*>(E + row * ES + cc * VO);
             f32x4 hi = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -213,11 +214,20 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const PhaseDesc
     } else {
         for (int id = tid; id < BM * BN; id += NTH) {
             const int col = id / BM, row = id - (id / BM) * BM;
-            const int m = m0 + row, n = n0 + col;
-            if (m >= Mph || n >= a.Cout) continue;
+            const int m = rowm(row), n = n0 + col;
+            if (m < 0 || n >= a.Cout) continue;
             store_out_scalar<T>(a, P, plane, m, n, E[row * ES + col]);
         }
     }
+}
+
+template <typename T, int BM, int BN, int WM, int WN, int NTH>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const PhaseDesc& P, int plane, int Mph, int m0,
+                                              int n0, float* E, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16]) {
+    conv_epilogue_rows<T, BM, BN, WM, WN, NTH>(a, P, plane, n0, E, acc, [=](int row) {
+        const int m = m0 + row;
+        return m < Mph ? m : -1;
+    });
 }
 
 template <typename T, typename C>
@@ -407,6 +417,21 @@ __device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
                                      (lvoid_ptr)(reinterpret_cast<uintptr_t>(lds_wave_base)), 16, 0, 0);
 }
 
+// The same DMA hidden from the compiler.  The waitcnt pass books an LDS DMA as an LDS event of unknown
+// order, so while one is in flight every later wait on a fragment read becomes lgkmcnt(0); issued from
+// inline asm it is invisible, and the ring's vmcnt waits are explicit anyway.  M0 carries the wave's LDS
+// base and is restored after the DMA (the compiler reserves it).
+__device__ __forceinline__ void glds16_asm(const void* g, const char* lds_wave_base) {
+    const unsigned lds = __builtin_amdgcn_readfirstlane((unsigned)reinterpret_cast<uintptr_t>(lds_wave_base));
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(lds)
+                 : "memory");
+}
+
+#define GLDS glds16_asm
+
 template <typename C>
 __global__ __launch_bounds__(512, 1) void conv_glds_kernel(const ConvArgs a) {
     constexpr int BM = C::BM, BN = C::BN, WM = C::WM, WN = C::WN;
@@ -474,12 +499,12 @@ __global__ __launch_bounds__(512, 1) void conv_glds_kernel(const ConvArgs a) {
             const int iy = ay[i] + dy, ix = ax[i] + dx;
             const bool ok = (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW;
             const void* src = ok ? (const void*)(X + abase[i] + delta) : (const void*)cai_zero_page;
-            glds16(src, sbase + i * 64 * 128);
+            GLDS(src, sbase + i * 64 * 128);
         }
 #pragma unroll
         for (int i = 0; i < BG; ++i) {
             const void* src = boff[i] >= 0 ? (const void*)(Wb + boff[i] + kg * 128) : (const void*)cai_zero_page;
-            glds16(src, sbase + BM * 128 + i * 64 * 128);
+            GLDS(src, sbase + BM * 128 + i * 64 * 128);
         }
     };
 
@@ -493,38 +518,293 @@ __global__ __launch_bounds__(512, 1) void conv_glds_kernel(const ConvArgs a) {
     if (nk > 1) issue(1, 1);
     for (int kt = 0; kt < nk; ++kt) {
         if (kt + 1 < nk)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+            wait_vmcnt<G>();
         else
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            wait_vmcnt<0>();
+        wait_lgkmcnt0();
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
-        if (kt + 2 < nk) issue(kt + 2, (kt + 2) % 3);
         const char* As = smem + (kt % 3) * C::STAGE;
         const char* Bs = As + BM * 128;
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            const int lsr = c * 4 + (lane >> 4);
-            u32x4 fa[TM], fb[TN];
+        // every fragment of the K-tile is requested up front; the second half's reads and the next
+        // DMA issue overlap the first half's MFMAs (one exposed LDS latency per K-tile, not four)
+        u32x4 fa[2][TM], fb[2][TN];
+        auto rd_a = [&](int c) {
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm) {
                 const int row = wm * WTM + tm * 16 + (lane & 15);
-                fa[tm] = *reinterpret_cast<const u32x4*>(As + row * 128 + swz(row, lsr) * 16);
+                fa[c][tm] = *reinterpret_cast<const u32x4*>(As + row * 128 + swz(row, c * 4 + (lane >> 4)) * 16);
             }
+        };
+        auto rd_b = [&](int c) {
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn) {
                 const int row = wn * WTN + tn * 16 + (lane & 15);
-                fb[tn] = *reinterpret_cast<const u32x4*>(Bs + row * 128 + swz(row, lsr) * 16);
+                fb[c][tn] = *reinterpret_cast<const u32x4*>(Bs + row * 128 + swz(row, c * 4 + (lane >> 4)) * 16);
             }
+        };
+        // lgkmcnt holds 15 reads: the first half's fragments and the second half's A go out first, the
+        // second half's B behind the first 16 MFMAs
+        rd_a(0);
+        rd_b(0);
+        rd_a(1);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * TM + TN, 0);
 #pragma unroll
-            for (int tm = 0; tm < TM; ++tm)
+        for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-                for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mma16<bf16>(fa[tm], fb[tn], acc[tm][tn]);
-        }
+            for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mma16<bf16>(fa[0][tm], fb[0][tn], acc[tm][tn]);
+        __builtin_amdgcn_sched_group_barrier(0x008, TM * TN, 0);
+        rd_b(1);
+        __builtin_amdgcn_sched_group_barrier(0x100, TN, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (kt + 2 < nk) issue(kt + 2, (kt + 2) % 3);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mma16<bf16>(fa[1][tm], fb[1][tn], acc[tm][tn]);
         __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();
     conv_epilogue<bf16, BM, BN, WM, WN, 512>(a, P, plane, Mph, m0, n0, reinterpret_cast<float*>(smem), acc);
+}
+
+// ---------------------------------------------------------------------------
+// Halo-staged implicit GEMM for the stride-2 gather convolutions (Conv2d k3/k5 s2 p=k/2 forward and the
+// matching ConvTranspose2d input gradient), bf16.  The tap-gather kernel above fetches every input pixel
+// once per tap (25 times for k5), and its speed is set by how fast a CU can pull bytes into LDS, not by
+// the MFMAs (a no-MFMA build of it runs within 1 % of the real one).  Here a block owns an 8 x 32 output
+// tile and all 128 output channels; per 32-channel chunk it stages the tile's input footprint
+// ((2*7+k) x (2*31+k) pixels) in LDS once, and the k*k taps read their A fragments from that patch at a
+// per-tap offset: the A bytes fetched per block drop ~4.5x.  The weights stream through a 4-stage
+// LDS-DMA ring (one 16-byte DMA per lane per tap, three taps ahead).
+//
+// Patch layout: four planes (8 channels each) of 16-byte cells; inside a plane, patch row r, column c
+// sits at r*PW + (c&1)*PWE + c/2 (even columns, then odd), so the 16 lanes of one A fragment (16
+// consecutive output columns, stride-2 input columns) read 16 consecutive cells.  PLANE = 4 (mod 16)
+// keeps the staging writes (4 pixels x 4 planes per 16 lanes) conflict-free too.  The next chunk's
+// patch is loaded into registers while the current one is consumed.
+// ---------------------------------------------------------------------------
+// loads issued after weight tap t+1 that step t's wait leaves in flight: taps t+2 .. t+NSTB-1, the patch
+// cells issued at steps j in [t+1-NSTB, t-1] (j < NPI), and the four fence loads that follow cell NPI-1
+__host__ __device__ constexpr int halo_younger(int t, int nstb, int npi) {
+    const int lo = t + 1 - nstb > 0 ? t + 1 - nstb : 0;
+    const int hi = t - 1 < npi - 1 ? t - 1 : npi - 1;
+    const int cells = hi >= lo ? hi - lo + 1 : 0;
+    const int fences = (npi - 1 >= t + 1 - nstb && npi - 1 <= t - 1) ? 4 : 0;
+    return nstb - 2 + cells + fences;
+}
+
+__device__ __forceinline__ void wait_vmcnt_n(int n) {    // n folds to a constant after unrolling
+    switch (n) {
+        case 0: wait_vmcnt<0>(); break;
+        case 1: wait_vmcnt<1>(); break;
+        case 2: wait_vmcnt<2>(); break;
+        case 3: wait_vmcnt<3>(); break;
+        case 4: wait_vmcnt<4>(); break;
+        case 5: wait_vmcnt<5>(); break;
+        case 6: wait_vmcnt<6>(); break;
+        case 7: wait_vmcnt<7>(); break;
+        case 8: wait_vmcnt<8>(); break;
+        case 9: wait_vmcnt<9>(); break;
+        case 10: wait_vmcnt<10>(); break;
+        case 11: wait_vmcnt<11>(); break;
+        case 12: wait_vmcnt<12>(); break;
+        case 13: wait_vmcnt<13>(); break;
+        case 14: wait_vmcnt<14>(); break;
+        default: wait_vmcnt<15>(); break;
+    }
+}
+
+template <int KS>
+struct HaloCfg {
+    static constexpr int TH = 8, TW = 32, BM = TH * TW, BN = 128, WM = 4, WN = 2, CK = 32;
+    static constexpr int PH = 2 * (TH - 1) + KS, PW = 2 * (TW - 1) + KS;
+    static constexpr int ODD = ((PW + 1) / 2 + 3) / 8 * 8 + 4;   // first odd-column cell of a row: = 4 (mod 8)
+    static constexpr int PWR = ODD + PW / 2;                      // cells per patch row
+    static constexpr int NPOS = PH * PW;
+    static constexpr int PLANE = (PH * PWR + 15) / 16 * 16;       // = 0 (mod 16)
+    static constexpr int PATCH = 4 * PLANE * 16;
+    static constexpr int NPI = (4 * NPOS + 511) / 512;
+    static constexpr int NTAP = KS * KS;
+    static constexpr int BSTAGE = BN * CK * 2, NSTB = KS;         // NTAP % NSTB == 0: a tap's stage is t % KS
+    static constexpr int EPI = BM * (BN + 4) * 4;
+    static constexpr int BYTES = (PATCH + NSTB * BSTAGE > EPI) ? PATCH + NSTB * BSTAGE : EPI;
+};
+
+template <int KS>
+__global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvArgs a, int tiles_x, int tiles_y) {
+    using H = HaloCfg<KS>;
+    constexpr int BM = H::BM, BN = H::BN, WM = H::WM, WN = H::WN;
+    constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
+    constexpr int NPI = H::NPI, NTAP = H::NTAP, NSTB = H::NSTB;
+    static_assert(WM * WN == 8 && WTM == 2 * H::TW && H::BYTES <= 160 * 1024 && NTAP > NSTB + 3, "halo tile");
+    __shared__ __attribute__((aligned(16))) char smem[H::BYTES];
+    char* const patch = smem;
+    char* const bring = smem + H::PATCH;
+
+    const PhaseDesc& P = a.ph[0];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    // consecutive tiles of an image on one XCD: their halos overlap in its L2
+    const int ntiles = gridDim.x;
+    const int bid = (ntiles & 7) == 0 ? (blockIdx.x & 7) * (ntiles >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+    const int per_img = tiles_x * tiles_y;
+    const int b = bid / per_img;
+    const int rt = bid - b * per_img;
+    const int ty0 = (rt / tiles_x) * H::TH, tx0 = (rt % tiles_x) * H::TW;
+    const int nch = a.Cin_pad / H::CK;
+    const int per = (nch + a.ksplit - 1) / a.ksplit;
+    const int c0 = blockIdx.z * per;
+    const int nc = max(0, min(nch, c0 + per) - c0);
+    const char* X = reinterpret_cast<const char*>(a.x);
+    const int ld_b = a.x_ld * 2;
+
+    // this thread's patch cells (8 pixels x 4 planes per 32 lanes), recomputed per chunk to keep them out
+    // of the loop's registers.  Chunk indices past the block's range load the zero page (the pipeline
+    // issues a patch batch after every chunk, so its wait counts stay fixed).
+    const int iyb = ty0 * 2 + P.dy0, ixb = tx0 * 2 + P.dx0;
+    u32x4 pr_[NPI];
+    unsigned fence_[4] = {0u, 0u, 0u, 0u};
+    auto load_cell = [&](int ci, int i) {
+        const bool real = ci < nc;
+        const int cc = c0 + ci;
+        const int q4 = tid + 512 * i, g = (q4 >> 3) & 3, q = ((q4 >> 5) << 3) | (q4 & 7);
+        const int pr = q / H::PW, pc = q - (q / H::PW) * H::PW;
+        const int iy = iyb + pr, ix = ixb + pc;
+        const bool in = real && q < H::NPOS && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW;
+        const void* src = in ? (const void*)(X + ((b * a.IH + iy) * a.IW + ix) * ld_b + g * 16 + cc * (H::CK * 2))
+                             : (const void*)cai_zero_page;
+        pr_[i] = *reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(reinterpret_cast<uintptr_t>(src));
+    };
+    // four compiler-visible loads behind a patch batch: the compiler's waits before the patch store then
+    // leave the (invisible) weight DMAs issued since in flight instead of draining them
+    auto fence_loads = [&]() {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            asm volatile("" ::"v"(fence_[j]));
+            fence_[j] = *reinterpret_cast<const __attribute__((address_space(1))) unsigned*>(
+                reinterpret_cast<uintptr_t>(cai_zero_page + 16 * j));
+        }
+    };
+    auto store_patch = [&]() {
+#pragma unroll
+        for (int i = 0; i < NPI; ++i) {
+            const int q4 = tid + 512 * i, g = (q4 >> 3) & 3, q = ((q4 >> 5) << 3) | (q4 & 7);
+            const int pr = q / H::PW, pc = q - (q / H::PW) * H::PW;
+            if (q < H::NPOS)
+                *reinterpret_cast<u32x4*>(patch + (g * H::PLANE + pr * H::PWR + (pc & 1) * H::ODD + (pc >> 1)) * 16) =
+                    pr_[i];
+        }
+    };
+
+    // weight ring: LDS cell p of a stage holds (n = p/4, 16-byte slot s) at p = 4n + (s ^ 3*((n/8) & 1)),
+    // conflict-free for ds_read_b128's lane groups.  Taps past the block's range read the zero page.
+    const int bp = wid * 64 + lane;
+    const int bn_ = bp >> 2, bs_ = (bp & 3) ^ (((bn_ >> 3) & 1) * 3);
+    const char* Wrow = bn_ < a.Npad ? reinterpret_cast<const char*>(a.w) + bn_ * a.Kp * 2 + bs_ * 16 : nullptr;
+    auto issue_b = [&](int ci, int t) {    // tap t of chunk ci into stage t % NSTB
+        const void* src = (Wrow && ci < nc) ? (const void*)(Wrow + (t * a.Cin_pad + (c0 + ci) * H::CK) * 2)
+                                            : (const void*)cai_zero_page;
+        glds16_asm(src, bring + (t % NSTB) * H::BSTAGE + wid * 1024);
+    };
+
+    // per-lane fragment cells
+    const int g_ = lane >> 4, i16 = lane & 15;
+    int apos[TM];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+        const int r = wm * WTM + tm * 16 + i16;
+        apos[tm] = (g_ * H::PLANE + 2 * (r / H::TW) * H::PWR + (r % H::TW)) * 16;
+    }
+    int bpos[TN];
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+        const int n = wn * WTN + tn * 16 + i16;
+        bpos[tn] = H::PATCH + (4 * n + (g_ ^ (((n >> 3) & 1) * 3))) * 16;
+    }
+    auto read_frags = [&](int t, u32x4 (&fa)[TM], u32x4 (&fb)[TN]) {
+        const int ty = t / KS, tx = t % KS;
+        const int toff = (ty * H::PWR + (tx & 1) * H::ODD + (tx >> 1)) * 16;
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) fa[tm] = *reinterpret_cast<const u32x4*>(smem + apos[tm] + toff);
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+            fb[tn] = *reinterpret_cast<const u32x4*>(smem + bpos[tn] + (t % NSTB) * H::BSTAGE);
+    };
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // Step (ci, t) multiplies the fragments read during the previous step while the next step's are read.
+    // Its wait retires weight tap t+1; tap t+NSTB then streams into the stage tap t has left.  The next
+    // chunk's patch is loaded one cell per step over the first NPI steps (a batch would hold up the taps
+    // issued after it: vmcnt retires in issue order), and stored at the chunk's last step.  Every step
+    // issues one tap and every chunk one patch (zero page past the block's range), so the number of
+    // loads younger than tap t+1 depends on t alone (halo_younger).
+    u32x4 fa[TM], fb[TN];
+    if (nc > 0) {
+#pragma unroll
+        for (int i = 0; i < NPI; ++i) load_cell(0, i);
+#pragma unroll
+        for (int t = 0; t < NSTB; ++t) issue_b(0, t);
+        store_patch();
+        wait_vmcnt<NSTB - 1>();
+        wait_lgkmcnt0();
+        __builtin_amdgcn_s_barrier();
+        read_frags(0, fa, fb);
+    }
+    for (int ci = 0; ci < nc; ++ci) {
+#pragma unroll
+        for (int t = 0; t < NTAP; ++t) {
+            wait_vmcnt_n(halo_younger(t, NSTB, NPI));
+            wait_lgkmcnt0();
+            __builtin_amdgcn_s_barrier();
+            if (t == NTAP - 1) {
+                // every wave has read its last fragment of this chunk: stage the next chunk's patch
+                store_patch();
+                wait_lgkmcnt0();
+                __builtin_amdgcn_s_barrier();
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (t + NSTB < NTAP)
+                issue_b(ci, t + NSTB);
+            else
+                issue_b(ci + 1, t + NSTB - NTAP);
+            if (t < NPI) load_cell(ci + 1, t);    // the next chunk's patch, one cell per step
+            if (t == NPI - 1) fence_loads();
+            u32x4 na[TM], nb[TN];
+            read_frags(t + 1 == NTAP ? 0 : t + 1, na, nb);
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mma16<bf16>(fa[tm], fb[tn], acc[tm][tn]);
+            // the next step's reads (separate registers) alternate with this step's first MFMAs (measured:
+            // a read burst ahead of the MFMAs, or reads every other MFMA, ran 2-6 % slower)
+#pragma unroll
+            for (int i = 0; i < TM + TN; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, TM * TN - (TM + TN), 0);
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm) fa[tm] = na[tm];
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) fb[tn] = nb[tn];
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    wait_vmcnt<0>();
+    asm volatile("" ::"v"(fence_[0]), "v"(fence_[1]), "v"(fence_[2]), "v"(fence_[3]));
+    __syncthreads();
+    const int plane = P.OHg * P.OWg;
+    conv_epilogue_rows<bf16, BM, BN, WM, WN, 512>(a, P, plane, 0, reinterpret_cast<float*>(smem), acc, [=](int row) {
+        const int oy = ty0 + row / H::TW, ox = tx0 + row % H::TW;
+        return (oy < P.OHg && ox < P.OWg) ? b * plane + oy * P.OWg + ox : -1;
+    });
 }
 
 // split-K reduce: out = epilogue(sum_s ws[ph*S + s][m][n]) in a fixed order
@@ -1040,10 +1320,10 @@ __global__ __launch_bounds__(512, 1) void wgrad_glds_kernel(const WgradArgs a) {
     if (nsteps > 1) issue(1, 1);
     for (int st = 0; st < nsteps; ++st) {
         if (st + 1 < nsteps)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+            wait_vmcnt<G>();
         else
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            wait_vmcnt<0>();
+        wait_lgkmcnt0();
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
         if (st + 2 < nsteps) issue(st + 2, (st + 2) % 3);
@@ -1367,13 +1647,46 @@ static bool glds_eligible(const Plan& P, int dtype, int in_abs) {
 struct ConvLaunch {
     int cfg, BM, BN, mtiles, ntiles, mmax, ksplit, ws_ld;
     bool glds;
+    int halo, tiles_x, tiles_y;    // halo: kernel size of the halo-staged path (0: not taken)
     size_t ws_bytes;
 };
+
+// the halo-staged kernel: stride-2 gather convolutions with k in {3, 5}, pad k/2, <= 128 output channels
+static bool halo_off() {
+    static const bool off = [] {
+        const char* e = getenv("CAI_HALO_OFF");
+        return e && *e && *e != '0';
+    }();
+    return off;
+}
+static int halo_ks(const cai_conv_geom* g, const Plan& P, bool glds) {
+    if (!glds || P.phase || halo_off() || g->stride != 2 || (g->kernel != 3 && g->kernel != 5) ||
+        g->pad != g->kernel / 2 || P.Cin_pad % 32 != 0 || P.kout_c > 128 || P.OHg[0] < 8 || P.OWg[0] < 32)
+        return 0;
+    return g->kernel;
+}
 
 static ConvLaunch conv_launch(const cai_conv_geom* g, int dtype, int direction, int in_abs) {
     const Plan P = make_plan(g, dtype, direction);
     ConvLaunch L{};
     L.glds = glds_eligible(P, dtype, in_abs);
+    L.halo = halo_ks(g, P, L.glds);
+    if (L.halo) {
+        L.BM = 256;
+        L.BN = 128;
+        L.tiles_x = (P.OWg[0] + 31) / 32;
+        L.tiles_y = (P.OHg[0] + 7) / 8;
+        L.mmax = g->batch * P.OHg[0] * P.OWg[0];
+        L.mtiles = g->batch * L.tiles_x * L.tiles_y;
+        L.ntiles = 1;
+        const int nch = P.Cin_pad / 32;
+        L.ksplit = L.mtiles >= 256 ? 1 : std::min(nch, (256 + L.mtiles - 1) / L.mtiles);
+        // every split gets a chunk: per = ceil(nch / ks) must leave no empty split
+        while (L.ksplit > 1 && (L.ksplit - 1) * ((nch + L.ksplit - 1) / L.ksplit) >= nch) --L.ksplit;
+        L.ws_ld = 128;
+        L.ws_bytes = L.ksplit > 1 ? (size_t)L.ksplit * L.mmax * L.ws_ld * sizeof(float) : 0;
+        return L;
+    }
     L.cfg = L.glds ? pick_cfg_glds(P.kout_c, P.nphase, L.BM, L.BN) : pick_cfg(P.kout_c, L.BM, L.BN);
     int kmax = 0;
     for (int ph = 0; ph < P.nphase; ++ph) {
@@ -1419,9 +1732,27 @@ static void launch_conv_glds(const ConvArgs& a, const ConvLaunch& L, hipStream_t
     }
 }
 
+static void launch_conv_halo(const ConvArgs& a, const ConvLaunch& L, hipStream_t st) {
+    dim3 grid(L.mtiles, 1, a.ksplit);
+    if (L.halo == 5)
+        hipLaunchKernelGGL(conv_halo_kernel<5>, grid, dim3(512), 0, st, a, L.tiles_x, L.tiles_y);
+    else
+        hipLaunchKernelGGL(conv_halo_kernel<3>, grid, dim3(512), 0, st, a, L.tiles_x, L.tiles_y);
+    if (a.ksplit > 1) {
+        const int VO = (a.y_vec && a.y_dtype == CAI_BF16) ? 8 : 4;
+        const int64_t total = (int64_t)L.mmax * ((a.Cout + VO - 1) / VO);
+        const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, (total + 255) / 256));
+        hipLaunchKernelGGL((conv_splitk_reduce_kernel<bf16>), dim3(gx, 1), dim3(256), 0, st, a);
+    }
+}
+
 template <typename T>
 static void dispatch_conv(const ConvArgs& a, const ConvLaunch& L, hipStream_t st) {
     if constexpr (sizeof(T) == 2) {
+        if (L.halo) {
+            launch_conv_halo(a, L, st);
+            return;
+        }
         switch (L.cfg) {
             case CFG_G1: launch_conv_glds<CfgG1>(a, L, st); return;
             case CFG_G2: launch_conv_glds<CfgG2>(a, L, st); return;

@@ -576,10 +576,10 @@ __global__ __launch_bounds__(NT, 1) void edge_wgrad_dma_kernel(const EdgeArgs A)
     if (nsteps > 1) issue(1, 1);
     for (int st = 0; st < nsteps; ++st) {
         if (st + 1 < nsteps)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WG) : "memory");
+            wait_vmcnt<WG>();
         else
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            wait_vmcnt<0>();
+        wait_lgkmcnt0();
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
         if (st + 2 < nsteps) issue(st + 2, (st + 2) % 3);

@@ -63,7 +63,7 @@ def dominant_kernel_roofline(B, size, reps=20):
     """g_a[2]: Conv2d(128,128,k5,s2,p2) at (size/2)^2 -> (size/4)^2, bf16 implicit GEMM."""
     H = size // 2
     r = conv_roofline(B, 128, H, H, 128, 5, 2, reps)
-    r["kernel"] = ("conv_glds_kernel<256x128> (g_a[2] fwd: Conv2d 128->128 k5 s2, %dx%d->%dx%d, B=%d)"
+    r["kernel"] = ("conv_halo_kernel<5> (g_a[2] fwd: Conv2d 128->128 k5 s2, %dx%d->%dx%d, B=%d)"
                    % (H, H, H // 2, H // 2, B))
     r["traffic"] = pmc_traffic(B, size)
     return r

@@ -58,6 +58,11 @@ CONV_CASES = [
     ("conv", 2, 64, 256, 8, 8, 3, 1),
     ("conv", 2, 64, 12, 8, 8, 3, 1),
     ("conv", 1, 64, 1152, 4, 4, 3, 1),    # cheng2020 q6 h_s sub-pixel conv: > 1024 bias channels
+    # halo-staged stride-2 gather kernel: partial column tiles, split-K over 32-channel chunks, k3, Cout < 128
+    ("conv", 2, 128, 128, 64, 96, 5, 2),
+    ("conv", 2, 96, 40, 40, 70, 3, 2),
+    ("deconv", 2, 128, 128, 32, 32, 5, 2),
+    ("deconv", 1, 96, 64, 20, 36, 3, 2),
     # Spatial_aligner patch embedding / recovery (master.py:708-724): kernel = stride = 2, no padding
     ("conv", 2, 64, 96, 32, 24, 2, 2, 0, 0),
     ("conv", 2, 3, 96, 16, 16, 2, 2, 0, 0),
@@ -509,3 +514,32 @@ def test_multiphase_conv(cuda, kind):
         yr = F.conv2d(xr, mod.weight.detach().bfloat16().float(), mod.bias.detach(), stride=2, padding=2)
         yr.backward(g.bfloat16().float())
         assert relerr(x.grad, xr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("B", [16, 14])
+def test_halo_conv_full(cuda, B):
+    """Full-size stride-2 gather GEMMs on the halo-staged kernel: the C2 g_a[2] forward (Conv2d 128->128 k5 s2,
+    128^2 -> 64^2; B=16 is one block per CU, B=14 splits K over two chunk ranges) and the g_s[4] input gradient
+    (ConvTranspose2d 128->128 k5 s2, the same gather).  Reference: torch fp32 on the GPU over the same
+    bf16-rounded operands; relative max error <= 1e-2."""
+    from compressai.layers import Conv2d, ConvTranspose2d
+
+    torch.manual_seed(5)
+    mod = Conv2d(128, 128, 5, stride=2, padding=2).to(cuda)
+    x = torch.randn(B, 128, 128, 128, device=cuda)
+    with _autocast(True):
+        y = mod(x)
+    ref = F.conv2d(x.bfloat16().float(), mod.weight.bfloat16().float(), mod.bias, stride=2, padding=2)
+    assert relerr(y, ref) < 1e-2
+
+    dec = ConvTranspose2d(128, 128, 5, stride=2, padding=2, output_padding=1).to(cuda)
+    xs = torch.randn(B, 128, 64, 64, device=cuda).requires_grad_()
+    g = torch.randn(B, 128, 128, 128, device=cuda)
+    with _autocast(True):
+        ys = dec(xs)
+    ys.backward(g)
+    xr = xs.detach().bfloat16().float().requires_grad_()
+    yr = F.conv_transpose2d(xr, dec.weight.detach().bfloat16().float(), dec.bias.detach(), stride=2, padding=2,
+                            output_padding=1)
+    yr.backward(g.bfloat16().float())
+    assert relerr(xs.grad, xr.grad) < 1e-2

@@ -13,7 +13,7 @@ import json
 import os
 import sys
 
-KERNEL = "conv_glds_kernel"
+KERNEL = "conv_halo_kernel"
 
 
 def per_dispatch(d, counter):
@@ -35,7 +35,7 @@ def main():
     w_kib = sum(write) / len(write)
     rd = 2.0 * f_kib * 1024
     wr = w_kib * 1024
-    print(json.dumps({"kernel": KERNEL + "<256x128> g_a[2] fwd", "batch": 16, "size": 256,
+    print(json.dumps({"kernel": KERNEL + "<5> g_a[2] fwd", "batch": 16, "size": 256,
                       "dispatches": [len(fetch), len(write)], "fetch_size_kib": round(f_kib, 1),
                       "write_size_kib": round(w_kib, 1), "read_bytes_per_launch": round(rd),
                       "write_bytes_per_launch": round(wr), "hbm_bytes_per_launch": round(rd + wr),
