@@ -65,7 +65,7 @@ def dominant_kernel_roofline(B, size, reps=20):
     r = conv_roofline(B, 128, H, H, 128, 5, 2, reps)
     r["kernel"] = ("conv_halo_kernel<5> (g_a[2] fwd: Conv2d 128->128 k5 s2, %dx%d->%dx%d, B=%d)"
                    % (H, H, H // 2, H // 2, B))
-    r["traffic"] = pmc_traffic(B, size)
+    r["traffic"] = pmc_traffic(B, size, r["kernel"].split()[0])
     return r
 
 
@@ -110,7 +110,7 @@ def conv_roofline(B, C, H, W, N, k, stride, reps=20):
             "algorithmic_bytes_per_launch": B * H * W * C * 2 + N * C * k * k * 2 + B * OH * OW * N * 2}
 
 
-def pmc_traffic(B, size):
+def pmc_traffic(B, size, kernel):
     """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC passes
     (profiles/pmc_traffic.json, written by tools/pmc_summary.py: 2 x FETCH_SIZE + WRITE_SIZE,
     MI355X_MICROARCH.md 'HBM'); null when no measurement for this workload is committed."""
@@ -119,7 +119,7 @@ def pmc_traffic(B, size):
         rec = json.load(open(path))
     except (OSError, ValueError):
         return None
-    if rec.get("batch") != B or rec.get("size") != size:
+    if rec.get("batch") != B or rec.get("size") != size or rec.get("kernel", "").split()[0] != kernel:
         return None
     return rec.get("hbm_bytes_per_launch")
 
