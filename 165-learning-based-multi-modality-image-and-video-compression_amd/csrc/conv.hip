@@ -807,6 +807,207 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvArgs a, int
     });
 }
 
+// Halo-staged s^2-phase implicit GEMM for the stride-2 k5 transposed convolutions (ConvTranspose2d k5 s2 p2
+// op1 forward and the matching Conv2d k5 s2 p2 input gradient), bf16.  Output phase (py, px) is a stride-1
+// convolution of the input with NA x NC taps (3x3, 3x2, 2x3, 2x2 for the four phases), and all of a phase's
+// taps read inside the input footprint of its output tile.  A block owns an 8 x 32 tile of one phase's
+// output grid and all 128 output channels; per 64-channel chunk it stages the footprint ((8+NA-1) x
+// (32+NC-1) pixels, eight planes of 8 channels, rows contiguous so one A fragment reads 16 consecutive
+// cells) in LDS once and runs the NA*NC taps x two 32-channel halves out of it.  The weights stream through
+// the same hand-ordered LDS-DMA ring as conv_halo_kernel (one 16-byte DMA per lane per step, NSTB-1 steps
+// ahead); the next chunk's footprint is loaded into registers while the current one is consumed.
+template <int NA, int NC>
+struct HaloPhCfg {
+    static constexpr int TH = 8, TW = 32, BM = TH * TW, BN = 128, WM = 4, WN = 2, CK = 64;
+    static constexpr int PH = TH + NA - 1, PW = TW + NC - 1;
+    static constexpr int NPOS = PH * PW;
+    static constexpr int PLANE = (NPOS + 15) / 16 * 16;       // = 0 (mod 16): conflict-free fragment reads
+    static constexpr int PATCH = 8 * PLANE * 16;
+    static constexpr int NPI = (8 * NPOS + 511) / 512;
+    static constexpr int NTAP = NA * NC, NST = 2 * NTAP;       // steps per chunk: (half, tap)
+    static constexpr int NSTB = NST % 3 == 0 ? 3 : 2;         // NST % NSTB == 0: a step's stage is t % NSTB
+    static constexpr int BSTAGE = BN * 32 * 2;
+    static constexpr int EPI = BM * (BN + 4) * 4;
+    static constexpr int BYTES = (PATCH + NSTB * BSTAGE > EPI) ? PATCH + NSTB * BSTAGE : EPI;
+    static_assert(NPI <= NST - NSTB, "the next chunk's footprint must retire before the chunk's last step");
+};
+
+template <int NA, int NC>
+__device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* smem, int ph, int split,
+                                                     int tiles_x, int tiles_y) {
+    using H = HaloPhCfg<NA, NC>;
+    constexpr int BM = H::BM, BN = H::BN, WM = H::WM, WN = H::WN;
+    constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
+    constexpr int NPI = H::NPI, NTAP = H::NTAP, NST = H::NST, NSTB = H::NSTB;
+    static_assert(WM * WN == 8 && WTM == 2 * H::TW && H::BYTES <= 160 * 1024, "halo phase tile");
+    char* const patch = smem;
+    char* const bring = smem + H::PATCH;
+
+    const PhaseDesc& P = a.ph[ph];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    const int ntiles = gridDim.x;
+    const int bid = (ntiles & 7) == 0 ? (blockIdx.x & 7) * (ntiles >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+    const int per_img = tiles_x * tiles_y;
+    const int b = bid / per_img;
+    const int rt = bid - b * per_img;
+    const int ty0 = (rt / tiles_x) * H::TH, tx0 = (rt % tiles_x) * H::TW;
+    const int nch = a.Cin_pad / H::CK;
+    const int per = (nch + a.ksplit - 1) / a.ksplit;
+    const int c0 = split * per;
+    const int nc = max(0, min(nch, c0 + per) - c0);
+    const char* X = reinterpret_cast<const char*>(a.x);
+    const int ld_b = a.x_ld * 2;
+
+    // tap (ty, tx) reads input (qy + dy0 - ty, qx + dx0 - tx): the footprint starts NA-1 rows / NC-1 columns
+    // before the tile's dy0/dx0 offset
+    const int iyb = ty0 + P.dy0 - (NA - 1), ixb = tx0 + P.dx0 - (NC - 1);
+    u32x4 pr_[NPI];
+    unsigned fence_[4] = {0u, 0u, 0u, 0u};
+    auto load_cell = [&](int ci, int i) {
+        const bool real = ci < nc;
+        const int cc = c0 + ci;
+        const int q8 = tid + 512 * i, g = (q8 >> 3) & 7, q = ((q8 >> 6) << 3) | (q8 & 7);
+        const int pr = q / H::PW, pc = q - (q / H::PW) * H::PW;
+        const int iy = iyb + pr, ix = ixb + pc;
+        const bool in = real && q < H::NPOS && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW;
+        const void* src = in ? (const void*)(X + ((b * a.IH + iy) * a.IW + ix) * ld_b + g * 16 + cc * (H::CK * 2))
+                             : (const void*)cai_zero_page;
+        pr_[i] = *reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(reinterpret_cast<uintptr_t>(src));
+    };
+    auto fence_loads = [&]() {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            asm volatile("" ::"v"(fence_[j]));
+            fence_[j] = *reinterpret_cast<const __attribute__((address_space(1))) unsigned*>(
+                reinterpret_cast<uintptr_t>(cai_zero_page + 16 * j));
+        }
+    };
+    auto store_patch = [&]() {
+#pragma unroll
+        for (int i = 0; i < NPI; ++i) {
+            const int q8 = tid + 512 * i, g = (q8 >> 3) & 7, q = ((q8 >> 6) << 3) | (q8 & 7);
+            if (q < H::NPOS) *reinterpret_cast<u32x4*>(patch + (g * H::PLANE + q) * 16) = pr_[i];
+        }
+    };
+
+    const int bp = wid * 64 + lane;
+    const int bn_ = bp >> 2, bs_ = (bp & 3) ^ (((bn_ >> 3) & 1) * 3);
+    const char* Wrow =
+        bn_ < a.Npad ? reinterpret_cast<const char*>(a.w) + (P.w_off + (int64_t)bn_ * a.Kp) * 2 + bs_ * 16 : nullptr;
+    auto issue_b = [&](int ci, int t) {    // step t = (half t / NTAP, tap t % NTAP) of chunk ci into stage t % NSTB
+        const int hf = t / NTAP, tap = t - hf * NTAP;
+        const void* src = (Wrow && ci < nc)
+                              ? (const void*)(Wrow + (tap * a.Cin_pad + (c0 + ci) * H::CK + hf * 32) * 2)
+                              : (const void*)cai_zero_page;
+        glds16_asm(src, bring + (t % NSTB) * H::BSTAGE + wid * 1024);
+    };
+
+    const int g_ = lane >> 4, i16 = lane & 15;
+    int apos[TM];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+        const int r = wm * WTM + tm * 16 + i16;
+        apos[tm] = (g_ * H::PLANE + (r / H::TW) * H::PW + (r % H::TW)) * 16;
+    }
+    int bpos[TN];
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+        const int n = wn * WTN + tn * 16 + i16;
+        bpos[tn] = H::PATCH + (4 * n + (g_ ^ (((n >> 3) & 1) * 3))) * 16;
+    }
+    auto read_frags = [&](int t, u32x4 (&fa)[TM], u32x4 (&fb)[TN]) {
+        const int hf = t / NTAP, tap = t - hf * NTAP;
+        const int ty = tap / NC, tx = tap - (tap / NC) * NC;
+        const int toff = (hf * 4 * H::PLANE + (NA - 1 - ty) * H::PW + (NC - 1 - tx)) * 16;
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) fa[tm] = *reinterpret_cast<const u32x4*>(smem + apos[tm] + toff);
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+            fb[tn] = *reinterpret_cast<const u32x4*>(smem + bpos[tn] + (t % NSTB) * H::BSTAGE);
+    };
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // the step pipeline of conv_halo_kernel, NST steps per chunk
+    u32x4 fa[TM], fb[TN];
+    if (nc > 0) {
+#pragma unroll
+        for (int i = 0; i < NPI; ++i) load_cell(0, i);
+#pragma unroll
+        for (int t = 0; t < NSTB; ++t) issue_b(0, t);
+        store_patch();
+        wait_vmcnt<NSTB - 1>();
+        wait_lgkmcnt0();
+        __builtin_amdgcn_s_barrier();
+        read_frags(0, fa, fb);
+    }
+    for (int ci = 0; ci < nc; ++ci) {
+#pragma unroll
+        for (int t = 0; t < NST; ++t) {
+            wait_vmcnt_n(halo_younger(t, NSTB, NPI));
+            wait_lgkmcnt0();
+            __builtin_amdgcn_s_barrier();
+            if (t == NST - 1) {
+                store_patch();
+                wait_lgkmcnt0();
+                __builtin_amdgcn_s_barrier();
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (t + NSTB < NST)
+                issue_b(ci, t + NSTB);
+            else
+                issue_b(ci + 1, t + NSTB - NST);
+            if (t < NPI) load_cell(ci + 1, t);
+            if (t == NPI - 1) fence_loads();
+            u32x4 na[TM], nb[TN];
+            read_frags(t + 1 == NST ? 0 : t + 1, na, nb);
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mma16<bf16>(fa[tm], fb[tn], acc[tm][tn]);
+#pragma unroll
+            for (int i = 0; i < TM + TN; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, TM * TN - (TM + TN), 0);
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm) fa[tm] = na[tm];
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) fb[tn] = nb[tn];
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    wait_vmcnt<0>();
+    asm volatile("" ::"v"(fence_[0]), "v"(fence_[1]), "v"(fence_[2]), "v"(fence_[3]));
+    __syncthreads();
+    const int plane = P.OHg * P.OWg;
+    conv_epilogue_rows<bf16, BM, BN, WM, WN, 512>(a, P, plane, 0, reinterpret_cast<float*>(smem), acc, [=](int row) {
+        const int oy = ty0 + row / H::TW, ox = tx0 + row % H::TW;
+        return (oy < P.OHg && ox < P.OWg) ? b * plane + oy * P.OWg + ox : -1;
+    });
+}
+
+// grid: x = output tiles of one phase, z = phase * ksplit + split (the split-K slab index of the epilogue)
+__global__ __launch_bounds__(512, 1) void conv_halo_phase_kernel(const ConvArgs a, int tiles_x, int tiles_y) {
+    constexpr int BYTES = HaloPhCfg<3, 3>::BYTES > HaloPhCfg<2, 2>::BYTES ? HaloPhCfg<3, 3>::BYTES
+                                                                           : HaloPhCfg<2, 2>::BYTES;
+    static_assert(BYTES >= HaloPhCfg<3, 2>::BYTES && BYTES >= HaloPhCfg<2, 3>::BYTES, "halo phase LDS");
+    __shared__ __attribute__((aligned(16))) char smem[BYTES];
+    const int ph = blockIdx.z / a.ksplit, split = blockIdx.z - ph * a.ksplit;
+    switch (ph) {    // k5 s2 p2 phases: (py, px) = (0,0) 3x3, (0,1) 3x2, (1,0) 2x3, (1,1) 2x2 taps
+        case 0: conv_halo_phase_body<3, 3>(a, smem, 0, split, tiles_x, tiles_y); break;
+        case 1: conv_halo_phase_body<3, 2>(a, smem, 1, split, tiles_x, tiles_y); break;
+        case 2: conv_halo_phase_body<2, 3>(a, smem, 2, split, tiles_x, tiles_y); break;
+        default: conv_halo_phase_body<2, 2>(a, smem, 3, split, tiles_x, tiles_y); break;
+    }
+}
+
 // split-K reduce: out = epilogue(sum_s ws[ph*S + s][m][n]) in a fixed order
 template <typename T>
 __global__ __launch_bounds__(256) void conv_splitk_reduce_kernel(const ConvArgs a) {
@@ -1648,6 +1849,7 @@ struct ConvLaunch {
     int cfg, BM, BN, mtiles, ntiles, mmax, ksplit, ws_ld;
     bool glds;
     int halo, tiles_x, tiles_y;    // halo: kernel size of the halo-staged path (0: not taken)
+    bool halo_ph;                  // the halo-staged s^2-phase path (k5 s2 p2 transposed direction)
     size_t ws_bytes;
 };
 
@@ -1666,11 +1868,46 @@ static int halo_ks(const cai_conv_geom* g, const Plan& P, bool glds) {
     return g->kernel;
 }
 
+// the halo-staged phase kernel: the s^2-phase direction of k5 s2 p2 (phase taps 3x3, 3x2, 2x3, 2x2),
+// 64-channel input chunks, <= 128 output channels
+static bool halo_phase_off() {
+    static const bool off = [] {
+        const char* e = getenv("CAI_HALO_PH_OFF");
+        return e && *e && *e != '0';
+    }();
+    return off;
+}
+static bool halo_phase_ok(const cai_conv_geom* g, const Plan& P, bool glds) {
+    static const int nt[4] = {9, 6, 6, 4}, nx[4] = {3, 2, 3, 2};
+    if (!glds || !P.phase || halo_off() || halo_phase_off() || P.nphase != 4 || g->stride != 2 || g->kernel != 5 || g->pad != 2 ||
+        P.Cin_pad % 64 != 0 || P.kout_c > 128 || P.OHg[0] < 8 || P.OWg[0] < 32)
+        return false;
+    for (int ph = 0; ph < 4; ++ph)
+        if (P.ntaps[ph] != nt[ph] || P.ntx[ph] != nx[ph]) return false;
+    return true;
+}
+
 static ConvLaunch conv_launch(const cai_conv_geom* g, int dtype, int direction, int in_abs) {
     const Plan P = make_plan(g, dtype, direction);
     ConvLaunch L{};
     L.glds = glds_eligible(P, dtype, in_abs);
     L.halo = halo_ks(g, P, L.glds);
+    L.halo_ph = !L.halo && halo_phase_ok(g, P, L.glds);
+    if (L.halo_ph) {
+        L.BM = 256;
+        L.BN = 128;
+        L.tiles_x = (P.OWg[0] + 31) / 32;
+        L.tiles_y = (P.OHg[0] + 7) / 8;
+        for (int ph = 0; ph < 4; ++ph) L.mmax = std::max(L.mmax, g->batch * P.OHg[ph] * P.OWg[ph]);
+        L.mtiles = g->batch * L.tiles_x * L.tiles_y;
+        L.ntiles = 1;
+        const int nch = P.Cin_pad / 64, blocks = 4 * L.mtiles;
+        L.ksplit = blocks >= 256 ? 1 : std::min(nch, (256 + blocks - 1) / blocks);
+        while (L.ksplit > 1 && (L.ksplit - 1) * ((nch + L.ksplit - 1) / L.ksplit) >= nch) --L.ksplit;
+        L.ws_ld = 128;
+        L.ws_bytes = L.ksplit > 1 ? (size_t)4 * L.ksplit * L.mmax * L.ws_ld * sizeof(float) : 0;
+        return L;
+    }
     if (L.halo) {
         L.BM = 256;
         L.BN = 128;
@@ -1746,11 +1983,26 @@ static void launch_conv_halo(const ConvArgs& a, const ConvLaunch& L, hipStream_t
     }
 }
 
+static void launch_conv_halo_phase(const ConvArgs& a, const ConvLaunch& L, hipStream_t st) {
+    hipLaunchKernelGGL(conv_halo_phase_kernel, dim3(L.mtiles, 1, 4 * a.ksplit), dim3(512), 0, st, a, L.tiles_x,
+                       L.tiles_y);
+    if (a.ksplit > 1) {
+        const int VO = (a.y_vec && a.y_dtype == CAI_BF16) ? 8 : 4;
+        const int64_t total = (int64_t)L.mmax * ((a.Cout + VO - 1) / VO);
+        const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, (total + 255) / 256));
+        hipLaunchKernelGGL((conv_splitk_reduce_kernel<bf16>), dim3(gx, 4), dim3(256), 0, st, a);
+    }
+}
+
 template <typename T>
 static void dispatch_conv(const ConvArgs& a, const ConvLaunch& L, hipStream_t st) {
     if constexpr (sizeof(T) == 2) {
         if (L.halo) {
             launch_conv_halo(a, L, st);
+            return;
+        }
+        if (L.halo_ph) {
+            launch_conv_halo_phase(a, L, st);
             return;
         }
         switch (L.cfg) {

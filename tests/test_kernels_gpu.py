@@ -63,6 +63,11 @@ CONV_CASES = [
     ("conv", 2, 96, 40, 40, 70, 3, 2),
     ("deconv", 2, 128, 128, 32, 32, 5, 2),
     ("deconv", 1, 96, 64, 20, 36, 3, 2),
+    # halo-staged s^2-phase kernel (ConvTranspose2d k5 s2 forward, Conv2d k5 s2 input gradient): 64-channel
+    # chunks split over K, partial row / column tiles, Cout < 128, 192 input channels
+    ("deconv", 2, 192, 128, 16, 40, 5, 2),
+    ("deconv", 2, 64, 64, 20, 36, 5, 2),
+    ("conv", 2, 96, 192, 48, 64, 5, 2),
     # Spatial_aligner patch embedding / recovery (master.py:708-724): kernel = stride = 2, no padding
     ("conv", 2, 64, 96, 32, 24, 2, 2, 0, 0),
     ("conv", 2, 3, 96, 16, 16, 2, 2, 0, 0),
@@ -518,19 +523,25 @@ def test_multiphase_conv(cuda, kind):
 
 @pytest.mark.parametrize("B", [16, 14])
 def test_halo_conv_full(cuda, B):
-    """Full-size stride-2 gather GEMMs on the halo-staged kernel: the C2 g_a[2] forward (Conv2d 128->128 k5 s2,
+    """Full-size stride-2 GEMMs on the halo-staged kernels: the C2 g_a[2] forward (Conv2d 128->128 k5 s2,
     128^2 -> 64^2; B=16 is one block per CU, B=14 splits K over two chunk ranges) and the g_s[4] input gradient
-    (ConvTranspose2d 128->128 k5 s2, the same gather).  Reference: torch fp32 on the GPU over the same
-    bf16-rounded operands; relative max error <= 1e-2."""
+    (ConvTranspose2d 128->128 k5 s2, the same gather) on conv_halo_kernel; the g_a[2] input gradient and the
+    g_s[4] forward (the s^2-phase direction) on conv_halo_phase_kernel.  Reference: torch fp32 on the GPU over
+    the same bf16-rounded operands; relative max error <= 1e-2."""
     from compressai.layers import Conv2d, ConvTranspose2d
 
     torch.manual_seed(5)
     mod = Conv2d(128, 128, 5, stride=2, padding=2).to(cuda)
-    x = torch.randn(B, 128, 128, 128, device=cuda)
+    x = torch.randn(B, 128, 128, 128, device=cuda).requires_grad_()
+    gy = torch.randn(B, 128, 64, 64, device=cuda)
     with _autocast(True):
         y = mod(x)
-    ref = F.conv2d(x.bfloat16().float(), mod.weight.bfloat16().float(), mod.bias, stride=2, padding=2)
+    y.backward(gy)
+    xr = x.detach().bfloat16().float().requires_grad_()
+    ref = F.conv2d(xr, mod.weight.detach().bfloat16().float(), mod.bias.detach(), stride=2, padding=2)
+    ref.backward(gy.bfloat16().float())
     assert relerr(y, ref) < 1e-2
+    assert relerr(x.grad, xr.grad) < 1e-2
 
     dec = ConvTranspose2d(128, 128, 5, stride=2, padding=2, output_padding=1).to(cuda)
     xs = torch.randn(B, 128, 64, 64, device=cuda).requires_grad_()
@@ -542,4 +553,5 @@ def test_halo_conv_full(cuda, B):
     yr = F.conv_transpose2d(xr, dec.weight.detach().bfloat16().float(), dec.bias.detach(), stride=2, padding=2,
                             output_padding=1)
     yr.backward(g.bfloat16().float())
+    assert relerr(ys, yr) < 1e-2
     assert relerr(xs.grad, xr.grad) < 1e-2
