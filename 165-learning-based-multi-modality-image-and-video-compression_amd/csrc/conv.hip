@@ -595,6 +595,16 @@ __host__ __device__ constexpr int halo_younger(int t, int nstb, int npi) {
     return nstb - 2 + cells + fences;
 }
 
+// the same count when footprint cell i is issued at step i * csp (fences after the last cell)
+__host__ __device__ constexpr int halo_younger_sp(int t, int nstb, int npi, int csp) {
+    const int lo = t + 1 - nstb > 0 ? t + 1 - nstb : 0;
+    int cells = 0;
+    for (int j = lo; j <= t - 1; ++j)
+        if (j % csp == 0 && j / csp < npi) ++cells;
+    const int last = (npi - 1) * csp;
+    return nstb - 2 + cells + ((last >= lo && last <= t - 1) ? 4 : 0);
+}
+
 __device__ __forceinline__ void wait_vmcnt_n(int n) {    // n folds to a constant after unrolling
     switch (n) {
         case 0: wait_vmcnt<0>(); break;
@@ -612,7 +622,16 @@ __device__ __forceinline__ void wait_vmcnt_n(int n) {    // n folds to a constan
         case 12: wait_vmcnt<12>(); break;
         case 13: wait_vmcnt<13>(); break;
         case 14: wait_vmcnt<14>(); break;
-        default: wait_vmcnt<15>(); break;
+        case 15: wait_vmcnt<15>(); break;
+        case 16: wait_vmcnt<16>(); break;
+        case 17: wait_vmcnt<17>(); break;
+        case 18: wait_vmcnt<18>(); break;
+        case 19: wait_vmcnt<19>(); break;
+        case 20: wait_vmcnt<20>(); break;
+        case 21: wait_vmcnt<21>(); break;
+        case 22: wait_vmcnt<22>(); break;
+        case 23: wait_vmcnt<23>(); break;
+        default: wait_vmcnt<24>(); break;
     }
 }
 
@@ -627,7 +646,12 @@ struct HaloCfg {
     static constexpr int PATCH = 4 * PLANE * 16;
     static constexpr int NPI = (4 * NPOS + 511) / 512;
     static constexpr int NTAP = KS * KS;
-    static constexpr int BSTAGE = BN * CK * 2, NSTB = KS;         // NTAP % NSTB == 0: a tap's stage is t % KS
+    // NTAP % NSTB == 0: a tap's stage is t % NSTB.  (A 9-deep ring, stage tracked at run time, measured 6 %
+    // slower for k5: the compiler's wait before the footprint store then drains taps still in flight.)
+    static constexpr int BSTAGE = BN * CK * 2, NSTB = KS;
+    // footprint cells are spread over the chunk, one every CSP steps: issued back to back, the next chunk's
+    // footprint is requested by all blocks at once and the burst queues at HBM
+    static constexpr int CSP = (NTAP - 1) / NPI > 1 ? (NTAP - 1) / NPI : 1;
     static constexpr int EPI = BM * (BN + 4) * 4;
     static constexpr int BYTES = (PATCH + NSTB * BSTAGE > EPI) ? PATCH + NSTB * BSTAGE : EPI;
 };
@@ -637,8 +661,9 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvArgs a, int
     using H = HaloCfg<KS>;
     constexpr int BM = H::BM, BN = H::BN, WM = H::WM, WN = H::WN;
     constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
-    constexpr int NPI = H::NPI, NTAP = H::NTAP, NSTB = H::NSTB;
-    static_assert(WM * WN == 8 && WTM == 2 * H::TW && H::BYTES <= 160 * 1024 && NTAP > NSTB + 3, "halo tile");
+    constexpr int NPI = H::NPI, NTAP = H::NTAP, NSTB = H::NSTB, CSP = H::CSP;
+    static_assert(WM * WN == 8 && WTM == 2 * H::TW && H::BYTES <= 160 * 1024 && NPI <= NTAP &&
+                  NTAP % NSTB == 0 && (NPI - 1) * CSP <= NTAP - 1, "halo tile");
     __shared__ __attribute__((aligned(16))) char smem[H::BYTES];
     char* const patch = smem;
     char* const bring = smem + H::PATCH;
@@ -672,7 +697,11 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvArgs a, int
         const int q4 = tid + 512 * i, g = (q4 >> 3) & 3, q = ((q4 >> 5) << 3) | (q4 & 7);
         const int pr = q / H::PW, pc = q - (q / H::PW) * H::PW;
         const int iy = iyb + pr, ix = ixb + pc;
+#ifndef CAI_PROBE_NOCELL    // timing probe only (results invalid): footprint loads from the zero page
         const bool in = real && q < H::NPOS && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW;
+#else
+        const bool in = false && real && iy + ix;
+#endif
         const void* src = in ? (const void*)(X + ((b * a.IH + iy) * a.IW + ix) * ld_b + g * 16 + cc * (H::CK * 2))
                              : (const void*)cai_zero_page;
         pr_[i] = *reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(reinterpret_cast<uintptr_t>(src));
@@ -703,10 +732,10 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvArgs a, int
     const int bp = wid * 64 + lane;
     const int bn_ = bp >> 2, bs_ = (bp & 3) ^ (((bn_ >> 3) & 1) * 3);
     const char* Wrow = bn_ < a.Npad ? reinterpret_cast<const char*>(a.w) + bn_ * a.Kp * 2 + bs_ * 16 : nullptr;
-    auto issue_b = [&](int ci, int t) {    // tap t of chunk ci into stage t % NSTB
+    auto issue_b = [&](int ci, int t, int stage) {    // tap t of chunk ci into `stage` (= t % NSTB)
         const void* src = (Wrow && ci < nc) ? (const void*)(Wrow + (t * a.Cin_pad + (c0 + ci) * H::CK) * 2)
                                             : (const void*)cai_zero_page;
-        glds16_asm(src, bring + (t % NSTB) * H::BSTAGE + wid * 1024);
+        glds16_asm(src, bring + stage * H::BSTAGE + wid * 1024);
     };
 
     // per-lane fragment cells
@@ -723,14 +752,14 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvArgs a, int
         const int n = wn * WTN + tn * 16 + i16;
         bpos[tn] = H::PATCH + (4 * n + (g_ ^ (((n >> 3) & 1) * 3))) * 16;
     }
-    auto read_frags = [&](int t, u32x4 (&fa)[TM], u32x4 (&fb)[TN]) {
+    auto read_frags = [&](int t, int stage, u32x4 (&fa)[TM], u32x4 (&fb)[TN]) {
         const int ty = t / KS, tx = t % KS;
         const int toff = (ty * H::PWR + (tx & 1) * H::ODD + (tx >> 1)) * 16;
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) fa[tm] = *reinterpret_cast<const u32x4*>(smem + apos[tm] + toff);
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn)
-            fb[tn] = *reinterpret_cast<const u32x4*>(smem + bpos[tn] + (t % NSTB) * H::BSTAGE);
+            fb[tn] = *reinterpret_cast<const u32x4*>(smem + bpos[tn] + stage * H::BSTAGE);
     };
 
     f32x4 acc[TM][TN];
@@ -750,38 +779,52 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvArgs a, int
 #pragma unroll
         for (int i = 0; i < NPI; ++i) load_cell(0, i);
 #pragma unroll
-        for (int t = 0; t < NSTB; ++t) issue_b(0, t);
+        for (int t = 0; t < NSTB; ++t) issue_b(0, t, t);
         store_patch();
         wait_vmcnt<NSTB - 1>();
         wait_lgkmcnt0();
         __builtin_amdgcn_s_barrier();
-        read_frags(0, fa, fb);
+        read_frags(0, 0, fa, fb);
     }
     for (int ci = 0; ci < nc; ++ci) {
 #pragma unroll
         for (int t = 0; t < NTAP; ++t) {
-            wait_vmcnt_n(halo_younger(t, NSTB, NPI));
+            wait_vmcnt_n(halo_younger_sp(t, NSTB, NPI, CSP));
             wait_lgkmcnt0();
+#ifndef CAI_PROBE_NOBAR    // timing probe only (results invalid): no per-step barrier
             __builtin_amdgcn_s_barrier();
+#else
+            if (t == NTAP - 1) __builtin_amdgcn_s_barrier();
+#endif
             if (t == NTAP - 1) {
-                // every wave has read its last fragment of this chunk: stage the next chunk's patch
+                // every wave has read its last fragment of this chunk: stage the next chunk's patch (when the
+                // footprint needs a cell per step of the chunk (k3: NPI == NTAP), the last one is loaded here)
+                if (NPI == NTAP) load_cell(ci + 1, NTAP - 1);
                 store_patch();
                 wait_lgkmcnt0();
                 __builtin_amdgcn_s_barrier();
             }
             __builtin_amdgcn_sched_barrier(0);
+            // step g + NSTB reuses the stage of step g (read during the previous step, so free after the barrier)
             if (t + NSTB < NTAP)
-                issue_b(ci, t + NSTB);
+                issue_b(ci, t + NSTB, t % NSTB);
             else
-                issue_b(ci + 1, t + NSTB - NTAP);
-            if (t < NPI) load_cell(ci + 1, t);    // the next chunk's patch, one cell per step
-            if (t == NPI - 1) fence_loads();
+                issue_b(ci + 1, t + NSTB - NTAP, t % NSTB);
+            // the next chunk's patch, one cell every CSP steps
+            if (t % CSP == 0 && t / CSP < NPI && t < NTAP - 1) load_cell(ci + 1, t / CSP);
+            if (t == (NPI - 1) * CSP) fence_loads();
             u32x4 na[TM], nb[TN];
-            read_frags(t + 1 == NTAP ? 0 : t + 1, na, nb);
+            read_frags(t + 1 == NTAP ? 0 : t + 1, (t + 1) % NSTB, na, nb);
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-                for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mma16<bf16>(fa[tm], fb[tn], acc[tm][tn]);
+                for (int tn = 0; tn < TN; ++tn) {
+#ifndef CAI_PROBE_NOMFMA    // timing probe only (results invalid): fragments read, no MFMA
+                    acc[tm][tn] = mma16<bf16>(fa[tm], fb[tn], acc[tm][tn]);
+#else
+                    asm volatile("" ::"v"(fa[tm]), "v"(fb[tn]));
+#endif
+                }
             // the next step's reads (separate registers) alternate with this step's first MFMAs (measured:
             // a read burst ahead of the MFMAs, or reads every other MFMA, ran 2-6 % slower)
 #pragma unroll

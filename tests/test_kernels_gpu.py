@@ -63,6 +63,7 @@ CONV_CASES = [
     ("conv", 2, 96, 40, 40, 70, 3, 2),
     ("deconv", 2, 128, 128, 32, 32, 5, 2),
     ("deconv", 1, 96, 64, 20, 36, 3, 2),
+    ("conv", 2, 512, 64, 128, 128, 3, 2),    # k3: two chunks per block (the last footprint cell loads at the store)
     # halo-staged s^2-phase kernel (ConvTranspose2d k5 s2 forward, Conv2d k5 s2 input gradient): 64-channel
     # chunks split over K, partial row / column tiles, Cout < 128, 192 input channels
     ("deconv", 2, 192, 128, 16, 40, 5, 2),
