@@ -704,6 +704,9 @@ class RdLossFn(torch.autograd.Function):
         lib.cai_rd_loss_fwd(ctypes.byref(desc), float(lmbda), bpp_coef, _p(out), _p(ws), ws.numel(), _stream())
         ctx.save_for_backward(xh, tg, *lbufs)
         ctx.cfg = (float(lmbda), bpp_coef, [l.shape for l in liks], x_hat.shape)
+        # unused outputs (mse, bpp when only the loss is backpropagated) reach backward as None, not as
+        # zero-filled tensors (two fill launches per step); the kernel reads a null gradient as 0
+        ctx.set_materialize_grads(False)
         return out[0], out[1], out[2]
 
     @staticmethod
