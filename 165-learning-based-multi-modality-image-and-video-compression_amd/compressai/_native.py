@@ -104,6 +104,7 @@ SIGNATURES = {
     "cai_channel_mean": (_I, [_I, _P, c_int32, _P, c_int32, c_int32, _I64, c_int32, _P, _F, _P, _S, _P]),
     "cai_channel_affine": (_I, [_I, _P, c_int32, _P, _P, _F, _P, c_int32, c_int32, _I64, c_int32, _P]),
     "cai_gdn_reparam": (_I, [_P, _P, c_int32, _F, _F, _I, _P, _P, _P]),
+    "cai_gdn_reparam_describe": (_I, [_P, _P, c_int32, _F, _F, _P, _P, _P]),
     "cai_gdn_fwd": (_I, [_I, _P, c_int32, _I64, c_int32, _P, _P, c_int32, _P, c_int32, _P]),
     "cai_gdn_bwd": (_I, [_I, _P, c_int32, _P, c_int32, _I64, c_int32, _P, _P, c_int32, _P, c_int32, _P, _P]),
     "cai_gdn_param_grad_workspace_bytes": (_S, [_I64, c_int32, _I]),

@@ -49,8 +49,14 @@ class Prepacker:
             mask = m.mask if isinstance(m, MaskedConv2d) else None
             yield m, mask
 
+    def _gdns(self):
+        from .layers.gdn import GDN
+
+        return [m for m in self.model.modules() if isinstance(m, GDN)]
+
     def _signature(self):
-        return tuple((m.weight.data_ptr(), None if k is None else k.data_ptr()) for m, k in self._convs())
+        return (tuple((m.weight.data_ptr(), None if k is None else k.data_ptr()) for m, k in self._convs()) +
+                tuple((m.beta.data_ptr(), m.gamma.data_ptr()) for m in self._gdns()))
 
     def _build(self, dtype):
         dev = next(self.model.parameters()).device
@@ -87,6 +93,27 @@ class Prepacker:
                 descs.append(d.raw)
                 buffers.append(buf)
                 table[(w.data_ptr(), direction)] = buf
+        # GDN / IGDN reparametrisations (beta, gamma operand) in the same launch (an older library without the
+        # entry point, as in A/B runs, leaves them to GdnFn)
+        try:
+            lib.cai_gdn_reparam_describe
+            gdns = self._gdns()
+        except AttributeError:
+            gdns = []
+        for m in gdns:
+            br, gr = m.beta.detach(), m.gamma.detach()
+            if br.dtype != torch.float32 or gr.dtype != torch.float32 or not (br.is_contiguous() and gr.is_contiguous()):
+                continue   # GdnFn reparametrises this layer itself
+            C = br.numel()
+            beta = torch.empty(C, dtype=torch.float32, device=dev)
+            gop = torch.empty(2 * C * C, dtype=dtype, device=dev)
+            d = ctypes.create_string_buffer(dsz)
+            lib.cai_gdn_reparam_describe(_p(br), _p(gr), C, float(m.beta_reparam.minimum),
+                                         float(m.beta_reparam.reparam_offset), _p(beta), _p(gop), d)
+            descs.append(d.raw)
+            buffers += [beta, gop]
+            table[(gr.data_ptr(), ("gdn", float(m.beta_reparam.minimum), float(m.beta_reparam.reparam_offset)))] = (
+                beta, gop)
         if not descs:
             return None
         host = ctypes.create_string_buffer(b"".join(descs), len(descs) * dsz)

@@ -1124,6 +1124,9 @@ struct PackArgs {
     int items_pp;          // pack_many: 8-element items per phase (Npad * Kp / 8)
     int edge;              // 1: edge-layer MFMA fragments (edge_frag.hpp), one item per fragment
     EdgeFragSpec es;
+    int gdn;               // 1: GDN reparametrisation (w = gamma_raw, mask = beta_raw, out = gamma_op, D1 = C)
+    float* gdn_beta;       //    beta output (C floats)
+    float gdn_bb, gdn_gb, gdn_ped;
 };
 
 template <typename T>
@@ -1176,6 +1179,27 @@ __global__ __launch_bounds__(256) void pack_many_kernel(const PackArgs* __restri
                 *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(a.out) + (int64_t)local * 8) = h;
                 continue;
             }
+        }
+        if (a.gdn) {
+            // gdn_reparam_kernel's element rule for 8 consecutive gamma entries (and beta for i < C)
+            const int C = a.D1;
+            const int64_t CC = (int64_t)C * C;
+            T* gop = reinterpret_cast<T*>(a.out);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int64_t i = (int64_t)local * 8 + e;
+                if (i >= CC) break;
+                const int r = (int)(i / C), c = (int)(i - (int64_t)r * C);
+                const float lb = fmaxf(a.w[i], a.gdn_gb);
+                const float v = lb * lb - a.gdn_ped;
+                gop[i] = from_f32<T>(v);
+                gop[CC + (int64_t)c * C + r] = from_f32<T>(v);
+                if (i < C) {
+                    const float lbb = fmaxf(a.mask[i], a.gdn_bb);
+                    a.gdn_beta[i] = lbb * lbb - a.gdn_ped;
+                }
+            }
+            continue;
         }
         const int ph = local / a.items_pp;
         const int e0 = (local - ph * a.items_pp) * 8;
@@ -1930,6 +1954,16 @@ static bool halo_phase_ok(const cai_conv_geom* g, const Plan& P, bool glds) {
     return true;
 }
 
+// A/B knob: an upper bound on the split-K factor of every conv launch (CAI_KSPLIT_MAX, read once; 0 = none)
+static int ksplit_cap() {
+    static const int cap = [] {
+        const char* e = getenv("CAI_KSPLIT_MAX");
+        return (e && *e) ? std::max(0, atoi(e)) : 0;
+    }();
+    return cap;
+}
+static int capped(int ks) { return ksplit_cap() > 0 ? std::max(1, std::min(ks, ksplit_cap())) : ks; }
+
 static ConvLaunch conv_launch(const cai_conv_geom* g, int dtype, int direction, int in_abs) {
     const Plan P = make_plan(g, dtype, direction);
     ConvLaunch L{};
@@ -1945,7 +1979,7 @@ static ConvLaunch conv_launch(const cai_conv_geom* g, int dtype, int direction, 
         L.mtiles = g->batch * L.tiles_x * L.tiles_y;
         L.ntiles = 1;
         const int nch = P.Cin_pad / 64, blocks = 4 * L.mtiles;
-        L.ksplit = blocks >= 256 ? 1 : std::min(nch, (256 + blocks - 1) / blocks);
+        L.ksplit = capped(blocks >= 256 ? 1 : std::min(nch, (256 + blocks - 1) / blocks));
         while (L.ksplit > 1 && (L.ksplit - 1) * ((nch + L.ksplit - 1) / L.ksplit) >= nch) --L.ksplit;
         L.ws_ld = 128;
         L.ws_bytes = L.ksplit > 1 ? (size_t)4 * L.ksplit * L.mmax * L.ws_ld * sizeof(float) : 0;
@@ -1960,7 +1994,7 @@ static ConvLaunch conv_launch(const cai_conv_geom* g, int dtype, int direction, 
         L.mtiles = g->batch * L.tiles_x * L.tiles_y;
         L.ntiles = 1;
         const int nch = P.Cin_pad / 32;
-        L.ksplit = L.mtiles >= 256 ? 1 : std::min(nch, (256 + L.mtiles - 1) / L.mtiles);
+        L.ksplit = capped(L.mtiles >= 256 ? 1 : std::min(nch, (256 + L.mtiles - 1) / L.mtiles));
         // every split gets a chunk: per = ceil(nch / ks) must leave no empty split
         while (L.ksplit > 1 && (L.ksplit - 1) * ((nch + L.ksplit - 1) / L.ksplit) >= nch) --L.ksplit;
         L.ws_ld = 128;
@@ -1982,7 +2016,7 @@ static ConvLaunch conv_launch(const cai_conv_geom* g, int dtype, int direction, 
     int ks = 1;
     const int target = L.glds ? 256 : 512;    // one 512-thread block per CU vs two 256-thread ones
     if (tiles < 256) ks = std::min({(target + tiles - 1) / tiles, std::max(1, nk / 4), 16});
-    L.ksplit = std::max(1, ks);
+    L.ksplit = capped(std::max(1, ks));
     L.ws_ld = L.ntiles * L.BN;
     L.ws_bytes = L.ksplit > 1 ? (size_t)P.nphase * L.ksplit * L.mmax * L.ws_ld * sizeof(float) : 0;
     return L;
@@ -2254,6 +2288,27 @@ int cai_edge_pack_describe(const cai_conv_geom* g, int dtype, int direction, con
     a.edge = 1;
     a.nphase = 1;
     a.Npad = a.es.nfrag * 8;   // finalize: items_pp = Npad * Kp / 8 = one item per fragment
+    a.Kp = 1;
+    memcpy(desc, &a, sizeof(a));
+    return CAI_OK;
+}
+
+int cai_gdn_reparam_describe(const float* beta_raw, const float* gamma_raw, int32_t C, float beta_min,
+                             float reparam_offset, float* beta, void* gamma_op, void* desc) {
+    CAI_CHECK_ARG(desc && beta_raw && gamma_raw && beta && gamma_op && C > 0, "gdn_reparam_describe: bad arguments");
+    PackArgs a{};
+    const float ped = reparam_offset * reparam_offset;
+    a.gdn = 1;
+    a.w = gamma_raw;
+    a.mask = beta_raw;
+    a.out = gamma_op;
+    a.D1 = C;
+    a.gdn_beta = beta;
+    a.gdn_bb = sqrtf(beta_min + ped);
+    a.gdn_gb = sqrtf(0.f + ped);
+    a.gdn_ped = ped;
+    a.nphase = 1;
+    a.Npad = (int)(((int64_t)C * C + 7) / 8 * 8);   // finalize: one item per 8 gamma entries
     a.Kp = 1;
     memcpy(desc, &a, sizeof(a));
     return CAI_OK;

@@ -103,6 +103,13 @@ int cai_conv_pack_describe(const cai_conv_geom* g, int dtype, int direction, con
 /* host side, once: number the 8-element work items of a contiguous table of n
  * descriptors; returns the total item count (total_items of pack_many). */
 int64_t cai_conv_pack_finalize(void* descs, int32_t n);
+/* A GDN / IGDN reparametrisation (cai_gdn_reparam's outputs: beta, gamma_op in
+ * the pack_many dtype) as one more pack_many descriptor, so a model's GDN layers
+ * are reparametrised in the same launch as its conv weights are packed
+ * (replaces the per-layer NonNegativeParametrizer calls, layers/gdn.py:77-92,
+ * ops/parametrizers.py:47-64). */
+int cai_gdn_reparam_describe(const float* beta_raw, const float* gamma_raw, int32_t C, float beta_min,
+                             float reparam_offset, float* beta, void* gamma_op, void* desc);
 int cai_conv_pack_many(const void* descs, int32_t n, int dtype, int64_t total_items, void* stream);
 
 /* NCHW (fp32, contiguous) -> pixel-major [B*H*W][ld] of dtype with zero
