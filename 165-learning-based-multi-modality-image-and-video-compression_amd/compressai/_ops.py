@@ -598,8 +598,24 @@ class BottleneckFn(torch.autograd.Function):
         return (dx, dq, None, None, None, *grads)
 
 
+_UNIT_GRAD = {}
+
+
+def _unit_grad(device) -> torch.Tensor:
+    """A persistent device scalar 1.0 (created once per device, outside any captured graph's steady state)."""
+    t = _UNIT_GRAD.get(device)
+    if t is None:
+        t = torch.ones((), dtype=torch.float32, device=device)
+        _UNIT_GRAD[device] = t
+    return t
+
+
 class BottleneckAuxFn(torch.autograd.Function):
-    """EntropyBottleneck.loss (entropy_models.py:450-454): gradient reaches only `quantiles`."""
+    """EntropyBottleneck.loss (entropy_models.py:450-454): gradient reaches only `quantiles`.
+
+    The loss is |F(quantiles) - target| summed, so d loss / d quantiles is linear in the upstream gradient:
+    the forward launch also produces it for an upstream gradient of 1, and the backward only scales it
+    (one elementwise op instead of a second pass through the 5-layer CDF chains)."""
 
     @staticmethod
     def forward(ctx, quantiles, target, *params):
@@ -609,22 +625,23 @@ class BottleneckAuxFn(torch.autograd.Function):
         C = q_.shape[0]
         t = target.float().contiguous()
         loss = torch.empty((), dtype=torch.float32, device=quantiles.device)
+        dq1 = torch.empty_like(q_)
         P = _eb_params(prm, q_)
-        lib.cai_eb_aux_loss(C, ctypes.byref(P), _p(t), _p(loss), None, None, 0, _stream())
-        ctx.save_for_backward(q_, t, *prm)
+        lib.cai_eb_aux_loss(C, ctypes.byref(P), _p(t), _p(loss), _p(_unit_grad(quantiles.device)), _p(dq1), 0,
+                            _stream())
+        ctx.save_for_backward(dq1)
         ctx.qparam = quantiles
+        ctx.nparams = len(prm)
         return loss
 
     @staticmethod
     def backward(ctx, g):
-        q_, t, *prm = ctx.saved_tensors
-        C = q_.shape[0]
-        gl = g.float().contiguous().reshape(())
-        direct = direct_grad(ctx.qparam)
-        dq = ctx.qparam.grad if direct else torch.empty_like(q_)
-        P = _eb_params(prm, q_)
-        lib.cai_eb_aux_loss(C, ctypes.byref(P), _p(t), None, _p(gl), _p(dq), int(direct), _stream())
-        return (None if direct else dq, None, *([None] * len(prm)))
+        (dq1,) = ctx.saved_tensors
+        gl = g.float().reshape(())
+        if direct_grad(ctx.qparam):
+            ctx.qparam.grad.view_as(dq1).addcmul_(dq1, gl)
+            return (None, None, *([None] * ctx.nparams))
+        return ((dq1 * gl).view_as(ctx.qparam), None, *([None] * ctx.nparams))
 
 
 # ---------------------------------------------------------------------------
