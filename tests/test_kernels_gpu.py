@@ -556,3 +556,37 @@ def test_halo_conv_full(cuda, B):
     yr.backward(g.bfloat16().float())
     assert relerr(ys, yr) < 1e-2
     assert relerr(xs.grad, xr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("C", [64, 128, 192])
+def test_gdn_reparam_in_pack_many_matches_standalone(cuda, C, dtype):
+    """A GDN reparametrisation issued as a pack_many descriptor (cai_gdn_reparam_describe, the path every model
+    forward takes) writes exactly what cai_gdn_reparam writes: beta and the gamma / gamma^T operands, bit for
+    bit (same LowerBound rule, same rounding to the operand dtype)."""
+    import ctypes
+
+    from compressai._native import lib
+    from compressai._ops import _p, _stream, dcode
+
+    torch.manual_seed(3)
+    br = (torch.rand(C, device=cuda) * 2 - 0.5).contiguous()        # some entries below the bound
+    gr = (torch.rand(C, C, device=cuda) * 0.2 - 0.05).contiguous()
+    beta_min, off = 1e-6, 2 ** -18
+    b_ref = torch.empty(C, dtype=torch.float32, device=cuda)
+    g_ref = torch.empty(2 * C * C, dtype=dtype, device=cuda)
+    lib.cai_gdn_reparam(_p(br), _p(gr), C, beta_min, off, dcode(dtype), _p(b_ref), _p(g_ref), _stream())
+    b_new = torch.full_like(b_ref, float("nan"))
+    g_new = torch.full_like(g_ref, float("nan"))
+    dsz = lib.cai_conv_pack_desc_bytes()
+    d = ctypes.create_string_buffer(dsz)
+    lib.cai_gdn_reparam_describe(_p(br), _p(gr), C, beta_min, off, _p(b_new), _p(g_new), d)
+    host = ctypes.create_string_buffer(d.raw, dsz)
+    total = lib.cai_conv_pack_finalize(host, 1)
+    assert total == (C * C + 7) // 8
+    blob = torch.frombuffer(bytearray(host.raw), dtype=torch.uint8).to(cuda)
+    lib.cai_conv_pack_many(_p(blob), 1, dcode(dtype), total, _stream())
+    torch.cuda.synchronize()
+    assert torch.equal(b_new, b_ref)
+    assert torch.equal(g_new.view(torch.int16 if dtype == torch.bfloat16 else torch.int32),
+                       g_ref.view(torch.int16 if dtype == torch.bfloat16 else torch.int32))
