@@ -7,6 +7,7 @@ forward/backward arithmetic runs in HIP kernels through libcai.so
 """
 from . import entropy_models, layers, models, ops, zoo  # noqa: F401
 from ._native import available as native_available  # noqa: F401
+from ._ops import set_fp16_autocast_policy  # noqa: F401
 
 __version__ = "1.2.0.dev0+mi355x"
 

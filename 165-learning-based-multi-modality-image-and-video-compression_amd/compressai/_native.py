@@ -71,6 +71,8 @@ SIGNATURES = {
                           _P, _S, _P]),
     "cai_conv_dgrad": (_I, [_G, _I, _P, c_int32, _P, _P, c_int32, c_int32, _F, _P, c_int32, _P, _S, _P]),
     "cai_conv_wgrad_workspace_bytes": (_S, [_G, _I]),
+    "cai_conv_kernel_name": (c_char_p, [_G, _I, _I, c_int32]),
+    "cai_conv_split_factor": (c_int32, [_G, _I, _I, c_int32]),
     "cai_conv_wgrad": (_I, [_G, _I, _P, c_int32, c_int32, c_int32, _P, c_int32, _P, _P, c_int32, _P, _S, _P]),
     "cai_deconv_small_workspace_bytes": (_S, [_G, _I]),
     "cai_deconv_small_fwd": (_I, [_G, _I, _P, c_int32, _P, _P, _P, _P, _S, _P]),
@@ -163,7 +165,8 @@ class _Lib:
     def __getattr__(self, name):
         fn = self._bound(name)
 
-        if fn.restype is c_int and name not in ("cai_version", "cai_abi_count", "cai_edge_supported"):
+        if fn.restype is c_int and name not in ("cai_version", "cai_abi_count", "cai_edge_supported",
+                                                "cai_conv_split_factor"):
             def call(*args):
                 rc = fn(*args)
                 if rc != CAI_OK:

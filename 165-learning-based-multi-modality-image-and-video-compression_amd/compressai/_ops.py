@@ -25,6 +25,7 @@ from typing import Optional, Sequence, Tuple
 
 import torch
 
+from . import _ledger
 from ._native import (ACT_LEAKY, ACT_NONE, ACT_RELU, BF16, F32, MASK_LEAKY, MASK_NONE, MASK_POS, Q_DEQUANTIZE, Q_NOISE,
                       ConvGeom, EbGrads, EbParams, RdGrads, RdInputs, lib)
 
@@ -47,6 +48,14 @@ def direct_grad(p) -> bool:
             and p.grad.dtype == torch.float32 and p.grad.is_contiguous())
 
 
+def _es(dtype) -> int:
+    return 2 if dtype == torch.bfloat16 else 4
+
+
+def _conv_kernel(g, dt, direction, in_abs=0):
+    return lambda: lib.cai_conv_kernel_name(ctypes.byref(g), dcode(dt), direction, int(in_abs)).decode()
+
+
 def _stream() -> _VP:
     return _VP(torch.cuda.current_stream().cuda_stream)
 
@@ -63,9 +72,35 @@ def dcode(dtype: torch.dtype) -> int:
     raise ValueError(f"unsupported dtype {dtype} (bf16 / fp32 only)")
 
 
+_FP16_POLICY = os.environ.get("CAI_FP16_AUTOCAST", "error")   # "error" | "bf16"
+
+
+def set_fp16_autocast_policy(policy: str):
+    """What fp16 autocast means for this build: "error" (default) raises, "bf16" computes in bf16.
+
+    The reference trains under ``torch.cuda.amp.autocast()`` (fp16, examples/train.py:172,239).  The kernels
+    here have bf16 and fp32 paths only; running an fp16 region in bf16 has to be asked for explicitly."""
+    global _FP16_POLICY
+    if policy not in ("error", "bf16"):
+        raise ValueError(f"fp16 autocast policy must be 'error' or 'bf16', got {policy!r}")
+    _FP16_POLICY = policy
+
+
 def compute_dtype() -> torch.dtype:
-    """bf16 inside torch.autocast('cuda'), exact fp32 otherwise."""
-    return torch.bfloat16 if torch.is_autocast_enabled("cuda") else torch.float32
+    """bf16 inside torch.autocast('cuda', dtype=torch.bfloat16), exact fp32 outside autocast.
+
+    fp16 autocast raises unless set_fp16_autocast_policy("bf16") (or CAI_FP16_AUTOCAST=bf16) asked for bf16."""
+    if not torch.is_autocast_enabled("cuda"):
+        return torch.float32
+    dt = torch.get_autocast_dtype("cuda")
+    if dt == torch.bfloat16:
+        return dt
+    if dt == torch.float16 and _FP16_POLICY == "bf16":
+        return torch.bfloat16
+    raise RuntimeError(
+        f"autocast dtype {dt} is not supported by the MI355X kernels (bf16 / fp32 only): use "
+        "torch.autocast('cuda', dtype=torch.bfloat16), or call "
+        "compressai.set_fp16_autocast_policy('bf16') to run fp16 autocast regions in bf16")
 
 
 def _vec(dtype: torch.dtype) -> int:
@@ -241,9 +276,13 @@ def _small_deconv_bwd(ctx, xpm, weight, gy):
             dw = torch.empty(weight.shape, dtype=torch.float32, device=gy.device)
             db = torch.empty(g.out_c, dtype=torch.float32, device=gy.device) if ctx.has_bias else None
     ws, wsb = _small_ws(g, dt, gy.device)
-    lib.cai_deconv_small_bwd(ctypes.byref(g), dcode(dt), _p(xpm), ctx.xld, _p(weight.detach().float().contiguous()),
-                             _p(gy), _p(dx), ldx if dx is not None else 0, _p(dw), _p(db), int(direct), _p(ws), wsb,
-                             _stream())
+    w32 = weight.detach().float().contiguous()
+    fl, nb = _ledger.conv_cost(g, _es(dt), 2, y_bytes=4)
+    fl2, nb2 = _ledger.conv_cost(g, _es(dt), 1, y_bytes=4) if dx is not None else (0.0, 0.0)
+    _ledger.run(lambda dw=dw, db=db: lib.cai_deconv_small_bwd(ctypes.byref(g), dcode(dt), _p(xpm), ctx.xld, _p(w32),
+                                                              _p(gy), _p(dx), ldx if dx is not None else 0, _p(dw),
+                                                              _p(db), int(direct), _p(ws), wsb, _stream()),
+                "conv_bwd", "deconv_small (im2col + 1x1 GEMMs)", fl + fl2, nb + nb2, dt, _ledger.shape_of(g))
     if direct:
         dw = db = None
     elif dw is not None and weight.dtype != torch.float32:
@@ -295,7 +334,9 @@ def _edge_bwd(ctx, xs, weight, gy):
             ldx = (g.in_c + 7) // 8 * 8
             dx = empty_pm(g.batch, g.in_c, g.in_h, g.in_w, dt, gy.device, ld=ldx)
             frag = ctx.frag_bwd if ctx.frag_bwd is not None else _edge_frag(g, dt, 1, weight)
-            lib.cai_edge_deconv_dgrad(ctypes.byref(g), _p(img), _p(frag), _p(dx), ldx, st)
+            fl, nb = _ledger.conv_cost(g, _es(dt), 1, y_bytes=4)
+            _ledger.run(lambda: lib.cai_edge_deconv_dgrad(ctypes.byref(g), _p(img), _p(frag), _p(dx), ldx, st),
+                        "conv_dgrad", "edge_s2d_kernel (deconv dgrad)", fl, nb, dt, _ledger.shape_of(g))
     if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
         wparam, bparam = ctx.params
         direct = direct_grad(wparam) and (bparam is None or direct_grad(bparam))
@@ -306,7 +347,10 @@ def _edge_bwd(ctx, xs, weight, gy):
             dbt = torch.empty(g.out_c, dtype=torch.float32, device=gy.device) if ctx.has_bias else None
         nbytes = lib.cai_edge_workspace_bytes(ctypes.byref(g), dcode(dt))
         ws = torch.empty(nbytes, dtype=torch.uint8, device=gy.device)
-        lib.cai_edge_wgrad(ctypes.byref(g), _p(img), _p(feat), fld, _p(dwt), _p(dbt), int(direct), _p(ws), nbytes, st)
+        fl, nb = _ledger.conv_cost(g, _es(dt), 2, **({"x_bytes": 4} if ctx.edge == 1 else {"y_bytes": 4}))
+        _ledger.run(lambda: lib.cai_edge_wgrad(ctypes.byref(g), _p(img), _p(feat), fld, _p(dwt), _p(dbt), int(direct),
+                                               _p(ws), nbytes, st),
+                    "conv_wgrad", "edge_wgrad_dma_kernel (+pack, reduce)", fl, nb, dt, _ledger.shape_of(g))
         if not direct:
             dw = dwt if weight.dtype == torch.float32 else dwt.to(weight.dtype)
             db = dbt
@@ -331,16 +375,21 @@ class ConvFn(torch.autograd.Function):
         if ctx.edge == 1:   # space-to-depth first layer: reads the NCHW fp32 image directly
             x32 = x.detach().float().contiguous()
             y = empty_pm(B, cout, g.out_h, g.out_w, dt, x.device)
-            lib.cai_edge_conv_fwd(ctypes.byref(g), _p(x32), _p(_edge_frag(g, dt, 0, weight)), _p(b), _p(y), cout,
-                                  _stream())
+            frag = _edge_frag(g, dt, 0, weight)
+            fl, nb = _ledger.conv_cost(g, _es(dt), 0, x_bytes=4)
+            _ledger.run(lambda: lib.cai_edge_conv_fwd(ctypes.byref(g), _p(x32), _p(frag), _p(b), _p(y), cout, _stream()),
+                        "conv_fwd", "edge_s2d_kernel (conv fwd)", fl, nb, dt, _ledger.shape_of(g))
             ctx.xld = 0
             ctx.save_for_backward(x32, weight, None)
             return y
         xpm, xld = to_pm(x, dt, vec)
         if ctx.edge == 2:   # depth-to-space last layer: writes the NCHW fp32 image directly
             y = torch.empty((B, cout, g.out_h, g.out_w), dtype=torch.float32, device=x.device)
-            lib.cai_edge_deconv_fwd(ctypes.byref(g), _p(xpm), xld, _p(_edge_frag(g, dt, 0, weight)), _p(b), _p(y),
-                                    _stream())
+            frag = _edge_frag(g, dt, 0, weight)
+            fl, nb = _ledger.conv_cost(g, _es(dt), 0, y_bytes=4)
+            _ledger.run(lambda: lib.cai_edge_deconv_fwd(ctypes.byref(g), _p(xpm), xld, _p(frag), _p(b), _p(y),
+                                                        _stream()),
+                        "conv_fwd", "edge_d2s_kernel (deconv fwd)", fl, nb, dt, _ledger.shape_of(g))
             packer = _prepack_active()   # the input-gradient fragments of this step's weights
             ctx.frag_bwd = packer.lookup(weight, dt, ("edge", 1)) if packer is not None else None
             ctx.xld = xld
@@ -357,8 +406,11 @@ class ConvFn(torch.autograd.Function):
         ctx.small = _small_deconv(spec, g, xld, dt)
         if ctx.small:   # few output channels: per-input-pixel GEMM + col2im (csrc/deconv_small.hip)
             ws, wsb = _small_ws(g, dt, x.device)
-            lib.cai_deconv_small_fwd(ctypes.byref(g), dcode(dt), _p(xpm), xld, _p(weight.detach().float().contiguous()),
-                                     _p(b), _p(y), _p(ws), wsb, _stream())
+            w32 = weight.detach().float().contiguous()
+            fl, nb = _ledger.conv_cost(g, _es(dt), 0, y_bytes=4)
+            _ledger.run(lambda: lib.cai_deconv_small_fwd(ctypes.byref(g), dcode(dt), _p(xpm), xld, _p(w32), _p(b),
+                                                         _p(y), _p(ws), wsb, _stream()),
+                        "conv_fwd", "deconv_small (GEMM + col2im)", fl, nb, dt, _ledger.shape_of(g))
         else:
             packer = _prepack_active()
             wp = packer.lookup(weight, dt, 0) if packer is not None else None
@@ -366,8 +418,11 @@ class ConvFn(torch.autograd.Function):
             if wp is None:
                 wp = _pack_weight(g, dt, 0, weight)
             ws, wsb = _conv_ws(g, dt, 0, x.device)
-            lib.cai_conv_fwd(ctypes.byref(g), dcode(dt), _p(xpm), xld, int(spec.in_abs), _p(wp), _p(b), spec.act,
-                             spec.act_param, _p(y), ydt, *ys, _p(ws), wsb, _stream())
+            fl, nb = _ledger.conv_cost(g, _es(dt), 0, y_bytes=4 if spec.out_nchw32 else None)
+            _ledger.run(lambda: lib.cai_conv_fwd(ctypes.byref(g), dcode(dt), _p(xpm), xld, int(spec.in_abs), _p(wp),
+                                                 _p(b), spec.act, spec.act_param, _p(y), ydt, *ys, _p(ws), wsb,
+                                                 _stream()),
+                        "conv_fwd", _conv_kernel(g, dt, 0, spec.in_abs), fl, nb, dt, _ledger.shape_of(g))
         ctx.xld = xld
         ctx.save_for_backward(xpm, weight, y if spec.act != ACT_NONE else None)
         return y
@@ -388,8 +443,11 @@ class ConvFn(torch.autograd.Function):
             mode = 1 if spec.act == 1 else 2
             out = empty_pm(g.batch, g.out_c, g.out_h, g.out_w, dt, gy.device)
             yld = pixel_major_ld(y)
-            lib.cai_act_bwd(mode, spec.act_param, _p(y), yld, _p(gpm), gld, _p(out), g.out_c,
-                            g.batch * g.out_h * g.out_w, g.out_c, code, st)
+            n_el = g.batch * g.out_h * g.out_w * g.out_c
+            _ledger.run(lambda gpm=gpm, gld=gld: lib.cai_act_bwd(mode, spec.act_param, _p(y), yld, _p(gpm), gld,
+                                                                 _p(out), g.out_c, g.batch * g.out_h * g.out_w,
+                                                                 g.out_c, code, st),
+                        "act_bwd", "act_bwd_kernel", 0, 3 * n_el * _es(dt), dt)
             gpm, gld = out, g.out_c
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
@@ -398,11 +456,14 @@ class ConvFn(torch.autograd.Function):
             dx = empty_pm(g.batch, g.in_c, g.in_h, g.in_w, dt, gy.device, ld=ldx)
             aux = xpm if spec.in_mask != MASK_NONE else None
             ws, wsb = _conv_ws(g, dt, 1, gy.device)
-            lib.cai_conv_dgrad(ctypes.byref(g), code, _p(gpm), gld, _p(wt), _p(dx), ldx, spec.in_mask,
-                               spec.in_mask_param, _p(aux), ctx.xld if aux is not None else 0, _p(ws), wsb, st)
+            fl, nb = _ledger.conv_cost(g, _es(dt), 1)
+            _ledger.run(lambda: lib.cai_conv_dgrad(ctypes.byref(g), code, _p(gpm), gld, _p(wt), _p(dx), ldx,
+                                                   spec.in_mask, spec.in_mask_param, _p(aux),
+                                                   ctx.xld if aux is not None else 0, _p(ws), wsb, st),
+                        "conv_dgrad", _conv_kernel(g, dt, 1), fl, nb, dt, _ledger.shape_of(g))
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             nbytes = lib.cai_conv_wgrad_workspace_bytes(ctypes.byref(g), code)
-            ws = torch.empty(nbytes, dtype=torch.uint8, device=gy.device)
+            wws = torch.empty(nbytes, dtype=torch.uint8, device=gy.device)
             wparam, bparam = ctx.params
             direct = direct_grad(wparam) and (bparam is None or direct_grad(bparam))
             if direct:   # accumulate straight into the optimizer's flat gradient buffer
@@ -410,8 +471,11 @@ class ConvFn(torch.autograd.Function):
             else:
                 dw = torch.empty(weight.shape, dtype=torch.float32, device=gy.device)
                 db = torch.empty(g.out_c, dtype=torch.float32, device=gy.device) if ctx.has_bias else None
-            lib.cai_conv_wgrad(ctypes.byref(g), code, _p(xpm), ctx.xld, int(spec.in_abs), 0, _p(gpm), gld, _p(dw),
-                               _p(db), int(direct), _p(ws), nbytes, st)
+            fl, nb = _ledger.conv_cost(g, _es(dt), 2)
+            _ledger.run(lambda dw=dw, db=db: lib.cai_conv_wgrad(ctypes.byref(g), code, _p(xpm), ctx.xld,
+                                                                int(spec.in_abs), 0, _p(gpm), gld, _p(dw), _p(db),
+                                                                int(direct), _p(wws), nbytes, st),
+                        "conv_wgrad", _conv_kernel(g, dt, 2, spec.in_abs), fl, nb, dt, _ledger.shape_of(g))
             if direct:
                 dw = db = None
             elif weight.dtype != torch.float32:
@@ -446,7 +510,9 @@ class GdnFn(torch.autograd.Function):
             gop = torch.empty(2 * C * C, dtype=dt, device=x.device)
             lib.cai_gdn_reparam(_p(br), _p(gr), C, beta_min, reparam_offset, code, _p(beta), _p(gop), st)
         y = empty_pm(B, C, H, W, dt, x.device)
-        lib.cai_gdn_fwd(code, _p(xpm), xld, npix, C, _p(gop), _p(beta), int(inverse), _p(y), C, st)
+        _ledger.run(lambda: lib.cai_gdn_fwd(code, _p(xpm), xld, npix, C, _p(gop), _p(beta), int(inverse), _p(y), C, st),
+                    "gdn_fwd", "gdn_fwd_kernel", 2.0 * npix * C * C, 2 * npix * C * _es(dt) + C * C * _es(dt), dt,
+                    f"{'IGDN' if inverse else 'GDN'} C={C} npix={npix}")
         ctx.save_for_backward(xpm, br, gr, beta, gop)
         ctx.cfg = (dt, xld, int(inverse), float(beta_min), float(reparam_offset))
         ctx.params = (beta_raw, gamma_raw)
@@ -481,8 +547,12 @@ class GdnFn(torch.autograd.Function):
                                    _p(dgr), int(direct), _p(ws2), nb2, st)
         else:
             # dx and the parameter gradients in one call (fused pass for bf16, C in {64, 128})
-            lib.cai_gdn_backward(code, _p(xpm), xld, _p(gpm), gld, npix, C, _p(gop), _p(beta), inverse, _p(dx), C,
-                                 _p(br), _p(gr), beta_min, off, _p(dbr), _p(dgr), int(direct), _p(ws), nbytes, st)
+            _ledger.run(lambda dbr=dbr, dgr=dgr: lib.cai_gdn_backward(code, _p(xpm), xld, _p(gpm), gld, npix, C, _p(gop),
+                                                                      _p(beta), inverse, _p(dx), C, _p(br), _p(gr),
+                                                                      beta_min, off, _p(dbr), _p(dgr), int(direct),
+                                                                      _p(ws), nbytes, st),
+                        "gdn_bwd", "gdn_bwd (fused / two-pass)", 4.0 * npix * C * C,
+                        3 * npix * C * _es(dt) + 8 * C * C, dt, f"{'IGDN' if inverse else 'GDN'} C={C} npix={npix}")
         if direct:
             dbr = dgr = None
         return dx, dbr, dgr, None, None, None
@@ -507,8 +577,13 @@ class GaussianFn(torch.autograd.Function):
         smdt = dcode(scales.dtype)
         q, qbuf = empty_rows_like(x.shape, x.dtype, x.device)
         lik, lbuf = empty_rows_like(x.shape, torch.float32, x.device)
-        lib.cai_gc_fwd(mode, npix, C, _p(xr), dcode(x.dtype), xld, _p(sr), sld, _p(mr), mld, smdt, _p(nr), nld,
-                       scale_bound, lik_bound, _p(qbuf), dcode(x.dtype), C, _p(lbuf), C, _stream())
+        n_el = npix * C
+        _ledger.run(lambda: lib.cai_gc_fwd(mode, npix, C, _p(xr), dcode(x.dtype), xld, _p(sr), sld, _p(mr), mld, smdt,
+                                           _p(nr), nld, scale_bound, lik_bound, _p(qbuf), dcode(x.dtype), C, _p(lbuf),
+                                           C, _stream()),
+                    "gc_fwd", "gc_fwd_kernel", 0,
+                    n_el * (2 * x.element_size() + scales.element_size() * (2 if means is not None else 1) + 4
+                            + (4 if noise is not None else 0)), torch.float32, f"{n_el} elements")
         ctx.save_for_backward(xr, sr, mr, nr)
         ctx.cfg = (mode, scale_bound, lik_bound, xld, sld, mld, nld, npix, C, x.shape, x.dtype, scales.shape,
                    scales.dtype, means is not None)
@@ -527,9 +602,16 @@ class GaussianFn(torch.autograd.Function):
         dx, dxb = empty_rows_like(xshape, xdtype, xr.device)
         ds, dsb = empty_rows_like(sshape, sdtype, xr.device)
         dm, dmb = empty_rows_like(sshape, sdtype, xr.device) if has_m else (None, None)
-        lib.cai_gc_bwd(mode, npix, C, _p(xr), dcode(xdtype), xld, _p(sr), sld, _p(mr), mld, dcode(sdtype), _p(nr),
-                       nld, sb, lb, _p(gl), glld, _p(gq_r), dcode(gq_r.dtype) if gq_r is not None else F32, gqld,
-                       _p(dxb), C, _p(dsb), C, _p(dmb), C, _stream())
+        n_el = npix * C
+        es_x, es_s = xr.element_size(), sr.element_size()
+        _ledger.run(lambda: lib.cai_gc_bwd(mode, npix, C, _p(xr), dcode(xdtype), xld, _p(sr), sld, _p(mr), mld,
+                                           dcode(sdtype), _p(nr), nld, sb, lb, _p(gl), glld, _p(gq_r),
+                                           dcode(gq_r.dtype) if gq_r is not None else F32, gqld, _p(dxb), C, _p(dsb),
+                                           C, _p(dmb), C, _stream()),
+                    "gc_bwd", "gc_bwd_kernel", 0,
+                    n_el * (2 * es_x + (4 if mr is not None else 2) * es_s + (4 if nr is not None else 0)
+                            + (4 if gl is not None else 0) + (es_x if gq_r is not None else 0)),
+                    torch.float32, f"{n_el} elements")
         return dx, ds, dm, None, None, None, None
 
 
@@ -557,8 +639,11 @@ class BottleneckFn(torch.autograd.Function):
         q, qbuf = empty_rows_like(x.shape, x.dtype, x.device)
         lik, lbuf = empty_rows_like(x.shape, torch.float32, x.device)
         P = _eb_params(prm, q_)
-        lib.cai_eb_fwd(mode, npix, C, ctypes.byref(P), _p(xr), dcode(x.dtype), xld, _p(nr), nld, lik_bound,
-                       _p(qbuf), dcode(x.dtype), C, _p(lbuf), C, _stream())
+        n_el = npix * C
+        _ledger.run(lambda: lib.cai_eb_fwd(mode, npix, C, ctypes.byref(P), _p(xr), dcode(x.dtype), xld, _p(nr), nld,
+                                           lik_bound, _p(qbuf), dcode(x.dtype), C, _p(lbuf), C, _stream()),
+                    "eb_fwd", "eb_fwd_kernel", 0, n_el * (2 * x.element_size() + 4 + (4 if noise is not None else 0)),
+                    torch.float32, f"{n_el} elements")
         ctx.save_for_backward(xr, nr, q_, *prm)
         ctx.cfg = (mode, lik_bound, xld, nld, npix, C, x.shape, x.dtype)
         ctx.params = (quantiles,) + tuple(params)
@@ -590,9 +675,12 @@ class BottleneckFn(torch.autograd.Function):
         G.quantiles = dq.data_ptr()
         G.accumulate = int(direct)
         P = _eb_params(prm, q_)
-        lib.cai_eb_bwd(mode, npix, C, ctypes.byref(P), _p(xr), dcode(xdtype), xld, _p(nr), nld, lb, _p(gl), glld,
-                       _p(gq_r), dcode(gq_r.dtype) if gq_r is not None else F32, gqld, _p(dxb), C, ctypes.byref(G),
-                       _stream())
+        n_el = npix * C
+        _ledger.run(lambda: lib.cai_eb_bwd(mode, npix, C, ctypes.byref(P), _p(xr), dcode(xdtype), xld, _p(nr), nld, lb,
+                                           _p(gl), glld, _p(gq_r), dcode(gq_r.dtype) if gq_r is not None else F32,
+                                           gqld, _p(dxb), C, ctypes.byref(G), _stream()),
+                    "eb_bwd", "eb_bwd_kernel", 0, n_el * (3 * xr.element_size() + 8), torch.float32,
+                    f"{n_el} elements")
         if direct:
             return (dx, None, None, None, None, *([None] * len(grads)))
         return (dx, dq, None, None, None, *grads)
@@ -725,7 +813,10 @@ class RdLossFn(torch.autograd.Function):
         desc.nlik, desc.x_hat, desc.target, desc.n = len(lbufs), xh.data_ptr(), tg.data_ptr(), xh.numel()
         out = torch.empty(3, dtype=torch.float32, device=xh.device)
         ws = torch.empty(lib.cai_rd_loss_workspace_bytes(), dtype=torch.uint8, device=xh.device)
-        lib.cai_rd_loss_fwd(ctypes.byref(desc), float(lmbda), bpp_coef, _p(out), _p(ws), ws.numel(), _stream())
+        nl = sum(r.numel() for r in lbufs)
+        _ledger.run(lambda: lib.cai_rd_loss_fwd(ctypes.byref(desc), float(lmbda), bpp_coef, _p(out), _p(ws),
+                                                ws.numel(), _stream()),
+                    "rd_fwd", "rd_stage1/2", 0, 8 * xh.numel() + 4 * nl, torch.float32)
         ctx.save_for_backward(xh, tg, *lbufs)
         ctx.cfg = (float(lmbda), bpp_coef, [l.shape for l in liks], x_hat.shape)
         # unused outputs (mse, bpp when only the loss is backpropagated) reach backward as None, not as
@@ -749,8 +840,10 @@ class RdLossFn(torch.autograd.Function):
         desc.nlik, desc.x_hat, desc.target, desc.n = len(lbufs), xh.data_ptr(), tg.data_ptr(), xh.numel()
         dxh = torch.empty_like(xh)
         g = [None if t is None else t.float().contiguous() for t in (gl, gm, gb)]
-        lib.cai_rd_loss_bwd(ctypes.byref(desc), lmbda, bpp_coef, _p(g[0]), _p(g[1]), _p(g[2]), _p(dxh),
-                            ctypes.byref(grads), _stream())
+        nl = sum(r.numel() for r in lbufs)
+        _ledger.run(lambda: lib.cai_rd_loss_bwd(ctypes.byref(desc), lmbda, bpp_coef, _p(g[0]), _p(g[1]), _p(g[2]),
+                                                _p(dxh), ctypes.byref(grads), _stream()),
+                    "rd_bwd", "rd_bwd_kernel", 0, 12 * xh.numel() + 8 * nl, torch.float32)
         # each likelihood gradient in the layout of its buffer, viewed with the logical shape
         outs = []
         for d, r, shp in zip(dliks, lbufs, lshapes):
@@ -787,8 +880,9 @@ def _act_grad(g, y, ld_y, act, prm, dtype):
         return gp
     out, old = _out_pm_like(g, dtype)
     B, C, H, W = g.shape
-    lib.cai_act_bwd(_MASK_OF_ACT[act], prm, _p(y), ld_y, _p(gp), gld, _p(out), old, B * H * W, C, dcode(dtype),
-                    _stream())
+    _ledger.run(lambda: lib.cai_act_bwd(_MASK_OF_ACT[act], prm, _p(y), ld_y, _p(gp), gld, _p(out), old, B * H * W, C,
+                                        dcode(dtype), _stream()),
+                "act_bwd", "act_bwd_kernel", 0, 3 * B * H * W * C * _es(dtype), dtype)
     return out
 
 
@@ -806,7 +900,9 @@ class AddActFn(torch.autograd.Function):
         bp, bld = to_pm(b, dt, vec)
         y, yld = _out_pm_like(a, dt)
         B, C, H, W = a.shape
-        lib.cai_add_act(dcode(dt), _p(ap), ald, _p(bp), bld, _p(y), yld, B * H * W, C, act, prm, _stream())
+        _ledger.run(lambda: lib.cai_add_act(dcode(dt), _p(ap), ald, _p(bp), bld, _p(y), yld, B * H * W, C, act, prm,
+                                            _stream()),
+                    "add_act", "add_act_kernel", 0, 3 * B * H * W * C * _es(dt), dt)
         ctx.cfg = (act, prm, dt, yld)
         ctx.save_for_backward(y if act != ACT_NONE else None)
         return y
@@ -860,7 +956,8 @@ class GateFn(torch.autograd.Function):
             return tp
         ap, bp, xp = same(a), same(b), same(x)
         y = empty_pm(B, C, H, W, dt, a.device, ld=ld)
-        lib.cai_gate_fwd(dcode(dt), _p(ap), _p(bp), _p(xp), _p(y), ld, B * H * W, C, _stream())
+        _ledger.run(lambda: lib.cai_gate_fwd(dcode(dt), _p(ap), _p(bp), _p(xp), _p(y), ld, B * H * W, C, _stream()),
+                    "gate_fwd", "gate_fwd_kernel", 0, 4 * B * H * W * C * _es(dt), dt)
         ctx.cfg = (dt, ld)
         ctx.save_for_backward(ap, bp)
         return y
@@ -873,7 +970,9 @@ class GateFn(torch.autograd.Function):
         gp, gld = to_pm(g, dt, _vec(dt))
         da = empty_pm(B, C, H, W, dt, g.device, ld=ld)
         db = empty_pm(B, C, H, W, dt, g.device, ld=ld)
-        lib.cai_gate_bwd(dcode(dt), _p(ap), _p(bp), _p(gp), gld, _p(da), _p(db), ld, B * H * W, C, _stream())
+        _ledger.run(lambda: lib.cai_gate_bwd(dcode(dt), _p(ap), _p(bp), _p(gp), gld, _p(da), _p(db), ld, B * H * W, C,
+                                             _stream()),
+                    "gate_bwd", "gate_bwd_kernel", 0, 5 * B * H * W * C * _es(dt), dt)
         return da, db, g
 
 

@@ -371,8 +371,14 @@ class GaussianConditional(EntropyModel):
                 training: Optional[bool] = None) -> Tuple[torch.Tensor, torch.Tensor]:
         if training is None:
             training = self.training
-        if scales.shape != inputs.shape or (means is not None and means.shape != inputs.shape):
-            raise ValueError("inputs, scales and means must have the same shape")
+        # the reference's _likelihood broadcasts scales / means against the inputs (entropy_models.py:692-709)
+        try:
+            if scales.shape != inputs.shape:
+                scales = scales.expand_as(inputs)
+            if means is not None and means.shape != inputs.shape:
+                means = means.expand_as(inputs)
+        except RuntimeError as e:
+            raise ValueError(f"scales / means do not broadcast to the inputs' shape {tuple(inputs.shape)}") from e
         noise = _draw_noise(inputs) if training else None
         sb = self._scale_bound_value
         return GaussianFn.apply(inputs, scales, means, noise, Q_NOISE if training else Q_DEQUANTIZE, sb,

@@ -1,22 +1,35 @@
 """Fused Adam over one flat fp32 parameter buffer (examples/train.py:111-142,176-186).
 
-``FusedAdam(params, lr, betas, eps)`` behaves like ``torch.optim.Adam`` (no
-weight decay, no amsgrad): the parameters are re-homed as views of a single
-flat buffer and their ``.grad`` as views of a flat gradient buffer (autograd
-accumulates into it in place), so one ``cai_adam`` launch updates everything
-and ``step(max_norm=...)`` folds ``clip_grad_norm_`` in: the squared norm is a
-deterministic device reduction and the clip coefficient is applied inside the
-Adam kernel -- no host synchronisation, so a whole training step can be
-captured in one HIP graph.  The flat gradient is also the single buffer the
-data-parallel all-reduce runs on (compressai.distributed).
+``FusedAdam(params, lr, betas, eps)`` is a ``torch.optim.Optimizer`` with
+``torch.optim.Adam`` semantics (no weight decay, no amsgrad), so the
+reference's callers work on it unchanged: ``GradScaler.unscale_/step``,
+``clip_grad_norm_``, ``StepLR`` (it reads ``param_groups[0]["lr"]`` at every
+``step``) and ``state_dict()`` / ``load_state_dict()`` in torch's per-parameter
+Adam format (train.py:407,419,475).
+
+The parameters are re-homed as views of a single flat buffer and their
+``.grad`` as views of a flat gradient buffer (autograd and the backward
+kernels accumulate into it in place), so one ``cai_adam`` launch updates
+everything and ``step(max_norm=...)`` folds ``clip_grad_norm_`` in: the squared
+norm is a deterministic device reduction and the clip coefficient is applied
+inside the Adam kernel -- no host synchronisation, so a whole training step can
+be captured in one HIP graph.  A non-finite gradient norm skips the update on
+the device (GradScaler's skip rule).  The flat gradient is also the single
+buffer the data-parallel all-reduce runs on (compressai.distributed).
+
+If a caller breaks the gradient views (``model.zero_grad()`` with torch's
+default ``set_to_none=True``, or ``p.grad = None``), ``step`` copies the fresh
+gradients back into the flat buffer and re-attaches the views, so no update
+ever runs on stale gradients.
 """
 from __future__ import annotations
 
-import ctypes
+import math
 from typing import Iterable, List, Optional, Tuple
 
 import torch
 
+from . import _ledger
 from ._native import lib
 from ._ops import DIRECT_GRAD_ATTR, _p, _stream
 
@@ -25,22 +38,35 @@ def _align(n: int, a: int = 4) -> int:
     return (n + a - 1) // a * a
 
 
-class FusedAdam:
+class FusedAdam(torch.optim.Optimizer):
     def __init__(self, params: Iterable[torch.nn.Parameter], lr: float = 1e-3, betas: Tuple[float, float] = (0.9, 0.999),
-                 eps: float = 1e-8):
-        self.params: List[torch.nn.Parameter] = [p for p in params]
-        if not self.params:
+                 eps: float = 1e-8, skip_nonfinite: bool = True):
+        params = [p for p in params]
+        if not params:
             raise ValueError("optimizer got an empty parameter list")
+        if not 0.0 <= lr:
+            raise ValueError(f"Invalid learning rate: {lr}")
+        if not 0.0 <= eps:
+            raise ValueError(f"Invalid epsilon value: {eps}")
+        if not (0.0 <= betas[0] < 1.0 and 0.0 <= betas[1] < 1.0):
+            raise ValueError(f"Invalid beta parameters: {betas}")
+        super().__init__(params, dict(lr=float(lr), betas=(float(betas[0]), float(betas[1])), eps=float(eps)))
+        if len(self.param_groups) != 1:
+            raise ValueError("FusedAdam takes one parameter group")
+        self.params: List[torch.nn.Parameter] = list(self.param_groups[0]["params"])
         dev = self.params[0].device
         if dev.type != "cuda":
             raise ValueError("FusedAdam runs on GPU parameters only")
-        self.lr, self.betas, self.eps = float(lr), (float(betas[0]), float(betas[1])), float(eps)
+        self.skip_nonfinite = bool(skip_nonfinite)
         offs, n = [], 0
         for p in self.params:
             if p.dtype != torch.float32:
                 raise ValueError("FusedAdam expects fp32 master parameters")
+            if p.device != dev:
+                raise ValueError("FusedAdam expects all parameters on one device")
             offs.append(n)
             n += _align(p.numel())
+        self.offsets = offs
         self.numel = n
         self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
         self.flat_grad = torch.zeros(n, dtype=torch.float32, device=dev)
@@ -49,41 +75,135 @@ class FusedAdam:
         self.step_count = torch.zeros(1, dtype=torch.float32, device=dev)
         self.sqnorm = torch.zeros(1, dtype=torch.float32, device=dev)
         self._ws = torch.empty(lib.cai_reduce_workspace_bytes(n), dtype=torch.uint8, device=dev)
+        self._grad_views = []
         with torch.no_grad():
             for p, o in zip(self.params, offs):
                 view = self.flat[o:o + p.numel()].view_as(p)
                 view.copy_(p.data)
                 p.data = view
-                p.grad = self.flat_grad[o:o + p.numel()].view_as(p)
+                self._grad_views.append(self.flat_grad[o:o + p.numel()].view_as(p))
                 # let the backward kernels accumulate into p.grad directly
                 setattr(p, DIRECT_GRAD_ATTR, True)
+        self._attach_views()
 
-    def zero_grad(self, set_to_none: bool = False):
-        # grads stay views of the flat buffer (set_to_none is ignored on purpose)
+    # -- compatibility knobs read by older callers -------------------------------------------------
+    @property
+    def lr(self) -> float:
+        return float(self.param_groups[0]["lr"])
+
+    @lr.setter
+    def lr(self, v: float):
+        self.param_groups[0]["lr"] = float(v)
+
+    @property
+    def betas(self) -> Tuple[float, float]:
+        return tuple(self.param_groups[0]["betas"])
+
+    @property
+    def eps(self) -> float:
+        return float(self.param_groups[0]["eps"])
+
+    # -- gradient views ------------------------------------------------------------------------------
+    def _attach_views(self):
+        for p, v in zip(self.params, self._grad_views):
+            p.grad = v
+
+    def _sync_grad_views(self):
+        """Re-home gradients a caller detached from the flat buffer (host-side pointer check; launches
+        only when a view was actually broken)."""
+        for p, v in zip(self.params, self._grad_views):
+            g = p.grad
+            if g is None:
+                v.zero_()
+            elif g.data_ptr() != v.data_ptr() or g.shape != v.shape:
+                v.copy_(g)
+            else:
+                continue
+            p.grad = v
+
+    def zero_grad(self, set_to_none: bool = True):
+        # the gradients stay views of the flat buffer; set_to_none zeroes them instead of unlinking them
         self.flat_grad.zero_()
+        self._attach_views()
 
     def grad_sqnorm(self) -> torch.Tensor:
-        lib.cai_sqnorm(_p(self.flat_grad), self.numel, _p(self.sqnorm), _p(self._ws), self._ws.numel(), _stream())
+        _ledger.run(lambda: lib.cai_sqnorm(_p(self.flat_grad), self.numel, _p(self.sqnorm), _p(self._ws),
+                                           self._ws.numel(), _stream()),
+                    "sqnorm", "sqnorm (reduce)", 2.0 * self.numel, 4 * self.numel, torch.float32)
         return self.sqnorm
 
-    def step(self, max_norm: Optional[float] = None):
+    @torch.no_grad()
+    def step(self, closure=None, max_norm: Optional[float] = None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        self._sync_grad_views()
+        clip = max_norm is not None and max_norm > 0
         sq = None
-        if max_norm is not None and max_norm > 0:
+        if clip or self.skip_nonfinite:
             self.grad_sqnorm()
             sq = self.sqnorm
-        lib.cai_adam(_p(self.flat), _p(self.flat_grad), _p(self.exp_avg), _p(self.exp_avg_sq), self.numel, self.lr,
-                     self.betas[0], self.betas[1], self.eps, _p(self.step_count), _p(sq),
-                     float(max_norm) if sq is not None else 0.0, _stream())
+        g = self.param_groups[0]
+        b1, b2 = g["betas"]
+        _ledger.run(lambda: lib.cai_adam(_p(self.flat), _p(self.flat_grad), _p(self.exp_avg), _p(self.exp_avg_sq),
+                                         self.numel, float(g["lr"]), float(b1), float(b2), float(g["eps"]),
+                                         _p(self.step_count), _p(sq), float(max_norm) if clip else math.inf,
+                                         _stream()),
+                    "adam", "adam_kernel", 0, 28 * self.numel, torch.float32, f"{self.numel} parameters")
+        return loss
 
+    # -- checkpoints in torch.optim.Adam's format (train.py:407,419,475) -------------------------------
     def state_dict(self):
-        return {"lr": self.lr, "betas": self.betas, "eps": self.eps, "step": self.step_count.clone(),
-                "exp_avg": self.exp_avg.clone(), "exp_avg_sq": self.exp_avg_sq.clone()}
+        steps = float(self.step_count.item())
+        state = {}
+        if steps > 0:
+            for i, (p, o) in enumerate(zip(self.params, self.offsets)):
+                n = p.numel()
+                state[i] = {"step": torch.tensor(steps),
+                            "exp_avg": self.exp_avg[o:o + n].view_as(p).clone(),
+                            "exp_avg_sq": self.exp_avg_sq[o:o + n].view_as(p).clone()}
+        g = self.param_groups[0]
+        group = {"lr": g["lr"], "betas": tuple(g["betas"]), "eps": g["eps"], "weight_decay": 0, "amsgrad": False,
+                 "maximize": False, "foreach": None, "capturable": False, "differentiable": False, "fused": None,
+                 "params": list(range(len(self.params)))}
+        if "initial_lr" in g:
+            group["initial_lr"] = g["initial_lr"]
+        return {"state": state, "param_groups": [group]}
 
     def load_state_dict(self, sd):
-        self.lr, self.betas, self.eps = sd["lr"], tuple(sd["betas"]), sd["eps"]
-        self.step_count.copy_(sd["step"])
-        self.exp_avg.copy_(sd["exp_avg"])
-        self.exp_avg_sq.copy_(sd["exp_avg_sq"])
+        if "exp_avg" in sd and "state" not in sd:    # the flat layout of round-1 checkpoints
+            self.param_groups[0].update(lr=float(sd["lr"]), betas=tuple(sd["betas"]), eps=float(sd["eps"]))
+            self.step_count.copy_(sd["step"])
+            self.exp_avg.copy_(sd["exp_avg"])
+            self.exp_avg_sq.copy_(sd["exp_avg_sq"])
+            return
+        groups = sd["param_groups"]
+        if len(groups) != 1 or len(groups[0]["params"]) != len(self.params):
+            raise ValueError("loaded state dict does not match this optimizer's parameters")
+        if groups[0].get("weight_decay", 0) or groups[0].get("amsgrad", False) or groups[0].get("maximize", False):
+            raise ValueError("FusedAdam supports Adam without weight decay, amsgrad or maximize")
+        g = self.param_groups[0]
+        for k in ("lr", "eps", "initial_lr"):
+            if k in groups[0]:
+                g[k] = float(groups[0][k])
+        g["betas"] = tuple(float(b) for b in groups[0]["betas"])
+        state = sd["state"]
+        self.exp_avg.zero_()
+        self.exp_avg_sq.zero_()
+        steps = 0.0
+        for slot, pid in enumerate(groups[0]["params"]):
+            s = state.get(pid)
+            if not s:
+                continue
+            p, o = self.params[slot], self.offsets[slot]
+            n = p.numel()
+            if s["exp_avg"].numel() != n:
+                raise ValueError(f"state of parameter {pid}: {s['exp_avg'].numel()} elements, expected {n}")
+            self.exp_avg[o:o + n].copy_(s["exp_avg"].reshape(-1))
+            self.exp_avg_sq[o:o + n].copy_(s["exp_avg_sq"].reshape(-1))
+            steps = float(s["step"])
+        self.step_count.fill_(steps)
 
 
 def parameter_groups(net):

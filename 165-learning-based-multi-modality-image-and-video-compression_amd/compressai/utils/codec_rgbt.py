@@ -274,6 +274,13 @@ def decode_image(inputpath: str, net, guided: Optional[torch.Tensor] = None) -> 
     return hdr, crop(x_hat, hdr.original_size)
 
 
+def _device(args) -> str:
+    """This build's kernels are GPU-only: the CLIs always use the GPU and fail up front without one."""
+    if not torch.cuda.is_available():
+        raise SystemExit("codec_rgbt: this build runs on the GPU only (MI355X HIP kernels) and no GPU is visible")
+    return "cuda"
+
+
 def _load_nets(model: str, paths: Sequence[str], channel: int, device):
     from compressai.utils.eval_model.__main__ import load_checkpoint
 
@@ -297,7 +304,7 @@ def _common_args(p: argparse.ArgumentParser):
     p.add_argument("-ch", "--channel", type=int, default=3, help="master image channels")
     p.add_argument("--guided", default=None, help="guide-modality image (default: derived from the input path)")
     p.add_argument("-c", "--coder", default="ans")
-    p.add_argument("--cuda", action="store_true")
+    p.add_argument("--cuda", action="store_true", help="accepted for compatibility: this build always runs on the GPU")
     p.add_argument("-o", "--output", required=True)
 
 
@@ -311,7 +318,7 @@ def encode(argv):
     _common_args(p)
     a = p.parse_args(argv)
     compressai.set_entropy_coder(a.coder)
-    device = "cuda" if a.cuda else "cpu"
+    device = _device(a)
     net = _load_nets(a.model, a.path, a.channel, device)
     x = load_master_image(a.input, a.channel, device)
     guided = None
@@ -330,7 +337,7 @@ def decode(argv):
     _common_args(p)
     a = p.parse_args(argv)
     compressai.set_entropy_coder(a.coder)
-    device = "cuda" if a.cuda else "cpu"
+    device = _device(a)
     net = _load_nets(a.model, a.path, a.channel, device)
     guided = None
     if a.model == "Master_compresser":

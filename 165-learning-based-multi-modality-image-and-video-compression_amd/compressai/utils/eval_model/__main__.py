@@ -231,7 +231,7 @@ def setup_args():
     parent.add_argument("-a", "--architecture", type=str, required=True, help="model architecture")
     parent.add_argument("-c", "--entropy-coder", choices=compressai.available_entropy_coders(),
                         default=compressai.available_entropy_coders()[0], help="entropy coder (default: %(default)s)")
-    parent.add_argument("--cuda", action="store_true", help="enable the GPU (MI355X)")
+    parent.add_argument("--cuda", action="store_true", help="accepted for compatibility: this build always runs on the GPU")
     parent.add_argument("--half", action="store_true", help="bf16 autocast transforms")
     parent.add_argument("--entropy-estimation", action="store_true",
                         help="use evaluated entropy estimation (no entropy coding)")
@@ -267,7 +267,9 @@ def main(argv):
         print("Error: no images found in directory.", file=sys.stderr)
         raise SystemExit(1)
     compressai.set_entropy_coder(args.entropy_coder)
-    device = "cuda" if args.cuda and torch.cuda.is_available() else "cpu"
+    if not torch.cuda.is_available():
+        raise SystemExit("eval_model: this build runs on the GPU only (MI355X HIP kernels) and no GPU is visible")
+    device = "cuda"
     paired = args.guided_dataset is not None
     results = defaultdict(list)
     for run in args.paths:

@@ -2379,6 +2379,34 @@ int cai_conv_dgrad(const cai_conv_geom* g, int dtype, const void* dy, int32_t dy
                     mask_param, workspace, ws_bytes, stream, "conv_dgrad");
 }
 
+const char* cai_conv_kernel_name(const cai_conv_geom* g, int dtype, int direction, int32_t in_abs) {
+    if (check_geom(g) || (dtype != CAI_BF16 && dtype != CAI_F32) || direction < 0 || direction > 2) return "";
+    if (direction == 2) {
+        const WgradPlan W = make_wgrad_plan(g, dtype, true);
+        if (!W.glds) return dtype == CAI_BF16 ? "wgrad_kernel<bf16>" : "wgrad_kernel<float>";
+        return W.ct == 256 ? "wgrad_glds_kernel<256>" : "wgrad_glds_kernel<128>";
+    }
+    const ConvLaunch L = conv_launch(g, dtype, direction, in_abs);
+    if (L.halo) return L.halo == 5 ? "conv_halo_kernel<5>" : "conv_halo_kernel<3>";
+    if (L.halo_ph) return "conv_halo_phase_kernel";
+    switch (L.cfg) {
+        case CFG_G1: return "conv_glds_kernel<256x128>";
+        case CFG_G2: return "conv_glds_kernel<128x192>";
+        case CFG_G3: return "conv_glds_kernel<256x64>";
+        case CFG_G4: return "conv_glds_kernel<128x128>";
+        case CFG_S: return dtype == CAI_BF16 ? "conv_gemm_kernel<bf16,256x16>" : "conv_gemm_kernel<float,256x16>";
+        case CFG_M: return dtype == CAI_BF16 ? "conv_gemm_kernel<bf16,128x64>" : "conv_gemm_kernel<float,128x64>";
+        case CFG_W: return dtype == CAI_BF16 ? "conv_gemm_kernel<bf16,64x192>" : "conv_gemm_kernel<float,64x192>";
+        default: return dtype == CAI_BF16 ? "conv_gemm_kernel<bf16,128x128>" : "conv_gemm_kernel<float,128x128>";
+    }
+}
+
+int32_t cai_conv_split_factor(const cai_conv_geom* g, int dtype, int direction, int32_t in_abs) {
+    if (check_geom(g) || (dtype != CAI_BF16 && dtype != CAI_F32) || direction < 0 || direction > 2) return 0;
+    if (direction == 2) return make_wgrad_plan(g, dtype, true).S;
+    return conv_launch(g, dtype, direction, in_abs).ksplit;
+}
+
 size_t cai_conv_wgrad_workspace_bytes(const cai_conv_geom* g, int dtype) {
     if (check_geom(g)) return 0;
     const WgradPlan W0 = make_wgrad_plan(g, dtype, false), W1 = make_wgrad_plan(g, dtype, true);

@@ -6,6 +6,9 @@
 // clip_grad_norm_(max_norm) (train.py:178) is folded in: the kernel scales g
 // by min(1, max_norm/(||g|| + 1e-6)) read from the device-side squared norm,
 // so the whole step stays on the stream (graph-capturable, no host sync).
+// A non-finite squared norm skips the whole update, step counter included:
+// what GradScaler.step does when unscale_ found inf/NaN gradients
+// (train.py:176-179).
 #include "common.hpp"
 
 #include <stdarg.h>
@@ -25,6 +28,7 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
                             float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps,
                             const float* __restrict__ step, const float* __restrict__ sqnorm, float max_norm) {
     // *step holds the number of steps already taken; this step is t = *step + 1
+    if (sqnorm && !isfinite(*sqnorm)) return;
     const float t = *step + 1.f;
     const float bc1 = 1.f - powf(b1, t);
     const float bc2s = sqrtf(1.f - powf(b2, t));
@@ -59,7 +63,10 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
     }
 }
 
-__global__ void step_incr_kernel(float* step) { *step += 1.f; }
+__global__ void step_incr_kernel(float* step, const float* __restrict__ sqnorm) {
+    if (sqnorm && !isfinite(*sqnorm)) return;
+    *step += 1.f;
+}
 
 }  // namespace cai
 
@@ -69,7 +76,7 @@ extern "C" {
 
 const char* cai_last_error(void) { return g_err; }
 int cai_version(void) { return 1; }
-int cai_abi_count(void) { return 69; }
+int cai_abi_count(void) { return 71; }
 
 int cai_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps,
              float* step, const float* sqnorm, float max_norm, void* stream) {
@@ -82,7 +89,7 @@ int cai_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, 
         hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), p, g, m, v, n, lr,
                            beta1, beta2, eps, step, sqnorm, max_norm);
     }
-    hipLaunchKernelGGL(step_incr_kernel, dim3(1), dim3(1), 0, as_stream(stream), step);
+    hipLaunchKernelGGL(step_incr_kernel, dim3(1), dim3(1), 0, as_stream(stream), step, sqnorm);
     CAI_LAUNCH_CHECK("adam");
     return CAI_OK;
 }

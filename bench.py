@@ -6,22 +6,38 @@ quality 1 -> N=128, M=192), bf16 autocast, 16 synthetic U[0,1) 256x256 RGB
 patches per GPU, one step = forward + RD loss + backward + clip_grad_norm(1.0)
 + Adam (main) + aux-loss backward + Adam (aux), i.e. examples/train.py:155-186.
 Inputs live in HBM before the timed region; the whole step is replayed from
-HIP graphs.  Multi-GPU: one process per GPU (torchrun), per-patch data
-parallelism, one RCCL all-reduce (average) of the flat gradient per step;
-per-GPU batch is fixed (weak scaling) and `value` is the whole-job rate.
+HIP graphs.
 
-Also reported:
-  roofline     -- the dominant kernel timed live with HIP events on its own
-                  stream, algorithmic FLOPs / average launch time vs the bf16
-                  dense MFMA peak (2.5 PFLOP/s);
-  cpu_baseline -- the CPU oracle (op-for-op restatement of the reference path,
-                  fp32) timed on this host on a bounded sample (rank 0, N=1).
+Multi-GPU: one process per GPU.  `python bench.py --gpus N` starts N rank
+processes itself (before anything touches the GPU) with RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR=127.0.0.1 set; under torchrun the ranks come from its
+environment.  Per-patch data parallelism with one RCCL all-reduce (average) of
+the flat gradient per step; each rank seeds its training noise differently;
+per-GPU batch is fixed (weak scaling) and `value` is the whole-job rate over
+the max-over-ranks time.
+
+Also reported (rank 0):
+  roofline      -- the step's dominant launch (the instrumented call with the
+                   largest GPU time in a profiled step, compressai/_ledger.py),
+                   replayed alone and timed with HIP events on the stream it
+                   runs on: algorithmic FLOPs (or bytes) / average launch time
+                   vs the bf16 dense MFMA peak (or HBM peak); `traffic` from the
+                   committed rocprofv3 PMC passes for that launch, if any;
+  step_roofline -- SURVEY.md §8(d): roofline seconds per step = sum over the
+                   step's launches of max(FLOP/P_mfma, bytes/BW_hbm), divided by
+                   the measured seconds per step;
+  cpu_baseline  -- the CPU oracle (op-for-op restatement of the reference path,
+                   fp32) timed on this host on a bounded sample at the same
+                   per-step batch: all available cores, plus one thread
+                   (rank 0, N=1).
 """
 import argparse
 import ctypes
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,13 +47,8 @@ for _p in (PKG, os.path.join(ROOT, "oracle")):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
-
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
-BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 MM_IR = (512, 640)          # FLIR IR frame (ResearchReport.pdf 4.2; image_rgbt_rgb.py:133-141)
-HBM_PEAK_GBS = 8000.0
 
 
 def parse():
@@ -52,119 +63,224 @@ def parse():
                          "guided by Guided_compresser on RGB 1024x1280, train.py:208-274)")
     ap.add_argument("--quality", type=int, default=1)
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
-    ap.add_argument("--cpu-batch", type=int, default=2)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-batch", type=int, default=None, help="CPU baseline batch (default: the GPU per-step batch)")
+    ap.add_argument("--no-profile", action="store_true", help="skip the profiled step (no roofline fields)")
+    ap.add_argument("--ops-json", default=None, help="write the profiled step's per-launch table here")
     ap.add_argument("--roofline-only", action="store_true",
-                    help="only launch the roofline kernel --steps times (for rocprofv3 --pmc passes)")
+                    help="profile one step, then replay only its dominant launch --steps times "
+                         "(for rocprofv3 --pmc passes)")
+    ap.add_argument("--replay", default=None,
+                    help="with --roofline-only: replay this launch instead of the dominant one "
+                         "('kind:index' of the ops table, e.g. conv_wgrad:3)")
     return ap.parse_args()
 
 
-def dominant_kernel_roofline(B, size, reps=20):
-    """g_a[2]: Conv2d(128,128,k5,s2,p2) at (size/2)^2 -> (size/4)^2, bf16 implicit GEMM."""
-    H = size // 2
-    r = conv_roofline(B, 128, H, H, 128, 5, 2, reps)
-    r["kernel"] = ("conv_halo_kernel<5> (g_a[2] fwd: Conv2d 128->128 k5 s2, %dx%d->%dx%d, B=%d)"
-                   % (H, H, H // 2, H // 2, B))
-    r["traffic"] = pmc_traffic(B, size, r["kernel"].split()[0])
-    return r
+# --------------------------------------------------------------------------------------------------------
+# launcher: N rank processes, started before anything touches the GPU
+# --------------------------------------------------------------------------------------------------------
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
-def conv_roofline(B, C, H, W, N, k, stride, reps=20):
-    """One bf16 Conv2d(C, N, k, s, k//2) launch on its own stream, HIP-event timed."""
-    from compressai._native import BF16, ConvGeom, lib
-    from compressai._ops import _pack_weight, _p
-
-    OH, OW = (H + 2 * (k // 2) - k) // stride + 1, (W + 2 * (k // 2) - k) // stride + 1
-    g = ConvGeom(B, C, H, W, N, OH, OW, k, stride, k // 2, 0, 0)
-    dev = torch.device("cuda")
-    x = torch.randn(B, H, W, C, device=dev).to(torch.bfloat16)
-    w = torch.randn(N, C, k, k, device=dev) * 0.02
-    b = torch.zeros(N, device=dev)
-    y = torch.empty(B, OH, OW, N, device=dev, dtype=torch.bfloat16)
-    s = torch.cuda.Stream()
-    with torch.cuda.stream(s):
-        from compressai import _ops
-        wp = _pack_weight(g, torch.bfloat16, 0, w)
-        st = ctypes.c_void_p(s.cuda_stream)
-        nws = lib.cai_conv_workspace_bytes(ctypes.byref(g), BF16, 0)
-        ws = torch.empty(max(nws, 16), dtype=torch.uint8, device=dev)   # split-K scratch at small batch
-
-        def launch():
-            lib.cai_conv_fwd(ctypes.byref(g), BF16, _p(x), C, 0, _p(wp), _p(b), 0, 0.0, _p(y), BF16,
-                             OH * OW * N, 1, OW * N, N, _p(ws), nws, st)
-        for _ in range(3):
-            launch()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(s)
-        for _ in range(reps):
-            launch()
-        e1.record(s)
-    e1.synchronize()
-    ms = e0.elapsed_time(e1) / reps
-    flops = 2.0 * (B * OH * OW) * N * (k * k * C)
-    tflops = flops / (ms * 1e-3) / 1e12
-    name = "conv (Conv2d %d->%d k%d s%d, %dx%d->%dx%d, B=%d)" % (C, N, k, stride, H, W, OH, OW, B)
-    return {"kernel": name, "bound": "mfma", "achieved": round(tflops, 2), "peak": BF16_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(tflops / BF16_PEAK_TFLOPS, 4), "traffic": None,
-            "avg_launch_ms": round(ms, 4), "algorithmic_flop_per_launch": flops,
-            "algorithmic_bytes_per_launch": B * H * W * C * 2 + N * C * k * k * 2 + B * OH * OW * N * 2}
+def spawn_ranks(n: int) -> int:
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        c = p.wait()
+        if c and not rc:
+            rc = c
+    return rc
 
 
-def pmc_traffic(B, size, kernel):
-    """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC passes
-    (profiles/pmc_traffic.json, written by tools/pmc_summary.py: 2 x FETCH_SIZE + WRITE_SIZE,
-    MI355X_MICROARCH.md 'HBM'); null when no measurement for this workload is committed."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+# --------------------------------------------------------------------------------------------------------
+# measurement helpers
+# --------------------------------------------------------------------------------------------------------
+
+def host_cores() -> int:
+    """CPUs this process may use: affinity mask, capped by a cgroup v2 CPU quota when one is set."""
     try:
-        rec = json.load(open(path))
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def profile_step(step_fn):
+    """One step under the ledger with the GPU queue pre-filled (a sleep kernel holds the stream while the host
+    enqueues the whole step), so each launch's event pair brackets GPU time only."""
+    import torch
+
+    from compressai import _ledger
+
+    torch.cuda.synchronize()
+    torch.cuda._sleep(int(1e9))        # ~0.4 s of GPU spin: the host runs ahead of the device
+    with _ledger.recording() as led:
+        step_fn()
+    led.finish()
+    return led
+
+
+def replay_time(entry, reps: int) -> float:
+    """Average ms of one launch, replayed alone `reps` times between two HIP events on the current stream."""
+    import torch
+
+    for _ in range(3):
+        entry.replay()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        entry.replay()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def pmc_traffic(workload: str, kernel: str, shape: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/pmc_traffic.json, written by
+    tools/pmc_summary.py: 2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md 'HBM'); None when no measurement
+    of this exact launch is committed."""
+    try:
+        recs = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
     except (OSError, ValueError):
         return None
-    if rec.get("batch") != B or rec.get("size") != size or rec.get("kernel", "").split()[0] != kernel:
-        return None
-    return rec.get("hbm_bytes_per_launch")
+    if isinstance(recs, dict):
+        recs = [recs]
+    for r in recs:
+        if r.get("workload") == workload and r.get("kernel") == kernel and r.get("shape") == shape:
+            return r.get("hbm_bytes_per_launch")
+    return None
+
+
+def dominant_roofline(led, workload: str, reps: int = 20, pick=None):
+    from compressai import _ledger
+
+    ents = led.entries
+    if pick is not None:
+        kind, idx = pick.split(":")
+        e = [x for x in ents if x.kind == kind][int(idx)]
+    else:
+        e = max(ents, key=lambda x: x.ms)
+    ms = replay_time(e, reps)
+    bound = e.bound()
+    if bound == "mfma":
+        achieved, peak, unit = e.flops / (ms * 1e9), e.peak_tflops(), "TFLOP/s"
+    else:
+        achieved, peak, unit = e.nbytes / (ms * 1e6), _ledger.HBM_PEAK_GBS, "GB/s"
+    return {"kernel": e.kernel, "launch": f"{e.kind}: {e.shape}", "bound": bound, "achieved": round(achieved, 2),
+            "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
+            "traffic": pmc_traffic(workload, e.kernel, e.shape),
+            "avg_launch_ms": round(ms, 5), "in_step_ms": round(e.ms, 5),
+            "algorithmic_flop_per_launch": e.flops, "algorithmic_bytes_per_launch": e.nbytes,
+            "timing": f"HIP events on the launch's stream, {reps} back-to-back replays"}
+
+
+def step_roofline(led, ms_per_step: float):
+    rl = sum(e.roofline_ms() for e in led.entries)
+    busy = sum(e.ms for e in led.entries)
+    flops = sum(e.flops for e in led.entries)
+    nbytes = sum(e.nbytes for e in led.entries)
+    return {"roofline_ms_per_step": round(rl, 4), "measured_ms_per_step": round(ms_per_step, 4),
+            "frac": round(rl / ms_per_step, 4), "launches_instrumented": len(led.entries),
+            "instrumented_gpu_ms": round(busy, 4), "flop_per_step": flops, "bytes_per_step": nbytes,
+            "achieved_tflops": round(flops / (ms_per_step * 1e9), 2),
+            "note": "sum over the step's launches of max(FLOP/2.5 PF/s bf16 | 157 TF/s fp32, bytes/8 TB/s) "
+                    "(SURVEY.md 8(d)); algorithmic FLOPs / bytes per launch from compressai/_ledger.py"}
+
+
+def ops_table(led):
+    rows = [e.as_dict() for e in led.entries]
+    by_kernel = {}
+    for r in rows:
+        k = by_kernel.setdefault(r["kernel"], {"kernel": r["kernel"], "launches": 0, "ms": 0.0, "flops": 0.0,
+                                               "bytes": 0.0, "roofline_ms": 0.0})
+        k["launches"] += 1
+        k["ms"] += r["ms"]
+        k["flops"] += r["flops"]
+        k["bytes"] += r["bytes"]
+        k["roofline_ms"] += r["roofline_ms"]
+    kernels = sorted(by_kernel.values(), key=lambda k: -k["ms"])
+    return {"launches": rows, "by_kernel": kernels}
 
 
 def cpu_baseline(model_name, quality, batch, size, seconds):
+    import torch
+
     import cai_oracle as O
 
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
-    torch.manual_seed(0)
-    net = O.build(model_name, quality)
-    opt, aux_opt = O.configure_optimizers(net)
-    crit = O.RateDistortionLoss(quality)
-    x = torch.rand(batch, 3, size, size, generator=torch.Generator().manual_seed(0))
-    O.train_step(net, crit, x, opt, aux_opt)           # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
-        O.train_step(net, crit, x, opt, aux_opt)
-        n += 1
-        dt = time.perf_counter() - t0
-        if dt >= seconds or n >= 50:
-            break
-    return {"value": round(n * batch / dt, 4), "unit": "patches/s", "cores": threads, "kind": "port",
-            "sample": f"oracle {model_name} q{quality} fp32 train step (fwd+bwd+clip+Adam+aux), batch {batch} "
-                      f"@ {size}x{size}, {n} timed steps after 1 warm-up, torch CPU threads={threads}"}
+    cores = host_cores()
 
+    def run(threads, min_steps, budget):
+        torch.set_num_threads(threads)
+        torch.manual_seed(0)
+        net = O.build(model_name, quality)
+        opt, aux_opt = O.configure_optimizers(net)
+        crit = O.RateDistortionLoss(quality)
+        x = torch.rand(batch, 3, size, size, generator=torch.Generator().manual_seed(0))
+        xw = x[: min(2, batch)]
+        O.train_step(net, crit, xw, opt, aux_opt)           # warm-up (small batch)
+        n, t0 = 0, time.perf_counter()
+        while True:
+            O.train_step(net, crit, x, opt, aux_opt)
+            n += 1
+            dt = time.perf_counter() - t0
+            if n >= min_steps and (dt >= budget or n >= 50):
+                break
+        return n, dt
+
+    n, dt = run(cores, 1, seconds)
+    n1, dt1 = run(1, 1, 0.0)
+    torch.set_num_threads(cores)
+    return {"value": round(n * batch / dt, 4), "unit": "patches/s", "cores": cores, "kind": "port",
+            "host_cpus": os.cpu_count(), "value_1thread": round(n1 * batch / dt1, 4),
+            "sample": f"oracle {model_name} q{quality} fp32 train step (fwd+bwd+clip+Adam+aux), batch {batch} "
+                      f"@ {size}x{size} (same per-step batch as the GPU), {n} timed steps after a batch-2 warm-up "
+                      f"on {cores} threads (the CPUs this process may use: affinity / cgroup quota; "
+                      f"os.cpu_count()={os.cpu_count()}); value_1thread: {n1} step(s) on 1 thread "
+                      f"(the reference eval scripts' torch.set_num_threads(1), __main__t.py:61)"}
+
+
+# --------------------------------------------------------------------------------------------------------
+# the benchmark
+# --------------------------------------------------------------------------------------------------------
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     if args.batch is None:
         args.batch = 2 if args.model == "multimodal" else 16
+
+    import torch
+    import torch.distributed as dist
+
     from compressai.distributed import allreduce_mean_, broadcast_parameters_, init_from_env
     from compressai.losses import RateDistortionLoss
     from compressai.optim import configure_optimizers
     from compressai.zoo import image_models
 
-    if args.roofline_only:
-        torch.cuda.set_device(0)
-        print(json.dumps(dominant_kernel_roofline(args.batch, args.size, reps=args.steps)))
-        return
     rank, world = init_from_env()
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but the job has {world} ranks")
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    torch.manual_seed(0)
+    torch.manual_seed(0)                     # identical initial weights (rank 0's are broadcast anyway)
     multimodal = args.model == "multimodal"
     gen = torch.Generator().manual_seed(1234 + rank)
     if multimodal:
@@ -182,6 +298,7 @@ def main():
         net = image_models[args.model](args.quality).to(dev).train()
         x = torch.rand(args.batch, 3, args.size, args.size, generator=gen).to(dev)
     broadcast_parameters_(net)
+    torch.cuda.manual_seed(1000 + rank)      # per-rank training noise
     opt, aux_opt = configure_optimizers(net)
     criterion = RateDistortionLoss(args.quality)
     state = {}
@@ -204,10 +321,32 @@ def main():
         aux.backward()
         aux_opt.step()
 
+    def local_step():
+        fwd_bwd()
+        opt_part()
+
     def eager_step():
         fwd_bwd()
         allreduce_mean_(opt.flat_grad)
         opt_part()
+
+    if multimodal:
+        workload = ("multimodal paired codec: Master_compresser(IR 1x%dx%d) + Guided_compresser(RGB 3x%dx%d, "
+                    "no_grad fp32) RD-loss training step (fwd+bwd+clip+Adam+aux), HIP-graph replay"
+                    % (MM_IR[0], MM_IR[1], 2 * MM_IR[0], 2 * MM_IR[1]))
+    else:
+        workload = (f"{args.model} q{args.quality} B={args.batch} {args.size}x{args.size} RD-loss training step "
+                    f"(fwd+bwd+clip+Adam+aux), HIP-graph replay")
+
+    if args.roofline_only:
+        for _ in range(2):
+            local_step()
+        led = profile_step(local_step)
+        if rank == 0:
+            print(json.dumps(dominant_roofline(led, workload, reps=args.steps, pick=args.replay)), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     step = eager_step
     if not args.no_graph:
@@ -234,6 +373,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -247,34 +387,34 @@ def main():
     loss = float(state["loss"].item())
     if not math.isfinite(loss):
         raise RuntimeError(f"non-finite loss {loss}")
+    ms_per_step = dt / args.steps * 1e3
 
-    roof = None
-    if rank == 0:
-        # multimodal: Channel_aligner conv2 (256->256 k3 at 512x640), ~70 % of its FLOPs
-        roof = (conv_roofline(args.batch, 256, MM_IR[0], MM_IR[1], 256, 3, 1) if multimodal
-                else dominant_kernel_roofline(args.batch, args.size))
+    roof = step_roof = None
+    if rank == 0 and not args.no_profile:
+        led = profile_step(local_step)
+        roof = dominant_roofline(led, workload)
+        step_roof = step_roofline(led, ms_per_step)
+        if args.ops_json:
+            with open(args.ops_json, "w") as f:
+                json.dump(ops_table(led), f, indent=1)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0 and not multimodal:
-        cpu = cpu_baseline(args.model, args.quality, args.cpu_batch, args.size, args.cpu_seconds)
+        cpu = cpu_baseline(args.model, args.quality, args.cpu_batch or args.batch, args.size, args.cpu_seconds)
     if rank == 0:
         value = world * args.batch * args.steps / dt
         unit = "IR+RGB pairs/s" if multimodal else "patches/s"
-        workload = ("multimodal paired codec: Master_compresser(IR 1x%dx%d) + Guided_compresser(RGB 3x%dx%d, "
-                    "no_grad fp32) RD-loss training step (fwd+bwd+clip+Adam+aux), HIP-graph replay"
-                    % (MM_IR[0], MM_IR[1], 2 * MM_IR[0], 2 * MM_IR[1]) if multimodal else
-                    f"{args.model} q{args.quality} RD-loss training step (fwd+bwd+clip+Adam+aux), HIP-graph replay")
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": unit, "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": ("synthetic U[0,1) IR/RGB frame pairs, random-init weights" if multimodal else
                      "synthetic U[0,1) 256x256 RGB patches, random-init weights"),
             "config": {"workload": workload,
-                       "model": args.model, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
-                       "seq_len": None, "patch": list(MM_IR) if multimodal else args.size,
-                       "parallelism": f"dp{world}"},
+                       "model": args.model, "quality": args.quality, "global_batch": args.batch * world,
+                       "per_gpu_batch": args.batch, "seq_len": None,
+                       "patch": list(MM_IR) if multimodal else args.size, "parallelism": f"dp{world}"},
             "final_loss": round(loss, 5),
-            "roofline": roof, "cpu_baseline": cpu,
+            "roofline": roof, "step_roofline": step_roof, "cpu_baseline": cpu,
         }
         if cpu:
             line["gpu_over_cpu"] = round(value / cpu["value"], 1)

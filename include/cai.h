@@ -141,6 +141,13 @@ int cai_conv_dgrad(const cai_conv_geom* g, int dtype,
                    int32_t mask_mode, float mask_param, const void* aux, int32_t aux_ld,
                    void* workspace, size_t ws_bytes, void* stream);
 
+/* Diagnostics for measurement (bench.py's per-launch roofline):
+ * the kernel a conv call would launch (direction 0 = forward, 1 = input
+ * gradient, 2 = weight gradient) as the name rocprofv3 reports, "" for an
+ * invalid call; and its split factor (split-K slabs / wgrad pixel splits). */
+const char* cai_conv_kernel_name(const cai_conv_geom* g, int dtype, int direction, int32_t in_abs);
+int32_t cai_conv_split_factor(const cai_conv_geom* g, int dtype, int direction, int32_t in_abs);
+
 /* weight / bias gradient (fp32, torch layout; overwritten, or added to the
  * existing values when accumulate != 0 -- the .grad += semantics of autograd,
  * used to write straight into an optimizer's flat gradient buffer).
@@ -424,8 +431,11 @@ int cai_sqdiff_bwd(const float* a, const float* b, int64_t n, const float* scale
 /* state[0] = sum(g^2) (fp32); workspace >= cai_reduce_workspace_bytes(n) */
 int cai_sqnorm(const float* g, int64_t n, float* out, void* workspace, size_t ws_bytes, void* stream);
 /* One Adam step on n parameters; grads are first scaled by
- * min(1, max_norm / (sqrt(*sqnorm) + 1e-6)) when sqnorm != NULL (clip_grad_norm_).
- * *step (fp32, device) is incremented by the kernel's first block before use. */
+ * min(1, max_norm / (sqrt(*sqnorm) + 1e-6)) when sqnorm != NULL (clip_grad_norm_;
+ * max_norm = +inf: finiteness check only).  A non-finite *sqnorm skips the step
+ * (parameters, moments and *step untouched), like GradScaler.step after
+ * unscale_ found inf/NaN (examples/train.py:176-179).
+ * *step (fp32, device) counts the steps taken. */
 int cai_adam(float* p, const float* g, float* m, float* v, int64_t n,
              float lr, float beta1, float beta2, float eps,
              float* step, const float* sqnorm, float max_norm, void* stream);

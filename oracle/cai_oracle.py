@@ -734,4 +734,4 @@ def entropy_estimation(net, x):
     N, _, H, W = x.shape
     npix = N * H * W
     bpp = sum(torch.log(l).sum() / (-math.log(2) * npix) for l in out["likelihoods"].values())
-    return {"bpp": float(bpp), "psnr": psnr(out["x_hat"].clamp(0, 1), x), "x_hat": out["x_hat"]}
+    return {"bpp": float(bpp), "psnr": psnr(out["x_hat"], x), "x_hat": out["x_hat"]}   # no clamp: __main__t.py:169,207

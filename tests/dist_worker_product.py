@@ -1,0 +1,82 @@
+"""One rank of tests/test_distributed_gpu.py (not collected by pytest).
+
+Rank r of a world-2 job on cuda:0 (gloo over CUDA tensors): the product ScaleHyperprior, FusedAdam, a
+HIP-graph-captured forward + RD loss + backward with the injected noise read from static device buffers, then
+compressai.distributed.allreduce_mean_(opt.flat_grad) -- the exchange bench.py runs between its two graphs.
+Writes the averaged flat gradient (rank 0) to $CAI_DIST_OUT.
+"""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+for p in (os.path.join(ROOT, "165-learning-based-multi-modality-image-and-video-compression_amd"),
+          os.path.join(ROOT, "oracle")):
+    sys.path.insert(0, p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def main():
+    from compressai.distributed import allreduce_mean_, broadcast_parameters_, init_from_env
+    from compressai.entropy_models import set_noise_source
+    from compressai.losses import RateDistortionLoss
+    from compressai.models import ScaleHyperprior
+    from compressai.optim import configure_optimizers, parameter_groups
+
+    inp = torch.load(os.environ["CAI_DIST_IN"], weights_only=True)
+    rank, world = init_from_env(backend="gloo")
+    assert world == 2
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    net = ScaleHyperprior(32, 48)
+    net.load_state_dict(inp["state_dict"])
+    net = net.to(dev).train()
+    broadcast_parameters_(net)
+    opt, aux_opt = configure_optimizers(net)
+    b = inp["x"].shape[0] // world
+    sl = slice(rank * b, (rank + 1) * b)
+    x = inp["x"][sl].to(dev)
+    noise = [n[sl].to(dev) for n in inp["noise"]]
+    draw = {"i": 0}
+
+    def source(t):
+        n = noise[draw["i"] % len(noise)]
+        draw["i"] += 1
+        return n
+
+    set_noise_source(source)
+    crit = RateDistortionLoss(1)
+
+    def fwd_bwd():
+        opt.zero_grad()
+        aux_opt.zero_grad()
+        out = net(x)
+        crit(out, x)["loss"].backward()
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            fwd_bwd()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        fwd_bwd()
+    opt.flat_grad.fill_(123.0)           # the replay must overwrite this
+    graph.replay()
+    allreduce_mean_(opt.flat_grad)
+    torch.cuda.synchronize()
+    set_noise_source(None)
+    if rank == 0:
+        main_names, _ = parameter_groups(net)
+        torch.save({"flat_grad": opt.flat_grad.cpu(), "offsets": list(opt.offsets), "names": main_names,
+                    "numels": [p.numel() for p in opt.params]}, os.environ["CAI_DIST_OUT"])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
