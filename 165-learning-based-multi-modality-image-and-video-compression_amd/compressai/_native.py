@@ -88,6 +88,9 @@ SIGNATURES = {
     "cai_edge_wgrad": (_I, [_G, _P, _P, c_int32, _P, _P, c_int32, _P, _S, _P]),
     "cai_add_act": (_I, [_I, _P, c_int32, _P, c_int32, _P, c_int32, _I64, c_int32, c_int32, _F, _P]),
     "cai_act": (_I, [_I, _P, c_int32, _P, c_int32, _I64, c_int32, c_int32, _F, _P]),
+    "cai_gdn1_out": (_I, [_I, _P, c_int32, _P, c_int32, _P, c_int32, _I64, c_int32, c_int32, _P]),
+    "cai_gdn1_out_bwd": (_I, [_I, _P, c_int32, _P, c_int32, _P, c_int32, _P, c_int32, _P, c_int32, _I64, c_int32,
+                              c_int32, _P]),
     "cai_gate_fwd": (_I, [_I, _P, _P, _P, _P, c_int32, _I64, c_int32, _P]),
     "cai_gate_bwd": (_I, [_I, _P, _P, _P, c_int32, _P, _P, c_int32, _I64, c_int32, _P]),
     "cai_pixel_shuffle": (_I, [_I, _P, POINTER(c_int64), _P, POINTER(c_int64), c_int32, c_int32, c_int32, c_int32,

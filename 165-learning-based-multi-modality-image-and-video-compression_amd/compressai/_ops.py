@@ -558,6 +558,38 @@ class GdnFn(torch.autograd.Function):
         return dx, dbr, dgr, None, None, None
 
 
+class Gdn1OutFn(torch.autograd.Function):
+    """GDN1 (layers/gdn.py:111-121) after its |x| 1x1 conv: y = x * (1 / norm)  (inverse: x * norm)."""
+
+    @staticmethod
+    def forward(ctx, x, norm, inverse: bool):
+        _check_cuda(x, norm)
+        dt = compute_dtype()
+        B, C, H, W = x.shape
+        xp, xld = to_pm(x, dt, _vec(dt))
+        npm, nld = to_pm(norm, dt, _vec(dt))
+        y, yld = _out_pm_like(x, dt)
+        _ledger.run(lambda: lib.cai_gdn1_out(dcode(dt), _p(xp), xld, _p(npm), nld, _p(y), yld, B * H * W, C,
+                                             int(inverse), _stream()),
+                    "gdn1_out", "gdn1_out_kernel", 0, 3 * B * H * W * C * _es(dt), dt)
+        ctx.save_for_backward(xp, npm)
+        ctx.cfg = (dt, xld, nld, bool(inverse))
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        xp, npm = ctx.saved_tensors
+        dt, xld, nld, inverse = ctx.cfg
+        B, C, H, W = xp.shape
+        gp, gld = to_pm(g, dt, _vec(dt))
+        dx, dxld = _out_pm_like(xp, dt)
+        dn, dnld = _out_pm_like(xp, dt)
+        _ledger.run(lambda: lib.cai_gdn1_out_bwd(dcode(dt), _p(xp), xld, _p(npm), nld, _p(gp), gld, _p(dx), dxld,
+                                                 _p(dn), dnld, B * H * W, C, int(inverse), _stream()),
+                    "gdn1_out_bwd", "gdn1_out_bwd_kernel", 0, 5 * B * H * W * C * _es(dt), dt)
+        return dx, dn, None
+
+
 # ---------------------------------------------------------------------------
 # entropy models
 # ---------------------------------------------------------------------------

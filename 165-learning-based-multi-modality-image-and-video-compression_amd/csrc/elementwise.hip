@@ -8,6 +8,8 @@
 //   gate fwd     y = a * sigmoid(b) + x               AttentionBlock.forward, layers.py:236-243
 //   gate bwd     da = g * s(b), db = g * a * s(b)(1 - s(b))
 //   pixel shuffle / its inverse (torch.nn.PixelShuffle channel order c*r^2 + i*r + j)
+//   gdn1 out     y = x / norm  (inverse: x * norm)    GDN1.forward after its |x| 1x1 conv, gdn.py:111-121
+//   gdn1 bwd     dx = g / norm, dnorm = -g x / norm^2  (inverse: g norm, g x)
 #include "common.hpp"
 
 #include <algorithm>
@@ -140,6 +142,42 @@ __global__ void pixel_shuffle_kernel(const ShuffleArgs s) {
     }
 }
 
+// GDN1 (layers/gdn.py:95-121): norm = beta + gamma |x| comes from a 1x1 conv on |x|; this is the
+// remaining  out = x * (1 / norm)  (inverse: x * norm)  and its backward
+template <typename T>
+__global__ void gdn1_out_kernel(const T* __restrict__ x, int xld, const T* __restrict__ nrm, int nld,
+                                T* __restrict__ y, int yld, int npix, int C, int inverse) {
+    const int64_t total = (int64_t)npix * C;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int p = (int)(i / C), c = (int)(i - (int64_t)p * C);
+        const float xv = to_f32(x[(int64_t)p * xld + c]), nv = to_f32(nrm[(int64_t)p * nld + c]);
+        y[(int64_t)p * yld + c] = from_f32<T>(inverse ? xv * nv : xv * (1.f / nv));
+    }
+}
+
+template <typename T>
+__global__ void gdn1_out_bwd_kernel(const T* __restrict__ x, int xld, const T* __restrict__ nrm, int nld,
+                                    const T* __restrict__ g, int gld, T* __restrict__ dx, int dxld,
+                                    T* __restrict__ dn, int dnld, int npix, int C, int inverse) {
+    const int64_t total = (int64_t)npix * C;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int p = (int)(i / C), c = (int)(i - (int64_t)p * C);
+        const float xv = to_f32(x[(int64_t)p * xld + c]), nv = to_f32(nrm[(int64_t)p * nld + c]);
+        const float gv = to_f32(g[(int64_t)p * gld + c]);
+        float a, b;
+        if (inverse) {
+            a = gv * nv;
+            b = gv * xv;
+        } else {
+            const float r = 1.f / nv;
+            a = gv * r;
+            b = -gv * xv * r * r;
+        }
+        dx[(int64_t)p * dxld + c] = from_f32<T>(a);
+        dn[(int64_t)p * dnld + c] = from_f32<T>(b);
+    }
+}
+
 static int ew_grid2(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(16384, (n + 255) / 256)); }
 
 }  // namespace cai
@@ -218,6 +256,46 @@ int cai_gate_bwd(int dtype, const void* a, const void* b, const void* g, int32_t
         hipLaunchKernelGGL(gate_bwd_kernel<float>, dim3(ew_grid2(n)), dim3(256), 0, st, (const float*)a,
                            (const float*)b, (const float*)g, g_ld, (float*)da, (float*)db, ld, (int)npix, C);
     CAI_LAUNCH_CHECK("gate_bwd");
+    return CAI_OK;
+}
+
+int cai_gdn1_out(int dtype, const void* x, int32_t x_ld, const void* norm, int32_t n_ld, void* y, int32_t y_ld,
+                 int64_t npix, int32_t C, int32_t inverse, void* stream) {
+    CAI_CHECK_ARG(dtype == CAI_BF16 || dtype == CAI_F32, "gdn1_out: bad dtype");
+    CAI_CHECK_ARG(x && norm && y && x_ld >= C && n_ld >= C && y_ld >= C && npix < (1ll << 31),
+                  "gdn1_out: bad arguments");
+    const int64_t n = npix * C;
+    if (n == 0) return CAI_OK;
+    hipStream_t st = as_stream(stream);
+    if (dtype == CAI_BF16)
+        hipLaunchKernelGGL(gdn1_out_kernel<bf16>, dim3(ew_grid2(n)), dim3(256), 0, st, (const bf16*)x, x_ld,
+                           (const bf16*)norm, n_ld, (bf16*)y, y_ld, (int)npix, C, inverse);
+    else
+        hipLaunchKernelGGL(gdn1_out_kernel<float>, dim3(ew_grid2(n)), dim3(256), 0, st, (const float*)x, x_ld,
+                           (const float*)norm, n_ld, (float*)y, y_ld, (int)npix, C, inverse);
+    CAI_LAUNCH_CHECK("gdn1_out");
+    return CAI_OK;
+}
+
+int cai_gdn1_out_bwd(int dtype, const void* x, int32_t x_ld, const void* norm, int32_t n_ld, const void* g,
+                     int32_t g_ld, void* dx, int32_t dx_ld, void* dnorm, int32_t dn_ld, int64_t npix, int32_t C,
+                     int32_t inverse, void* stream) {
+    CAI_CHECK_ARG(dtype == CAI_BF16 || dtype == CAI_F32, "gdn1_out_bwd: bad dtype");
+    CAI_CHECK_ARG(x && norm && g && dx && dnorm && x_ld >= C && n_ld >= C && g_ld >= C && dx_ld >= C && dn_ld >= C &&
+                      npix < (1ll << 31),
+                  "gdn1_out_bwd: bad arguments");
+    const int64_t n = npix * C;
+    if (n == 0) return CAI_OK;
+    hipStream_t st = as_stream(stream);
+    if (dtype == CAI_BF16)
+        hipLaunchKernelGGL(gdn1_out_bwd_kernel<bf16>, dim3(ew_grid2(n)), dim3(256), 0, st, (const bf16*)x, x_ld,
+                           (const bf16*)norm, n_ld, (const bf16*)g, g_ld, (bf16*)dx, dx_ld, (bf16*)dnorm, dn_ld,
+                           (int)npix, C, inverse);
+    else
+        hipLaunchKernelGGL(gdn1_out_bwd_kernel<float>, dim3(ew_grid2(n)), dim3(256), 0, st, (const float*)x, x_ld,
+                           (const float*)norm, n_ld, (const float*)g, g_ld, (float*)dx, dx_ld, (float*)dnorm, dn_ld,
+                           (int)npix, C, inverse);
+    CAI_LAUNCH_CHECK("gdn1_out_bwd");
     return CAI_OK;
 }
 

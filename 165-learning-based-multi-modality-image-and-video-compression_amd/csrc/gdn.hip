@@ -193,7 +193,7 @@ __device__ __forceinline__ T* lds_elem(char* lds, int rs, int row, int col) {
 }
 
 template <typename T, int C>
-__global__ __launch_bounds__(GNT, sizeof(T) == 2 ? 2 : 1) void gdn_fwd_kernel(const T* __restrict__ x, int x_ld, int64_t npix,
+__global__ __launch_bounds__(GNT, (sizeof(T) == 2 && C <= 192) ? 2 : 1) void gdn_fwd_kernel(const T* __restrict__ x, int x_ld, int64_t npix,
                                                          const T* __restrict__ gamma, const float* __restrict__ beta,
                                                          int inverse, T* __restrict__ y, int y_ld) {
     using G = GdnGeo<T, C>;
@@ -714,28 +714,36 @@ static void launch_gdn_bwd(const void* x, int x_ld, const void* dy, int dy_ld, i
                        reinterpret_cast<const T*>(g), b, inv, reinterpret_cast<T*>(dx), dx_ld, reinterpret_cast<T*>(u));
 }
 
+// every channel count that is a multiple of 32 up to 256 (bf16) / 192 (fp32: three fp32 tiles of the
+// two-pass backward fill the LDS at 192); other counts are zero-padded by the caller (layers/gdn.py)
+#define GDN_CASE(FN, T, CC, ...) \
+    case CC: FN<T, CC>(__VA_ARGS__); break;
 #define GDN_DISPATCH(FN, ...)                                                  \
     do {                                                                       \
         if (dtype == CAI_BF16) {                                               \
             switch (C) {                                                       \
-                case 32: FN<bf16, 32>(__VA_ARGS__); break;                     \
-                case 64: FN<bf16, 64>(__VA_ARGS__); break;                     \
-                case 96: FN<bf16, 96>(__VA_ARGS__); break;                     \
-                case 128: FN<bf16, 128>(__VA_ARGS__); break;                   \
-                case 192: FN<bf16, 192>(__VA_ARGS__); break;                   \
+                GDN_CASE(FN, bf16, 32, __VA_ARGS__)                            \
+                GDN_CASE(FN, bf16, 64, __VA_ARGS__)                            \
+                GDN_CASE(FN, bf16, 96, __VA_ARGS__)                            \
+                GDN_CASE(FN, bf16, 128, __VA_ARGS__)                           \
+                GDN_CASE(FN, bf16, 160, __VA_ARGS__)                           \
+                GDN_CASE(FN, bf16, 192, __VA_ARGS__)                           \
+                GDN_CASE(FN, bf16, 224, __VA_ARGS__)                           \
+                GDN_CASE(FN, bf16, 256, __VA_ARGS__)                           \
             }                                                                  \
         } else {                                                               \
             switch (C) {                                                       \
-                case 32: FN<float, 32>(__VA_ARGS__); break;                    \
-                case 64: FN<float, 64>(__VA_ARGS__); break;                    \
-                case 96: FN<float, 96>(__VA_ARGS__); break;                    \
-                case 128: FN<float, 128>(__VA_ARGS__); break;                  \
-                case 192: FN<float, 192>(__VA_ARGS__); break;                  \
+                GDN_CASE(FN, float, 32, __VA_ARGS__)                           \
+                GDN_CASE(FN, float, 64, __VA_ARGS__)                           \
+                GDN_CASE(FN, float, 96, __VA_ARGS__)                           \
+                GDN_CASE(FN, float, 128, __VA_ARGS__)                          \
+                GDN_CASE(FN, float, 160, __VA_ARGS__)                          \
+                GDN_CASE(FN, float, 192, __VA_ARGS__)                          \
             }                                                                  \
         }                                                                      \
     } while (0)
 
-static bool gdn_c_ok(int C) { return C == 32 || C == 64 || C == 96 || C == 128 || C == 192; }
+static bool gdn_c_ok(int C, int dtype) { return C % 32 == 0 && C >= 32 && C <= (dtype == CAI_BF16 ? 256 : 192); }
 
 }  // namespace cai
 
@@ -757,7 +765,7 @@ int cai_gdn_reparam(const float* beta_raw, const float* gamma_raw, int32_t C, fl
 
 int cai_gdn_fwd(int dtype, const void* x, int32_t x_ld, int64_t npix, int32_t C, const void* gamma_op,
                 const float* beta, int32_t inverse, void* y, int32_t y_ld, void* stream) {
-    CAI_CHECK_ARG(gdn_c_ok(C), "gdn_fwd: unsupported channel count %d", C);
+    CAI_CHECK_ARG(gdn_c_ok(C, dtype), "gdn_fwd: unsupported channel count %d", C);
     CAI_CHECK_ARG(x && gamma_op && beta && y && x_ld >= C && y_ld >= C, "gdn_fwd: bad arguments");
     CAI_CHECK_ARG(x_ld % 8 == 0 && y_ld % 8 == 0, "gdn_fwd: ld must be a multiple of 8");
     if (npix == 0) return CAI_OK;
@@ -769,7 +777,7 @@ int cai_gdn_fwd(int dtype, const void* x, int32_t x_ld, int64_t npix, int32_t C,
 int cai_gdn_bwd(int dtype, const void* x, int32_t x_ld, const void* dy, int32_t dy_ld, int64_t npix, int32_t C,
                 const void* gamma_op, const float* beta, int32_t inverse, void* dx, int32_t dx_ld, void* u,
                 void* stream) {
-    CAI_CHECK_ARG(gdn_c_ok(C), "gdn_bwd: unsupported channel count %d", C);
+    CAI_CHECK_ARG(gdn_c_ok(C, dtype), "gdn_bwd: unsupported channel count %d", C);
     CAI_CHECK_ARG(x && dy && gamma_op && beta && dx && u, "gdn_bwd: bad arguments");
     CAI_CHECK_ARG(x_ld % 8 == 0 && dy_ld % 8 == 0 && dx_ld % 8 == 0 && x_ld >= C && dy_ld >= C && dx_ld >= C,
                   "gdn_bwd: bad leading dimensions");
@@ -823,7 +831,7 @@ int cai_gdn_param_grad(int dtype, const void* x, int32_t x_ld, const void* u, in
 static bool fused_ok(int dtype, int C) { return dtype == CAI_BF16 && (C == 64 || C == 128); }
 
 size_t cai_gdn_backward_workspace_bytes(int64_t npix, int32_t C, int dtype) {
-    if (npix <= 0 || !gdn_c_ok(C)) return 0;
+    if (npix <= 0 || !gdn_c_ok(C, dtype)) return 0;
     if (fused_ok(dtype, C)) return (size_t)fused_blocks(npix) * ((size_t)C * C + C) * sizeof(float);
     const size_t ub = ((size_t)npix * C * dtype_size(dtype) + 255) / 256 * 256;
     return ub + cai_gdn_param_grad_workspace_bytes(npix, C, dtype);
@@ -834,7 +842,7 @@ int cai_gdn_backward(int dtype, const void* x, int32_t x_ld, const void* dy, int
                      const float* beta_raw, const float* gamma_raw, float beta_min, float reparam_offset,
                      float* dbeta_raw, float* dgamma_raw, int32_t accumulate, void* workspace, size_t ws_bytes,
                      void* stream) {
-    CAI_CHECK_ARG(gdn_c_ok(C), "gdn_backward: unsupported channel count %d", C);
+    CAI_CHECK_ARG(gdn_c_ok(C, dtype), "gdn_backward: unsupported channel count %d", C);
     CAI_CHECK_ARG(x && dy && gamma_op && beta && dx && beta_raw && gamma_raw && dbeta_raw && dgamma_raw,
                   "gdn_backward: null pointer");
     CAI_CHECK_ARG(x_ld % 8 == 0 && dy_ld % 8 == 0 && dx_ld % 8 == 0 && x_ld >= C && dy_ld >= C && dx_ld >= C,

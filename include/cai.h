@@ -222,6 +222,13 @@ int cai_act(int dtype, const void* x, int32_t x_ld, void* y, int32_t y_ld, int64
             float act_param, void* stream);
 /* AttentionBlock gate (layers.py:238-243): y = a * sigmoid(b) + x;
  * backward da = g * s(b), db = g * a * s(b) * (1 - s(b)) (dx = g). */
+/* GDN1 (layers/gdn.py:95-121): y = x / norm (inverse: x * norm), norm from a 1x1 conv of |x|
+ * (cai_conv_fwd with in_abs); backward dx = g / norm, dnorm = -g x / norm^2 (inverse: g norm, g x). */
+int cai_gdn1_out(int dtype, const void* x, int32_t x_ld, const void* norm, int32_t n_ld, void* y, int32_t y_ld,
+                 int64_t npix, int32_t C, int32_t inverse, void* stream);
+int cai_gdn1_out_bwd(int dtype, const void* x, int32_t x_ld, const void* norm, int32_t n_ld, const void* g,
+                     int32_t g_ld, void* dx, int32_t dx_ld, void* dnorm, int32_t dn_ld, int64_t npix, int32_t C,
+                     int32_t inverse, void* stream);
 int cai_gate_fwd(int dtype, const void* a, const void* b, const void* x, void* y, int32_t ld, int64_t npix, int32_t C,
                  void* stream);
 int cai_gate_bwd(int dtype, const void* a, const void* b, const void* g, int32_t g_ld, void* da, void* db, int32_t ld,
@@ -285,7 +292,8 @@ int cai_channel_affine(int dtype, const void* x, int32_t x_ld, const float* gamm
                        void* y, int32_t y_ld, int32_t B, int64_t HW, int32_t C, void* stream);
 
 /* =======================================================================
- * GDN / IGDN (layers/gdn.py:41-92), C in {32,64,96,128,192}.
+ * GDN / IGDN (layers/gdn.py:41-92), C a multiple of 32 up to 256 (bf16) / 192 (fp32);
+ * layers/gdn.py zero-pads other channel counts.
  * ======================================================================= */
 /* beta = max(beta_raw, sqrt(beta_min + ped))^2 - ped ; gamma likewise with
  * bound sqrt(ped); gamma_op is written in the operand dtype in both the
