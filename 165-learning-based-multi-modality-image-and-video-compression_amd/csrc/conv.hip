@@ -25,6 +25,8 @@
 // reduce: deterministic).  Both operands arrive [pixel][channel]; bf16 MFMA
 // fragments are read with ds_read_b64_tr_b16 (hardware transpose).
 #include "common.hpp"
+
+#include <type_traits>
 #include "edge_frag.hpp"
 #include "mfma.hpp"
 
@@ -1658,6 +1660,257 @@ __global__ __launch_bounds__(512, 1) void wgrad_glds_kernel(const WgradArgs a) {
         }
 }
 
+// ---------------------------------------------------------------------------
+// Halo-staged weight gradient of the stride-2 gather convolutions (Conv2d k3/k5 s2 p=k/2, and the
+// ConvTranspose2d of that geometry, whose wgrad gathers its output gradient the same way), bf16, for
+// G maps whose width is a multiple of 64.  wgrad_glds_kernel gathers the X operand per (pixel, tap)
+// column: for a 256-column tile (two taps) every step pulls 32 KB of X plus 16 KB of G through LDS, and
+// the kernel runs at the rate L2 / MALL deliver those bytes (45 % of wave time parked on the DMA waits,
+// profiles/r02_*).  Here a block owns one KERNEL ROW kh, all KS taps of it and 64 channels (KS*64
+// columns), and a K-step is one 64-pixel strip of a G row: the strip's whole X footprint for that kernel
+// row -- input row 2j-p+kh, x offsets 0 .. 2*63+KS-1 from 2*i0-p, 64 channels -- is ONE LDS image of
+// 2*63+KS cells (16.8 KB for k5) that all KS taps read at a per-tap offset.  Bytes per step drop to
+// 33 KB for 1.25x the MFMA work, so a 4-stage ring (3 strips in flight) fits in LDS.
+//
+// Footprint layout: x offset t -> plane t&1 (even offsets first, then odd), cell t>>1, so tap kw reads
+// pixel p at cell p + kw/2 of plane kw&1: 16 consecutive pixels = 16 consecutive cells.  A cell is 64
+// channels (128 B = four 32-B groups of 16 channels); the group of a 16-channel block is XOR-swizzled
+// by h(cell) = bit1 | bit3<<1 of the cell index, which puts the 8 cells a half-wave's
+// ds_read_b64_tr_b16 touches (p..p+3, p+8..p+11) on 8 distinct 32-B bank groups.  The DMA writes LDS
+// lane-linearly, so the swizzle is applied to the per-lane SOURCE slot (both-sides rule).
+// Partials leave through the same [split][Ng][ncols] slab as wgrad_glds_kernel (same reduce).
+// ---------------------------------------------------------------------------
+template <int KS>
+struct WhCfg {
+    static constexpr int NCELL = 2 * 63 + KS;         // footprint cells of one 64-pixel strip
+    static constexpr int NE = (NCELL + 1) / 2;        // even-offset plane
+    static constexpr int XSLOTS = NCELL * 8;          // 16-byte pieces of the footprint
+    static constexpr int XGRP = (XSLOTS + 63) / 64;   // wave-instructions that fill it
+    static constexpr int NXI = (XGRP + 7) / 8;        // per thread (8 waves); spare instructions hit a sink
+    static constexpr int NST = 4;                     // ring stages (3 strips in flight)
+    static constexpr int GIMG = 64 * 256;             // G strip [64 px][128 ch]; the 4 G images first ...
+    static constexpr int XBASE = NST * GIMG;          // ... then the 4 footprints: every stage offset < 64 KB
+    static constexpr int XSTRIDE = XGRP * 1024 + 1024;   // footprint + a 1 KB sink for the spare DMAs
+    static constexpr int BYTES = XBASE + NST * XSTRIDE;
+    static constexpr int NLOAD = 2 + NXI;             // DMA instructions per thread per step
+    static constexpr int CT = KS * 64;                // tile columns
+    static constexpr int WCOL = CT / 4;               // columns per column-wave
+    static constexpr int TN = WCOL / 16;
+};
+
+__device__ __forceinline__ int wh_h(int cell) { return ((cell >> 1) & 1) | (((cell >> 3) & 1) << 1); }
+
+// keep a per-lane value opaque to the optimiser: it stays one materialised VGPR instead of being
+// re-derived from its parts at every use
+__device__ __forceinline__ int opaque(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+template <int KS, int FLAGS>
+__global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
+    using W = WhCfg<KS>;
+    __shared__ __attribute__((aligned(16))) char smem[W::BYTES];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wr = wid >> 2, wc = wid & 3;            // 2 (rows) x 4 (cols) waves
+    const int nqc = a.Cq_pad / 64;
+    const int ntile = KS * nqc * a.rtiles;
+    const int L = xcd_remap((int)blockIdx.x, (int)gridDim.x);
+    const int split = L / ntile;
+    const int tl = L - split * ntile;
+    const int ctile = tl % (KS * nqc), rtile = tl / (KS * nqc);
+    const int kh = ctile / nqc, q0 = (ctile - kh * nqc) * 64, r0 = rtile * 128;
+    const int nsr = a.Wg / 64;                        // strips per G row
+    const int nstrip = a.B * a.Hg * nsr;
+    const int sbeg = min(nstrip, split * a.nsplit), send = min(nstrip, sbeg + a.nsplit);   // a.nsplit: strips per split
+    const int nsteps = send - sbeg;
+    float* out = a.ws + (int64_t)split * a.Ng * a.ncols;
+
+    // G DMA: rows prow0 + 32 i of the strip, source slot sl (the tr-read swizzle of that row)
+    const int prow0 = wid * 4 + (lane >> 4);
+    const int sl = (lane & 15) ^ ((((lane >> 4) & 3) << 1) | (((wid >> 1) & 1) << 3));
+    const char* Gp = reinterpret_cast<const char*>(a.g);
+    const char* Xp = reinterpret_cast<const char*>(a.x);
+    const int gch = r0 + sl * 8;
+    const bool gvalid = gch < a.Ng;
+    // X DMA: this lane's footprint piece of each instruction (x offset t, channel byte offset), or the sink
+    int xt[W::NXI];
+    bool xin[W::NXI];
+    int64_t xlane[W::NXI];                            // byte offset of the piece inside a strip's footprint row
+    const int64_t xpix = (int64_t)a.x_ld * 2;         // bytes per X pixel
+#pragma unroll
+    for (int n = 0; n < W::NXI; ++n) {
+        const int grp = n * 8 + wid;
+        const int Ls = grp * 64 + lane;
+        xin[n] = grp < W::XGRP && Ls < W::XSLOTS;
+        const int pc = xin[n] ? Ls >> 3 : 0, ps = Ls & 7;
+        xt[n] = pc < W::NE ? 2 * pc : 2 * (pc - W::NE) + 1;
+        const int ls = (((ps >> 1) ^ wh_h(pc)) << 1) | (ps & 1);
+        xlane[n] = xt[n] * xpix + (q0 + ls * 8) * 2;
+    }
+    // strip coordinates (column block, row, image) of the next strip to issue: strips are issued in order,
+    // so they advance by carries instead of integer divisions per step
+    int cib = sbeg % nsr, cj = (sbeg / nsr) % a.Hg, cb = (sbeg / nsr) / a.Hg;
+    const char* gsrc = Gp + ((int64_t)(sbeg * 64 + prow0) * a.g_ld + gch) * 2;   // strips are 64 G pixels
+    const int64_t gstep = (int64_t)64 * a.g_ld * 2, ghalf = (int64_t)32 * a.g_ld * 2;
+
+    auto issue = [&](int stage) {
+        char* gb = smem + stage * W::GIMG;
+        char* xb = smem + W::XBASE + stage * W::XSTRIDE;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            glds16(gvalid ? (const void*)(gsrc + i * ghalf) : (const void*)cai_zero_page,
+                   gb + wid * 4 * 256 + i * 32 * 256);
+        gsrc += gstep;
+        const int y = cj * 2 - a.p + kh;
+        const int x0 = cib * 128 - a.p;
+        const bool yok = (unsigned)y < (unsigned)a.Hx;
+        const char* xrow = Xp + (((int64_t)cb * a.Hx + (yok ? y : 0)) * a.Wx + x0) * xpix;
+#pragma unroll
+        for (int n = 0; n < W::NXI; ++n) {
+            const int grp = n * 8 + wid;
+            const bool ok = xin[n] && yok && (unsigned)(x0 + xt[n]) < (unsigned)a.Wx;
+            glds16(ok ? (const void*)(xrow + xlane[n]) : (const void*)cai_zero_page,
+                   xb + (grp < W::XGRP ? grp * 1024 : W::XGRP * 1024));
+        }
+        if (++cib == nsr) {
+            cib = 0;
+            if (++cj == a.Hg) {
+                cj = 0;
+                ++cb;
+            }
+        }
+    };
+
+    f32x4 acc[4][W::TN];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < W::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int g_ = lane >> 4, i16 = lane & 15, q_ = i16 >> 2, p4 = i16 & 3;
+    const bool do_bias = (FLAGS & WG_BIAS) && ctile == 0;
+    float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+    const int wcol = wc * W::WCOL;
+    // LDS byte offsets of every fragment read, fixed for the launch (stage 0; the other stages add a
+    // compile-time immediate): B (footprint) per (ks, column block, pixel half) -- the tap's plane / cell
+    // shift and the block's swizzled 32-B group -- and A (G strip)
+    int boff[2][W::TN][2], aoff[2][4][2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+        const int rr = 32 * ks + 8 * g_ + q_;
+#pragma unroll
+        for (int tn = 0; tn < W::TN; ++tn) {
+            const int col = wcol + tn * 16, kw = col / 64, cg = (col % 64) / 16;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int c = (kw & 1) * W::NE + (kw >> 1) + rr + 4 * h;
+                boff[ks][tn][h] = opaque(W::XBASE + c * 128 + (((cg ^ wh_h(c)) << 1) | (p4 >> 1)) * 16 + (p4 & 1) * 8);
+            }
+        }
+#pragma unroll
+        for (int tm = 0; tm < 4; ++tm) {
+            const int colA = wr * 64 + tm * 16 + 4 * p4;
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                aoff[ks][tm][h] = opaque(trswz(rr + 4 * h, colA >> 3) + ((colA & 7) << 1));
+        }
+    }
+
+    auto step = [&](auto ustage) {
+        constexpr int U = decltype(ustage)::value;
+        const char* Gs = smem + U * W::GIMG;
+        const char* Xs = smem + U * W::XSTRIDE;      // boff carries XBASE
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            u32x4 fb[W::TN];
+#pragma unroll
+            for (int t = 0; t < W::TN; ++t) {
+                s16x4 b0 = ds_tr16(Xs, boff[ks][t][0]);
+                s16x4 b1 = ds_tr16(Xs, boff[ks][t][1]);
+                s16x8 bv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+                fb[t] = __builtin_bit_cast(u32x4, bv);
+            }
+#pragma unroll
+            for (int tm = 0; tm < 4; ++tm) {
+                s16x4 a0 = ds_tr16(Gs, aoff[ks][tm][0]);
+                s16x4 a1 = ds_tr16(Gs, aoff[ks][tm][1]);
+                s16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+                const u32x4 fa = __builtin_bit_cast(u32x4, av);
+                if constexpr ((FLAGS & WG_BIAS) != 0) {
+                    if (do_bias && tm == wc) {
+                        const bf16x8 h = __builtin_bit_cast(bf16x8, fa);
+                        float sacc = 0.f;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) sacc += (float)h[e];
+                        bsum[tm] += sacc;
+                    }
+                }
+#pragma unroll
+                for (int tn = 0; tn < W::TN; ++tn) acc[tm][tn] = mma16<bf16>(fa, fb[tn], acc[tm][tn]);
+            }
+        }
+    };
+
+#pragma unroll
+    for (int s = 0; s < W::NST - 1; ++s)
+        if (s < nsteps) issue(s);
+    // the ring position is a compile-time constant: the loop runs NST strips per trip
+    for (int st0 = 0; st0 < nsteps; st0 += W::NST) {
+        auto one = [&](auto ustage) {
+            constexpr int U = decltype(ustage)::value;
+            const int st = st0 + U;
+            if (st >= nsteps) return;
+            const int ahead = min(W::NST - 2, nsteps - 1 - st);   // later strips already issued
+            if (ahead >= 2)
+                wait_vmcnt<2 * W::NLOAD>();
+            else if (ahead == 1)
+                wait_vmcnt<W::NLOAD>();
+            else
+                wait_vmcnt<0>();
+            wait_lgkmcnt0();
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            if (st + W::NST - 1 < nsteps) issue((U + W::NST - 1) % W::NST);
+            step(ustage);
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        one(std::integral_constant<int, 0>());
+        one(std::integral_constant<int, 1>());
+        one(std::integral_constant<int, 2>());
+        one(std::integral_constant<int, 3>());
+    }
+    if constexpr ((FLAGS & WG_BIAS) != 0) {
+        if (do_bias) {
+            float v = bsum[0] + bsum[1] + bsum[2] + bsum[3];
+            v += __shfl_xor(v, 16);
+            v += __shfl_xor(v, 32);
+            const int n = r0 + wr * 64 + wc * 16 + lane;
+            if (lane < 16 && n < a.Ng) a.bws[(int64_t)split * a.Ng + n] = v;
+        }
+    }
+#pragma unroll
+    for (int tn = 0; tn < W::TN; ++tn) {
+        const int col = wcol + tn * 16 + (lane & 15), kw = col / 64;
+        const int gcol = (kh * KS + kw) * a.Cq_pad + q0 + col % 64;
+#pragma unroll
+        for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = r0 + wr * 64 + tm * 16 + (lane >> 4) * 4 + r;
+                if (row < a.Ng) out[(int64_t)row * a.ncols + gcol] = acc[tm][tn][r];
+            }
+    }
+}
+
+template <int KS>
+static void launch_wgrad_halo(const WgradArgs& a, int nblocks, bool bias, hipStream_t st) {
+    if (bias)
+        hipLaunchKernelGGL((wgrad_halo_kernel<KS, WG_BIAS>), dim3(nblocks), dim3(512), 0, st, a);
+    else
+        hipLaunchKernelGGL((wgrad_halo_kernel<KS, 0>), dim3(nblocks), dim3(512), 0, st, a);
+}
+
 template <int CT>
 static void launch_wgrad_glds(const WgradArgs& a, int nblocks, int in_abs, int in_sq, bool bias, hipStream_t st) {
     const int f = (in_abs ? WG_ABS : 0) | (in_sq ? WG_SQ : 0) | (bias ? WG_BIAS : 0);
@@ -2148,6 +2401,8 @@ static int run_conv(const cai_conv_geom* g, int dtype, int direction, const void
 }
 
 struct WgradPlan {
+    int halo;        // kernel size of the halo-staged kernel (0: not taken); S then counts strip ranges
+    int strips_per_split;
     bool glds, fused_bias;
     int ct;
     size_t ws_bias;
@@ -2159,11 +2414,26 @@ struct WgradPlan {
     size_t ws_slab, ws_col;
 };
 
+// the halo-staged wgrad: stride-2 gather geometry with k in {3, 5}, pad k/2, G width a multiple of 64,
+// 64-channel X chunks (G channels beyond 128 take more row tiles)
+static bool halo_wgrad_off() {
+    static const bool off = [] {
+        const char* e = getenv("CAI_HALO_WGRAD_OFF");
+        return e && *e && *e != '0';
+    }();
+    return off;
+}
+static bool halo_wgrad_ks(const cai_conv_geom* g, const WgradPlan& W) {
+    const int Wg = g->transposed ? g->in_w : g->out_w;
+    return !halo_wgrad_off() && g->stride == 2 && (g->kernel == 3 || g->kernel == 5) && g->pad == g->kernel / 2 &&
+           Wg % 64 == 0 && W.Cq_pad % 64 == 0;
+}
+
 static int colsum_nchunk(int64_t npix) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(1024, (npix + 255) / 256));
 }
 
-static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype, bool glds) {
+static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype, bool glds, bool in_tf = false) {
     WgradPlan W{};
     W.glds = glds && dtype == CAI_BF16;
     const int VEC = dtype == CAI_BF16 ? 8 : 4;
@@ -2196,6 +2466,17 @@ static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype, bool glds) {
         S = (int)std::max<int64_t>(1, std::min<int64_t>(S, W.M / 256));
         W.split_len = ((W.M + S - 1) / S + 63) / 64 * 64;
         W.S = (int)((W.M + W.split_len - 1) / W.split_len);
+    }
+    if (W.glds && !in_tf && halo_wgrad_ks(g, W)) {
+        W.halo = g->kernel;
+        const int Wg = g->transposed ? g->in_w : g->out_w;
+        const int Hg = g->transposed ? g->in_h : g->out_h;
+        const int64_t nstrip = (int64_t)g->batch * Hg * (Wg / 64);
+        W.tiles = W.halo * (W.Cq_pad / 64) * ((W.Ng + 127) / 128);
+        int S = std::max(1, 256 / W.tiles);
+        S = (int)std::max<int64_t>(1, std::min<int64_t>(S, nstrip / 4));   // >= 4 strips per split
+        W.strips_per_split = (int)((nstrip + S - 1) / S);
+        W.S = (int)((nstrip + W.strips_per_split - 1) / W.strips_per_split);
     }
     W.ws_slab = (size_t)W.S * W.Ng * W.ncols * sizeof(float);
     W.fused_bias = W.glds && !g->transposed;
@@ -2382,8 +2663,9 @@ int cai_conv_dgrad(const cai_conv_geom* g, int dtype, const void* dy, int32_t dy
 const char* cai_conv_kernel_name(const cai_conv_geom* g, int dtype, int direction, int32_t in_abs) {
     if (check_geom(g) || (dtype != CAI_BF16 && dtype != CAI_F32) || direction < 0 || direction > 2) return "";
     if (direction == 2) {
-        const WgradPlan W = make_wgrad_plan(g, dtype, true);
+        const WgradPlan W = make_wgrad_plan(g, dtype, true, in_abs != 0);
         if (!W.glds) return dtype == CAI_BF16 ? "wgrad_kernel<bf16>" : "wgrad_kernel<float>";
+        if (W.halo) return W.halo == 5 ? "wgrad_halo_kernel<5>" : "wgrad_halo_kernel<3>";
         return W.ct == 256 ? "wgrad_glds_kernel<256>" : "wgrad_glds_kernel<128>";
     }
     const ConvLaunch L = conv_launch(g, dtype, direction, in_abs);
@@ -2403,14 +2685,17 @@ const char* cai_conv_kernel_name(const cai_conv_geom* g, int dtype, int directio
 
 int32_t cai_conv_split_factor(const cai_conv_geom* g, int dtype, int direction, int32_t in_abs) {
     if (check_geom(g) || (dtype != CAI_BF16 && dtype != CAI_F32) || direction < 0 || direction > 2) return 0;
-    if (direction == 2) return make_wgrad_plan(g, dtype, true).S;
+    if (direction == 2) return make_wgrad_plan(g, dtype, true, in_abs != 0).S;
     return conv_launch(g, dtype, direction, in_abs).ksplit;
 }
 
 size_t cai_conv_wgrad_workspace_bytes(const cai_conv_geom* g, int dtype) {
     if (check_geom(g)) return 0;
-    const WgradPlan W0 = make_wgrad_plan(g, dtype, false), W1 = make_wgrad_plan(g, dtype, true);
-    return std::max(W0.ws_slab + W0.ws_col, W1.ws_slab + W1.ws_bias + W1.ws_col) + 256;
+    // the plan depends on whether the input is transformed (|x|, x^2): cover every variant
+    const WgradPlan W0 = make_wgrad_plan(g, dtype, false), W1 = make_wgrad_plan(g, dtype, true),
+                    W2 = make_wgrad_plan(g, dtype, true, true);
+    return std::max({W0.ws_slab + W0.ws_col, W1.ws_slab + W1.ws_bias + W1.ws_col,
+                     W2.ws_slab + W2.ws_bias + W2.ws_col}) + 256;
 }
 
 int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_ld, int32_t in_abs, int32_t in_sq,
@@ -2419,7 +2704,7 @@ int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_l
     int rc = check_geom(g);
     if (rc) return rc;
     CAI_CHECK_ARG(x && dy && dw, "conv_wgrad: null pointer");
-    const WgradPlan W = make_wgrad_plan(g, dtype, true);
+    const WgradPlan W = make_wgrad_plan(g, dtype, true, in_abs || in_sq);
     CAI_CHECK_ARG(workspace && ws_bytes >= W.ws_slab + W.ws_bias + W.ws_col + 256, "conv_wgrad: workspace too small");
     const int VEC = dtype == CAI_BF16 ? 8 : 4;
     WgradArgs a{};
@@ -2456,7 +2741,14 @@ int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_l
         a.nsplit = W.S;
         if (W.fused_bias && db) bws = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + W.ws_slab);
         a.bws = bws;
-        if (W.ct == 256)
+        if (W.halo) {
+            a.nsplit = W.strips_per_split;
+            a.rtiles = (W.Ng + 127) / 128;
+            if (W.halo == 5)
+                launch_wgrad_halo<5>(a, W.S * W.tiles, bws != nullptr, st);
+            else
+                launch_wgrad_halo<3>(a, W.S * W.tiles, bws != nullptr, st);
+        } else if (W.ct == 256)
             launch_wgrad_glds<256>(a, W.S * W.tiles, in_abs, in_sq, bws != nullptr, st);
         else
             launch_wgrad_glds<128>(a, W.S * W.tiles, in_abs, in_sq, bws != nullptr, st);

@@ -358,9 +358,13 @@ __global__ __launch_bounds__(GNT, 1) void gdn_bwd_kernel(const T* __restrict__ x
 // ---------------------------------------------------------------------------
 constexpr int FNT = 512;   // 8 waves
 
+#ifndef CAI_GDN_RS_PAD
+#define CAI_GDN_RS_PAD 32       // bytes of padding per LDS row of the fused backward's tiles (A/B: 16 / 32 / 48 / 80 -> 32 best, -2 %)
+#endif
+
 template <int C>
 struct FusedGeo {
-    static constexpr int RS = 2 * C + 16;           // padded LDS row (bf16)
+    static constexpr int RS = 2 * C + CAI_GDN_RS_PAD;   // padded LDS row (bf16)
     static constexpr int KB = C / 32;               // 32-deep K blocks over channels
     static constexpr int NB = C / 16;               // 16-channel blocks
     static constexpr int WN = NB < 8 ? NB : 8;      // waves across channels (pixel GEMMs)

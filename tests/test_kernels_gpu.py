@@ -69,6 +69,12 @@ CONV_CASES = [
     ("deconv", 2, 192, 128, 16, 40, 5, 2),
     ("deconv", 2, 64, 64, 20, 36, 5, 2),
     ("conv", 2, 96, 192, 48, 64, 5, 2),
+    # halo-staged weight gradient (G width a multiple of 64): split strips, 192 G channels (two row tiles),
+    # k3 transposed, 64-channel X chunks
+    ("conv", 2, 128, 128, 64, 128, 5, 2),
+    ("conv", 1, 64, 192, 20, 128, 5, 2),
+    ("deconv", 1, 64, 128, 6, 64, 3, 2),
+    ("deconv", 2, 128, 64, 5, 64, 5, 2),
     # Spatial_aligner patch embedding / recovery (master.py:708-724): kernel = stride = 2, no padding
     ("conv", 2, 64, 96, 32, 24, 2, 2, 0, 0),
     ("conv", 2, 3, 96, 16, 16, 2, 2, 0, 0),
@@ -543,6 +549,11 @@ def test_halo_conv_full(cuda, B):
     ref.backward(gy.bfloat16().float())
     assert relerr(y, ref) < 1e-2
     assert relerr(x.grad, xr.grad) < 1e-2
+    wr = mod.weight.detach().bfloat16().float().requires_grad_()
+    br = mod.bias.detach().clone().requires_grad_()
+    F.conv2d(x.detach().bfloat16().float(), wr, br, stride=2, padding=2).backward(gy.bfloat16().float())
+    assert relerr(mod.weight.grad, wr.grad) < 1e-2      # wgrad_halo_kernel<5> (G width 64)
+    assert relerr(mod.bias.grad, br.grad) < 1e-2
 
     dec = ConvTranspose2d(128, 128, 5, stride=2, padding=2, output_padding=1).to(cuda)
     xs = torch.randn(B, 128, 64, 64, device=cuda).requires_grad_()
@@ -556,6 +567,12 @@ def test_halo_conv_full(cuda, B):
     yr.backward(g.bfloat16().float())
     assert relerr(ys, yr) < 1e-2
     assert relerr(xs.grad, xr.grad) < 1e-2
+    wr = dec.weight.detach().bfloat16().float().requires_grad_()
+    br = dec.bias.detach().clone().requires_grad_()
+    F.conv_transpose2d(xs.detach().bfloat16().float(), wr, br, stride=2, padding=2,
+                       output_padding=1).backward(g.bfloat16().float())
+    assert relerr(dec.weight.grad, wr.grad) < 1e-2
+    assert relerr(dec.bias.grad, br.grad) < 1e-2
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
