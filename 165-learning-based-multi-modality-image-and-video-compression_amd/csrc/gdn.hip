@@ -614,6 +614,192 @@ __global__ __launch_bounds__(FNT, 1) void gdn_bwd_fused_kernel(const bf16* __res
         }
 }
 
+// ---------------------------------------------------------------------------
+// Fused backward for wide layers (bf16, C = 160 / 192: the q6-8 hyperpriors, mbt2018, cheng2020 at N=192).
+// The C <= 128 kernel above holds gamma AND gamma^T fragments plus its dgamma tile in registers; at
+// C = 192 that no longer fits (the dgamma partial alone is 144 16x16 tiles).  Here one wave owns 16
+// channels (C / 16 waves: 12 at C = 192), gamma^T lives in LDS (C x C bf16, row reads for the dx GEMM),
+// gamma fragments of the wave's 16 rows stay in registers (norm GEMM), tiles are 32 pixels, and
+// each wave accumulates one 16-column block of dgamma (C / 16 tiles).  Per tile:
+//   norm = x^2 gamma^T + beta (MFMA)  ->  u, t1 (fp32)  ->  dgamma += u^T x^2 (MFMA, pixels as K,
+//   ds_read_b64_tr_b16)  ->  dx = t1 + 2 x (u gamma) (MFMA, gamma^T rows from LDS)
+// HBM traffic per pixel: read x, dy, write dx (6C B) -- the two-pass path moves 12C B.
+// ---------------------------------------------------------------------------
+template <int C>
+struct WideGeo {
+    static constexpr int NW = C / 16;                 // waves = 16-channel blocks
+    static constexpr int NT = NW * 64;
+    static constexpr int GB = 32;                     // pixels per tile
+    static constexpr int RS = 2 * C + 16;             // LDS row stride (bytes): 16 rows x 16 B conflict-free
+    static constexpr int KB = C / 32;                 // 32-deep K blocks over channels
+    static constexpr int TM = GB / 16;
+    static constexpr int CPT = GB * (2 * C / 16) / NT;   // 16-byte chunks per thread per tile (= 1)
+    static constexpr int TILE = GB * RS;
+    static constexpr int GT = C * RS;                 // gamma^T image
+    static constexpr int BYTES = GT + 4 * TILE;
+    static_assert(C % 32 == 0 && NW <= 16 && CPT >= 1 && GB * (2 * C / 16) % NT == 0, "unsupported C");
+};
+
+template <int C, bool INV>
+__global__ __launch_bounds__(WideGeo<C>::NT, 1) void gdn_bwd_wide_kernel(const bf16* __restrict__ x, int x_ld,
+                                                                        const bf16* __restrict__ dy, int dy_ld,
+                                                                        int64_t npix, const bf16* __restrict__ gamma_op,
+                                                                        const float* __restrict__ beta,
+                                                                        bf16* __restrict__ dx, int dx_ld,
+                                                                        float* __restrict__ part) {
+    using G = WideGeo<C>;
+    __shared__ __attribute__((aligned(16))) char lds[G::BYTES];
+    char* Lt = lds;                       // gamma^T [C][C]
+    char* Lx = lds + G::GT;
+    char* Lg = Lx + G::TILE;
+    char* Lu = Lg + G::TILE;
+    char* Lq = Lu + G::TILE;              // x^2
+    constexpr int CHR = 2 * C / 16;       // 16-byte chunks per pixel row
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int n0 = wave * 16;
+    const int g_ = lane >> 4, i16 = lane & 15, q_ = i16 >> 2, p4 = i16 & 3;
+    const bf16* gammaT = gamma_op + (int64_t)C * C;
+
+    // gamma^T into LDS (row j = column j of gamma), gamma fragments of this wave's rows into registers
+    for (int id = threadIdx.x; id < C * CHR; id += G::NT) {
+        const int r = id / CHR, ch = id - r * CHR;
+        *reinterpret_cast<u32x4*>(Lt + r * G::RS + ch * 16) =
+            *reinterpret_cast<const u32x4*>(gammaT + (int64_t)r * C + ch * 8);
+    }
+    u32x4 fb[G::KB];
+#pragma unroll
+    for (int kb = 0; kb < G::KB; ++kb)
+        fb[kb] = *reinterpret_cast<const u32x4*>(gamma_op + (int64_t)(n0 + i16) * C + kb * 32 + 8 * g_);
+    const float bv = beta[n0 + i16];
+    f32x4 dg[G::NW];
+#pragma unroll
+    for (int t = 0; t < G::NW; ++t) dg[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float dbeta = 0.f;
+
+    // one tile in flight: the next tile's x / dy chunk (one 16-byte chunk per thread each) loads while
+    // this tile is computed
+    const int64_t ntiles = (npix + G::GB - 1) / G::GB;
+    const int crow = threadIdx.x / CHR, cch = threadIdx.x - (threadIdx.x / CHR) * CHR;
+    auto load = [&](int64_t t, u32x4& rx, u32x4& rg) {
+        const int64_t p = min(t * G::GB + crow, npix - 1);   // clamped: every load is issued
+        rx = *reinterpret_cast<const u32x4*>(x + p * x_ld + cch * 8);
+        rg = *reinterpret_cast<const u32x4*>(dy + p * dy_ld + cch * 8);
+    };
+    u32x4 rx, rg;
+    int64_t tile = blockIdx.x;
+    if (tile < ntiles) load(tile, rx, rg);
+    for (; tile < ntiles; tile += gridDim.x) {
+        const int64_t p0 = tile * G::GB;
+        const int nvalid = (int)min((int64_t)G::GB, npix - p0);
+        lds_barrier();                    // the previous tile's dx store has read Lg
+        {
+            const bool ok = crow < nvalid;   // rows past the end are zero: nothing reaches dgamma / dbeta
+            const u32x4 vx = ok ? rx : u32x4{0u, 0u, 0u, 0u};
+            const u32x4 vg = ok ? rg : u32x4{0u, 0u, 0u, 0u};
+            *reinterpret_cast<u32x4*>(Lx + crow * G::RS + cch * 16) = vx;
+            *reinterpret_cast<u32x4*>(Lq + crow * G::RS + cch * 16) = sq_chunk<bf16>(vx);
+            *reinterpret_cast<u32x4*>(Lg + crow * G::RS + cch * 16) = vg;
+        }
+        if (tile + gridDim.x < ntiles) load(tile + gridDim.x, rx, rg);
+        lds_barrier();
+        // ---- norm = x^2 gamma^T (+ beta): rows = pixels, columns = this wave's 16 channels ----
+        f32x4 acc[G::TM];
+#pragma unroll
+        for (int tm = 0; tm < G::TM; ++tm) acc[tm] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kb = 0; kb < G::KB; ++kb)
+#pragma unroll
+            for (int tm = 0; tm < G::TM; ++tm) {
+                const u32x4 a = *reinterpret_cast<const u32x4*>(Lq + (tm * 16 + i16) * G::RS + kb * 64 + 16 * g_);
+                acc[tm] = mma16<bf16>(a, fb[kb], acc[tm]);
+            }
+        // ---- u, t1 (element rows tm*16 + 4 g_ + r, column n0 + i16) ----
+        float xr[G::TM][4], tr[G::TM][4];
+#pragma unroll
+        for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = tm * 16 + g_ * 4 + r;
+                xr[tm][r] = (float)*lds_elem<bf16>(Lx, G::RS, row, n0 + i16);
+                tr[tm][r] = (float)*lds_elem<bf16>(Lg, G::RS, row, n0 + i16);
+            }
+#pragma unroll
+        for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = tm * 16 + g_ * 4 + r;
+                const float xv = xr[tm][r], gv = tr[tm][r];
+                const float nv = acc[tm][r] + bv;
+                const float rs = rsqrtf(nv);
+                float uv, t1;
+                if constexpr (INV) {
+                    t1 = gv * nv * rs;
+                    uv = 0.5f * gv * xv * rs;
+                } else {
+                    t1 = gv * rs;
+                    uv = -0.5f * gv * xv * rs * rs * rs;
+                }
+                if (row >= nvalid) uv = 0.f;
+                dbeta += uv;
+                tr[tm][r] = (float)(bf16)t1;
+                *lds_elem<bf16>(Lu, G::RS, row, n0 + i16) = (bf16)uv;
+            }
+        lds_barrier();
+        // ---- dgamma[:, n0 .. n0+15] += u^T x^2 (K = the tile's 32 pixels) ----
+        {
+            const int rr = 8 * g_ + q_;
+            const int colB = n0 + 4 * p4;
+            const s16x4 b0 = ds_tr16(Lq, rr * G::RS + colB * 2);
+            const s16x4 b1 = ds_tr16(Lq, (rr + 4) * G::RS + colB * 2);
+            const s16x8 bvv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+            const u32x4 fbx = __builtin_bit_cast(u32x4, bvv);
+#pragma unroll
+            for (int t = 0; t < G::NW; ++t) {
+                const int colA = t * 16 + 4 * p4;
+                const s16x4 a0 = ds_tr16(Lu, rr * G::RS + colA * 2);
+                const s16x4 a1 = ds_tr16(Lu, (rr + 4) * G::RS + colA * 2);
+                const s16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+                dg[t] = mma16<bf16>(__builtin_bit_cast(u32x4, av), fbx, dg[t]);
+            }
+        }
+        // ---- dx = t1 + 2 x (u gamma): B = gamma^T rows of this wave's channels ----
+#pragma unroll
+        for (int tm = 0; tm < G::TM; ++tm) acc[tm] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kb = 0; kb < G::KB; ++kb) {
+            const u32x4 bt = *reinterpret_cast<const u32x4*>(Lt + (n0 + i16) * G::RS + kb * 64 + 16 * g_);
+#pragma unroll
+            for (int tm = 0; tm < G::TM; ++tm) {
+                const u32x4 a = *reinterpret_cast<const u32x4*>(Lu + (tm * 16 + i16) * G::RS + kb * 64 + 16 * g_);
+                acc[tm] = mma16<bf16>(a, bt, acc[tm]);
+            }
+        }
+#pragma unroll
+        for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = tm * 16 + g_ * 4 + r;
+                *lds_elem<bf16>(Lg, G::RS, row, n0 + i16) = (bf16)(tr[tm][r] + 2.f * xr[tm][r] * acc[tm][r]);
+            }
+        lds_barrier();
+        if (crow < nvalid)
+            *reinterpret_cast<u32x4*>(dx + (p0 + crow) * dx_ld + cch * 8) =
+                *reinterpret_cast<const u32x4*>(Lg + crow * G::RS + cch * 16);
+    }
+    // ---- partials: dbeta of this wave's channels (lanes of one column: xor 16, 32), dgamma column block ----
+    dbeta += __shfl_xor(dbeta, 16, 64);
+    dbeta += __shfl_xor(dbeta, 32, 64);
+    float* pb = part + (int64_t)blockIdx.x * (C * C + C);
+    if (lane < 16) pb[C * C + n0 + lane] = dbeta;
+#pragma unroll
+    for (int t = 0; t < G::NW; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = t * 16 + g_ * 4 + r, j = n0 + i16;
+            pb[(int64_t)i * C + j] = dg[t][r];
+        }
+}
+
 // sum the per-block partials in a fixed order, then the NonNegativeParametrizer /
 // LowerBound backward rule (as gdn_reparam_bwd_kernel).  256 threads = 16
 // element columns x 16 partial-block groups; groups combine through LDS in
@@ -832,7 +1018,7 @@ int cai_gdn_param_grad(int dtype, const void* x, int32_t x_ld, const void* u, in
 }
 
 
-static bool fused_ok(int dtype, int C) { return dtype == CAI_BF16 && (C == 64 || C == 128); }
+static bool fused_ok(int dtype, int C) { return dtype == CAI_BF16 && (C == 64 || C == 128 || C == 160 || C == 192); }
 
 size_t cai_gdn_backward_workspace_bytes(int64_t npix, int32_t C, int dtype) {
     if (npix <= 0 || !gdn_c_ok(C, dtype)) return 0;
@@ -873,7 +1059,18 @@ int cai_gdn_backward(int dtype, const void* x, int32_t x_ld, const void* dy, int
                            reinterpret_cast<const bf16*>(dy), dy_ld, npix, reinterpret_cast<const bf16*>(gamma_op),
                            beta, inverse, reinterpret_cast<bf16*>(dx), dx_ld, part);
     };
-    if (C == 128)
+    auto launch_wide = [&](auto kern, int nt) {
+        hipLaunchKernelGGL(kern, dim3(nblk), dim3(nt), 0, st, reinterpret_cast<const bf16*>(x), x_ld,
+                           reinterpret_cast<const bf16*>(dy), dy_ld, npix, reinterpret_cast<const bf16*>(gamma_op),
+                           beta, reinterpret_cast<bf16*>(dx), dx_ld, part);
+    };
+    if (C == 192)
+        inverse ? launch_wide(gdn_bwd_wide_kernel<192, true>, WideGeo<192>::NT)
+                : launch_wide(gdn_bwd_wide_kernel<192, false>, WideGeo<192>::NT);
+    else if (C == 160)
+        inverse ? launch_wide(gdn_bwd_wide_kernel<160, true>, WideGeo<160>::NT)
+                : launch_wide(gdn_bwd_wide_kernel<160, false>, WideGeo<160>::NT);
+    else if (C == 128)
         inverse ? launch(gdn_bwd_fused_kernel<128, true>) : launch(gdn_bwd_fused_kernel<128, false>);
     else
         inverse ? launch(gdn_bwd_fused_kernel<64, true>) : launch(gdn_bwd_fused_kernel<64, false>);

@@ -193,7 +193,7 @@ def test_gdn(cuda, C, inverse, bf16):
 
 
 @pytest.mark.parametrize("inverse", [False, True])
-@pytest.mark.parametrize("C", [64, 128])
+@pytest.mark.parametrize("C", [64, 128, 160, 192])
 def test_gdn_fused_backward_many_blocks(cuda, C, inverse):
     """bf16 fused backward (cai_gdn_backward: dx + per-block dgamma/dbeta partials, fixed-order
     reduce) over many tiles and blocks, against the fp32 oracle; and equal (to bf16 rounding of u)
