@@ -18,6 +18,7 @@ from typing import Dict, Optional, Tuple
 
 import torch
 
+from . import _ledger
 from ._native import ConvGeom, lib
 from ._ops import _p, _stream, compute_dtype, conv_geom, dcode, edge_eligible
 
@@ -119,8 +120,11 @@ class Prepacker:
         host = ctypes.create_string_buffer(b"".join(descs), len(descs) * dsz)
         total = lib.cai_conv_pack_finalize(host, len(descs))
         blob = torch.frombuffer(bytearray(host.raw), dtype=torch.uint8).to(dev)
+        # algorithmic bytes of one pack launch (ledger): every packed buffer written once, and its fp32 source
+        # read once per descriptor (approximated as 2x a bf16 buffer / 1x an fp32 one)
+        written = sum(b.numel() * b.element_size() for b in buffers)
         return {"sig": self._signature(), "table": table, "buffers": buffers, "descs": blob, "n": len(descs),
-                "total": total}
+                "total": total, "bytes": written * (3 if dtype == torch.bfloat16 else 2)}
 
     # -------------------------------------------------------------------- use
     def refresh(self):
@@ -132,7 +136,8 @@ class Prepacker:
             if plan is None:
                 return None
             self._plans[dtype] = plan
-        lib.cai_conv_pack_many(_p(plan["descs"]), plan["n"], dcode(dtype), plan["total"], _stream())
+        _ledger.run(lambda: lib.cai_conv_pack_many(_p(plan["descs"]), plan["n"], dcode(dtype), plan["total"], _stream()),
+                    "pack", "pack_many_kernel", 0, plan.get("bytes", 0), dtype, f"{plan['n']} descriptors")
         return plan
 
     def lookup(self, weight: torch.Tensor, dtype, direction: int) -> Optional[torch.Tensor]:

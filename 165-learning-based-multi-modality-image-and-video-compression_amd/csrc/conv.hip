@@ -1122,8 +1122,11 @@ struct PackArgs {
     int nphase;
     int ntaps[4], ntx[4], kh0[4], kw0[4], step;   // step = tap stride inside the kernel (s for phase, 1 for gather)
     int64_t off[4];
-    int64_t item_begin;    // pack_many: first global 8-element item of this descriptor
+    int64_t item_begin;    // pack_many: first global 8-element item of this descriptor (item-mode descriptors)
     int items_pp;          // pack_many: 8-element items per phase (Npad * Kp / 8)
+    int64_t row_begin;     // pack_many: first global row of this descriptor (row-mode conv descriptors)
+    int64_t rows_total;    // pack_many: rows of the whole table (the same in every descriptor)
+    int rowmode;           // 1: packed one output row (all phases) per block from an LDS copy of its sources
     int edge;              // 1: edge-layer MFMA fragments (edge_frag.hpp), one item per fragment
     EdgeFragSpec es;
     int gdn;               // 1: GDN reparametrisation (w = gamma_raw, mask = beta_raw, out = gamma_op, D1 = C)
@@ -1157,86 +1160,161 @@ __global__ void pack_weight_kernel(const PackArgs a) {
     pack_weight_body<T>(a, blockIdx.z);
 }
 
-// all the convs of a model in one launch: one flat space of 8-element items
-// over (descriptor, phase, row, k); a thread finds its descriptor by binary
-// search on item_begin, then writes 8 consecutive packed elements (16 B bf16)
+// all the convs of a model in one launch.  Conv descriptors go row by row: a block copies the fp32 source
+// row of one output channel n (all input channels x k*k taps: contiguous for the forward direction, k*k
+// runs for the transposed one) into LDS with coalesced loads, then writes the packed row of every phase
+// with 16-byte stores.  Edge-fragment and GDN descriptors (and conv rows too long for the LDS copy) go by
+// 8-element items, a thread per item.  Work units: rows_total row blocks, then blocks of 256 items.
+#ifndef CAI_PACK_ROW_MAX
+#define CAI_PACK_ROW_MAX 12288
+#endif
+constexpr int PACK_ROW_MAX = CAI_PACK_ROW_MAX;   // source floats per row that fit the LDS copy
+
 template <typename T>
-__global__ __launch_bounds__(256) void pack_many_kernel(const PackArgs* __restrict__ descs, int n, int64_t total) {
-    for (int64_t gi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; gi < total;
-         gi += (int64_t)gridDim.x * blockDim.x) {
-        int lo = 0, hi = n - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (descs[mid].item_begin <= gi) lo = mid; else hi = mid - 1;
-        }
-        const PackArgs& a = descs[lo];
-        const int local = (int)(gi - a.item_begin);
-        if constexpr (sizeof(T) == 2) {
-            if (a.edge) {
-                float v[8];
-                edge_frag_values(a.w, a.es.C, a.es.N, a.es.k, a.es.p, a.es.emode, local, v);
-                bf16x8 h;
+__device__ __forceinline__ void pack_item(const PackArgs* __restrict__ descs, int n, int64_t gi) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (descs[mid].item_begin <= gi) lo = mid; else hi = mid - 1;
+    }
+    const PackArgs& a = descs[lo];
+    const int local = (int)(gi - a.item_begin);
+    if constexpr (sizeof(T) == 2) {
+        if (a.edge) {
+            float v[8];
+            edge_frag_values(a.w, a.es.C, a.es.N, a.es.k, a.es.p, a.es.emode, local, v);
+            bf16x8 h;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) h[e] = (bf16)v[e];
-                *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(a.out) + (int64_t)local * 8) = h;
-                continue;
+            for (int e = 0; e < 8; ++e) h[e] = (bf16)v[e];
+            *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(a.out) + (int64_t)local * 8) = h;
+            return;
+        }
+    }
+    if (a.gdn) {
+        // gdn_reparam_kernel's element rule for 8 consecutive gamma entries (and beta for i < C)
+        const int C = a.D1;
+        const int64_t CC = (int64_t)C * C;
+        T* gop = reinterpret_cast<T*>(a.out);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int64_t i = (int64_t)local * 8 + e;
+            if (i >= CC) break;
+            const int r = (int)(i / C), c = (int)(i - (int64_t)r * C);
+            const float lb = fmaxf(a.w[i], a.gdn_gb);
+            const float v = lb * lb - a.gdn_ped;
+            gop[i] = from_f32<T>(v);
+            gop[CC + (int64_t)c * C + r] = from_f32<T>(v);
+            if (i < C) {
+                const float lbb = fmaxf(a.mask[i], a.gdn_bb);
+                a.gdn_beta[i] = lbb * lbb - a.gdn_ped;
             }
         }
-        if (a.gdn) {
-            // gdn_reparam_kernel's element rule for 8 consecutive gamma entries (and beta for i < C)
-            const int C = a.D1;
-            const int64_t CC = (int64_t)C * C;
-            T* gop = reinterpret_cast<T*>(a.out);
+        return;
+    }
+    const int ph = local / a.items_pp;
+    const int e0 = (local - ph * a.items_pp) * 8;
+    const int nrow = e0 / a.Kp;
+    const int kk0 = e0 - nrow * a.Kp;
+    int t = kk0 / a.Cpad, c = kk0 - t * a.Cpad;
+    const int ntaps = ph == 0 ? a.ntaps[0] : (ph == 1 ? a.ntaps[1] : (ph == 2 ? a.ntaps[2] : a.ntaps[3]));
+    const int ntx = ph == 0 ? a.ntx[0] : (ph == 1 ? a.ntx[1] : (ph == 2 ? a.ntx[2] : a.ntx[3]));
+    const int kh0 = ph == 0 ? a.kh0[0] : (ph == 1 ? a.kh0[1] : (ph == 2 ? a.kh0[2] : a.kh0[3]));
+    const int kw0 = ph == 0 ? a.kw0[0] : (ph == 1 ? a.kw0[1] : (ph == 2 ? a.kw0[2] : a.kw0[3]));
+    const int64_t off = ph == 0 ? a.off[0] : (ph == 1 ? a.off[1] : (ph == 2 ? a.off[2] : a.off[3]));
+    float v[8];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int64_t i = (int64_t)local * 8 + e;
-                if (i >= CC) break;
-                const int r = (int)(i / C), c = (int)(i - (int64_t)r * C);
-                const float lb = fmaxf(a.w[i], a.gdn_gb);
-                const float v = lb * lb - a.gdn_ped;
-                gop[i] = from_f32<T>(v);
-                gop[CC + (int64_t)c * C + r] = from_f32<T>(v);
-                if (i < C) {
-                    const float lbb = fmaxf(a.mask[i], a.gdn_bb);
-                    a.gdn_beta[i] = lbb * lbb - a.gdn_ped;
-                }
-            }
-            continue;
+    for (int e = 0; e < 8; ++e) {
+        float x = 0.f;
+        if (nrow < a.Nreal && c < a.Creal && t < ntaps) {
+            const int ty = t / ntx;
+            const int kh = kh0 + a.step * ty, kw = kw0 + a.step * (t - ty * ntx);
+            const int d0 = a.n_is_d0 ? nrow : c, d1 = a.n_is_d0 ? c : nrow;
+            const int64_t src = (((int64_t)d0 * a.D1 + d1) * a.k + kh) * a.k + kw;
+            x = a.w[src];
+            if (a.mask) x *= a.mask[src];
         }
-        const int ph = local / a.items_pp;
-        const int e0 = (local - ph * a.items_pp) * 8;
-        const int nrow = e0 / a.Kp;
-        const int kk0 = e0 - nrow * a.Kp;
-        int t = kk0 / a.Cpad, c = kk0 - t * a.Cpad;
+        v[e] = x;
+        if (++c == a.Cpad) { c = 0; ++t; }
+    }
+    T* out = reinterpret_cast<T*>(a.out) + off + e0;
+    if constexpr (sizeof(T) == 2) {
+        bf16x8 h;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) h[e] = (bf16)v[e];
+        *reinterpret_cast<bf16x8*>(out) = h;
+    } else {
+        *reinterpret_cast<f32x4*>(out) = f32x4{v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<f32x4*>(out + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void pack_row(const PackArgs& a, int n, float* S) {
+    const int KK = a.k * a.k;
+    const int nsrc = a.Creal * KK;
+    if (n < a.Nreal) {
+        for (int i = threadIdx.x; i < nsrc; i += blockDim.x) {
+            const int c = i / KK, tap = i - c * KK;
+            const int64_t src = a.n_is_d0 ? (int64_t)n * a.D1 * KK + i : ((int64_t)c * a.D1 + n) * KK + tap;
+            float v = a.w[src];
+            if (a.mask) v *= a.mask[src];
+            S[i] = v;
+        }
+    }
+    __syncthreads();
+    const int nch = a.Kp / 8;
+    for (int ph = 0; ph < a.nphase; ++ph) {
         const int ntaps = ph == 0 ? a.ntaps[0] : (ph == 1 ? a.ntaps[1] : (ph == 2 ? a.ntaps[2] : a.ntaps[3]));
         const int ntx = ph == 0 ? a.ntx[0] : (ph == 1 ? a.ntx[1] : (ph == 2 ? a.ntx[2] : a.ntx[3]));
         const int kh0 = ph == 0 ? a.kh0[0] : (ph == 1 ? a.kh0[1] : (ph == 2 ? a.kh0[2] : a.kh0[3]));
         const int kw0 = ph == 0 ? a.kw0[0] : (ph == 1 ? a.kw0[1] : (ph == 2 ? a.kw0[2] : a.kw0[3]));
         const int64_t off = ph == 0 ? a.off[0] : (ph == 1 ? a.off[1] : (ph == 2 ? a.off[2] : a.off[3]));
-        float v[8];
+        T* out = reinterpret_cast<T*>(a.out) + off + (int64_t)n * a.Kp;
+        for (int ch = threadIdx.x; ch < nch; ch += blockDim.x) {
+            const int e0 = ch * 8;
+            int t = e0 / a.Cpad, c = e0 - t * a.Cpad;   // fp32 (Cpad % 4 == 0): the 8 may span two taps
+            float v[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            float x = 0.f;
-            if (nrow < a.Nreal && c < a.Creal && t < ntaps) {
-                const int ty = t / ntx;
-                const int kh = kh0 + a.step * ty, kw = kw0 + a.step * (t - ty * ntx);
-                const int d0 = a.n_is_d0 ? nrow : c, d1 = a.n_is_d0 ? c : nrow;
-                const int64_t src = (((int64_t)d0 * a.D1 + d1) * a.k + kh) * a.k + kw;
-                x = a.w[src];
-                if (a.mask) x *= a.mask[src];
+            for (int e = 0; e < 8; ++e) {
+                float x = 0.f;
+                if (n < a.Nreal && c < a.Creal && t < ntaps) {
+                    const int ty = t / ntx;
+                    x = S[c * KK + (kh0 + a.step * ty) * a.k + kw0 + a.step * (t - ty * ntx)];
+                }
+                v[e] = x;
+                if (++c == a.Cpad) { c = 0; ++t; }
             }
-            v[e] = x;
-            if (++c == a.Cpad) { c = 0; ++t; }
-        }
-        T* out = reinterpret_cast<T*>(a.out) + off + e0;
-        if constexpr (sizeof(T) == 2) {
-            bf16x8 h;
+            if constexpr (sizeof(T) == 2) {
+                bf16x8 h;
 #pragma unroll
-            for (int e = 0; e < 8; ++e) h[e] = (bf16)v[e];
-            *reinterpret_cast<bf16x8*>(out) = h;
+                for (int e = 0; e < 8; ++e) h[e] = (bf16)v[e];
+                *reinterpret_cast<bf16x8*>(out + e0) = h;
+            } else {
+                *reinterpret_cast<f32x4*>(out + e0) = f32x4{v[0], v[1], v[2], v[3]};
+                *reinterpret_cast<f32x4*>(out + e0 + 4) = f32x4{v[4], v[5], v[6], v[7]};
+            }
+        }
+    }
+    __syncthreads();   // the next row reuses S
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void pack_many_kernel(const PackArgs* __restrict__ descs, int n, int64_t total) {
+    __shared__ float S[PACK_ROW_MAX];
+    const int64_t R = descs[0].rows_total;
+    const int64_t I = total - R;
+    const int64_t units = R + (I + 255) / 256;
+    for (int64_t u = blockIdx.x; u < units; u += gridDim.x) {
+        if (u < R) {
+            int lo = 0, hi = n - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (descs[mid].row_begin <= u) lo = mid; else hi = mid - 1;
+            }
+            pack_row<T>(descs[lo], (int)(u - descs[lo].row_begin), S);
         } else {
-            *reinterpret_cast<f32x4*>(out) = f32x4{v[0], v[1], v[2], v[3]};
-            *reinterpret_cast<f32x4*>(out + 4) = f32x4{v[4], v[5], v[6], v[7]};
+            const int64_t gi = (u - R) * 256 + threadIdx.x;
+            if (gi < I) pack_item<T>(descs, n, gi);
         }
     }
 }
@@ -1269,6 +1347,10 @@ struct WgradArgs {
     int ctiles, rtiles, nsub, grp_len, chunk;
     int nsplit;        // glds kernel: pixel splits (split_len pixels each)
     float* bws;        // glds kernel: per-split bias partials [nsplit][Ng] (NULL: none)
+    // ConvTranspose2d bias gradient from the X operand (WG_TBIAS): the column sums of the taps
+    // (tb_kh0 + a, tb_kw0 + b), a, b < tb_s, which together visit every output pixel exactly once;
+    // partials [nsplit * tb_s^2][nbias]
+    int tb_kh0, tb_kw0, tb_s, nbias;
 };
 
 constexpr int WG_CHUNK = 1024;   // max pixels per L2-resident wgrad chunk (multiple of 64)
@@ -1482,7 +1564,21 @@ __global__ __launch_bounds__(NT, 2) void wgrad_kernel(const WgradArgs a) {
 // Block b works on pixel split (xcd-remapped index / tiles): the tiles of one
 // pixel range share an XCD's L2.
 // ---------------------------------------------------------------------------
-enum { WG_ABS = 1, WG_SQ = 2, WG_BIAS = 4 };
+enum { WG_ABS = 1, WG_SQ = 2, WG_BIAS = 4, WG_TBIAS = 8 };
+
+__device__ __forceinline__ float sum8_bf16(u32x4 v) {
+    const bf16x8 h = __builtin_bit_cast(bf16x8, v);
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += (float)h[e];
+    return s;
+}
+
+// index of tap (kh, kw) in the transposed-bias tap set, or -1
+__device__ __forceinline__ int tbias_sel(const WgradArgs& a, int kh, int kw) {
+    const int dh = kh - a.tb_kh0, dw = kw - a.tb_kw0;
+    return ((unsigned)dh < (unsigned)a.tb_s && (unsigned)dw < (unsigned)a.tb_s) ? dh * a.tb_s + dw : -1;
+}
 
 template <int CT, int FLAGS>
 __global__ __launch_bounds__(512, 1) void wgrad_glds_kernel(const WgradArgs a) {
@@ -1586,6 +1682,21 @@ __global__ __launch_bounds__(512, 1) void wgrad_glds_kernel(const WgradArgs a) {
     float bsum[4] = {0.f, 0.f, 0.f, 0.f};
     const int wcol = wc * WCOL;
     const int ximg = 1 + wcol / 128, xcb = wcol % 128;
+    // transposed bias: this lane's column (tap, q) of each column block, if its tap is in the set
+    int tsel[TN], tq[TN];
+    float tsum[TN];
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+        tsum[t] = 0.f;
+        tsel[t] = -1;
+        tq[t] = 0;
+        if constexpr ((FLAGS & WG_TBIAS) != 0) {
+            const int col = c0 + wcol + t * 16 + (lane & 15);
+            const int tap = col / a.Cq_pad, q = col - tap * a.Cq_pad;
+            if (col < a.ncols && q < a.nbias && rtile == 0 && wr == 0) tsel[t] = tbias_sel(a, tap / a.k, tap % a.k);
+            tq[t] = q;
+        }
+    }
     if (nsteps > 0) issue(0, 0);
     if (nsteps > 1) issue(1, 1);
     for (int st = 0; st < nsteps; ++st) {
@@ -1612,6 +1723,9 @@ __global__ __launch_bounds__(512, 1) void wgrad_glds_kernel(const WgradArgs a) {
                 fb[t] = __builtin_bit_cast(u32x4, bv);
                 if constexpr ((FLAGS & WG_ABS) != 0) fb[t] = abs_chunk(fb[t], 2);
                 if constexpr ((FLAGS & WG_SQ) != 0) fb[t] = sq_chunk<bf16>(fb[t]);
+                if constexpr ((FLAGS & WG_TBIAS) != 0) {
+                    if (tsel[t] >= 0) tsum[t] += sum8_bf16(fb[t]);
+                }
             }
 #pragma unroll
             for (int tm = 0; tm < 4; ++tm) {
@@ -1644,6 +1758,17 @@ __global__ __launch_bounds__(512, 1) void wgrad_glds_kernel(const WgradArgs a) {
             v += __shfl_xor(v, 32);
             const int n = r0 + wr * 64 + wc * 16 + lane;
             if (lane < 16 && n < a.Ng) a.bws[(int64_t)split * a.Ng + n] = v;
+        }
+    }
+    if constexpr ((FLAGS & WG_TBIAS) != 0) {
+        // a column's 4 lane groups (lane >> 4) hold disjoint pixels: fold them, one lane writes
+#pragma unroll
+        for (int t = 0; t < TN; ++t) {
+            float v = tsum[t];
+            v += __shfl_xor(v, 16);
+            v += __shfl_xor(v, 32);
+            if (lane < 16 && tsel[t] >= 0)
+                a.bws[((int64_t)split * a.tb_s * a.tb_s + tsel[t]) * a.nbias + tq[t]] = v;
         }
     }
 #pragma unroll
@@ -1792,6 +1917,17 @@ __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
     const bool do_bias = (FLAGS & WG_BIAS) && ctile == 0;
     float bsum[4] = {0.f, 0.f, 0.f, 0.f};
     const int wcol = wc * W::WCOL;
+    int tsel[W::TN];
+    float tsum[W::TN];
+#pragma unroll
+    for (int t = 0; t < W::TN; ++t) {
+        tsum[t] = 0.f;
+        tsel[t] = -1;
+        if constexpr ((FLAGS & WG_TBIAS) != 0) {
+            const int col = wcol + t * 16 + (lane & 15);
+            if (q0 + col % 64 < a.nbias && rtile == 0 && wr == 0) tsel[t] = tbias_sel(a, kh, col / 64);
+        }
+    }
     // LDS byte offsets of every fragment read, fixed for the launch (stage 0; the other stages add a
     // compile-time immediate): B (footprint) per (ks, column block, pixel half) -- the tap's plane / cell
     // shift and the block's swizzled 32-B group -- and A (G strip)
@@ -1830,6 +1966,9 @@ __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
                 s16x4 b1 = ds_tr16(Xs, boff[ks][t][1]);
                 s16x8 bv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
                 fb[t] = __builtin_bit_cast(u32x4, bv);
+                if constexpr ((FLAGS & WG_TBIAS) != 0) {
+                    if (tsel[t] >= 0) tsum[t] += sum8_bf16(fb[t]);
+                }
             }
 #pragma unroll
             for (int tm = 0; tm < 4; ++tm) {
@@ -1889,6 +2028,17 @@ __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
             if (lane < 16 && n < a.Ng) a.bws[(int64_t)split * a.Ng + n] = v;
         }
     }
+    if constexpr ((FLAGS & WG_TBIAS) != 0) {
+#pragma unroll
+        for (int t = 0; t < W::TN; ++t) {
+            float v = tsum[t];
+            v += __shfl_xor(v, 16);
+            v += __shfl_xor(v, 32);
+            const int col = wcol + t * 16 + (lane & 15);
+            if (lane < 16 && tsel[t] >= 0)
+                a.bws[((int64_t)split * a.tb_s * a.tb_s + tsel[t]) * a.nbias + q0 + col % 64] = v;
+        }
+    }
 #pragma unroll
     for (int tn = 0; tn < W::TN; ++tn) {
         const int col = wcol + tn * 16 + (lane & 15), kw = col / 64;
@@ -1904,17 +2054,20 @@ __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
 }
 
 template <int KS>
-static void launch_wgrad_halo(const WgradArgs& a, int nblocks, bool bias, hipStream_t st) {
-    if (bias)
+static void launch_wgrad_halo(const WgradArgs& a, int nblocks, int bias, hipStream_t st) {
+    if (bias == WG_BIAS)
         hipLaunchKernelGGL((wgrad_halo_kernel<KS, WG_BIAS>), dim3(nblocks), dim3(512), 0, st, a);
+    else if (bias == WG_TBIAS)
+        hipLaunchKernelGGL((wgrad_halo_kernel<KS, WG_TBIAS>), dim3(nblocks), dim3(512), 0, st, a);
     else
         hipLaunchKernelGGL((wgrad_halo_kernel<KS, 0>), dim3(nblocks), dim3(512), 0, st, a);
 }
 
 template <int CT>
-static void launch_wgrad_glds(const WgradArgs& a, int nblocks, int in_abs, int in_sq, bool bias, hipStream_t st) {
-    const int f = (in_abs ? WG_ABS : 0) | (in_sq ? WG_SQ : 0) | (bias ? WG_BIAS : 0);
+static void launch_wgrad_glds(const WgradArgs& a, int nblocks, int in_abs, int in_sq, int bias, hipStream_t st) {
+    const int f = (in_abs ? WG_ABS : 0) | (in_sq ? WG_SQ : 0) | bias;
     switch (f) {
+        case WG_TBIAS: hipLaunchKernelGGL((wgrad_glds_kernel<CT, WG_TBIAS>), dim3(nblocks), dim3(512), 0, st, a); break;
         case 0: hipLaunchKernelGGL((wgrad_glds_kernel<CT, 0>), dim3(nblocks), dim3(512), 0, st, a); break;
         case WG_ABS: hipLaunchKernelGGL((wgrad_glds_kernel<CT, WG_ABS>), dim3(nblocks), dim3(512), 0, st, a); break;
         case WG_SQ: hipLaunchKernelGGL((wgrad_glds_kernel<CT, WG_SQ>), dim3(nblocks), dim3(512), 0, st, a); break;
@@ -1931,26 +2084,26 @@ static void launch_wgrad_glds(const WgradArgs& a, int nblocks, int in_abs, int i
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int S, int Ng, int ncols,
                                                            int Cq, int Cq_pad, int k, float* __restrict__ dw,
                                                            int accumulate, const float* __restrict__ bws,
-                                                           float* __restrict__ db) {
+                                                           float* __restrict__ db, int Sb, int nbias) {
     // one thread per 16-byte column chunk summing its S split partials in split order; the loads go out
     // in batches of 8 independent requests (the partials stream from HBM once)
     const int c4 = ncols >> 2;
     const int64_t total = (int64_t)Ng * c4;
     const int wblocks = (int)((total + 255) / 256);
     if ((int)blockIdx.x >= wblocks) {
-        // trailing blocks: bias partials [S][Ng] -> db, one thread per channel
+        // trailing blocks: bias partials [Sb][nbias] -> db, one thread per channel
         const int n = ((int)blockIdx.x - wblocks) * 256 + threadIdx.x;
-        if (n >= Ng) return;
+        if (n >= nbias) return;
         float v = 0.f;
         int sp = 0;
-        for (; sp + 8 <= S; sp += 8) {
+        for (; sp + 8 <= Sb; sp += 8) {
             float b[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) b[j] = bws[(int64_t)(sp + j) * Ng + n];
+            for (int j = 0; j < 8; ++j) b[j] = bws[(int64_t)(sp + j) * nbias + n];
 #pragma unroll
             for (int j = 0; j < 8; ++j) v += b[j];
         }
-        for (; sp < S; ++sp) v += bws[(int64_t)sp * Ng + n];
+        for (; sp < Sb; ++sp) v += bws[(int64_t)sp * nbias + n];
         db[n] = accumulate ? db[n] + v : v;
         return;
     }
@@ -2402,6 +2555,8 @@ static int run_conv(const cai_conv_geom* g, int dtype, int direction, const void
 
 struct WgradPlan {
     int halo;        // kernel size of the halo-staged kernel (0: not taken); S then counts strip ranges
+    int tbias, tb_kh0, tb_kw0;   // ConvTranspose2d bias from the X operand's tap set (WG_TBIAS)
+    int Sb, nbias;               // bias partial slabs and their length
     int strips_per_split;
     bool glds, fused_bias;
     int ct;
@@ -2427,6 +2582,28 @@ static bool halo_wgrad_ks(const cai_conv_geom* g, const WgradPlan& W) {
     const int Wg = g->transposed ? g->in_w : g->out_w;
     return !halo_wgrad_off() && g->stride == 2 && (g->kernel == 3 || g->kernel == 5) && g->pad == g->kernel / 2 &&
            Wg % 64 == 0 && W.Cq_pad % 64 == 0;
+}
+
+// ConvTranspose2d: an s x s block of taps (kh0 + a, kw0 + b) such that every output pixel is reached
+// from exactly one (input pixel, tap) pair -- the bias gradient is then the sum of those taps' X columns
+static bool tbias_axis(int k, int s, int p, int in, int out, int& k0) {
+    for (k0 = 0; k0 + s <= k; ++k0) {
+        bool ok = true;
+        for (int o = 0; o < out && ok; ++o) {
+            int cnt = 0;
+            for (int kk = k0; kk < k0 + s; ++kk) {
+                const int t = o + p - kk;
+                if (t >= 0 && t % s == 0 && t / s < in) ++cnt;
+            }
+            ok = cnt == 1;
+        }
+        if (ok) return true;
+    }
+    return false;
+}
+static bool tbias_taps(const cai_conv_geom* g, int& kh0, int& kw0) {
+    return g->transposed && tbias_axis(g->kernel, g->stride, g->pad, g->in_h, g->out_h, kh0) &&
+           tbias_axis(g->kernel, g->stride, g->pad, g->in_w, g->out_w, kw0);
 }
 
 static int colsum_nchunk(int64_t npix) {
@@ -2480,7 +2657,10 @@ static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype, bool glds, b
     }
     W.ws_slab = (size_t)W.S * W.Ng * W.ncols * sizeof(float);
     W.fused_bias = W.glds && !g->transposed;
-    W.ws_bias = W.fused_bias ? ((size_t)W.S * W.Ng * sizeof(float) + 255) / 256 * 256 : 0;
+    W.tbias = W.glds && g->transposed && !in_tf && tbias_taps(g, W.tb_kh0, W.tb_kw0);
+    W.Sb = W.fused_bias ? W.S : (W.tbias ? W.S * g->stride * g->stride : 0);
+    W.nbias = W.fused_bias ? W.Ng : W.Cq;
+    W.ws_bias = W.Sb ? ((size_t)W.Sb * W.nbias * sizeof(float) + 255) / 256 * 256 : 0;
     // bias grad: columns of the module output gradient
     const int64_t npix_out = (int64_t)g->batch * g->out_h * g->out_w;
     W.nchunk = colsum_nchunk(npix_out);
@@ -2598,20 +2778,29 @@ int cai_gdn_reparam_describe(const float* beta_raw, const float* gamma_raw, int3
 int64_t cai_conv_pack_finalize(void* descs, int32_t n) {
     if (!descs || n <= 0) return -1;
     PackArgs* d = reinterpret_cast<PackArgs*>(descs);
-    int64_t begin = 0;
+    // row mode for conv descriptors whose source row fits the LDS copy; zero-size entries in the other
+    // numbering keep both begin arrays non-decreasing (a unit's descriptor is the LAST one at or below it)
+    int64_t items = 0, rows = 0;
     for (int i = 0; i < n; ++i) {
         d[i].items_pp = (int)((int64_t)d[i].Npad * d[i].Kp / 8);
-        d[i].item_begin = begin;
-        begin += (int64_t)d[i].items_pp * d[i].nphase;
+        d[i].rowmode = !d[i].edge && !d[i].gdn && d[i].Creal * d[i].k * d[i].k <= PACK_ROW_MAX;
+        d[i].item_begin = items;
+        d[i].row_begin = rows;
+        if (d[i].rowmode)
+            rows += d[i].Npad;
+        else
+            items += (int64_t)d[i].items_pp * d[i].nphase;
     }
-    return begin;
+    for (int i = 0; i < n; ++i) d[i].rows_total = rows;
+    return rows + items;
 }
 
 int cai_conv_pack_many(const void* descs, int32_t n, int dtype, int64_t total_items, void* stream) {
     CAI_CHECK_ARG(descs && n > 0 && total_items > 0, "pack_many: bad arguments");
     CAI_CHECK_ARG(dtype == CAI_BF16 || dtype == CAI_F32, "pack_many: bad dtype");
     CAI_CHECK_ARG(((uintptr_t)descs & 7) == 0, "pack_many: descriptor table not 8-byte aligned");
-    const int blocks = (int)std::min<int64_t>(4096, (total_items + 255) / 256);
+    // work units: one block per row-mode row, one per 256 items; total_items = rows + items bounds them
+    const int blocks = (int)std::min<int64_t>(8192, total_items);
     const PackArgs* d = reinterpret_cast<const PackArgs*>(descs);
     if (dtype == CAI_BF16)
         hipLaunchKernelGGL(pack_many_kernel<bf16>, dim3(blocks), dim3(256), 0, as_stream(stream), d, n, total_items);
@@ -2739,19 +2928,21 @@ int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_l
         a.ctiles = (W.ncols + W.ct - 1) / W.ct;
         a.split_len = W.split_len;
         a.nsplit = W.S;
-        if (W.fused_bias && db) bws = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + W.ws_slab);
+        if ((W.fused_bias || W.tbias) && db) bws = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + W.ws_slab);
         a.bws = bws;
+        a.tb_kh0 = W.tb_kh0; a.tb_kw0 = W.tb_kw0; a.tb_s = g->stride; a.nbias = W.nbias;
+        const int bflag = !bws ? 0 : (W.tbias ? WG_TBIAS : WG_BIAS);
         if (W.halo) {
             a.nsplit = W.strips_per_split;
             a.rtiles = (W.Ng + 127) / 128;
             if (W.halo == 5)
-                launch_wgrad_halo<5>(a, W.S * W.tiles, bws != nullptr, st);
+                launch_wgrad_halo<5>(a, W.S * W.tiles, bflag, st);
             else
-                launch_wgrad_halo<3>(a, W.S * W.tiles, bws != nullptr, st);
+                launch_wgrad_halo<3>(a, W.S * W.tiles, bflag, st);
         } else if (W.ct == 256)
-            launch_wgrad_glds<256>(a, W.S * W.tiles, in_abs, in_sq, bws != nullptr, st);
+            launch_wgrad_glds<256>(a, W.S * W.tiles, in_abs, in_sq, bflag, st);
         else
-            launch_wgrad_glds<128>(a, W.S * W.tiles, in_abs, in_sq, bws != nullptr, st);
+            launch_wgrad_glds<128>(a, W.S * W.tiles, in_abs, in_sq, bflag, st);
     } else {
         dim3 grid(8 * a.ctiles * a.rtiles * a.nsub);
         if (dtype == CAI_BF16)
@@ -2760,8 +2951,9 @@ int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_l
             hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(NT), 0, st, a);
     }
     const int64_t tot = (int64_t)W.Ng * (W.ncols / 4);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((tot + 255) / 256) + (bws ? (W.Ng + 255) / 256 : 0)), dim3(256), 0,
-                       st, slab, W.S, W.Ng, W.ncols, W.Cq, W.Cq_pad, g->kernel, dw, accumulate, bws, db);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((tot + 255) / 256) + (bws ? (W.nbias + 255) / 256 : 0)),
+                       dim3(256), 0, st, slab, W.S, W.Ng, W.ncols, W.Cq, W.Cq_pad, g->kernel, dw, accumulate, bws, db,
+                       W.Sb, W.nbias);
     if (db && !bws) {
         float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + W.ws_slab + W.ws_bias);
         const int64_t npix = (int64_t)g->batch * g->out_h * g->out_w;
