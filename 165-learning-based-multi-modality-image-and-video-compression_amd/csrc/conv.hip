@@ -1166,7 +1166,7 @@ __global__ void pack_weight_kernel(const PackArgs a) {
 // with 16-byte stores.  Edge-fragment and GDN descriptors (and conv rows too long for the LDS copy) go by
 // 8-element items, a thread per item.  Work units: rows_total row blocks, then blocks of 256 items.
 #ifndef CAI_PACK_ROW_MAX
-#define CAI_PACK_ROW_MAX 12288
+#define CAI_PACK_ROW_MAX 6144   // 24 KB: A/B 12288 / 6144 / 4096 / item-only -> 47 / 33 / 35 / 47 us (C2)
 #endif
 constexpr int PACK_ROW_MAX = CAI_PACK_ROW_MAX;   // source floats per row that fit the LDS copy
 
