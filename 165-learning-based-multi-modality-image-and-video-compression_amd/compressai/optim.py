@@ -40,7 +40,10 @@ def _align(n: int, a: int = 4) -> int:
 
 class FusedAdam(torch.optim.Optimizer):
     def __init__(self, params: Iterable[torch.nn.Parameter], lr: float = 1e-3, betas: Tuple[float, float] = (0.9, 0.999),
-                 eps: float = 1e-8, skip_nonfinite: bool = True):
+                 eps: float = 1e-8, skip_nonfinite: bool = True, layout: Optional[List[int]] = None):
+        """layout: optional permutation of the parameter indices giving their order in the flat buffers
+        (param_groups / state_dict keep the given order); distributed.OverlappedAllReduce puts the
+        parameters whose gradients finish last at the end so the rest can be exchanged early."""
         params = [p for p in params]
         if not params:
             raise ValueError("optimizer got an empty parameter list")
@@ -58,13 +61,17 @@ class FusedAdam(torch.optim.Optimizer):
         if dev.type != "cuda":
             raise ValueError("FusedAdam runs on GPU parameters only")
         self.skip_nonfinite = bool(skip_nonfinite)
-        offs, n = [], 0
-        for p in self.params:
+        order = list(range(len(self.params))) if layout is None else [int(i) for i in layout]
+        if sorted(order) != list(range(len(self.params))):
+            raise ValueError("layout must be a permutation of the parameter indices")
+        offs, n = [0] * len(self.params), 0
+        for i in order:
+            p = self.params[i]
             if p.dtype != torch.float32:
                 raise ValueError("FusedAdam expects fp32 master parameters")
             if p.device != dev:
                 raise ValueError("FusedAdam expects all parameters on one device")
-            offs.append(n)
+            offs[i] = n
             n += _align(p.numel())
         self.offsets = offs
         self.numel = n
@@ -215,8 +222,16 @@ def parameter_groups(net):
     return main, aux
 
 
-def configure_optimizers(net, lr: float = 1e-4, aux_lr: float = 1e-3):
-    """train.py:111-142: main Adam on all but `.quantiles`, aux Adam on `.quantiles` (sorted by name)."""
+def configure_optimizers(net, lr: float = 1e-4, aux_lr: float = 1e-3, tail: Tuple[str, ...] = ()):
+    """train.py:111-142: main Adam on all but `.quantiles`, aux Adam on `.quantiles` (sorted by name).
+
+    tail: name prefixes whose parameters go last in the main flat buffers (FusedAdam layout); the
+    optimizer's ``tail_offset`` is where they start (distributed.OverlappedAllReduce)."""
     named = dict(net.named_parameters())
     main, aux = parameter_groups(net)
-    return FusedAdam((named[n] for n in main), lr=lr), FusedAdam((named[n] for n in aux), lr=aux_lr)
+    is_tail = [any(n.startswith(t) for t in tail) for n in main]
+    layout = [i for i, t in enumerate(is_tail) if not t] + [i for i, t in enumerate(is_tail) if t]
+    opt = FusedAdam((named[n] for n in main), lr=lr, layout=layout)
+    tails = [opt.offsets[i] for i, t in enumerate(is_tail) if t]
+    opt.tail_offset = min(tails) if tails else opt.numel
+    return opt, FusedAdam((named[n] for n in aux), lr=aux_lr)

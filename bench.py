@@ -63,6 +63,11 @@ def parse():
                          "guided by Guided_compresser on RGB 1024x1280, train.py:208-274)")
     ap.add_argument("--quality", type=int, default=1)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--dist-backend", default=None, help="torch.distributed backend (default: nccl = RCCL)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal on a 1-GPU box: every rank on cuda:0 (needs --dist-backend gloo)")
+    ap.add_argument("--serial-allreduce", action="store_true",
+                    help="N > 1: one all-reduce after the backward instead of the two overlapped buckets")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-batch", type=int, default=None, help="CPU baseline batch (default: the GPU per-step batch)")
     ap.add_argument("--no-profile", action="store_true", help="skip the profiled step (no roofline fields)")
@@ -269,15 +274,15 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from compressai.distributed import allreduce_mean_, broadcast_parameters_, init_from_env
+    from compressai.distributed import OverlappedAllReduce, allreduce_mean_, broadcast_parameters_, init_from_env
     from compressai.losses import RateDistortionLoss
     from compressai.optim import configure_optimizers
     from compressai.zoo import image_models
 
-    rank, world = init_from_env()
+    rank, world = init_from_env(backend=args.dist_backend)
     if world != args.gpus:
         raise SystemExit(f"bench: --gpus {args.gpus} but the job has {world} ranks")
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     torch.manual_seed(0)                     # identical initial weights (rank 0's are broadcast anyway)
@@ -299,11 +304,18 @@ def main():
         x = torch.rand(args.batch, 3, args.size, args.size, generator=gen).to(dev)
     broadcast_parameters_(net)
     torch.cuda.manual_seed(1000 + rank)      # per-rank training noise
-    opt, aux_opt = configure_optimizers(net)
+    # N > 1: the gradient exchange in two buckets, the first overlapped with the analysis transform's
+    # backward (compressai.distributed.OverlappedAllReduce); Master_compresser keeps the single exchange
+    overlap = world > 1 and not multimodal and hasattr(net, "g_a") and not args.serial_allreduce
+    opt, aux_opt = configure_optimizers(net, tail=("g_a.",) if overlap else ())
+    sync = None
+    if overlap:
+        head = [p for n, p in net.named_parameters() if not n.startswith("g_a.") and not n.endswith(".quantiles")]
+        sync = OverlappedAllReduce(opt.flat_grad, opt.tail_offset, net.g_a, head)
     criterion = RateDistortionLoss(args.quality)
     state = {}
 
-    def fwd_bwd():
+    def fwd(two_phase=False):
         opt.zero_grad()
         aux_opt.zero_grad()
         if multimodal:
@@ -312,8 +324,14 @@ def main():
         with torch.autocast("cuda", dtype=torch.bfloat16):
             out = net(x, guide, hidden) if multimodal else net(x)
             crit = criterion(out, x)
-        crit["loss"].backward()
         state["loss"] = crit["loss"].detach()
+        if two_phase:
+            sync.backward_head(crit["loss"])    # everything but g_a: the head bucket is final
+        else:
+            crit["loss"].backward()
+
+    def fwd_bwd():
+        fwd()
 
     def opt_part():
         opt.step(max_norm=1.0)
@@ -326,8 +344,14 @@ def main():
         opt_part()
 
     def eager_step():
-        fwd_bwd()
-        allreduce_mean_(opt.flat_grad)
+        if sync is None:
+            fwd_bwd()
+            allreduce_mean_(opt.flat_grad)
+        else:
+            fwd(two_phase=True)
+            sync.reduce_head()      # side stream, overlapped with g_a's backward
+            sync.backward_tail()
+            sync.finish()
         opt_part()
 
     if multimodal:
@@ -358,14 +382,26 @@ def main():
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         gA, gB = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(gA):
-            fwd_bwd()
+        if sync is None:
+            with torch.cuda.graph(gA):
+                fwd_bwd()
+        else:
+            gT = torch.cuda.CUDAGraph()             # g_a's backward: the second phase
+            with torch.cuda.graph(gA):
+                fwd(two_phase=True)
+            with torch.cuda.graph(gT, pool=gA.pool()):
+                sync.backward_tail()
         with torch.cuda.graph(gB, pool=gA.pool()):
             opt_part()
 
         def step():
             gA.replay()
-            allreduce_mean_(opt.flat_grad)
+            if sync is None:
+                allreduce_mean_(opt.flat_grad)
+            else:
+                sync.reduce_head()                  # overlaps gT on the compute stream
+                gT.replay()
+                sync.finish()
             gB.replay()
 
     for _ in range(args.warmup):
@@ -412,7 +448,9 @@ def main():
             "config": {"workload": workload,
                        "model": args.model, "quality": args.quality, "global_batch": args.batch * world,
                        "per_gpu_batch": args.batch, "seq_len": None,
-                       "patch": list(MM_IR) if multimodal else args.size, "parallelism": f"dp{world}"},
+                       "patch": list(MM_IR) if multimodal else args.size, "parallelism": f"dp{world}",
+                       "grad_exchange": ("2-bucket all-reduce, head overlapped with g_a backward (2-phase backward)" if sync else
+                                         "1 all-reduce after backward") if world > 1 else None},
             "final_loss": round(loss, 5),
             "roofline": roof, "step_roofline": step_roof, "cpu_baseline": cpu,
         }

@@ -18,8 +18,12 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 
+gT = None
+
+
 def main():
-    from compressai.distributed import allreduce_mean_, broadcast_parameters_, init_from_env
+    global gT
+    from compressai.distributed import OverlappedAllReduce, allreduce_mean_, broadcast_parameters_, init_from_env
     from compressai.entropy_models import set_noise_source
     from compressai.losses import RateDistortionLoss
     from compressai.models import ScaleHyperprior
@@ -34,7 +38,11 @@ def main():
     net.load_state_dict(inp["state_dict"])
     net = net.to(dev).train()
     broadcast_parameters_(net)
-    opt, aux_opt = configure_optimizers(net)
+    mode = os.environ.get("CAI_DIST_MODE", "serial")
+    overlap = mode.startswith("overlap")
+    opt, aux_opt = configure_optimizers(net, tail=("g_a.",) if overlap else ())
+    head = [p for n, p in net.named_parameters() if not n.startswith("g_a.") and not n.endswith(".quantiles")]
+    sync = OverlappedAllReduce(opt.flat_grad, opt.tail_offset, net.g_a, head) if overlap else None
     b = inp["x"].shape[0] // world
     sl = slice(rank * b, (rank + 1) * b)
     x = inp["x"][sl].to(dev)
@@ -53,21 +61,46 @@ def main():
         opt.zero_grad()
         aux_opt.zero_grad()
         out = net(x)
-        crit(out, x)["loss"].backward()
+        loss = crit(out, x)["loss"]
+        if sync is None:
+            loss.backward()
+        else:
+            sync.backward_head(loss)
+
+    def exchange(replayed):
+        if sync is None:
+            allreduce_mean_(opt.flat_grad)
+            return
+        sync.reduce_head()
+        if replayed:
+            gT.replay()
+        else:
+            sync.backward_tail()
+        sync.finish()
 
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
         for _ in range(2):
             fwd_bwd()
+            exchange(False)
     torch.cuda.current_stream().wait_stream(side)
     torch.cuda.synchronize()
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
+    if mode == "overlap-eager":
+        opt.flat_grad.fill_(123.0)
         fwd_bwd()
-    opt.flat_grad.fill_(123.0)           # the replay must overwrite this
-    graph.replay()
-    allreduce_mean_(opt.flat_grad)
+        exchange(False)
+    else:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            fwd_bwd()
+        if sync is not None:
+            gT = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gT, pool=graph.pool()):
+                sync.backward_tail()
+        opt.flat_grad.fill_(123.0)           # the replay must overwrite this
+        graph.replay()
+        exchange(True)
     torch.cuda.synchronize()
     set_noise_source(None)
     if rank == 0:

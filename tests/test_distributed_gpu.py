@@ -23,7 +23,11 @@ def _port():
         return s.getsockname()[1]
 
 
-def test_world2_allreduced_flat_grad_matches_oracle(cuda, tmp_path):
+@pytest.mark.parametrize("mode", ["serial", "overlap", "overlap-eager"])
+def test_world2_allreduced_flat_grad_matches_oracle(cuda, tmp_path, mode):
+    """serial: one all-reduce after the graph replay (bench.py --serial-allreduce); overlap: the two-bucket
+    exchange of compressai.distributed.OverlappedAllReduce, the head bucket issued behind the graph's event
+    node while g_a's backward runs; overlap-eager: the same with the head bucket issued from the hook."""
     torch.manual_seed(0)
     ref = O.ScaleHyperprior(32, 48)
     x = torch.rand(4, 3, 64, 64, generator=torch.Generator().manual_seed(11))
@@ -38,7 +42,7 @@ def test_world2_allreduced_flat_grad_matches_oracle(cuda, tmp_path):
     procs = []
     for r in range(2):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=port, CAI_DIST_IN=str(inp), CAI_DIST_OUT=str(outp))
+                   MASTER_PORT=port, CAI_DIST_IN=str(inp), CAI_DIST_OUT=str(outp), CAI_DIST_MODE=mode)
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker_product.py")], env=env))
     codes = []
     for p in procs:
