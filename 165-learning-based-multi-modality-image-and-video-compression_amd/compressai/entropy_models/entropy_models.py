@@ -368,7 +368,10 @@ class GaussianConditional(EntropyModel):
         return torch.Tensor(tuple(float(s) for s in scale_table))
 
     def forward(self, inputs: torch.Tensor, scales: torch.Tensor, means: Optional[torch.Tensor] = None,
-                training: Optional[bool] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+                training: Optional[bool] = None, noise: Optional[torch.Tensor] = None
+                ) -> Tuple[torch.Tensor, torch.Tensor]:
+        """noise: the U(-1/2, 1/2) draw to use in training mode (the models' concurrent forward shares one
+        draw between g_s's input and this likelihood); None draws it here, as the reference does."""
         if training is None:
             training = self.training
         # the reference's _likelihood broadcasts scales / means against the inputs (entropy_models.py:692-709)
@@ -379,7 +382,10 @@ class GaussianConditional(EntropyModel):
                 means = means.expand_as(inputs)
         except RuntimeError as e:
             raise ValueError(f"scales / means do not broadcast to the inputs' shape {tuple(inputs.shape)}") from e
-        noise = _draw_noise(inputs) if training else None
+        if training and noise is None:
+            noise = _draw_noise(inputs)
+        elif not training:
+            noise = None
         sb = self._scale_bound_value
         return GaussianFn.apply(inputs, scales, means, noise, Q_NOISE if training else Q_DEQUANTIZE, sb,
                                 self._lik_bound())

@@ -1064,6 +1064,12 @@ int cai_gdn_backward(int dtype, const void* x, int32_t x_ld, const void* dy, int
                            reinterpret_cast<const bf16*>(dy), dy_ld, npix, reinterpret_cast<const bf16*>(gamma_op),
                            beta, reinterpret_cast<bf16*>(dx), dx_ld, part);
     };
+#ifdef CAI_GDN_WIDE128
+    if (C == 128) {
+        inverse ? launch_wide(gdn_bwd_wide_kernel<128, true>, WideGeo<128>::NT)
+                : launch_wide(gdn_bwd_wide_kernel<128, false>, WideGeo<128>::NT);
+    } else
+#endif
     if (C == 192)
         inverse ? launch_wide(gdn_bwd_wide_kernel<192, true>, WideGeo<192>::NT)
                 : launch_wide(gdn_bwd_wide_kernel<192, false>, WideGeo<192>::NT);

@@ -37,6 +37,20 @@ def relerr(a, b):
 
 @pytest.mark.parametrize("name", MODELS)
 def test_train_forward_backward_parity(cuda, name):
+    _train_parity(cuda, name)
+
+
+@pytest.mark.parametrize("stream", ["0", "1"])
+@pytest.mark.parametrize("name", ["bmshj2018-hyperprior", "mbt2018-mean", "mbt2018", "cheng2020-anchor"])
+def test_hyper_branch_stream_parity(cuda, monkeypatch, name, stream):
+    """The hyper branch serial (0) and on its own stream (1), whatever the model's default (google.py)."""
+    from compressai.models import google
+
+    monkeypatch.setattr(google, "_HYPER_STREAM", stream)
+    _train_parity(cuda, name)
+
+
+def _train_parity(cuda, name):
     from compressai.entropy_models import set_noise_source
     from compressai.losses import RateDistortionLoss
 
