@@ -60,6 +60,62 @@ def _stream() -> _VP:
     return _VP(torch.cuda.current_stream().cuda_stream)
 
 
+# ---------------------------------------------------------------------------
+# weight gradients on a side stream
+# ---------------------------------------------------------------------------
+# A conv's weight gradient feeds nothing but the optimizer, so when it lands straight in the optimizer's flat
+# buffer (direct_grad) it is launched on a per-device side stream: the input-gradient chain -- the backward's
+# critical path -- goes on without it, and inside a captured graph the two become parallel branches on two
+# hardware queues.  The side stream joins the caller's stream in an autograd final callback (as
+# DistributedDataParallel finalises its buckets), i.e. before backward() returns, so .grad reads after
+# backward see the finished values.  Off by default (CAI_WGRAD_STREAM=1 turns it on): measured on MI355X,
+# 50-step A/B x2, it costs 1.5-3.5 % on bmshj2018-hyperprior q1/q6 and mbt2018 (cheng2020-anchor even) --
+# the captured graph's cross-queue edges cost more than the overlap returns (profiles/r02_wgrad_stream_ab.log).
+# The per-launch ledger always runs in-stream.
+_WGRAD_STREAM = os.environ.get("CAI_WGRAD_STREAM", "0") == "1"
+_WSIDE = {}
+_WPENDING = set()
+
+
+def _join_wgrad(device):
+    _WPENDING.discard(device)
+    torch.cuda.current_stream(device).wait_stream(_WSIDE[device])
+
+
+class _WgradLaunch:
+    """Context for one direct weight-gradient launch: on the side stream (after the current stream's work
+    so far), with the inputs' memory kept alive for it; None-valued side when not applicable."""
+
+    def __init__(self, device, direct: bool, *inputs):
+        self.side = None
+        if not (_WGRAD_STREAM and direct and _ledger.active() is None):
+            return
+        side = _WSIDE.get(device)
+        if side is None:
+            side = _WSIDE[device] = torch.cuda.Stream(device=device)
+        self.side, self.inputs = side, inputs
+
+    def __enter__(self):
+        if self.side is not None:
+            self.side.wait_stream(torch.cuda.current_stream(self.side.device))
+            self._ctx = torch.cuda.stream(self.side)
+            self._ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.side is None:
+            return False
+        self._ctx.__exit__(*exc)
+        for t in self.inputs:
+            if t is not None:
+                t.record_stream(self.side)
+        dev = self.side.device
+        if dev not in _WPENDING:
+            _WPENDING.add(dev)
+            torch.autograd.Variable._execution_engine.queue_callback(lambda: _join_wgrad(dev))
+        return False
+
+
 def _p(t: Optional[torch.Tensor]) -> Optional[_VP]:
     return None if t is None else _VP(t.data_ptr())
 
@@ -346,11 +402,13 @@ def _edge_bwd(ctx, xs, weight, gy):
             dwt = torch.empty(weight.shape, dtype=torch.float32, device=gy.device)
             dbt = torch.empty(g.out_c, dtype=torch.float32, device=gy.device) if ctx.has_bias else None
         nbytes = lib.cai_edge_workspace_bytes(ctypes.byref(g), dcode(dt))
-        ws = torch.empty(nbytes, dtype=torch.uint8, device=gy.device)
         fl, nb = _ledger.conv_cost(g, _es(dt), 2, **({"x_bytes": 4} if ctx.edge == 1 else {"y_bytes": 4}))
-        _ledger.run(lambda: lib.cai_edge_wgrad(ctypes.byref(g), _p(img), _p(feat), fld, _p(dwt), _p(dbt), int(direct),
-                                               _p(ws), nbytes, st),
-                    "conv_wgrad", "edge_wgrad_dma_kernel (+pack, reduce)", fl, nb, dt, _ledger.shape_of(g))
+        with _WgradLaunch(gy.device, direct, img, feat):
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=gy.device)
+            sw = _stream()
+            _ledger.run(lambda: lib.cai_edge_wgrad(ctypes.byref(g), _p(img), _p(feat), fld, _p(dwt), _p(dbt),
+                                                   int(direct), _p(ws), nbytes, sw),
+                        "conv_wgrad", "edge_wgrad_dma_kernel (+pack, reduce)", fl, nb, dt, _ledger.shape_of(g))
         if not direct:
             dw = dwt if weight.dtype == torch.float32 else dwt.to(weight.dtype)
             db = dbt
@@ -463,7 +521,6 @@ class ConvFn(torch.autograd.Function):
                         "conv_dgrad", _conv_kernel(g, dt, 1), fl, nb, dt, _ledger.shape_of(g))
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             nbytes = lib.cai_conv_wgrad_workspace_bytes(ctypes.byref(g), code)
-            wws = torch.empty(nbytes, dtype=torch.uint8, device=gy.device)
             wparam, bparam = ctx.params
             direct = direct_grad(wparam) and (bparam is None or direct_grad(bparam))
             if direct:   # accumulate straight into the optimizer's flat gradient buffer
@@ -472,10 +529,13 @@ class ConvFn(torch.autograd.Function):
                 dw = torch.empty(weight.shape, dtype=torch.float32, device=gy.device)
                 db = torch.empty(g.out_c, dtype=torch.float32, device=gy.device) if ctx.has_bias else None
             fl, nb = _ledger.conv_cost(g, _es(dt), 2)
-            _ledger.run(lambda dw=dw, db=db: lib.cai_conv_wgrad(ctypes.byref(g), code, _p(xpm), ctx.xld,
-                                                                int(spec.in_abs), 0, _p(gpm), gld, _p(dw), _p(db),
-                                                                int(direct), _p(wws), nbytes, st),
-                        "conv_wgrad", _conv_kernel(g, dt, 2, spec.in_abs), fl, nb, dt, _ledger.shape_of(g))
+            with _WgradLaunch(gy.device, direct, xpm, gpm):
+                wws = torch.empty(nbytes, dtype=torch.uint8, device=gy.device)
+                sw = _stream()
+                _ledger.run(lambda dw=dw, db=db: lib.cai_conv_wgrad(ctypes.byref(g), code, _p(xpm), ctx.xld,
+                                                                    int(spec.in_abs), 0, _p(gpm), gld, _p(dw),
+                                                                    _p(db), int(direct), _p(wws), nbytes, sw),
+                            "conv_wgrad", _conv_kernel(g, dt, 2, spec.in_abs), fl, nb, dt, _ledger.shape_of(g))
             if direct:
                 dw = db = None
             elif weight.dtype != torch.float32:
