@@ -91,6 +91,11 @@ struct GdnGeo {
     static constexpr int TILE_LDS = GBM * RS;
 };
 
+// Rows past the end are stored to a sink instead of being skipped: every store is issued, so the
+// compiler's vmcnt bookkeeping never meets a path with fewer memory operations (a skipped store there
+// turns the next wait on the register prefetch into vmcnt(0), draining the prefetched tiles).
+__device__ __attribute__((aligned(64))) u32x4 cai_gdn_sink[4];
+
 template <typename T, int C>
 struct TileRegs {
     u32x4 v[GdnGeo<T, C>::CPT];
@@ -120,6 +125,32 @@ __device__ __forceinline__ void tile_load(TileRegs<T, C>& R, const T* src, int l
             r[i] = u32x4{0u, 0u, 0u, 0u};
     }
 }
+// the same with every load issued: rows past the end re-read the last pixel (the forward's rows are
+// independent; those results go to the sink)
+template <typename T, int C>
+__device__ __forceinline__ void tile_load_all(TileRegs<T, C>& R, const T* src, int ld, int64_t p0, int64_t npix) {
+    using G = GdnGeo<T, C>;
+    static_assert(G::TILE_CH % GNT == 0, "tile chunks");
+#pragma unroll
+    for (int i = 0; i < G::CPT; ++i) {
+        const int id = i * GNT + threadIdx.x;
+        const int row = id / G::CHR, ch = id - (id / G::CHR) * G::CHR;
+        const int64_t p = min(p0 + row, npix - 1);
+        R.v[i] = *reinterpret_cast<const u32x4*>(src + p * ld + ch * (16 / sizeof(T)));
+    }
+}
+template <typename T, int C>
+__device__ __forceinline__ void lds_to_global_all(const char* lds, T* dst, int ld, int64_t p0, int64_t npix) {
+    using G = GdnGeo<T, C>;
+#pragma unroll
+    for (int i = 0; i < G::CPT; ++i) {
+        const int id = i * GNT + threadIdx.x;
+        const int row = id / G::CHR, ch = id - (id / G::CHR) * G::CHR;
+        const int64_t p = p0 + row;
+        u32x4* d = p < npix ? reinterpret_cast<u32x4*>(dst + p * ld + ch * (16 / sizeof(T))) : cai_gdn_sink;
+        *d = *reinterpret_cast<const u32x4*>(lds + row * G::RS + ch * 16);
+    }
+}
 template <typename T, int C>
 __device__ __forceinline__ void tile_to_lds(const TileRegs<T, C>& R, char* lds) {
     using G = GdnGeo<T, C>;
@@ -128,7 +159,7 @@ __device__ __forceinline__ void tile_to_lds(const TileRegs<T, C>& R, char* lds) 
     for (int i = 0; i < G::CPT; ++i) {
         const int id = i * GNT + threadIdx.x;
         const int row = id / G::CHR, ch = id - (id / G::CHR) * G::CHR;
-        if (id < G::TILE_CH) *reinterpret_cast<u32x4*>(lds + row * G::RS + ch * 16) = r[i];
+        if (G::TILE_CH % GNT == 0 || id < G::TILE_CH) *reinterpret_cast<u32x4*>(lds + row * G::RS + ch * 16) = r[i];
     }
 }
 template <typename T, int C>
@@ -206,11 +237,26 @@ __global__ __launch_bounds__(GNT, (sizeof(T) == 2 && C <= 192) ? 2 : 1) void gdn
 #pragma unroll
     for (int tn = 0; tn < G::TN; ++tn) bv[tn] = beta[G::col0(wave) + tn * 16 + (lane & 15)];
 
+    // persistent blocks, two tiles in flight per block (register sets A / B), every load and store issued
+    // (clamped rows, sink stores) and a counted loop over tile pairs: the straight-line body lets each
+    // step wait for its own set only (see the fused backward below)
     const int64_t ntiles = (npix + GBM - 1) / GBM;
-    TileRegs<T, C> rx;
+    const int64_t stride = gridDim.x;
+    const int64_t last = ntiles - 1;
+    // the widest tiles keep one set (a second one would spill: C = 160+ bf16, 128+ fp32)
+    constexpr bool PAIR = sizeof(T) == 2 ? C <= 128 : C <= 96;
+    TileRegs<T, C> ra, rb;
     int64_t tile = blockIdx.x;
-    if (tile < ntiles) tile_load<T, C>(rx, x, x_ld, tile * GBM, npix);
-    for (; tile < ntiles; tile += gridDim.x) {
+    tile_load_all<T, C>(ra, x, x_ld, min(tile, last) * GBM, npix);
+#pragma unroll
+    for (int i = 0; i < G::CPT; ++i) cai_gdn_sink[1] = u32x4{0u, 0u, 0u, 0u};
+    if constexpr (PAIR) {
+        tile_load_all<T, C>(rb, x, x_ld, min(tile + stride, last) * GBM, npix);
+#pragma unroll
+        for (int i = 0; i < G::CPT; ++i) cai_gdn_sink[2] = u32x4{0u, 0u, 0u, 0u};
+    }
+    auto step = [&](TileRegs<T, C>& rx, int64_t cur, int64_t nxt) {
+        lds_barrier();                       // the previous tile's store has read lds
         tile_to_lds<T, C>(rx, lds);
         {
             TileRegs<T, C> sq;
@@ -218,9 +264,8 @@ __global__ __launch_bounds__(GNT, (sizeof(T) == 2 && C <= 192) ? 2 : 1) void gdn
             for (int i = 0; i < G::CPT; ++i) sq.v[i] = sq_chunk<T>(rx.v[i]);
             tile_to_lds<T, C>(sq, lsq);
         }
+        tile_load_all<T, C>(rx, x, x_ld, nxt * GBM, npix);
         lds_barrier();
-        const int64_t nxt = tile + gridDim.x;
-        if (nxt < ntiles) tile_load<T, C>(rx, x, x_ld, nxt * GBM, npix);
         Acc<T, C> A;
         tile_gemm<T, C>(A, lsq, fb, false, wave);
         auto& acc = A.v;
@@ -250,8 +295,17 @@ __global__ __launch_bounds__(GNT, (sizeof(T) == 2 && C <= 192) ? 2 : 1) void gdn
                     *lds_elem<T>(lds, G::RS, G::row0(wave) + tm * 16 + (lane >> 4) * 4 + r, col) = from_f32<T>(acc[tm][tn][r]);
             }
         lds_barrier();
-        lds_to_global<T, C>(lds, y, y_ld, tile * GBM, npix);
-        lds_barrier();
+        lds_to_global_all<T, C>(lds, y, y_ld, cur * GBM, npix);
+    };
+    const int64_t mine = tile < ntiles ? (ntiles - tile + stride - 1) / stride : 0;
+    if constexpr (PAIR) {
+        for (int64_t it = 0; it < mine / 2; ++it, tile += 2 * stride) {
+            step(ra, tile, min(tile + 2 * stride, last));
+            step(rb, tile + stride, min(tile + 3 * stride, last));
+        }
+        if (mine & 1) step(ra, tile, last);
+    } else {
+        for (int64_t it = 0; it < mine; ++it, tile += stride) step(ra, tile, min(tile + stride, last));
     }
 }
 
@@ -434,6 +488,19 @@ __device__ __forceinline__ void lds_to_global_rows(const char* lds, bf16* dst, i
     }
 }
 
+template <int C>
+__device__ __forceinline__ void lds_to_global_rows_all(const char* lds, bf16* dst, int ld, int64_t p0, int64_t npix) {
+    using G = FusedGeo<C>;
+    constexpr int CHR = 2 * C / 16;
+#pragma unroll
+    for (int i = 0; i < G::CPT; ++i) {
+        const int id = i * FNT + threadIdx.x;
+        const int row = id / CHR, ch = id - (id / CHR) * CHR;
+        u32x4* d = (p0 + row < npix) ? reinterpret_cast<u32x4*>(dst + (p0 + row) * ld + ch * 8) : cai_gdn_sink;
+        *d = *reinterpret_cast<const u32x4*>(lds + row * G::RS + ch * 16);
+    }
+}
+
 template <int C, bool INV>
 __global__ __launch_bounds__(FNT, 1) void gdn_bwd_fused_kernel(const bf16* __restrict__ x, int x_ld,
                                                                const bf16* __restrict__ dy, int dy_ld, int64_t npix,
@@ -469,39 +536,32 @@ __global__ __launch_bounds__(FNT, 1) void gdn_bwd_fused_kernel(const bf16* __res
     for (int t = 0; t < G::TI; ++t) dg[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     float dbeta = 0.f;
 
-    // two tiles in flight: registers set A holds tile t + 2*stride while set B
-    // waits with t + stride (the loop body alternates A / B, unrolled by hand)
+    // two tiles in flight: register set A holds tile t + 2*stride while set B waits with t + stride.  The
+    // loop body is the A step then the B step in straight-line code, every prefetch is issued (past the
+    // end it re-reads the last tile, an L2 hit) and every store too (lds_to_global_rows_all): no path with
+    // fewer memory operations, so each step waits only for its own set, not vmcnt(0).
     const int64_t ntiles = (npix + GBM - 1) / GBM;
     const int64_t stride = gridDim.x;
+    const int64_t last = ntiles - 1;
     u32x4 rxa[G::CPT], rga[G::CPT], rxb[G::CPT], rgb[G::CPT];
     int64_t tile = blockIdx.x;
-    if (tile < ntiles) {
-        ftile_load<C>(rxa, x, x_ld, tile * GBM, npix);
-        ftile_load<C>(rga, dy, dy_ld, tile * GBM, npix);
-    }
-    if (tile + stride < ntiles) {
-        ftile_load<C>(rxb, x, x_ld, (tile + stride) * GBM, npix);
-        ftile_load<C>(rgb, dy, dy_ld, (tile + stride) * GBM, npix);
-    }
-    for (int parity = 0; tile < ntiles; tile += stride, parity ^= 1) {
-        const int64_t p0 = tile * GBM;
+    // the prologue issues what a loop iteration leaves in flight: set A, CPT stores, set B, CPT stores
+    // (to the sink), so the loop's first wait is the same counted wait as the steady state's
+    ftile_load<C>(rxa, x, x_ld, min(tile, last) * GBM, npix);
+    ftile_load<C>(rga, dy, dy_ld, min(tile, last) * GBM, npix);
+#pragma unroll
+    for (int i = 0; i < G::CPT; ++i) cai_gdn_sink[1] = u32x4{0u, 0u, 0u, 0u};
+    ftile_load<C>(rxb, x, x_ld, min(tile + stride, last) * GBM, npix);
+    ftile_load<C>(rgb, dy, dy_ld, min(tile + stride, last) * GBM, npix);
+#pragma unroll
+    for (int i = 0; i < G::CPT; ++i) cai_gdn_sink[2] = u32x4{0u, 0u, 0u, 0u};
+    auto step = [&](u32x4 (&rx)[G::CPT], u32x4 (&rg)[G::CPT], int64_t cur, int64_t nxt) {
+        const int64_t p0 = cur * GBM;
         lds_barrier();                       // previous tile's dx store has read Lg
-        const int64_t nxt = tile + 2 * stride;
-        if (parity == 0) {
-            ftile_to_lds_sq<C>(rxa, Lx, Lq, p0, npix);
-            ftile_to_lds<C>(rga, Lg, p0, npix);
-            if (nxt < ntiles) {
-                ftile_load<C>(rxa, x, x_ld, nxt * GBM, npix);
-                ftile_load<C>(rga, dy, dy_ld, nxt * GBM, npix);
-            }
-        } else {
-            ftile_to_lds_sq<C>(rxb, Lx, Lq, p0, npix);
-            ftile_to_lds<C>(rgb, Lg, p0, npix);
-            if (nxt < ntiles) {
-                ftile_load<C>(rxb, x, x_ld, nxt * GBM, npix);
-                ftile_load<C>(rgb, dy, dy_ld, nxt * GBM, npix);
-            }
-        }
+        ftile_to_lds_sq<C>(rx, Lx, Lq, p0, npix);
+        ftile_to_lds<C>(rg, Lg, p0, npix);
+        ftile_load<C>(rx, x, x_ld, nxt * GBM, npix);
+        ftile_load<C>(rg, dy, dy_ld, nxt * GBM, npix);
         lds_barrier();
         const int nvalid = (int)min((int64_t)GBM, npix - p0);
         // ---- norm = x^2 gamma^T (+ beta) ----
@@ -590,8 +650,15 @@ __global__ __launch_bounds__(FNT, 1) void gdn_bwd_fused_kernel(const bf16* __res
                 *lds_elem<bf16>(Lg, G::RS, row, n0 + i16) = (bf16)(gr[tm][r] + 2.f * xr[tm][r] * acc[tm][r]);
             }
         lds_barrier();
-        lds_to_global_rows<C>(Lg, dx, dx_ld, p0, npix);
+        lds_to_global_rows_all<C>(Lg, dx, dx_ld, p0, npix);
+    };
+    // a counted loop over tile pairs (one path through the body), then the odd tile
+    const int64_t mine = tile < ntiles ? (ntiles - tile + stride - 1) / stride : 0;
+    for (int64_t it = 0; it < mine / 2; ++it, tile += 2 * stride) {
+        step(rxa, rga, tile, min(tile + 2 * stride, last));
+        step(rxb, rgb, tile + stride, min(tile + 3 * stride, last));
     }
+    if (mine & 1) step(rxa, rga, tile, last);
     // ---- partials: dbeta (lanes of one column: xor 16, 32; waves of one column block via LDS) ----
     dbeta += __shfl_xor(dbeta, 16, 64);
     dbeta += __shfl_xor(dbeta, 32, 64);
@@ -891,7 +958,9 @@ template <typename T, int C>
 static void launch_gdn_fwd(const void* x, int x_ld, int64_t npix, const void* g, const float* b, int inv, void* y,
                            int y_ld, hipStream_t st) {
     const int64_t ntiles = (npix + GBM - 1) / GBM;
-    const int grid = (int)std::min<int64_t>(ntiles, 1024);
+    // persistent: one wave of resident blocks (2 per CU where the launch bounds allow it)
+    const int occ = (sizeof(T) == 2 && C <= 192) ? 2 : 1;
+    const int grid = (int)std::min<int64_t>(ntiles, 256 * occ);
     hipLaunchKernelGGL((gdn_fwd_kernel<T, C>), dim3(grid), dim3(GNT), 0, st, reinterpret_cast<const T*>(x), x_ld, npix,
                        reinterpret_cast<const T*>(g), b, inv, reinterpret_cast<T*>(y), y_ld);
 }
