@@ -572,6 +572,167 @@ __global__ __launch_bounds__(512, 1) void conv_glds_kernel(const ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Latent-size convolutions (the hyper branch and the latent ends of g_a / g_s: 4x4 .. 16x16 latents at the
+// training batch): the whole K reduction in ONE launch, no split-K partial slabs and no reduce launch.
+// These GEMMs have M = B*H*W of a few hundred to a few thousand rows against K = taps*Cin = 1-3 thousand:
+// a tile grid cannot fill the chip, and the split-K path paid a second launch for the combine.  Here a
+// block owns a small BM x BN output tile (16..32 x 32..64) and its 8 waves split K eight ways inside the
+// block; each wave loads its MFMA fragments straight from global memory into registers (no operand is
+// shared between the waves, so there is nothing to stage in LDS), D K-steps ahead, every load issued as
+// a buffer load whose out-of-range lanes (padding taps, rows past M, K-steps past the wave's range) carry
+// an offset beyond the buffer and read 0 -- no branch around any load, so the compiler's counted waits
+// never see a shorter path.  The 8 partial tiles meet in LDS and are summed in wave order (deterministic), then the usual
+// epilogue (bias, ReLU / LeakyReLU, gradient mask, 16-byte stores).  Gather and phase modes as above;
+// K steps of 32 channels inside one tap (Cin_pad % 32 == 0), bf16, |x| on load for h_a's first conv.
+// ---------------------------------------------------------------------------
+constexpr int SMALL_NW = 8, SMALL_D = 4;
+
+template <int RT, int CT>
+struct SmallCfg {
+    static constexpr int BM = 16 * RT, BN = 16 * CT, ES = BN + 4;
+    static constexpr int BYTES = SMALL_NW * BM * ES * 4;
+};
+
+template <int RT, int CT>
+__global__ __launch_bounds__(512, 1) void conv_small_kernel(const ConvArgs a) {
+    using SC = SmallCfg<RT, CT>;
+    constexpr int BM = SC::BM, BN = SC::BN, ES = SC::ES, D = SMALL_D;
+    __shared__ __attribute__((aligned(16))) float red[SMALL_NW * BM * ES];
+
+    const int ph = blockIdx.z;
+    const PhaseDesc P = ph == 0 ? a.ph[0] : (ph == 1 ? a.ph[1] : (ph == 2 ? a.ph[2] : a.ph[3]));
+    const int plane = P.OHg * P.OWg;
+    const int Mph = a.B * plane;
+    const int m0 = blockIdx.x * BM;
+    if (m0 >= Mph) return;
+    const int n0 = blockIdx.y * BN;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int kq = 8 * (lane >> 4);               // this lane's 8 K elements of a 32-wide step
+
+    constexpr unsigned OOB = 0x80000000u;          // beyond every buffer: the load returns 0
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<void*>(a.x), (short)0, (int)((int64_t)a.B * a.IH * a.IW * a.x_ld * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<void*>(a.w), (short)0, (int)((int64_t)a.nphase * a.Npad * a.Kp * 2), 0x00020000);
+    int abase[RT];                                 // element offsets (inputs < 2 GiB: checked by run_conv)
+    int ay[RT], ax[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+        const int m = m0 + rt * 16 + (lane & 15);
+        if (m < Mph) {
+            const int b = m / plane;
+            const int r = m - b * plane;
+            const int j = r / P.OWg;
+            ay[rt] = j * a.row_stride;
+            ax[rt] = (r - j * P.OWg) * a.row_stride;
+            abase[rt] = ((b * a.IH + ay[rt]) * a.IW + ax[rt]) * a.x_ld + kq;
+        } else {
+            ay[rt] = -(1 << 28);
+            ax[rt] = 0;
+            abase[rt] = 0;
+        }
+    }
+    int boff[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+        const int n = n0 + ct * 16 + (lane & 15);
+        boff[ct] = n < a.Npad ? (int)P.w_off + n * a.Kp + kq : -1;
+    }
+    // this wave's K steps: [k0, k0 + per), padded to whole groups of D (the padding reads the zero page)
+    const int nk = P.K / 32;
+    const int per = (nk + SMALL_NW - 1) / SMALL_NW;
+    const int k0 = wave * per, k1 = min(nk, k0 + per);
+    const int ngroups = (per + D - 1) / D;
+
+    auto load = [&](int ks, u32x4 (&fa)[RT], u32x4 (&fb)[CT]) {
+        const bool kok = ks < k1;
+        const int kg = ks * 32;
+        const int t = kg / a.Cin_pad;
+        const int ci0 = kg - t * a.Cin_pad;
+        const int ty = t / P.ntx;
+        const int dy = P.dy0 + a.tap_sy * ty, dx = P.dx0 + a.tap_sx * (t - ty * P.ntx);
+        const int delta = (dy * a.IW + dx) * a.x_ld + ci0;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            // bitwise tests and an unconditional offset: a short-circuit && here becomes a branch
+            const int iy = ay[rt] + dy, ix = ax[rt] + dx;
+            const bool ok = kok & ((unsigned)iy < (unsigned)a.IH) & ((unsigned)ix < (unsigned)a.IW);
+            const unsigned off = (unsigned)(abase[rt] + delta) * 2u;
+            fa[rt] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? off : OOB, 0, 0));
+        }
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+            const unsigned off = (unsigned)(boff[ct] + kg) * 2u;
+            const bool ok = kok & (boff[ct] >= 0);
+            fb[ct] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, ok ? off : OOB, 0, 0));
+        }
+    };
+
+    f32x4 acc[RT][CT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) acc[rt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+    u32x4 fa[D][RT], fb[D][CT];
+#pragma unroll
+    for (int d = 0; d < D; ++d) load(k0 + d, fa[d], fb[d]);
+    for (int g = 0; g < ngroups; ++g) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            u32x4 ca[RT], cb[CT];
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) ca[rt] = a.in_abs ? abs_chunk(fa[d][rt], 2) : fa[d][rt];
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) cb[ct] = fb[d][ct];
+            load(k0 + (g + 1) * D + d, fa[d], fb[d]);
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int ct = 0; ct < CT; ++ct) acc[rt][ct] = mma16<bf16>(ca[rt], cb[ct], acc[rt][ct]);
+        }
+    }
+    // the 8 partial tiles -> LDS, summed in wave order by the epilogue threads
+    float* mine = red + wave * BM * ES;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) mine[(rt * 16 + (lane >> 4) * 4 + r) * ES + ct * 16 + (lane & 15)] = acc[rt][ct][r];
+    __syncthreads();
+    const int VO = a.y_dtype == CAI_BF16 ? 8 : 4;
+    const int cpr = BN / VO;
+    for (int id = tid; id < BM * cpr; id += 512) {
+        const int row = id / cpr, cc = id - (id / cpr) * cpr;
+        const int m = m0 + row, nb = n0 + cc * VO;
+        if (m >= Mph || nb >= a.Cout) continue;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = 0.f;
+#pragma unroll
+        for (int w = 0; w < SMALL_NW; ++w) {
+            const float* src = red + (w * BM + row) * ES + cc * VO;
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                if (e < VO) v[e] += src[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int n = nb + e;
+            const float bv = (a.bias && e < VO && n < a.Cout) ? a.bias[n] : 0.f;
+            v[e] = apply_act(v[e] + bv, a.act, a.act_param);
+        }
+        if (a.y_vec) {
+            store_out_chunk<bf16>(a, P, plane, m, nb, v, VO);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                if (e < VO && nb + e < a.Cout) store_out_scalar<bf16>(a, P, plane, m, nb + e, v[e]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Halo-staged implicit GEMM for the stride-2 gather convolutions (Conv2d k3/k5 s2 p=k/2 forward and the
 // matching ConvTranspose2d input gradient), bf16.  The tap-gather kernel above fetches every input pixel
 // once per tap (25 times for k5), and its speed is set by how fast a CU can pull bytes into LDS, not by
@@ -1549,6 +1710,235 @@ __global__ __launch_bounds__(NT, 2) void wgrad_kernel(const WgradArgs a) {
         }
 }
 
+// ---------------------------------------------------------------------------
+// Latent-size weight gradients (M = B*H*W <= 1024 G pixels: the hyper branch's 4x4 / 8x8 latents): one
+// launch writing dW (and the bias gradient) in torch layout -- no pixel-split partial
+// slabs and no reduce launch.  dW has few rows of K here (a few thousand pixels) but many output columns
+// (taps x channels), so the output is tiled finely instead: a block owns 64 G channels x 64 X columns of
+// one tap, and its 8 waves split the pixels eight ways.  Per 32-pixel step a wave stages its own G and X
+// tiles ([32 px][64 ch] bf16, XOR-swizzled 16-byte slots) in a private LDS region -- no block barrier in
+// the loop -- and reads the MFMA fragments (pixels as K) with ds_read_b64_tr_b16, the next step's loads
+// already in flight (two register sets; buffer loads: padding taps and pixels past M read 0).  The 8
+// partial tiles are summed in wave order in LDS (deterministic).  Bias gradient: Conv2d's is the column
+// sums of G, accumulated by the (tap 0, q 0) blocks from the chunks they stage; ConvTranspose2d's (column
+// sums of dy = X, 4x the pixels) is taken by trailing blocks (blockIdx.x == ncb), 64 channels each.
+// ---------------------------------------------------------------------------
+struct SwArgs {
+    const void* g;
+    int g_ld, Ng;
+    const void* x;
+    int x_ld, Cq, Cq_pad, in_abs, in_sq;
+    int B, Hg, Wg, Hx, Wx, k, s, p;
+    int M;            // G pixels
+    int ncb;          // 64-wide column blocks: k*k*Cq_pad / 64
+    float* dw;
+    int accumulate;
+    const void* bsrc; // bias: column sums of bsrc [bnpix][bc] (ld bsrc_ld) -> db; db == NULL: none
+    int bsrc_ld, bnpix, bc;
+    float* db;
+    int bias_from_g;  // Conv2d: db = column sums of G, taken by the main blocks; else by trailing blocks
+};
+
+constexpr int SW_NW = 8, SW_STEPS = 4;   // waves; 32-pixel steps per wave (M <= SW_NW * SW_STEPS * 32)
+// 16-byte slot swizzle of a [32][128 B] tile read by ds_read_b64_tr_b16: the 8 rows one half-wave reads
+// (4 per 16-lane group, groups 8 rows apart) land on distinct bank groups
+__device__ __forceinline__ int swz_sw(int row, int slot) {
+    return row * 128 + ((slot ^ ((((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2))) << 4);
+}
+
+template <int XT>   // X transform on load: 0 none, 1 |x| (h_a's first conv), 2 x^2 (GDN's gamma gradient)
+__global__ __launch_bounds__(512, 1) void wgrad_small_kernel(const SwArgs a) {
+    // 8 x (64 x 68 fp32) partial tiles (the loop's staging uses the first 64 KB) + 512 x 8 bias partials
+    __shared__ __attribute__((aligned(16))) char smem[SW_NW * 64 * 68 * 4 + 512 * 8 * 4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr unsigned OOB = 0x80000000u;
+    if ((int)blockIdx.x == a.ncb) {
+        // bias: 64 channels per block, pixels over 64 row groups of 8 threads (8 channels each)
+        if (!a.db || a.bias_from_g) return;
+        float* red = reinterpret_cast<float*>(smem);
+        const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<void*>(a.bsrc), (short)0, (int)((int64_t)a.bnpix * a.bsrc_ld * 2), 0x00020000);
+        for (int c0 = blockIdx.y * 64; c0 < a.bc; c0 += gridDim.y * 64) {
+            const int slot = tid & 7, r = tid >> 3;
+            const int c = c0 + slot * 8;
+            float sacc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            // 8 rows (512 pixels apart) per batch, all loads issued before the adds
+            for (int pb = r; pb < a.bnpix; pb += 512) {
+                u32x4 v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int pp = pb + u * 64;
+                    const unsigned off = (unsigned)(pp * a.bsrc_ld + c) * 2u;
+                    v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                          br, ((pp < a.bnpix) & (c < a.bc)) ? off : OOB, 0, 0));
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const bf16x8 h = __builtin_bit_cast(bf16x8, v[u]);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) sacc[e] += (float)h[e];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < 8; ++e) red[r * 64 + slot * 8 + e] = sacc[e];
+            __syncthreads();
+            if (tid < 64 && c0 + tid < a.bc) {
+                float v = 0.f;
+                for (int rr = 0; rr < 64; ++rr) v += red[rr * 64 + tid];
+                float* d = a.db + c0 + tid;
+                *d = a.accumulate ? *d + v : v;
+            }
+        }
+        return;
+    }
+    const int n0 = blockIdx.y * 64;
+    const int col0 = blockIdx.x * 64;
+    const int t = col0 / a.Cq_pad, q0 = col0 - t * a.Cq_pad;
+    const int kh = t / a.k, kw = t - kh * a.k;
+    const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<void*>(a.g), (short)0, (int)((int64_t)a.M * a.g_ld * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<void*>(a.x), (short)0, (int)((int64_t)a.B * a.Hx * a.Wx * a.x_ld * 2), 0x00020000);
+    char* const Gs = smem + wave * 8192;
+    char* const Xs = Gs + 4096;
+    const int nsteps = (a.M + 31) / 32;
+    const int per = (nsteps + SW_NW - 1) / SW_NW;
+    const int s0 = wave * per, s1 = min(nsteps, s0 + per);
+    const int plane = a.Hg * a.Wg;
+    const int slot = lane & 7;
+    // Conv2d: the bias gradient is the column sums of G -- taken by the (tap 0, q 0) blocks from the G
+    // chunks they stage anyway (the pixel rows each thread loads: 8 channels, summed over its rows)
+    const bool gsum = a.db && a.bias_from_g && t == 0 && q0 == 0;
+    const float gsf = gsum ? 1.f : 0.f;
+    float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    u32x4 rga[4], rxa[4], rgb[4], rxb[4];
+    auto load = [&](int st, u32x4 (&rg)[4], u32x4 (&rx)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = i * 8 + (lane >> 3);
+            const int m = st * 32 + row;
+            const bool okm = (st < s1) & (m < a.M);
+            const unsigned goff = (unsigned)(m * a.g_ld + n0 + slot * 8) * 2u;
+            rg[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(gr, okm ? goff : OOB, 0, 0));
+            const int b = m / plane;
+            const int r = m - b * plane;
+            const int j = r / a.Wg;
+            const int iy = j * a.s - a.p + kh, ix = (r - j * a.Wg) * a.s - a.p + kw;
+            const bool okx = okm & ((unsigned)iy < (unsigned)a.Hx) & ((unsigned)ix < (unsigned)a.Wx);
+            const unsigned xoff = (unsigned)(((b * a.Hx + iy) * a.Wx + ix) * a.x_ld + q0 + slot * 8) * 2u;
+            rx[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, okx ? xoff : OOB, 0, 0));
+        }
+    };
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int g_ = lane >> 4, i16 = lane & 15, q_ = i16 >> 2, p4 = i16 & 3;
+    const int r0 = 8 * g_ + q_;
+    // two steps in flight (register sets A / B, straight-line pair loop; steps past s1 read zeros)
+    load(s0, rga, rxa);
+    load(s0 + 1, rgb, rxb);
+    auto step = [&](int st, u32x4 (&rg)[4], u32x4 (&rx)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = i * 8 + (lane >> 3);
+            u32x4 xv = rx[i];
+            if constexpr (XT == 1) xv = abs_chunk(xv, 2);
+            if constexpr (XT == 2) xv = sq_chunk<bf16>(xv);
+            *reinterpret_cast<u32x4*>(Gs + swz_sw(row, slot)) = rg[i];
+            *reinterpret_cast<u32x4*>(Xs + swz_sw(row, slot)) = xv;
+            // branch-free (a branch here costs the counted waits): scaled by 0 outside the bias blocks
+            const bf16x8 h = __builtin_bit_cast(bf16x8, rg[i]);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) bsum[e] += gsf * (float)h[e];
+        }
+        load(st + 2, rg, rx);
+        u32x4 fb[4];
+#pragma unroll
+        for (int tn = 0; tn < 4; ++tn) {
+            const int c = tn * 16 + 4 * p4;
+            const s16x4 b0 = ds_tr16(Xs, swz_sw(r0, c >> 3) + ((c & 7) << 1));
+            const s16x4 b1 = ds_tr16(Xs, swz_sw(r0 + 4, c >> 3) + ((c & 7) << 1));
+            const s16x8 bv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+            fb[tn] = __builtin_bit_cast(u32x4, bv);
+        }
+#pragma unroll
+        for (int tm = 0; tm < 4; ++tm) {
+            const int c = tm * 16 + 4 * p4;
+            const s16x4 a0 = ds_tr16(Gs, swz_sw(r0, c >> 3) + ((c & 7) << 1));
+            const s16x4 a1 = ds_tr16(Gs, swz_sw(r0 + 4, c >> 3) + ((c & 7) << 1));
+            const s16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+            const u32x4 fa = __builtin_bit_cast(u32x4, av);
+#pragma unroll
+            for (int tn = 0; tn < 4; ++tn) acc[tm][tn] = mma16<bf16>(fa, fb[tn], acc[tm][tn]);
+        }
+    };
+    // M <= 1024 (host check): at most SW_STEPS steps per wave, straight-line code (no loop-carried
+    // register sets, whose back-edge copies would wait for the prefetch); steps past s1 multiply zeros
+    static_assert(SW_STEPS % 2 == 0, "pairs");
+#pragma unroll
+    for (int it = 0; it < SW_STEPS / 2; ++it) {
+        step(s0 + 2 * it, rga, rxa);
+        step(s0 + 2 * it + 1, rgb, rxb);
+    }
+    // partial tiles: wave w -> fp32 [64][68] at w * 17 KB (the staging regions are dead past this barrier)
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);
+    float* mine = red + wave * 64 * 68;
+#pragma unroll
+    for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < 4; ++tn)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) mine[(tm * 16 + (lane >> 4) * 4 + r) * 68 + tn * 16 + (lane & 15)] = acc[tm][tn][r];
+    __syncthreads();
+    float* bred = red + SW_NW * 64 * 68;
+    if (gsum) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bred[tid * 8 + e] = bsum[e];
+    }
+    __syncthreads();
+    if (gsum && tid < 64 && n0 + tid < a.Ng) {
+        // channel n0 + tid: slot tid / 8, element tid % 8, summed over (wave, row group) in fixed order
+        float v = 0.f;
+        for (int w = 0; w < SW_NW; ++w)
+#pragma unroll
+            for (int lr = 0; lr < 8; ++lr) v += bred[(w * 64 + lr * 8 + (tid >> 3)) * 8 + (tid & 7)];
+        float* d = a.db + n0 + tid;
+        *d = a.accumulate ? *d + v : v;
+    }
+    // torch layout dw[n][q][kh][kw]: 8 elements per thread, their old values (accumulate) loaded together
+    // before any store -- one dependent round trip instead of eight
+    const int kk = a.k * a.k;
+    float v[8];
+    float* d[8];
+    bool ok[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        const int id = u * 512 + tid;
+        const int nl = id >> 6, ql = id & 63;
+        const int n = n0 + nl, q = q0 + ql;
+        ok[u] = n < a.Ng && q < a.Cq;
+        d[u] = a.dw + ((int64_t)(ok[u] ? n : 0) * a.Cq + (ok[u] ? q : 0)) * kk + t;
+        float s_ = 0.f;
+#pragma unroll
+        for (int w = 0; w < SW_NW; ++w) s_ += red[(w * 64 + nl) * 68 + ql];
+        v[u] = s_;
+    }
+    if (a.accumulate) {
+        float old[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) old[u] = *d[u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] += old[u];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+        if (ok[u]) *d[u] = v[u];
+}
+
 // dw[n][q][kh][kw] (+)= sum_s ws[s][n][(kh*k+kw)*Cq_pad + q]
 // Block = 16 float4 column groups x 16 split groups: reads walk the slabs in
 // memory order (256-byte runs), the 16 split partials meet in LDS in a fixed
@@ -2323,8 +2713,33 @@ struct ConvLaunch {
     bool glds;
     int halo, tiles_x, tiles_y;    // halo: kernel size of the halo-staged path (0: not taken)
     bool halo_ph;                  // the halo-staged s^2-phase path (k5 s2 p2 transposed direction)
+    int small;                     // conv_small_kernel tile (SMALL_*; 0: not taken)
     size_t ws_bytes;
 };
+
+// latent-size problems: conv_small_kernel instead of split-K + reduce (A/B knob CAI_SMALL_CONV_OFF)
+enum { SMALL_NONE = 0, SMALL_16x32, SMALL_32x32, SMALL_32x64 };
+static bool small_off() {
+    static const bool off = [] {
+        const char* e = getenv("CAI_SMALL_CONV_OFF");
+        return e && *e && *e != '0';
+    }();
+    return off;
+}
+// Taken where it measured faster than split-K + reduce on MI355X (B=16 hyperprior, per-launch trace):
+// M <= 512 rows (4x4 latents), or K <= 2048 with either <= 256 blocks or M <= 1024 (h_a[0] k3 192->128 at
+// 16x16: 16.4 vs 22.8 us; h_s[0] 4->8: 9.3 vs 15.5).  At K = 3200 with M >= 1024 the per-wave K loop is
+// latency-bound and the small tiles re-read the weights too often (g_a[6] 48.9 vs 22.6 us): split-K stays.
+static int pick_small(const Plan& P, int dtype, int mmax, int big_ksplit) {
+    if (small_off() || dtype != CAI_BF16 || P.Cin_pad % 32 != 0 || big_ksplit <= 1 || mmax > 8192) return SMALL_NONE;
+    int kmax = 0;
+    for (int ph = 0; ph < P.nphase; ++ph) kmax = std::max(kmax, P.ntaps[ph] * P.Cin_pad);
+    const int cfg = mmax <= 512 ? SMALL_16x32 : (mmax <= 2048 ? SMALL_32x32 : SMALL_32x64);
+    static const int bm[] = {0, 16, 32, 32}, bn[] = {0, 32, 32, 64};
+    const int blocks = (mmax + bm[cfg] - 1) / bm[cfg] * ((P.kout_c + bn[cfg] - 1) / bn[cfg]) * P.nphase;
+    if (mmax <= 512 || (kmax <= 2048 && (blocks <= 256 || mmax <= 1024))) return cfg;
+    return SMALL_NONE;
+}
 
 // the halo-staged kernel: stride-2 gather convolutions with k in {3, 5}, pad k/2, <= 128 output channels
 static bool halo_off() {
@@ -2423,6 +2838,15 @@ static ConvLaunch conv_launch(const cai_conv_geom* g, int dtype, int direction, 
     const int target = L.glds ? 256 : 512;    // one 512-thread block per CU vs two 256-thread ones
     if (tiles < 256) ks = std::min({(target + tiles - 1) / tiles, std::max(1, nk / 4), 16});
     L.ksplit = capped(std::max(1, ks));
+    L.small = pick_small(P, dtype, L.mmax, L.ksplit);
+    if (L.small) {
+        static const int bm[] = {0, 16, 32, 32}, bn[] = {0, 32, 32, 64};
+        L.BM = bm[L.small];
+        L.BN = bn[L.small];
+        L.mtiles = (L.mmax + L.BM - 1) / L.BM;
+        L.ntiles = (P.kout_c + L.BN - 1) / L.BN;
+        L.ksplit = 1;
+    }
     L.ws_ld = L.ntiles * L.BN;
     L.ws_bytes = L.ksplit > 1 ? (size_t)P.nphase * L.ksplit * L.mmax * L.ws_ld * sizeof(float) : 0;
     return L;
@@ -2477,9 +2901,23 @@ static void launch_conv_halo_phase(const ConvArgs& a, const ConvLaunch& L, hipSt
     }
 }
 
+static void launch_conv_small(const ConvArgs& a, const ConvLaunch& L, hipStream_t st) {
+    const dim3 grid(L.mtiles, L.ntiles, a.nphase);
+    if (L.small == SMALL_16x32)
+        hipLaunchKernelGGL((conv_small_kernel<1, 2>), grid, dim3(512), 0, st, a);
+    else if (L.small == SMALL_32x32)
+        hipLaunchKernelGGL((conv_small_kernel<2, 2>), grid, dim3(512), 0, st, a);
+    else
+        hipLaunchKernelGGL((conv_small_kernel<2, 4>), grid, dim3(512), 0, st, a);
+}
+
 template <typename T>
 static void dispatch_conv(const ConvArgs& a, const ConvLaunch& L, hipStream_t st) {
     if constexpr (sizeof(T) == 2) {
+        if (L.small) {
+            launch_conv_small(a, L, st);
+            return;
+        }
         if (L.halo) {
             launch_conv_halo(a, L, st);
             return;
@@ -2669,6 +3107,22 @@ static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype, bool glds, b
     return W;
 }
 
+// the latent-size weight-gradient kernel: bf16, <= 1024 G pixels (8x8 latents at B = 16; at 4096 the
+// pixel-split glds kernel + reduce measured faster: 21-34 vs 31-75 us), 64-channel tiles on both sides
+static bool small_wgrad_off() {
+    static const bool off = [] {
+        const char* e = getenv("CAI_SMALL_WGRAD_OFF");
+        return e && *e && *e != '0';
+    }();
+    return off;
+}
+static bool small_wgrad_ok(const cai_conv_geom* g, int dtype) {
+    const WgradPlan W = make_wgrad_plan(g, dtype, true);
+    return !small_wgrad_off() && dtype == CAI_BF16 && W.M <= SW_NW * SW_STEPS * 32 && W.Ng % 64 == 0 &&
+           W.Cq_pad % 64 == 0;
+}
+
+
 template <typename T>
 static void launch_colsum(const void* g, int64_t npix, int C, int ld, int nchunk, int64_t chunk, float* part,
                           float* out, int accumulate, hipStream_t st) {
@@ -2852,6 +3306,7 @@ int cai_conv_dgrad(const cai_conv_geom* g, int dtype, const void* dy, int32_t dy
 const char* cai_conv_kernel_name(const cai_conv_geom* g, int dtype, int direction, int32_t in_abs) {
     if (check_geom(g) || (dtype != CAI_BF16 && dtype != CAI_F32) || direction < 0 || direction > 2) return "";
     if (direction == 2) {
+        if (small_wgrad_ok(g, dtype)) return "wgrad_small_kernel";
         const WgradPlan W = make_wgrad_plan(g, dtype, true, in_abs != 0);
         if (!W.glds) return dtype == CAI_BF16 ? "wgrad_kernel<bf16>" : "wgrad_kernel<float>";
         if (W.halo) return W.halo == 5 ? "wgrad_halo_kernel<5>" : "wgrad_halo_kernel<3>";
@@ -2860,6 +3315,8 @@ const char* cai_conv_kernel_name(const cai_conv_geom* g, int dtype, int directio
     const ConvLaunch L = conv_launch(g, dtype, direction, in_abs);
     if (L.halo) return L.halo == 5 ? "conv_halo_kernel<5>" : "conv_halo_kernel<3>";
     if (L.halo_ph) return "conv_halo_phase_kernel";
+    if (L.small) return L.small == SMALL_16x32 ? "conv_small_kernel<16x32>"
+                        : (L.small == SMALL_32x32 ? "conv_small_kernel<32x32>" : "conv_small_kernel<32x64>");
     switch (L.cfg) {
         case CFG_G1: return "conv_glds_kernel<256x128>";
         case CFG_G2: return "conv_glds_kernel<128x192>";
@@ -2923,6 +3380,28 @@ int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_l
     a.grp_len = W.grp_len;
     a.chunk = W.px_chunk;
     hipStream_t st = as_stream(stream);
+    if (small_wgrad_ok(g, dtype)) {
+        SwArgs sa{};
+        sa.g = a.g; sa.g_ld = a.g_ld; sa.Ng = W.Ng;
+        sa.x = a.x; sa.x_ld = a.x_ld; sa.Cq = W.Cq; sa.Cq_pad = W.Cq_pad; sa.in_abs = a.in_abs; sa.in_sq = a.in_sq;
+        sa.B = g->batch; sa.Hg = a.Hg; sa.Wg = a.Wg; sa.Hx = a.Hx; sa.Wx = a.Wx;
+        sa.k = g->kernel; sa.s = g->stride; sa.p = g->pad;
+        sa.M = (int)W.M; sa.ncb = W.ncols / 64;
+        sa.dw = dw; sa.accumulate = accumulate;
+        sa.bsrc = dy; sa.bsrc_ld = dy_ld; sa.bnpix = g->batch * g->out_h * g->out_w; sa.bc = g->out_c; sa.db = db;
+        sa.bias_from_g = !g->transposed;
+        CAI_CHECK_ARG((int64_t)sa.bnpix * dy_ld * 2 < (1ll << 31) && (int64_t)a.B * a.Hx * a.Wx * a.x_ld * 2 < (1ll << 31),
+                      "conv_wgrad: operand larger than 2 GiB");
+        const dim3 grid(sa.ncb + ((db && g->transposed) ? 1 : 0), W.Ng / 64);
+        if (sa.in_abs)
+            hipLaunchKernelGGL(wgrad_small_kernel<1>, grid, dim3(512), 0, st, sa);
+        else if (sa.in_sq)
+            hipLaunchKernelGGL(wgrad_small_kernel<2>, grid, dim3(512), 0, st, sa);
+        else
+            hipLaunchKernelGGL(wgrad_small_kernel<0>, grid, dim3(512), 0, st, sa);
+        CAI_LAUNCH_CHECK("conv_wgrad");
+        return CAI_OK;
+    }
     float* bws = nullptr;
     if (W.glds) {
         a.ctiles = (W.ncols + W.ct - 1) / W.ct;

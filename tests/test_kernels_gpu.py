@@ -75,6 +75,17 @@ CONV_CASES = [
     ("conv", 1, 64, 192, 20, 128, 5, 2),
     ("deconv", 1, 64, 128, 6, 64, 3, 2),
     ("deconv", 2, 128, 64, 5, 64, 5, 2),
+    # latent-size convs at the training batch (conv_small_kernel: one launch, 8-wave in-block split-K):
+    # h_a / h_s / the latent ends of g_a and g_s, all three tile shapes, phase mode, 192 channels
+    ("conv", 16, 128, 128, 16, 16, 5, 2),
+    ("conv", 16, 128, 128, 8, 8, 5, 2),
+    ("deconv", 16, 128, 128, 4, 4, 5, 2),
+    ("deconv", 16, 128, 128, 8, 8, 5, 2),
+    ("conv", 16, 192, 128, 16, 16, 3, 1),
+    ("conv", 16, 128, 192, 16, 16, 3, 1),
+    ("conv", 16, 128, 192, 32, 32, 5, 2),
+    ("deconv", 16, 192, 128, 16, 16, 5, 2),
+    ("conv", 3, 96, 40, 6, 10, 3, 1),
     # Spatial_aligner patch embedding / recovery (master.py:708-724): kernel = stride = 2, no padding
     ("conv", 2, 64, 96, 32, 24, 2, 2, 0, 0),
     ("conv", 2, 3, 96, 16, 16, 2, 2, 0, 0),
@@ -141,25 +152,31 @@ def test_fused_conv_act_chain(cuda, act):
         assert relerr(a.grad, b.grad) < FP32_TOL
 
 
-def test_abs_input_fusion(cuda):
-    """h_a(|y|): abs on the operand load, sign mask in the dgrad epilogue."""
+@pytest.mark.parametrize("shape", [(2, 64, 32, 8), (16, 192, 128, 16)], ids=["fp32-8x8", "bf16-latent16x16"])
+def test_abs_input_fusion(cuda, shape):
+    """h_a(|y|): abs on the operand load, sign mask in the dgrad epilogue.  The second shape is the
+    hyperprior's h_a[0] at the training batch in bf16 (conv_small_kernel with |x| on load)."""
     from compressai.layers import Conv2d, Sequential
 
+    B, cin, cout, H = shape
+    bf16 = B == 16
     torch.manual_seed(2)
-    ref = nn.Sequential(nn.Conv2d(64, 32, 3, padding=1))
-    mod = Sequential(Conv2d(64, 32, 3, padding=1))
+    ref = nn.Sequential(nn.Conv2d(cin, cout, 3, padding=1))
+    mod = Sequential(Conv2d(cin, cout, 3, padding=1))
     mod.load_state_dict(ref.state_dict())
     mod = mod.to(cuda)
-    x = torch.randn(2, 64, 8, 8)
+    x = torch.randn(B, cin, H, H)
     xr = x.clone().requires_grad_()
     yr = ref(torch.abs(xr))
     g = torch.randn_like(yr)
     yr.backward(g)
     xd = x.to(cuda).requires_grad_()
-    y = mod(xd, input_abs=True)
+    with _autocast(bf16):
+        y = mod(xd, input_abs=True)
     y.backward(g.to(cuda))
-    assert relerr(y, yr) < FP32_TOL
-    assert relerr(xd.grad, xr.grad) < FP32_TOL
+    tol = BF16_TOL if bf16 else FP32_TOL
+    assert relerr(y, yr) < tol
+    assert relerr(xd.grad, xr.grad) < tol
 
 
 @pytest.mark.parametrize("bf16", [False, True])
