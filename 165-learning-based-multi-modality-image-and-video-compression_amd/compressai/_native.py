@@ -19,6 +19,8 @@ F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_LEAKY = 0, 1, 2
 MASK_NONE, MASK_POS, MASK_LEAKY, MASK_SIGN = 0, 1, 2, 3
 Q_NOISE, Q_DEQUANTIZE, Q_SYMBOLS = 0, 1, 2
+ADAM_CLIP, ADAM_SKIP_NONFINITE = 1, 2          # cai_adam_step flags (include/cai.h)
+ADAM_SMALL_N = 1 << 16                         # cai_adam_step: one-block path at or below this many parameters
 
 
 class ConvGeom(Structure):
@@ -137,6 +139,8 @@ SIGNATURES = {
     "cai_sqdiff_bwd": (_I, [_P, _P, _I64, _P, _F, _P, _P]),
     "cai_sqnorm": (_I, [_P, _I64, _P, _P, _S, _P]),
     "cai_adam": (_I, [_P, _P, _P, _P, _I64, _F, _F, _F, _F, _P, _P, _F, _P]),
+    "cai_adam_step_workspace_bytes": (c_size_t, [_I64]),
+    "cai_adam_step": (_I, [_P, _P, _P, _P, _I64, _F, _F, _F, _F, _P, _P, _F, c_int32, _P, c_size_t, _P]),
     "cai_act_bwd": (_I, [_I, _F, _P, c_int32, _P, c_int32, _P, c_int32, _I64, c_int32, _I, _P]),
     "cai_cast": (_I, [_P, _I, _P, _I, _I64, _P]),
 }

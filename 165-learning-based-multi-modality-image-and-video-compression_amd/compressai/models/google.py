@@ -97,7 +97,15 @@ class CompressionModel(nn.Module):
             warnings.warn("init_weights was removed as it was never functional", DeprecationWarning)
 
     def aux_loss(self):
-        return sum(m.loss() for m in self.modules() if isinstance(m, EntropyBottleneck))
+        # the reference's sum(...) (google.py:79-86) without its int 0 start value: 0 + loss is one more
+        # device launch per step; the same value (a lone module's loss itself)
+        losses = [m.loss() for m in self.modules() if isinstance(m, EntropyBottleneck)]
+        if not losses:
+            return 0
+        total = losses[0]
+        for extra in losses[1:]:
+            total = total + extra
+        return total
 
     def forward(self, *args):
         raise NotImplementedError()

@@ -30,7 +30,7 @@ from typing import Iterable, List, Optional, Tuple
 import torch
 
 from . import _ledger
-from ._native import lib
+from ._native import ADAM_CLIP, ADAM_SKIP_NONFINITE, ADAM_SMALL_N, lib
 from ._ops import DIRECT_GRAD_ATTR, _p, _stream
 
 
@@ -81,7 +81,8 @@ class FusedAdam(torch.optim.Optimizer):
         self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=dev)
         self.step_count = torch.zeros(1, dtype=torch.float32, device=dev)
         self.sqnorm = torch.zeros(1, dtype=torch.float32, device=dev)
-        self._ws = torch.empty(lib.cai_reduce_workspace_bytes(n), dtype=torch.uint8, device=dev)
+        self._ws = torch.empty(max(lib.cai_reduce_workspace_bytes(n), lib.cai_adam_step_workspace_bytes(n)),
+                               dtype=torch.uint8, device=dev)
         self._grad_views = []
         with torch.no_grad():
             for p, o in zip(self.params, offs):
@@ -147,17 +148,20 @@ class FusedAdam(torch.optim.Optimizer):
                 loss = closure()
         self._sync_grad_views()
         clip = max_norm is not None and max_norm > 0
-        sq = None
-        if clip or self.skip_nonfinite:
-            self.grad_sqnorm()
-            sq = self.sqnorm
+        flags = (ADAM_CLIP if clip else 0) | (ADAM_SKIP_NONFINITE if self.skip_nonfinite else 0)
         g = self.param_groups[0]
         b1, b2 = g["betas"]
-        _ledger.run(lambda: lib.cai_adam(_p(self.flat), _p(self.flat_grad), _p(self.exp_avg), _p(self.exp_avg_sq),
-                                         self.numel, float(g["lr"]), float(b1), float(b2), float(g["eps"]),
-                                         _p(self.step_count), _p(sq), float(max_norm) if clip else math.inf,
-                                         _stream()),
-                    "adam", "adam_kernel", 0, 28 * self.numel, torch.float32, f"{self.numel} parameters")
+        # norm + clip + Adam + step count in 2 launches (1 for small buffers): cai_adam_step; self.sqnorm
+        # receives sum(g^2) whenever it is computed
+        small = self.numel <= ADAM_SMALL_N
+        _ledger.run(lambda: lib.cai_adam_step(_p(self.flat), _p(self.flat_grad), _p(self.exp_avg),
+                                              _p(self.exp_avg_sq), self.numel, float(g["lr"]), float(b1), float(b2),
+                                              float(g["eps"]), _p(self.step_count), _p(self.sqnorm),
+                                              float(max_norm) if clip else math.inf, flags, _p(self._ws),
+                                              self._ws.numel(), _stream()),
+                    "adam", "adam_small_kernel" if small else "sq_part + adam_fused_kernel", 2.0 * self.numel if flags
+                    else 0.0, 32 * self.numel if flags else 28 * self.numel, torch.float32,
+                    f"{self.numel} parameters")
         return loss
 
     # -- checkpoints in torch.optim.Adam's format (train.py:407,419,475) -------------------------------

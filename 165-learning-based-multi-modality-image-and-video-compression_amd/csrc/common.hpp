@@ -95,6 +95,20 @@ __device__ __forceinline__ float block_sum(float v, float* smem) {
     return r;
 }
 
+// the same sum in every thread (each adds the wave partials in thread 0's order: the same float)
+template <int NT>
+__device__ __forceinline__ float block_sum_all(float v, float* smem) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) smem[w] = v;
+    __syncthreads();
+    float r = 0.f;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) r += smem[i];
+    __syncthreads();
+    return r;
+}
+
 // ---------------------------------------------------------------------------
 // counted waits as compiler builtins (gfx9 s_waitcnt encoding: vmcnt[3:0] + [15:14], expcnt[6:4],
 // lgkmcnt[11:8]).  Unlike inline asm these are visible to the waitcnt pass, which otherwise falls

@@ -448,6 +448,19 @@ int cai_adam(float* p, const float* g, float* m, float* v, int64_t n,
              float lr, float beta1, float beta2, float eps,
              float* step, const float* sqnorm, float max_norm, void* stream);
 
+/* The whole optimiser step of FusedAdam in as few launches as possible (2 for n > 65536, else 1):
+ * flags CAI_ADAM_CLIP scales the grads by min(1, max_norm / (||g|| + 1e-6)) (clip_grad_norm_),
+ * CAI_ADAM_SKIP_NONFINITE skips the step on a non-finite norm (either flag computes the norm; a
+ * non-finite norm always skips, as cai_adam).  *sqnorm (nullable) receives sum(g^2).  Same update
+ * and step counting as cai_sqnorm + cai_adam.  Workspace >= cai_adam_step_workspace_bytes(n). */
+#define CAI_ADAM_CLIP 1
+#define CAI_ADAM_SKIP_NONFINITE 2
+size_t cai_adam_step_workspace_bytes(int64_t n);
+int cai_adam_step(float* p, const float* g, float* m, float* v, int64_t n,
+                  float lr, float beta1, float beta2, float eps,
+                  float* step, float* sqnorm, float max_norm, int32_t flags,
+                  void* workspace, size_t ws_bytes, void* stream);
+
 /* elementwise helpers */
 int cai_act_bwd(int mask_mode, float param, const void* y, int32_t y_ld, const void* g, int32_t g_ld,
                 void* out, int32_t out_ld, int64_t npix, int32_t C, int dtype, void* stream);

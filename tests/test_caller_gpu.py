@@ -142,9 +142,10 @@ def test_fp16_autocast_policy(cuda):
     assert torch.equal(outs[0], outs[1])
 
 
-def _param_set(dev, seed=9):
+def _param_set(dev, seed=9, large=False):
+    """large: > 65536 parameters in all (cai_adam_step's two-launch path instead of the one-block one)."""
     torch.manual_seed(seed)
-    shapes = [(16, 3, 5, 5), (16,), (7,), (24, 24)]
+    shapes = [(16, 3, 5, 5), (16,), (7,), (24, 24)] + ([(192, 128, 3, 3)] if large else [])
     base = [torch.randn(s) for s in shapes]
     return shapes, [torch.nn.Parameter(b.clone().to(dev)) for b in base], [torch.nn.Parameter(b.clone().to(dev))
                                                                            for b in base]
@@ -231,11 +232,12 @@ def test_fused_adam_survives_detached_grads(cuda):
         assert (a.detach() - b.detach()).abs().max().item() < 1e-6
 
 
-def test_fused_adam_skips_nonfinite_step(cuda):
+@pytest.mark.parametrize("large", [False, True], ids=["one-block", "two-launch"])
+def test_fused_adam_skips_nonfinite_step(cuda, large):
     """An inf / NaN gradient skips the update on the device (GradScaler's rule) and leaves the step count."""
     from compressai.optim import FusedAdam
 
-    shapes, _, pb = _param_set(cuda)
+    shapes, _, pb = _param_set(cuda, large=large)
     opt = FusedAdam(pb, lr=1e-2)
     for p in pb:
         p.grad.fill_(0.5)

@@ -121,12 +121,14 @@ def test_optimizer_step_parity(cuda, name):
     assert diffs.median().item() < 1e-3 * lr
 
 
-def test_fused_adam_matches_torch_adam(cuda):
-    """FusedAdam(+clip) == torch.optim.Adam + clip_grad_norm_ on identical gradients."""
+@pytest.mark.parametrize("large", [False, True], ids=["one-block", "two-launch"])
+def test_fused_adam_matches_torch_adam(cuda, large):
+    """FusedAdam(+clip) == torch.optim.Adam + clip_grad_norm_ on identical gradients, on both launch paths of
+    cai_adam_step (<= 65536 parameters: one block; above: norm partials + fused update)."""
     from compressai.optim import FusedAdam
 
     torch.manual_seed(9)
-    shapes = [(128, 3, 5, 5), (128,), (7,), (64, 64)]
+    shapes = [(128, 3, 5, 5), (128,), (7,), (64, 64)] + ([(192, 128, 3, 3)] if large else [])
     ref = [torch.nn.Parameter(torch.randn(s)) for s in shapes]
     dev = [torch.nn.Parameter(p.detach().clone().to(cuda)) for p in ref]
     opt_r = torch.optim.Adam(ref, lr=1e-3)
