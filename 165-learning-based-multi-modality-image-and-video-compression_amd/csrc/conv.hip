@@ -1031,7 +1031,12 @@ struct HaloPhCfg {
     static constexpr int PATCH = 8 * PLANE * 16;
     static constexpr int NPI = (8 * NPOS + 511) / 512;
     static constexpr int NTAP = NA * NC, NST = 2 * NTAP;       // steps per chunk: (half, tap)
-    static constexpr int NSTB = NST % 3 == 0 ? 3 : 2;         // NST % NSTB == 0: a step's stage is t % NSTB
+#ifndef CAI_HALO_PH_NSTB6
+#define CAI_HALO_PH_NSTB6 0
+#endif
+    // NST % NSTB == 0: a step's stage is t % NSTB.  A 6-stage ring (CAI_HALO_PH_NSTB6=1) measured slower on
+    // MI355X (C2 8180 vs 8430 patches/s; the big launch 91.6 vs 88 us): the latency is not in the ring
+    static constexpr int NSTB = (CAI_HALO_PH_NSTB6 && NST % 6 == 0) ? 6 : (NST % 3 == 0 ? 3 : 2);
     static constexpr int BSTAGE = BN * 32 * 2;
     static constexpr int EPI = BM * (BN + 4) * 4;
     static constexpr int BYTES = (PATCH + NSTB * BSTAGE > EPI) ? PATCH + NSTB * BSTAGE : EPI;
