@@ -94,7 +94,17 @@ struct GdnGeo {
 // Rows past the end are stored to a sink instead of being skipped: every store is issued, so the
 // compiler's vmcnt bookkeeping never meets a path with fewer memory operations (a skipped store there
 // turns the next wait on the register prefetch into vmcnt(0), draining the prefetched tiles).
-__device__ __attribute__((aligned(64))) u32x4 cai_gdn_sink[4];
+__device__ __attribute__((aligned(64))) u32x4 cai_gdn_sink[16];
+
+// CPT stores to distinct sink slots (identical stores to one address would be merged into one, and the
+// prologue would no longer match the loop's per-iteration store count), pinned in issue order
+template <int CPT>
+__device__ __forceinline__ void sink_stores(int base) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) cai_gdn_sink[base + i] = u32x4{0u, 0u, 0u, 0u};
+    __builtin_amdgcn_sched_barrier(0);
+}
 
 template <typename T, int C>
 struct TileRegs {
@@ -218,6 +228,52 @@ __device__ __forceinline__ void tile_gemm(Acc<T, C>& ACC, const char* lds, const
     }
 }
 
+// The same product transposed, norm^T = gamma . (x^2)^T: gamma's fragments as the A operand, the x^2 tile as
+// B.  Each lane then holds 4 CONSECUTIVE channels of one pixel (acc[tn][tm][r]: channel col0 + 16 tn +
+// 4 (lane >> 4) + r, pixel row0 + 16 tm + (lane & 15)), so the elementwise stage reads x and writes y as one
+// 8-byte (bf16) / 16-byte (fp32) LDS access per 4 elements -- conflict-free across the wave -- instead of
+// four 2-byte accesses that share bank words.
+template <typename T, int C>
+struct AccT {
+    f32x4 v[GdnGeo<T, C>::TN][GdnGeo<T, C>::TM];
+};
+template <typename T, int C>
+__device__ __forceinline__ void tile_gemm_t(AccT<T, C>& ACC, const char* lds, const BFrags<T, C>& FB, int wave) {
+    using G = GdnGeo<T, C>;
+    auto& acc = ACC.v;
+    const auto& fb = FB.v;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int tn = 0; tn < G::TN; ++tn)
+#pragma unroll
+        for (int tm = 0; tm < G::TM; ++tm) acc[tn][tm] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < G::KB; ++kb) {
+        u32x4 fx[G::TM];
+#pragma unroll
+        for (int tm = 0; tm < G::TM; ++tm) {
+            const int row = G::row0(wave) + tm * 16 + (lane & 15);
+            fx[tm] = *reinterpret_cast<const u32x4*>(lds + row * G::RS + kb * 64 + 16 * (lane >> 4));
+        }
+#pragma unroll
+        for (int tn = 0; tn < G::TN; ++tn)
+#pragma unroll
+            for (int tm = 0; tm < G::TM; ++tm) acc[tn][tm] = mma16<T>(fb[tn][kb], fx[tm], acc[tn][tm]);
+    }
+}
+
+// 4 consecutive elements of a row at an element offset that is a multiple of 4
+template <typename T>
+struct Quad;
+template <>
+struct Quad<bf16> {
+    typedef bf16x4 V;
+};
+template <>
+struct Quad<float> {
+    typedef f32x4 V;
+};
+
 template <typename T>
 __device__ __forceinline__ T* lds_elem(char* lds, int rs, int row, int col) {
     return reinterpret_cast<T*>(lds + row * rs) + col;
@@ -233,9 +289,11 @@ __global__ __launch_bounds__(GNT, (sizeof(T) == 2 && C <= 192) ? 2 : 1) void gdn
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     BFrags<T, C> fb;
     load_bfrag<T, C>(fb, gamma, wave);
-    float bv[G::TN];
+    float bq[G::TN][4];   // beta of this lane's 4 channels per channel tile (transposed GEMM layout)
 #pragma unroll
-    for (int tn = 0; tn < G::TN; ++tn) bv[tn] = beta[G::col0(wave) + tn * 16 + (lane & 15)];
+    for (int tn = 0; tn < G::TN; ++tn)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bq[tn][r] = beta[G::col0(wave) + tn * 16 + (lane >> 4) * 4 + r];
 
     // persistent blocks, two tiles in flight per block (register sets A / B), every load and store issued
     // (clamped rows, sink stores) and a counted loop over tile pairs: the straight-line body lets each
@@ -248,12 +306,10 @@ __global__ __launch_bounds__(GNT, (sizeof(T) == 2 && C <= 192) ? 2 : 1) void gdn
     TileRegs<T, C> ra, rb;
     int64_t tile = blockIdx.x;
     tile_load_all<T, C>(ra, x, x_ld, min(tile, last) * GBM, npix);
-#pragma unroll
-    for (int i = 0; i < G::CPT; ++i) cai_gdn_sink[1] = u32x4{0u, 0u, 0u, 0u};
+    sink_stores<G::CPT>(0);
     if constexpr (PAIR) {
         tile_load_all<T, C>(rb, x, x_ld, min(tile + stride, last) * GBM, npix);
-#pragma unroll
-        for (int i = 0; i < G::CPT; ++i) cai_gdn_sink[2] = u32x4{0u, 0u, 0u, 0u};
+        sink_stores<G::CPT>(8);
     }
     auto step = [&](TileRegs<T, C>& rx, int64_t cur, int64_t nxt) {
         lds_barrier();                       // the previous tile's store has read lds
@@ -266,33 +322,36 @@ __global__ __launch_bounds__(GNT, (sizeof(T) == 2 && C <= 192) ? 2 : 1) void gdn
         }
         tile_load_all<T, C>(rx, x, x_ld, nxt * GBM, npix);
         lds_barrier();
-        Acc<T, C> A;
-        tile_gemm<T, C>(A, lsq, fb, false, wave);
+        AccT<T, C> A;
+        tile_gemm_t<T, C>(A, lsq, fb, wave);
         auto& acc = A.v;
-        // normalise: out = x * rsqrt(norm)  (or sqrt)
+        // normalise: out = x * rsqrt(norm)  (or sqrt); lane: 4 consecutive channels of one pixel
+        typedef typename Quad<T>::V QV;
 #pragma unroll
-        for (int tm = 0; tm < G::TM; ++tm)
+        for (int tn = 0; tn < G::TN; ++tn)
 #pragma unroll
-            for (int tn = 0; tn < G::TN; ++tn) {
-                const int col = G::col0(wave) + tn * 16 + (lane & 15);
+            for (int tm = 0; tm < G::TM; ++tm) {
+                const int col = G::col0(wave) + tn * 16 + (lane >> 4) * 4;
+                const int row = G::row0(wave) + tm * 16 + (lane & 15);
+                const QV xq = *reinterpret_cast<const QV*>(lds + row * G::RS + col * (int)sizeof(T));
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int row = G::row0(wave) + tm * 16 + (lane >> 4) * 4 + r;
-                    const float xv = to_f32(*lds_elem<T>(lds, G::RS, row, col));
-                    const float nv = acc[tm][tn][r] + bv[tn];
+                    const float nv = acc[tn][tm][r] + bq[tn][r];
                     const float rs = rsqrtf(nv);
-                    acc[tm][tn][r] = xv * (inverse ? nv * rs : rs);
+                    acc[tn][tm][r] = to_f32(xq[r]) * (inverse ? nv * rs : rs);
                 }
             }
         lds_barrier();
 #pragma unroll
-        for (int tm = 0; tm < G::TM; ++tm)
+        for (int tn = 0; tn < G::TN; ++tn)
 #pragma unroll
-            for (int tn = 0; tn < G::TN; ++tn) {
-                const int col = G::col0(wave) + tn * 16 + (lane & 15);
+            for (int tm = 0; tm < G::TM; ++tm) {
+                const int col = G::col0(wave) + tn * 16 + (lane >> 4) * 4;
+                const int row = G::row0(wave) + tm * 16 + (lane & 15);
+                QV yq;
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    *lds_elem<T>(lds, G::RS, G::row0(wave) + tm * 16 + (lane >> 4) * 4 + r, col) = from_f32<T>(acc[tm][tn][r]);
+                for (int r = 0; r < 4; ++r) yq[r] = from_f32<T>(acc[tn][tm][r]);
+                *reinterpret_cast<QV*>(lds + row * G::RS + col * (int)sizeof(T)) = yq;
             }
         lds_barrier();
         lds_to_global_all<T, C>(lds, y, y_ld, cur * GBM, npix);
@@ -549,12 +608,10 @@ __global__ __launch_bounds__(FNT, 1) void gdn_bwd_fused_kernel(const bf16* __res
     // (to the sink), so the loop's first wait is the same counted wait as the steady state's
     ftile_load<C>(rxa, x, x_ld, min(tile, last) * GBM, npix);
     ftile_load<C>(rga, dy, dy_ld, min(tile, last) * GBM, npix);
-#pragma unroll
-    for (int i = 0; i < G::CPT; ++i) cai_gdn_sink[1] = u32x4{0u, 0u, 0u, 0u};
+    sink_stores<G::CPT>(0);
     ftile_load<C>(rxb, x, x_ld, min(tile + stride, last) * GBM, npix);
     ftile_load<C>(rgb, dy, dy_ld, min(tile + stride, last) * GBM, npix);
-#pragma unroll
-    for (int i = 0; i < G::CPT; ++i) cai_gdn_sink[2] = u32x4{0u, 0u, 0u, 0u};
+    sink_stores<G::CPT>(8);
     auto step = [&](u32x4 (&rx)[G::CPT], u32x4 (&rg)[G::CPT], int64_t cur, int64_t nxt) {
         const int64_t p0 = cur * GBM;
         lds_barrier();                       // previous tile's dx store has read Lg

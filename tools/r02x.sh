@@ -1,0 +1,11 @@
+cd $GRAFT_REPO_ROOT
+o=gpurun_out
+timeout -k 10 600 python -u -m pytest tests -x -q -m gpu -k "gdn or models or golden or wide" --timeout 300 --timeout-method thread -p no:cacheprovider > $o/r02x_test.log 2>&1 || exit 1
+: > $o/r02x_bench.log
+for i in 1 2; do
+  timeout -k 10 200 python bench.py --steps 50 --warmup 5 --cpu-seconds 0 2>/dev/null | python -c "import json,sys; print('C2', json.loads(sys.stdin.read())['value'])" >> $o/r02x_bench.log || exit 1
+done
+timeout -k 10 200 python tools/membench.py > $o/r02x_mem.log 2>&1 || exit 1
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace -d $GRAFT_REPO_ROOT/gpurun_out/r02x_prof -o run --output-format csv -- \
+    python3 $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 3 --cpu-seconds 0 --no-profile > $GRAFT_REPO_ROOT/gpurun_out/r02x_prof.log 2>&1
