@@ -568,7 +568,7 @@ __global__ __launch_bounds__(FNT, 1) void gdn_bwd_fused_kernel(const bf16* __res
                                                                bf16* __restrict__ dx, int dx_ld,
                                                                float* __restrict__ part) {
     using G = FusedGeo<C>;
-    __shared__ __attribute__((aligned(16))) char lds[4 * G::TILE];
+    __shared__ __attribute__((aligned(16))) char lds[4 * G::TILE + C * 4];
     char* Lx = lds;
     char* Lg = lds + G::TILE;
     char* Lu = lds + 2 * G::TILE;
@@ -589,11 +589,14 @@ __global__ __launch_bounds__(FNT, 1) void gdn_bwd_fused_kernel(const bf16* __res
         fb[kb] = *reinterpret_cast<const u32x4*>(gamma_op + (int64_t)n * C + kb * 32 + 8 * g_);
         fbT[kb] = *reinterpret_cast<const u32x4*>(gammaT + (int64_t)n * C + kb * 32 + 8 * g_);
     }
-    const float bv = beta[n0 + i16];
+    // transposed GEMM layout (as the forward): a lane owns channels n0 + 4 g_ + r (r < 4) of one pixel.
+    // beta sits in LDS (one 16-byte read per tile) rather than in 4 more live registers
+    float dbeta[4] = {0.f, 0.f, 0.f, 0.f};
+    float* const Lb = reinterpret_cast<float*>(lds + 4 * G::TILE);
+    for (int c = threadIdx.x; c < C; c += FNT) Lb[c] = beta[c];
     f32x4 dg[G::TI];
 #pragma unroll
     for (int t = 0; t < G::TI; ++t) dg[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float dbeta = 0.f;
 
     // two tiles in flight: register set A holds tile t + 2*stride while set B waits with t + stride.  The
     // loop body is the A step then the B step in straight-line code, every prefetch is issued (past the
@@ -621,7 +624,7 @@ __global__ __launch_bounds__(FNT, 1) void gdn_bwd_fused_kernel(const bf16* __res
         ftile_load<C>(rg, dy, dy_ld, nxt * GBM, npix);
         lds_barrier();
         const int nvalid = (int)min((int64_t)GBM, npix - p0);
-        // ---- norm = x^2 gamma^T (+ beta) ----
+        // ---- norm^T = gamma (x^2)^T (+ beta): gamma's fragments as A, the x^2 tile as B ----
         f32x4 acc[G::TM];
 #pragma unroll
         for (int tm = 0; tm < G::TM; ++tm) acc[tm] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -630,29 +633,24 @@ __global__ __launch_bounds__(FNT, 1) void gdn_bwd_fused_kernel(const bf16* __res
 #pragma unroll
             for (int tm = 0; tm < G::TM; ++tm) {
                 const int row = r0 + tm * 16 + i16;
-                const u32x4 a = *reinterpret_cast<const u32x4*>(Lq + row * G::RS + kb * 64 + 16 * g_);
-                acc[tm] = mma16<bf16>(a, fb[kb], acc[tm]);
+                const u32x4 b = *reinterpret_cast<const u32x4*>(Lq + row * G::RS + kb * 64 + 16 * g_);
+                acc[tm] = mma16<bf16>(fb[kb], b, acc[tm]);
             }
-        // ---- u, t1 (thread-owned elements: row (lane>>4)*4 + r, column n0 + i16) ----
-        // all LDS reads first: Lx / Lg / Lu share one array, so a read after a store would be
-        // issued (and waited for) one element at a time
-        float xr[G::TM][4], gr[G::TM][4];
+        // ---- u, t1: lane = pixel r0 + 16 tm + i16, channels n0 + 4 g_ + r: one 8-byte LDS access per
+        // 4 elements (x, g in; u out), conflict-free across the wave ----
+        bf16x4 t1q[G::TM];   // t1 rounded to bf16 (as the dx tile it feeds): half the registers
+        const f32x4 bq = *reinterpret_cast<const f32x4*>(Lb + n0 + 4 * g_);
 #pragma unroll
-        for (int tm = 0; tm < G::TM; ++tm)
+        for (int tm = 0; tm < G::TM; ++tm) {
+            const int row = r0 + tm * 16 + i16;
+            const bf16x4 xq = *reinterpret_cast<const bf16x4*>(Lx + row * G::RS + (n0 + 4 * g_) * 2);
+            const bf16x4 gq = *reinterpret_cast<const bf16x4*>(Lg + row * G::RS + (n0 + 4 * g_) * 2);
+            bf16x4 uq;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int row = r0 + tm * 16 + g_ * 4 + r;
-                xr[tm][r] = (float)*lds_elem<bf16>(Lx, G::RS, row, n0 + i16);
-                gr[tm][r] = (float)*lds_elem<bf16>(Lg, G::RS, row, n0 + i16);
-            }
-#pragma unroll
-        for (int tm = 0; tm < G::TM; ++tm)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = r0 + tm * 16 + g_ * 4 + r;
-                const float xv = xr[tm][r];
-                const float gv = gr[tm][r];
-                const float nv = acc[tm][r] + bv;
+                const float xv = (float)xq[r];
+                const float gv = (float)gq[r];
+                const float nv = acc[tm][r] + bq[r];
                 // one v_rsq per element for both forms (no IEEE divide / sqrt sequences)
                 const float rs = rsqrtf(nv);
                 float uv, t1;
@@ -664,10 +662,12 @@ __global__ __launch_bounds__(FNT, 1) void gdn_bwd_fused_kernel(const bf16* __res
                     uv = -0.5f * gv * xv * rs * rs * rs;
                 }
                 if (row >= nvalid) uv = 0.f;
-                dbeta += uv;
-                gr[tm][r] = (float)(bf16)t1;   // t1 stays in registers for the dx phase
-                *lds_elem<bf16>(Lu, G::RS, row, n0 + i16) = (bf16)uv;
+                dbeta[r] += uv;
+                t1q[tm][r] = (bf16)t1;   // t1 stays in registers for the dx phase
+                uq[r] = (bf16)uv;
             }
+            *reinterpret_cast<bf16x4*>(Lu + row * G::RS + (n0 + 4 * g_) * 2) = uq;
+        }
         lds_barrier();
         // ---- dgamma += u^T x^2 (K = the tile's 64 pixels; column reads by hardware transpose) ----
 #pragma unroll
@@ -687,7 +687,7 @@ __global__ __launch_bounds__(FNT, 1) void gdn_bwd_fused_kernel(const bf16* __res
                 dg[t] = mma16<bf16>(__builtin_bit_cast(u32x4, av), fbx, dg[t]);
             }
         }
-        // ---- dx = t1 + 2 x (u gamma) ----
+        // ---- dx^T = gamma^T u^T: gamma^T's fragments as A, the u tile as B ----
 #pragma unroll
         for (int tm = 0; tm < G::TM; ++tm) acc[tm] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -695,17 +695,20 @@ __global__ __launch_bounds__(FNT, 1) void gdn_bwd_fused_kernel(const bf16* __res
 #pragma unroll
             for (int tm = 0; tm < G::TM; ++tm) {
                 const int row = r0 + tm * 16 + i16;
-                const u32x4 a = *reinterpret_cast<const u32x4*>(Lu + row * G::RS + kb * 64 + 16 * g_);
-                acc[tm] = mma16<bf16>(a, fbT[kb], acc[tm]);
+                const u32x4 b = *reinterpret_cast<const u32x4*>(Lu + row * G::RS + kb * 64 + 16 * g_);
+                acc[tm] = mma16<bf16>(fbT[kb], b, acc[tm]);
             }
-        // dx = t1 + 2 x (u gamma): x and t1 are still in registers (xr, gr)
+        // dx = t1 + 2 x (u gamma): t1 still in registers, x re-read from its tile (8 bytes: cheaper than
+        // keeping it live through the dgamma phase), the same 4 channels of the same pixel
 #pragma unroll
-        for (int tm = 0; tm < G::TM; ++tm)
+        for (int tm = 0; tm < G::TM; ++tm) {
+            const int row = r0 + tm * 16 + i16;
+            const bf16x4 xqq = *reinterpret_cast<const bf16x4*>(Lx + row * G::RS + (n0 + 4 * g_) * 2);
+            bf16x4 dq;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = r0 + tm * 16 + g_ * 4 + r;
-                *lds_elem<bf16>(Lg, G::RS, row, n0 + i16) = (bf16)(gr[tm][r] + 2.f * xr[tm][r] * acc[tm][r]);
-            }
+            for (int r = 0; r < 4; ++r) dq[r] = (bf16)((float)t1q[tm][r] + 2.f * (float)xqq[r] * acc[tm][r]);
+            *reinterpret_cast<bf16x4*>(Lg + row * G::RS + (n0 + 4 * g_) * 2) = dq;
+        }
         lds_barrier();
         lds_to_global_rows_all<C>(Lg, dx, dx_ld, p0, npix);
     };
@@ -716,12 +719,18 @@ __global__ __launch_bounds__(FNT, 1) void gdn_bwd_fused_kernel(const bf16* __res
         step(rxb, rgb, tile + stride, min(tile + 3 * stride, last));
     }
     if (mine & 1) step(rxa, rga, tile, last);
-    // ---- partials: dbeta (lanes of one column: xor 16, 32; waves of one column block via LDS) ----
-    dbeta += __shfl_xor(dbeta, 16, 64);
-    dbeta += __shfl_xor(dbeta, 32, 64);
+    // ---- partials: dbeta (lanes of one channel quad: the 16 pixels i16, xor 1..8; waves of one column
+    // block via LDS) ----
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) dbeta[r] += __shfl_xor(dbeta[r], o, 64);
     __syncthreads();
     float* red = reinterpret_cast<float*>(lds);
-    if (lane < 16) red[wm * C + n0 + lane] = dbeta;
+    if (i16 == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[wm * C + n0 + 4 * g_ + r] = dbeta[r];
+    }
     __syncthreads();
     float* pb = part + (int64_t)blockIdx.x * (C * C + C);
     for (int c = threadIdx.x; c < C; c += FNT) {
