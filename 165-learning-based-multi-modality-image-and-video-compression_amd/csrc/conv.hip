@@ -155,9 +155,12 @@ __device__ __forceinline__ void store_out_scalar(const ConvArgs& a, const PhaseD
 // act / mask applied by the reduce), otherwise bias + act (+ mask) and 16-byte
 // stores.  `E` must hold BM*(BN+4) floats and may alias the operand stages.
 // rowm(row): the GEMM row m of tile row `row`, or -1 outside the phase
+// slab: the split-K partial slab this block writes (-1: blockIdx.z, the phase * ksplit + split of the
+// phase-major grids)
 template <typename T, int BM, int BN, int WM, int WN, int NTH, class RowMap>
 __device__ __forceinline__ void conv_epilogue_rows(const ConvArgs& a, const PhaseDesc& P, int plane, int n0, float* E,
-                                                   const f32x4 (&acc)[BM / WM / 16][BN / WN / 16], RowMap rowm) {
+                                                   const f32x4 (&acc)[BM / WM / 16][BN / WN / 16], RowMap rowm,
+                                                   int slab = -1) {
     constexpr int WTM = BM / WM, WTN = BN / WN;
     constexpr int TM = WTM / 16, TN = WTN / 16;
     constexpr int ES = BN + 4;
@@ -173,7 +176,7 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvArgs& a, const Phas
                 for (int r = 0; r < 4; ++r) E[(wm * WTM + tm * 16 + (lane >> 4) * 4 + r) * ES + col] = acc[tm][tn][r];
             }
         __syncthreads();
-        float* dst = a.ws + (int64_t)blockIdx.z * a.ws_rows * a.ws_ld;
+        float* dst = a.ws + (int64_t)(slab >= 0 ? slab : (int)blockIdx.z) * a.ws_rows * a.ws_ld;
         constexpr int cpr = BN / 4;
         for (int id = tid; id < BM * cpr; id += NTH) {
             const int row = id / cpr, cc = id - (id / cpr) * cpr;
@@ -1022,6 +1025,10 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvArgs a, int
 // cells) in LDS once and runs the NA*NC taps x two 32-channel halves out of it.  The weights stream through
 // the same hand-ordered LDS-DMA ring as conv_halo_kernel (one 16-byte DMA per lane per step, NSTB-1 steps
 // ahead); the next chunk's footprint is loaded into registers while the current one is consumed.
+#ifndef CAI_HALO_PH_MIX
+#define CAI_HALO_PH_MIX 0
+#endif
+
 template <int NA, int NC>
 struct HaloPhCfg {
     static constexpr int TH = 8, TW = 32, BM = TH * TW, BN = 128, WM = 4, WN = 2, CK = 64;
@@ -1044,7 +1051,7 @@ struct HaloPhCfg {
 };
 
 template <int NA, int NC>
-__device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* smem, int ph, int split,
+__device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* smem, int ph, int split, int bid,
                                                      int tiles_x, int tiles_y) {
     using H = HaloPhCfg<NA, NC>;
     constexpr int BM = H::BM, BN = H::BN, WM = H::WM, WN = H::WN;
@@ -1057,8 +1064,6 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
     const PhaseDesc& P = a.ph[ph];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / WN, wn = wid % WN;
-    const int ntiles = gridDim.x;
-    const int bid = (ntiles & 7) == 0 ? (blockIdx.x & 7) * (ntiles >> 3) + (blockIdx.x >> 3) : blockIdx.x;
     const int per_img = tiles_x * tiles_y;
     const int b = bid / per_img;
     const int rt = bid - b * per_img;
@@ -1201,21 +1206,38 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
     conv_epilogue_rows<bf16, BM, BN, WM, WN, 512>(a, P, plane, 0, reinterpret_cast<float*>(smem), acc, [=](int row) {
         const int oy = ty0 + row / H::TW, ox = tx0 + row % H::TW;
         return (oy < P.OHg && ox < P.OWg) ? b * plane + oy * P.OWg + ox : -1;
-    });
+    }, ph * a.ksplit + split);
 }
 
-// grid: x = output tiles of one phase, z = phase * ksplit + split (the split-K slab index of the epilogue)
+// grid: x = 4 x the output tiles of one phase, z = split (the split-K slab index of the epilogue).  Block
+// order: phase-major (tiles XCD-remapped within a phase).  CAI_HALO_PH_MIX=1 makes the four phases of one
+// output tile consecutive logical blocks on one XCD (shared input footprint from its L2, every round mixing
+// 9-, 6- and 4-tap blocks): measured on MI355X the big launch unchanged (88-90 us) and the C2 step 2 %
+// slower (8316 vs 8465 patches/s), so it is off.
 __global__ __launch_bounds__(512, 1) void conv_halo_phase_kernel(const ConvArgs a, int tiles_x, int tiles_y) {
     constexpr int BYTES = HaloPhCfg<3, 3>::BYTES > HaloPhCfg<2, 2>::BYTES ? HaloPhCfg<3, 3>::BYTES
                                                                            : HaloPhCfg<2, 2>::BYTES;
     static_assert(BYTES >= HaloPhCfg<3, 2>::BYTES && BYTES >= HaloPhCfg<2, 3>::BYTES, "halo phase LDS");
     __shared__ __attribute__((aligned(16))) char smem[BYTES];
-    const int ph = blockIdx.z / a.ksplit, split = blockIdx.z - ph * a.ksplit;
+    const int nb = gridDim.x;
+    const int lid = CAI_HALO_PH_MIX ? ((nb & 7) == 0 ? (blockIdx.x & 7) * (nb >> 3) + (blockIdx.x >> 3) : blockIdx.x)
+                                    : blockIdx.x;
+    const int nt = nb >> 2;
+    int ph, bid;
+    if (CAI_HALO_PH_MIX) {
+        ph = lid & 3;
+        bid = lid >> 2;
+    } else {   // the previous order: phase-major, tiles XCD-remapped within a phase
+        ph = blockIdx.x / nt;
+        const int t = blockIdx.x - ph * nt;
+        bid = (nt & 7) == 0 ? (t & 7) * (nt >> 3) + (t >> 3) : t;
+    }
+    const int split = blockIdx.z;
     switch (ph) {    // k5 s2 p2 phases: (py, px) = (0,0) 3x3, (0,1) 3x2, (1,0) 2x3, (1,1) 2x2 taps
-        case 0: conv_halo_phase_body<3, 3>(a, smem, 0, split, tiles_x, tiles_y); break;
-        case 1: conv_halo_phase_body<3, 2>(a, smem, 1, split, tiles_x, tiles_y); break;
-        case 2: conv_halo_phase_body<2, 3>(a, smem, 2, split, tiles_x, tiles_y); break;
-        default: conv_halo_phase_body<2, 2>(a, smem, 3, split, tiles_x, tiles_y); break;
+        case 0: conv_halo_phase_body<3, 3>(a, smem, 0, split, bid, tiles_x, tiles_y); break;
+        case 1: conv_halo_phase_body<3, 2>(a, smem, 1, split, bid, tiles_x, tiles_y); break;
+        case 2: conv_halo_phase_body<2, 3>(a, smem, 2, split, bid, tiles_x, tiles_y); break;
+        default: conv_halo_phase_body<2, 2>(a, smem, 3, split, bid, tiles_x, tiles_y); break;
     }
 }
 
@@ -2896,7 +2918,7 @@ static void launch_conv_halo(const ConvArgs& a, const ConvLaunch& L, hipStream_t
 }
 
 static void launch_conv_halo_phase(const ConvArgs& a, const ConvLaunch& L, hipStream_t st) {
-    hipLaunchKernelGGL(conv_halo_phase_kernel, dim3(L.mtiles, 1, 4 * a.ksplit), dim3(512), 0, st, a, L.tiles_x,
+    hipLaunchKernelGGL(conv_halo_phase_kernel, dim3(4 * L.mtiles, 1, a.ksplit), dim3(512), 0, st, a, L.tiles_x,
                        L.tiles_y);
     if (a.ksplit > 1) {
         const int VO = (a.y_vec && a.y_dtype == CAI_BF16) ? 8 : 4;
