@@ -367,7 +367,8 @@ def main():
             local_step()
         led = profile_step(local_step)
         if rank == 0:
-            print(json.dumps(dominant_roofline(led, workload, reps=args.steps, pick=args.replay)), flush=True)
+            print(json.dumps(dict(dominant_roofline(led, workload, reps=args.steps, pick=args.replay),
+                                  workload=workload)), flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
