@@ -226,6 +226,102 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvArgs& a, const Phas
     }
 }
 
+// Epilogue for TRANSPOSED accumulators (weights as the MFMA's A operand): lane (i16, g_) of tile (tm, tn)
+// holds output channels wn*WTN + tn*16 + 4*g_ + 0..3 of tile row wm*WTM + tm*16 + i16, so the common cases
+// store straight from registers: split-K partials as 16-byte fp32 stores into the slab, bf16 outputs
+// (bias + act) as 8-byte stores.  Masked or non-bf16 / scalar outputs go through LDS as in
+// conv_epilogue_rows (E must then hold BM*(BN+4) floats).
+template <typename T, int BM, int BN, int WM, int WN, int NTH, class RowMap>
+__device__ __forceinline__ void conv_epilogue_rows_t(const ConvArgs& a, const PhaseDesc& P, int plane, int n0,
+                                                     float* E, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
+                                                     RowMap rowm, int slab) {
+    constexpr int WTM = BM / WM, WTN = BN / WN;
+    constexpr int TM = WTM / 16, TN = WTN / 16;
+    constexpr int ES = BN + 4;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    const int g_ = lane >> 4, i16 = lane & 15;
+    if (a.ksplit > 1) {
+        float* dst = a.ws + (int64_t)slab * a.ws_rows * a.ws_ld;
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+            const int m = rowm(wm * WTM + tm * 16 + i16);
+            if (m < 0) continue;
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                const int n = n0 + wn * WTN + tn * 16 + 4 * g_;
+                if (n < a.ws_ld) *reinterpret_cast<f32x4*>(dst + (int64_t)m * a.ws_ld + n) = acc[tm][tn];
+            }
+        }
+        return;
+    }
+    if (a.y_vec && a.y_dtype == CAI_BF16 && !a.mask_mode && (a.Cout & 3) == 0) {
+        f32x4 bv[TN];
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int n = n0 + wn * WTN + tn * 16 + 4 * g_;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bv[tn][r] = (a.bias && n + r < a.Cout) ? a.bias[n + r] : 0.f;
+        }
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+            const int m = rowm(wm * WTM + tm * 16 + i16);
+            if (m < 0) continue;
+            int b, oy, ox;
+            out_pixel<T>(a, P, plane, m, b, oy, ox);
+            bf16* Y = reinterpret_cast<bf16*>(a.y) + (int64_t)b * a.ysb + (int64_t)oy * a.ysy + (int64_t)ox * a.ysx;
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                const int n = n0 + wn * WTN + tn * 16 + 4 * g_;
+                if (n >= a.Cout) continue;
+                bf16x4 h;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) h[r] = (bf16)apply_act(acc[tm][tn][r] + bv[tn][r], a.act, a.act_param);
+                *reinterpret_cast<bf16x4*>(Y + n) = h;
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int row = wm * WTM + tm * 16 + i16, col = wn * WTN + tn * 16 + 4 * g_;
+            f32x4 v;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int n = n0 + col + r;
+                const float bvr = (a.bias && n < a.Cout) ? a.bias[n] : 0.f;
+                v[r] = apply_act(acc[tm][tn][r] + bvr, a.act, a.act_param);
+            }
+            *reinterpret_cast<f32x4*>(E + row * ES + col) = v;
+        }
+    __syncthreads();
+    if (a.y_vec) {
+        const int VO = a.y_dtype == CAI_BF16 ? 8 : 4;
+        const int cpr = BN / VO;
+        for (int id = tid; id < BM * cpr; id += NTH) {
+            const int row = id / cpr, cc = id - (id / cpr) * cpr;
+            const int m = rowm(row), n = n0 + cc * VO;
+            if (m < 0 || n >= a.Cout) continue;
+            float v[8];
+            const f32x4 lo = *reinterpret_cast<const f32x4*>(E + row * ES + cc * VO);
+            f32x4 hi = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (VO == 8) hi = *reinterpret_cast<const f32x4*>(E + row * ES + cc * VO + 4);
+            v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+            v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+            store_out_chunk<T>(a, P, plane, m, n, v, VO);
+        }
+    } else {
+        for (int id = tid; id < BM * BN; id += NTH) {
+            const int col = id / BM, row = id - (id / BM) * BM;
+            const int m = rowm(row), n = n0 + col;
+            if (m < 0 || n >= a.Cout) continue;
+            store_out_scalar<T>(a, P, plane, m, n, E[row * ES + col]);
+        }
+    }
+}
+
 template <typename T, int BM, int BN, int WM, int WN, int NTH>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const PhaseDesc& P, int plane, int Mph, int m0,
                                               int n0, float* E, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16]) {
@@ -801,6 +897,15 @@ __device__ __forceinline__ void wait_vmcnt_n(int n) {    // n folds to a constan
     }
 }
 
+// transposed accumulators + register-direct epilogue (conv_epilogue_rows_t) in the halo kernels: the
+// phase kernel's launches 57.8 vs 59.7 us average in the C2 step (profiles/r02_edge_s2d_ab.log, r02af)
+#ifndef CAI_HALO_T
+#define CAI_HALO_T 1
+#endif
+#ifndef CAI_HALO_PH_T
+#define CAI_HALO_PH_T 1
+#endif
+
 template <int KS>
 struct HaloCfg {
     static constexpr int TH = 8, TW = 32, BM = TH * TW, BN = 128, WM = 4, WN = 2, CK = 32;
@@ -986,7 +1091,8 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvArgs a, int
 #pragma unroll
                 for (int tn = 0; tn < TN; ++tn) {
 #ifndef CAI_PROBE_NOMFMA    // timing probe only (results invalid): fragments read, no MFMA
-                    acc[tm][tn] = mma16<bf16>(fa[tm], fb[tn], acc[tm][tn]);
+                    acc[tm][tn] = CAI_HALO_T ? mma16<bf16>(fb[tn], fa[tm], acc[tm][tn])
+                                             : mma16<bf16>(fa[tm], fb[tn], acc[tm][tn]);
 #else
                     asm volatile("" ::"v"(fa[tm]), "v"(fb[tn]));
 #endif
@@ -1010,10 +1116,15 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvArgs a, int
     asm volatile("" ::"v"(fence_[0]), "v"(fence_[1]), "v"(fence_[2]), "v"(fence_[3]));
     __syncthreads();
     const int plane = P.OHg * P.OWg;
-    conv_epilogue_rows<bf16, BM, BN, WM, WN, 512>(a, P, plane, 0, reinterpret_cast<float*>(smem), acc, [=](int row) {
+    auto rowm = [=](int row) {
         const int oy = ty0 + row / H::TW, ox = tx0 + row % H::TW;
         return (oy < P.OHg && ox < P.OWg) ? b * plane + oy * P.OWg + ox : -1;
-    });
+    };
+    if (CAI_HALO_T)
+        conv_epilogue_rows_t<bf16, BM, BN, WM, WN, 512>(a, P, plane, 0, reinterpret_cast<float*>(smem), acc, rowm,
+                                                        (int)blockIdx.z);
+    else
+        conv_epilogue_rows<bf16, BM, BN, WM, WN, 512>(a, P, plane, 0, reinterpret_cast<float*>(smem), acc, rowm);
 }
 
 // Halo-staged s^2-phase implicit GEMM for the stride-2 k5 transposed convolutions (ConvTranspose2d k5 s2 p2
@@ -1028,6 +1139,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvArgs a, int
 #ifndef CAI_HALO_PH_MIX
 #define CAI_HALO_PH_MIX 0
 #endif
+
 
 template <int NA, int NC>
 struct HaloPhCfg {
@@ -1185,7 +1297,9 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-                for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mma16<bf16>(fa[tm], fb[tn], acc[tm][tn]);
+                for (int tn = 0; tn < TN; ++tn)
+                    acc[tm][tn] = CAI_HALO_PH_T ? mma16<bf16>(fb[tn], fa[tm], acc[tm][tn])
+                                                : mma16<bf16>(fa[tm], fb[tn], acc[tm][tn]);
 #pragma unroll
             for (int i = 0; i < TM + TN; ++i) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -1203,10 +1317,16 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
     asm volatile("" ::"v"(fence_[0]), "v"(fence_[1]), "v"(fence_[2]), "v"(fence_[3]));
     __syncthreads();
     const int plane = P.OHg * P.OWg;
-    conv_epilogue_rows<bf16, BM, BN, WM, WN, 512>(a, P, plane, 0, reinterpret_cast<float*>(smem), acc, [=](int row) {
+    auto rowm = [=](int row) {
         const int oy = ty0 + row / H::TW, ox = tx0 + row % H::TW;
         return (oy < P.OHg && ox < P.OWg) ? b * plane + oy * P.OWg + ox : -1;
-    }, ph * a.ksplit + split);
+    };
+    if (CAI_HALO_PH_T)
+        conv_epilogue_rows_t<bf16, BM, BN, WM, WN, 512>(a, P, plane, 0, reinterpret_cast<float*>(smem), acc, rowm,
+                                                        ph * a.ksplit + split);
+    else
+        conv_epilogue_rows<bf16, BM, BN, WM, WN, 512>(a, P, plane, 0, reinterpret_cast<float*>(smem), acc, rowm,
+                                                      ph * a.ksplit + split);
 }
 
 // grid: x = 4 x the output tiles of one phase, z = split (the split-K slab index of the epilogue).  Block

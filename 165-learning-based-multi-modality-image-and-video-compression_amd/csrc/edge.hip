@@ -26,6 +26,7 @@
 #include "mfma.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace cai {
 namespace {
@@ -55,6 +56,25 @@ struct EdgeArgs {
     float* cs_part;       // per-pack-block fp32 column sums of the image side [npack][16]
     int npack, prow;      // pack blocks, superpixel rows per pack block
 };
+
+// s2d A/B knobs, measured on MI355X (the C2 g_a[0] forward / g_s[6] input gradient, 16 x 128 x 128 x 128
+// bf16 out, profiles/r02_edge_s2d_ab.log): one tile per block with an LDS-staged epilogue 27.6 us;
+// persistent + 8-byte register stores 31.6; 16-byte register stores 27.2; + grid-stride tile order 23.3
+// (the default); prefetch distance 2 23.4; nt stores 28.5 / 26.9 (grid-stride).  Timing probes (results
+// invalid): stores skipped at run time 12.9, no in-loop image loads 18.8 -- the kernel is issue-bound
+// (MFMA + VALU per tile) with the stores on top, against 11.3 us for a torch fill of the same bytes.
+#ifndef CAI_EDGE_PROBE
+#define CAI_EDGE_PROBE 0      // timing probes: 1 stores skipped at run time, 2 no in-loop image loads
+#endif
+#ifndef CAI_EDGE_S2D_PD
+#define CAI_EDGE_S2D_PD 1     // prefetch distance in tiles (1 or 2)
+#endif
+#ifndef CAI_EDGE_S2D_GS
+#define CAI_EDGE_S2D_GS 1     // tile order: 1 grid-stride (one output window sweeping), 0 contiguous runs
+#endif
+#ifndef CAI_EDGE_ST_AUX
+#define CAI_EDGE_ST_AUX 0     // cache-policy bits of the output stores (2: nt)
+#endif
 
 __device__ __attribute__((aligned(64))) unsigned edge_zero_page[64];
 
@@ -184,70 +204,189 @@ __device__ __forceinline__ void s_store(const SPre<C>& L, char* Ss) {
 // ---------------------------------------------------------------------------
 // S (image side) -> P (feature side): conv forward, deconv input gradient.
 // Tile = 64 superpixels of one row x all N channels; wave w owns the n-tiles [w*NPW, (w+1)*NPW).
-// K = 9 taps x 16 channels in 5 k-steps of two taps (the 10th tap is zero).
+// K = 9 taps x 16 channels in 5 k-steps of two taps (the 10th tap is zero).  Persistent, tiles in
+// grid-stride order (the tiles in flight form one contiguous window of the output); the weight fragments
+// are loaded once per block and the next tile's image loads are in flight while the current tile is
+// computed.  The GEMM is the transposed one
+// (weights as A, superpixels as B): each lane holds 4 consecutive channels of one pixel and writes
+// them as one 8-byte store, no LDS round trip for the output.
 // ---------------------------------------------------------------------------
-template <int C, int NPW>
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+constexpr unsigned EOOB = 0x80000000u;   // beyond every buffer: loads return 0, stores are dropped
+
+// the 2C float2 image loads of one staged superpixel (s_load as branch-free buffer loads; every
+// thread issues all of them, so the waitcnt pass can count them past the tile's stores)
+template <int C>
+struct SPreB {
+    u32x2 q[2 * C];
+};
+
+template <int C>
+__device__ __forceinline__ void s_load_b(const EdgeArgs& A, __amdgpu_buffer_rsrc_t ir, int n, int a, int b0,
+                                         SPreB<C>& L) {
+    const int it = min((int)threadIdx.x, 3 * TBH - 1);
+    const int dyi = it / TBH, j = it - dyi * TBH;
+    const int sa = a - 1 + dyi, sb = b0 - 1 + j;
+    const bool ok = ((int)threadIdx.x < 3 * TBH) & (sa >= 0) & (sa < A.Hs) & (sb >= 0) & (sb < A.Ws);
+    const int W2 = 2 * A.Ws;
+#pragma unroll
+    for (int ci = 0; ci < C; ++ci) {
+        const unsigned off = (unsigned)((((n * C + ci) * (2 * A.Hs) + 2 * sa) * W2 + 2 * sb) * 4);
+        L.q[2 * ci] = __builtin_amdgcn_raw_buffer_load_b64(ir, ok ? off : EOOB, 0, 0);
+        L.q[2 * ci + 1] = __builtin_amdgcn_raw_buffer_load_b64(ir, ok ? off + (unsigned)W2 * 4u : EOOB, 0, 0);
+    }
+}
+
+// out-of-image superpixels arrive as zeros; the constant-1 channel is 1 everywhere (its weights are 0
+// in the forward fragments)
+template <int C>
+__device__ __forceinline__ void s_store_b(const SPreB<C>& L, char* Ss) {
+    const int it = threadIdx.x;
+    if (it >= 3 * TBH) return;
+    const int dyi = it / TBH, j = it - dyi * TBH;
+    float v[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) v[e] = 0.f;
+    v[ONES] = 1.f;
+#pragma unroll
+    for (int ci = 0; ci < C; ++ci) {
+        const float2 q0 = __builtin_bit_cast(float2, L.q[2 * ci]), q1 = __builtin_bit_cast(float2, L.q[2 * ci + 1]);
+        v[0 * C + ci] = q0.x;
+        v[1 * C + ci] = q0.y;
+        v[2 * C + ci] = q1.x;
+        v[3 * C + ci] = q1.y;
+    }
+    bf16x8 lo, hi;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        lo[e] = (bf16)v[e];
+        hi[e] = (bf16)v[8 + e];
+    }
+    *reinterpret_cast<u32x4*>(Ss + dyi * SROW + j * 32) = __builtin_bit_cast(u32x4, lo);
+    *reinterpret_cast<u32x4*>(Ss + dyi * SROW + j * 32 + 16) = __builtin_bit_cast(u32x4, hi);
+}
+
+template <int C, int NPW, int PD>
 __global__ __launch_bounds__(NT) void edge_s2d_kernel(const EdgeArgs A) {
-    constexpr int N = 64 * NPW, RS = N * 2 + 16, NTL = N / 16;
-    __shared__ __attribute__((aligned(16))) char Ss[3 * SROW];
-    __shared__ __attribute__((aligned(16))) char Ls[TB * RS];
+    constexpr int N = 64 * NPW, NTL = N / 16;
+    __shared__ __attribute__((aligned(16))) char Ss[2][3 * SROW];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g_ = lane >> 4, i16 = lane & 15;
-    // one tile per block (the neighbouring rows of a tile share an XCD's L2)
-    const int tile = xcd_remap_e((int)blockIdx.x, (int)gridDim.x);
-    const int cb = tile % A.ncb, rest = tile / A.ncb;
-    const int a = rest % A.Hs, n = rest / A.Hs;
-    const int b0 = cb * TB;
-    SPre<C> pre;
-    s_load<C>(A, n, a, b0, pre);
+    const int tiles = A.B * A.Hs * A.ncb;
+#if CAI_EDGE_S2D_GS
+    // grid-stride: the blocks' current tiles form one contiguous window of the output sweeping through it
+    const int t0 = (int)blockIdx.x, t1 = tiles, TS = (int)gridDim.x;
+#else
+    const int lb = xcd_remap_e((int)blockIdx.x, (int)gridDim.x);
+    const int per = tiles / (int)gridDim.x, extra = tiles % (int)gridDim.x;
+    const int t0 = lb * per + min(lb, extra), t1 = t0 + per + (lb < extra ? 1 : 0), TS = 1;
+#endif
+    if (t0 >= t1) return;
+    // byte sizes < 2 GiB: launch_s2d splits the batch
+    const __amdgpu_buffer_rsrc_t ir = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(A.img), (short)0, A.B * A.C * 16 * A.Hs * A.Ws, 0x00020000);
+    const __amdgpu_buffer_rsrc_t orr = __builtin_amdgcn_make_buffer_rsrc(
+        A.out_feat, (short)0, A.B * A.Hs * A.Ws * A.out_ld * 2, 0x00020000);
+    auto decode = [&](int t, int& n, int& a, int& b0) {
+        if (t >= t1) t -= TS;   // past the run: reload the last tile (harmless, keeps the load count fixed)
+        a = t % A.Hs;
+        const int rest = t / A.Hs;
+        b0 = (rest % A.ncb) * TB;
+        n = rest / A.ncb;
+    };
+    int n0, a0, b00, n1 = 0, a1 = 0, b01 = 0;
+    SPreB<C> pre0, pre1;
+    decode(t0, n0, a0, b00);
+    s_load_b<C>(A, ir, n0, a0, b00, pre0);
+    if (PD == 2) {
+        decode(t0 + TS, n1, a1, b01);
+        s_load_b<C>(A, ir, n1, a1, b01, pre1);
+    }
+    // A-operand rows of the first two n-tiles of a wave are permuted so that lane (i16, g_) ends up with
+    // channels 8*g_ .. 8*g_ + 7 of the wave's first 32 (row 4*g_ + r of tile j <-> channel 8*g_ + 4*j + r):
+    // one 16-byte store per pixel and lane.  A third tile (N = 192) keeps the natural order.
     u32x4 bw[5][NPW];
-    float bias[NPW];
+    f32x4 bias[NPW];
 #pragma unroll
     for (int j = 0; j < NPW; ++j) {
-        const int nt = wave * NPW + j;
-        bias[j] = A.bias ? A.bias[nt * 16 + i16] : 0.f;
+        int fnt, flane;   // fragment holding this lane's A row
+        if (j < 2) {
+            const int c = wave * NPW * 16 + 8 * (i16 >> 2) + 4 * j + (i16 & 3);
+            fnt = c >> 4;
+            flane = g_ * 16 + (c & 15);
+        } else {
+            fnt = wave * NPW + j;
+            flane = lane;
+        }
 #pragma unroll
-        for (int ks = 0; ks < 5; ++ks) bw[ks][j] = A.frag[(ks * NTL + nt) * 64 + lane];
+        for (int r = 0; r < 4; ++r) {
+            const int c = j < 2 ? wave * NPW * 16 + 8 * g_ + 4 * j + r : (wave * NPW + j) * 16 + 4 * g_ + r;
+            bias[j][r] = A.bias ? A.bias[c] : 0.f;
+        }
+#pragma unroll
+        for (int ks = 0; ks < 5; ++ks) bw[ks][j] = A.frag[(ks * NTL + fnt) * 64 + flane];
     }
-    s_store<C>(pre, Ss);
-    __syncthreads();
-    f32x4 acc[4][NPW];
+    // weights and first tiles landed: inside the loop the only outstanding operations are the next
+    // tiles' loads and the stores (the loop-header merge would otherwise wait for them all)
+    wait_vmcnt<0>();
+    // one tile: stage its superpixels, put the load of tile t + PD in flight, MFMAs, 8-byte stores
+    auto tile = [&](char* S, SPreB<C>& P, int& n, int& a, int& b0, int t) {
+        s_store_b<C>(P, S);
+        __syncthreads();
+        const int tn = n, ta = a, tb0 = b0;
+        decode(t + PD * TS, n, a, b0);
+        if (!(CAI_EDGE_PROBE & 2)) s_load_b<C>(A, ir, n, a, b0, P);
+        f32x4 acc[4][NPW];
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
+        for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int j = 0; j < NPW; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < NPW; ++j) acc[m][j] = bias[j];
 #pragma unroll
-    for (int ks = 0; ks < 5; ++ks) {
-        const int t = 2 * ks + (g_ >> 1);
-        const int tt = t < 9 ? t : 4;
-        const int off = (tt / 3) * SROW + (tt % 3) * 32 + 16 * (g_ & 1);
+        for (int ks = 0; ks < 5; ++ks) {
+            const int tap = 2 * ks + (g_ >> 1);
+            const int tt = tap < 9 ? tap : 4;
+            const int off = (tt / 3) * SROW + (tt % 3) * 32 + 16 * (g_ & 1);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                u32x4 av = *reinterpret_cast<const u32x4*>(S + off + (16 * m + i16) * 32);
+                if (tap > 8) av = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int j = 0; j < NPW; ++j) acc[m][j] = mma16<bf16>(bw[ks][j], av, acc[m][j]);
+            }
+        }
+        if ((CAI_EDGE_PROBE & 1) && A.Hs > 0) return;   // probe: stores skipped at run time, code kept
+        const int rowoff = ((tn * A.Hs + ta) * A.Ws + tb0) * A.out_ld;
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
-            u32x4 av = *reinterpret_cast<const u32x4*>(Ss + off + (16 * m + i16) * 32);
-            if (t > 8) av = u32x4{0u, 0u, 0u, 0u};
+            const int px = 16 * m + i16;
+            const bool ok = tb0 + px < A.Ws;
+            {
+                bf16x8 h;
 #pragma unroll
-            for (int j = 0; j < NPW; ++j) acc[m][j] = mma16<bf16>(av, bw[ks][j], acc[m][j]);
-        }
-    }
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int j = 0; j < NPW; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int px = 16 * m + 4 * g_ + r, col = (wave * NPW + j) * 16 + i16;
-                *reinterpret_cast<bf16*>(Ls + px * RS + col * 2) = (bf16)(acc[m][j][r] + bias[j]);
+                for (int r = 0; r < 4; ++r) {
+                    h[r] = (bf16)acc[m][0][r];
+                    h[4 + r] = (bf16)acc[m][1][r];
+                }
+                const unsigned off = (unsigned)((rowoff + px * A.out_ld + wave * NPW * 16 + 8 * g_) * 2);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, h), orr, ok ? off : EOOB, 0, CAI_EDGE_ST_AUX);
             }
-    __syncthreads();
-    const int npx = min(TB, A.Ws - b0);
-    bf16* dst = A.out_feat + ((int64_t)n * A.Hs + a) * A.Ws * A.out_ld;
+            if (NPW == 3) {
+                bf16x4 h;
 #pragma unroll
-    for (int i = 0; i < TB * (N / 8) / NT; ++i) {
-        const int c = threadIdx.x + i * NT;
-        const int px = c / (N / 8), part = c - px * (N / 8);
-        if (px < npx)
-            *reinterpret_cast<u32x4*>(dst + (int64_t)(b0 + px) * A.out_ld + part * 8) =
-                *reinterpret_cast<const u32x4*>(Ls + px * RS + part * 16);
+                for (int r = 0; r < 4; ++r) h[r] = (bf16)acc[m][NPW - 1][r];
+                const unsigned off =
+                    (unsigned)((rowoff + px * A.out_ld + (wave * NPW + NPW - 1) * 16 + 4 * g_) * 2);
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, h), orr, ok ? off : EOOB, 0, CAI_EDGE_ST_AUX);
+            }
+        }
+    };
+    for (int t = t0; t < t1; t += PD * TS) {
+        tile(Ss[0], pre0, n0, a0, b00, t);
+        if (PD == 2 && t + TS < t1) tile(Ss[1], pre1, n1, a1, b01, t + TS);
+        if (PD == 1 && t + TS < t1) {   // alternate the staging buffer
+            tile(Ss[1], pre0, n0, a0, b00, t + TS);
+            t += TS;
+        }
     }
 }
 
@@ -749,13 +888,40 @@ WgradWs wgrad_ws(const EdgeArgs& A) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// persistent blocks per CU of the s2d kernel (A/B knob CAI_EDGE_S2D_BPC, read once; 0: one tile per block)
+int s2d_blocks_per_cu() {
+    static const int v = [] {
+        const char* e = std::getenv("CAI_EDGE_S2D_BPC");
+        return e ? std::max(0, std::atoi(e)) : 3;
+    }();
+    return v;
+}
+
 template <int C>
 void launch_s2d(const EdgeArgs& A, hipStream_t st) {
-    const int tiles = A.B * A.Hs * A.ncb;
-    if (A.N == 128)
-        edge_s2d_kernel<C, 2><<<tiles, NT, 0, st>>>(A);
-    else
-        edge_s2d_kernel<C, 3><<<tiles, NT, 0, st>>>(A);
+    const int bpc = s2d_blocks_per_cu();
+    // the kernel addresses image and output with 32-bit byte offsets: batches of < 2 GiB each
+    const int64_t per_img = std::max<int64_t>((int64_t)A.C * 16 * A.Hs * A.Ws, (int64_t)A.Hs * A.Ws * A.out_ld * 2);
+    const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(A.B, ((int64_t)1 << 31) / 2 / per_img));
+    for (int b = 0; b < A.B; b += nb) {
+        EdgeArgs P = A;
+        P.B = std::min(nb, A.B - b);
+        P.img = A.img + (int64_t)b * A.C * 4 * A.Hs * A.Ws;
+        P.out_feat = A.out_feat + (int64_t)b * A.Hs * A.Ws * A.out_ld;
+        const int pt = P.B * P.Hs * P.ncb;
+        const int grid = bpc == 0 ? pt : std::min(pt, 256 * bpc);
+        if (CAI_EDGE_S2D_PD == 2) {
+            if (A.N == 128)
+                edge_s2d_kernel<C, 2, 2><<<grid, NT, 0, st>>>(P);
+            else
+                edge_s2d_kernel<C, 3, 2><<<grid, NT, 0, st>>>(P);
+        } else {
+            if (A.N == 128)
+                edge_s2d_kernel<C, 2, 1><<<grid, NT, 0, st>>>(P);
+            else
+                edge_s2d_kernel<C, 3, 1><<<grid, NT, 0, st>>>(P);
+        }
+    }
 }
 
 template <int C>

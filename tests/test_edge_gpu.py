@@ -31,12 +31,15 @@ CONV = [  # B, C, N, H, W, k  (image H x W, feature grid H/2 x W/2)
     (2, 1, 128, 32, 34, 3),
     (3, 2, 192, 20, 132, 1),
     (2, 3, 128, 256, 256, 5),
+    (8, 3, 128, 256, 256, 5),     # more tiles than resident blocks: several tiles per persistent block
+    (6, 3, 192, 200, 330, 5),     # ragged column blocks, several tiles per block
 ]
 DECONV = [  # B, N, C, H, W, k  (feature grid H x W, image 2H x 2W)
     (2, 128, 3, 32, 32, 5),
     (2, 192, 3, 20, 33, 5),
     (2, 128, 1, 17, 70, 3),
     (1, 128, 3, 128, 128, 5),
+    (4, 128, 3, 128, 128, 5),     # input-gradient tiles > resident blocks
 ]
 
 
