@@ -19,7 +19,7 @@ F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_LEAKY = 0, 1, 2
 MASK_NONE, MASK_POS, MASK_LEAKY, MASK_SIGN = 0, 1, 2, 3
 Q_NOISE, Q_DEQUANTIZE, Q_SYMBOLS = 0, 1, 2
-ADAM_CLIP, ADAM_SKIP_NONFINITE = 1, 2          # cai_adam_step flags (include/cai.h)
+ADAM_CLIP, ADAM_SKIP_NONFINITE, ADAM_ZERO_GRAD = 1, 2, 4          # cai_adam_step flags (include/cai.h)
 ADAM_SMALL_N = 1 << 16                         # cai_adam_step: one-block path at or below this many parameters
 
 
@@ -119,6 +119,7 @@ SIGNATURES = {
     "cai_gdn_backward_workspace_bytes": (_S, [_I64, c_int32, _I]),
     "cai_gdn_backward": (_I, [_I, _P, c_int32, _P, c_int32, _I64, c_int32, _P, _P, c_int32, _P, c_int32, _P, _P, _F, _F,
                               _P, _P, c_int32, _P, _S, _P]),
+    "cai_uniform_noise": (_I, [_P, _I64, _P, _P]),
     "cai_quantize": (_I, [_I, _I64, c_int32, _P, _I, c_int32, _P, c_int32, c_int32, _P, c_int32, _P, _I, c_int32, _P]),
     "cai_gc_fwd": (_I, [_I, _I64, c_int32, _P, _I, c_int32, _P, c_int32, _P, c_int32, _I, _P, c_int32, _F, _F,
                         _P, _I, c_int32, _P, c_int32, _P]),

@@ -6,8 +6,13 @@ buffers, constructor arguments, ValueError checks and the
 ``forward(...) -> (outputs, likelihoods)`` contract are kept; the forward
 and backward of the likelihood path are single fused kernels
 (cai_eb_fwd/_bwd, cai_gc_fwd/_bwd) instead of ~40 small torch ops, and
-training-mode noise is U(-1/2, 1/2) drawn with torch's generator exactly like
-the reference (``empty_like(x).uniform_(-0.5, 0.5)``), consumed by the kernel.
+training-mode noise is U(-1/2, 1/2) as in the reference
+(``empty_like(x).uniform_(-0.5, 0.5)``, entropy_models.py:170), drawn on the
+device by cai_uniform_noise (Philox4x32-10, counter kept in device memory: a
+captured graph draws new noise on every replay without torch's generator and
+its per-replay re-seeding launches); seeded from torch.cuda.initial_seed(), so
+torch.cuda.manual_seed() keeps runs reproducible.  Tests inject their own
+draws (set_noise_source) to compare against the CPU oracle.
 
 The bitstream side follows the reference too:
 update() evaluates the pmfs with the reference's torch expressions on the
@@ -20,6 +25,7 @@ decompress() decodes them (cai_rans_decode_batch) and dequantizes.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Any, Callable, List, Optional, Tuple, Union
 
 import numpy as np
@@ -33,7 +39,7 @@ from .._native import F32, Q_DEQUANTIZE, Q_NOISE, Q_SYMBOLS, lib
 from .._ops import BottleneckAuxFn, BottleneckFn, GaussianFn, _check_cuda, _p, _stream, as_rows, dcode, empty_rows_like
 from ..ops import LowerBound
 
-__all__ = ["EntropyModel", "EntropyBottleneck", "GaussianConditional", "set_noise_source"]
+__all__ = ["EntropyModel", "EntropyBottleneck", "GaussianConditional", "set_noise_source", "seed_noise"]
 
 # ---------------------------------------------------------------------------
 # noise source: torch's generator by default; tests inject identical tensors
@@ -48,13 +54,62 @@ def set_noise_source(fn: Optional[Callable[[torch.Tensor], torch.Tensor]]):
     _noise_source = fn
 
 
+# on-device generator state per GPU: [seed, draw index, arrival ticket] (uint64 bit patterns)
+_noise_states: dict = {}
+# A/B knob (read once): CAI_TORCH_NOISE=1 draws with torch's generator instead (`uniform_`, as the reference)
+_TORCH_NOISE = os.environ.get("CAI_TORCH_NOISE", "0") == "1"
+
+
+def _as_i64(v: int) -> int:
+    v &= (1 << 64) - 1
+    return v - (1 << 64) if v >= (1 << 63) else v
+
+
+def seed_noise(seed: int, device=None) -> None:
+    """Seed the training-noise generator of `device` (default: the current GPU) and restart its stream."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    st = _noise_states.get(idx)
+    if st is None:
+        st = [None, None]
+        _noise_states[idx] = st
+    if st[0] is None:
+        st[0] = torch.zeros(3, dtype=torch.int64, device=torch.device("cuda", idx))
+    st[0].copy_(torch.tensor([_as_i64(seed), 0, 0], dtype=torch.int64))
+    with torch.cuda.device(idx):
+        st[1] = torch.cuda.initial_seed()   # torch's seed at this point: a later manual_seed() re-seeds
+
+
+def _noise_state(dev: torch.device) -> torch.Tensor:
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    st = _noise_states.get(idx)
+    seed = None
+    if not torch.cuda.is_current_stream_capturing():
+        with torch.cuda.device(idx):
+            seed = torch.cuda.initial_seed()
+    # (re)seed on first use and whenever torch.cuda.manual_seed() changed the device seed (eager mode; a
+    # capture keeps the state it finds)
+    if st is None and seed is None:
+        raise RuntimeError("training noise: run one eager training-mode forward (or call seed_noise()) before "
+                           "capturing a graph; the generator state must exist outside the capture")
+    if st is None or (seed is not None and seed != st[1]):
+        seed_noise(seed, torch.device("cuda", idx))
+        st = _noise_states[idx]
+    return st[0]
+
+
 def _draw_noise(x: torch.Tensor) -> torch.Tensor:
     if _noise_source is not None:
         n = _noise_source(x)
         if tuple(n.shape) != tuple(x.shape):
             raise ValueError(f"noise source returned shape {tuple(n.shape)}, expected {tuple(x.shape)}")
         return n.to(device=x.device, dtype=torch.float32)
-    return torch.empty_like(x, dtype=torch.float32).uniform_(-0.5, 0.5)
+    if _TORCH_NOISE:
+        return torch.empty_like(x, dtype=torch.float32).uniform_(-0.5, 0.5)
+    _check_cuda(x)
+    out = torch.empty_like(x, dtype=torch.float32)   # dense storage: numel() values from data_ptr()
+    lib.cai_uniform_noise(_p(out), out.numel(), _p(_noise_state(x.device)), _stream())
+    return out
 
 
 class _QuantizeFn(torch.autograd.Function):

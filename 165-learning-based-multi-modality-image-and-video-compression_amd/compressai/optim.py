@@ -30,7 +30,7 @@ from typing import Iterable, List, Optional, Tuple
 import torch
 
 from . import _ledger
-from ._native import ADAM_CLIP, ADAM_SKIP_NONFINITE, ADAM_SMALL_N, lib
+from ._native import ADAM_CLIP, ADAM_SKIP_NONFINITE, ADAM_SMALL_N, ADAM_ZERO_GRAD, lib
 from ._ops import DIRECT_GRAD_ATTR, _p, _stream
 
 
@@ -40,10 +40,15 @@ def _align(n: int, a: int = 4) -> int:
 
 class FusedAdam(torch.optim.Optimizer):
     def __init__(self, params: Iterable[torch.nn.Parameter], lr: float = 1e-3, betas: Tuple[float, float] = (0.9, 0.999),
-                 eps: float = 1e-8, skip_nonfinite: bool = True, layout: Optional[List[int]] = None):
+                 eps: float = 1e-8, skip_nonfinite: bool = True, layout: Optional[List[int]] = None,
+                 zero_grad_in_step: bool = False):
         """layout: optional permutation of the parameter indices giving their order in the flat buffers
         (param_groups / state_dict keep the given order); distributed.OverlappedAllReduce puts the
-        parameters whose gradients finish last at the end so the rest can be exchanged early."""
+        parameters whose gradients finish last at the end so the rest can be exchanged early.
+
+        zero_grad_in_step: step() consumes the gradients (the Adam kernel zeroes each one as it reads it)
+        and zero_grad() right after a step() launches nothing.  For the reference's loop order
+        (zero_grad, forward, backward, step: train.py:172-186); p.grad reads zero after step()."""
         params = [p for p in params]
         if not params:
             raise ValueError("optimizer got an empty parameter list")
@@ -61,6 +66,8 @@ class FusedAdam(torch.optim.Optimizer):
         if dev.type != "cuda":
             raise ValueError("FusedAdam runs on GPU parameters only")
         self.skip_nonfinite = bool(skip_nonfinite)
+        self.zero_grad_in_step = bool(zero_grad_in_step)
+        self._grads_consumed = False
         order = list(range(len(self.params))) if layout is None else [int(i) for i in layout]
         if sorted(order) != list(range(len(self.params))):
             raise ValueError("layout must be a permutation of the parameter indices")
@@ -130,8 +137,11 @@ class FusedAdam(torch.optim.Optimizer):
             p.grad = v
 
     def zero_grad(self, set_to_none: bool = True):
-        # the gradients stay views of the flat buffer; set_to_none zeroes them instead of unlinking them
-        self.flat_grad.zero_()
+        # the gradients stay views of the flat buffer; set_to_none zeroes them instead of unlinking them.
+        # Right after a consuming step() they are zero already.
+        if not self._grads_consumed:
+            self.flat_grad.zero_()
+        self._grads_consumed = False
         self._attach_views()
 
     def grad_sqnorm(self) -> torch.Tensor:
@@ -149,6 +159,8 @@ class FusedAdam(torch.optim.Optimizer):
         self._sync_grad_views()
         clip = max_norm is not None and max_norm > 0
         flags = (ADAM_CLIP if clip else 0) | (ADAM_SKIP_NONFINITE if self.skip_nonfinite else 0)
+        zero = self.zero_grad_in_step and (flags or self.numel <= ADAM_SMALL_N)
+        flags |= ADAM_ZERO_GRAD if zero else 0
         g = self.param_groups[0]
         b1, b2 = g["betas"]
         # norm + clip + Adam + step count in 2 launches (1 for small buffers): cai_adam_step; self.sqnorm
@@ -162,6 +174,7 @@ class FusedAdam(torch.optim.Optimizer):
                     "adam", "adam_small_kernel" if small else "sq_part + adam_fused_kernel", 2.0 * self.numel if flags
                     else 0.0, 32 * self.numel if flags else 28 * self.numel, torch.float32,
                     f"{self.numel} parameters")
+        self._grads_consumed = zero
         return loss
 
     # -- checkpoints in torch.optim.Adam's format (train.py:407,419,475) -------------------------------
@@ -226,16 +239,18 @@ def parameter_groups(net):
     return main, aux
 
 
-def configure_optimizers(net, lr: float = 1e-4, aux_lr: float = 1e-3, tail: Tuple[str, ...] = ()):
+def configure_optimizers(net, lr: float = 1e-4, aux_lr: float = 1e-3, tail: Tuple[str, ...] = (),
+                         zero_grad_in_step: bool = False):
     """train.py:111-142: main Adam on all but `.quantiles`, aux Adam on `.quantiles` (sorted by name).
 
     tail: name prefixes whose parameters go last in the main flat buffers (FusedAdam layout); the
-    optimizer's ``tail_offset`` is where they start (distributed.OverlappedAllReduce)."""
+    optimizer's ``tail_offset`` is where they start (distributed.OverlappedAllReduce).
+    zero_grad_in_step: see FusedAdam (both optimizers)."""
     named = dict(net.named_parameters())
     main, aux = parameter_groups(net)
     is_tail = [any(n.startswith(t) for t in tail) for n in main]
     layout = [i for i, t in enumerate(is_tail) if not t] + [i for i, t in enumerate(is_tail) if t]
-    opt = FusedAdam((named[n] for n in main), lr=lr, layout=layout)
+    opt = FusedAdam((named[n] for n in main), lr=lr, layout=layout, zero_grad_in_step=zero_grad_in_step)
     tails = [opt.offsets[i] for i, t in enumerate(is_tail) if t]
     opt.tail_offset = min(tails) if tails else opt.numel
-    return opt, FusedAdam((named[n] for n in aux), lr=aux_lr)
+    return opt, FusedAdam((named[n] for n in aux), lr=aux_lr, zero_grad_in_step=zero_grad_in_step)

@@ -99,12 +99,21 @@ __global__ __launch_bounds__(256) void sq_part_kernel(const float* __restrict__ 
     }
 }
 
-__device__ __forceinline__ void adam_range(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+// zero_g: the gradient buffer is consumed -- each element is overwritten with 0 once read (CAI_ADAM_ZERO_GRAD:
+// the next backward then needs no zero-fill launch)
+__device__ __forceinline__ void zero_range(float* __restrict__ g, int64_t n, int64_t i0, int64_t stride) {
+    const int64_t n4 = n / 4;
+    for (int64_t i = i0; i < n4; i += stride) reinterpret_cast<f32x4*>(g)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int64_t i = n4 * 4 + i0; i < n; i += stride) g[i] = 0.f;
+}
+
+__device__ __forceinline__ void adam_range(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                                            float* __restrict__ v, int64_t n, int64_t i0, int64_t stride, float scale,
-                                           float b1, float b2, float eps, float step_size, float bc2s) {
+                                           float b1, float b2, float eps, float step_size, float bc2s, bool zero_g) {
     const int64_t n4 = n / 4;
     for (int64_t i = i0; i < n4; i += stride) {
         f32x4 gv = reinterpret_cast<const f32x4*>(g)[i] * scale;
+        if (zero_g) reinterpret_cast<f32x4*>(g)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
         f32x4 mv = reinterpret_cast<f32x4*>(m)[i];
         f32x4 vv = reinterpret_cast<f32x4*>(v)[i];
         f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
@@ -120,38 +129,41 @@ __device__ __forceinline__ void adam_range(float* __restrict__ p, const float* _
     }
     for (int64_t i = n4 * 4 + i0; i < n; i += stride) {
         const float gv = g[i] * scale;
+        if (zero_g) g[i] = 0.f;
         m[i] = b1 * m[i] + (1.f - b1) * gv;
         v[i] = b2 * v[i] + (1.f - b2) * gv * gv;
         p[i] -= step_size * m[i] / (sqrtf(v[i]) / bc2s + eps);
     }
 }
 
-__global__ __launch_bounds__(256) void adam_fused_kernel(float* __restrict__ p, const float* __restrict__ g,
+__global__ __launch_bounds__(256) void adam_fused_kernel(float* __restrict__ p, float* __restrict__ g,
                                                          float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                          float lr, float b1, float b2, float eps, float* step,
                                                          const float* __restrict__ part, int nparts,
-                                                         float* __restrict__ sqnorm_out, float max_norm) {
+                                                         float* __restrict__ sqnorm_out, float max_norm, int zero_g) {
     __shared__ float red[4];
     float acc = 0.f;
     for (int i = threadIdx.x; i < nparts; i += 256) acc += part[i];
     const float sq = block_sum_all<256>(acc, red);
     const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
     if (lead && sqnorm_out) *sqnorm_out = sq;
+    const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
     if (!isfinite(sq)) {
         if (lead) *step -= 1.f;   // no block reads the count on this path
+        if (zero_g) zero_range(g, n, i0, stride);
         return;
     }
     const float t = *step;       // counted by sq_part_kernel
     const float coef = max_norm / (sqrtf(sq) + 1e-6f);
-    adam_range(p, g, m, v, n, blockIdx.x * (int64_t)blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x,
-               coef < 1.f ? coef : 1.f, b1, b2, eps, lr / (1.f - powf(b1, t)), sqrtf(1.f - powf(b2, t)));
+    adam_range(p, g, m, v, n, i0, stride, coef < 1.f ? coef : 1.f, b1, b2, eps, lr / (1.f - powf(b1, t)),
+               sqrtf(1.f - powf(b2, t)), zero_g != 0);
 }
 
-__global__ __launch_bounds__(1024) void adam_small_kernel(float* __restrict__ p, const float* __restrict__ g,
+__global__ __launch_bounds__(1024) void adam_small_kernel(float* __restrict__ p, float* __restrict__ g,
                                                           float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                           float lr, float b1, float b2, float eps, float* step,
                                                           float* __restrict__ sqnorm_out, float max_norm,
-                                                          int use_norm) {
+                                                          int use_norm, int zero_g) {
     __shared__ float red[16];
     float scale = 1.f;
     if (use_norm) {
@@ -159,14 +171,17 @@ __global__ __launch_bounds__(1024) void adam_small_kernel(float* __restrict__ p,
         for (int64_t i = threadIdx.x; i < n; i += 1024) acc += g[i] * g[i];
         const float sq = block_sum_all<1024>(acc, red);
         if (threadIdx.x == 0 && sqnorm_out) *sqnorm_out = sq;
-        if (!isfinite(sq)) return;
+        if (!isfinite(sq)) {
+            if (zero_g) zero_range(g, n, threadIdx.x, 1024);   // the norm pass read g: block_sum_all synced
+            return;
+        }
         const float coef = max_norm / (sqrtf(sq) + 1e-6f);
         scale = coef < 1.f ? coef : 1.f;
     }
     const float t = *step + 1.f;
     __syncthreads();             // every thread has read the count before thread 0 advances it
     adam_range(p, g, m, v, n, threadIdx.x, 1024, scale, b1, b2, eps, lr / (1.f - powf(b1, t)),
-               sqrtf(1.f - powf(b2, t)));
+               sqrtf(1.f - powf(b2, t)), zero_g != 0);
     if (threadIdx.x == 0) *step = t;
 }
 
@@ -178,7 +193,7 @@ extern "C" {
 
 const char* cai_last_error(void) { return g_err; }
 int cai_version(void) { return 1; }
-int cai_abi_count(void) { return 75; }
+int cai_abi_count(void) { return 76; }
 
 int cai_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps,
              float* step, const float* sqnorm, float max_norm, void* stream) {
@@ -198,19 +213,21 @@ int cai_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, 
 
 size_t cai_adam_step_workspace_bytes(int64_t n) { return (size_t)sq_parts(n) * sizeof(float); }
 
-int cai_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
+int cai_adam_step(float* p, float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
                   float eps, float* step, float* sqnorm, float max_norm, int32_t flags, void* workspace,
                   size_t ws_bytes, void* stream) {
     CAI_CHECK_ARG(p && g && m && v && step && n >= 0, "adam_step: bad arguments");
     CAI_CHECK_ARG(((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16 == 0,
                   "adam_step: buffers must be 16-byte aligned");
     const bool clip = (flags & CAI_ADAM_CLIP) != 0, use_norm = clip || (flags & CAI_ADAM_SKIP_NONFINITE);
+    const int zero_g = (flags & CAI_ADAM_ZERO_GRAD) ? 1 : 0;
     const float mn = clip ? max_norm : INFINITY;
     hipStream_t st = as_stream(stream);
     if (n <= ADAM_SMALL_N) {
         hipLaunchKernelGGL(adam_small_kernel, dim3(1), dim3(1024), 0, st, p, g, m, v, n, lr, beta1, beta2, eps, step,
-                           sqnorm, mn, (int)use_norm);
+                           sqnorm, mn, (int)use_norm, zero_g);
     } else if (!use_norm) {
+        CAI_CHECK_ARG(!zero_g, "adam_step: ZERO_GRAD needs CLIP or SKIP_NONFINITE above the one-block size");
         return cai_adam(p, g, m, v, n, lr, beta1, beta2, eps, step, nullptr, INFINITY, stream);
     } else {
         CAI_CHECK_ARG(workspace && ws_bytes >= cai_adam_step_workspace_bytes(n), "adam_step: workspace too small");
@@ -220,7 +237,7 @@ int cai_adam_step(float* p, const float* g, float* m, float* v, int64_t n, float
         int64_t blocks = (n / 4 + 255) / 256;
         blocks = blocks > 2048 ? 2048 : (blocks < 1 ? 1 : blocks);
         hipLaunchKernelGGL(adam_fused_kernel, dim3((unsigned)blocks), dim3(256), 0, st, p, g, m, v, n, lr, beta1,
-                           beta2, eps, step, part, np, sqnorm, mn);
+                           beta2, eps, step, part, np, sqnorm, mn, zero_g);
     }
     CAI_LAUNCH_CHECK("adam_step");
     return CAI_OK;

@@ -71,6 +71,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-batch", type=int, default=None, help="CPU baseline batch (default: the GPU per-step batch)")
     ap.add_argument("--no-profile", action="store_true", help="skip the profiled step (no roofline fields)")
+    ap.add_argument("--keep-grads", action="store_true",
+                    help="A/B: optimizers without zero_grad_in_step (zero_grad() fills the gradient buffers)")
     ap.add_argument("--ops-json", default=None, help="write the profiled step's per-launch table here")
     ap.add_argument("--roofline-only", action="store_true",
                     help="profile one step, then replay only its dominant launch --steps times "
@@ -307,7 +309,9 @@ def main():
     # N > 1: the gradient exchange in two buckets, the first overlapped with the analysis transform's
     # backward (compressai.distributed.OverlappedAllReduce); Master_compresser keeps the single exchange
     overlap = world > 1 and not multimodal and hasattr(net, "g_a") and not args.serial_allreduce
-    opt, aux_opt = configure_optimizers(net, tail=("g_a.",) if overlap else ())
+    # the reference loop order (zero_grad, forward, backward, step): the Adam kernels consume the gradients
+    # and zero_grad() launches nothing (FusedAdam zero_grad_in_step)
+    opt, aux_opt = configure_optimizers(net, tail=("g_a.",) if overlap else (), zero_grad_in_step=not args.keep_grads)
     sync = None
     if overlap:
         head = [p for n, p in net.named_parameters() if not n.startswith("g_a.") and not n.endswith(".quantiles")]

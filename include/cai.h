@@ -332,6 +332,13 @@ int cai_gdn_backward(int dtype, const void* x, int32_t x_ld, const void* dy, int
 /* =======================================================================
  * Entropy models.  Element (p, c) of every operand at ptr[p*ld + c].
  * ======================================================================= */
+/* Training noise: out[0..n) = U(-1/2, 1/2) (fp32, 24-bit mantissas), Philox4x32-10 keyed by state[0] (the
+ * seed) with counter (element quad, state[1]).  state: 3 uint64 in device memory, caller-owned, state[2]
+ * zero before the first call; every call advances state[1] by one on the device (its last block to finish),
+ * so a captured graph draws fresh noise on each replay.  Replaces the reference's
+ * torch.empty_like(x).uniform_(-0.5, 0.5) (entropy_models.py:170) -- same distribution, its own stream. */
+int cai_uniform_noise(float* out, int64_t n, unsigned long long* state, void* stream);
+
 /* quantize: NOISE  out = x + noise  (noise required, fp32 ld noise_ld)
  *           DEQUANTIZE out = rint(x - means) + means  (means nullable)
  *           SYMBOLS    out(int32) = (int)rint(x - means)
@@ -452,11 +459,14 @@ int cai_adam(float* p, const float* g, float* m, float* v, int64_t n,
  * flags CAI_ADAM_CLIP scales the grads by min(1, max_norm / (||g|| + 1e-6)) (clip_grad_norm_),
  * CAI_ADAM_SKIP_NONFINITE skips the step on a non-finite norm (either flag computes the norm; a
  * non-finite norm always skips, as cai_adam).  *sqnorm (nullable) receives sum(g^2).  Same update
- * and step counting as cai_sqnorm + cai_adam.  Workspace >= cai_adam_step_workspace_bytes(n). */
+ * and step counting as cai_sqnorm + cai_adam.  CAI_ADAM_ZERO_GRAD consumes the gradients: g is left
+ * all zero (skipped step included), so the next backward needs no zero-fill (with n > 65536 it needs
+ * CLIP or SKIP_NONFINITE).  Workspace >= cai_adam_step_workspace_bytes(n). */
 #define CAI_ADAM_CLIP 1
 #define CAI_ADAM_SKIP_NONFINITE 2
+#define CAI_ADAM_ZERO_GRAD 4
 size_t cai_adam_step_workspace_bytes(int64_t n);
-int cai_adam_step(float* p, const float* g, float* m, float* v, int64_t n,
+int cai_adam_step(float* p, float* g, float* m, float* v, int64_t n,
                   float lr, float beta1, float beta2, float eps,
                   float* step, float* sqnorm, float max_norm, int32_t flags,
                   void* workspace, size_t ws_bytes, void* stream);

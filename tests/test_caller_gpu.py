@@ -260,3 +260,24 @@ def test_fused_adam_skips_nonfinite_step(cuda, large):
         assert torch.equal(a.detach(), b)
     assert torch.equal(opt.exp_avg, m_before)
     assert float(opt.step_count.item()) == 1.0
+
+
+@pytest.mark.parametrize("large", [False, True], ids=["one-block", "two-launch"])
+def test_fused_adam_skipped_step_consumes_grads(cuda, large):
+    """zero_grad_in_step: a skipped (non-finite) step still leaves the gradient buffer zeroed, so the next
+    zero_grad() (which then launches nothing) starts the following backward from zero."""
+    from compressai.optim import FusedAdam
+
+    shapes, _, pb = _param_set(cuda, large=large)
+    opt = FusedAdam(pb, lr=1e-2, zero_grad_in_step=True)
+    opt.zero_grad()
+    for p in pb:
+        p.grad.fill_(0.5)
+    pb[1].grad[3] = float("nan")
+    before = [p.detach().clone() for p in pb]
+    opt.step(max_norm=1.0)
+    opt.zero_grad()
+    torch.cuda.synchronize()
+    assert float(opt.step_count.item()) == 0.0
+    assert all(torch.equal(a.detach(), b) for a, b in zip(pb, before))
+    assert float(opt.flat_grad.abs().max()) == 0.0

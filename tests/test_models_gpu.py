@@ -121,10 +121,13 @@ def test_optimizer_step_parity(cuda, name):
     assert diffs.median().item() < 1e-3 * lr
 
 
+@pytest.mark.parametrize("zg", [False, True], ids=["keep-grads", "zero-grad-in-step"])
 @pytest.mark.parametrize("large", [False, True], ids=["one-block", "two-launch"])
-def test_fused_adam_matches_torch_adam(cuda, large):
+def test_fused_adam_matches_torch_adam(cuda, large, zg):
     """FusedAdam(+clip) == torch.optim.Adam + clip_grad_norm_ on identical gradients, on both launch paths of
-    cai_adam_step (<= 65536 parameters: one block; above: norm partials + fused update)."""
+    cai_adam_step (<= 65536 parameters: one block; above: norm partials + fused update), with and without
+    the step consuming (zeroing) the gradients (zero_grad_in_step: zero_grad() then launches nothing and
+    the next backward accumulates into the zeroed buffer)."""
     from compressai.optim import FusedAdam
 
     torch.manual_seed(9)
@@ -132,17 +135,19 @@ def test_fused_adam_matches_torch_adam(cuda, large):
     ref = [torch.nn.Parameter(torch.randn(s)) for s in shapes]
     dev = [torch.nn.Parameter(p.detach().clone().to(cuda)) for p in ref]
     opt_r = torch.optim.Adam(ref, lr=1e-3)
-    opt = FusedAdam(dev, lr=1e-3)
+    opt = FusedAdam(dev, lr=1e-3, zero_grad_in_step=zg)
     for it in range(5):
         grads = [torch.randn(s) * (10.0 if it % 2 else 0.01) for s in shapes]
         for p, g in zip(ref, grads):
             p.grad = g.clone()
         opt.zero_grad()
         for p, g in zip(dev, grads):
-            p.grad.copy_(g)
+            p.grad.add_(g.to(cuda))          # accumulate, as a backward does
         torch.nn.utils.clip_grad_norm_(ref, 1.0)
         opt_r.step()
         opt.step(max_norm=1.0)
+        if zg:
+            assert float(opt.flat_grad.abs().max()) == 0.0
     for a, b in zip(dev, ref):
         assert (a.detach().cpu() - b.detach()).abs().max().item() < 1e-6
 
