@@ -31,6 +31,7 @@
 #include "mfma.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <vector>
 
 namespace cai {
@@ -68,6 +69,8 @@ struct ConvArgs {
     int ksplit;              // K splits per phase (grid.z = nphase * ksplit)
     float* ws;               // split-K partials [nphase*ksplit][ws_rows][ws_ld] fp32
     int ws_rows, ws_ld;
+    int cnt;                 // split-K fold: 1 + the first per-tile arrival counter in cai_splitk_cnt (0, as
+                             // zero-initialised: a reduce launch sums the slabs)
     PhaseDesc ph[4];
 };
 
@@ -150,6 +153,70 @@ __device__ __forceinline__ void store_out_scalar(const ConvArgs& a, const PhaseD
     st_any(a.y, a.y_dtype, (int64_t)b * a.ysb + (int64_t)n * a.ysc + (int64_t)oy * a.ysy + (int64_t)ox * a.ysx, v);
 }
 
+// Split-K fold: after a block has written its partial tile, the block that completes the tile's last split
+// sums the tile's ksplit slabs in split order -- the order and arithmetic of conv_splitk_reduce_kernel, so
+// the output is bit-identical -- and runs the epilogue (bias, act, mask, store).  Release: every thread
+// fences its partial stores at agent scope before thread 0 counts the arrival; the last block fences again
+// before reading the other blocks' slabs (they were written through other XCDs' L2).  The counter is reset
+// by the last block, ready for the next launch / graph replay.  Tile index: the grid position with the
+// split factored out of z (z = phase * ksplit + split in every split-K conv grid).
+constexpr unsigned SPLITK_POOL = 1u << 20;
+__device__ unsigned cai_splitk_cnt[SPLITK_POOL];
+
+template <typename T, int BM, int BN, int NTH, class RowMap>
+__device__ __forceinline__ void splitk_fold(const ConvArgs& a, const PhaseDesc& P, int plane, int n0, RowMap rowm,
+                                            int slab) {
+    __shared__ int s_last;
+    // every wave's partial stores complete (in its XCD's L2) before the barrier; one wave then releases the
+    // L2 at agent scope (one write-back per block instead of one per wave)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        const unsigned tile = ((blockIdx.z / (unsigned)a.ksplit) * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+        unsigned* c = cai_splitk_cnt + (a.cnt - 1) + tile;
+        const unsigned prev = atomicAdd(c, 1u);
+        s_last = prev == (unsigned)a.ksplit - 1u;
+        if (s_last) atomicExch(c, 0u);
+        if (s_last) __threadfence();    // acquire: invalidates this XCD's L2 and the CU's L1 for every wave
+    }
+    __syncthreads();
+    if (!s_last) return;
+    const int s0 = slab - slab % a.ksplit;
+    const int64_t sl = (int64_t)a.ws_rows * a.ws_ld;
+    const int VO = (a.y_vec && a.y_dtype == CAI_BF16) ? 8 : 4;
+    const int cpr = BN / VO;
+    for (int id = threadIdx.x; id < BM * cpr; id += NTH) {
+        const int row = id / cpr;
+        const int n = n0 + (id - row * cpr) * VO;
+        const int m = rowm(row);
+        if (m < 0 || n >= a.Cout) continue;
+        const float* src = a.ws + (int64_t)s0 * sl + (int64_t)m * a.ws_ld + n;
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int s = 0; s < a.ksplit; ++s) {
+            const f32x4 lo = *reinterpret_cast<const f32x4*>(src + s * sl);
+            v[0] += lo[0]; v[1] += lo[1]; v[2] += lo[2]; v[3] += lo[3];
+            if (VO == 8) {
+                const f32x4 hi = *reinterpret_cast<const f32x4*>(src + s * sl + 4);
+                v[4] += hi[0]; v[5] += hi[1]; v[6] += hi[2]; v[7] += hi[3];
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int nn = n + e;
+            const float bv = (a.bias && nn < a.Cout) ? a.bias[nn] : 0.f;
+            v[e] = apply_act(v[e] + bv, a.act, a.act_param);
+        }
+        if (a.y_vec) {
+            store_out_chunk<T>(a, P, plane, m, n, v, VO);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (n + e < a.Cout) store_out_scalar<T>(a, P, plane, m, n + e, v[e]);
+        }
+    }
+}
+
 // Epilogue shared by the conv kernels: the wave accumulators go through LDS as
 // fp32 [BM][BN+4]; split-K writes the raw partial tile to ws[z][m][n] (bias /
 // act / mask applied by the reduce), otherwise bias + act (+ mask) and 16-byte
@@ -176,7 +243,8 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvArgs& a, const Phas
                 for (int r = 0; r < 4; ++r) E[(wm * WTM + tm * 16 + (lane >> 4) * 4 + r) * ES + col] = acc[tm][tn][r];
             }
         __syncthreads();
-        float* dst = a.ws + (int64_t)(slab >= 0 ? slab : (int)blockIdx.z) * a.ws_rows * a.ws_ld;
+        const int sb = slab >= 0 ? slab : (int)blockIdx.z;
+        float* dst = a.ws + (int64_t)sb * a.ws_rows * a.ws_ld;
         constexpr int cpr = BN / 4;
         for (int id = tid; id < BM * cpr; id += NTH) {
             const int row = id / cpr, cc = id - (id / cpr) * cpr;
@@ -185,6 +253,7 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvArgs& a, const Phas
             *reinterpret_cast<f32x4*>(dst + (int64_t)m * a.ws_ld + n) =
                 *reinterpret_cast<const f32x4*>(E + row * ES + cc * 4);
         }
+        if (a.cnt > 0) splitk_fold<T, BM, BN, NTH>(a, P, plane, n0, rowm, sb);
         return;
     }
 #pragma unroll
@@ -230,8 +299,14 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvArgs& a, const Phas
 // holds output channels wn*WTN + tn*16 + 4*g_ + 0..3 of tile row wm*WTM + tm*16 + i16, so the common cases
 // store straight from registers: split-K partials as 16-byte fp32 stores into the slab, bf16 outputs
 // (bias + act) as 8-byte stores.  Masked or non-bf16 / scalar outputs go through LDS as in
-// conv_epilogue_rows (E must then hold BM*(BN+4) floats).
-template <typename T, int BM, int BN, int WM, int WN, int NTH, class RowMap>
+// conv_epilogue_rows (E must then hold BM*(BN+4) floats; NOLDS tiles have no such buffer and are only
+// launched where epi_t_direct holds or K is split).
+__host__ __device__ __forceinline__ bool epi_t_direct(const ConvArgs& a) {
+    return a.y_vec && a.y_dtype == CAI_BF16 && (a.Cout & 3) == 0 &&
+           (!a.mask_mode || ((a.aux_ld & 3) == 0 && (reinterpret_cast<uintptr_t>(a.aux) & 7) == 0));
+}
+
+template <typename T, int BM, int BN, int WM, int WN, int NTH, class RowMap, bool NOLDS = false>
 __device__ __forceinline__ void conv_epilogue_rows_t(const ConvArgs& a, const PhaseDesc& P, int plane, int n0,
                                                      float* E, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
                                                      RowMap rowm, int slab) {
@@ -253,9 +328,11 @@ __device__ __forceinline__ void conv_epilogue_rows_t(const ConvArgs& a, const Ph
                 if (n < a.ws_ld) *reinterpret_cast<f32x4*>(dst + (int64_t)m * a.ws_ld + n) = acc[tm][tn];
             }
         }
+        if (a.cnt > 0) splitk_fold<T, BM, BN, NTH>(a, P, plane, n0, rowm, slab);
         return;
     }
-    if (a.y_vec && a.y_dtype == CAI_BF16 && !a.mask_mode && (a.Cout & 3) == 0) {
+    // (the mask variant only in the NOLDS tiles: in the 128-channel halo kernels its registers spill the loop)
+    if (NOLDS ? epi_t_direct(a) : (a.y_vec && a.y_dtype == CAI_BF16 && !a.mask_mode && (a.Cout & 3) == 0)) {
         f32x4 bv[TN];
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn) {
@@ -270,18 +347,32 @@ __device__ __forceinline__ void conv_epilogue_rows_t(const ConvArgs& a, const Ph
             int b, oy, ox;
             out_pixel<T>(a, P, plane, m, b, oy, ox);
             bf16* Y = reinterpret_cast<bf16*>(a.y) + (int64_t)b * a.ysb + (int64_t)oy * a.ysy + (int64_t)ox * a.ysx;
+            // gradient mask (dgrad): the aux tensor at the same pixel, 4 channels per lane as in store_out_chunk
+            const bf16* AUX = (NOLDS && a.mask_mode) ? reinterpret_cast<const bf16*>(a.aux) +
+                                                           (((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.aux_ld
+                                                     : nullptr;
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn) {
                 const int n = n0 + wn * WTN + tn * 16 + 4 * g_;
                 if (n >= a.Cout) continue;
+                f32x4 v;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = apply_act(acc[tm][tn][r] + bv[tn][r], a.act, a.act_param);
+                if (NOLDS && AUX) {
+                    const bf16x4 mv = *reinterpret_cast<const bf16x4*>(AUX + n);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] *= mask_val(a.mask_mode, (float)mv[r], a.mask_param);
+                }
                 bf16x4 h;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) h[r] = (bf16)apply_act(acc[tm][tn][r] + bv[tn][r], a.act, a.act_param);
+                for (int r = 0; r < 4; ++r) h[r] = (bf16)v[r];
                 *reinterpret_cast<bf16x4*>(Y + n) = h;
             }
         }
         return;
     }
+    if constexpr (NOLDS) return;    // host guarantees epi_t_direct (or split-K) for these tiles
+    else {
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
@@ -319,6 +410,7 @@ __device__ __forceinline__ void conv_epilogue_rows_t(const ConvArgs& a, const Ph
             if (m < 0 || n >= a.Cout) continue;
             store_out_scalar<T>(a, P, plane, m, n, E[row * ES + col]);
         }
+    }
     }
 }
 
@@ -1141,9 +1233,12 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvArgs a, int
 #endif
 
 
-template <int NA, int NC>
+template <int NA, int NC, int BN_ = 128>
 struct HaloPhCfg {
-    static constexpr int TH = 8, TW = 32, BM = TH * TW, BN = 128, WM = 4, WN = 2, CK = 64;
+    static constexpr int TH = 8, TW = 32, BM = TH * TW, BN = BN_, WM = 4, WN = 2, CK = 64;
+    // 16-byte weight DMAs per lane per step: 512 lanes stage 128 rows x 64 bytes; BN = 192 issues a second
+    // round (rows 128..255, those past the tile reading the zero page into unread cells)
+    static constexpr int DPS = BN > 128 ? 2 : 1;
     static constexpr int PH = TH + NA - 1, PW = TW + NC - 1;
     static constexpr int NPOS = PH * PW;
     static constexpr int PLANE = (NPOS + 15) / 16 * 16;       // = 0 (mod 16): conflict-free fragment reads
@@ -1156,17 +1251,22 @@ struct HaloPhCfg {
     // NST % NSTB == 0: a step's stage is t % NSTB.  A 6-stage ring (CAI_HALO_PH_NSTB6=1) measured slower on
     // MI355X (C2 8180 vs 8430 patches/s; the big launch 91.6 vs 88 us): the latency is not in the ring
     static constexpr int NSTB = (CAI_HALO_PH_NSTB6 && NST % 6 == 0) ? 6 : (NST % 3 == 0 ? 3 : 2);
-    static constexpr int BSTAGE = BN * 32 * 2;
-    static constexpr int EPI = BM * (BN + 4) * 4;
+    static constexpr int BSTAGE = DPS * 128 * 32 * 2;
+    // BN > 128: register-direct epilogue only (no LDS staging buffer), see conv_epilogue_rows_t
+    static constexpr int EPI = BN > 128 ? 0 : BM * (BN + 4) * 4;
     static constexpr int BYTES = (PATCH + NSTB * BSTAGE > EPI) ? PATCH + NSTB * BSTAGE : EPI;
     static_assert(NPI <= NST - NSTB, "the next chunk's footprint must retire before the chunk's last step");
 };
 
-template <int NA, int NC>
+// GATHER = false: the s^2-phase form (tap (ty, tx) reads footprint cell (NA-1-ty, NC-1-tx) from an origin
+// NA-1 / NC-1 before dy0 / dx0).  GATHER = true: a stride-1 gather convolution (Conv2d k3 s1 forward): tap
+// (ty, tx) = kernel (kh, kw) reads cell (ty, tx) from the origin dy0 = -pad.  n0: the tile's first output
+// channel (grid y).
+template <int NA, int NC, int BN_ = 128, bool GATHER = false>
 __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* smem, int ph, int split, int bid,
-                                                     int tiles_x, int tiles_y) {
-    using H = HaloPhCfg<NA, NC>;
-    constexpr int BM = H::BM, BN = H::BN, WM = H::WM, WN = H::WN;
+                                                     int tiles_x, int tiles_y, int n0 = 0) {
+    using H = HaloPhCfg<NA, NC, BN_>;
+    constexpr int BM = H::BM, BN = H::BN, WM = H::WM, WN = H::WN, DPS = H::DPS;
     constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
     constexpr int NPI = H::NPI, NTAP = H::NTAP, NST = H::NST, NSTB = H::NSTB;
     static_assert(WM * WN == 8 && WTM == 2 * H::TW && H::BYTES <= 160 * 1024, "halo phase tile");
@@ -1189,7 +1289,7 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
 
     // tap (ty, tx) reads input (qy + dy0 - ty, qx + dx0 - tx): the footprint starts NA-1 rows / NC-1 columns
     // before the tile's dy0/dx0 offset
-    const int iyb = ty0 + P.dy0 - (NA - 1), ixb = tx0 + P.dx0 - (NC - 1);
+    const int iyb = GATHER ? ty0 + P.dy0 : ty0 + P.dy0 - (NA - 1), ixb = GATHER ? tx0 + P.dx0 : tx0 + P.dx0 - (NC - 1);
     u32x4 pr_[NPI];
     unsigned fence_[4] = {0u, 0u, 0u, 0u};
     auto load_cell = [&](int ci, int i) {
@@ -1221,14 +1321,22 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
 
     const int bp = wid * 64 + lane;
     const int bn_ = bp >> 2, bs_ = (bp & 3) ^ (((bn_ >> 3) & 1) * 3);
-    const char* Wrow =
-        bn_ < a.Npad ? reinterpret_cast<const char*>(a.w) + (P.w_off + (int64_t)bn_ * a.Kp) * 2 + bs_ * 16 : nullptr;
+    const char* Wrow = n0 + bn_ < a.Npad
+                           ? reinterpret_cast<const char*>(a.w) + (P.w_off + (int64_t)(n0 + bn_) * a.Kp) * 2 + bs_ * 16
+                           : nullptr;
+    const char* Wrow2 = (DPS == 2 && n0 + 128 + bn_ < a.Npad)
+                            ? reinterpret_cast<const char*>(a.w) + (P.w_off + (int64_t)(n0 + 128 + bn_) * a.Kp) * 2 +
+                                  bs_ * 16
+                            : nullptr;
     auto issue_b = [&](int ci, int t) {    // step t = (half t / NTAP, tap t % NTAP) of chunk ci into stage t % NSTB
         const int hf = t / NTAP, tap = t - hf * NTAP;
-        const void* src = (Wrow && ci < nc)
-                              ? (const void*)(Wrow + (tap * a.Cin_pad + (c0 + ci) * H::CK + hf * 32) * 2)
-                              : (const void*)cai_zero_page;
+        const int koff = (tap * a.Cin_pad + (c0 + ci) * H::CK + hf * 32) * 2;
+        const void* src = (Wrow && ci < nc) ? (const void*)(Wrow + koff) : (const void*)cai_zero_page;
         glds16_asm(src, bring + (t % NSTB) * H::BSTAGE + wid * 1024);
+        if constexpr (DPS == 2) {
+            const void* src2 = (Wrow2 && ci < nc) ? (const void*)(Wrow2 + koff) : (const void*)cai_zero_page;
+            glds16_asm(src2, bring + (t % NSTB) * H::BSTAGE + 8192 + wid * 1024);
+        }
     };
 
     const int g_ = lane >> 4, i16 = lane & 15;
@@ -1247,7 +1355,8 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
     auto read_frags = [&](int t, u32x4 (&fa)[TM], u32x4 (&fb)[TN]) {
         const int hf = t / NTAP, tap = t - hf * NTAP;
         const int ty = tap / NC, tx = tap - (tap / NC) * NC;
-        const int toff = (hf * 4 * H::PLANE + (NA - 1 - ty) * H::PW + (NC - 1 - tx)) * 16;
+        const int toff = GATHER ? (hf * 4 * H::PLANE + ty * H::PW + tx) * 16
+                                : (hf * 4 * H::PLANE + (NA - 1 - ty) * H::PW + (NC - 1 - tx)) * 16;
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) fa[tm] = *reinterpret_cast<const u32x4*>(smem + apos[tm] + toff);
 #pragma unroll
@@ -1269,7 +1378,7 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
 #pragma unroll
         for (int t = 0; t < NSTB; ++t) issue_b(0, t);
         store_patch();
-        wait_vmcnt<NSTB - 1>();
+        wait_vmcnt<DPS * (NSTB - 1)>();
         wait_lgkmcnt0();
         __builtin_amdgcn_s_barrier();
         read_frags(0, fa, fb);
@@ -1277,7 +1386,8 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
     for (int ci = 0; ci < nc; ++ci) {
 #pragma unroll
         for (int t = 0; t < NST; ++t) {
-            wait_vmcnt_n(halo_younger(t, NSTB, NPI));
+            // halo_younger counts one DMA per younger step; DPS DMAs per step add (DPS - 1) per younger tap
+            wait_vmcnt_n(halo_younger(t, NSTB, NPI) + (DPS - 1) * (NSTB - 2));
             wait_lgkmcnt0();
             __builtin_amdgcn_s_barrier();
             if (t == NST - 1) {
@@ -1298,7 +1408,7 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
                 for (int tn = 0; tn < TN; ++tn)
-                    acc[tm][tn] = CAI_HALO_PH_T ? mma16<bf16>(fb[tn], fa[tm], acc[tm][tn])
+                    acc[tm][tn] = (CAI_HALO_PH_T || BN > 128) ? mma16<bf16>(fb[tn], fa[tm], acc[tm][tn])
                                                 : mma16<bf16>(fa[tm], fb[tn], acc[tm][tn]);
 #pragma unroll
             for (int i = 0; i < TM + TN; ++i) {
@@ -1321,11 +1431,11 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
         const int oy = ty0 + row / H::TW, ox = tx0 + row % H::TW;
         return (oy < P.OHg && ox < P.OWg) ? b * plane + oy * P.OWg + ox : -1;
     };
-    if (CAI_HALO_PH_T)
-        conv_epilogue_rows_t<bf16, BM, BN, WM, WN, 512>(a, P, plane, 0, reinterpret_cast<float*>(smem), acc, rowm,
-                                                        ph * a.ksplit + split);
+    if (CAI_HALO_PH_T || BN > 128)
+        conv_epilogue_rows_t<bf16, BM, BN, WM, WN, 512, decltype(rowm), (BN > 128)>(
+            a, P, plane, n0, reinterpret_cast<float*>(smem), acc, rowm, ph * a.ksplit + split);
     else
-        conv_epilogue_rows<bf16, BM, BN, WM, WN, 512>(a, P, plane, 0, reinterpret_cast<float*>(smem), acc, rowm,
+        conv_epilogue_rows<bf16, BM, BN, WM, WN, 512>(a, P, plane, n0, reinterpret_cast<float*>(smem), acc, rowm,
                                                       ph * a.ksplit + split);
 }
 
@@ -1334,11 +1444,194 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
 // output tile consecutive logical blocks on one XCD (shared input footprint from its L2, every round mixing
 // 9-, 6- and 4-tap blocks): measured on MI355X the big launch unchanged (88-90 us) and the C2 step 2 %
 // slower (8316 vs 8465 patches/s), so it is off.
+// 256 x 192 tiles of the halo phase / stride-1 kernels (192-, 384-, 768-channel layers).  The 96 accumulator
+// registers leave no room for register-staged footprint cells or a second B fragment set, so:
+//  * the next chunk's footprint goes global -> LDS by DMA into the other half of a double-buffered patch
+//    (wave w owns plane w, one 64-pixel run per step of the chunk's first RUNS steps; pixels outside the
+//    image or past the footprint read the zero page), no footprint store, no fence loads;
+//  * the weight stage holds 256 rows (two DMAs per lane per step; rows past the layer read the zero page);
+//  * MFMAs go column by column: the next step's A set is read during the first column, B fragment tn of the
+//    next step is read into fb[tn] once column tn's MFMAs are issued.
+// Waits: before step t reads step t+1's operands, the loads younger than tap t+1 are the 2 (NSTB - 2) tap
+// DMAs of steps t+2-NSTB .. t-1 and the footprint runs of steps t+1-NSTB .. t-1.
+template <int NA, int NC>
+struct HaloWideCfg {
+    static constexpr int TH = 8, TW = 32, BM = TH * TW, BN = 192, WM = 4, WN = 2, CK = 64;
+    static constexpr int PH = TH + NA - 1, PW = TW + NC - 1;
+    static constexpr int NPOS = PH * PW;
+    static constexpr int PLANE = (NPOS + 63) / 64 * 64;      // whole 64-cell runs per plane, = 0 (mod 16)
+    static constexpr int RUNS = PLANE / 64;
+    static constexpr int PATCH = 8 * PLANE * 16;
+    static constexpr int NTAP = NA * NC, NST = 2 * NTAP;
+    static constexpr int NSTB = NST % 3 == 0 ? 3 : 2;
+    static constexpr int BSTAGE = 256 * 32 * 2;
+    static constexpr int BYTES = 2 * PATCH + NSTB * BSTAGE;
+    static_assert(RUNS <= NST - NSTB, "the next chunk's footprint must retire before the chunk's last step");
+};
+
+__host__ __device__ constexpr int wide_younger(int t, int nstb, int runs) {
+    const int lo = t + 1 - nstb > 0 ? t + 1 - nstb : 0;
+    const int hi = t - 1 < runs - 1 ? t - 1 : runs - 1;
+    return 2 * (nstb - 2) + (hi >= lo ? hi - lo + 1 : 0);
+}
+
+template <int NA, int NC, bool GATHER>
+__device__ __forceinline__ void conv_halo_wide_body(const ConvArgs& a, char* smem, int ph, int split, int bid,
+                                                    int tiles_x, int tiles_y, int n0) {
+    using H = HaloWideCfg<NA, NC>;
+    constexpr int BM = H::BM, BN = H::BN, WM = H::WM, WN = H::WN;
+    constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
+    constexpr int RUNS = H::RUNS, NTAP = H::NTAP, NST = H::NST, NSTB = H::NSTB;
+    static_assert(WM * WN == 8 && WTM == 2 * H::TW && H::BYTES <= 160 * 1024, "halo wide tile");
+    char* const bring = smem + 2 * H::PATCH;
+
+    const PhaseDesc& P = a.ph[ph];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    const int per_img = tiles_x * tiles_y;
+    const int b = bid / per_img;
+    const int rt = bid - b * per_img;
+    const int ty0 = (rt / tiles_x) * H::TH, tx0 = (rt % tiles_x) * H::TW;
+    const int nch = a.Cin_pad / H::CK;
+    const int per = (nch + a.ksplit - 1) / a.ksplit;
+    const int c0 = split * per;
+    const int nc = max(0, min(nch, c0 + per) - c0);
+    const char* X = reinterpret_cast<const char*>(a.x);
+    const int ld_b = a.x_ld * 2;
+
+    const int iyb = GATHER ? ty0 + P.dy0 : ty0 + P.dy0 - (NA - 1), ixb = GATHER ? tx0 + P.dx0 : tx0 + P.dx0 - (NC - 1);
+    // footprint run j of this wave: plane wid (channels 8 wid .. 8 wid + 7 of the chunk), pixels 64 j + lane
+    auto dma_run = [&](int ci, int j) {
+        int q = j * 64 + lane;
+        asm volatile("" : "+v"(q));    // recomputed per run: hoisted run addresses would spill
+        const int pr = q / H::PW, pc = q - (q / H::PW) * H::PW;
+        const int iy = iyb + pr, ix = ixb + pc;
+        const bool in = ci < nc && q < H::NPOS && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW;
+        const void* src = in ? (const void*)(X + ((b * a.IH + iy) * a.IW + ix) * ld_b + wid * 16 + (c0 + ci) * 128)
+                             : (const void*)cai_zero_page;
+        glds16_asm(src, smem + (ci & 1) * H::PATCH + (wid * H::PLANE + j * 64) * 16);
+    };
+
+    const int bp = wid * 64 + lane;
+    const int bn_ = bp >> 2, bs_ = (bp & 3) ^ (((bn_ >> 3) & 1) * 3);
+    const char* W0 = reinterpret_cast<const char*>(a.w) + P.w_off * 2 + bs_ * 16;
+    const char* Wrow = n0 + bn_ < a.Npad ? W0 + (int64_t)(n0 + bn_) * a.Kp * 2 : nullptr;
+    const char* Wrow2 = n0 + 128 + bn_ < a.Npad ? W0 + (int64_t)(n0 + 128 + bn_) * a.Kp * 2 : nullptr;
+    auto issue_b = [&](int ci, int t) {    // step t = (half t / NTAP, tap t % NTAP) of chunk ci into stage t % NSTB
+        const int hf = t / NTAP, tap = t - hf * NTAP;
+        const int koff = (tap * a.Cin_pad + (c0 + ci) * H::CK + hf * 32) * 2;
+        const bool real = ci < nc;
+        glds16_asm((Wrow && real) ? (const void*)(Wrow + koff) : (const void*)cai_zero_page,
+                   bring + (t % NSTB) * H::BSTAGE + wid * 1024);
+        glds16_asm((Wrow2 && real) ? (const void*)(Wrow2 + koff) : (const void*)cai_zero_page,
+                   bring + (t % NSTB) * H::BSTAGE + 8192 + wid * 1024);
+    };
+
+    const int g_ = lane >> 4, i16 = lane & 15;
+    int apos[TM];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+        const int r = wm * WTM + tm * 16 + i16;
+        apos[tm] = (g_ * H::PLANE + (r / H::TW) * H::PW + (r % H::TW)) * 16;
+    }
+    int bpos[TN];
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+        const int n = wn * WTN + tn * 16 + i16;
+        bpos[tn] = (4 * n + (g_ ^ (((n >> 3) & 1) * 3))) * 16;
+    }
+    auto toff_of = [&](int t) {
+        const int hf = t / NTAP, tap = t - hf * NTAP;
+        const int ty = tap / NC, tx = tap - (tap / NC) * NC;
+        return GATHER ? (hf * 4 * H::PLANE + ty * H::PW + tx) * 16
+                      : (hf * 4 * H::PLANE + (NA - 1 - ty) * H::PW + (NC - 1 - tx)) * 16;
+    };
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    u32x4 fa[TM], fb[TN];
+    if (nc > 0) {
+#pragma unroll
+        for (int j = 0; j < RUNS; ++j) dma_run(0, j);
+#pragma unroll
+        for (int t = 0; t < NSTB; ++t) issue_b(0, t);
+        wait_vmcnt<2 * (NSTB - 1)>();
+        __builtin_amdgcn_s_barrier();
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) fa[tm] = *reinterpret_cast<const u32x4*>(smem + apos[tm] + toff_of(0));
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) fb[tn] = *reinterpret_cast<const u32x4*>(bring + bpos[tn]);
+    }
+    for (int ci = 0; ci < nc; ++ci) {
+        const char* cur = smem + (ci & 1) * H::PATCH;
+        const char* nxt = smem + ((ci + 1) & 1) * H::PATCH;
+#pragma unroll
+        for (int t = 0; t < NST; ++t) {
+            wait_vmcnt_n(wide_younger(t, NSTB, RUNS));
+            wait_lgkmcnt0();
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            if (t + NSTB < NST)
+                issue_b(ci, t + NSTB);
+            else
+                issue_b(ci + 1, t + NSTB - NST);
+            if (t < RUNS) dma_run(ci + 1, t);
+            const int t1 = t + 1 == NST ? 0 : t + 1;
+            const char* abase = (t + 1 == NST ? nxt : cur) + toff_of(t1);
+            const char* bst = bring + (t1 % NSTB) * H::BSTAGE;
+            u32x4 na[TM];
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm) {
+                    acc[tm][tn] = mma16<bf16>(fb[tn], fa[tm], acc[tm][tn]);
+                    if (tn == 0) na[tm] = *reinterpret_cast<const u32x4*>(abase + apos[tm]);
+                }
+                fb[tn] = *reinterpret_cast<const u32x4*>(bst + bpos[tn]);
+            }
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#pragma unroll
+            for (int tn = 1; tn < TN; ++tn) {
+                __builtin_amdgcn_sched_group_barrier(0x008, TM, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm) fa[tm] = na[tm];
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    wait_vmcnt<0>();
+    __syncthreads();
+    const int plane = P.OHg * P.OWg;
+    auto rowm = [=](int row) {
+        const int oy = ty0 + row / H::TW, ox = tx0 + row % H::TW;
+        return (oy < P.OHg && ox < P.OWg) ? b * plane + oy * P.OWg + ox : -1;
+    };
+    conv_epilogue_rows_t<bf16, BM, BN, WM, WN, 512, decltype(rowm), true>(a, P, plane, n0, nullptr, acc, rowm,
+                                                                          ph * a.ksplit + split);
+}
+
+// grid y: output-channel tiles of BN (192-channel layers: BN = 192, one tile per 192 channels).
+template <int BN>
 __global__ __launch_bounds__(512, 1) void conv_halo_phase_kernel(const ConvArgs a, int tiles_x, int tiles_y) {
-    constexpr int BYTES = HaloPhCfg<3, 3>::BYTES > HaloPhCfg<2, 2>::BYTES ? HaloPhCfg<3, 3>::BYTES
-                                                                           : HaloPhCfg<2, 2>::BYTES;
-    static_assert(BYTES >= HaloPhCfg<3, 2>::BYTES && BYTES >= HaloPhCfg<2, 3>::BYTES, "halo phase LDS");
+    constexpr int BYTES =
+        BN > 128 ? HaloWideCfg<3, 3>::BYTES
+                 : (HaloPhCfg<3, 3>::BYTES > HaloPhCfg<2, 2>::BYTES ? HaloPhCfg<3, 3>::BYTES : HaloPhCfg<2, 2>::BYTES);
+    static_assert(BN > 128 ? (BYTES >= HaloWideCfg<3, 2>::BYTES && BYTES >= HaloWideCfg<2, 3>::BYTES &&
+                              BYTES >= HaloWideCfg<2, 2>::BYTES)
+                           : (BYTES >= HaloPhCfg<3, 2>::BYTES && BYTES >= HaloPhCfg<2, 3>::BYTES),
+                  "halo phase LDS");
     __shared__ __attribute__((aligned(16))) char smem[BYTES];
+    const int n0 = blockIdx.y * BN;
     const int nb = gridDim.x;
     const int lid = CAI_HALO_PH_MIX ? ((nb & 7) == 0 ? (blockIdx.x & 7) * (nb >> 3) + (blockIdx.x >> 3) : blockIdx.x)
                                     : blockIdx.x;
@@ -1353,12 +1646,37 @@ __global__ __launch_bounds__(512, 1) void conv_halo_phase_kernel(const ConvArgs 
         bid = (nt & 7) == 0 ? (t & 7) * (nt >> 3) + (t >> 3) : t;
     }
     const int split = blockIdx.z;
-    switch (ph) {    // k5 s2 p2 phases: (py, px) = (0,0) 3x3, (0,1) 3x2, (1,0) 2x3, (1,1) 2x2 taps
-        case 0: conv_halo_phase_body<3, 3>(a, smem, 0, split, bid, tiles_x, tiles_y); break;
-        case 1: conv_halo_phase_body<3, 2>(a, smem, 1, split, bid, tiles_x, tiles_y); break;
-        case 2: conv_halo_phase_body<2, 3>(a, smem, 2, split, bid, tiles_x, tiles_y); break;
-        default: conv_halo_phase_body<2, 2>(a, smem, 3, split, bid, tiles_x, tiles_y); break;
+    if constexpr (BN > 128) {
+        switch (ph) {
+            case 0: conv_halo_wide_body<3, 3, false>(a, smem, 0, split, bid, tiles_x, tiles_y, n0); break;
+            case 1: conv_halo_wide_body<3, 2, false>(a, smem, 1, split, bid, tiles_x, tiles_y, n0); break;
+            case 2: conv_halo_wide_body<2, 3, false>(a, smem, 2, split, bid, tiles_x, tiles_y, n0); break;
+            default: conv_halo_wide_body<2, 2, false>(a, smem, 3, split, bid, tiles_x, tiles_y, n0); break;
+        }
+    } else {
+        switch (ph) {    // k5 s2 p2 phases: (py, px) = (0,0) 3x3, (0,1) 3x2, (1,0) 2x3, (1,1) 2x2 taps
+            case 0: conv_halo_phase_body<3, 3>(a, smem, 0, split, bid, tiles_x, tiles_y, n0); break;
+            case 1: conv_halo_phase_body<3, 2>(a, smem, 1, split, bid, tiles_x, tiles_y, n0); break;
+            case 2: conv_halo_phase_body<2, 3>(a, smem, 2, split, bid, tiles_x, tiles_y, n0); break;
+            default: conv_halo_phase_body<2, 2>(a, smem, 3, split, bid, tiles_x, tiles_y, n0); break;
+        }
     }
+}
+
+// Halo-staged stride-1 k3 p1 convolution (the 3x3 convs of cheng2020's residual / attention blocks and
+// sub-pixel convs, conv3x3 layers/layers.py:38-49 / 86-91): the phase body with one phase of 3x3 taps.
+// GATHER: Conv2d forward (tap = kernel (kh, kw), footprint origin -pad); otherwise the input gradient in the
+// phase form of make_plan (flipped taps).  grid: x = output tiles (XCD-remapped), y = BN-channel tiles,
+// z = split.
+template <int BN, bool GATHER>
+__global__ __launch_bounds__(512, 1) void conv_halo_s1_kernel(const ConvArgs a, int tiles_x, int tiles_y) {
+    __shared__ __attribute__((aligned(16))) char smem[BN > 128 ? HaloWideCfg<3, 3>::BYTES : HaloPhCfg<3, 3>::BYTES];
+    const int nt = gridDim.x, t = blockIdx.x;
+    const int bid = (nt & 7) == 0 ? (t & 7) * (nt >> 3) + (t >> 3) : t;
+    if constexpr (BN > 128)
+        conv_halo_wide_body<3, 3, GATHER>(a, smem, 0, blockIdx.z, bid, tiles_x, tiles_y, blockIdx.y * BN);
+    else
+        conv_halo_phase_body<3, 3, 128, GATHER>(a, smem, 0, blockIdx.z, bid, tiles_x, tiles_y, blockIdx.y * BN);
 }
 
 // split-K reduce: out = epilogue(sum_s ws[ph*S + s][m][n]) in a fixed order
@@ -2342,10 +2660,10 @@ __global__ __launch_bounds__(512, 1) void wgrad_glds_kernel(const WgradArgs a) {
 // lane-linearly, so the swizzle is applied to the per-lane SOURCE slot (both-sides rule).
 // Partials leave through the same [split][Ng][ncols] slab as wgrad_glds_kernel (same reduce).
 // ---------------------------------------------------------------------------
-template <int KS>
+template <int KS, int S = 2>
 struct WhCfg {
-    static constexpr int NCELL = 2 * 63 + KS;         // footprint cells of one 64-pixel strip
-    static constexpr int NE = (NCELL + 1) / 2;        // even-offset plane
+    static constexpr int NCELL = S * 63 + KS;         // footprint cells of one 64-pixel strip
+    static constexpr int NE = S == 2 ? (NCELL + 1) / 2 : NCELL;   // even-offset plane (stride 1: one plane)
     static constexpr int XSLOTS = NCELL * 8;          // 16-byte pieces of the footprint
     static constexpr int XGRP = (XSLOTS + 63) / 64;   // wave-instructions that fill it
     static constexpr int NXI = (XGRP + 7) / 8;        // per thread (8 waves); spare instructions hit a sink
@@ -2369,9 +2687,10 @@ __device__ __forceinline__ int opaque(int v) {
     return v;
 }
 
-template <int KS, int FLAGS>
+// S = 1: the stride-1 k3 p1 Conv2d (cheng2020's 3x3 convs): one footprint plane, tap kw at cell p + kw.
+template <int KS, int S, int FLAGS>
 __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
-    using W = WhCfg<KS>;
+    using W = WhCfg<KS, S>;
     __shared__ __attribute__((aligned(16))) char smem[W::BYTES];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wr = wid >> 2, wc = wid & 3;            // 2 (rows) x 4 (cols) waves
@@ -2406,7 +2725,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
         const int Ls = grp * 64 + lane;
         xin[n] = grp < W::XGRP && Ls < W::XSLOTS;
         const int pc = xin[n] ? Ls >> 3 : 0, ps = Ls & 7;
-        xt[n] = pc < W::NE ? 2 * pc : 2 * (pc - W::NE) + 1;
+        xt[n] = S == 1 ? pc : (pc < W::NE ? 2 * pc : 2 * (pc - W::NE) + 1);
         const int ls = (((ps >> 1) ^ wh_h(pc)) << 1) | (ps & 1);
         xlane[n] = xt[n] * xpix + (q0 + ls * 8) * 2;
     }
@@ -2424,8 +2743,8 @@ __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
             glds16(gvalid ? (const void*)(gsrc + i * ghalf) : (const void*)cai_zero_page,
                    gb + wid * 4 * 256 + i * 32 * 256);
         gsrc += gstep;
-        const int y = cj * 2 - a.p + kh;
-        const int x0 = cib * 128 - a.p;
+        const int y = cj * S - a.p + kh;
+        const int x0 = cib * (64 * S) - a.p;
         const bool yok = (unsigned)y < (unsigned)a.Hx;
         const char* xrow = Xp + (((int64_t)cb * a.Hx + (yok ? y : 0)) * a.Wx + x0) * xpix;
 #pragma unroll
@@ -2477,7 +2796,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
             const int col = wcol + tn * 16, kw = col / 64, cg = (col % 64) / 16;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const int c = (kw & 1) * W::NE + (kw >> 1) + rr + 4 * h;
+                const int c = (S == 1 ? kw : (kw & 1) * W::NE + (kw >> 1)) + rr + 4 * h;
                 boff[ks][tn][h] = opaque(W::XBASE + c * 128 + (((cg ^ wh_h(c)) << 1) | (p4 >> 1)) * 16 + (p4 & 1) * 8);
             }
         }
@@ -2590,14 +2909,14 @@ __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
     }
 }
 
-template <int KS>
+template <int KS, int S>
 static void launch_wgrad_halo(const WgradArgs& a, int nblocks, int bias, hipStream_t st) {
     if (bias == WG_BIAS)
-        hipLaunchKernelGGL((wgrad_halo_kernel<KS, WG_BIAS>), dim3(nblocks), dim3(512), 0, st, a);
-    else if (bias == WG_TBIAS)
-        hipLaunchKernelGGL((wgrad_halo_kernel<KS, WG_TBIAS>), dim3(nblocks), dim3(512), 0, st, a);
+        hipLaunchKernelGGL((wgrad_halo_kernel<KS, S, WG_BIAS>), dim3(nblocks), dim3(512), 0, st, a);
+    else if (S == 2 && bias == WG_TBIAS)
+        hipLaunchKernelGGL((wgrad_halo_kernel<KS, S, WG_TBIAS>), dim3(nblocks), dim3(512), 0, st, a);
     else
-        hipLaunchKernelGGL((wgrad_halo_kernel<KS, 0>), dim3(nblocks), dim3(512), 0, st, a);
+        hipLaunchKernelGGL((wgrad_halo_kernel<KS, S, 0>), dim3(nblocks), dim3(512), 0, st, a);
 }
 
 template <int CT>
@@ -2860,6 +3179,8 @@ struct ConvLaunch {
     bool glds;
     int halo, tiles_x, tiles_y;    // halo: kernel size of the halo-staged path (0: not taken)
     bool halo_ph;                  // the halo-staged s^2-phase path (k5 s2 p2 transposed direction)
+    bool halo_s1;                  // the halo-staged stride-1 k3 path
+    int hbn;                       // output-channel tile of the halo phase / s1 paths (128 / 192)
     int small;                     // conv_small_kernel tile (SMALL_*; 0: not taken)
     size_t ws_bytes;
 };
@@ -2912,15 +3233,38 @@ static bool halo_phase_off() {
     }();
     return off;
 }
-static bool halo_phase_ok(const cai_conv_geom* g, const Plan& P, bool glds) {
+// output-channel tile of the halo phase / s1 kernels: 128 up to 128 channels, else 192 unless the width
+// is a multiple of 128 but not of 192 (256, 512: no padded columns)
+static int halo_bn(int cout) { return (cout <= 128 || (cout % 128 == 0 && cout % 192 != 0)) ? 128 : 192; }
+static bool halo_phase_ok(const cai_conv_geom* g, const Plan& P, bool glds, bool wide) {
     static const int nt[4] = {9, 6, 6, 4}, nx[4] = {3, 2, 3, 2};
     if (!glds || !P.phase || halo_off() || halo_phase_off() || P.nphase != 4 || g->stride != 2 || g->kernel != 5 || g->pad != 2 ||
-        P.Cin_pad % 64 != 0 || P.kout_c > 128 || P.OHg[0] < 8 || P.OWg[0] < 32)
+        P.Cin_pad % 64 != 0 || (halo_bn(P.kout_c) > 128 && !wide) || P.OHg[0] < 8 || P.OWg[0] < 32)
         return false;
     for (int ph = 0; ph < 4; ++ph)
         if (P.ntaps[ph] != nt[ph] || P.ntx[ph] != nx[ph]) return false;
     return true;
 }
+
+// the halo-staged stride-1 k3 p1 kernel (both directions), 64-channel input chunks, any output width in
+// BN-channel tiles; A/B knob CAI_HALO_S1_OFF
+static bool halo_s1_off() {
+    static const bool off = [] {
+        const char* e = getenv("CAI_HALO_S1_OFF");
+        return e && *e && *e != '0';
+    }();
+    return off;
+}
+// Taken with >= 128 tiles: at B = 4 the 64x64 / 32x32 maps (16-64 tiles, split K) measured slower than
+// conv_glds_kernel (192->192 64x64: 43 vs 38 us, 32x32: 31 vs 24 us; 128x128: 58 vs 73 us fwd, 71 vs 94 dgrad)
+static bool halo_s1_ok(const cai_conv_geom* g, const Plan& P, bool glds, bool wide) {
+    const int bn = halo_bn(P.kout_c);
+    const int64_t tiles = (int64_t)g->batch * ((P.OWg[0] + 31) / 32) * ((P.OHg[0] + 7) / 8) * ((P.kout_c + bn - 1) / bn);
+    return glds && !halo_off() && !halo_s1_off() && g->stride == 1 && g->kernel == 3 && g->pad == 1 &&
+           P.nphase == 1 && P.ntaps[0] == 9 && P.Cin_pad % 64 == 0 && (bn == 128 || wide) && P.OHg[0] >= 8 &&
+           P.OWg[0] >= 32 && tiles >= 128;
+}
+
 
 // A/B knob: an upper bound on the split-K factor of every conv launch (CAI_KSPLIT_MAX, read once; 0 = none)
 static int ksplit_cap() {
@@ -2932,25 +3276,30 @@ static int ksplit_cap() {
 }
 static int capped(int ks) { return ksplit_cap() > 0 ? std::max(1, std::min(ks, ksplit_cap())) : ks; }
 
-static ConvLaunch conv_launch(const cai_conv_geom* g, int dtype, int direction, int in_abs) {
+// wide: the 192-channel halo tiles may be taken (their epilogue has no LDS path: the caller's output must
+// satisfy epi_t_direct, or K must be split)
+static ConvLaunch conv_launch(const cai_conv_geom* g, int dtype, int direction, int in_abs, bool wide = true) {
     const Plan P = make_plan(g, dtype, direction);
     ConvLaunch L{};
     L.glds = glds_eligible(P, dtype, in_abs);
     L.halo = halo_ks(g, P, L.glds);
-    L.halo_ph = !L.halo && halo_phase_ok(g, P, L.glds);
-    if (L.halo_ph) {
+    L.halo_ph = !L.halo && halo_phase_ok(g, P, L.glds, wide);
+    L.halo_s1 = !L.halo && !L.halo_ph && halo_s1_ok(g, P, L.glds, wide);
+    if (L.halo_ph || L.halo_s1) {
+        const int np = L.halo_ph ? 4 : 1;
+        L.hbn = halo_bn(P.kout_c);
         L.BM = 256;
-        L.BN = 128;
+        L.BN = L.hbn;
         L.tiles_x = (P.OWg[0] + 31) / 32;
         L.tiles_y = (P.OHg[0] + 7) / 8;
-        for (int ph = 0; ph < 4; ++ph) L.mmax = std::max(L.mmax, g->batch * P.OHg[ph] * P.OWg[ph]);
+        for (int ph = 0; ph < np; ++ph) L.mmax = std::max(L.mmax, g->batch * P.OHg[ph] * P.OWg[ph]);
         L.mtiles = g->batch * L.tiles_x * L.tiles_y;
-        L.ntiles = 1;
-        const int nch = P.Cin_pad / 64, blocks = 4 * L.mtiles;
+        L.ntiles = (P.kout_c + L.hbn - 1) / L.hbn;
+        const int nch = P.Cin_pad / 64, blocks = np * L.mtiles * L.ntiles;
         L.ksplit = capped(blocks >= 256 ? 1 : std::min(nch, (256 + blocks - 1) / blocks));
         while (L.ksplit > 1 && (L.ksplit - 1) * ((nch + L.ksplit - 1) / L.ksplit) >= nch) --L.ksplit;
-        L.ws_ld = 128;
-        L.ws_bytes = L.ksplit > 1 ? (size_t)4 * L.ksplit * L.mmax * L.ws_ld * sizeof(float) : 0;
+        L.ws_ld = L.ntiles * L.hbn;
+        L.ws_bytes = L.ksplit > 1 ? (size_t)np * L.ksplit * L.mmax * L.ws_ld * sizeof(float) : 0;
         return L;
     }
     if (L.halo) {
@@ -3003,7 +3352,7 @@ template <typename T, typename C>
 static void launch_conv(const ConvArgs& a, const ConvLaunch& L, hipStream_t st) {
     dim3 grid(L.mtiles, L.ntiles, a.nphase * a.ksplit);
     hipLaunchKernelGGL((conv_gemm_kernel<T, C>), grid, dim3(NT), 0, st, a);
-    if (a.ksplit > 1) {
+    if (a.ksplit > 1 && a.cnt == 0) {
         const int VO = (a.y_vec && a.y_dtype == CAI_BF16) ? 8 : 4;
         const int64_t total = (int64_t)L.mmax * ((a.Cout + VO - 1) / VO);
         const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, (total + 255) / 256));
@@ -3015,7 +3364,7 @@ template <typename C>
 static void launch_conv_glds(const ConvArgs& a, const ConvLaunch& L, hipStream_t st) {
     dim3 grid(L.mtiles, L.ntiles, a.nphase * a.ksplit);
     hipLaunchKernelGGL((conv_glds_kernel<C>), grid, dim3(512), 0, st, a);
-    if (a.ksplit > 1) {
+    if (a.ksplit > 1 && a.cnt == 0) {
         const int VO = (a.y_vec && a.y_dtype == CAI_BF16) ? 8 : 4;
         const int64_t total = (int64_t)L.mmax * ((a.Cout + VO - 1) / VO);
         const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, (total + 255) / 256));
@@ -3029,7 +3378,7 @@ static void launch_conv_halo(const ConvArgs& a, const ConvLaunch& L, hipStream_t
         hipLaunchKernelGGL(conv_halo_kernel<5>, grid, dim3(512), 0, st, a, L.tiles_x, L.tiles_y);
     else
         hipLaunchKernelGGL(conv_halo_kernel<3>, grid, dim3(512), 0, st, a, L.tiles_x, L.tiles_y);
-    if (a.ksplit > 1) {
+    if (a.ksplit > 1 && a.cnt == 0) {
         const int VO = (a.y_vec && a.y_dtype == CAI_BF16) ? 8 : 4;
         const int64_t total = (int64_t)L.mmax * ((a.Cout + VO - 1) / VO);
         const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, (total + 255) / 256));
@@ -3038,13 +3387,31 @@ static void launch_conv_halo(const ConvArgs& a, const ConvLaunch& L, hipStream_t
 }
 
 static void launch_conv_halo_phase(const ConvArgs& a, const ConvLaunch& L, hipStream_t st) {
-    hipLaunchKernelGGL(conv_halo_phase_kernel, dim3(4 * L.mtiles, 1, a.ksplit), dim3(512), 0, st, a, L.tiles_x,
-                       L.tiles_y);
-    if (a.ksplit > 1) {
+    const dim3 grid(L.halo_ph ? 4 * L.mtiles : L.mtiles, L.ntiles, a.ksplit);
+    if (L.halo_ph) {
+        if (L.hbn == 192)
+            hipLaunchKernelGGL(conv_halo_phase_kernel<192>, grid, dim3(512), 0, st, a, L.tiles_x, L.tiles_y);
+        else
+            hipLaunchKernelGGL(conv_halo_phase_kernel<128>, grid, dim3(512), 0, st, a, L.tiles_x, L.tiles_y);
+    } else {
+        const bool gather = a.tap_sy > 0;
+        if (L.hbn == 192) {
+            if (gather)
+                hipLaunchKernelGGL((conv_halo_s1_kernel<192, true>), grid, dim3(512), 0, st, a, L.tiles_x, L.tiles_y);
+            else
+                hipLaunchKernelGGL((conv_halo_s1_kernel<192, false>), grid, dim3(512), 0, st, a, L.tiles_x, L.tiles_y);
+        } else {
+            if (gather)
+                hipLaunchKernelGGL((conv_halo_s1_kernel<128, true>), grid, dim3(512), 0, st, a, L.tiles_x, L.tiles_y);
+            else
+                hipLaunchKernelGGL((conv_halo_s1_kernel<128, false>), grid, dim3(512), 0, st, a, L.tiles_x, L.tiles_y);
+        }
+    }
+    if (a.ksplit > 1 && a.cnt == 0) {
         const int VO = (a.y_vec && a.y_dtype == CAI_BF16) ? 8 : 4;
         const int64_t total = (int64_t)L.mmax * ((a.Cout + VO - 1) / VO);
         const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, (total + 255) / 256));
-        hipLaunchKernelGGL((conv_splitk_reduce_kernel<bf16>), dim3(gx, 4), dim3(256), 0, st, a);
+        hipLaunchKernelGGL((conv_splitk_reduce_kernel<bf16>), dim3(gx, a.nphase), dim3(256), 0, st, a);
     }
 }
 
@@ -3069,7 +3436,7 @@ static void dispatch_conv(const ConvArgs& a, const ConvLaunch& L, hipStream_t st
             launch_conv_halo(a, L, st);
             return;
         }
-        if (L.halo_ph) {
+        if (L.halo_ph || L.halo_s1) {
             launch_conv_halo_phase(a, L, st);
             return;
         }
@@ -3089,6 +3456,30 @@ static void dispatch_conv(const ConvArgs& a, const ConvLaunch& L, hipStream_t st
     }
 }
 
+// Split-K fold counters: one pool for the library, handed out in consecutive ranges (one counter per output
+// tile of a split-K launch).  Every launch leaves its counters at zero, so a range may be reused by any later
+// launch on the same stream; ranges of launches that can run concurrently (side streams, graphs) are disjoint
+// unless 2^20 counters were handed out in between.
+// Opt-in (CAI_SPLITK_FOLD=1): measured on MI355X the fold costs more than the reduce launch it removes --
+// C2 7530 vs 8594 patches/s with one agent-scope release per block (6250 with one per wave): each release
+// writes back the XCD's L2 and each acquire invalidates it, for every split-K block of every layer
+// (profiles/r02_splitk_fold_ab.log)
+static bool splitk_fold_off() {
+    static const bool off = [] {
+        const char* e = getenv("CAI_SPLITK_FOLD");
+        return !(e && *e && *e != '0');
+    }();
+    return off;
+}
+
+static int splitk_counters(unsigned n) {
+    static std::atomic<unsigned> next{0};
+    if (n == 0 || n > SPLITK_POOL) return 0;
+    unsigned off = next.fetch_add(n) % SPLITK_POOL;
+    if (off + n > SPLITK_POOL) off = 0;    // wrap: the oldest ranges
+    return (int)off + 1;
+}
+
 static int run_conv(const cai_conv_geom* g, int dtype, int direction, const void* x, int x_ld, int in_abs,
                     const void* w, const float* bias, int act, float act_param, void* y, int y_dtype, int64_t ysb,
                     int64_t ysc, int64_t ysy, int64_t ysx, const void* aux, int aux_ld, int mask_mode,
@@ -3098,7 +3489,7 @@ static int run_conv(const cai_conv_geom* g, int dtype, int direction, const void
     CAI_CHECK_ARG(dtype == CAI_BF16 || dtype == CAI_F32, "%s: bad dtype", name);
     CAI_CHECK_ARG(x && w && y, "%s: null pointer", name);
     const Plan P = make_plan(g, dtype, direction);
-    const ConvLaunch L = conv_launch(g, dtype, direction, in_abs);
+    ConvLaunch L = conv_launch(g, dtype, direction, in_abs);
     const int VEC = dtype == CAI_BF16 ? 8 : 4;
     CAI_CHECK_ARG(x_ld >= P.Cin_pad && x_ld % VEC == 0, "%s: input ld %d must be >= %d and a multiple of %d", name,
                   x_ld, P.Cin_pad, VEC);
@@ -3121,7 +3512,18 @@ static int run_conv(const cai_conv_geom* g, int dtype, int direction, const void
                ((uintptr_t)y & 15) == 0);
     a.bias = bias; a.act = act; a.act_param = act_param;
     a.aux = aux; a.aux_ld = aux_ld; a.mask_mode = mask_mode; a.mask_param = mask_param;
+    if ((L.halo_ph || L.halo_s1) && L.hbn > 128 && L.ksplit == 1 && !epi_t_direct(a))
+        L = conv_launch(g, dtype, direction, in_abs, false);    // the 192-channel tiles store from registers only
+    CAI_CHECK_ARG(L.ws_bytes == 0 || (workspace && ws_bytes >= L.ws_bytes && ((uintptr_t)workspace & 15) == 0),
+                  "%s: workspace of %zu bytes required", name, L.ws_bytes);
     a.ksplit = L.ksplit; a.ws = reinterpret_cast<float*>(workspace); a.ws_rows = L.mmax; a.ws_ld = L.ws_ld;
+    a.cnt = 0;
+    if (L.ksplit > 1 && !L.small && !splitk_fold_off()) {
+        // tiles of the launch grid with the split factored out (dispatch_conv's grids)
+        const unsigned tiles = (L.halo_ph ? 4u : 1u) * (unsigned)L.mtiles * (unsigned)L.ntiles *
+                               (unsigned)((L.halo || L.halo_ph || L.halo_s1) ? 1 : P.nphase);
+        a.cnt = splitk_counters(tiles);
+    }
     for (int ph = 0; ph < P.nphase; ++ph) {
         PhaseDesc& d = a.ph[ph];
         d.oy0 = P.oy0[ph]; d.ox0 = P.ox0[ph]; d.OHg = P.OHg[ph]; d.OWg = P.OWg[ph];
@@ -3163,10 +3565,22 @@ static bool halo_wgrad_off() {
     }();
     return off;
 }
+// opt-in (CAI_HALO_WGRAD_S1=1): on cheng2020-attn q6 (192->192 k3 s1 128x128, B = 4) the stride-1 halo
+// wgrad measured 117 us per launch against 120 for wgrad_glds_kernel -- its 192-column tile (three taps) and
+// the 192-row G side (two 128-row tiles) leave it LDS-read bound -- so the glds kernel stays the default
+static bool halo_wgrad_s1_off() {
+    static const bool off = [] {
+        const char* e = getenv("CAI_HALO_WGRAD_S1");
+        return !(e && *e && *e != '0');
+    }();
+    return off;
+}
+// stride 2 (k3/k5, pad k/2, both conv kinds) or the stride-1 k3 p1 Conv2d
 static bool halo_wgrad_ks(const cai_conv_geom* g, const WgradPlan& W) {
     const int Wg = g->transposed ? g->in_w : g->out_w;
-    return !halo_wgrad_off() && g->stride == 2 && (g->kernel == 3 || g->kernel == 5) && g->pad == g->kernel / 2 &&
-           Wg % 64 == 0 && W.Cq_pad % 64 == 0;
+    const bool s2 = g->stride == 2 && (g->kernel == 3 || g->kernel == 5) && g->pad == g->kernel / 2;
+    const bool s1 = g->stride == 1 && g->kernel == 3 && g->pad == 1 && !g->transposed && !halo_wgrad_s1_off();
+    return !halo_wgrad_off() && (s1 || s2) && Wg % 64 == 0 && W.Cq_pad % 64 == 0;
 }
 
 // ConvTranspose2d: an s x s block of taps (kh0 + a, kw0 + b) such that every output pixel is reached
@@ -3429,7 +3843,9 @@ int cai_pack_nchw(const float* x, int32_t B, int32_t C, int32_t H, int32_t W, in
 size_t cai_conv_workspace_bytes(const cai_conv_geom* g, int dtype, int direction) {
     if (check_geom(g)) return 0;
     // the kernel choice may depend on in_abs (not known here): cover both
-    return std::max(conv_launch(g, dtype, direction, 0).ws_bytes, conv_launch(g, dtype, direction, 1).ws_bytes);
+    // and on whether the output allows the 192-channel halo tiles (run_conv falls back)
+    return std::max({conv_launch(g, dtype, direction, 0).ws_bytes, conv_launch(g, dtype, direction, 1).ws_bytes,
+                     conv_launch(g, dtype, direction, 0, false).ws_bytes});
 }
 
 int cai_conv_fwd(const cai_conv_geom* g, int dtype, const void* x, int32_t x_ld, int32_t in_abs, const void* packed_w,
@@ -3456,12 +3872,13 @@ const char* cai_conv_kernel_name(const cai_conv_geom* g, int dtype, int directio
         if (small_wgrad_ok(g, dtype)) return "wgrad_small_kernel";
         const WgradPlan W = make_wgrad_plan(g, dtype, true, in_abs != 0);
         if (!W.glds) return dtype == CAI_BF16 ? "wgrad_kernel<bf16>" : "wgrad_kernel<float>";
-        if (W.halo) return W.halo == 5 ? "wgrad_halo_kernel<5>" : "wgrad_halo_kernel<3>";
+        if (W.halo) return W.halo == 5 ? "wgrad_halo_kernel<5>" : (g->stride == 1 ? "wgrad_halo_kernel<3,s1>" : "wgrad_halo_kernel<3>");
         return W.ct == 256 ? "wgrad_glds_kernel<256>" : "wgrad_glds_kernel<128>";
     }
     const ConvLaunch L = conv_launch(g, dtype, direction, in_abs);
     if (L.halo) return L.halo == 5 ? "conv_halo_kernel<5>" : "conv_halo_kernel<3>";
-    if (L.halo_ph) return "conv_halo_phase_kernel";
+    if (L.halo_ph) return L.hbn == 192 ? "conv_halo_phase_kernel<192>" : "conv_halo_phase_kernel";
+    if (L.halo_s1) return L.hbn == 192 ? "conv_halo_s1_kernel<192>" : "conv_halo_s1_kernel<128>";
     if (L.small) return L.small == SMALL_16x32 ? "conv_small_kernel<16x32>"
                         : (L.small == SMALL_32x32 ? "conv_small_kernel<32x32>" : "conv_small_kernel<32x64>");
     switch (L.cfg) {
@@ -3562,9 +3979,11 @@ int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_l
             a.nsplit = W.strips_per_split;
             a.rtiles = (W.Ng + 127) / 128;
             if (W.halo == 5)
-                launch_wgrad_halo<5>(a, W.S * W.tiles, bflag, st);
+                launch_wgrad_halo<5, 2>(a, W.S * W.tiles, bflag, st);
+            else if (g->stride == 1)
+                launch_wgrad_halo<3, 1>(a, W.S * W.tiles, bflag, st);
             else
-                launch_wgrad_halo<3>(a, W.S * W.tiles, bflag, st);
+                launch_wgrad_halo<3, 2>(a, W.S * W.tiles, bflag, st);
         } else if (W.ct == 256)
             launch_wgrad_glds<256>(a, W.S * W.tiles, in_abs, in_sq, bflag, st);
         else

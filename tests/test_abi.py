@@ -118,3 +118,34 @@ def test_edge_gate(native):
         assert lib.cai_edge_workspace_bytes(ctypes.byref(g), native.BF16) == 0
     with pytest.raises(ValueError, match="unsupported geometry"):
         native.lib.cai_edge_conv_fwd(ctypes.byref(no[0]), None, None, None, None, 128, None)
+
+
+def test_halo_kernel_selection(native):
+    """Host-side kernel choice (no launch): the halo-staged stride-1 k3 kernel takes both directions of
+    3x3 s1 p1 convs with 64-multiple input channels on >= 8 x 32 outputs (192-channel tiles for 192/384/768
+    output channels), and the s^2-phase kernel's 192-channel tiles take the k5 s2 transposed direction at N = 192
+    (test_kernels_gpu.py CONV_CASES runs these geometries on the GPU)."""
+    lib = native.lib.load()
+    G = native.ConvGeom
+
+    def name(g, d):
+        return lib.cai_conv_kernel_name(ctypes.byref(g), native.BF16, d, 0).decode()
+
+    assert name(G(4, 192, 128, 128, 192, 128, 128, 3, 1, 1, 0, 0), 0) == "conv_halo_s1_kernel<192>"
+    assert name(G(4, 192, 128, 128, 192, 128, 128, 3, 1, 1, 0, 0), 1) == "conv_halo_s1_kernel<192>"
+    assert name(G(4, 192, 64, 64, 768, 64, 64, 3, 1, 1, 0, 0), 0) == "conv_halo_s1_kernel<192>"
+    assert name(G(4, 128, 64, 128, 96, 64, 128, 3, 1, 1, 0, 0), 0) == "conv_halo_s1_kernel<128>"
+    assert name(G(4, 128, 64, 64, 256, 64, 64, 3, 1, 1, 0, 0), 0) == "conv_halo_s1_kernel<128>"
+    assert name(G(4, 96, 64, 128, 128, 64, 128, 3, 1, 1, 0, 0), 0) != "conv_halo_s1_kernel<128>"   # Cin % 64
+    assert "halo" not in name(G(16, 192, 16, 16, 192, 16, 16, 3, 1, 1, 0, 0), 0)                 # 16 wide
+    assert name(G(16, 192, 64, 64, 192, 128, 128, 5, 2, 2, 1, 1), 0) == "conv_halo_phase_kernel<192>"
+    assert name(G(16, 192, 128, 128, 192, 64, 64, 5, 2, 2, 0, 0), 1) == "conv_halo_phase_kernel<192>"
+    assert name(G(16, 128, 64, 64, 128, 128, 128, 5, 2, 2, 1, 1), 0) == "conv_halo_phase_kernel"
+    # weight gradient: the halo-staged kernel's stride-1 form is opt-in (CAI_HALO_WGRAD_S1=1, measured no gain)
+    if os.environ.get("CAI_HALO_WGRAD_S1", "0") not in ("", "0"):
+        assert name(G(4, 192, 128, 128, 192, 128, 128, 3, 1, 1, 0, 0), 2) == "wgrad_halo_kernel<3,s1>"
+    assert "halo" not in name(G(4, 192, 32, 32, 192, 32, 32, 3, 1, 1, 0, 0), 2)
+    # the stride-1 conv kernel needs >= 128 tiles (64x64 at B = 4: 64 tiles, conv_glds_kernel)
+    assert "halo" not in name(G(4, 192, 64, 64, 192, 64, 64, 3, 1, 1, 0, 0), 0)
+    assert lib.cai_conv_kernel_name(ctypes.byref(G(4, 192, 128, 128, 192, 128, 128, 3, 1, 1, 0, 0)), native.F32,
+                                    0, 0).decode().startswith("conv_gemm")
