@@ -1454,9 +1454,10 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
 //    next step is read into fb[tn] once column tn's MFMAs are issued.
 // Waits: before step t reads step t+1's operands, the loads younger than tap t+1 are the 2 (NSTB - 2) tap
 // DMAs of steps t+2-NSTB .. t-1 and the footprint runs of steps t+1-NSTB .. t-1.
-template <int NA, int NC>
+template <int NA, int NC, int BN_ = 192>
 struct HaloWideCfg {
-    static constexpr int TH = 8, TW = 32, BM = TH * TW, BN = 192, WM = 4, WN = 2, CK = 64;
+    static constexpr int TH = 8, TW = 32, BM = TH * TW, BN = BN_, WM = 4, WN = 2, CK = 64;
+    static constexpr int DPS = BN > 128 ? 2 : 1;               // weight DMAs per lane per step
     static constexpr int PH = TH + NA - 1, PW = TW + NC - 1;
     static constexpr int NPOS = PH * PW;
     static constexpr int PLANE = (NPOS + 63) / 64 * 64;      // whole 64-cell runs per plane, = 0 (mod 16)
@@ -1464,22 +1465,23 @@ struct HaloWideCfg {
     static constexpr int PATCH = 8 * PLANE * 16;
     static constexpr int NTAP = NA * NC, NST = 2 * NTAP;
     static constexpr int NSTB = NST % 3 == 0 ? 3 : 2;
-    static constexpr int BSTAGE = 256 * 32 * 2;
-    static constexpr int BYTES = 2 * PATCH + NSTB * BSTAGE;
+    static constexpr int BSTAGE = DPS * 128 * 32 * 2;
+    static constexpr int EPI = BN > 128 ? 0 : BM * (BN + 4) * 4;   // BN = 128: LDS epilogue fallback
+    static constexpr int BYTES = 2 * PATCH + NSTB * BSTAGE > EPI ? 2 * PATCH + NSTB * BSTAGE : EPI;
     static_assert(RUNS <= NST - NSTB, "the next chunk's footprint must retire before the chunk's last step");
 };
 
-__host__ __device__ constexpr int wide_younger(int t, int nstb, int runs) {
+__host__ __device__ constexpr int wide_younger(int t, int nstb, int runs, int dps) {
     const int lo = t + 1 - nstb > 0 ? t + 1 - nstb : 0;
     const int hi = t - 1 < runs - 1 ? t - 1 : runs - 1;
-    return 2 * (nstb - 2) + (hi >= lo ? hi - lo + 1 : 0);
+    return dps * (nstb - 2) + (hi >= lo ? hi - lo + 1 : 0);
 }
 
-template <int NA, int NC, bool GATHER>
+template <int NA, int NC, bool GATHER, int BN_ = 192>
 __device__ __forceinline__ void conv_halo_wide_body(const ConvArgs& a, char* smem, int ph, int split, int bid,
                                                     int tiles_x, int tiles_y, int n0) {
-    using H = HaloWideCfg<NA, NC>;
-    constexpr int BM = H::BM, BN = H::BN, WM = H::WM, WN = H::WN;
+    using H = HaloWideCfg<NA, NC, BN_>;
+    constexpr int BM = H::BM, BN = H::BN, WM = H::WM, WN = H::WN, DPS = H::DPS;
     constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
     constexpr int RUNS = H::RUNS, NTAP = H::NTAP, NST = H::NST, NSTB = H::NSTB;
     static_assert(WM * WN == 8 && WTM == 2 * H::TW && H::BYTES <= 160 * 1024, "halo wide tile");
@@ -1523,8 +1525,9 @@ __device__ __forceinline__ void conv_halo_wide_body(const ConvArgs& a, char* sme
         const bool real = ci < nc;
         glds16_asm((Wrow && real) ? (const void*)(Wrow + koff) : (const void*)cai_zero_page,
                    bring + (t % NSTB) * H::BSTAGE + wid * 1024);
-        glds16_asm((Wrow2 && real) ? (const void*)(Wrow2 + koff) : (const void*)cai_zero_page,
-                   bring + (t % NSTB) * H::BSTAGE + 8192 + wid * 1024);
+        if constexpr (DPS == 2)
+            glds16_asm((Wrow2 && real) ? (const void*)(Wrow2 + koff) : (const void*)cai_zero_page,
+                       bring + (t % NSTB) * H::BSTAGE + 8192 + wid * 1024);
     };
 
     const int g_ = lane >> 4, i16 = lane & 15;
@@ -1559,7 +1562,7 @@ __device__ __forceinline__ void conv_halo_wide_body(const ConvArgs& a, char* sme
         for (int j = 0; j < RUNS; ++j) dma_run(0, j);
 #pragma unroll
         for (int t = 0; t < NSTB; ++t) issue_b(0, t);
-        wait_vmcnt<2 * (NSTB - 1)>();
+        wait_vmcnt<DPS * (NSTB - 1)>();
         __builtin_amdgcn_s_barrier();
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) fa[tm] = *reinterpret_cast<const u32x4*>(smem + apos[tm] + toff_of(0));
@@ -1571,7 +1574,7 @@ __device__ __forceinline__ void conv_halo_wide_body(const ConvArgs& a, char* sme
         const char* nxt = smem + ((ci + 1) & 1) * H::PATCH;
 #pragma unroll
         for (int t = 0; t < NST; ++t) {
-            wait_vmcnt_n(wide_younger(t, NSTB, RUNS));
+            wait_vmcnt_n(wide_younger(t, NSTB, RUNS, DPS));
             wait_lgkmcnt0();
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
@@ -1616,19 +1619,25 @@ __device__ __forceinline__ void conv_halo_wide_body(const ConvArgs& a, char* sme
         const int oy = ty0 + row / H::TW, ox = tx0 + row % H::TW;
         return (oy < P.OHg && ox < P.OWg) ? b * plane + oy * P.OWg + ox : -1;
     };
-    conv_epilogue_rows_t<bf16, BM, BN, WM, WN, 512, decltype(rowm), true>(a, P, plane, n0, nullptr, acc, rowm,
-                                                                          ph * a.ksplit + split);
+    conv_epilogue_rows_t<bf16, BM, BN, WM, WN, 512, decltype(rowm), (BN > 128)>(
+        a, P, plane, n0, reinterpret_cast<float*>(smem), acc, rowm, ph * a.ksplit + split);
 }
+
+// CAI_HALO_DMA=1: the 128-channel phase / stride-1 kernels on the DMA-footprint body as well (A/B)
+#ifndef CAI_HALO_DMA
+#define CAI_HALO_DMA 0
+#endif
 
 // grid y: output-channel tiles of BN (192-channel layers: BN = 192, one tile per 192 channels).
 template <int BN>
 __global__ __launch_bounds__(512, 1) void conv_halo_phase_kernel(const ConvArgs a, int tiles_x, int tiles_y) {
+    constexpr bool DMA = BN > 128 || CAI_HALO_DMA;
     constexpr int BYTES =
-        BN > 128 ? HaloWideCfg<3, 3>::BYTES
-                 : (HaloPhCfg<3, 3>::BYTES > HaloPhCfg<2, 2>::BYTES ? HaloPhCfg<3, 3>::BYTES : HaloPhCfg<2, 2>::BYTES);
-    static_assert(BN > 128 ? (BYTES >= HaloWideCfg<3, 2>::BYTES && BYTES >= HaloWideCfg<2, 3>::BYTES &&
-                              BYTES >= HaloWideCfg<2, 2>::BYTES)
-                           : (BYTES >= HaloPhCfg<3, 2>::BYTES && BYTES >= HaloPhCfg<2, 3>::BYTES),
+        DMA ? HaloWideCfg<3, 3, BN>::BYTES
+            : (HaloPhCfg<3, 3>::BYTES > HaloPhCfg<2, 2>::BYTES ? HaloPhCfg<3, 3>::BYTES : HaloPhCfg<2, 2>::BYTES);
+    static_assert(DMA ? (BYTES >= HaloWideCfg<3, 2, BN>::BYTES && BYTES >= HaloWideCfg<2, 3, BN>::BYTES &&
+                         BYTES >= HaloWideCfg<2, 2, BN>::BYTES)
+                      : (BYTES >= HaloPhCfg<3, 2>::BYTES && BYTES >= HaloPhCfg<2, 3>::BYTES),
                   "halo phase LDS");
     __shared__ __attribute__((aligned(16))) char smem[BYTES];
     const int n0 = blockIdx.y * BN;
@@ -1646,12 +1655,12 @@ __global__ __launch_bounds__(512, 1) void conv_halo_phase_kernel(const ConvArgs 
         bid = (nt & 7) == 0 ? (t & 7) * (nt >> 3) + (t >> 3) : t;
     }
     const int split = blockIdx.z;
-    if constexpr (BN > 128) {
+    if constexpr (DMA) {
         switch (ph) {
-            case 0: conv_halo_wide_body<3, 3, false>(a, smem, 0, split, bid, tiles_x, tiles_y, n0); break;
-            case 1: conv_halo_wide_body<3, 2, false>(a, smem, 1, split, bid, tiles_x, tiles_y, n0); break;
-            case 2: conv_halo_wide_body<2, 3, false>(a, smem, 2, split, bid, tiles_x, tiles_y, n0); break;
-            default: conv_halo_wide_body<2, 2, false>(a, smem, 3, split, bid, tiles_x, tiles_y, n0); break;
+            case 0: conv_halo_wide_body<3, 3, false, BN>(a, smem, 0, split, bid, tiles_x, tiles_y, n0); break;
+            case 1: conv_halo_wide_body<3, 2, false, BN>(a, smem, 1, split, bid, tiles_x, tiles_y, n0); break;
+            case 2: conv_halo_wide_body<2, 3, false, BN>(a, smem, 2, split, bid, tiles_x, tiles_y, n0); break;
+            default: conv_halo_wide_body<2, 2, false, BN>(a, smem, 3, split, bid, tiles_x, tiles_y, n0); break;
         }
     } else {
         switch (ph) {    // k5 s2 p2 phases: (py, px) = (0,0) 3x3, (0,1) 3x2, (1,0) 2x3, (1,1) 2x2 taps
@@ -1670,11 +1679,12 @@ __global__ __launch_bounds__(512, 1) void conv_halo_phase_kernel(const ConvArgs 
 // z = split.
 template <int BN, bool GATHER>
 __global__ __launch_bounds__(512, 1) void conv_halo_s1_kernel(const ConvArgs a, int tiles_x, int tiles_y) {
-    __shared__ __attribute__((aligned(16))) char smem[BN > 128 ? HaloWideCfg<3, 3>::BYTES : HaloPhCfg<3, 3>::BYTES];
+    constexpr bool DMA = BN > 128 || CAI_HALO_DMA;
+    __shared__ __attribute__((aligned(16))) char smem[DMA ? HaloWideCfg<3, 3, BN>::BYTES : HaloPhCfg<3, 3>::BYTES];
     const int nt = gridDim.x, t = blockIdx.x;
     const int bid = (nt & 7) == 0 ? (t & 7) * (nt >> 3) + (t >> 3) : t;
-    if constexpr (BN > 128)
-        conv_halo_wide_body<3, 3, GATHER>(a, smem, 0, blockIdx.z, bid, tiles_x, tiles_y, blockIdx.y * BN);
+    if constexpr (DMA)
+        conv_halo_wide_body<3, 3, GATHER, BN>(a, smem, 0, blockIdx.z, bid, tiles_x, tiles_y, blockIdx.y * BN);
     else
         conv_halo_phase_body<3, 3, 128, GATHER>(a, smem, 0, blockIdx.z, bid, tiles_x, tiles_y, blockIdx.y * BN);
 }
@@ -2660,10 +2670,14 @@ __global__ __launch_bounds__(512, 1) void wgrad_glds_kernel(const WgradArgs a) {
 // lane-linearly, so the swizzle is applied to the per-lane SOURCE slot (both-sides rule).
 // Partials leave through the same [split][Ng][ncols] slab as wgrad_glds_kernel (same reduce).
 // ---------------------------------------------------------------------------
-template <int KS, int S = 2>
+// R > 1 (G width 64 / R = 32 or 16): a strip is R whole G rows of 64 / R pixels (still 64 consecutive G
+// pixels); each row has its own footprint row image of NCR cells (even / odd planes), rows stacked.
+template <int KS, int S = 2, int R = 1>
 struct WhCfg {
-    static constexpr int NCELL = S * 63 + KS;         // footprint cells of one 64-pixel strip
-    static constexpr int NE = S == 2 ? (NCELL + 1) / 2 : NCELL;   // even-offset plane (stride 1: one plane)
+    static constexpr int WR = 64 / R;                 // pixels per strip row
+    static constexpr int NCR = S * (WR - 1) + KS;     // footprint cells of one strip row
+    static constexpr int NE = S == 2 ? (NCR + 1) / 2 : NCR;   // even-offset plane of a row (stride 1: one plane)
+    static constexpr int NCELL = R * NCR;             // footprint cells of one strip
     static constexpr int XSLOTS = NCELL * 8;          // 16-byte pieces of the footprint
     static constexpr int XGRP = (XSLOTS + 63) / 64;   // wave-instructions that fill it
     static constexpr int NXI = (XGRP + 7) / 8;        // per thread (8 waves); spare instructions hit a sink
@@ -2688,9 +2702,9 @@ __device__ __forceinline__ int opaque(int v) {
 }
 
 // S = 1: the stride-1 k3 p1 Conv2d (cheng2020's 3x3 convs): one footprint plane, tap kw at cell p + kw.
-template <int KS, int S, int FLAGS>
+template <int KS, int S, int FLAGS, int R = 1>
 __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
-    using W = WhCfg<KS, S>;
+    using W = WhCfg<KS, S, R>;
     __shared__ __attribute__((aligned(16))) char smem[W::BYTES];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wr = wid >> 2, wc = wid & 3;            // 2 (rows) x 4 (cols) waves
@@ -2701,8 +2715,9 @@ __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
     const int tl = L - split * ntile;
     const int ctile = tl % (KS * nqc), rtile = tl / (KS * nqc);
     const int kh = ctile / nqc, q0 = (ctile - kh * nqc) * 64, r0 = rtile * 128;
-    const int nsr = a.Wg / 64;                        // strips per G row
-    const int nstrip = a.B * a.Hg * nsr;
+    const int nsr = R == 1 ? a.Wg / 64 : 1;           // strips per G row (R > 1: one strip spans R rows)
+    const int nrg = a.Hg / R;                         // strip rows per image
+    const int nstrip = a.B * nrg * nsr;
     const int sbeg = min(nstrip, split * a.nsplit), send = min(nstrip, sbeg + a.nsplit);   // a.nsplit: strips per split
     const int nsteps = send - sbeg;
     float* out = a.ws + (int64_t)split * a.Ng * a.ncols;
@@ -2716,6 +2731,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
     const bool gvalid = gch < a.Ng;
     // X DMA: this lane's footprint piece of each instruction (x offset t, channel byte offset), or the sink
     int xt[W::NXI];
+    int xr[W::NXI];                                   // strip row of the piece (R > 1)
     bool xin[W::NXI];
     int64_t xlane[W::NXI];                            // byte offset of the piece inside a strip's footprint row
     const int64_t xpix = (int64_t)a.x_ld * 2;         // bytes per X pixel
@@ -2725,13 +2741,15 @@ __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
         const int Ls = grp * 64 + lane;
         xin[n] = grp < W::XGRP && Ls < W::XSLOTS;
         const int pc = xin[n] ? Ls >> 3 : 0, ps = Ls & 7;
-        xt[n] = S == 1 ? pc : (pc < W::NE ? 2 * pc : 2 * (pc - W::NE) + 1);
+        const int rc = pc % W::NCR;                   // cell inside its row image
+        xr[n] = pc / W::NCR;
+        xt[n] = S == 1 ? rc : (rc < W::NE ? 2 * rc : 2 * (rc - W::NE) + 1);
         const int ls = (((ps >> 1) ^ wh_h(pc)) << 1) | (ps & 1);
         xlane[n] = xt[n] * xpix + (q0 + ls * 8) * 2;
     }
     // strip coordinates (column block, row, image) of the next strip to issue: strips are issued in order,
     // so they advance by carries instead of integer divisions per step
-    int cib = sbeg % nsr, cj = (sbeg / nsr) % a.Hg, cb = (sbeg / nsr) / a.Hg;
+    int cib = sbeg % nsr, cj = ((sbeg / nsr) % nrg) * R, cb = (sbeg / nsr) / nrg;
     const char* gsrc = Gp + ((int64_t)(sbeg * 64 + prow0) * a.g_ld + gch) * 2;   // strips are 64 G pixels
     const int64_t gstep = (int64_t)64 * a.g_ld * 2, ghalf = (int64_t)32 * a.g_ld * 2;
 
@@ -2750,13 +2768,22 @@ __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
 #pragma unroll
         for (int n = 0; n < W::NXI; ++n) {
             const int grp = n * 8 + wid;
-            const bool ok = xin[n] && yok && (unsigned)(x0 + xt[n]) < (unsigned)a.Wx;
-            glds16(ok ? (const void*)(xrow + xlane[n]) : (const void*)cai_zero_page,
-                   xb + (grp < W::XGRP ? grp * 1024 : W::XGRP * 1024));
+            if constexpr (R == 1) {
+                const bool ok = xin[n] && yok && (unsigned)(x0 + xt[n]) < (unsigned)a.Wx;
+                glds16(ok ? (const void*)(xrow + xlane[n]) : (const void*)cai_zero_page,
+                       xb + (grp < W::XGRP ? grp * 1024 : W::XGRP * 1024));
+            } else {
+                const int yr = y + S * xr[n];            // input row of the piece's strip row
+                const bool ok = xin[n] && (unsigned)yr < (unsigned)a.Hx && (unsigned)(x0 + xt[n]) < (unsigned)a.Wx;
+                const char* src = Xp + (((int64_t)cb * a.Hx + yr) * a.Wx + x0) * xpix + xlane[n];
+                glds16(ok ? (const void*)src : (const void*)cai_zero_page,
+                       xb + (grp < W::XGRP ? grp * 1024 : W::XGRP * 1024));
+            }
         }
         if (++cib == nsr) {
             cib = 0;
-            if (++cj == a.Hg) {
+            cj += R;
+            if (cj == a.Hg) {
                 cj = 0;
                 ++cb;
             }
@@ -2791,12 +2818,13 @@ __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
         const int rr = 32 * ks + 8 * g_ + q_;
+        const int row0 = (rr / W::WR) * W::NCR, px = rr % W::WR;   // strip row image, pixel in the row
 #pragma unroll
         for (int tn = 0; tn < W::TN; ++tn) {
             const int col = wcol + tn * 16, kw = col / 64, cg = (col % 64) / 16;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const int c = (S == 1 ? kw : (kw & 1) * W::NE + (kw >> 1)) + rr + 4 * h;
+                const int c = row0 + (S == 1 ? kw : (kw & 1) * W::NE + (kw >> 1)) + px + 4 * h;
                 boff[ks][tn][h] = opaque(W::XBASE + c * 128 + (((cg ^ wh_h(c)) << 1) | (p4 >> 1)) * 16 + (p4 & 1) * 8);
             }
         }
@@ -2909,14 +2937,14 @@ __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
     }
 }
 
-template <int KS, int S>
+template <int KS, int S, int R = 1>
 static void launch_wgrad_halo(const WgradArgs& a, int nblocks, int bias, hipStream_t st) {
     if (bias == WG_BIAS)
-        hipLaunchKernelGGL((wgrad_halo_kernel<KS, S, WG_BIAS>), dim3(nblocks), dim3(512), 0, st, a);
+        hipLaunchKernelGGL((wgrad_halo_kernel<KS, S, WG_BIAS, R>), dim3(nblocks), dim3(512), 0, st, a);
     else if (S == 2 && bias == WG_TBIAS)
-        hipLaunchKernelGGL((wgrad_halo_kernel<KS, S, WG_TBIAS>), dim3(nblocks), dim3(512), 0, st, a);
+        hipLaunchKernelGGL((wgrad_halo_kernel<KS, S, WG_TBIAS, R>), dim3(nblocks), dim3(512), 0, st, a);
     else
-        hipLaunchKernelGGL((wgrad_halo_kernel<KS, S, 0>), dim3(nblocks), dim3(512), 0, st, a);
+        hipLaunchKernelGGL((wgrad_halo_kernel<KS, S, 0, R>), dim3(nblocks), dim3(512), 0, st, a);
 }
 
 template <int CT>
@@ -3236,10 +3264,15 @@ static bool halo_phase_off() {
 // output-channel tile of the halo phase / s1 kernels: 128 up to 128 channels, else 192 unless the width
 // is a multiple of 128 but not of 192 (256, 512: no padded columns)
 static int halo_bn(int cout) { return (cout <= 128 || (cout % 128 == 0 && cout % 192 != 0)) ? 128 : 192; }
+// 192-channel tiles only with >= 512 blocks: on C2' / C3' (B = 16) the 64x64 -> 128x128 layers gain (203 ->
+// 176 us, 193 -> 176 us against conv_glds_kernel<128x192>) but the 32x32 -> 64x64 ones (256 blocks) lose
+// (57 -> 61 us)
 static bool halo_phase_ok(const cai_conv_geom* g, const Plan& P, bool glds, bool wide) {
     static const int nt[4] = {9, 6, 6, 4}, nx[4] = {3, 2, 3, 2};
+    const int bn = halo_bn(P.kout_c);
+    const int64_t blocks = 4ll * g->batch * ((P.OWg[0] + 31) / 32) * ((P.OHg[0] + 7) / 8) * ((P.kout_c + bn - 1) / bn);
     if (!glds || !P.phase || halo_off() || halo_phase_off() || P.nphase != 4 || g->stride != 2 || g->kernel != 5 || g->pad != 2 ||
-        P.Cin_pad % 64 != 0 || (halo_bn(P.kout_c) > 128 && !wide) || P.OHg[0] < 8 || P.OWg[0] < 32)
+        P.Cin_pad % 64 != 0 || (bn > 128 && (!wide || blocks < 512)) || P.OHg[0] < 8 || P.OWg[0] < 32)
         return false;
     for (int ph = 0; ph < 4; ++ph)
         if (P.ntaps[ph] != nt[ph] || P.ntx[ph] != nx[ph]) return false;
@@ -3575,12 +3608,27 @@ static bool halo_wgrad_s1_off() {
     }();
     return off;
 }
+// G rows per 64-pixel strip: 1 for G widths that are multiples of 64, 2 / 4 for widths 32 / 16 (stride 2
+// only, whole rows; A/B knob CAI_HALO_WGRAD_ROWS_OFF), 0: not taken
+static bool halo_wgrad_rows_off() {
+    static const bool off = [] {
+        const char* e = getenv("CAI_HALO_WGRAD_ROWS_OFF");
+        return e && *e && *e != '0';
+    }();
+    return off;
+}
+static int halo_wgrad_rows(const cai_conv_geom* g) {
+    const int Wg = g->transposed ? g->in_w : g->out_w, Hg = g->transposed ? g->in_h : g->out_h;
+    if (Wg % 64 == 0) return 1;
+    if (g->stride != 2 || halo_wgrad_rows_off()) return 0;
+    const int R = Wg == 32 ? 2 : (Wg == 16 ? 4 : 0);
+    return (R && Hg % R == 0) ? R : 0;
+}
 // stride 2 (k3/k5, pad k/2, both conv kinds) or the stride-1 k3 p1 Conv2d
 static bool halo_wgrad_ks(const cai_conv_geom* g, const WgradPlan& W) {
-    const int Wg = g->transposed ? g->in_w : g->out_w;
     const bool s2 = g->stride == 2 && (g->kernel == 3 || g->kernel == 5) && g->pad == g->kernel / 2;
     const bool s1 = g->stride == 1 && g->kernel == 3 && g->pad == 1 && !g->transposed && !halo_wgrad_s1_off();
-    return !halo_wgrad_off() && (s1 || s2) && Wg % 64 == 0 && W.Cq_pad % 64 == 0;
+    return !halo_wgrad_off() && (s1 || s2) && halo_wgrad_rows(g) > 0 && W.Cq_pad % 64 == 0;
 }
 
 // ConvTranspose2d: an s x s block of taps (kh0 + a, kw0 + b) such that every output pixel is reached
@@ -3647,7 +3695,7 @@ static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype, bool glds, b
         W.halo = g->kernel;
         const int Wg = g->transposed ? g->in_w : g->out_w;
         const int Hg = g->transposed ? g->in_h : g->out_h;
-        const int64_t nstrip = (int64_t)g->batch * Hg * (Wg / 64);
+        const int64_t nstrip = (int64_t)g->batch * Hg * Wg / 64;    // 64-pixel strips (R rows each)
         W.tiles = W.halo * (W.Cq_pad / 64) * ((W.Ng + 127) / 128);
         int S = std::max(1, 256 / W.tiles);
         S = (int)std::max<int64_t>(1, std::min<int64_t>(S, nstrip / 4));   // >= 4 strips per split
@@ -3872,7 +3920,14 @@ const char* cai_conv_kernel_name(const cai_conv_geom* g, int dtype, int directio
         if (small_wgrad_ok(g, dtype)) return "wgrad_small_kernel";
         const WgradPlan W = make_wgrad_plan(g, dtype, true, in_abs != 0);
         if (!W.glds) return dtype == CAI_BF16 ? "wgrad_kernel<bf16>" : "wgrad_kernel<float>";
-        if (W.halo) return W.halo == 5 ? "wgrad_halo_kernel<5>" : (g->stride == 1 ? "wgrad_halo_kernel<3,s1>" : "wgrad_halo_kernel<3>");
+        if (W.halo) {
+            static const char* const nm[2][5] = {{"", "wgrad_halo_kernel<3>", "wgrad_halo_kernel<3,r2>", "",
+                                                  "wgrad_halo_kernel<3,r4>"},
+                                                 {"", "wgrad_halo_kernel<5>", "wgrad_halo_kernel<5,r2>", "",
+                                                  "wgrad_halo_kernel<5,r4>"}};
+            if (g->stride == 1) return "wgrad_halo_kernel<3,s1>";
+            return nm[W.halo == 5][halo_wgrad_rows(g)];
+        }
         return W.ct == 256 ? "wgrad_glds_kernel<256>" : "wgrad_glds_kernel<128>";
     }
     const ConvLaunch L = conv_launch(g, dtype, direction, in_abs);
@@ -3978,8 +4033,14 @@ int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_l
         if (W.halo) {
             a.nsplit = W.strips_per_split;
             a.rtiles = (W.Ng + 127) / 128;
+            const int R = halo_wgrad_rows(g);
             if (W.halo == 5)
-                launch_wgrad_halo<5, 2>(a, W.S * W.tiles, bflag, st);
+                R == 1 ? launch_wgrad_halo<5, 2>(a, W.S * W.tiles, bflag, st)
+                       : (R == 2 ? launch_wgrad_halo<5, 2, 2>(a, W.S * W.tiles, bflag, st)
+                                 : launch_wgrad_halo<5, 2, 4>(a, W.S * W.tiles, bflag, st));
+            else if (g->stride == 2 && R > 1)
+                R == 2 ? launch_wgrad_halo<3, 2, 2>(a, W.S * W.tiles, bflag, st)
+                       : launch_wgrad_halo<3, 2, 4>(a, W.S * W.tiles, bflag, st);
             else if (g->stride == 1)
                 launch_wgrad_halo<3, 1>(a, W.S * W.tiles, bflag, st);
             else

@@ -140,6 +140,9 @@ def test_halo_kernel_selection(native):
     assert "halo" not in name(G(16, 192, 16, 16, 192, 16, 16, 3, 1, 1, 0, 0), 0)                 # 16 wide
     assert name(G(16, 192, 64, 64, 192, 128, 128, 5, 2, 2, 1, 1), 0) == "conv_halo_phase_kernel<192>"
     assert name(G(16, 192, 128, 128, 192, 64, 64, 5, 2, 2, 0, 0), 1) == "conv_halo_phase_kernel<192>"
+    assert name(G(8, 64, 64, 64, 192, 128, 128, 5, 2, 2, 1, 1), 0) == "conv_halo_phase_kernel<192>"
+    assert name(G(8, 192, 128, 128, 64, 64, 64, 5, 2, 2, 0, 0), 1) == "conv_halo_phase_kernel<192>"
+    assert "halo" not in name(G(16, 192, 32, 32, 192, 64, 64, 5, 2, 2, 1, 1), 0)    # 256 blocks
     assert name(G(16, 128, 64, 64, 128, 128, 128, 5, 2, 2, 1, 1), 0) == "conv_halo_phase_kernel"
     # weight gradient: the halo-staged kernel's stride-1 form is opt-in (CAI_HALO_WGRAD_S1=1, measured no gain)
     if os.environ.get("CAI_HALO_WGRAD_S1", "0") not in ("", "0"):

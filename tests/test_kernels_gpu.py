@@ -75,6 +75,11 @@ CONV_CASES = [
     ("conv", 1, 64, 192, 20, 128, 5, 2),
     ("deconv", 1, 64, 128, 6, 64, 3, 2),
     ("deconv", 2, 128, 64, 5, 64, 5, 2),
+    # halo-staged weight gradient with multi-row strips (G width 32: 2 rows, 16: 4 rows per 64-pixel strip),
+    # fused Conv2d bias, ConvTranspose2d bias from the X taps, k3 and k5, 192 G channels
+    ("conv", 4, 128, 128, 64, 64, 5, 2),
+    ("conv", 8, 64, 64, 32, 32, 3, 2),
+    ("deconv", 8, 128, 64, 16, 16, 3, 2),
     # latent-size convs at the training batch (conv_small_kernel: one launch, 8-wave in-block split-K):
     # h_a / h_s / the latent ends of g_a and g_s, all three tile shapes, phase mode, 192 channels
     ("conv", 16, 128, 128, 16, 16, 5, 2),
@@ -95,10 +100,11 @@ CONV_CASES = [
     ("conv", 1, 64, 384, 128, 128, 3, 1),
     ("conv", 4, 128, 96, 64, 128, 3, 1),
     ("conv", 4, 128, 320, 64, 64, 3, 1),
-    # 192-channel halo phase kernel (ConvTranspose2d k5 s2 forward / Conv2d k5 s2 input gradient at N = 192)
+    # 192-channel halo phase kernel (ConvTranspose2d k5 s2 forward / Conv2d k5 s2 input gradient at N = 192,
+    # >= 512 blocks); the smaller 192-channel phase-direction layers stay on conv_glds_kernel<128x192>
+    ("deconv", 8, 64, 192, 64, 64, 5, 2),
+    ("conv", 8, 192, 64, 128, 128, 5, 2),
     ("deconv", 2, 192, 192, 32, 32, 5, 2),
-    ("conv", 2, 192, 192, 64, 64, 5, 2),
-    ("deconv", 1, 64, 192, 64, 64, 5, 2),
     # Spatial_aligner patch embedding / recovery (master.py:708-724): kernel = stride = 2, no padding
     ("conv", 2, 64, 96, 32, 24, 2, 2, 0, 0),
     ("conv", 2, 3, 96, 16, 16, 2, 2, 0, 0),
