@@ -3289,13 +3289,15 @@ static bool halo_s1_off() {
     return off;
 }
 // Taken with >= 128 tiles: at B = 4 the 64x64 / 32x32 maps (16-64 tiles, split K) measured slower than
-// conv_glds_kernel (192->192 64x64: 43 vs 38 us, 32x32: 31 vs 24 us; 128x128: 58 vs 73 us fwd, 71 vs 94 dgrad)
+// conv_glds_kernel (192->192 64x64: 43 vs 38 us, 32x32: 31 vs 24 us; 128x128: 58 vs 73 us fwd, 71 vs 94 dgrad),
+// and with > 64 output channels: 64-channel outputs fill half the 128-channel tile (multimodal 64->64 at
+// 512x640 input gradient 200 vs 157 us on conv_glds_kernel<256x64>)
 static bool halo_s1_ok(const cai_conv_geom* g, const Plan& P, bool glds, bool wide) {
     const int bn = halo_bn(P.kout_c);
     const int64_t tiles = (int64_t)g->batch * ((P.OWg[0] + 31) / 32) * ((P.OHg[0] + 7) / 8) * ((P.kout_c + bn - 1) / bn);
     return glds && !halo_off() && !halo_s1_off() && g->stride == 1 && g->kernel == 3 && g->pad == 1 &&
            P.nphase == 1 && P.ntaps[0] == 9 && P.Cin_pad % 64 == 0 && (bn == 128 || wide) && P.OHg[0] >= 8 &&
-           P.OWg[0] >= 32 && tiles >= 128;
+           P.OWg[0] >= 32 && tiles >= 128 && P.kout_c > 64;
 }
 
 

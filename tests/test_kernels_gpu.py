@@ -99,6 +99,7 @@ CONV_CASES = [
     ("conv", 2, 64, 768, 48, 72, 3, 1),
     ("conv", 1, 64, 384, 128, 128, 3, 1),
     ("conv", 4, 128, 96, 64, 128, 3, 1),
+    ("conv", 4, 128, 192, 64, 128, 3, 1),
     ("conv", 4, 128, 320, 64, 64, 3, 1),
     # 192-channel halo phase kernel (ConvTranspose2d k5 s2 forward / Conv2d k5 s2 input gradient at N = 192,
     # >= 512 blocks); the smaller 192-channel phase-direction layers stay on conv_glds_kernel<128x192>
