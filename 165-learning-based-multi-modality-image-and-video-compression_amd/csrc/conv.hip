@@ -2510,7 +2510,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_glds_kernel(const WgradArgs a) {
             const bool mok = m < pend;
             const void* gs = (mok && gvalid) ? (const void*)(Gp + ((int64_t)m * a.g_ld + gch) * 2)
                                              : (const void*)cai_zero_page;
-            glds16(gs, sb + i * 32 * 256);
+            glds16_asm(gs, sb + i * 32 * 256);
             const int b = cb[i], j = cj[i];
             const int yb = j * a.s - a.p, xb = cx[i] * a.s - a.p;
             cx[i] += 64;
@@ -2528,7 +2528,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_glds_kernel(const WgradArgs a) {
                 const int iy = yb + xkh[h], ix = xb + xkw[h];
                 const bool ok = mok && xvalid[h] && (unsigned)iy < (unsigned)a.Hx && (unsigned)ix < (unsigned)a.Wx;
                 const void* xs = ok ? (const void*)(xrow + xoff[h]) : (const void*)cai_zero_page;
-                glds16(xs, sb + (1 + h) * OPB + i * 32 * 256);
+                glds16_asm(xs, sb + (1 + h) * OPB + i * 32 * 256);
             }
         }
     };
@@ -2588,9 +2588,6 @@ __global__ __launch_bounds__(512, 1) void wgrad_glds_kernel(const WgradArgs a) {
                 fb[t] = __builtin_bit_cast(u32x4, bv);
                 if constexpr ((FLAGS & WG_ABS) != 0) fb[t] = abs_chunk(fb[t], 2);
                 if constexpr ((FLAGS & WG_SQ) != 0) fb[t] = sq_chunk<bf16>(fb[t]);
-                if constexpr ((FLAGS & WG_TBIAS) != 0) {
-                    if (tsel[t] >= 0) tsum[t] += sum8_bf16(fb[t]);
-                }
             }
 #pragma unroll
             for (int tm = 0; tm < 4; ++tm) {
@@ -2610,6 +2607,12 @@ __global__ __launch_bounds__(512, 1) void wgrad_glds_kernel(const WgradArgs a) {
                 }
 #pragma unroll
                 for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mma16<bf16>(fa, fb[tn], acc[tm][tn]);
+            }
+            // transposed bias sums after the MFMAs: inside the read loop they made each B read wait
+            if constexpr ((FLAGS & WG_TBIAS) != 0) {
+#pragma unroll
+                for (int t = 0; t < TN; ++t)
+                    if (tsel[t] >= 0) tsum[t] += sum8_bf16(fb[t]);
             }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -2758,7 +2761,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
         char* xb = smem + W::XBASE + stage * W::XSTRIDE;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
-            glds16(gvalid ? (const void*)(gsrc + i * ghalf) : (const void*)cai_zero_page,
+            glds16_asm(gvalid ? (const void*)(gsrc + i * ghalf) : (const void*)cai_zero_page,
                    gb + wid * 4 * 256 + i * 32 * 256);
         gsrc += gstep;
         const int y = cj * S - a.p + kh;
@@ -2770,13 +2773,13 @@ __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
             const int grp = n * 8 + wid;
             if constexpr (R == 1) {
                 const bool ok = xin[n] && yok && (unsigned)(x0 + xt[n]) < (unsigned)a.Wx;
-                glds16(ok ? (const void*)(xrow + xlane[n]) : (const void*)cai_zero_page,
+                glds16_asm(ok ? (const void*)(xrow + xlane[n]) : (const void*)cai_zero_page,
                        xb + (grp < W::XGRP ? grp * 1024 : W::XGRP * 1024));
             } else {
                 const int yr = y + S * xr[n];            // input row of the piece's strip row
                 const bool ok = xin[n] && (unsigned)yr < (unsigned)a.Hx && (unsigned)(x0 + xt[n]) < (unsigned)a.Wx;
                 const char* src = Xp + (((int64_t)cb * a.Hx + yr) * a.Wx + x0) * xpix + xlane[n];
-                glds16(ok ? (const void*)src : (const void*)cai_zero_page,
+                glds16_asm(ok ? (const void*)src : (const void*)cai_zero_page,
                        xb + (grp < W::XGRP ? grp * 1024 : W::XGRP * 1024));
             }
         }
@@ -2850,9 +2853,6 @@ __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
                 s16x4 b1 = ds_tr16(Xs, boff[ks][t][1]);
                 s16x8 bv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
                 fb[t] = __builtin_bit_cast(u32x4, bv);
-                if constexpr ((FLAGS & WG_TBIAS) != 0) {
-                    if (tsel[t] >= 0) tsum[t] += sum8_bf16(fb[t]);
-                }
             }
 #pragma unroll
             for (int tm = 0; tm < 4; ++tm) {
@@ -2871,6 +2871,12 @@ __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
                 }
 #pragma unroll
                 for (int tn = 0; tn < W::TN; ++tn) acc[tm][tn] = mma16<bf16>(fa, fb[tn], acc[tm][tn]);
+            }
+            // transposed bias sums after the MFMAs: inside the read loop they made each B read wait
+            if constexpr ((FLAGS & WG_TBIAS) != 0) {
+#pragma unroll
+                for (int t = 0; t < W::TN; ++t)
+                    if (tsel[t] >= 0) tsum[t] += sum8_bf16(fb[t]);
             }
         }
     };
