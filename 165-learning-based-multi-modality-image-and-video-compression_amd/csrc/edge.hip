@@ -81,9 +81,17 @@ __device__ __attribute__((aligned(64))) unsigned edge_zero_page[64];
 typedef const void __attribute__((address_space(1)))* gvoid_ptr;
 typedef void __attribute__((address_space(3)))* lvoid_ptr;
 
+// The LDS DMA issued from inline asm: the builtin is booked by the compiler's waitcnt pass as an LDS write
+// of unknown order, so every later fragment read waited for vmcnt(0) -- the ring's prefetches included.
+// The kernels here count their DMAs themselves (wait_vmcnt<N> before each step's barrier).  M0 carries the
+// wave's LDS base and is restored after the DMA (the compiler reserves it).
 __device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
-    __builtin_amdgcn_global_load_lds((gvoid_ptr)(reinterpret_cast<uintptr_t>(g)),
-                                     (lvoid_ptr)(reinterpret_cast<uintptr_t>(lds_wave_base)), 16, 0, 0);
+    const unsigned lds = __builtin_amdgcn_readfirstlane((unsigned)reinterpret_cast<uintptr_t>(lds_wave_base));
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(lds)
+                 : "memory");
 }
 
 // LDS byte offset of 16-byte slot `slot` of row `row` in a [rows][256 B] bf16 image read by
