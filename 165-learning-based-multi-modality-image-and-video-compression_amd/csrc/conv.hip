@@ -1884,28 +1884,44 @@ __device__ __forceinline__ void pack_item(const PackArgs* __restrict__ descs, in
     }
 }
 
+// TO[ph * 64 + t]: the source tap (kernel offset kh * k + kw) of packed tap t of phase ph, filled once per row
+// (k <= 7: <= 49 taps) so the packing loop reads S without an integer division per element
 template <typename T>
-__device__ __forceinline__ void pack_row(const PackArgs& a, int n, float* S) {
+__device__ __forceinline__ void pack_row(const PackArgs& a, int n, float* S, int* TO) {
     const int KK = a.k * a.k;
     const int nsrc = a.Creal * KK;
     if (n < a.Nreal) {
-        for (int i = threadIdx.x; i < nsrc; i += blockDim.x) {
-            const int c = i / KK, tap = i - c * KK;
-            const int64_t src = a.n_is_d0 ? (int64_t)n * a.D1 * KK + i : ((int64_t)c * a.D1 + n) * KK + tap;
-            float v = a.w[src];
-            if (a.mask) v *= a.mask[src];
-            S[i] = v;
+        // four independent loads in flight per thread
+        for (int i0 = threadIdx.x; i0 < nsrc; i0 += 4 * blockDim.x) {
+            float v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int i = min(i0 + j * (int)blockDim.x, nsrc - 1);
+                const int c = i / KK, tap = i - c * KK;
+                const int64_t src = a.n_is_d0 ? (int64_t)n * a.D1 * KK + i : ((int64_t)c * a.D1 + n) * KK + tap;
+                v[j] = a.w[src];
+                if (a.mask) v[j] *= a.mask[src];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (i0 + j * (int)blockDim.x < nsrc) S[i0 + j * blockDim.x] = v[j];
         }
+    }
+    for (int idx = threadIdx.x; idx < a.nphase * 64; idx += blockDim.x) {
+        const int ph = idx >> 6, t = idx & 63;
+        const int ntx = ph == 0 ? a.ntx[0] : (ph == 1 ? a.ntx[1] : (ph == 2 ? a.ntx[2] : a.ntx[3]));
+        const int kh0 = ph == 0 ? a.kh0[0] : (ph == 1 ? a.kh0[1] : (ph == 2 ? a.kh0[2] : a.kh0[3]));
+        const int kw0 = ph == 0 ? a.kw0[0] : (ph == 1 ? a.kw0[1] : (ph == 2 ? a.kw0[2] : a.kw0[3]));
+        const int ty = t / ntx;
+        TO[idx] = (kh0 + a.step * ty) * a.k + kw0 + a.step * (t - ty * ntx);
     }
     __syncthreads();
     const int nch = a.Kp / 8;
     for (int ph = 0; ph < a.nphase; ++ph) {
         const int ntaps = ph == 0 ? a.ntaps[0] : (ph == 1 ? a.ntaps[1] : (ph == 2 ? a.ntaps[2] : a.ntaps[3]));
-        const int ntx = ph == 0 ? a.ntx[0] : (ph == 1 ? a.ntx[1] : (ph == 2 ? a.ntx[2] : a.ntx[3]));
-        const int kh0 = ph == 0 ? a.kh0[0] : (ph == 1 ? a.kh0[1] : (ph == 2 ? a.kh0[2] : a.kh0[3]));
-        const int kw0 = ph == 0 ? a.kw0[0] : (ph == 1 ? a.kw0[1] : (ph == 2 ? a.kw0[2] : a.kw0[3]));
         const int64_t off = ph == 0 ? a.off[0] : (ph == 1 ? a.off[1] : (ph == 2 ? a.off[2] : a.off[3]));
         T* out = reinterpret_cast<T*>(a.out) + off + (int64_t)n * a.Kp;
+        const int* TOp = TO + ph * 64;
         for (int ch = threadIdx.x; ch < nch; ch += blockDim.x) {
             const int e0 = ch * 8;
             int t = e0 / a.Cpad, c = e0 - t * a.Cpad;   // fp32 (Cpad % 4 == 0): the 8 may span two taps
@@ -1913,10 +1929,7 @@ __device__ __forceinline__ void pack_row(const PackArgs& a, int n, float* S) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 float x = 0.f;
-                if (n < a.Nreal && c < a.Creal && t < ntaps) {
-                    const int ty = t / ntx;
-                    x = S[c * KK + (kh0 + a.step * ty) * a.k + kw0 + a.step * (t - ty * ntx)];
-                }
+                if (n < a.Nreal && c < a.Creal && t < ntaps) x = S[c * KK + TOp[t]];
                 v[e] = x;
                 if (++c == a.Cpad) { c = 0; ++t; }
             }
@@ -1937,6 +1950,7 @@ __device__ __forceinline__ void pack_row(const PackArgs& a, int n, float* S) {
 template <typename T>
 __global__ __launch_bounds__(256) void pack_many_kernel(const PackArgs* __restrict__ descs, int n, int64_t total) {
     __shared__ float S[PACK_ROW_MAX];
+    __shared__ int TO[4 * 64];
     const int64_t R = descs[0].rows_total;
     const int64_t I = total - R;
     const int64_t units = R + (I + 255) / 256;
@@ -1947,7 +1961,7 @@ __global__ __launch_bounds__(256) void pack_many_kernel(const PackArgs* __restri
                 const int mid = (lo + hi + 1) >> 1;
                 if (descs[mid].row_begin <= u) lo = mid; else hi = mid - 1;
             }
-            pack_row<T>(descs[lo], (int)(u - descs[lo].row_begin), S);
+            pack_row<T>(descs[lo], (int)(u - descs[lo].row_begin), S, TO);
         } else {
             const int64_t gi = (u - R) * 256 + threadIdx.x;
             if (gi < I) pack_item<T>(descs, n, gi);
