@@ -584,8 +584,9 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(const ConvArgs a) {
 // bf16 implicit GEMM with LDS-DMA staging (global_load_lds_dwordx4) and a
 // 3-stage ring: tile kt+2 streams into LDS while tile kt is multiplied, one
 // raw barrier per K-tile behind a counted vmcnt (cdna_hip_programming.md §5
-// "Pipelining across barriers").  512 threads = 8 waves.  Requires
-// Cin_pad % 64 == 0 so every 64-channel K-tile lies inside one tap: the tap's
+// "Pipelining across barriers").  512 threads = 8 waves.  With
+// Cin_pad % 64 == 0 every 64-channel K-tile lies inside one tap (Cin_pad % 64 == 32: each 32-channel half
+// of a K-tile lies inside one tap and is addressed on its own): the tap's
 // (dy, dx) shift is uniform per tile and the per-lane gather is one add + a
 // bounds test.  Padding taps read a zero page.  The LDS image is lane-linear
 // (DMA), so the XOR swizzle that keeps the fragment reads conflict-free is
@@ -648,6 +649,11 @@ __global__ __launch_bounds__(512, 1) void conv_glds_kernel(const ConvArgs a) {
     // this thread's DMA rows: i*64 + wid*8 + lane/8; all share one logical slot
     const int rsub = wid * 8 + (lane >> 3);
     const int ls = (lane & 7) ^ ((rsub >> 1) & 7);
+    // Cin_pad % 64 == 32 (96-, 160-channel inputs): a 64-element K-tile may straddle two taps; slots 0-3 and
+    // 4-7 are then addressed separately (half = the 32-element half this lane's slot belongs to), and
+    // elements past K (the packed rows' zero padding) read the zero page
+    const bool halves = (a.Cin_pad & 63) != 0;
+    const int hsel = ls >> 2;
     const char* X = reinterpret_cast<const char*>(a.x);
     const int ld_b = a.x_ld * 2;                 // bytes per pixel row
     int abase[AG], ay[AG], ax[AG];
@@ -660,7 +666,7 @@ __global__ __launch_bounds__(512, 1) void conv_glds_kernel(const ConvArgs a) {
             const int j = r / P.OWg;
             ay[i] = j * a.row_stride;
             ax[i] = (r - j * P.OWg) * a.row_stride;
-            abase[i] = ((b * a.IH + ay[i]) * a.IW + ax[i]) * ld_b + ls * 16;
+            abase[i] = ((b * a.IH + ay[i]) * a.IW + ax[i]) * ld_b + (halves ? (ls & 3) : ls) * 16;
         } else {
             ay[i] = -(1 << 28);
             ax[i] = 0;
@@ -674,23 +680,26 @@ __global__ __launch_bounds__(512, 1) void conv_glds_kernel(const ConvArgs a) {
         const int row = n0 + i * 64 + rsub;
         boff[i] = row < a.Npad ? row * a.Kp * 2 : -1;
     }
-    const int nk_all = P.K / 64;
+    const int nk_all = (P.K + 63) / 64;
     const int per = (nk_all + a.ksplit - 1) / a.ksplit;
     const int kt0 = split * per;
     const int nk = max(0, min(nk_all, kt0 + per) - kt0);
 
     auto issue = [&](int kt, int stage) {
         const int kg = kt0 + kt;
-        const int t = (kg * 64) / a.Cin_pad;
-        const int ci0 = kg * 64 - t * a.Cin_pad;
+        // the K element this lane's slot starts its 32-element half at (whole tile when !halves)
+        const int k0 = kg * 64 + (halves ? hsel * 32 : 0);
+        const int t = k0 / a.Cin_pad;
+        const int ci0 = k0 - t * a.Cin_pad;
         const int ty = t / P.ntx;
         const int dy = P.dy0 + a.tap_sy * ty, dx = P.dx0 + a.tap_sx * (t - ty * P.ntx);
         const int delta = (dy * a.IW + dx) * ld_b + ci0 * 2;
+        const bool kin = k0 < P.K;
         char* sbase = smem + stage * C::STAGE + wid * 8 * 128;
 #pragma unroll
         for (int i = 0; i < AG; ++i) {
             const int iy = ay[i] + dy, ix = ax[i] + dx;
-            const bool ok = (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW;
+            const bool ok = kin && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW;
             const void* src = ok ? (const void*)(X + abase[i] + delta) : (const void*)cai_zero_page;
             GLDS(src, sbase + i * 64 * 128);
         }
@@ -3217,8 +3226,15 @@ static int pick_cfg_glds(int C, int nphase, int& BM, int& BN) {
 
 // the LDS-DMA kernel needs bf16 operands read as stored (no |x| on load) and
 // 64-channel K-tiles inside one tap
+static bool glds_off32() {    // A/B knob: CAI_GLDS32_OFF=1 keeps 32-mod-64 input widths on conv_gemm_kernel
+    static const bool off = [] {
+        const char* e = getenv("CAI_GLDS32_OFF");
+        return e && *e && *e != '0';
+    }();
+    return off;
+}
 static bool glds_eligible(const Plan& P, int dtype, int in_abs) {
-    return dtype == CAI_BF16 && !in_abs && P.Cin_pad % 64 == 0;
+    return dtype == CAI_BF16 && !in_abs && (P.Cin_pad % 64 == 0 || (P.Cin_pad % 32 == 0 && !glds_off32()));
 }
 
 // Launch geometry of one conv call: tiles, split-K factor and its workspace.

@@ -106,6 +106,12 @@ CONV_CASES = [
     ("deconv", 8, 64, 192, 64, 64, 5, 2),
     ("conv", 8, 192, 64, 128, 128, 5, 2),
     ("deconv", 2, 192, 192, 32, 32, 5, 2),
+    # LDS-DMA conv kernel with 32-mod-64 input widths (cheng2020 attention blocks: 96 channels; 160): K-tiles
+    # straddling two taps, the last tile past K, 1x1 and 3x3, both directions, the s^2-phase direction
+    ("conv", 4, 96, 96, 64, 64, 3, 1),
+    ("conv", 4, 96, 192, 32, 32, 1, 1),
+    ("conv", 8, 160, 128, 32, 32, 3, 1),
+    ("deconv", 4, 96, 64, 32, 32, 5, 2),
     # Spatial_aligner patch embedding / recovery (master.py:708-724): kernel = stride = 2, no padding
     ("conv", 2, 64, 96, 32, 24, 2, 2, 0, 0),
     ("conv", 2, 3, 96, 16, 16, 2, 2, 0, 0),
