@@ -606,15 +606,11 @@ struct Cfg2 {
 typedef const void __attribute__((address_space(1)))* gvoid_ptr;
 typedef void __attribute__((address_space(3)))* lvoid_ptr;
 
-__device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
-    __builtin_amdgcn_global_load_lds((gvoid_ptr)(reinterpret_cast<uintptr_t>(g)),
-                                     (lvoid_ptr)(reinterpret_cast<uintptr_t>(lds_wave_base)), 16, 0, 0);
-}
-
-// The same DMA hidden from the compiler.  The waitcnt pass books an LDS DMA as an LDS event of unknown
-// order, so while one is in flight every later wait on a fragment read becomes lgkmcnt(0); issued from
-// inline asm it is invisible, and the ring's vmcnt waits are explicit anyway.  M0 carries the wave's LDS
-// base and is restored after the DMA (the compiler reserves it).
+// The LDS DMA (global_load_lds_dwordx4) issued from inline asm.  The waitcnt pass books the builtin
+// (__builtin_amdgcn_global_load_lds) as an LDS write of unknown order: with one in flight every later fragment
+// read waits for lgkmcnt(0) and vmcnt(0) -- every DMA, prefetches included (the weight-gradient kernels measured
+// 97 -> 81 us once their DMAs moved here).  Issued from asm it is invisible; every ring counts its DMAs with
+// explicit vmcnt waits.  M0 carries the wave's LDS base and is restored after the DMA (the compiler reserves it).
 __device__ __forceinline__ void glds16_asm(const void* g, const char* lds_wave_base) {
     const unsigned lds = __builtin_amdgcn_readfirstlane((unsigned)reinterpret_cast<uintptr_t>(lds_wave_base));
     unsigned keep;
