@@ -3632,13 +3632,14 @@ static bool halo_wgrad_off() {
     }();
     return off;
 }
-// opt-in (CAI_HALO_WGRAD_S1=1): on cheng2020-attn q6 (192->192 k3 s1 128x128, B = 4) the stride-1 halo
-// wgrad measured 117 us per launch against 120 for wgrad_glds_kernel -- its 192-column tile (three taps) and
-// the 192-row G side (two 128-row tiles) leave it LDS-read bound -- so the glds kernel stays the default
+// A/B knob CAI_HALO_WGRAD_S1_OFF=1.  Measured before the weight-gradient DMAs moved to asm, the stride-1 form
+// only tied wgrad_glds_kernel (117 vs 120 us); with both kernels' rings overlapping it wins: cheng2020-attn q6
+// 192->192 at 128x128 122 -> 100 us, 64x64 44 -> 39 us (390 -> 397.6 patches/s); multimodal 256->256 at
+// 512x640 1124 -> 976 us, 64->64 188 -> 123 us (profiles/r02_halo_wgrad_s1_ab.log)
 static bool halo_wgrad_s1_off() {
     static const bool off = [] {
-        const char* e = getenv("CAI_HALO_WGRAD_S1");
-        return !(e && *e && *e != '0');
+        const char* e = getenv("CAI_HALO_WGRAD_S1_OFF");
+        return e && *e && *e != '0';
     }();
     return off;
 }

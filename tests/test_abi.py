@@ -144,9 +144,10 @@ def test_halo_kernel_selection(native):
     assert name(G(8, 192, 128, 128, 64, 64, 64, 5, 2, 2, 0, 0), 1) == "conv_halo_phase_kernel<192>"
     assert "halo" not in name(G(16, 192, 32, 32, 192, 64, 64, 5, 2, 2, 1, 1), 0)    # 256 blocks
     assert name(G(16, 128, 64, 64, 128, 128, 128, 5, 2, 2, 1, 1), 0) == "conv_halo_phase_kernel"
-    # weight gradient: the halo-staged kernel's stride-1 form is opt-in (CAI_HALO_WGRAD_S1=1, measured no gain)
-    if os.environ.get("CAI_HALO_WGRAD_S1", "0") not in ("", "0"):
+    # weight gradient: the halo-staged kernel's stride-1 form for 64-multiple G widths
+    if os.environ.get("CAI_HALO_WGRAD_S1_OFF", "0") in ("", "0"):
         assert name(G(4, 192, 128, 128, 192, 128, 128, 3, 1, 1, 0, 0), 2) == "wgrad_halo_kernel<3,s1>"
+        assert name(G(2, 64, 512, 640, 64, 512, 640, 3, 1, 1, 0, 0), 2) == "wgrad_halo_kernel<3,s1>"
     assert "halo" not in name(G(4, 192, 32, 32, 192, 32, 32, 3, 1, 1, 0, 0), 2)
     # the stride-1 conv kernel needs >= 128 tiles (64x64 at B = 4: 64 tiles, conv_glds_kernel)
     assert "halo" not in name(G(4, 192, 64, 64, 192, 64, 64, 3, 1, 1, 0, 0), 0)
