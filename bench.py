@@ -181,9 +181,13 @@ def dominant_roofline(led, workload: str, reps: int = 20, pick=None):
     if pick is not None:
         kind, idx = pick.split(":")
         e = [x for x in ents if x.kind == kind][int(idx)]
+        ms = replay_time(e, reps)
     else:
-        e = max(ents, key=lambda x: x.ms)
-    ms = replay_time(e, reps)
+        # the single profiled step's per-launch times are noisy for short launches (a 15 us kernel can read 80 us
+        # once): the three longest launches are re-timed by replay and the longest replay is the dominant launch
+        cands = sorted(ents, key=lambda x: -x.ms)[:3]
+        timed = [(replay_time(c, reps), i, c) for i, c in enumerate(cands)]
+        ms, _, e = max(timed, key=lambda t: (t[0], -t[1]))
     bound = e.bound()
     if bound == "mfma":
         achieved, peak, unit = e.flops / (ms * 1e9), e.peak_tflops(), "TFLOP/s"
