@@ -54,7 +54,10 @@ def set_noise_source(fn: Optional[Callable[[torch.Tensor], torch.Tensor]]):
     _noise_source = fn
 
 
-# on-device generator state per GPU: [seed, draw index, arrival ticket] (uint64 bit patterns)
+# on-device generator state per GPU: [seed, draw index, arrival ticket] (uint64 bit patterns).  ONE state per
+# device: draws that use it must be ordered (one stream, or event-ordered) -- two concurrent launches would read
+# the same draw index and mix their arrival tickets.  The models' hyper-branch fork therefore draws z's noise on
+# the caller's stream before forking (models/google.py, _fork_noise).
 _noise_states: dict = {}
 # A/B knob (read once): CAI_TORCH_NOISE=1 draws with torch's generator instead (`uniform_`, as the reference)
 _TORCH_NOISE = os.environ.get("CAI_TORCH_NOISE", "0") == "1"
@@ -318,12 +321,21 @@ class EntropyBottleneck(EntropyModel):
     def loss(self) -> torch.Tensor:
         return BottleneckAuxFn.apply(self.quantiles, self.target, *self._params())
 
-    def forward(self, x: torch.Tensor, training: Optional[bool] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    def forward(self, x: torch.Tensor, training: Optional[bool] = None, noise: Optional[torch.Tensor] = None
+                ) -> Tuple[torch.Tensor, torch.Tensor]:
+        """noise: the U(-1/2, 1/2) draw to use in training mode (the models' concurrent forward draws it on the
+        caller's stream before forking the hyper branch, so every draw of a step runs on one stream); None
+        draws it here, as the reference does (entropy_models.py:495-540)."""
         if training is None:
             training = self.training
         if x.dim() < 2 or x.shape[1] != self.channels:
             raise ValueError(f"expected [B, {self.channels}, ...] input, got {tuple(x.shape)}")
-        noise = _draw_noise(x) if training else None
+        if training and noise is None:
+            noise = _draw_noise(x)
+        elif training and tuple(noise.shape) != tuple(x.shape):
+            raise ValueError(f"noise shape {tuple(noise.shape)} does not match the input's {tuple(x.shape)}")
+        elif not training:
+            noise = None
         return BottleneckFn.apply(x, self.quantiles, noise, Q_NOISE if training else Q_DEQUANTIZE,
                                   self._lik_bound(), *self._params())
 

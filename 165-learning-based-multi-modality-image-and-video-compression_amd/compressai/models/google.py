@@ -76,9 +76,24 @@ def _quantize_y(y, training):
     return _QuantizeFn.apply(y, None, noise, Q_NOISE if training else Q_DEQUANTIZE), noise
 
 
-def _cross(main, side, y, noise, outs):
+def _z_noise(model, y):
+    """z's training noise, drawn on the caller's stream BEFORE the hyper branch forks (the reference's draw
+    order: z first, entropy_models.py:495-540 called from google.py:281-295): every draw of the step then
+    runs on one stream, so the device generator's draw index and arrival ticket are never shared by two
+    concurrent launches.  z = h_a(y) has the EntropyBottleneck's channels and two stride-2 halvings
+    (k5 s2 p2 / k3 s2 p1: ceil(n / 2) each) of y's grid."""
+    if not model.training:
+        return None
+    B, _, H, W = y.shape
+    shape = (B, model.entropy_bottleneck.channels, -(-(-(-H // 2)) // 2), -(-(-(-W // 2)) // 2))
+    return _draw_noise(y.new_empty(shape, dtype=torch.float32, memory_format=torch.channels_last))
+
+
+def _cross(main, side, y, noise, outs, z_noise=None):
     """Caching-allocator bookkeeping of the tensors that cross between the two streams."""
     y.record_stream(side)
+    if z_noise is not None:
+        z_noise.record_stream(side)
     if noise is not None:
         noise.record_stream(side)
     for t in outs:
@@ -210,10 +225,11 @@ class ScaleHyperprior(CompressionModel):
             x_hat = self.g_s(y_hat)
             return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods, "z": z_likelihoods}}
         main = torch.cuda.current_stream()
+        z_noise = _z_noise(self, y)
         side.wait_stream(main)
         with torch.cuda.stream(side):
             z = self.h_a(y, input_abs=True)
-            z_hat, z_likelihoods = self.entropy_bottleneck(z)
+            z_hat, z_likelihoods = self.entropy_bottleneck(z, noise=z_noise)
             scales_hat = self.h_s(z_hat)
         y_hat, noise = _quantize_y(y, self.training)
         ready = torch.cuda.Event()
@@ -223,7 +239,7 @@ class ScaleHyperprior(CompressionModel):
             side.wait_event(ready)
             _, y_likelihoods = self.gaussian_conditional(y, scales_hat, noise=noise)
         main.wait_stream(side)
-        _cross(main, side, y, noise, (z_likelihoods, y_likelihoods))
+        _cross(main, side, y, noise, (z_likelihoods, y_likelihoods), z_noise)
         return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods, "z": z_likelihoods}}
 
     def load_state_dict(self, state_dict, strict: bool = True):
@@ -289,10 +305,11 @@ class MeanScaleHyperprior(ScaleHyperprior):
             x_hat = self.g_s(y_hat)
             return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods, "z": z_likelihoods}}
         main = torch.cuda.current_stream()
+        z_noise = _z_noise(self, y)
         side.wait_stream(main)
         with torch.cuda.stream(side):
             z = self.h_a(y)
-            z_hat, z_likelihoods = self.entropy_bottleneck(z)
+            z_hat, z_likelihoods = self.entropy_bottleneck(z, noise=z_noise)
             scales_hat, means_hat = self.h_s(z_hat).chunk(2, 1)
         y_hat, noise = _quantize_y(y, True)         # noise mode ignores the means
         ready = torch.cuda.Event()
@@ -302,7 +319,7 @@ class MeanScaleHyperprior(ScaleHyperprior):
             side.wait_event(ready)
             _, y_likelihoods = self.gaussian_conditional(y, scales_hat, means=means_hat, noise=noise)
         main.wait_stream(side)
-        _cross(main, side, y, noise, (z_likelihoods, y_likelihoods))
+        _cross(main, side, y, noise, (z_likelihoods, y_likelihoods), z_noise)
         return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods, "z": z_likelihoods}}
 
     @torch.no_grad()
@@ -444,10 +461,11 @@ class JointAutoregressiveHierarchicalPriors(_ARCoding, MeanScaleHyperprior):
             x_hat = self.g_s(y_hat)
             return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods, "z": z_likelihoods}}
         main = torch.cuda.current_stream()
+        z_noise = _z_noise(self, y)
         side.wait_stream(main)
         with torch.cuda.stream(side):
             z = self.h_a(y)
-            z_hat, z_likelihoods = self.entropy_bottleneck(z)
+            z_hat, z_likelihoods = self.entropy_bottleneck(z, noise=z_noise)
             params = self.h_s(z_hat)
         # the reference's draws in its order (z, then y_hat's, then the likelihood's)
         y_hat, noise = _quantize_y(y, self.training)
@@ -465,7 +483,7 @@ class JointAutoregressiveHierarchicalPriors(_ARCoding, MeanScaleHyperprior):
         y_hat.record_stream(side)
         if noise2 is not None:
             noise2.record_stream(side)
-        _cross(main, side, y, noise, (z_likelihoods, y_likelihoods))
+        _cross(main, side, y, noise, (z_likelihoods, y_likelihoods), z_noise)
         return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods, "z": z_likelihoods}}
 
     @torch.no_grad()

@@ -31,7 +31,6 @@
 #include "mfma.hpp"
 
 #include <algorithm>
-#include <atomic>
 #include <vector>
 
 namespace cai {
@@ -69,8 +68,6 @@ struct ConvArgs {
     int ksplit;              // K splits per phase (grid.z = nphase * ksplit)
     float* ws;               // split-K partials [nphase*ksplit][ws_rows][ws_ld] fp32
     int ws_rows, ws_ld;
-    int cnt;                 // split-K fold: 1 + the first per-tile arrival counter in cai_splitk_cnt (0, as
-                             // zero-initialised: a reduce launch sums the slabs)
     PhaseDesc ph[4];
 };
 
@@ -153,70 +150,6 @@ __device__ __forceinline__ void store_out_scalar(const ConvArgs& a, const PhaseD
     st_any(a.y, a.y_dtype, (int64_t)b * a.ysb + (int64_t)n * a.ysc + (int64_t)oy * a.ysy + (int64_t)ox * a.ysx, v);
 }
 
-// Split-K fold: after a block has written its partial tile, the block that completes the tile's last split
-// sums the tile's ksplit slabs in split order -- the order and arithmetic of conv_splitk_reduce_kernel, so
-// the output is bit-identical -- and runs the epilogue (bias, act, mask, store).  Release: every thread
-// fences its partial stores at agent scope before thread 0 counts the arrival; the last block fences again
-// before reading the other blocks' slabs (they were written through other XCDs' L2).  The counter is reset
-// by the last block, ready for the next launch / graph replay.  Tile index: the grid position with the
-// split factored out of z (z = phase * ksplit + split in every split-K conv grid).
-constexpr unsigned SPLITK_POOL = 1u << 20;
-__device__ unsigned cai_splitk_cnt[SPLITK_POOL];
-
-template <typename T, int BM, int BN, int NTH, class RowMap>
-__device__ __forceinline__ void splitk_fold(const ConvArgs& a, const PhaseDesc& P, int plane, int n0, RowMap rowm,
-                                            int slab) {
-    __shared__ int s_last;
-    // every wave's partial stores complete (in its XCD's L2) before the barrier; one wave then releases the
-    // L2 at agent scope (one write-back per block instead of one per wave)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        const unsigned tile = ((blockIdx.z / (unsigned)a.ksplit) * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-        unsigned* c = cai_splitk_cnt + (a.cnt - 1) + tile;
-        const unsigned prev = atomicAdd(c, 1u);
-        s_last = prev == (unsigned)a.ksplit - 1u;
-        if (s_last) atomicExch(c, 0u);
-        if (s_last) __threadfence();    // acquire: invalidates this XCD's L2 and the CU's L1 for every wave
-    }
-    __syncthreads();
-    if (!s_last) return;
-    const int s0 = slab - slab % a.ksplit;
-    const int64_t sl = (int64_t)a.ws_rows * a.ws_ld;
-    const int VO = (a.y_vec && a.y_dtype == CAI_BF16) ? 8 : 4;
-    const int cpr = BN / VO;
-    for (int id = threadIdx.x; id < BM * cpr; id += NTH) {
-        const int row = id / cpr;
-        const int n = n0 + (id - row * cpr) * VO;
-        const int m = rowm(row);
-        if (m < 0 || n >= a.Cout) continue;
-        const float* src = a.ws + (int64_t)s0 * sl + (int64_t)m * a.ws_ld + n;
-        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        for (int s = 0; s < a.ksplit; ++s) {
-            const f32x4 lo = *reinterpret_cast<const f32x4*>(src + s * sl);
-            v[0] += lo[0]; v[1] += lo[1]; v[2] += lo[2]; v[3] += lo[3];
-            if (VO == 8) {
-                const f32x4 hi = *reinterpret_cast<const f32x4*>(src + s * sl + 4);
-                v[4] += hi[0]; v[5] += hi[1]; v[6] += hi[2]; v[7] += hi[3];
-            }
-        }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int nn = n + e;
-            const float bv = (a.bias && nn < a.Cout) ? a.bias[nn] : 0.f;
-            v[e] = apply_act(v[e] + bv, a.act, a.act_param);
-        }
-        if (a.y_vec) {
-            store_out_chunk<T>(a, P, plane, m, n, v, VO);
-        } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if (n + e < a.Cout) store_out_scalar<T>(a, P, plane, m, n + e, v[e]);
-        }
-    }
-}
-
 // Epilogue shared by the conv kernels: the wave accumulators go through LDS as
 // fp32 [BM][BN+4]; split-K writes the raw partial tile to ws[z][m][n] (bias /
 // act / mask applied by the reduce), otherwise bias + act (+ mask) and 16-byte
@@ -253,7 +186,6 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvArgs& a, const Phas
             *reinterpret_cast<f32x4*>(dst + (int64_t)m * a.ws_ld + n) =
                 *reinterpret_cast<const f32x4*>(E + row * ES + cc * 4);
         }
-        if (a.cnt > 0) splitk_fold<T, BM, BN, NTH>(a, P, plane, n0, rowm, sb);
         return;
     }
 #pragma unroll
@@ -328,7 +260,6 @@ __device__ __forceinline__ void conv_epilogue_rows_t(const ConvArgs& a, const Ph
                 if (n < a.ws_ld) *reinterpret_cast<f32x4*>(dst + (int64_t)m * a.ws_ld + n) = acc[tm][tn];
             }
         }
-        if (a.cnt > 0) splitk_fold<T, BM, BN, NTH>(a, P, plane, n0, rowm, slab);
         return;
     }
     // (the mask variant only in the NOLDS tiles: in the 128-channel halo kernels its registers spill the loop)
@@ -3419,7 +3350,7 @@ template <typename T, typename C>
 static void launch_conv(const ConvArgs& a, const ConvLaunch& L, hipStream_t st) {
     dim3 grid(L.mtiles, L.ntiles, a.nphase * a.ksplit);
     hipLaunchKernelGGL((conv_gemm_kernel<T, C>), grid, dim3(NT), 0, st, a);
-    if (a.ksplit > 1 && a.cnt == 0) {
+    if (a.ksplit > 1) {
         const int VO = (a.y_vec && a.y_dtype == CAI_BF16) ? 8 : 4;
         const int64_t total = (int64_t)L.mmax * ((a.Cout + VO - 1) / VO);
         const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, (total + 255) / 256));
@@ -3431,7 +3362,7 @@ template <typename C>
 static void launch_conv_glds(const ConvArgs& a, const ConvLaunch& L, hipStream_t st) {
     dim3 grid(L.mtiles, L.ntiles, a.nphase * a.ksplit);
     hipLaunchKernelGGL((conv_glds_kernel<C>), grid, dim3(512), 0, st, a);
-    if (a.ksplit > 1 && a.cnt == 0) {
+    if (a.ksplit > 1) {
         const int VO = (a.y_vec && a.y_dtype == CAI_BF16) ? 8 : 4;
         const int64_t total = (int64_t)L.mmax * ((a.Cout + VO - 1) / VO);
         const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, (total + 255) / 256));
@@ -3445,7 +3376,7 @@ static void launch_conv_halo(const ConvArgs& a, const ConvLaunch& L, hipStream_t
         hipLaunchKernelGGL(conv_halo_kernel<5>, grid, dim3(512), 0, st, a, L.tiles_x, L.tiles_y);
     else
         hipLaunchKernelGGL(conv_halo_kernel<3>, grid, dim3(512), 0, st, a, L.tiles_x, L.tiles_y);
-    if (a.ksplit > 1 && a.cnt == 0) {
+    if (a.ksplit > 1) {
         const int VO = (a.y_vec && a.y_dtype == CAI_BF16) ? 8 : 4;
         const int64_t total = (int64_t)L.mmax * ((a.Cout + VO - 1) / VO);
         const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, (total + 255) / 256));
@@ -3474,7 +3405,7 @@ static void launch_conv_halo_phase(const ConvArgs& a, const ConvLaunch& L, hipSt
                 hipLaunchKernelGGL((conv_halo_s1_kernel<128, false>), grid, dim3(512), 0, st, a, L.tiles_x, L.tiles_y);
         }
     }
-    if (a.ksplit > 1 && a.cnt == 0) {
+    if (a.ksplit > 1) {
         const int VO = (a.y_vec && a.y_dtype == CAI_BF16) ? 8 : 4;
         const int64_t total = (int64_t)L.mmax * ((a.Cout + VO - 1) / VO);
         const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, (total + 255) / 256));
@@ -3523,30 +3454,9 @@ static void dispatch_conv(const ConvArgs& a, const ConvLaunch& L, hipStream_t st
     }
 }
 
-// Split-K fold counters: one pool for the library, handed out in consecutive ranges (one counter per output
-// tile of a split-K launch).  Every launch leaves its counters at zero, so a range may be reused by any later
-// launch on the same stream; ranges of launches that can run concurrently (side streams, graphs) are disjoint
-// unless 2^20 counters were handed out in between.
-// Opt-in (CAI_SPLITK_FOLD=1): measured on MI355X the fold costs more than the reduce launch it removes --
-// C2 7530 vs 8594 patches/s with one agent-scope release per block (6250 with one per wave): each release
-// writes back the XCD's L2 and each acquire invalidates it, for every split-K block of every layer
-// (profiles/r02_splitk_fold_ab.log)
-static bool splitk_fold_off() {
-    static const bool off = [] {
-        const char* e = getenv("CAI_SPLITK_FOLD");
-        return !(e && *e && *e != '0');
-    }();
-    return off;
-}
-
-static int splitk_counters(unsigned n) {
-    static std::atomic<unsigned> next{0};
-    if (n == 0 || n > SPLITK_POOL) return 0;
-    unsigned off = next.fetch_add(n) % SPLITK_POOL;
-    if (off + n > SPLITK_POOL) off = 0;    // wrap: the oldest ranges
-    return (int)off + 1;
-}
-
+// (A split-K "fold" -- the last-arriving block of a tile sums the slabs, no reduce launch -- was measured and
+// removed: C2 7530 vs 8594 patches/s, every agent-scope release writes back and every acquire invalidates the
+// XCD's L2, and it needed a library-global device counter pool; profiles/r02_splitk_fold_ab.log.)
 static int run_conv(const cai_conv_geom* g, int dtype, int direction, const void* x, int x_ld, int in_abs,
                     const void* w, const float* bias, int act, float act_param, void* y, int y_dtype, int64_t ysb,
                     int64_t ysc, int64_t ysy, int64_t ysx, const void* aux, int aux_ld, int mask_mode,
@@ -3584,13 +3494,6 @@ static int run_conv(const cai_conv_geom* g, int dtype, int direction, const void
     CAI_CHECK_ARG(L.ws_bytes == 0 || (workspace && ws_bytes >= L.ws_bytes && ((uintptr_t)workspace & 15) == 0),
                   "%s: workspace of %zu bytes required", name, L.ws_bytes);
     a.ksplit = L.ksplit; a.ws = reinterpret_cast<float*>(workspace); a.ws_rows = L.mmax; a.ws_ld = L.ws_ld;
-    a.cnt = 0;
-    if (L.ksplit > 1 && !L.small && !splitk_fold_off()) {
-        // tiles of the launch grid with the split factored out (dispatch_conv's grids)
-        const unsigned tiles = (L.halo_ph ? 4u : 1u) * (unsigned)L.mtiles * (unsigned)L.ntiles *
-                               (unsigned)((L.halo || L.halo_ph || L.halo_s1) ? 1 : P.nphase);
-        a.cnt = splitk_counters(tiles);
-    }
     for (int ph = 0; ph < P.nphase; ++ph) {
         PhaseDesc& d = a.ph[ph];
         d.oy0 = P.oy0[ph]; d.ox0 = P.ox0[ph]; d.OHg = P.OHg[ph]; d.OWg = P.OWg[ph];

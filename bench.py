@@ -160,7 +160,7 @@ def replay_time(entry, reps: int) -> float:
 
 def pmc_traffic(workload: str, kernel: str, shape: str):
     """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/pmc_traffic.json, written by
-    tools/r02_traffic.sh + tools/pmc_traffic_update.py: 2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md 'HBM'); None when no measurement
+    tools/pmc_traffic.sh + tools/pmc_traffic_update.py: 2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md 'HBM'); None when no measurement
     of this exact launch is committed."""
     try:
         recs = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))

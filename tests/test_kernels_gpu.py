@@ -92,7 +92,7 @@ CONV_CASES = [
     ("deconv", 16, 192, 128, 16, 16, 5, 2),
     ("conv", 3, 96, 40, 6, 10, 3, 1),
     # halo-staged stride-1 k3 kernel (cheng2020 residual / attention / sub-pixel 3x3 convs, >= 128 tiles), both
-    # directions: 192-channel tiles with split-K (folded into the last-arriving block), four 192-channel N tiles
+    # directions: 192-channel tiles with split-K (slabs summed by conv_splitk_reduce_kernel), four 192-channel N tiles
     # with partial column tiles, no split (one 64-channel chunk), 128-channel tiles with Cout < 128 and split-K,
     # a partial 192 + 128 N tiling
     ("conv", 2, 192, 192, 64, 256, 3, 1),

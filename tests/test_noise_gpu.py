@@ -88,3 +88,67 @@ def test_manual_seed_reproducible(cuda):
     seed_noise(2024)
     d = _draw_noise(x).clone()
     assert torch.equal(a, b) and torch.equal(a, d) and not torch.equal(a, c)
+
+
+@pytest.mark.parametrize("arch,draws", [("bmshj2018-hyperprior", 2), ("mbt2018", 3)])
+def test_hyper_stream_device_noise_one_stream(cuda, monkeypatch, arch, draws):
+    """The models' hyper branch on a side stream with the DEVICE generator (no injected noise): every draw
+    of a step runs on the caller's stream (z's before the fork), so after N graph replays the draw index
+    advanced by exactly N x the draws per step, the arrival ticket is back at 0, and z's noise, y's and
+    (mbt2018) the likelihood's second draw come from distinct counter ranges."""
+    import compressai.models.google as G
+    from compressai.entropy_models import seed_noise
+    from compressai.entropy_models.entropy_models import _as_i64, _noise_state
+    from compressai.zoo import image_models
+
+    monkeypatch.setattr(G, "_HYPER_STREAM", "1")
+    drawn = []
+    real = G._draw_noise
+
+    def rec(t):
+        n = real(t)
+        drawn.append((torch.cuda.current_stream().cuda_stream, n.detach().clone()))
+        return n
+
+    monkeypatch.setattr(G, "_draw_noise", rec)
+    import compressai.entropy_models.entropy_models as E
+
+    monkeypatch.setattr(E, "_draw_noise", rec)
+    torch.manual_seed(0)
+    net = image_models[arch](1).cuda().train()
+    x = torch.rand(2, 3, 64, 64, generator=torch.Generator().manual_seed(1)).cuda()
+    seed_noise(4321)
+    st = _noise_state(x.device)
+    main = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        out = net(x)
+        loss = sum(v.float().log().sum() for v in out["likelihoods"].values()) + out["x_hat"].float().sum()
+        loss.backward()
+
+    step()
+    torch.cuda.synchronize()
+    assert int(st[1].item()) == draws and int(st[2].item()) == 0
+    assert len(drawn) == draws and all(s == main for s, _ in drawn)
+    flat = [n.flatten() for _, n in drawn]
+    for i in range(draws):
+        for j in range(i + 1, draws):
+            k = min(flat[i].numel(), flat[j].numel())
+            assert not torch.equal(flat[i][:k], flat[j][:k]), (i, j)
+    # captured: the same invariants over replays
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        step()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    torch.cuda.synchronize()
+    before = int(st[1].item())
+    reps = 7
+    for _ in range(reps):
+        g.replay()
+    torch.cuda.synchronize()
+    assert int(st[1].item()) == _as_i64(before + reps * draws) and int(st[2].item()) == 0

@@ -1,6 +1,6 @@
 # GPU-box routine: FETCH_SIZE / WRITE_SIZE passes (one counter group per rocprofv3 run) of replayed launches
 # of the C2 step; the counter outputs land in gpurun_out/trf_<kind>_<index>_{f,w}; record them on the host
-# with tools/pmc_traffic_update.py.  usage: bash tools/r02_traffic.sh kind:index [kind:index ...]
+# with tools/pmc_traffic_update.py.  usage: bash tools/pmc_traffic.sh kind:index [kind:index ...]
 out=$GRAFT_REPO_ROOT/gpurun_out
 cd /tmp && export TMPDIR=/tmp
 for rep in "$@"; do

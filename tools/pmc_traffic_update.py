@@ -3,7 +3,7 @@ roofline `traffic` field looks up by workload / kernel / shape).
 
 usage: python tools/pmc_traffic_update.py <fetch_dir> <write_dir> <replay_log>
   fetch_dir / write_dir: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE outputs of `bench.py --roofline-only --replay
-  kind:index --steps R` (tools/r02_traffic.sh); replay_log: that run's stdout (its JSON line names the launch).
+  kind:index --steps R` (tools/pmc_traffic.sh); replay_log: that run's stdout (its JSON line names the launch).
 Per launch: read = 2 x FETCH_SIZE (gfx950 counts half the bytes of 16-byte-per-lane reads,
 MI355X_MICROARCH.md 'HBM'), write = WRITE_SIZE, both over the last R dispatches of the kernel (the replays);
 Infinity-Cache hits are included in both counts."""
