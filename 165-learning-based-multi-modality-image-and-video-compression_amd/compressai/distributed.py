@@ -7,10 +7,17 @@ flat gradient buffer of FusedAdam (20.3 MB fp32 for bmshj2018-hyperprior).
 The aux loss (EntropyBottleneck.loss) depends only on replicated parameters,
 so its gradients are identical on every rank and need no exchange.
 
-OverlappedAllReduce splits that exchange in two buckets: every gradient but
-the analysis transform's is final once the backward has reached g_a's output
-y (y feeds every other branch), so that bucket is all-reduced on a side
-stream while g_a's backward runs; the g_a bucket follows.
+OverlappedAllReduce splits that exchange in two buckets at a CUT of the
+model's graph: a set of tensors through which every path from the "tail"
+parameters to the loss runs.  Once the backward has reached the cut, every
+other ("head") gradient is final, so that bucket is all-reduced on a side
+stream while the tail's backward runs; the tail bucket follows.  The zoo
+models cut at y = g_a(x) (tail: g_a); Master_compresser cuts at its feature
+encoder / channel-aligner outputs (x_feature, guided_align -- the aligner is
+~70 % of the step's FLOPs; guided_align also feeds fdecoder, so g_a's output
+alone is not a cut).  Models declare their tail as ``dp_tail`` (parameter
+name prefixes) and mark the cut in forward with ``self._dp_cut(...)``
+(models/google.py CompressionModel).
 """
 from __future__ import annotations
 
@@ -66,40 +73,66 @@ class _Boundary(torch.autograd.Function):
 
 
 class OverlappedAllReduce:
-    """Two-bucket gradient all-reduce overlapped with the backward of `tail_module`.
+    """Two-bucket gradient all-reduce overlapped with the backward of the model's tail.
 
-    The backward runs in two phases: ``backward_head(loss)`` differentiates down to tail_module's output y
-    and into every other parameter (``torch.autograd.backward(loss, inputs=[y, *head_params])``), so
-    flat_grad[:split] -- every gradient but tail_module's (FusedAdam layout from
-    configure_optimizers(..., tail=("g_a.",))) -- is final; ``reduce_head()`` all-reduces it on a side
-    stream while ``backward_tail()`` runs tail_module's backward on the compute stream; ``finish()``
+    The backward runs in two phases: ``backward_head(loss)`` differentiates down to the cut tensors and
+    into every other parameter (``torch.autograd.backward(loss, inputs=[*cut, *head_params])``), so
+    flat_grad[:split] -- every gradient but the tail's (FusedAdam layout from
+    configure_optimizers(..., tail=model.dp_tail)) -- is final; ``reduce_head()`` all-reduces it on a side
+    stream while ``backward_tail()`` runs the tail's backward on the compute stream; ``finish()``
     all-reduces flat_grad[split:] and joins the streams.  Each phase can be captured in its own HIP
-    graph; the collectives stay outside the graphs (stream order only, no events)."""
+    graph; the collectives stay outside the graphs (stream order only, no events).
 
-    def __init__(self, flat_grad: torch.Tensor, split: int, tail_module: torch.nn.Module, head_params):
+    `tail`: a model with a ``_dp_cut`` marker (CompressionModel: the cut the model itself declares), or any
+    module whose output is a cut (a forward hook marks it: e.g. ``net.g_a`` of the zoo models).
+
+    Memory: backward_head keeps the graph (retain_graph) because backward_tail still needs the tail's saved
+    tensors; the head's saved tensors are released when the caller drops its loss tensor (bench.py's step
+    drops it on return) -- the serial backward's peak otherwise."""
+
+    def __init__(self, flat_grad: torch.Tensor, split: int, tail: torch.nn.Module, head_params):
         self.head = flat_grad[:split]
         self.tail = flat_grad[split:]
         self.head_params = [p for p in head_params if p.requires_grad]
         self.side = torch.cuda.Stream(device=flat_grad.device)
-        self._y = None
-        self._handle = tail_module.register_forward_hook(self._keep)
+        self._ys = []
+        self._model = None
+        self._handle = None
+        if hasattr(tail, "_dp_cut") and hasattr(tail, "dp_tail"):
+            self._model = tail
+            tail._dp_cut_fn = self._mark
+        else:
+            self._handle = tail.register_forward_hook(self._keep)
+
+    @classmethod
+    def for_model(cls, model: torch.nn.Module, opt):
+        """The exchange of `model` over FusedAdam `opt` built by configure_optimizers(model, tail=model.dp_tail)."""
+        tail = tuple(model.dp_tail)
+        head = [p for n, p in model.named_parameters()
+                if not n.startswith(tail) and not n.endswith(".quantiles")]
+        return cls(opt.flat_grad, opt.tail_offset, model, head)
+
+    def _mark(self, *ts):
+        # boundary nodes: phase 1's capture of a cut tensor's gradient may execute its grad_fn, which for
+        # the product convs writes parameter gradients as a side effect; an identity node in between has none
+        out = tuple(_Boundary.apply(t) for t in ts)
+        self._ys.extend(out)
+        return out
 
     def _keep(self, module, inputs, output):
-        # the boundary node: phase 1's capture of y's gradient may execute y's grad_fn, which for the
-        # product convs writes parameter gradients as a side effect; an identity node in between has none
-        self._y = _Boundary.apply(output)
-        return self._y
+        return self._mark(output)[0]
 
     def backward_head(self, loss: torch.Tensor):
-        if self._y is None:
-            raise RuntimeError("OverlappedAllReduce: the tail module did not run in this forward")
+        if not self._ys:
+            raise RuntimeError("OverlappedAllReduce: the forward did not reach the cut")
         # retain_graph: the engine releases the saved tensors of every node of the graph it was given,
-        # including g_a's, which backward_tail still needs
-        torch.autograd.backward(loss, inputs=[self._y] + self.head_params, retain_graph=True)
+        # including the tail's, which backward_tail still needs
+        torch.autograd.backward(loss, inputs=list(self._ys) + self.head_params, retain_graph=True)
 
     def backward_tail(self):
-        y, self._y = self._y, None
-        torch.autograd.backward(y, grad_tensors=y.grad)
+        ys, self._ys = self._ys, []
+        used = [y for y in ys if y.grad is not None]
+        torch.autograd.backward(used, grad_tensors=[y.grad for y in used])
 
     def reduce_head(self):
         self.side.wait_stream(torch.cuda.current_stream())
@@ -117,4 +150,7 @@ class OverlappedAllReduce:
         cur.wait_stream(self.side)
 
     def remove(self):
-        self._handle.remove()
+        if self._handle is not None:
+            self._handle.remove()
+        if self._model is not None:
+            self._model._dp_cut_fn = None

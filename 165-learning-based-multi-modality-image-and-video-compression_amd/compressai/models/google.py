@@ -86,7 +86,7 @@ def _z_noise(model, y):
         return None
     B, _, H, W = y.shape
     shape = (B, model.entropy_bottleneck.channels, -(-(-(-H // 2)) // 2), -(-(-(-W // 2)) // 2))
-    return _draw_noise(y.new_empty(shape, dtype=torch.float32, memory_format=torch.channels_last))
+    return _draw_noise(torch.empty(shape, dtype=torch.float32, device=y.device, memory_format=torch.channels_last))
 
 
 def _cross(main, side, y, noise, outs, z_noise=None):
@@ -105,6 +105,17 @@ def get_scale_table(min=SCALES_MIN, max=SCALES_MAX, levels=SCALES_LEVELS):
 
 
 class CompressionModel(nn.Module):
+    # data parallelism (compressai.distributed.OverlappedAllReduce): the parameters upstream of the cut the
+    # forward marks with _dp_cut (name prefixes), exchanged in the second bucket
+    dp_tail = ("g_a.",)
+    _dp_cut_fn = None
+
+    def _dp_cut(self, *ts):
+        """Identity, unless a two-bucket exchange is attached: then boundary nodes for its two-phase backward."""
+        if self._dp_cut_fn is not None:
+            ts = self._dp_cut_fn(*ts)
+        return ts[0] if len(ts) == 1 else ts
+
     def __init__(self, entropy_bottleneck_channels, init_weights=None):
         super().__init__()
         self.entropy_bottleneck = EntropyBottleneck(entropy_bottleneck_channels)
@@ -168,7 +179,7 @@ class FactorizedPrior(CompressionModel):
         return 2 ** 4
 
     def forward(self, x):
-        y = self.g_a(x)
+        y = self._dp_cut(self.g_a(x))
         y_hat, y_likelihoods = self.entropy_bottleneck(y)
         x_hat = self.g_s(y_hat)
         return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods}}
@@ -215,7 +226,7 @@ class ScaleHyperprior(CompressionModel):
         return 2 ** (4 + 2)
 
     def forward(self, x):
-        y = self.g_a(x)
+        y = self._dp_cut(self.g_a(x))
         side = _side_stream(y, False)
         if side is None:
             z = self.h_a(y, input_abs=True)          # h_a(|y|)
@@ -295,7 +306,7 @@ class MeanScaleHyperprior(ScaleHyperprior):
                               nn.LeakyReLU(inplace=True), conv(M * 3 // 2, M * 2, stride=1, kernel_size=3))
 
     def forward(self, x):
-        y = self.g_a(x)
+        y = self._dp_cut(self.g_a(x))
         side = _side_stream(y, False) if self.training else None   # eval: y_hat = round(y - means) + means
         if side is None:
             z = self.h_a(y)
@@ -447,7 +458,7 @@ class JointAutoregressiveHierarchicalPriors(_ARCoding, MeanScaleHyperprior):
         self.context_prediction = MaskedConv2d(M, 2 * M, kernel_size=5, padding=2, stride=1)
 
     def forward(self, x):
-        y = self.g_a(x)
+        y = self._dp_cut(self.g_a(x))
         side = _side_stream(y, True)
         if side is None:
             z = self.h_a(y)

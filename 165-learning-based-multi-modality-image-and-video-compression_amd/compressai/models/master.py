@@ -377,6 +377,11 @@ def _entropy(model, y):
 class Master_compresser(_ARCoding, MeanScaleHyperprior):
     """master.py:837-951: net(x, guided_hat, guided_hidden) -> {"x_hat", "likelihoods"}."""
 
+    # data parallelism: the feature encoders + channel aligner are the tail (guided_align also feeds fdecoder,
+    # so the cut is {x_feature, guided_align}, not g_a's output); the inherited g_s is never used (its
+    # gradients stay zero, as in the reference, master.py:839)
+    dp_tail = ("fencoder1.", "fencoder2.", "ch_aligner.")
+
     def __init__(self, width=256, height=256, channel=3, N=192, M=192):
         super().__init__(M, M)
         master_chl, guided_chl, master_stride, guided_stride = 3, 1, 2, 1
@@ -395,6 +400,7 @@ class Master_compresser(_ARCoding, MeanScaleHyperprior):
         x_feature = self.fencoder1(x)
         guided_feature = self.fencoder2(guided_hat)
         guided_align, beta, gamma = self.ch_aligner(x_feature, guided_feature)
+        x_feature, guided_align = self._dp_cut(x_feature, guided_align)
         y = self.g_a(CatFn.apply(x_feature, guided_align))
         y_hat, y_lik, z_lik = _entropy(self, y)
         res = self.decoder(y_hat, guided_hidden)

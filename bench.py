@@ -316,16 +316,14 @@ def main():
         x = torch.rand(args.batch, 3, args.size, args.size, generator=gen).to(dev)
     broadcast_parameters_(net)
     torch.cuda.manual_seed(1000 + rank)      # per-rank training noise
-    # N > 1: the gradient exchange in two buckets, the first overlapped with the analysis transform's
-    # backward (compressai.distributed.OverlappedAllReduce); Master_compresser keeps the single exchange
-    overlap = world > 1 and not multimodal and hasattr(net, "g_a") and not args.serial_allreduce
+    # N > 1: the gradient exchange in two buckets, the first overlapped with the backward of the model's tail
+    # (compressai.distributed.OverlappedAllReduce: g_a for the zoo models; the feature encoders + channel
+    # aligner for Master_compresser)
+    overlap = world > 1 and not args.serial_allreduce
     # the reference loop order (zero_grad, forward, backward, step): the Adam kernels consume the gradients
     # and zero_grad() launches nothing (FusedAdam zero_grad_in_step)
-    opt, aux_opt = configure_optimizers(net, tail=("g_a.",) if overlap else (), zero_grad_in_step=not args.keep_grads)
-    sync = None
-    if overlap:
-        head = [p for n, p in net.named_parameters() if not n.startswith("g_a.") and not n.endswith(".quantiles")]
-        sync = OverlappedAllReduce(opt.flat_grad, opt.tail_offset, net.g_a, head)
+    opt, aux_opt = configure_optimizers(net, tail=net.dp_tail if overlap else (), zero_grad_in_step=not args.keep_grads)
+    sync = OverlappedAllReduce.for_model(net, opt) if overlap else None
     criterion = RateDistortionLoss(args.quality)
     state = {}
 
@@ -464,7 +462,8 @@ def main():
                        "model": args.model, "quality": args.quality, "global_batch": args.batch * world,
                        "per_gpu_batch": args.batch, "seq_len": None,
                        "patch": list(MM_IR) if multimodal else args.size, "parallelism": f"dp{world}",
-                       "grad_exchange": ("2-bucket all-reduce, head overlapped with g_a backward (2-phase backward)" if sync else
+                       "grad_exchange": (f"2-bucket all-reduce, head overlapped with the {'+'.join(p.rstrip('.') for p in net.dp_tail)} "
+                                         "backward (2-phase backward)" if sync else
                                          "1 all-reduce after backward") if world > 1 else None},
             "final_loss": round(loss, 5),
             "roofline": roof, "step_roofline": step_roof, "cpu_baseline": cpu,

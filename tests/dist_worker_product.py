@@ -1,8 +1,11 @@
 """One rank of tests/test_distributed_gpu.py (not collected by pytest).
 
-Rank r of a world-2 job on cuda:0 (gloo over CUDA tensors): the product ScaleHyperprior, FusedAdam, a
-HIP-graph-captured forward + RD loss + backward with the injected noise read from static device buffers, then
-compressai.distributed.allreduce_mean_(opt.flat_grad) -- the exchange bench.py runs between its two graphs.
+Rank r of a world-2 job on cuda:0 (gloo over CUDA tensors): a product model ($CAI_DIST_MODEL: "c2" =
+ScaleHyperprior(32, 48), "cheng2020-attn" = Cheng2020Attention(192), "multimodal" = Master_compresser(IR)
+guided by a replicated, frozen Guided_compresser(RGB) run under no_grad in training mode, train.py:208-246),
+FusedAdam, a HIP-graph-captured forward + RD loss + backward with the injected noise read from static device
+buffers, then the gradient exchange bench.py runs: one all-reduce of the flat gradient (serial) or the
+two-bucket OverlappedAllReduce at the model's cut (overlap / overlap-eager).
 Writes the averaged flat gradient (rank 0) to $CAI_DIST_OUT.
 """
 import os
@@ -21,46 +24,70 @@ import torch.distributed as dist  # noqa: E402
 gT = None
 
 
+def build(kind):
+    """(model, guide model or None) of the product path for `kind` (the oracle side mirrors it in the test)."""
+    from compressai.models import Cheng2020Attention, Guided_compresser, Master_compresser, ScaleHyperprior
+
+    if kind == "c2":
+        return ScaleHyperprior(32, 48), None
+    if kind == "cheng2020-attn":
+        return Cheng2020Attention(192), None
+    if kind == "multimodal":
+        return Master_compresser(width=64, height=64, channel=1), Guided_compresser(channel=3)
+    raise ValueError(kind)
+
+
 def main():
     global gT
     from compressai.distributed import OverlappedAllReduce, allreduce_mean_, broadcast_parameters_, init_from_env
     from compressai.entropy_models import set_noise_source
     from compressai.losses import RateDistortionLoss
-    from compressai.models import ScaleHyperprior
     from compressai.optim import configure_optimizers, parameter_groups
 
     inp = torch.load(os.environ["CAI_DIST_IN"], weights_only=True)
+    kind = os.environ.get("CAI_DIST_MODEL", "c2")
     rank, world = init_from_env(backend="gloo")
     assert world == 2
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
-    net = ScaleHyperprior(32, 48)
+    net, guide = build(kind)
     net.load_state_dict(inp["state_dict"])
     net = net.to(dev).train()
     broadcast_parameters_(net)
+    if guide is not None:
+        guide.load_state_dict(inp["guide_state_dict"])
+        guide = guide.to(dev).train()
+        broadcast_parameters_(guide)                 # replicated, frozen: never exchanged
     mode = os.environ.get("CAI_DIST_MODE", "serial")
     overlap = mode.startswith("overlap")
-    opt, aux_opt = configure_optimizers(net, tail=("g_a.",) if overlap else ())
-    head = [p for n, p in net.named_parameters() if not n.startswith("g_a.") and not n.endswith(".quantiles")]
-    sync = OverlappedAllReduce(opt.flat_grad, opt.tail_offset, net.g_a, head) if overlap else None
+    opt, aux_opt = configure_optimizers(net, tail=net.dp_tail if overlap else ())
+    sync = OverlappedAllReduce.for_model(net, opt) if overlap else None
     b = inp["x"].shape[0] // world
     sl = slice(rank * b, (rank + 1) * b)
     x = inp["x"][sl].to(dev)
+    gx = inp["guide_x"][sl].to(dev) if guide is not None else None
     noise = [n[sl].to(dev) for n in inp["noise"]]
     draw = {"i": 0}
 
     def source(t):
         n = noise[draw["i"] % len(noise)]
         draw["i"] += 1
+        if tuple(n.shape) != tuple(t.shape):
+            raise RuntimeError(f"noise draw {draw['i'] - 1}: {tuple(n.shape)} vs {tuple(t.shape)}")
         return n
 
     set_noise_source(source)
-    crit = RateDistortionLoss(1)
+    crit = RateDistortionLoss(inp["quality"])
 
     def fwd_bwd():
         opt.zero_grad()
         aux_opt.zero_grad()
-        out = net(x)
+        if guide is not None:
+            with torch.no_grad():
+                hidden = guide(gx)["hidden"]
+            out = net(x, gx, hidden)
+        else:
+            out = net(x)
         loss = crit(out, x)["loss"]
         if sync is None:
             loss.backward()
@@ -106,7 +133,8 @@ def main():
     if rank == 0:
         main_names, _ = parameter_groups(net)
         torch.save({"flat_grad": opt.flat_grad.cpu(), "offsets": list(opt.offsets), "names": main_names,
-                    "numels": [p.numel() for p in opt.params]}, os.environ["CAI_DIST_OUT"])
+                    "numels": [p.numel() for p in opt.params], "tail_offset": int(opt.tail_offset)},
+                   os.environ["CAI_DIST_OUT"])
     dist.barrier()
     dist.destroy_process_group()
 
