@@ -12,7 +12,18 @@ conv_halo_phase_kernel<192> >= 512 blocks, so the 64-128 px model tests never di
   1024x1280 RGB, B=2: bf16 loss within 2 % of the HIP fp32 step, finite gradients.
 
 Bars as in test_models_wide_gpu.py (fp32: 1e-4 outputs / 2e-3 gradients against float64, or 2x the fp32
-oracle's own error; bf16: x_hat 1e-2, likelihoods 2e-2, loss 1e-3, gradient cosine)."""
+oracle's own error; bf16: x_hat 1e-2, loss 1e-3, gradient cosine), with two additions that production sizes
+force, both measured on MI355X (profiles/r03_graddiff_*.log):
+* ReLU / LeakyReLU mask flips.  A pre-activation within fp32 round-off of 0 takes the other branch in one fp32
+  path and not in the other; its gradient element then differs by the whole incoming gradient.  At 256x256
+  this happens in BOTH fp32 paths: with seed 32 the CPU fp32 oracle itself misses a cheng2020 attention-unit
+  weight gradient by 4.8e-3 (max norm) against float64, with seed 31 the HIP path misses another by 4.9e-3
+  while the CPU does not.  A tensor whose max-norm error exceeds the bar therefore passes on its relative L2
+  error (<= 5e-3: the flipped element is one term of the sum), and at most 2 % of the tensors may use that
+  allowance.
+* bf16 likelihoods: the max-norm error grows with the element count (196K y elements at B=4 vs 6K in the
+  64x64 tests: 2.2e-2 measured); bounded at 5e-2 max and 5e-3 relative L2.
+"""
 import math
 
 import pytest
@@ -98,15 +109,24 @@ def test_cheng2020_attn_fp32_parity_256(cuda):
     for k in ("loss", "bpp_loss", "mse_loss"):
         assert abs(c[k].item() - cr[k].item()) <= 1e-4 * max(1.0, abs(cr[k].item())), k
     pr, p64 = dict(ref.named_parameters()), dict(r64.named_parameters())
+    flips, total = [], 0
     for n, p in net.named_parameters():
         gr = pr[n].grad
         if gr is None:
             assert p.grad is None or p.grad.abs().max().item() == 0, n
             continue
-        check(p.grad, gr, p64[n].grad, 2e-3, n)
+        total += 1
+        e, e32 = relerr(p.grad, p64[n].grad), relerr(gr, p64[n].grad)
+        if e < max(2e-3, 2 * e32):
+            continue
+        el2 = rel_l2(p.grad, p64[n].grad)          # a mask flip: one term of the sum (module docstring)
+        assert el2 < 5e-3, (n, e, e32, el2)
+        flips.append((n, round(e, 6), round(el2, 6)))
+    print(f"\nfp32 cheng2020-attn 256: mask-flip allowance used by {len(flips)} of {total} tensors: {flips}")
+    assert len(flips) <= 0.02 * total, flips
 
 
-BF16_XHAT, BF16_LIK, BF16_LOSS, GRAD_COS, TENSOR_COS = 1e-2, 2e-2, 1e-3, 0.9999, 0.98
+BF16_XHAT, BF16_LIK, BF16_LIK_L2, BF16_LOSS, GRAD_COS, TENSOR_COS = 1e-2, 5e-2, 5e-3, 1e-3, 0.9999, 0.98
 
 
 @pytest.mark.parametrize("name,args,batch,quality,gated", [
@@ -118,6 +138,7 @@ def test_bf16_production_mix_256(cuda, name, args, batch, quality, gated):
     assert gated in kernels, sorted(kernels)
     ex = relerr(out["x_hat"], out_r["x_hat"])
     el = {k: relerr(out["likelihoods"][k], out_r["likelihoods"][k]) for k in out_r["likelihoods"]}
+    el2 = {k: rel_l2(out["likelihoods"][k], out_r["likelihoods"][k]) for k in out_r["likelihoods"]}
     eloss = abs(c["loss"].item() - cr["loss"].item()) / abs(cr["loss"].item())
     pr = dict(ref.named_parameters())
     tcos, dots, na, nb = {}, 0.0, 0.0, 0.0
@@ -133,10 +154,11 @@ def test_bf16_production_mix_256(cuda, name, args, batch, quality, gated):
         nb += float((gr.double() ** 2).sum())
     cos = dots / math.sqrt(na * nb)
     low = sorted(tcos.items(), key=lambda kv: kv[1])[:3]
-    print(f"\nbf16 {name} B={batch}: x_hat {ex:.3e} lik {el} loss {eloss:.3e} grad cos {cos:.6f} lowest {low}")
+    print(f"\nbf16 {name} B={batch}: x_hat {ex:.3e} lik {el} (L2 {el2}) loss {eloss:.3e} grad cos {cos:.6f} "
+          f"lowest {low}")
     assert ex < BF16_XHAT
     for k, v in el.items():
-        assert v < BF16_LIK, k
+        assert v < BF16_LIK and el2[k] < BF16_LIK_L2, k
     assert eloss < BF16_LOSS
     assert cos > GRAD_COS
     assert low[0][1] > TENSOR_COS, low
@@ -183,9 +205,17 @@ def test_spatial_aligner_paper_grids(cuda, res):
         assert relerr(p.grad, pr[n].grad) < 2e-3, n
 
 
-def test_channel_aligner_512x640(cuda):
+@pytest.mark.parametrize("bf16", [False, True], ids=["fp32", "bf16"])
+def test_channel_aligner_512x640(cuda, bf16):
     """Channel_aligner (4 x conv3x3(256) trunk per branch, conv5/conv6 heads, global pools) on the IR
-    config's 64-channel 512x640 features, fp32 B=1, against the oracle module on the GPU in fp32."""
+    config's 64-channel 512x640 features, B=1, against the oracle module run on the GPU in fp32 (torch's
+    convolutions, TF32 off).  fp32: outputs within 1e-4 (max norm); gradients within 5e-3 relative L2 --
+    84M pre-activations per LeakyReLU layer put some within round-off of 0 (module docstring), and the beta
+    branch's input gradient is the trunk's backward of a spatially uniform gradient, a sum with heavy
+    cancellation (measured: d1 1.3e-3 L2, everything else <= 2e-4).  bf16 (the production kernels: the
+    256-channel convs take conv_halo_s1_kernel): outputs 1e-2, every gradient's cosine >= 0.999 or within 2x
+    the distance of torch's own bf16 autocast of the same module (d1's cancelling sum: ~0.995 in bf16)."""
+    from compressai import _ledger
     from compressai.models.master import Channel_aligner
 
     prev = (torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32)
@@ -201,24 +231,47 @@ def test_channel_aligner_512x640(cuda):
         f2 = torch.randn(1, 64, 512, 640, generator=gen)
         g = torch.randn(1, 64, 512, 640, generator=gen).to(cuda)
         r1, r2 = f1.to(cuda).requires_grad_(), f2.to(cuda).requires_grad_()
+        tcos = {}
+        if bf16:
+            # torch's own bf16 autocast of the same module: the bf16 error the HIP path is measured against
+            t1, t2 = f1.to(cuda).requires_grad_(), f2.to(cuda).requires_grad_()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                ot = ref(t1, t2)[0]
+            (ot.float() * g).sum().backward()
+            tgr = {"d1": t1.grad, "d2": t2.grad, **{n: p.grad.clone() for n, p in ref.named_parameters()}}
+            ref.zero_grad(set_to_none=True)
         out_r, beta_r, gamma_r = ref(r1, r2)
         (out_r * g).sum().backward()
         d1 = f1.to(cuda).contiguous(memory_format=torch.channels_last).requires_grad_()
         d2 = f2.to(cuda).contiguous(memory_format=torch.channels_last).requires_grad_()
-        out, beta, gamma = mod(d1, d2)
-        (out * g).sum().backward()
-        errs = {"out": (relerr(out, out_r), rel_l2(out, out_r)), "beta": (relerr(beta, beta_r), rel_l2(beta, beta_r)),
-                "gamma": (relerr(gamma, gamma_r), rel_l2(gamma, gamma_r)),
-                "d1": (relerr(d1.grad, r1.grad), rel_l2(d1.grad, r1.grad)),
-                "d2": (relerr(d2.grad, r2.grad), rel_l2(d2.grad, r2.grad))}
+        with _ledger.recording(keep_replay=False) as led:
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=bf16):
+                out, beta, gamma = mod(d1, d2)
+            (out.float() * g).sum().backward()
+            torch.cuda.synchronize()
+        kernels = {e.kernel for e in led.entries}
+        outs = {"out": (out, out_r), "beta": (beta, beta_r), "gamma": (gamma, gamma_r)}
+        grads = {"d1": (d1.grad, r1.grad), "d2": (d2.grad, r2.grad)}
         pr = dict(ref.named_parameters())
         for n, p in mod.named_parameters():
-            errs[n] = (relerr(p.grad, pr[n].grad), rel_l2(p.grad, pr[n].grad))
-        print("\nChannel_aligner 512x640 (max, rel-L2):", {k: (f"{a:.2e}", f"{b:.2e}") for k, (a, b) in errs.items()})
-        for k in ("out", "beta", "gamma"):
-            assert errs[k][0] < 1e-4, (k, errs[k])
-        for k, (emax, el2) in errs.items():
-            assert el2 < 1e-4, (k, emax, el2)
+            grads[n] = (p.grad, pr[n].grad)
+        errs = {k: (relerr(a, b), rel_l2(a, b)) for k, (a, b) in {**outs, **grads}.items()}
+        cos = {k: float(torch.nn.functional.cosine_similarity(a.double().flatten(), b.double().flatten(), dim=0))
+               for k, (a, b) in grads.items()}
+        print(f"\nChannel_aligner 512x640 {'bf16' if bf16 else 'fp32'} (max, rel-L2):",
+              {k: (f"{a:.2e}", f"{b:.2e}") for k, (a, b) in errs.items()}, "lowest cos", min(cos.values()))
+        for k in outs:
+            assert errs[k][0] < (1e-2 if bf16 else 1e-4), (k, errs[k])
+        if bf16:
+            assert "conv_halo_s1_kernel<128>" in kernels or "conv_halo_s1_kernel<192>" in kernels, sorted(kernels)
+            tcos = {k: float(torch.nn.functional.cosine_similarity(tgr[k].double().flatten(), b.double().flatten(),
+                                                                    dim=0)) for k, (_, b) in grads.items()}
+            print("torch bf16 autocast lowest cos", min(tcos.values()), "d1", tcos["d1"], "HIP d1", cos["d1"])
+            for k, v in cos.items():        # >= 0.999, or no more than 2x torch's own bf16 distance
+                assert v >= min(0.999, 1 - 2 * (1 - tcos[k])), (k, v, tcos[k])
+        else:
+            for k in grads:
+                assert errs[k][1] < 5e-3, (k, errs[k])
     finally:
         torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32 = prev
 
