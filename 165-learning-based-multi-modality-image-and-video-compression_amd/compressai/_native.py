@@ -54,6 +54,13 @@ class EbGrads(Structure):
                 ("accumulate", c_int32)]
 
 
+JOB_NONE, JOB_WGRAD, JOB_GDN = 0, 1, 2           # cai_reduce_job kinds (include/cai.h)
+
+
+class ReduceJob(Structure):
+    _fields_ = [("kind", c_int32), ("nblocks", c_int32), ("i", c_int32 * 10), ("f", c_float * 2), ("p", c_void_p * 6)]
+
+
 # name -> (restype, argtypes)
 _P, _I, _I64, _F, _S = c_void_p, c_int, c_int64, c_float, c_size_t
 _G = POINTER(ConvGeom)
@@ -76,6 +83,9 @@ SIGNATURES = {
     "cai_conv_kernel_name": (c_char_p, [_G, _I, _I, c_int32]),
     "cai_conv_split_factor": (c_int32, [_G, _I, _I, c_int32]),
     "cai_conv_wgrad": (_I, [_G, _I, _P, c_int32, c_int32, c_int32, _P, c_int32, _P, _P, c_int32, _P, _S, _P]),
+    "cai_conv_wgrad_deferred": (_I, [_G, _I, _P, c_int32, c_int32, c_int32, _P, c_int32, _P, _P, c_int32, _P, _S, _P,
+                                     POINTER(ReduceJob)]),
+    "cai_reduce_jobs": (_I, [POINTER(ReduceJob), c_int32, _P]),
     "cai_deconv_small_workspace_bytes": (_S, [_G, _I]),
     "cai_deconv_small_fwd": (_I, [_G, _I, _P, c_int32, _P, _P, _P, _P, _S, _P]),
     "cai_deconv_small_bwd": (_I, [_G, _I, _P, c_int32, _P, _P, _P, c_int32, _P, _P, c_int32, _P, _S, _P]),
@@ -119,6 +129,8 @@ SIGNATURES = {
     "cai_gdn_backward_workspace_bytes": (_S, [_I64, c_int32, _I]),
     "cai_gdn_backward": (_I, [_I, _P, c_int32, _P, c_int32, _I64, c_int32, _P, _P, c_int32, _P, c_int32, _P, _P, _F, _F,
                               _P, _P, c_int32, _P, _S, _P]),
+    "cai_gdn_backward_deferred": (_I, [_I, _P, c_int32, _P, c_int32, _I64, c_int32, _P, _P, c_int32, _P, c_int32, _P,
+                                       _P, _F, _F, _P, _P, c_int32, _P, _S, _P, POINTER(ReduceJob)]),
     "cai_uniform_noise": (_I, [_P, _I64, _P, _P]),
     "cai_quantize": (_I, [_I, _I64, c_int32, _P, _I, c_int32, _P, c_int32, c_int32, _P, c_int32, _P, _I, c_int32, _P]),
     "cai_gc_fwd": (_I, [_I, _I64, c_int32, _P, _I, c_int32, _P, c_int32, _P, c_int32, _I, _P, c_int32, _F, _F,

@@ -27,7 +27,7 @@ import torch
 
 from . import _ledger
 from ._native import (ACT_LEAKY, ACT_NONE, ACT_RELU, BF16, F32, MASK_LEAKY, MASK_NONE, MASK_POS, Q_DEQUANTIZE, Q_NOISE,
-                      ConvGeom, EbGrads, EbParams, RdGrads, RdInputs, lib)
+                      JOB_NONE, ConvGeom, EbGrads, EbParams, RdGrads, RdInputs, ReduceJob, lib)
 
 _VP = ctypes.c_void_p
 _GDN_TWO_PASS = os.environ.get("CAI_GDN_TWO_PASS", "0") == "1"   # A/B knobs (tools/gpu_ab.sh)
@@ -114,6 +114,62 @@ class _WgradLaunch:
             _WPENDING.add(dev)
             torch.autograd.Variable._execution_engine.queue_callback(lambda: _join_wgrad(dev))
         return False
+
+
+# ---------------------------------------------------------------------------
+# deferred parameter-gradient reduces (cai_reduce_jobs, csrc/reduce_jobs.hip)
+# ---------------------------------------------------------------------------
+# The weight gradients that land straight in the optimizer's flat buffer (direct_grad) are read by nothing
+# before the optimizer, so their final fixed-order reduces (conv weight-gradient slabs, fused-GDN partials)
+# are queued per stream during the backward pass and run in ONE launch (per 16 jobs) from an autograd final
+# callback -- before backward() returns, so .grad reads after backward see the finished values -- instead of
+# one launch after every layer.  The job's workspace is kept alive until that launch.  Bit-identical to the
+# immediate path (same kernel).  Off under the per-launch ledger (it replays single calls) and when a weight
+# gradient runs on the side stream.  CAI_DEFER_REDUCE=0 turns it off (A/B).
+_DEFER_REDUCE = os.environ.get("CAI_DEFER_REDUCE", "1") == "1"
+_JOBS = {}          # device index -> [jobs, their streams, keep-alive tensors]
+
+
+def _flush_jobs(dev):
+    """Run the queued jobs of `dev` on the current stream (the backward caller's, as DDP's finalize uses it),
+    after it has waited for every other stream a job's partial kernel ran on (the hyper branch's side stream:
+    inside a captured graph this is the join edge)."""
+    pend = _JOBS.pop(dev, None)
+    if not pend or not pend[0]:
+        return
+    jobs, streams, keep = pend
+    cur = torch.cuda.current_stream(dev)
+    for s in {s.cuda_stream: s for s in streams}.values():
+        if s.cuda_stream != cur.cuda_stream:
+            cur.wait_stream(s)
+    arr = (ReduceJob * len(jobs))(*jobs)
+    lib.cai_reduce_jobs(arr, len(jobs), _VP(cur.cuda_stream))
+    for t in keep:
+        t.record_stream(cur)    # the caching allocator frees them for reuse only after these launches
+
+
+def defer_reduce_ok(direct: bool) -> bool:
+    return _DEFER_REDUCE and direct and _ledger.active() is None and not _WGRAD_STREAM
+
+
+def defer_job(job: "ReduceJob", device: torch.device, *keep: torch.Tensor):
+    """Queue `job` (filled by a cai_*_deferred call on the current stream) until the end of this backward."""
+    if job.kind == JOB_NONE:
+        return
+    dev = device.index if device.index is not None else torch.cuda.current_device()
+    pend = _JOBS.get(dev)
+    if pend is None:
+        pend = _JOBS[dev] = [[], [], []]
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: _flush_jobs(dev))
+    pend[0].append(job)
+    pend[1].append(torch.cuda.current_stream(dev))
+    pend[2].extend(t for t in keep if t is not None)
+
+
+def flush_deferred_reduces():
+    """Run every queued reduce now (callers that drive the kernels outside autograd)."""
+    for dev in list(_JOBS):
+        _flush_jobs(dev)
 
 
 def _p(t: Optional[torch.Tensor]) -> Optional[_VP]:
@@ -529,13 +585,20 @@ class ConvFn(torch.autograd.Function):
                 dw = torch.empty(weight.shape, dtype=torch.float32, device=gy.device)
                 db = torch.empty(g.out_c, dtype=torch.float32, device=gy.device) if ctx.has_bias else None
             fl, nb = _ledger.conv_cost(g, _es(dt), 2)
-            with _WgradLaunch(gy.device, direct, xpm, gpm):
+            if defer_reduce_ok(direct):
                 wws = torch.empty(nbytes, dtype=torch.uint8, device=gy.device)
-                sw = _stream()
-                _ledger.run(lambda dw=dw, db=db: lib.cai_conv_wgrad(ctypes.byref(g), code, _p(xpm), ctx.xld,
-                                                                    int(spec.in_abs), 0, _p(gpm), gld, _p(dw),
-                                                                    _p(db), int(direct), _p(wws), nbytes, sw),
-                            "conv_wgrad", _conv_kernel(g, dt, 2, spec.in_abs), fl, nb, dt, _ledger.shape_of(g))
+                job = ReduceJob()
+                lib.cai_conv_wgrad_deferred(ctypes.byref(g), code, _p(xpm), ctx.xld, int(spec.in_abs), 0, _p(gpm),
+                                            gld, _p(dw), _p(db), 1, _p(wws), nbytes, st, ctypes.byref(job))
+                defer_job(job, gy.device, wws)
+            else:
+                with _WgradLaunch(gy.device, direct, xpm, gpm):
+                    wws = torch.empty(nbytes, dtype=torch.uint8, device=gy.device)
+                    sw = _stream()
+                    _ledger.run(lambda dw=dw, db=db: lib.cai_conv_wgrad(ctypes.byref(g), code, _p(xpm), ctx.xld,
+                                                                        int(spec.in_abs), 0, _p(gpm), gld, _p(dw),
+                                                                        _p(db), int(direct), _p(wws), nbytes, sw),
+                                "conv_wgrad", _conv_kernel(g, dt, 2, spec.in_abs), fl, nb, dt, _ledger.shape_of(g))
             if direct:
                 dw = db = None
             elif weight.dtype != torch.float32:
@@ -605,6 +668,12 @@ class GdnFn(torch.autograd.Function):
             ws2 = torch.empty(nb2, dtype=torch.uint8, device=gy.device)
             lib.cai_gdn_param_grad(code, _p(xpm), xld, _p(u), npix, C, _p(br), _p(gr), beta_min, off, _p(dbr),
                                    _p(dgr), int(direct), _p(ws2), nb2, st)
+        elif defer_reduce_ok(direct):
+            job = ReduceJob()
+            lib.cai_gdn_backward_deferred(code, _p(xpm), xld, _p(gpm), gld, npix, C, _p(gop), _p(beta), inverse,
+                                          _p(dx), C, _p(br), _p(gr), beta_min, off, _p(dbr), _p(dgr), 1, _p(ws),
+                                          nbytes, st, ctypes.byref(job))
+            defer_job(job, gy.device, ws, br, gr)
         else:
             # dx and the parameter gradients in one call (fused pass for bf16, C in {64, 128})
             _ledger.run(lambda dbr=dbr, dgr=dgr: lib.cai_gdn_backward(code, _p(xpm), xld, _p(gpm), gld, npix, C, _p(gop),

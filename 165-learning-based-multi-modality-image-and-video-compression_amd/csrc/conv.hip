@@ -29,6 +29,7 @@
 #include <type_traits>
 #include "edge_frag.hpp"
 #include "mfma.hpp"
+#include "reduce_jobs.hpp"
 
 #include <algorithm>
 #include <vector>
@@ -2921,59 +2922,6 @@ static void launch_wgrad_glds(const WgradArgs& a, int nblocks, int in_abs, int i
     }
 }
 
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int S, int Ng, int ncols,
-                                                           int Cq, int Cq_pad, int k, float* __restrict__ dw,
-                                                           int accumulate, const float* __restrict__ bws,
-                                                           float* __restrict__ db, int Sb, int nbias) {
-    // one thread per 16-byte column chunk summing its S split partials in split order; the loads go out
-    // in batches of 8 independent requests (the partials stream from HBM once)
-    const int c4 = ncols >> 2;
-    const int64_t total = (int64_t)Ng * c4;
-    const int wblocks = (int)((total + 255) / 256);
-    if ((int)blockIdx.x >= wblocks) {
-        // trailing blocks: bias partials [Sb][nbias] -> db, one thread per channel
-        const int n = ((int)blockIdx.x - wblocks) * 256 + threadIdx.x;
-        if (n >= nbias) return;
-        float v = 0.f;
-        int sp = 0;
-        for (; sp + 8 <= Sb; sp += 8) {
-            float b[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) b[j] = bws[(int64_t)(sp + j) * nbias + n];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v += b[j];
-        }
-        for (; sp < Sb; ++sp) v += bws[(int64_t)sp * nbias + n];
-        db[n] = accumulate ? db[n] + v : v;
-        return;
-    }
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= total) return;
-    const int64_t slab4 = ((int64_t)Ng * ncols) >> 2;
-    const f32x4* src = reinterpret_cast<const f32x4*>(ws) + i;
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-    int sp = 0;
-    for (; sp + 8 <= S; sp += 8) {
-        f32x4 v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = src[(int64_t)(sp + j) * slab4];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc += v[j];
-    }
-    for (; sp < S; ++sp) acc += src[(int64_t)sp * slab4];
-    const int n = (int)(i / c4);
-    const int col = (int)(i - (int64_t)n * c4) * 4;
-    const int kk = k * k;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        const int cc = col + e;
-        const int t = cc / Cq_pad, q = cc - (cc / Cq_pad) * Cq_pad;
-        if (q >= Cq) continue;
-        float* d = dw + ((int64_t)n * Cq + q) * kk + t;
-        *d = accumulate ? *d + acc[e] : acc[e];
-    }
-}
-
 // Column sums of a pixel-major tensor (bias gradients, GDN dbeta).
 // stage 1: a block takes a pixel chunk and all channels: each thread owns one
 // 16-byte channel group and strides over rows (vector loads, fp32 sums), then
@@ -3901,9 +3849,10 @@ size_t cai_conv_wgrad_workspace_bytes(const cai_conv_geom* g, int dtype) {
                      W2.ws_slab + W2.ws_bias + W2.ws_col}) + 256;
 }
 
-int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_ld, int32_t in_abs, int32_t in_sq,
-                   const void* dy, int32_t dy_ld, float* dw, float* db, int32_t accumulate, void* workspace,
-                   size_t ws_bytes, void* stream) {
+static int run_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_ld, int32_t in_abs,
+                          int32_t in_sq, const void* dy, int32_t dy_ld, float* dw, float* db, int32_t accumulate,
+                          void* workspace, size_t ws_bytes, void* stream, cai_reduce_job* job) {
+    if (job) *job = cai_reduce_job{};
     int rc = check_geom(g);
     if (rc) return rc;
     CAI_CHECK_ARG(x && dy && dw, "conv_wgrad: null pointer");
@@ -3994,10 +3943,21 @@ int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_l
         else
             hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(NT), 0, st, a);
     }
+    // the fixed-order slab reduce into torch layout: a job (reduce_jobs.hip), returned to a deferring caller or
+    // run now
     const int64_t tot = (int64_t)W.Ng * (W.ncols / 4);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((tot + 255) / 256) + (bws ? (W.nbias + 255) / 256 : 0)),
-                       dim3(256), 0, st, slab, W.S, W.Ng, W.ncols, W.Cq, W.Cq_pad, g->kernel, dw, accumulate, bws, db,
-                       W.Sb, W.nbias);
+    cai_reduce_job J{};
+    J.kind = CAI_JOB_WGRAD;
+    J.nblocks = (int)((tot + 255) / 256) + (bws ? (W.nbias + 255) / 256 : 0);
+    J.p[0] = slab; J.p[1] = dw; J.p[2] = bws; J.p[3] = db;
+    J.i[0] = W.S; J.i[1] = W.Ng; J.i[2] = W.ncols; J.i[3] = W.Cq; J.i[4] = W.Cq_pad; J.i[5] = g->kernel;
+    J.i[6] = accumulate; J.i[7] = W.Sb; J.i[8] = W.nbias;
+    if (job) {
+        *job = J;
+    } else {
+        rc = launch_reduce_jobs(&J, 1, st);
+        if (rc) return rc;
+    }
     if (db && !bws) {
         float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + W.ws_slab + W.ws_bias);
         const int64_t npix = (int64_t)g->batch * g->out_h * g->out_w;
@@ -4008,6 +3968,21 @@ int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_l
     }
     CAI_LAUNCH_CHECK("conv_wgrad");
     return CAI_OK;
+}
+
+int cai_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_ld, int32_t in_abs, int32_t in_sq,
+                   const void* dy, int32_t dy_ld, float* dw, float* db, int32_t accumulate, void* workspace,
+                   size_t ws_bytes, void* stream) {
+    return run_conv_wgrad(g, dtype, x, x_ld, in_abs, in_sq, dy, dy_ld, dw, db, accumulate, workspace, ws_bytes, stream,
+                          nullptr);
+}
+
+int cai_conv_wgrad_deferred(const cai_conv_geom* g, int dtype, const void* x, int32_t x_ld, int32_t in_abs,
+                            int32_t in_sq, const void* dy, int32_t dy_ld, float* dw, float* db, int32_t accumulate,
+                            void* workspace, size_t ws_bytes, void* stream, cai_reduce_job* job) {
+    CAI_CHECK_ARG(job, "conv_wgrad_deferred: null job");
+    return run_conv_wgrad(g, dtype, x, x_ld, in_abs, in_sq, dy, dy_ld, dw, db, accumulate, workspace, ws_bytes, stream,
+                          job);
 }
 
 }  // extern "C"

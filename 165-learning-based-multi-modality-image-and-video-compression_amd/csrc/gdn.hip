@@ -21,6 +21,7 @@
 //   through the 1x1 wgrad kernel + fixed-order column sums), then the LowerBound rule.
 #include "common.hpp"
 #include "mfma.hpp"
+#include "reduce_jobs.hpp"
 
 #include <algorithm>
 
@@ -933,98 +934,6 @@ __global__ __launch_bounds__(WideGeo<C>::NT, 1) void gdn_bwd_wide_kernel(const b
         }
 }
 
-// sum the per-block partials in a fixed order, then the NonNegativeParametrizer /
-// LowerBound backward rule (as gdn_reparam_bwd_kernel).  256 threads = 16
-// element columns x 16 partial-block groups; groups combine through LDS in
-// a fixed tree (deterministic).
-__global__ __launch_bounds__(256) void gdn_fused_reduce_kernel(const float* __restrict__ part, int nblk, int C,
-                                                               const float* __restrict__ beta_raw,
-                                                               const float* __restrict__ gamma_raw, float bbound,
-                                                               float gbound, float* __restrict__ dbeta_raw,
-                                                               float* __restrict__ dgamma_raw, int accumulate) {
-    __shared__ float red[16][17];
-    const int64_t CC = (int64_t)C * C, stride = CC + C;
-    const int cg = threadIdx.x & 15, bg = threadIdx.x >> 4;
-    const int64_t i = (int64_t)blockIdx.x * 16 + cg;
-    float v = 0.f;
-    if (i < CC + C) {
-        // fixed block order; loads issued 8 at a time (independent requests in flight)
-        int b = bg;
-        for (; b + 16 * 7 < nblk; b += 16 * 8) {
-            float t[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) t[j] = part[(int64_t)(b + 16 * j) * stride + i];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v += t[j];
-        }
-        for (; b < nblk; b += 16) v += part[(int64_t)b * stride + i];
-    }
-    red[bg][cg] = v;
-    __syncthreads();
-    if (bg != 0 || i >= CC + C) return;
-#pragma unroll
-    for (int j = 1; j < 16; ++j) v += red[j][cg];
-    if (i < CC) {
-        const float gr = gamma_raw[i];
-        const float d = 2.f * fmaxf(gr, gbound) * v;
-        const float vg = (gr >= gbound || d < 0.f) ? d : 0.f;
-        dgamma_raw[i] = accumulate ? dgamma_raw[i] + vg : vg;
-    } else {
-        const int64_t c = i - CC;
-        const float br = beta_raw[c];
-        const float db = 2.f * fmaxf(br, bbound) * v;
-        const float vb = (br >= bbound || db < 0.f) ? db : 0.f;
-        dbeta_raw[c] = accumulate ? dbeta_raw[c] + vb : vb;
-    }
-}
-
-// The same reduce with 16-byte loads (C % 4 == 0: every partial row starts 16-byte aligned): a thread owns 4
-// consecutive elements, each summed in the same block order and LDS tree as gdn_fused_reduce_kernel
-// (bit-identical), a quarter of the load instructions and of the blocks.
-__global__ __launch_bounds__(256) void gdn_fused_reduce4_kernel(const float* __restrict__ part, int nblk, int C,
-                                                                const float* __restrict__ beta_raw,
-                                                                const float* __restrict__ gamma_raw, float bbound,
-                                                                float gbound, float* __restrict__ dbeta_raw,
-                                                                float* __restrict__ dgamma_raw, int accumulate) {
-    __shared__ f32x4 red[16][17];
-    const int64_t CC = (int64_t)C * C, stride = CC + C;
-    const int cg = threadIdx.x & 15, bg = threadIdx.x >> 4;
-    const int64_t i0 = ((int64_t)blockIdx.x * 16 + cg) * 4;
-    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (i0 < stride) {
-        int b = bg;
-        for (; b + 16 * 7 < nblk; b += 16 * 8) {
-            f32x4 t[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) t[j] = *reinterpret_cast<const f32x4*>(part + (int64_t)(b + 16 * j) * stride + i0);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v += t[j];
-        }
-        for (; b < nblk; b += 16) v += *reinterpret_cast<const f32x4*>(part + (int64_t)b * stride + i0);
-    }
-    red[bg][cg] = v;
-    __syncthreads();
-    if (bg != 0 || i0 >= stride) return;
-#pragma unroll
-    for (int j = 1; j < 16; ++j) v += red[j][cg];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        const int64_t i = i0 + e;
-        if (i < CC) {
-            const float gr = gamma_raw[i];
-            const float d = 2.f * fmaxf(gr, gbound) * v[e];
-            const float vg = (gr >= gbound || d < 0.f) ? d : 0.f;
-            dgamma_raw[i] = accumulate ? dgamma_raw[i] + vg : vg;
-        } else {
-            const int64_t c = i - CC;
-            const float br = beta_raw[c];
-            const float db = 2.f * fmaxf(br, bbound) * v[e];
-            const float vb = (br >= bbound || db < 0.f) ? db : 0.f;
-            dbeta_raw[c] = accumulate ? dbeta_raw[c] + vb : vb;
-        }
-    }
-}
-
 static int fused_blocks(int64_t npix) {
     const int64_t tiles = (npix + GBM - 1) / GBM;
     return (int)std::max<int64_t>(1, std::min<int64_t>(256, tiles));
@@ -1209,11 +1118,12 @@ size_t cai_gdn_backward_workspace_bytes(int64_t npix, int32_t C, int dtype) {
     return ub + cai_gdn_param_grad_workspace_bytes(npix, C, dtype);
 }
 
-int cai_gdn_backward(int dtype, const void* x, int32_t x_ld, const void* dy, int32_t dy_ld, int64_t npix, int32_t C,
-                     const void* gamma_op, const float* beta, int32_t inverse, void* dx, int32_t dx_ld,
-                     const float* beta_raw, const float* gamma_raw, float beta_min, float reparam_offset,
-                     float* dbeta_raw, float* dgamma_raw, int32_t accumulate, void* workspace, size_t ws_bytes,
-                     void* stream) {
+static int run_gdn_backward(int dtype, const void* x, int32_t x_ld, const void* dy, int32_t dy_ld, int64_t npix,
+                            int32_t C, const void* gamma_op, const float* beta, int32_t inverse, void* dx,
+                            int32_t dx_ld, const float* beta_raw, const float* gamma_raw, float beta_min,
+                            float reparam_offset, float* dbeta_raw, float* dgamma_raw, int32_t accumulate,
+                            void* workspace, size_t ws_bytes, void* stream, cai_reduce_job* job) {
+    if (job) *job = cai_reduce_job{};
     CAI_CHECK_ARG(gdn_c_ok(C, dtype), "gdn_backward: unsupported channel count %d", C);
     CAI_CHECK_ARG(x && dy && gamma_op && beta && dx && beta_raw && gamma_raw && dbeta_raw && dgamma_raw,
                   "gdn_backward: null pointer");
@@ -1262,17 +1172,43 @@ int cai_gdn_backward(int dtype, const void* x, int32_t x_ld, const void* dy, int
         inverse ? launch(gdn_bwd_fused_kernel<128, true>) : launch(gdn_bwd_fused_kernel<128, false>);
     else
         inverse ? launch(gdn_bwd_fused_kernel<64, true>) : launch(gdn_bwd_fused_kernel<64, false>);
-    const float ped = reparam_offset * reparam_offset;
-    const float bbound = sqrtf(beta_min + ped), gbound = sqrtf(ped);
-    const int64_t n = (int64_t)C * C + C;
-    if (C % 4 == 0 && ((uintptr_t)part & 15) == 0)
-        hipLaunchKernelGGL(gdn_fused_reduce4_kernel, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, part, nblk, C,
-                           beta_raw, gamma_raw, bbound, gbound, dbeta_raw, dgamma_raw, accumulate);
-    else
-        hipLaunchKernelGGL(gdn_fused_reduce_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0,
-                           st, part, nblk, C, beta_raw, gamma_raw, bbound, gbound, dbeta_raw, dgamma_raw, accumulate);
     CAI_LAUNCH_CHECK("gdn_backward");
-    return CAI_OK;
+    // the per-block partials -> dgamma_raw / dbeta_raw: a job (reduce_jobs.hip; C % 4 == 0 and the 256-byte
+    // aligned workspace give every partial row 16-byte alignment), returned to a deferring caller or run now
+    const float ped = reparam_offset * reparam_offset;
+    const int64_t n = (int64_t)C * C + C;
+    cai_reduce_job J{};
+    J.kind = CAI_JOB_GDN;
+    J.nblocks = (int)((n + 63) / 64);
+    J.p[0] = part; J.p[1] = beta_raw; J.p[2] = gamma_raw; J.p[3] = dbeta_raw; J.p[4] = dgamma_raw;
+    J.i[0] = nblk; J.i[1] = C; J.i[2] = accumulate;
+    J.f[0] = sqrtf(beta_min + ped); J.f[1] = sqrtf(ped);
+    if (job) {
+        *job = J;
+        return CAI_OK;
+    }
+    return launch_reduce_jobs(&J, 1, st);
+}
+
+int cai_gdn_backward(int dtype, const void* x, int32_t x_ld, const void* dy, int32_t dy_ld, int64_t npix, int32_t C,
+                     const void* gamma_op, const float* beta, int32_t inverse, void* dx, int32_t dx_ld,
+                     const float* beta_raw, const float* gamma_raw, float beta_min, float reparam_offset,
+                     float* dbeta_raw, float* dgamma_raw, int32_t accumulate, void* workspace, size_t ws_bytes,
+                     void* stream) {
+    return run_gdn_backward(dtype, x, x_ld, dy, dy_ld, npix, C, gamma_op, beta, inverse, dx, dx_ld, beta_raw,
+                            gamma_raw, beta_min, reparam_offset, dbeta_raw, dgamma_raw, accumulate, workspace,
+                            ws_bytes, stream, nullptr);
+}
+
+int cai_gdn_backward_deferred(int dtype, const void* x, int32_t x_ld, const void* dy, int32_t dy_ld, int64_t npix,
+                              int32_t C, const void* gamma_op, const float* beta, int32_t inverse, void* dx,
+                              int32_t dx_ld, const float* beta_raw, const float* gamma_raw, float beta_min,
+                              float reparam_offset, float* dbeta_raw, float* dgamma_raw, int32_t accumulate,
+                              void* workspace, size_t ws_bytes, void* stream, cai_reduce_job* job) {
+    CAI_CHECK_ARG(job, "gdn_backward_deferred: null job");
+    return run_gdn_backward(dtype, x, x_ld, dy, dy_ld, npix, C, gamma_op, beta, inverse, dx, dx_ld, beta_raw,
+                            gamma_raw, beta_min, reparam_offset, dbeta_raw, dgamma_raw, accumulate, workspace,
+                            ws_bytes, stream, job);
 }
 
 }  // extern "C"

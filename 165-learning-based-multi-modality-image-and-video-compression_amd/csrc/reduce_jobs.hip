@@ -1,0 +1,159 @@
+// Parameter-gradient reduces as jobs (cai_reduce_jobs): the fixed-order sums that turn a weight-gradient
+// kernel's per-split fp32 slabs (conv) or per-block partials (fused GDN backward) into the torch-layout
+// gradient.  One kernel runs any list of jobs -- each job owns a contiguous range of 256-thread blocks -- so
+// the reduces of a whole backward pass can go out as ONE launch before the optimizer reads the gradients,
+// instead of one launch after every layer (the per-layer launches were 14 of the 100 kernels of a C2 step).
+// The immediate paths (cai_conv_wgrad, cai_gdn_backward) run their single job through the same kernel, so
+// deferred and immediate reduces are bit-identical.
+//
+// Job bodies (the order and arithmetic of every sum is fixed: deterministic):
+//   WGRAD  one thread per 16-byte column chunk of the [Ng][ncols] slab sums its S split partials in split
+//          order (loads in batches of 8) and scatters into dw[n][q][k*k] (+ trailing blocks: the bias partials
+//          [Sb][nbias] -> db, one thread per channel)
+//   GDN    16 element columns x 16 partial-block groups per block (4 consecutive elements per thread), the
+//          groups combined through LDS in a fixed tree, then the NonNegativeParametrizer / LowerBound backward
+//          rule (ops/parametrizers.py:47-64, ops/bound_ops.py:36-80) into dgamma_raw / dbeta_raw
+#include "common.hpp"
+#include "reduce_jobs.hpp"
+
+namespace cai {
+
+__device__ __forceinline__ void wgrad_reduce_body(const cai_reduce_job& J, int bid) {
+    const float* __restrict__ ws = static_cast<const float*>(J.p[0]);
+    float* __restrict__ dw = static_cast<float*>(const_cast<void*>(J.p[1]));
+    const float* __restrict__ bws = static_cast<const float*>(J.p[2]);
+    float* __restrict__ db = static_cast<float*>(const_cast<void*>(J.p[3]));
+    const int S = J.i[0], Ng = J.i[1], ncols = J.i[2], Cq = J.i[3], Cq_pad = J.i[4], k = J.i[5];
+    const int accumulate = J.i[6], Sb = J.i[7], nbias = J.i[8];
+    const int c4 = ncols >> 2;
+    const int64_t total = (int64_t)Ng * c4;
+    const int wblocks = (int)((total + 255) / 256);
+    if (bid >= wblocks) {
+        const int n = (bid - wblocks) * 256 + threadIdx.x;
+        if (n >= nbias) return;
+        float v = 0.f;
+        int sp = 0;
+        for (; sp + 8 <= Sb; sp += 8) {
+            float b[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) b[j] = bws[(int64_t)(sp + j) * nbias + n];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v += b[j];
+        }
+        for (; sp < Sb; ++sp) v += bws[(int64_t)sp * nbias + n];
+        db[n] = accumulate ? db[n] + v : v;
+        return;
+    }
+    const int64_t i = (int64_t)bid * 256 + threadIdx.x;
+    if (i >= total) return;
+    const int64_t slab4 = ((int64_t)Ng * ncols) >> 2;
+    const f32x4* src = reinterpret_cast<const f32x4*>(ws) + i;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    int sp = 0;
+    for (; sp + 8 <= S; sp += 8) {
+        f32x4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = src[(int64_t)(sp + j) * slab4];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc += v[j];
+    }
+    for (; sp < S; ++sp) acc += src[(int64_t)sp * slab4];
+    const int n = (int)(i / c4);
+    const int col = (int)(i - (int64_t)n * c4) * 4;
+    const int kk = k * k;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int cc = col + e;
+        const int t = cc / Cq_pad, q = cc - (cc / Cq_pad) * Cq_pad;
+        if (q >= Cq) continue;
+        float* d = dw + ((int64_t)n * Cq + q) * kk + t;
+        *d = accumulate ? *d + acc[e] : acc[e];
+    }
+}
+
+__device__ __forceinline__ void gdn_reduce_body(const cai_reduce_job& J, int bid, f32x4 (*red)[17]) {
+    const float* __restrict__ part = static_cast<const float*>(J.p[0]);
+    const float* __restrict__ beta_raw = static_cast<const float*>(J.p[1]);
+    const float* __restrict__ gamma_raw = static_cast<const float*>(J.p[2]);
+    float* __restrict__ dbeta_raw = static_cast<float*>(const_cast<void*>(J.p[3]));
+    float* __restrict__ dgamma_raw = static_cast<float*>(const_cast<void*>(J.p[4]));
+    const int nblk = J.i[0], C = J.i[1], accumulate = J.i[2];
+    const float bbound = J.f[0], gbound = J.f[1];
+    const int64_t CC = (int64_t)C * C, stride = CC + C;
+    const int cg = threadIdx.x & 15, bg = threadIdx.x >> 4;
+    const int64_t i0 = ((int64_t)bid * 16 + cg) * 4;
+    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (i0 < stride) {
+        int b = bg;
+        for (; b + 16 * 7 < nblk; b += 16 * 8) {
+            f32x4 t[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) t[j] = *reinterpret_cast<const f32x4*>(part + (int64_t)(b + 16 * j) * stride + i0);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v += t[j];
+        }
+        for (; b < nblk; b += 16) v += *reinterpret_cast<const f32x4*>(part + (int64_t)b * stride + i0);
+    }
+    red[bg][cg] = v;
+    __syncthreads();
+    if (bg != 0 || i0 >= stride) return;
+#pragma unroll
+    for (int j = 1; j < 16; ++j) v += red[j][cg];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int64_t i = i0 + e;
+        if (i < CC) {
+            const float gr = gamma_raw[i];
+            const float d = 2.f * fmaxf(gr, gbound) * v[e];
+            const float vg = (gr >= gbound || d < 0.f) ? d : 0.f;
+            dgamma_raw[i] = accumulate ? dgamma_raw[i] + vg : vg;
+        } else if (i < stride) {
+            const int64_t c = i - CC;
+            const float br = beta_raw[c];
+            const float db = 2.f * fmaxf(br, bbound) * v[e];
+            const float vb = (br >= bbound || db < 0.f) ? db : 0.f;
+            dbeta_raw[c] = accumulate ? dbeta_raw[c] + vb : vb;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void reduce_jobs_kernel(const ReduceBatch B) {
+    __shared__ f32x4 red[16][17];
+    // the job owning this block (block-uniform linear scan over <= CAI_REDUCE_BATCH entries)
+    const int b = blockIdx.x;
+    int j = 0;
+    while (j + 1 < B.n && b >= B.start[j + 1]) ++j;
+    const cai_reduce_job& J = B.jobs[j];
+    const int bid = b - B.start[j];
+    if (J.kind == CAI_JOB_WGRAD)
+        wgrad_reduce_body(J, bid);
+    else if (J.kind == CAI_JOB_GDN)
+        gdn_reduce_body(J, bid, red);
+}
+
+int launch_reduce_jobs(const cai_reduce_job* jobs, int n, hipStream_t st) {
+    for (int j0 = 0; j0 < n;) {
+        ReduceBatch B{};
+        int blocks = 0;
+        for (; j0 < n && B.n < CAI_REDUCE_BATCH; ++j0) {
+            const cai_reduce_job& J = jobs[j0];
+            if (J.kind == CAI_JOB_NONE || J.nblocks <= 0) continue;
+            CAI_CHECK_ARG(J.kind == CAI_JOB_WGRAD || J.kind == CAI_JOB_GDN, "reduce_jobs: unknown job kind %d", J.kind);
+            B.jobs[B.n] = J;
+            B.start[B.n] = blocks;
+            blocks += J.nblocks;
+            ++B.n;
+        }
+        if (B.n == 0) continue;
+        hipLaunchKernelGGL(reduce_jobs_kernel, dim3((unsigned)blocks), dim3(256), 0, st, B);
+        CAI_LAUNCH_CHECK("reduce_jobs");
+    }
+    return CAI_OK;
+}
+
+}  // namespace cai
+
+extern "C" int cai_reduce_jobs(const cai_reduce_job* jobs, int32_t n, void* stream) {
+    CAI_CHECK_ARG(n >= 0 && (n == 0 || jobs), "reduce_jobs: bad arguments");
+    return cai::launch_reduce_jobs(jobs, n, cai::as_stream(stream));
+}

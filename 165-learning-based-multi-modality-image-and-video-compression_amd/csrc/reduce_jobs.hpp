@@ -1,0 +1,19 @@
+// Parameter-gradient reduce jobs (reduce_jobs.hip): the batch passed to reduce_jobs_kernel by value.
+#pragma once
+
+#include "common.hpp"
+
+namespace cai {
+
+constexpr int CAI_REDUCE_BATCH = 16;   // jobs per launch (the batch travels as kernel arguments)
+
+struct ReduceBatch {
+    int n;
+    int start[CAI_REDUCE_BATCH];       // first block of each job
+    cai_reduce_job jobs[CAI_REDUCE_BATCH];
+};
+
+// run `n` jobs (CAI_JOB_NONE entries skipped) in ceil(n / CAI_REDUCE_BATCH) launches
+int launch_reduce_jobs(const cai_reduce_job* jobs, int n, hipStream_t st);
+
+}  // namespace cai

@@ -194,10 +194,10 @@ def dominant_roofline(led, workload: str, reps: int = 20, pick=None):
     else:
         achieved, peak, unit = e.nbytes / (ms * 1e6), _ledger.HBM_PEAK_GBS, "GB/s"
     # the replayed op's kernels as rocprofv3 lists them: weight gradients through the pixel-split kernels end
-    # with their fixed-order slab reduce (compare the rocprof averages summed over both)
+    # with their fixed-order slab reduce (reduce_jobs_kernel: compare the rocprof averages summed over both)
     kernels = [e.kernel]
     if e.kind == "conv_wgrad" and e.kernel.startswith(("wgrad_halo", "wgrad_glds")):
-        kernels.append("wgrad_reduce_kernel")
+        kernels.append("reduce_jobs_kernel")
     return {"kernel": e.kernel, "op_kernels": kernels, "launch": f"{e.kind}: {e.shape}", "bound": bound,
             "achieved": round(achieved, 2),
             "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),

@@ -160,6 +160,29 @@ int cai_conv_wgrad(const cai_conv_geom* g, int dtype,
                    float* dw, float* db, int32_t accumulate,
                    void* workspace, size_t ws_bytes, void* stream);
 
+/* Deferred parameter-gradient reduces.  A weight-gradient call can leave its final fixed-order reduce
+ * (split slabs -> torch layout) as a job instead of launching it; cai_reduce_jobs runs any number of jobs in
+ * ceil(n / 16) launches, each job on its own range of blocks.  The caller keeps the job's workspace alive
+ * and unmodified, and reads the gradient only after cai_reduce_jobs on the same stream (compressai._ops
+ * queues the jobs of one backward pass and runs them in an autograd final callback).  Results are
+ * bit-identical to the immediate calls, which run their one job through the same kernel.  Job fields are
+ * the library's own (filled by the *_deferred calls); kind CAI_JOB_NONE: nothing left to reduce. */
+#define CAI_JOB_NONE 0
+#define CAI_JOB_WGRAD 1
+#define CAI_JOB_GDN 2
+typedef struct cai_reduce_job {
+    int32_t kind, nblocks;
+    int32_t i[10];
+    float f[2];
+    const void* p[6];
+} cai_reduce_job;
+int cai_conv_wgrad_deferred(const cai_conv_geom* g, int dtype,
+                            const void* x, int32_t x_ld, int32_t in_abs, int32_t in_sq,
+                            const void* dy, int32_t dy_ld,
+                            float* dw, float* db, int32_t accumulate,
+                            void* workspace, size_t ws_bytes, void* stream, cai_reduce_job* job);
+int cai_reduce_jobs(const cai_reduce_job* jobs, int32_t n, void* stream);
+
 /* ConvTranspose2d with out_c <= 16 (the synthesis transform's last layer,
  * models/utils.py:138-146, e.g. deconv(N, 3)): forward as one dense GEMM per
  * input pixel (N = k*k*out_c columns) + col2im, backward as im2col + two 1x1
@@ -328,6 +351,14 @@ int cai_gdn_backward(int dtype, const void* x, int32_t x_ld, const void* dy, int
                      const float* beta_raw, const float* gamma_raw, float beta_min, float reparam_offset,
                      float* dbeta_raw, float* dgamma_raw, int32_t accumulate, void* workspace, size_t ws_bytes,
                      void* stream);
+
+/* cai_gdn_backward with its parameter-gradient reduce left as a job (see cai_reduce_jobs); the fused
+ * pass only (bf16, C in {64, 128, 160, 192}), other cases run immediately and return CAI_JOB_NONE. */
+int cai_gdn_backward_deferred(int dtype, const void* x, int32_t x_ld, const void* dy, int32_t dy_ld, int64_t npix,
+                              int32_t C, const void* gamma_op, const float* beta, int32_t inverse, void* dx,
+                              int32_t dx_ld, const float* beta_raw, const float* gamma_raw, float beta_min,
+                              float reparam_offset, float* dbeta_raw, float* dgamma_raw, int32_t accumulate,
+                              void* workspace, size_t ws_bytes, void* stream, cai_reduce_job* job);
 
 /* =======================================================================
  * Entropy models.  Element (p, c) of every operand at ptr[p*ld + c].

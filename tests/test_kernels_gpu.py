@@ -682,3 +682,78 @@ def test_gdn_reparam_in_pack_many_matches_standalone(cuda, C, dtype):
     assert torch.equal(b_new, b_ref)
     assert torch.equal(g_new.view(torch.int16 if dtype == torch.bfloat16 else torch.int32),
                        g_ref.view(torch.int16 if dtype == torch.bfloat16 else torch.int32))
+
+
+@pytest.mark.parametrize("batch", [1, 3])
+def test_deferred_reduce_jobs_bit_identical(cuda, batch):
+    """Deferred parameter-gradient reduces (cai_*_deferred + one cai_reduce_jobs launch for all jobs) give the
+    same bits as the immediate calls, for a halo / glds / small weight gradient and the fused GDN backward,
+    accumulating into existing values."""
+    import ctypes
+
+    from compressai._native import ReduceJob, lib
+    from compressai._ops import _p, _stream
+    from compressai._native import ConvGeom
+
+    torch.manual_seed(batch)
+    dev = cuda
+    st = _stream()
+    jobs, keep, outs_def, outs_imm = [], [], [], []
+    # conv weight gradients (bf16, pixel-major operands): stride-2 k5 (halo), k3 s1 (glds), latent-size (small)
+    for (cin, cout, k, s, H) in [(128, 128, 5, 2, 64), (192, 128, 3, 1, 16), (128, 128, 5, 2, 8)]:
+        Ho = (H + 2 * (k // 2) - k) // s + 1
+        g = ConvGeom(batch, cin, H, H, cout, Ho, Ho, k, s, k // 2, 0, 0)
+        x = torch.randn(batch * H * H, cin, device=dev).to(torch.bfloat16)
+        dy = torch.randn(batch * Ho * Ho, cout, device=dev).to(torch.bfloat16)
+        nb = lib.cai_conv_wgrad_workspace_bytes(ctypes.byref(g), 1)
+        base_w = torch.randn(cout, cin, k, k, device=dev)
+        base_b = torch.randn(cout, device=dev)
+        for deferred in (True, False):
+            dw, db = base_w.clone(), base_b.clone()
+            ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+            if deferred:
+                job = ReduceJob()
+                lib.cai_conv_wgrad_deferred(ctypes.byref(g), 1, _p(x), cin, 0, 0, _p(dy), cout, _p(dw), _p(db), 1,
+                                            _p(ws), nb, st, ctypes.byref(job))
+                jobs.append(job)
+                keep.append(ws)
+                outs_def.append((dw, db))
+            else:
+                lib.cai_conv_wgrad(ctypes.byref(g), 1, _p(x), cin, 0, 0, _p(dy), cout, _p(dw), _p(db), 1, _p(ws), nb, st)
+                outs_imm.append((dw, db))
+    # fused GDN backward, C = 128 and 192
+    for C in (128, 192):
+        npix = batch * 32 * 32
+        x = (torch.randn(npix, C, device=dev) * 0.5).to(torch.bfloat16)
+        dy = torch.randn(npix, C, device=dev).to(torch.bfloat16)
+        br = torch.rand(C, device=dev) + 0.5
+        gr = torch.rand(C, C, device=dev) * 0.1
+        beta = torch.empty(C, device=dev)
+        gop = torch.empty(2 * C * C, dtype=torch.bfloat16, device=dev)
+        lib.cai_gdn_reparam(_p(br), _p(gr), C, 1e-6, 2 ** -18, 1, _p(beta), _p(gop), st)
+        nb = lib.cai_gdn_backward_workspace_bytes(npix, C, 1)
+        base_b, base_g = torch.randn(C, device=dev), torch.randn(C, C, device=dev)
+        for deferred in (True, False):
+            dx = torch.empty(npix, C, dtype=torch.bfloat16, device=dev)
+            dbr, dgr = base_b.clone(), base_g.clone()
+            ws = torch.empty(nb + 256, dtype=torch.uint8, device=dev)
+            wsp = ws[(-ws.data_ptr()) % 256:]
+            args = (1, _p(x), C, _p(dy), C, npix, C, _p(gop), _p(beta), 0, _p(dx), C, _p(br), _p(gr), 1e-6,
+                    2 ** -18, _p(dbr), _p(dgr), 1, _p(wsp), nb, st)
+            if deferred:
+                job = ReduceJob()
+                lib.cai_gdn_backward_deferred(*args, ctypes.byref(job))
+                jobs.append(job)
+                keep.extend((ws, br, gr))      # the job reads the raw parameters too (LowerBound rule)
+                outs_def.append((dbr, dgr))
+            else:
+                lib.cai_gdn_backward(*args)
+                outs_imm.append((dbr, dgr))
+    arr = (ReduceJob * len(jobs))(*jobs)
+    lib.cai_reduce_jobs(arr, len(jobs), st)
+    torch.cuda.synchronize()
+    assert len(outs_def) == len(outs_imm) == 5
+    bad = [(i, float((a0 - b0).abs().max()), float((a1 - b1).abs().max()))
+           for i, ((a0, a1), (b0, b1)) in enumerate(zip(outs_def, outs_imm))
+           if not (torch.equal(a0, b0) and torch.equal(a1, b1))]
+    assert not bad, bad
