@@ -3945,10 +3945,9 @@ static int run_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int3
     }
     // the fixed-order slab reduce into torch layout: a job (reduce_jobs.hip), returned to a deferring caller or
     // run now
-    const int64_t tot = (int64_t)W.Ng * (W.ncols / 4);
     cai_reduce_job J{};
     J.kind = CAI_JOB_WGRAD;
-    J.nblocks = (int)((tot + 255) / 256) + (bws ? (W.nbias + 255) / 256 : 0);
+    J.nblocks = wgrad_job_blocks(W.Ng, W.ncols, bws ? (W.nbias + 255) / 256 : 0);
     J.p[0] = slab; J.p[1] = dw; J.p[2] = bws; J.p[3] = db;
     J.i[0] = W.S; J.i[1] = W.Ng; J.i[2] = W.ncols; J.i[3] = W.Cq; J.i[4] = W.Cq_pad; J.i[5] = g->kernel;
     J.i[6] = accumulate; J.i[7] = W.Sb; J.i[8] = W.nbias;

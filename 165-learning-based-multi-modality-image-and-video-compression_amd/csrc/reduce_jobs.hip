@@ -7,9 +7,10 @@
 // deferred and immediate reduces are bit-identical.
 //
 // Job bodies (the order and arithmetic of every sum is fixed: deterministic):
-//   WGRAD  one thread per 16-byte column chunk of the [Ng][ncols] slab sums its S split partials in split
-//          order (loads in batches of 8) and scatters into dw[n][q][k*k] (+ trailing blocks: the bias partials
-//          [Sb][nbias] -> db, one thread per channel)
+//   WGRAD  one block per output row n of the [Ng][ncols] slab: each 16-byte column chunk summed over the S
+//          splits in split order (loads in batches of 8), the row transposed through LDS from [tap][q] to the
+//          torch layout dw[n][q][tap] and stored contiguously (rows wider than 8192 columns: one thread per
+//          chunk, scattered stores); trailing blocks: the bias partials [Sb][nbias] -> db, one thread per channel
 //   GDN    16 element columns x 16 partial-block groups per block (4 consecutive elements per thread), the
 //          groups combined through LDS in a fixed tree, then the NonNegativeParametrizer / LowerBound backward
 //          rule (ops/parametrizers.py:47-64, ops/bound_ops.py:36-80) into dgamma_raw / dbeta_raw
@@ -18,32 +19,71 @@
 
 namespace cai {
 
-__device__ __forceinline__ void wgrad_reduce_body(const cai_reduce_job& J, int bid) {
-    const float* __restrict__ ws = static_cast<const float*>(J.p[0]);
-    float* __restrict__ dw = static_cast<float*>(const_cast<void*>(J.p[1]));
+// rows of the weight-gradient slab small enough to transpose through LDS (floats)
+constexpr int WG_ROW_LDS = 8192;
+
+__device__ __forceinline__ void wgrad_bias_body(const cai_reduce_job& J, int bid) {
     const float* __restrict__ bws = static_cast<const float*>(J.p[2]);
     float* __restrict__ db = static_cast<float*>(const_cast<void*>(J.p[3]));
-    const int S = J.i[0], Ng = J.i[1], ncols = J.i[2], Cq = J.i[3], Cq_pad = J.i[4], k = J.i[5];
     const int accumulate = J.i[6], Sb = J.i[7], nbias = J.i[8];
+    const int n = bid * 256 + threadIdx.x;
+    if (n >= nbias) return;
+    float v = 0.f;
+    int sp = 0;
+    for (; sp + 8 <= Sb; sp += 8) {
+        float b[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[j] = bws[(int64_t)(sp + j) * nbias + n];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v += b[j];
+    }
+    for (; sp < Sb; ++sp) v += bws[(int64_t)sp * nbias + n];
+    db[n] = accumulate ? db[n] + v : v;
+}
+
+// one output row n per block: the row's ncols = k*k*Cq_pad columns (slab layout [tap][q]) summed over the S
+// splits in split order (16-byte loads, 8 splits in flight), transposed through LDS and written to dw[n][q][tap]
+// (the torch layout is contiguous over (q, tap) for a fixed n): coalesced read-modify-write stores instead of
+// one 4-byte access per k*k-strided element
+__device__ __forceinline__ void wgrad_row_body(const cai_reduce_job& J, int n, float* row) {
+    const float* __restrict__ ws = static_cast<const float*>(J.p[0]);
+    float* __restrict__ dw = static_cast<float*>(const_cast<void*>(J.p[1]));
+    const int S = J.i[0], Ng = J.i[1], ncols = J.i[2], Cq = J.i[3], Cq_pad = J.i[4], k = J.i[5];
+    const int accumulate = J.i[6];
+    const int c4 = ncols >> 2;
+    const int64_t slab4 = ((int64_t)Ng * ncols) >> 2;
+    const f32x4* src = reinterpret_cast<const f32x4*>(ws) + (int64_t)n * c4;
+    for (int c = threadIdx.x; c < c4; c += 256) {
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        int sp = 0;
+        for (; sp + 8 <= S; sp += 8) {
+            f32x4 v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = src[(int64_t)(sp + j) * slab4 + c];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc += v[j];
+        }
+        for (; sp < S; ++sp) acc += src[(int64_t)sp * slab4 + c];
+        *reinterpret_cast<f32x4*>(row + 4 * c) = acc;
+    }
+    __syncthreads();
+    const int kk = k * k, nout = Cq * kk;
+    float* d = dw + (int64_t)n * nout;
+    for (int i = threadIdx.x; i < nout; i += 256) {
+        const int q = i / kk, t = i - (i / kk) * kk;
+        const float v = row[t * Cq_pad + q];
+        d[i] = accumulate ? d[i] + v : v;
+    }
+}
+
+// the same sums for rows too wide for LDS: one thread per 16-byte column chunk, scattered 4-byte stores
+__device__ __forceinline__ void wgrad_scatter_body(const cai_reduce_job& J, int bid) {
+    const float* __restrict__ ws = static_cast<const float*>(J.p[0]);
+    float* __restrict__ dw = static_cast<float*>(const_cast<void*>(J.p[1]));
+    const int S = J.i[0], Ng = J.i[1], ncols = J.i[2], Cq = J.i[3], Cq_pad = J.i[4], k = J.i[5];
+    const int accumulate = J.i[6];
     const int c4 = ncols >> 2;
     const int64_t total = (int64_t)Ng * c4;
-    const int wblocks = (int)((total + 255) / 256);
-    if (bid >= wblocks) {
-        const int n = (bid - wblocks) * 256 + threadIdx.x;
-        if (n >= nbias) return;
-        float v = 0.f;
-        int sp = 0;
-        for (; sp + 8 <= Sb; sp += 8) {
-            float b[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) b[j] = bws[(int64_t)(sp + j) * nbias + n];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v += b[j];
-        }
-        for (; sp < Sb; ++sp) v += bws[(int64_t)sp * nbias + n];
-        db[n] = accumulate ? db[n] + v : v;
-        return;
-    }
     const int64_t i = (int64_t)bid * 256 + threadIdx.x;
     if (i >= total) return;
     const int64_t slab4 = ((int64_t)Ng * ncols) >> 2;
@@ -69,6 +109,27 @@ __device__ __forceinline__ void wgrad_reduce_body(const cai_reduce_job& J, int b
         float* d = dw + ((int64_t)n * Cq + q) * kk + t;
         *d = accumulate ? *d + acc[e] : acc[e];
     }
+}
+
+// blocks [0, wblocks): the weight rows (LDS-transposed: one row per block; else scattered chunks); then the
+// bias blocks
+__device__ __forceinline__ void wgrad_reduce_body(const cai_reduce_job& J, int bid, float* row) {
+    const int Ng = J.i[1], ncols = J.i[2];
+    const bool lds = ncols <= WG_ROW_LDS;
+    const int wblocks = lds ? Ng : (int)(((int64_t)Ng * (ncols >> 2) + 255) / 256);
+    if (bid >= wblocks) {
+        wgrad_bias_body(J, bid - wblocks);
+        return;
+    }
+    if (lds)
+        wgrad_row_body(J, bid, row);
+    else
+        wgrad_scatter_body(J, bid);
+}
+
+int wgrad_job_blocks(int Ng, int ncols, int nbias_blocks) {
+    const int wblocks = ncols <= WG_ROW_LDS ? Ng : (int)(((int64_t)Ng * (ncols >> 2) + 255) / 256);
+    return wblocks + nbias_blocks;
 }
 
 __device__ __forceinline__ void gdn_reduce_body(const cai_reduce_job& J, int bid, f32x4 (*red)[17]) {
@@ -119,6 +180,7 @@ __device__ __forceinline__ void gdn_reduce_body(const cai_reduce_job& J, int bid
 
 __global__ __launch_bounds__(256) void reduce_jobs_kernel(const ReduceBatch B) {
     __shared__ f32x4 red[16][17];
+    __shared__ __attribute__((aligned(16))) float row[WG_ROW_LDS];
     // the job owning this block (block-uniform linear scan over <= CAI_REDUCE_BATCH entries)
     const int b = blockIdx.x;
     int j = 0;
@@ -126,7 +188,7 @@ __global__ __launch_bounds__(256) void reduce_jobs_kernel(const ReduceBatch B) {
     const cai_reduce_job& J = B.jobs[j];
     const int bid = b - B.start[j];
     if (J.kind == CAI_JOB_WGRAD)
-        wgrad_reduce_body(J, bid);
+        wgrad_reduce_body(J, bid, row);
     else if (J.kind == CAI_JOB_GDN)
         gdn_reduce_body(J, bid, red);
 }

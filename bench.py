@@ -220,6 +220,28 @@ def step_roofline(led, ms_per_step: float):
                     "(SURVEY.md 8(d)); algorithmic FLOPs / bytes per launch from compressai/_ledger.py"}
 
 
+def dominant_class(led):
+    """The kernel class with the largest summed GPU time in the profiled step (all launches of one kernel
+    name), with its summed algorithmic work and roofline fraction: for launch-bound configs (cheng2020, 467
+    small convs) the time goes to a class of short launches, not to the single longest one."""
+    by = {}
+    for e in led.entries:
+        k = by.setdefault(e.kernel, {"kernel": e.kernel, "launches": 0, "ms": 0.0, "roofline_ms": 0.0, "flops": 0.0,
+                                     "bytes": 0.0})
+        k["launches"] += 1
+        k["ms"] += e.ms
+        k["roofline_ms"] += e.roofline_ms()
+        k["flops"] += e.flops
+        k["bytes"] += e.nbytes
+    top = max(by.values(), key=lambda k: k["ms"])
+    total = sum(k["ms"] for k in by.values())
+    return {"kernel": top["kernel"], "launches": top["launches"], "ms_per_step": round(top["ms"], 4),
+            "share_of_instrumented": round(top["ms"] / total, 4), "frac": round(top["roofline_ms"] / top["ms"], 4),
+            "achieved_tflops": round(top["flops"] / (top["ms"] * 1e9), 2),
+            "achieved_gbs": round(top["bytes"] / (top["ms"] * 1e6), 1),
+            "note": "frac = sum of max(FLOP/peak, bytes/BW) over the class's launches / their summed measured time"}
+
+
 def ops_table(led):
     rows = [e.as_dict() for e in led.entries]
     by_kernel = {}
@@ -438,11 +460,12 @@ def main():
         raise RuntimeError(f"non-finite loss {loss}")
     ms_per_step = dt / args.steps * 1e3
 
-    roof = step_roof = None
+    roof = step_roof = dom_class = None
     if rank == 0 and not args.no_profile:
         led = profile_step(local_step)
         roof = dominant_roofline(led, workload)
         step_roof = step_roofline(led, ms_per_step)
+        dom_class = dominant_class(led)
         if args.ops_json:
             with open(args.ops_json, "w") as f:
                 json.dump(ops_table(led), f, indent=1)
@@ -466,7 +489,7 @@ def main():
                                          "backward (2-phase backward)" if sync else
                                          "1 all-reduce after backward") if world > 1 else None},
             "final_loss": round(loss, 5),
-            "roofline": roof, "step_roofline": step_roof, "cpu_baseline": cpu,
+            "roofline": roof, "dominant_class": dom_class, "step_roofline": step_roof, "cpu_baseline": cpu,
         }
         if cpu:
             line["gpu_over_cpu"] = round(value / cpu["value"], 1)

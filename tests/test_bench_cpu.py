@@ -70,3 +70,25 @@ def test_bench_refuses_rank_mismatch():
                        env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode != 0
     assert "--gpus 2 but the job has 1 ranks" in (r.stdout + r.stderr)
+
+
+def test_dominant_class_sums_launches_of_one_kernel():
+    """bench.py's dominant_class: the kernel class with the largest SUMMED time wins over the single longest
+    launch (cheng2020: hundreds of short convs vs one Adam launch), with its class-level roofline fraction."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    class E:
+        def __init__(self, kernel, ms, flops, nbytes, roof):
+            self.kernel, self.ms, self.flops, self.nbytes, self._roof = kernel, ms, flops, nbytes, roof
+
+        def roofline_ms(self):
+            return self._roof
+
+    class L:
+        entries = [E("adam_fused_kernel", 0.05, 0, 1e8, 0.02)] + [E("conv_small_kernel", 0.02, 1e9, 1e6, 0.001)] * 10
+
+    d = bench.dominant_class(L())
+    assert d["kernel"] == "conv_small_kernel" and d["launches"] == 10
+    assert abs(d["ms_per_step"] - 0.2) < 1e-9 and abs(d["frac"] - 0.05) < 1e-9
+    assert abs(d["share_of_instrumented"] - 0.2 / 0.25) < 1e-4
