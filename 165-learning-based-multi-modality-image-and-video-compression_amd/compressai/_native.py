@@ -54,7 +54,7 @@ class EbGrads(Structure):
                 ("accumulate", c_int32)]
 
 
-JOB_NONE, JOB_WGRAD, JOB_GDN = 0, 1, 2           # cai_reduce_job kinds (include/cai.h)
+JOB_NONE, JOB_WGRAD, JOB_GDN, JOB_EDGE = 0, 1, 2, 3           # cai_reduce_job kinds (include/cai.h)
 
 
 class ReduceJob(Structure):
@@ -98,6 +98,7 @@ SIGNATURES = {
     "cai_edge_deconv_fwd": (_I, [_G, _P, c_int32, _P, _P, _P, _P]),
     "cai_edge_deconv_dgrad": (_I, [_G, _P, _P, _P, c_int32, _P]),
     "cai_edge_wgrad": (_I, [_G, _P, _P, c_int32, _P, _P, c_int32, _P, _S, _P]),
+    "cai_edge_wgrad_deferred": (_I, [_G, _P, _P, c_int32, _P, _P, c_int32, _P, _S, _P, POINTER(ReduceJob)]),
     "cai_add_act": (_I, [_I, _P, c_int32, _P, c_int32, _P, c_int32, _I64, c_int32, c_int32, _F, _P]),
     "cai_act": (_I, [_I, _P, c_int32, _P, c_int32, _I64, c_int32, c_int32, _F, _P]),
     "cai_gdn1_out": (_I, [_I, _P, c_int32, _P, c_int32, _P, c_int32, _I64, c_int32, c_int32, _P]),
@@ -139,9 +140,10 @@ SIGNATURES = {
                         _P, c_int32, _P, _I, c_int32, _P, c_int32, _P, c_int32, _P, c_int32, _P]),
     "cai_eb_fwd": (_I, [_I, _I64, c_int32, POINTER(EbParams), _P, _I, c_int32, _P, c_int32, _F, _P, _I, c_int32,
                         _P, c_int32, _P]),
+    "cai_eb_scratch_bytes": (_S, [_I64, c_int32]),
     "cai_eb_bwd": (_I, [_I, _I64, c_int32, POINTER(EbParams), _P, _I, c_int32, _P, c_int32, _F, _P, c_int32, _P,
-                        _I, c_int32, _P, c_int32, POINTER(EbGrads), _P]),
-    "cai_eb_aux_loss": (_I, [c_int32, POINTER(EbParams), _P, _P, _P, _P, c_int32, _P]),
+                        _I, c_int32, _P, c_int32, POINTER(EbGrads), _P, _S, _P, _P]),
+    "cai_eb_aux_loss": (_I, [c_int32, POINTER(EbParams), _P, _P, _P, _P, c_int32, _P, _S, _P, _P]),
     "cai_rd_loss_workspace_bytes": (_S, []),
     "cai_rd_loss_fwd": (_I, [POINTER(RdInputs), _F, _F, _P, _P, _S, _P]),
     "cai_rd_loss_bwd": (_I, [POINTER(RdInputs), _F, _F, _P, _P, _P, _P, POINTER(RdGrads), _P]),

@@ -459,12 +459,19 @@ def _edge_bwd(ctx, xs, weight, gy):
             dbt = torch.empty(g.out_c, dtype=torch.float32, device=gy.device) if ctx.has_bias else None
         nbytes = lib.cai_edge_workspace_bytes(ctypes.byref(g), dcode(dt))
         fl, nb = _ledger.conv_cost(g, _es(dt), 2, **({"x_bytes": 4} if ctx.edge == 1 else {"y_bytes": 4}))
-        with _WgradLaunch(gy.device, direct, img, feat):
+        if defer_reduce_ok(direct):
             ws = torch.empty(nbytes, dtype=torch.uint8, device=gy.device)
-            sw = _stream()
-            _ledger.run(lambda: lib.cai_edge_wgrad(ctypes.byref(g), _p(img), _p(feat), fld, _p(dwt), _p(dbt),
-                                                   int(direct), _p(ws), nbytes, sw),
-                        "conv_wgrad", "edge_wgrad_dma_kernel (+pack, reduce)", fl, nb, dt, _ledger.shape_of(g))
+            job = ReduceJob()
+            lib.cai_edge_wgrad_deferred(ctypes.byref(g), _p(img), _p(feat), fld, _p(dwt), _p(dbt), 1, _p(ws),
+                                        nbytes, st, ctypes.byref(job))
+            defer_job(job, gy.device, ws)
+        else:
+            with _WgradLaunch(gy.device, direct, img, feat):
+                ws = torch.empty(nbytes, dtype=torch.uint8, device=gy.device)
+                sw = _stream()
+                _ledger.run(lambda: lib.cai_edge_wgrad(ctypes.byref(g), _p(img), _p(feat), fld, _p(dwt), _p(dbt),
+                                                       int(direct), _p(ws), nbytes, sw),
+                            "conv_wgrad", "edge_wgrad_dma_kernel (+pack, reduce)", fl, nb, dt, _ledger.shape_of(g))
         if not direct:
             dw = dwt if weight.dtype == torch.float32 else dwt.to(weight.dtype)
             db = dbt
@@ -837,9 +844,13 @@ class BottleneckFn(torch.autograd.Function):
         G.accumulate = int(direct)
         P = _eb_params(prm, q_)
         n_el = npix * C
+        nsc = lib.cai_eb_scratch_bytes(npix, C)
+        scratch = torch.empty(nsc, dtype=torch.uint8, device=xr.device)
+        tickets = _eb_tickets(xr.device, C)
         _ledger.run(lambda: lib.cai_eb_bwd(mode, npix, C, ctypes.byref(P), _p(xr), dcode(xdtype), xld, _p(nr), nld, lb,
                                            _p(gl), glld, _p(gq_r), dcode(gq_r.dtype) if gq_r is not None else F32,
-                                           gqld, _p(dxb), C, ctypes.byref(G), _stream()),
+                                           gqld, _p(dxb), C, ctypes.byref(G), _p(scratch), nsc, _p(tickets),
+                                           _stream()),
                     "eb_bwd", "eb_bwd_kernel", 0, n_el * (3 * xr.element_size() + 8), torch.float32,
                     f"{n_el} elements")
         if direct:
@@ -848,6 +859,21 @@ class BottleneckFn(torch.autograd.Function):
 
 
 _UNIT_GRAD = {}
+_EB_TICKETS = {}
+_EB_AUX_SLOT = 1 << 12
+
+
+def _eb_tickets(device, C: int = 0, aux: bool = False) -> torch.Tensor:
+    """Zeroed uint32 hand-off tickets of the EntropyBottleneck kernels on `device` (cai_eb_bwd: one per channel;
+    cai_eb_aux_loss: one, in its own slot).  Every launch leaves them at zero, so one buffer per device serves
+    all calls and graph replays (EntropyBottleneck launches on one device never overlap: the forward's side
+    stream ends before its backward, the aux loss runs after the backward)."""
+    t = _EB_TICKETS.get(device)
+    if t is None:
+        t = _EB_TICKETS[device] = torch.zeros(_EB_AUX_SLOT + 64, dtype=torch.int32, device=device)
+    if C > _EB_AUX_SLOT:
+        raise ValueError(f"EntropyBottleneck with {C} channels: at most {_EB_AUX_SLOT}")
+    return t[_EB_AUX_SLOT:] if aux else t
 
 
 def _unit_grad(device) -> torch.Tensor:
@@ -876,8 +902,10 @@ class BottleneckAuxFn(torch.autograd.Function):
         loss = torch.empty((), dtype=torch.float32, device=quantiles.device)
         dq1 = torch.empty_like(q_)
         P = _eb_params(prm, q_)
+        nsc = lib.cai_eb_scratch_bytes(0, C)
+        scratch = torch.empty(nsc, dtype=torch.uint8, device=quantiles.device)
         lib.cai_eb_aux_loss(C, ctypes.byref(P), _p(t), _p(loss), _p(_unit_grad(quantiles.device)), _p(dq1), 0,
-                            _stream())
+                            _p(scratch), nsc, _p(_eb_tickets(quantiles.device, aux=True)), _stream())
         ctx.save_for_backward(dq1)
         ctx.qparam = quantiles
         ctx.nparams = len(prm)

@@ -22,6 +22,7 @@
 // weight-gradient partials are reduced in a fixed order (no float atomics) straight into the torch
 // layout of dW / db.
 #include "common.hpp"
+#include "reduce_jobs.hpp"
 #include "edge_frag.hpp"
 #include "mfma.hpp"
 
@@ -762,81 +763,6 @@ __global__ __launch_bounds__(NT, 1) void edge_wgrad_dma_kernel(const EdgeArgs A)
             for (int q = 0; q < 4; ++q) P[(t * 16 + 4 * g_ + q) * 128 + (wave * 2 + j) * 16 + i16] = acc[t][j][q];
 }
 
-// Fixed-order sum of the unit partials, scattered into the torch layout of dW (every element of dW /
-// db has exactly one source in G).  Block = 16 outputs x 16 unit groups; the image-side column sums
-// (16 outputs after G) come from cs_src[count][stride].
-template <int C>
-__global__ __launch_bounds__(256) void edge_wgrad_reduce_kernel(const EdgeArgs A, const float* __restrict__ cs_src,
-                                                                int cs_count, int cs_stride, float* __restrict__ dw,
-                                                                float* __restrict__ db, int accumulate) {
-    const int G = 9 * 16 * A.N, O = G + 16;
-    const int l = threadIdx.x & 15, grp = threadIdx.x >> 4;
-    const int o = blockIdx.x * 16 + l;
-    const float* src;
-    int cnt;
-    int64_t stride;
-    if (o < G) {
-        src = A.part + o;
-        cnt = A.units;
-        stride = O;
-    } else {
-        src = cs_src + (o - G);
-        cnt = cs_count;
-        stride = cs_stride;
-    }
-    float s = 0.f;
-    int u = grp;
-    for (; u + 16 * 7 < cnt; u += 16 * 8) {
-        float v[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = src[(int64_t)(u + 16 * i) * stride];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) s += v[i];
-    }
-    for (; u < cnt; u += 16) s += src[(int64_t)u * stride];
-    __shared__ float red[16][16];
-    __shared__ float tot[16];
-    red[grp][l] = s;
-    __syncthreads();
-    if (grp == 0) {
-        float v = 0.f;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) v += red[i][l];
-        tot[l] = v;
-    }
-    __syncthreads();
-    if (grp != 0) return;
-    s = tot[l];
-    if (o >= G) {   // G is a multiple of 16: this block holds exactly the 16 column sums
-        const int co = o - G;
-        if (A.mode == 1 && db && co < C) {
-            float v = 0.f;
-#pragma unroll
-            for (int sp = 0; sp < 4; ++sp) v += tot[sp * C + co];
-            db[co] = accumulate ? db[co] + v : v;
-        }
-        return;
-    }
-    const int nn = o % A.N, tc = o / A.N, t = tc / 16, chn = tc % 16;
-    int dst = -1;
-    if (A.mode == 0) {
-        if (chn == ONES) {
-            if (t == 4 && db) db[nn] = accumulate ? db[nn] + s : s;
-            return;
-        }
-        if (chn >= 4 * C) return;
-        const int sp = chn / C, ci = chn - sp * C;
-        const int ky = 2 * (t / 3 - 1) + (sp >> 1) + A.p, kx = 2 * (t % 3 - 1) + (sp & 1) + A.p;
-        if (ky >= 0 && ky < A.k && kx >= 0 && kx < A.k) dst = ((nn * C + ci) * A.k + ky) * A.k + kx;
-    } else {
-        if (chn >= 4 * C) return;
-        const int sp = chn / C, co = chn - sp * C, tf = 8 - t;
-        const int ky = (sp >> 1) - 2 * (tf / 3 - 1) + A.p, kx = (sp & 1) - 2 * (tf % 3 - 1) + A.p;
-        if (ky >= 0 && ky < A.k && kx >= 0 && kx < A.k) dst = ((nn * C + co) * A.k + ky) * A.k + kx;
-    }
-    if (dst >= 0) dw[dst] = accumulate ? dw[dst] + s : s;
-}
-
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -946,9 +872,17 @@ void launch_d2s(EdgeArgs A, hipStream_t st) {
         edge_d2s_kernel<C, 6><<<grid, 384, 0, st>>>(A);
 }
 
+// the weight-gradient kernels, then their fixed-order reduce as a job (reduce_jobs.hip): returned to a
+// deferring caller or run now
 template <int C>
-void launch_wgrad(EdgeArgs A, char* ws, float* dw, float* db, int accumulate, hipStream_t st) {
+void launch_wgrad(EdgeArgs A, char* ws, float* dw, float* db, int accumulate, hipStream_t st, cai_reduce_job* J) {
     const int O = 9 * 16 * A.N + 16;
+    *J = cai_reduce_job{};
+    J->kind = CAI_JOB_EDGE;
+    J->nblocks = O / 16;
+    J->p[0] = A.part; J->p[2] = dw; J->p[3] = db;
+    J->i[0] = A.N; J->i[1] = A.units; J->i[2] = A.mode; J->i[3] = A.k; J->i[4] = A.p; J->i[5] = C;
+    J->i[8] = accumulate;
     if (A.N == 128) {   // packed superpixels + LDS-DMA ring
         const WgradWs W = wgrad_ws(A);
         A.sbf = reinterpret_cast<bf16*>(ws + W.off_sbf);
@@ -957,10 +891,10 @@ void launch_wgrad(EdgeArgs A, char* ws, float* dw, float* db, int accumulate, hi
         A.prow = W.prow;
         edge_pack_s_kernel<C><<<W.npack, 256, 0, st>>>(A);
         edge_wgrad_dma_kernel<<<A.units, NT, 0, st>>>(A);
-        edge_wgrad_reduce_kernel<C><<<O / 16, 256, 0, st>>>(A, A.cs_part, W.npack, 16, dw, db, accumulate);
+        J->p[1] = A.cs_part; J->i[6] = W.npack; J->i[7] = 16;
     } else {
         edge_wgrad_kernel<C, 3><<<A.units, NT, 0, st>>>(A);
-        edge_wgrad_reduce_kernel<C><<<O / 16, 256, 0, st>>>(A, A.part + 9 * 16 * A.N, A.units, O, dw, db, accumulate);
+        J->p[1] = A.part + 9 * 16 * A.N; J->i[6] = A.units; J->i[7] = O;
     }
 }
 
@@ -1079,8 +1013,9 @@ int cai_edge_deconv_dgrad(const cai_conv_geom* g, const float* dy, const void* f
     return CAI_OK;
 }
 
-int cai_edge_wgrad(const cai_conv_geom* g, const float* img, const void* feat, int32_t feat_ld, float* dw, float* db,
-                   int32_t accumulate, void* workspace, size_t ws_bytes, void* stream) {
+static int run_edge_wgrad(const cai_conv_geom* g, const float* img, const void* feat, int32_t feat_ld, float* dw,
+                          float* db, int32_t accumulate, void* workspace, size_t ws_bytes, void* stream,
+                          cai_reduce_job* job) {
     EdgeArgs A;
     CAI_CHECK_ARG(edge_geo(g, CAI_BF16, A), "edge_wgrad: unsupported geometry");
     CAI_CHECK_ARG(img && feat && dw && aligned16(feat) && ((uintptr_t)img & 7) == 0,
@@ -1092,9 +1027,26 @@ int cai_edge_wgrad(const cai_conv_geom* g, const float* img, const void* feat, i
     A.feat_ld = feat_ld;
     A.part = static_cast<float*>(workspace);
     A.units = wgrad_units(A, &A.rch);
-    EDGE_BY_C(launch_wgrad, A, static_cast<char*>(workspace), dw, db, accumulate, as_stream(stream));
+    cai_reduce_job J{};
+    EDGE_BY_C(launch_wgrad, A, static_cast<char*>(workspace), dw, db, accumulate, as_stream(stream), &J);
     CAI_LAUNCH_CHECK("edge_wgrad");
-    return CAI_OK;
+    if (job) {
+        *job = J;
+        return CAI_OK;
+    }
+    return launch_reduce_jobs(&J, 1, as_stream(stream));
+}
+
+int cai_edge_wgrad(const cai_conv_geom* g, const float* img, const void* feat, int32_t feat_ld, float* dw, float* db,
+                   int32_t accumulate, void* workspace, size_t ws_bytes, void* stream) {
+    return run_edge_wgrad(g, img, feat, feat_ld, dw, db, accumulate, workspace, ws_bytes, stream, nullptr);
+}
+
+int cai_edge_wgrad_deferred(const cai_conv_geom* g, const float* img, const void* feat, int32_t feat_ld, float* dw,
+                            float* db, int32_t accumulate, void* workspace, size_t ws_bytes, void* stream,
+                            cai_reduce_job* job) {
+    CAI_CHECK_ARG(job, "edge_wgrad_deferred: null job");
+    return run_edge_wgrad(g, img, feat, feat_ld, dw, db, accumulate, workspace, ws_bytes, stream, job);
 }
 
 }  // extern "C"

@@ -196,9 +196,28 @@ __device__ __forceinline__ void eb_fill_tables(int c0, int nch, int C, const cai
     }
 }
 
-// forward of one chain; records pre-activations a[l][j] and outputs h[l][j]
+// tanh for the CDF chains: Cephes' single-precision tanhf (|x| < 0.625: odd polynomial, relative error
+// 1.3e-7; else 1 - 2 / (e^{2|x|} + 1) with the hardware exp; |x| > 9: +-1), ~12 instructions against ~100 for
+// the libm tanhf with its special-case branches -- the chains evaluate 12 per call and dominated the
+// EntropyBottleneck kernels.  The forward and backward kernels share it, so the backward re-derives exactly the
+// forward's values (sign, LowerBound mask) and reads tanh' = 1 - tanh^2 from the recorded values.
+__device__ __forceinline__ float eb_tanh(float x) {
+    const float ax = fabsf(x);
+    float r;
+    if (ax < 0.625f) {
+        const float z = x * x;
+        r = ((((-5.70498872745e-3f * z + 2.06390887954e-2f) * z - 5.37397155531e-2f) * z + 1.33314422036e-1f) * z -
+             3.33332819422e-1f) * z * x + x;
+    } else {
+        const float e = __expf(2.f * fminf(ax, 9.f));
+        r = copysignf(1.f - 2.f / (e + 1.f), x);
+    }
+    return r;
+}
+
+// forward of one chain; records the tanh of every hidden pre-activation and every hidden output
 struct EbTrace {
-    float a[4][3];
+    float t[4][3];   // tanh(a[l][j])
     float h[4][3];
 };
 
@@ -207,9 +226,10 @@ __device__ __forceinline__ float eb_chain(float x, const float* t, EbTrace* tr) 
     // layer 0: [3,1]
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        float a = t[EB_SP + j] * x + t[EB_B + j];
-        if (tr) tr->a[0][j] = a;
-        h[j] = a + t[EB_TF + j] * tanhf(a);
+        const float a = t[EB_SP + j] * x + t[EB_B + j];
+        const float th = eb_tanh(a);
+        if (tr) tr->t[0][j] = th;
+        h[j] = a + t[EB_TF + j] * th;
         if (tr) tr->h[0][j] = h[j];
     }
 #pragma unroll
@@ -217,9 +237,10 @@ __device__ __forceinline__ float eb_chain(float x, const float* t, EbTrace* tr) 
         const float* M = t + EB_SP + 3 + (l - 1) * 9;
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-            float a = M[j * 3 + 0] * h[0] + M[j * 3 + 1] * h[1] + M[j * 3 + 2] * h[2] + t[EB_B + l * 3 + j];
-            if (tr) tr->a[l][j] = a;
-            hn[j] = a + t[EB_TF + l * 3 + j] * tanhf(a);
+            const float a = M[j * 3 + 0] * h[0] + M[j * 3 + 1] * h[1] + M[j * 3 + 2] * h[2] + t[EB_B + l * 3 + j];
+            const float th = eb_tanh(a);
+            if (tr) tr->t[l][j] = th;
+            hn[j] = a + t[EB_TF + l * 3 + j] * th;
             if (tr) tr->h[l][j] = hn[j];
         }
 #pragma unroll
@@ -229,9 +250,8 @@ __device__ __forceinline__ float eb_chain(float x, const float* t, EbTrace* tr) 
     return M4[0] * h[0] + M4[1] * h[1] + M4[2] * h[2] + t[EB_B + 12];
 }
 
-// backward of one chain with upstream gradient d; accumulates d(softplus'd
-// matrix), d(bias), d(tanh'd factor) into g[] (same index layout as the
-// table) and returns d input.
+// backward of one chain with upstream gradient d; accumulates d(softplus'd matrix), d(bias), d(tanh'd factor)
+// into g[] (same index layout as the table) and returns d input.
 __device__ __forceinline__ float eb_chain_bwd(float x, float d, const float* t, const EbTrace& tr, float* g) {
     float dh[3];
     g[EB_B + 12] += d;
@@ -245,7 +265,7 @@ __device__ __forceinline__ float eb_chain_bwd(float x, float d, const float* t, 
         float da[3];
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-            const float th = tanhf(tr.a[l][j]);
+            const float th = tr.t[l][j];
             const float tf = t[EB_TF + l * 3 + j];
             g[EB_TF + l * 3 + j] += dh[j] * th;
             da[j] = dh[j] * (1.f + tf * (1.f - th * th));
@@ -286,7 +306,7 @@ __device__ __forceinline__ float eb_chain_dx(float d, const float* t, const EbTr
         float da[3];
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-            const float th = tanhf(tr.a[l][j]);
+            const float th = tr.t[l][j];
             da[j] = dh[j] * (1.f + t[EB_TF + l * 3 + j] * (1.f - th * th));
         }
         if (l == 0) return t[EB_SP + 0] * da[0] + t[EB_SP + 1] * da[1] + t[EB_SP + 2] * da[2];
@@ -328,26 +348,31 @@ __global__ __launch_bounds__(256) void eb_fwd_kernel(int mode, int64_t npix, int
     }
 }
 
-// bwd: one channel per block; its pixels spread over the 256 threads (one
-// chain pair per thread and pass), then the 60 per-channel parameter sums
-// reduce in a fixed order -- lanes by xor-shuffles, the 4 waves through LDS
-// (deterministic, no atomics).
+// bwd: grid (C, S): block (c, s) takes every S-th 256-pixel slice of channel c, one chain pair per thread and
+// pass; its 60 per-channel parameter sums reduce in a fixed order (lanes by xor-shuffles, the 4 waves through
+// LDS).  With S > 1 each block stores its 60 sums write-through (sc1) into part[c][s], and the block whose
+// arrival on the channel's ticket comes last sums them in split order (sc1 loads) -- the hand-off of
+// MI355X_MICROARCH.md's first hand-off row (every storing wave waits vmcnt(0), a workgroup barrier, one agent
+// atomic add per block; the last arriver learns it from the returned value), no fences -- resets the ticket
+// and applies the chain rule through softplus / tanh into the torch layout.  Deterministic.
 __global__ __launch_bounds__(256) void eb_bwd_kernel(int mode, int64_t npix, int C, cai_eb_params P,
                                                        const void* __restrict__ x, int xdt, int xld,
                                                        const float* __restrict__ noise, int nld, float lbound,
                                                        const float* __restrict__ glik, int glld,
                                                        const void* __restrict__ gq, int gqdt, int gqld,
-                                                       void* __restrict__ dx, int dxld, cai_eb_grads G) {
+                                                       void* __restrict__ dx, int dxld, cai_eb_grads G,
+                                                       float* __restrict__ part, unsigned* __restrict__ tickets) {
     __shared__ float tab[EB_NP];
     __shared__ float red[4][EB_NP];
-    const int c = blockIdx.x;
+    __shared__ int s_last;
+    const int c = blockIdx.x, S = gridDim.y, sp = blockIdx.y;
     eb_fill_tables<1>(c, 1, C, P, tab);
     __syncthreads();
     const float* t = tab;
     float g[EB_NP];
 #pragma unroll
     for (int k = 0; k < EB_NP; ++k) g[k] = 0.f;
-    for (int64_t p = threadIdx.x; p < npix; p += 256) {
+    for (int64_t p = (int64_t)sp * 256 + threadIdx.x; p < npix; p += (int64_t)S * 256) {
         const float xv = ld_any(x, xdt, p * xld + c);
         const float v = (mode == CAI_Q_NOISE) ? xv + noise[p * nld + c] : rintf(xv - t[EB_MED]) + t[EB_MED];
         EbTrace tl, tu;
@@ -379,11 +404,30 @@ __global__ __launch_bounds__(256) void eb_bwd_kernel(int mode, int64_t npix, int
         if (lane == 0) red[w][k] = v;
     }
     __syncthreads();
-    // one thread per table element: chain rule through softplus / tanh and the
-    // store to torch layout (independent loads and stores across threads)
     const int k = threadIdx.x;
+    float v = 0.f;
+    if (k < EB_NP) v = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
+    if (S > 1) {
+        float* mine = part + ((int64_t)c * S + sp) * EB_NP;
+        if (k < EB_NP) __hip_atomic_store(mine + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned prev = __hip_atomic_fetch_add(tickets + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_last = prev == (unsigned)S - 1;
+            if (s_last) __hip_atomic_store(tickets + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        if (!s_last) return;
+        if (k < EB_NP) {
+            const float* all = part + (int64_t)c * S * EB_NP + k;
+            v = 0.f;
+            for (int s2 = 0; s2 < S; ++s2)
+                v += __hip_atomic_load(all + (int64_t)s2 * EB_NP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    // one thread per table element: chain rule through softplus / tanh and the store to torch layout
     if (k >= EB_NP || k == 59) return;
-    const float v = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
     float* dst;
     float val;
     if (k < EB_B) {                                   // matrices: d softplus(raw) = sigmoid(raw)
@@ -416,39 +460,56 @@ __global__ __launch_bounds__(256) void eb_bwd_kernel(int mode, int64_t npix, int
     *dst = G.accumulate ? *dst + val : val;
 }
 
-// aux loss: one block, deterministic.  Channels in chunks of 128: the chunk's
-// tables are filled cooperatively into LDS, then one thread per (channel, k).
-constexpr int EB_AUX_CH = 128;   // PT = 8 loads per thread: no register spill at 1024 threads
-__global__ __launch_bounds__(1024) void eb_aux_kernel(int C, cai_eb_params P, const float* __restrict__ target,
-                                                       float* __restrict__ loss, const float* __restrict__ gloss,
-                                                       float* __restrict__ dq, int accumulate) {
-    __shared__ float red[16];
+// aux loss: blocks of 32 channels (96 (channel, k) threads, tables filled cooperatively into LDS).  Each block
+// stores its loss partial write-through and takes a ticket; the last block sums the partials in block order
+// (the eb_bwd hand-off) into *loss.  Deterministic.
+constexpr int EB_AUX_CH = 32;
+__global__ __launch_bounds__(256) void eb_aux_kernel(int C, cai_eb_params P, const float* __restrict__ target,
+                                                      float* __restrict__ loss, const float* __restrict__ gloss,
+                                                      float* __restrict__ dq, int accumulate,
+                                                      float* __restrict__ part, unsigned* __restrict__ ticket) {
+    __shared__ float red[4];
     __shared__ float tab[EB_AUX_CH * EB_NP];
+    __shared__ int s_last;
+    const int c0 = blockIdx.x * EB_AUX_CH;
+    const int nch = min(EB_AUX_CH, C - c0);
+    eb_fill_tables<(EB_AUX_CH * EB_NP + 255) / 256>(c0, nch, C, P, tab);
+    __syncthreads();
     float acc = 0.f;
     const float gs = gloss ? *gloss : 0.f;
-    for (int c0 = 0; c0 < C; c0 += EB_AUX_CH) {
-        const int nch = min(EB_AUX_CH, C - c0);
-        eb_fill_tables<(EB_AUX_CH * EB_NP + 1023) / 1024>(c0, nch, C, P, tab);
-        __syncthreads();
-        const int i = threadIdx.x;
-        if (i < 3 * nch) {
-            const int cl = i / 3, k = i - 3 * (i / 3), c = c0 + cl;
-            const float* t = tab + cl * EB_NP;
-            const float qv = P.quantiles[c * 3 + k];
-            EbTrace tr;
-            const float f = eb_chain(qv, t, &tr);
-            const float diff = f - target[k];
-            acc += fabsf(diff);
-            if (dq) {
-                const float sg = (diff > 0.f) ? 1.f : ((diff < 0.f) ? -1.f : 0.f);
-                const float v = eb_chain_dx(gs * sg, t, tr);
-                dq[c * 3 + k] = accumulate ? dq[c * 3 + k] + v : v;
-            }
+    const int i = threadIdx.x;
+    if (i < 3 * nch) {
+        const int cl = i / 3, k = i - 3 * (i / 3), c = c0 + cl;
+        const float* t = tab + cl * EB_NP;
+        const float qv = P.quantiles[c * 3 + k];
+        EbTrace tr;
+        const float f = eb_chain(qv, t, &tr);
+        const float diff = f - target[k];
+        acc = fabsf(diff);
+        if (dq) {
+            const float sg = (diff > 0.f) ? 1.f : ((diff < 0.f) ? -1.f : 0.f);
+            const float v = eb_chain_dx(gs * sg, t, tr);
+            dq[c * 3 + k] = accumulate ? dq[c * 3 + k] + v : v;
         }
-        __syncthreads();
     }
-    const float r = block_sum<1024>(acc, red);
-    if (threadIdx.x == 0 && loss) *loss = r;
+    const float r = block_sum<256>(acc, red);
+    const int nb = gridDim.x;
+    if (nb == 1) {
+        if (threadIdx.x == 0 && loss) *loss = r;
+        return;
+    }
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(part + blockIdx.x, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = prev == (unsigned)nb - 1;
+        if (s_last) {
+            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            float tot = 0.f;
+            for (int b = 0; b < nb; ++b) tot += __hip_atomic_load(part + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (loss) *loss = tot;
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -683,27 +744,48 @@ int cai_eb_fwd(int mode, int64_t npix, int32_t C, const cai_eb_params* prm, cons
     return CAI_OK;
 }
 
+static int eb_bwd_splits(int64_t npix) {
+    // one 256-pixel slice per block and pass; blocks of one channel hand their sums to the last arriver
+    return (int)std::max<int64_t>(1, std::min<int64_t>((npix + 255) / 256, 64));
+}
+static int eb_aux_blocks(int C) { return (C + EB_AUX_CH - 1) / EB_AUX_CH; }
+
+size_t cai_eb_scratch_bytes(int64_t npix, int32_t C) {
+    if (npix < 0 || C <= 0) return 0;
+    const size_t bwd = (size_t)C * eb_bwd_splits(npix) * EB_NP * sizeof(float);
+    const size_t aux = (size_t)eb_aux_blocks(C) * sizeof(float);
+    return std::max(bwd, aux) + 256;
+}
+
 int cai_eb_bwd(int mode, int64_t npix, int32_t C, const cai_eb_params* prm, const void* x, int x_dtype, int32_t x_ld,
                const float* noise, int32_t noise_ld, float lik_bound, const float* g_lik, int32_t gl_ld,
                const void* g_q, int gq_dtype, int32_t gq_ld, void* dx, int32_t dx_ld, const cai_eb_grads* grads,
-               void* stream) {
+               float* scratch, size_t scratch_bytes, uint32_t* tickets, void* stream) {
     CAI_CHECK_ARG(prm && grads, "eb_bwd: null params/grads");
     CAI_CHECK_ARG(mode == CAI_Q_NOISE || mode == CAI_Q_DEQUANTIZE, "eb_bwd: invalid mode %d", mode);
     for (int i = 0; i < 5; ++i) CAI_CHECK_ARG(grads->matrix[i] && grads->bias[i], "eb_bwd: null grad");
     for (int i = 0; i < 4; ++i) CAI_CHECK_ARG(grads->factor[i], "eb_bwd: null grad");
-    hipLaunchKernelGGL(eb_bwd_kernel, dim3(C), dim3(256), 0, as_stream(stream), mode, npix, C, *prm, x,
+    if (C == 0) return CAI_OK;
+    // without scratch / tickets: one block per channel (no hand-off)
+    const bool split = scratch && tickets && scratch_bytes >= cai_eb_scratch_bytes(npix, C);
+    const int S = split ? eb_bwd_splits(npix) : 1;
+    hipLaunchKernelGGL(eb_bwd_kernel, dim3(C, S), dim3(256), 0, as_stream(stream), mode, npix, C, *prm, x,
                        x_dtype, x_ld, noise, noise_ld, lik_bound, g_lik, gl_ld, g_q, gq_dtype, gq_ld, dx, dx_ld,
-                       *grads);
+                       *grads, scratch, tickets);
     CAI_LAUNCH_CHECK("eb_bwd");
     return CAI_OK;
 }
 
 int cai_eb_aux_loss(int32_t C, const cai_eb_params* prm, const float* target, float* loss, const float* g_loss,
-                    float* dquantiles, int32_t accumulate, void* stream) {
+                    float* dquantiles, int32_t accumulate, float* scratch, size_t scratch_bytes, uint32_t* ticket,
+                    void* stream) {
     CAI_CHECK_ARG(prm && target && C > 0, "eb_aux_loss: bad arguments");
     CAI_CHECK_ARG(!dquantiles || g_loss, "eb_aux_loss: dquantiles needs g_loss");
-    hipLaunchKernelGGL(eb_aux_kernel, dim3(1), dim3(1024), 0, as_stream(stream), C, *prm, target, loss, g_loss,
-                       dquantiles, accumulate);
+    const int nb = eb_aux_blocks(C);
+    CAI_CHECK_ARG(nb == 1 || (scratch && ticket && scratch_bytes >= (size_t)nb * sizeof(float)),
+                  "eb_aux_loss: %d channels need scratch and a ticket", C);
+    hipLaunchKernelGGL(eb_aux_kernel, dim3(nb), dim3(256), 0, as_stream(stream), C, *prm, target, loss, g_loss,
+                       dquantiles, accumulate, scratch, ticket);
     CAI_LAUNCH_CHECK("eb_aux_loss");
     return CAI_OK;
 }

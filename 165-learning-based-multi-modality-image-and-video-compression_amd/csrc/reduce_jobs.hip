@@ -11,6 +11,8 @@
 //          splits in split order (loads in batches of 8), the row transposed through LDS from [tap][q] to the
 //          torch layout dw[n][q][tap] and stored contiguously (rows wider than 8192 columns: one thread per
 //          chunk, scattered stores); trailing blocks: the bias partials [Sb][nbias] -> db, one thread per channel
+//   EDGE   the image-side layers' weight gradient (edge.hip): unit partials summed in unit order, scattered
+//          into dW / db (and the image-side column sums)
 //   GDN    16 element columns x 16 partial-block groups per block (4 consecutive elements per thread), the
 //          groups combined through LDS in a fixed tree, then the NonNegativeParametrizer / LowerBound backward
 //          rule (ops/parametrizers.py:47-64, ops/bound_ops.py:36-80) into dgamma_raw / dbeta_raw
@@ -178,9 +180,88 @@ __device__ __forceinline__ void gdn_reduce_body(const cai_reduce_job& J, int bid
     }
 }
 
+// EDGE: the image-side layers' weight gradient (edge.hip): unit partials [units][9*16*N + 16] summed in unit
+// order (16 outputs x 16 unit groups per block, groups combined through LDS), scattered into the torch layout
+// of dW / db; the 16 image-side column sums come from cs_src[count][stride]
+constexpr int EDGE_ONES = 12;   // edge.hip's constant-1 superpixel channel
+__device__ __forceinline__ void edge_reduce_body(const cai_reduce_job& J, int bid, float (*red)[16], float* tot) {
+    const float* __restrict__ part = static_cast<const float*>(J.p[0]);
+    const float* __restrict__ cs_src = static_cast<const float*>(J.p[1]);
+    float* __restrict__ dw = static_cast<float*>(const_cast<void*>(J.p[2]));
+    float* __restrict__ db = static_cast<float*>(const_cast<void*>(J.p[3]));
+    const int N = J.i[0], units = J.i[1], mode = J.i[2], k = J.i[3], pad = J.i[4], C = J.i[5];
+    const int cs_count = J.i[6], cs_stride = J.i[7], accumulate = J.i[8];
+    const int G = 9 * 16 * N, O = G + 16;
+    const int l = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    const int o = bid * 16 + l;
+    const float* src;
+    int cnt;
+    int64_t stride;
+    if (o < G) {
+        src = part + o;
+        cnt = units;
+        stride = O;
+    } else {
+        src = cs_src + (o - G);
+        cnt = cs_count;
+        stride = cs_stride;
+    }
+    float s = 0.f;
+    int u = grp;
+    for (; u + 16 * 7 < cnt; u += 16 * 8) {
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = src[(int64_t)(u + 16 * i) * stride];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s += v[i];
+    }
+    for (; u < cnt; u += 16) s += src[(int64_t)u * stride];
+    red[grp][l] = s;
+    __syncthreads();
+    if (grp == 0) {
+        float v = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v += red[i][l];
+        tot[l] = v;
+    }
+    __syncthreads();
+    if (grp != 0) return;
+    s = tot[l];
+    if (o >= G) {   // G is a multiple of 16: this block holds exactly the 16 column sums
+        const int co = o - G;
+        if (mode == 1 && db && co < C) {
+            float v = 0.f;
+#pragma unroll
+            for (int sp = 0; sp < 4; ++sp) v += tot[sp * C + co];
+            db[co] = accumulate ? db[co] + v : v;
+        }
+        return;
+    }
+    const int nn = o % N, tc = o / N, t = tc / 16, chn = tc % 16;
+    int dst = -1;
+    if (mode == 0) {
+        if (chn == EDGE_ONES) {
+            if (t == 4 && db) db[nn] = accumulate ? db[nn] + s : s;
+            return;
+        }
+        if (chn >= 4 * C) return;
+        const int sp = chn / C, ci = chn - sp * C;
+        const int ky = 2 * (t / 3 - 1) + (sp >> 1) + pad, kx = 2 * (t % 3 - 1) + (sp & 1) + pad;
+        if (ky >= 0 && ky < k && kx >= 0 && kx < k) dst = ((nn * C + ci) * k + ky) * k + kx;
+    } else {
+        if (chn >= 4 * C) return;
+        const int sp = chn / C, co = chn - sp * C, tf = 8 - t;
+        const int ky = (sp >> 1) - 2 * (tf / 3 - 1) + pad, kx = (sp & 1) - 2 * (tf % 3 - 1) + pad;
+        if (ky >= 0 && ky < k && kx >= 0 && kx < k) dst = ((nn * C + co) * k + ky) * k + kx;
+    }
+    if (dst >= 0) dw[dst] = accumulate ? dw[dst] + s : s;
+}
+
 __global__ __launch_bounds__(256) void reduce_jobs_kernel(const ReduceBatch B) {
     __shared__ f32x4 red[16][17];
     __shared__ __attribute__((aligned(16))) float row[WG_ROW_LDS];
+    __shared__ float ered[16][16];
+    __shared__ float etot[16];
     // the job owning this block (block-uniform linear scan over <= CAI_REDUCE_BATCH entries)
     const int b = blockIdx.x;
     int j = 0;
@@ -191,6 +272,8 @@ __global__ __launch_bounds__(256) void reduce_jobs_kernel(const ReduceBatch B) {
         wgrad_reduce_body(J, bid, row);
     else if (J.kind == CAI_JOB_GDN)
         gdn_reduce_body(J, bid, red);
+    else if (J.kind == CAI_JOB_EDGE)
+        edge_reduce_body(J, bid, ered, etot);
 }
 
 int launch_reduce_jobs(const cai_reduce_job* jobs, int n, hipStream_t st) {
@@ -200,7 +283,8 @@ int launch_reduce_jobs(const cai_reduce_job* jobs, int n, hipStream_t st) {
         for (; j0 < n && B.n < CAI_REDUCE_BATCH; ++j0) {
             const cai_reduce_job& J = jobs[j0];
             if (J.kind == CAI_JOB_NONE || J.nblocks <= 0) continue;
-            CAI_CHECK_ARG(J.kind == CAI_JOB_WGRAD || J.kind == CAI_JOB_GDN, "reduce_jobs: unknown job kind %d", J.kind);
+            CAI_CHECK_ARG(J.kind == CAI_JOB_WGRAD || J.kind == CAI_JOB_GDN || J.kind == CAI_JOB_EDGE,
+                          "reduce_jobs: unknown job kind %d", J.kind);
             B.jobs[B.n] = J;
             B.start[B.n] = blocks;
             blocks += J.nblocks;

@@ -170,6 +170,7 @@ int cai_conv_wgrad(const cai_conv_geom* g, int dtype,
 #define CAI_JOB_NONE 0
 #define CAI_JOB_WGRAD 1
 #define CAI_JOB_GDN 2
+#define CAI_JOB_EDGE 3
 typedef struct cai_reduce_job {
     int32_t kind, nblocks;
     int32_t i[10];
@@ -231,6 +232,10 @@ int cai_edge_deconv_dgrad(const cai_conv_geom* g, const float* dy, const void* f
  * conv: img = x, feat = dy; deconv: img = dy, feat = x.  Fixed-order reduction. */
 int cai_edge_wgrad(const cai_conv_geom* g, const float* img, const void* feat, int32_t feat_ld, float* dw, float* db,
                    int32_t accumulate, void* workspace, size_t ws_bytes, void* stream);
+/* cai_edge_wgrad with its final reduce left as a job (cai_reduce_jobs). */
+int cai_edge_wgrad_deferred(const cai_conv_geom* g, const float* img, const void* feat, int32_t feat_ld, float* dw,
+                            float* db, int32_t accumulate, void* workspace, size_t ws_bytes, void* stream,
+                            cai_reduce_job* job);
 
 /* =======================================================================
  * Pointwise glue of the residual / attention / sub-pixel blocks
@@ -421,16 +426,26 @@ int cai_eb_fwd(int mode, int64_t npix, int32_t C, const cai_eb_params* prm,
                const void* x, int x_dtype, int32_t x_ld,
                const float* noise, int32_t noise_ld, float lik_bound,
                void* q, int q_dtype, int32_t q_ld, float* lik, int32_t lik_ld, void* stream);
-/* parameter gradients (fp32, torch layout) per grads->accumulate. */
+/* Scratch of the split backward / the multi-block aux loss (fp32 partial sums).  Their hand-offs also take
+ * caller-owned uint32 tickets -- C for cai_eb_bwd, 1 for cai_eb_aux_loss -- zero before the first call; every
+ * call leaves them at zero (the last block of a hand-off resets its ticket), so one zeroed buffer serves every
+ * later call and graph replay on the same stream. */
+size_t cai_eb_scratch_bytes(int64_t npix, int32_t C);
+/* parameter gradients (fp32, torch layout) per grads->accumulate.  Each channel's pixels are split over up to
+ * 64 blocks whose sums the last arriving block adds in split order (deterministic); with scratch or tickets
+ * NULL (or scratch_bytes short) one block per channel. */
 int cai_eb_bwd(int mode, int64_t npix, int32_t C, const cai_eb_params* prm,
                const void* x, int x_dtype, int32_t x_ld,
                const float* noise, int32_t noise_ld, float lik_bound,
                const float* g_lik, int32_t gl_ld, const void* g_q, int gq_dtype, int32_t gq_ld,
-               void* dx, int32_t dx_ld, const cai_eb_grads* grads, void* stream);
+               void* dx, int32_t dx_ld, const cai_eb_grads* grads,
+               float* scratch, size_t scratch_bytes, uint32_t* tickets, void* stream);
 /* aux loss sum_c sum_k |F_c(quantiles[c,k]) - target[k]| -> *loss (fp32 scalar);
- * if dquantiles != NULL also writes d loss / d quantiles scaled by *g_loss. */
+ * if dquantiles != NULL also writes d loss / d quantiles scaled by *g_loss.  One block per 32 channels; more
+ * than 32 channels need scratch (cai_eb_scratch_bytes) and one ticket. */
 int cai_eb_aux_loss(int32_t C, const cai_eb_params* prm, const float* target,
-                    float* loss, const float* g_loss, float* dquantiles, int32_t accumulate, void* stream);
+                    float* loss, const float* g_loss, float* dquantiles, int32_t accumulate,
+                    float* scratch, size_t scratch_bytes, uint32_t* ticket, void* stream);
 
 /* =======================================================================
  * Rate-distortion loss reductions (examples/train.py:68-82).

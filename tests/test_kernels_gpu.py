@@ -387,12 +387,15 @@ def test_gaussian_conditional(cuda, with_means, training):
         assert relerr(md.grad, mr.grad) < FP32_TOL
 
 
-@pytest.mark.parametrize("training", [True, False])
-def test_entropy_bottleneck(cuda, training):
+@pytest.mark.parametrize("training,shape", [(True, (3, 40, 6, 5)), (False, (3, 40, 6, 5)),
+                                            (True, (4, 24, 32, 32)), (False, (2, 16, 40, 36))])
+def test_entropy_bottleneck(cuda, training, shape):
+    """Small maps: one block per channel; >= 512 pixels per channel: the split backward (up to 64 blocks per
+    channel, last-arriver sum in split order) -- also bit-identical over repeated calls."""
     from compressai.entropy_models import EntropyBottleneck, set_noise_source
 
     torch.manual_seed(5)
-    C = 40
+    C = shape[1]
     ref = O.EntropyBottleneck(C).train(training)
     with torch.no_grad():
         for n, p in ref.named_parameters():
@@ -400,7 +403,6 @@ def test_entropy_bottleneck(cuda, training):
     mod = EntropyBottleneck(C)
     mod.load_state_dict(ref.state_dict())
     mod = mod.to(cuda).train(training)
-    shape = (3, C, 6, 5)
     x = torch.randn(shape) * 3
     noise = torch.empty(shape).uniform_(-0.5, 0.5)
     xr = x.clone().requires_grad_()
@@ -426,16 +428,30 @@ def test_entropy_bottleneck(cuda, training):
             assert a.grad is None or a.grad.abs().max() == 0, n
         else:
             assert relerr(a.grad, b.grad) < 1e-3, n
+    # determinism of the split backward's hand-off: the same bits on a second pass
+    first = [p.grad.clone() for p in mod.parameters() if p.grad is not None] + [xd.grad.clone()]
+    mod.zero_grad()
+    xd.grad = None
+    set_noise_source(_noise_feed([noise]))
+    try:
+        q, lik = mod(xd)
+    finally:
+        set_noise_source(None)
+    torch.autograd.backward([q, lik], [gq.to(cuda), gl.to(cuda)])
+    second = [p.grad for p in mod.parameters() if p.grad is not None] + [xd.grad]
+    assert all(torch.equal(a, b) for a, b in zip(first, second))
 
 
-def test_entropy_bottleneck_aux_loss(cuda):
+@pytest.mark.parametrize("C", [64, 192, 20])
+def test_entropy_bottleneck_aux_loss(cuda, C):
+    """One block per 32 channels; the last arriving block sums the loss partials in block order."""
     from compressai.entropy_models import EntropyBottleneck
 
     torch.manual_seed(6)
-    ref = O.EntropyBottleneck(64)
+    ref = O.EntropyBottleneck(C)
     with torch.no_grad():
         ref.quantiles.add_(torch.randn_like(ref.quantiles))
-    mod = EntropyBottleneck(64)
+    mod = EntropyBottleneck(C)
     mod.load_state_dict(ref.state_dict())
     mod = mod.to(cuda)
     lr = ref.loss()
@@ -446,6 +462,7 @@ def test_entropy_bottleneck_aux_loss(cuda):
     assert relerr(l, lr) < FP32_TOL
     assert relerr(mod.quantiles.grad, ref.quantiles.grad) < FP32_TOL
     assert mod._matrix0.grad is None
+    assert torch.equal(mod.loss(), l)       # bit-stable
 
 
 def test_quantize_modes_bit_exact(cuda):
@@ -721,6 +738,25 @@ def test_deferred_reduce_jobs_bit_identical(cuda, batch):
             else:
                 lib.cai_conv_wgrad(ctypes.byref(g), 1, _p(x), cin, 0, 0, _p(dy), cout, _p(dw), _p(db), 1, _p(ws), nb, st)
                 outs_imm.append((dw, db))
+    # image-side layers (edge.hip): Conv2d(3, 128, 5, 2) weight gradient from the NCHW fp32 image
+    ge = ConvGeom(batch, 3, 64, 64, 128, 32, 32, 5, 2, 2, 0, 0)
+    img = torch.rand(batch, 3, 64, 64, device=dev)
+    feat = torch.randn(batch * 32 * 32, 128, device=dev).to(torch.bfloat16)
+    nbe = lib.cai_edge_workspace_bytes(ctypes.byref(ge), 1)
+    base_w, base_b = torch.randn(128, 3, 5, 5, device=dev), torch.randn(128, device=dev)
+    for deferred in (True, False):
+        dw, db = base_w.clone(), base_b.clone()
+        ws = torch.empty(nbe, dtype=torch.uint8, device=dev)
+        args = (ctypes.byref(ge), _p(img), _p(feat), 128, _p(dw), _p(db), 1, _p(ws), nbe, st)
+        if deferred:
+            job = ReduceJob()
+            lib.cai_edge_wgrad_deferred(*args, ctypes.byref(job))
+            jobs.append(job)
+            keep.append(ws)
+            outs_def.append((dw, db))
+        else:
+            lib.cai_edge_wgrad(*args)
+            outs_imm.append((dw, db))
     # fused GDN backward, C = 128 and 192
     for C in (128, 192):
         npix = batch * 32 * 32
@@ -752,7 +788,7 @@ def test_deferred_reduce_jobs_bit_identical(cuda, batch):
     arr = (ReduceJob * len(jobs))(*jobs)
     lib.cai_reduce_jobs(arr, len(jobs), st)
     torch.cuda.synchronize()
-    assert len(outs_def) == len(outs_imm) == 5
+    assert len(outs_def) == len(outs_imm) == 6
     bad = [(i, float((a0 - b0).abs().max()), float((a1 - b1).abs().max()))
            for i, ((a0, a1), (b0, b1)) in enumerate(zip(outs_def, outs_imm))
            if not (torch.equal(a0, b0) and torch.equal(a1, b1))]
