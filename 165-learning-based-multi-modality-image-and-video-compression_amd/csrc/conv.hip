@@ -3543,6 +3543,22 @@ static int colsum_nchunk(int64_t npix) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(1024, (npix + 255) / 256));
 }
 
+// A/B knobs of the weight-gradient pixel splits (read once): CAI_WG_BLOCKS = target blocks per launch (default
+// 256), CAI_WG_MIN_STRIPS = minimum 64-pixel strips per split of the halo kernels (default 4).  Fewer, larger
+// splits shrink the fp32 partial slabs (S x Ng x k*k*Cq floats, summed by the reduce job).
+static int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return (e && *e) ? std::max(1, atoi(e)) : dflt;
+}
+static int wg_blocks() {
+    static const int v = env_int("CAI_WG_BLOCKS", 256);
+    return v;
+}
+static int wg_min_strips() {
+    static const int v = env_int("CAI_WG_MIN_STRIPS", 4);
+    return v;
+}
+
 static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype, bool glds, bool in_tf = false) {
     WgradPlan W{};
     W.glds = glds && dtype == CAI_BF16;
@@ -3572,7 +3588,7 @@ static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype, bool glds, b
         // one 512-thread block per CU: ~256 blocks of (256-col tile, pixel split)
         W.ct = W.ncols <= 128 ? 128 : 256;      // 1x1 layers (GDN, small deconv): half-width tile
         W.tiles = ((W.ncols + W.ct - 1) / W.ct) * ((W.Ng + 127) / 128);
-        int S = std::max(1, 256 / W.tiles);
+        int S = std::max(1, wg_blocks() / W.tiles);
         S = (int)std::max<int64_t>(1, std::min<int64_t>(S, W.M / 256));
         W.split_len = ((W.M + S - 1) / S + 63) / 64 * 64;
         W.S = (int)((W.M + W.split_len - 1) / W.split_len);
@@ -3583,8 +3599,8 @@ static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype, bool glds, b
         const int Hg = g->transposed ? g->in_h : g->out_h;
         const int64_t nstrip = (int64_t)g->batch * Hg * Wg / 64;    // 64-pixel strips (R rows each)
         W.tiles = W.halo * (W.Cq_pad / 64) * ((W.Ng + 127) / 128);
-        int S = std::max(1, 256 / W.tiles);
-        S = (int)std::max<int64_t>(1, std::min<int64_t>(S, nstrip / 4));   // >= 4 strips per split
+        int S = std::max(1, wg_blocks() / W.tiles);
+        S = (int)std::max<int64_t>(1, std::min<int64_t>(S, nstrip / wg_min_strips()));   // >= 4 strips per split
         W.strips_per_split = (int)((nstrip + S - 1) / S);
         W.S = (int)((nstrip + W.strips_per_split - 1) / W.strips_per_split);
     }
