@@ -36,6 +36,14 @@ class WindowAttn(Structure):
                 ("scale", c_float)]
 
 
+NOISE_BUF, NOISE_DRAW, NOISE_REPLAY = 0, 1, 2             # cai_noise_src kinds (include/cai.h)
+NOISE_STATE_WORDS = 144                                  # CAI_NOISE_STATE_WORDS
+
+
+class NoiseSrc(Structure):
+    _fields_ = [("kind", c_int32), ("ld", c_int32), ("buf", c_void_p), ("state", c_void_p), ("slot", c_void_p)]
+
+
 class EbParams(Structure):
     _fields_ = [("matrix", c_void_p * 5), ("bias", c_void_p * 5), ("factor", c_void_p * 4), ("quantiles", c_void_p)]
 
@@ -64,6 +72,7 @@ class ReduceJob(Structure):
 # name -> (restype, argtypes)
 _P, _I, _I64, _F, _S = c_void_p, c_int, c_int64, c_float, c_size_t
 _G = POINTER(ConvGeom)
+_N = POINTER(NoiseSrc)
 SIGNATURES = {
     "cai_last_error": (c_char_p, []),
     "cai_version": (c_int, []),
@@ -133,15 +142,15 @@ SIGNATURES = {
     "cai_gdn_backward_deferred": (_I, [_I, _P, c_int32, _P, c_int32, _I64, c_int32, _P, _P, c_int32, _P, c_int32, _P,
                                        _P, _F, _F, _P, _P, c_int32, _P, _S, _P, POINTER(ReduceJob)]),
     "cai_uniform_noise": (_I, [_P, _I64, _P, _P]),
-    "cai_quantize": (_I, [_I, _I64, c_int32, _P, _I, c_int32, _P, c_int32, c_int32, _P, c_int32, _P, _I, c_int32, _P]),
-    "cai_gc_fwd": (_I, [_I, _I64, c_int32, _P, _I, c_int32, _P, c_int32, _P, c_int32, _I, _P, c_int32, _F, _F,
+    "cai_quantize": (_I, [_I, _I64, c_int32, _P, _I, c_int32, _P, c_int32, c_int32, _N, _P, _I, c_int32, _P]),
+    "cai_gc_fwd": (_I, [_I, _I64, c_int32, _P, _I, c_int32, _P, c_int32, _P, c_int32, _I, _N, _F, _F,
                         _P, _I, c_int32, _P, c_int32, _P]),
-    "cai_gc_bwd": (_I, [_I, _I64, c_int32, _P, _I, c_int32, _P, c_int32, _P, c_int32, _I, _P, c_int32, _F, _F,
+    "cai_gc_bwd": (_I, [_I, _I64, c_int32, _P, _I, c_int32, _P, c_int32, _P, c_int32, _I, _N, _F, _F,
                         _P, c_int32, _P, _I, c_int32, _P, c_int32, _P, c_int32, _P, c_int32, _P]),
-    "cai_eb_fwd": (_I, [_I, _I64, c_int32, POINTER(EbParams), _P, _I, c_int32, _P, c_int32, _F, _P, _I, c_int32,
+    "cai_eb_fwd": (_I, [_I, _I64, c_int32, POINTER(EbParams), _P, _I, c_int32, _N, _F, _P, _I, c_int32,
                         _P, c_int32, _P]),
     "cai_eb_scratch_bytes": (_S, [_I64, c_int32]),
-    "cai_eb_bwd": (_I, [_I, _I64, c_int32, POINTER(EbParams), _P, _I, c_int32, _P, c_int32, _F, _P, c_int32, _P,
+    "cai_eb_bwd": (_I, [_I, _I64, c_int32, POINTER(EbParams), _P, _I, c_int32, _N, _F, _P, c_int32, _P,
                         _I, c_int32, _P, c_int32, POINTER(EbGrads), _P, _S, _P, _P]),
     "cai_eb_aux_loss": (_I, [c_int32, POINTER(EbParams), _P, _P, _P, _P, c_int32, _P, _S, _P, _P]),
     "cai_rd_loss_workspace_bytes": (_S, []),

@@ -27,7 +27,8 @@ import torch
 
 from . import _ledger
 from ._native import (ACT_LEAKY, ACT_NONE, ACT_RELU, BF16, F32, MASK_LEAKY, MASK_NONE, MASK_POS, Q_DEQUANTIZE, Q_NOISE,
-                      JOB_NONE, ConvGeom, EbGrads, EbParams, RdGrads, RdInputs, ReduceJob, lib)
+                      JOB_NONE, NOISE_BUF, NOISE_DRAW, NOISE_REPLAY, ConvGeom, EbGrads, EbParams, NoiseSrc, RdGrads,
+                      RdInputs, ReduceJob, lib)
 
 _VP = ctypes.c_void_p
 _GDN_TWO_PASS = os.environ.get("CAI_GDN_TWO_PASS", "0") == "1"   # A/B knobs (tools/gpu_ab.sh)
@@ -730,29 +731,74 @@ class Gdn1OutFn(torch.autograd.Function):
 # entropy models
 # ---------------------------------------------------------------------------
 
+class DeviceDraw:
+    """A U(-1/2, 1/2) training-noise draw of `shape` that no kernel of its own makes and no buffer holds: the
+    first entropy kernel that consumes it draws it (cai_noise_src DRAW: reads the device generator's draw index,
+    records {seed, draw} in `slot`, advances the index) and every later consumer -- the other forward kernel
+    sharing the draw, the backward -- regenerates it from the slot (REPLAY).  Element (p, c) equals element
+    p*C + c of cai_uniform_noise's draw into a dense pixel-major buffer, so a DRAW launch reproduces a BUF
+    launch fed by cai_uniform_noise bit for bit (tests/test_noise_gpu.py).  Replaces the reference's
+    empty_like(x).uniform_(-0.5, 0.5) + add (entropy_models.py:170) like cai_uniform_noise, minus one launch
+    and the noise tensor's write + reads per draw."""
+
+    __slots__ = ("shape", "slot", "state", "drawn")
+
+    def __init__(self, shape, state: torch.Tensor):
+        self.shape = tuple(shape)
+        self.state = state
+        self.slot = torch.empty(2, dtype=torch.int64, device=state.device)
+        self.drawn = False
+
+    def record_stream(self, s):
+        self.slot.record_stream(s)
+
+    def src(self) -> NoiseSrc:
+        S = NoiseSrc()
+        S.kind = NOISE_REPLAY if self.drawn else NOISE_DRAW
+        S.state = self.state.data_ptr()
+        S.slot = self.slot.data_ptr()
+        self.drawn = True
+        return S
+
+
+def noise_src(noise, rows: Optional[torch.Tensor] = None, ld: int = 0):
+    """The cai_noise_src of a noise operand (None: no noise): a DeviceDraw, or a BUF over `rows` / ld."""
+    if noise is None:
+        return None
+    if isinstance(noise, DeviceDraw):
+        return ctypes.byref(noise.src())
+    S = NoiseSrc()
+    S.kind, S.ld, S.buf = NOISE_BUF, ld, rows.data_ptr()
+    return ctypes.byref(S)
+
+
 class GaussianFn(torch.autograd.Function):
     """GaussianConditional.forward (entropy_models.py:715-731) as one fused kernel pair."""
 
     @staticmethod
     def forward(ctx, x, scales, means, noise, mode: int, scale_bound: float, lik_bound: float):
-        _check_cuda(x, scales, means, noise)
+        """noise: None (DEQUANTIZE), an fp32 tensor, or a DeviceDraw."""
+        draw = noise if isinstance(noise, DeviceDraw) else None
+        _check_cuda(x, scales, means, None if draw is not None else noise)
         xr, xld, npix, C = as_rows(x)
         if means is not None and means.dtype != scales.dtype:
             means = means.to(scales.dtype)
         sr, sld, _, _ = as_rows(scales)
         mr, mld = (None, 0) if means is None else as_rows(means)[:2]
-        nr, nld = (None, 0) if noise is None else as_rows(noise)[:2]
+        nr, nld = (None, 0) if noise is None or draw is not None else as_rows(noise)[:2]
+        nsrc = noise_src(noise, nr, nld)
         smdt = dcode(scales.dtype)
         q, qbuf = empty_rows_like(x.shape, x.dtype, x.device)
         lik, lbuf = empty_rows_like(x.shape, torch.float32, x.device)
         n_el = npix * C
         _ledger.run(lambda: lib.cai_gc_fwd(mode, npix, C, _p(xr), dcode(x.dtype), xld, _p(sr), sld, _p(mr), mld, smdt,
-                                           _p(nr), nld, scale_bound, lik_bound, _p(qbuf), dcode(x.dtype), C, _p(lbuf),
+                                           nsrc, scale_bound, lik_bound, _p(qbuf), dcode(x.dtype), C, _p(lbuf),
                                            C, _stream()),
                     "gc_fwd", "gc_fwd_kernel", 0,
                     n_el * (2 * x.element_size() + scales.element_size() * (2 if means is not None else 1) + 4
-                            + (4 if noise is not None else 0)), torch.float32, f"{n_el} elements")
+                            + (4 if nr is not None else 0)), torch.float32, f"{n_el} elements")
         ctx.save_for_backward(xr, sr, mr, nr)
+        ctx.draw = draw
         ctx.cfg = (mode, scale_bound, lik_bound, xld, sld, mld, nld, npix, C, x.shape, x.dtype, scales.shape,
                    scales.dtype, means is not None)
         return q, lik
@@ -761,6 +807,7 @@ class GaussianFn(torch.autograd.Function):
     def backward(ctx, gq, glik):
         xr, sr, mr, nr = ctx.saved_tensors
         mode, sb, lb, xld, sld, mld, nld, npix, C, xshape, xdtype, sshape, sdtype, has_m = ctx.cfg
+        nsrc = noise_src(ctx.draw if ctx.draw is not None else nr, nr, nld)
         gl = gq_r = None
         glld = gqld = 0
         if glik is not None:
@@ -773,7 +820,7 @@ class GaussianFn(torch.autograd.Function):
         n_el = npix * C
         es_x, es_s = xr.element_size(), sr.element_size()
         _ledger.run(lambda: lib.cai_gc_bwd(mode, npix, C, _p(xr), dcode(xdtype), xld, _p(sr), sld, _p(mr), mld,
-                                           dcode(sdtype), _p(nr), nld, sb, lb, _p(gl), glld, _p(gq_r),
+                                           dcode(sdtype), nsrc, sb, lb, _p(gl), glld, _p(gq_r),
                                            dcode(gq_r.dtype) if gq_r is not None else F32, gqld, _p(dxb), C, _p(dsb),
                                            C, _p(dmb), C, _stream()),
                     "gc_bwd", "gc_bwd_kernel", 0,
@@ -799,20 +846,24 @@ class BottleneckFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, quantiles, noise, mode: int, lik_bound: float, *params):
-        _check_cuda(x, quantiles, noise)
+        """noise: None (DEQUANTIZE), an fp32 tensor, or a DeviceDraw."""
+        draw = noise if isinstance(noise, DeviceDraw) else None
+        _check_cuda(x, quantiles, None if draw is not None else noise)
         prm = [p.detach().float().contiguous() for p in params]
         q_ = quantiles.detach().float().contiguous()
         xr, xld, npix, C = as_rows(x)
-        nr, nld = (None, 0) if noise is None else as_rows(noise)[:2]
+        nr, nld = (None, 0) if noise is None or draw is not None else as_rows(noise)[:2]
+        nsrc = noise_src(noise, nr, nld)
         q, qbuf = empty_rows_like(x.shape, x.dtype, x.device)
         lik, lbuf = empty_rows_like(x.shape, torch.float32, x.device)
         P = _eb_params(prm, q_)
         n_el = npix * C
-        _ledger.run(lambda: lib.cai_eb_fwd(mode, npix, C, ctypes.byref(P), _p(xr), dcode(x.dtype), xld, _p(nr), nld,
+        _ledger.run(lambda: lib.cai_eb_fwd(mode, npix, C, ctypes.byref(P), _p(xr), dcode(x.dtype), xld, nsrc,
                                            lik_bound, _p(qbuf), dcode(x.dtype), C, _p(lbuf), C, _stream()),
-                    "eb_fwd", "eb_fwd_kernel", 0, n_el * (2 * x.element_size() + 4 + (4 if noise is not None else 0)),
+                    "eb_fwd", "eb_fwd_kernel", 0, n_el * (2 * x.element_size() + 4 + (4 if nr is not None else 0)),
                     torch.float32, f"{n_el} elements")
         ctx.save_for_backward(xr, nr, q_, *prm)
+        ctx.draw = draw
         ctx.cfg = (mode, lik_bound, xld, nld, npix, C, x.shape, x.dtype)
         ctx.params = (quantiles,) + tuple(params)
         return q, lik
@@ -821,6 +872,7 @@ class BottleneckFn(torch.autograd.Function):
     def backward(ctx, gq, glik):
         xr, nr, q_, *prm = ctx.saved_tensors
         mode, lb, xld, nld, npix, C, xshape, xdtype = ctx.cfg
+        nsrc = noise_src(ctx.draw if ctx.draw is not None else nr, nr, nld)
         gl = gq_r = None
         glld = gqld = 0
         if glik is not None:
@@ -847,7 +899,7 @@ class BottleneckFn(torch.autograd.Function):
         nsc = lib.cai_eb_scratch_bytes(npix, C)
         scratch = torch.empty(nsc, dtype=torch.uint8, device=xr.device)
         tickets = _eb_tickets(xr.device, C)
-        _ledger.run(lambda: lib.cai_eb_bwd(mode, npix, C, ctypes.byref(P), _p(xr), dcode(xdtype), xld, _p(nr), nld, lb,
+        _ledger.run(lambda: lib.cai_eb_bwd(mode, npix, C, ctypes.byref(P), _p(xr), dcode(xdtype), xld, nsrc, lb,
                                            _p(gl), glld, _p(gq_r), dcode(gq_r.dtype) if gq_r is not None else F32,
                                            gqld, _p(dxb), C, ctypes.byref(G), _p(scratch), nsc, _p(tickets),
                                            _stream()),

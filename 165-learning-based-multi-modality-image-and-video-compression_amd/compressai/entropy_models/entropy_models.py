@@ -11,8 +11,12 @@ training-mode noise is U(-1/2, 1/2) as in the reference
 device by cai_uniform_noise (Philox4x32-10, counter kept in device memory: a
 captured graph draws new noise on every replay without torch's generator and
 its per-replay re-seeding launches); seeded from torch.cuda.initial_seed(), so
-torch.cuda.manual_seed() keeps runs reproducible.  Tests inject their own
-draws (set_noise_source) to compare against the CPU oracle.
+torch.cuda.manual_seed() keeps runs reproducible.  By default no launch of its
+own makes the draw: the first kernel that consumes it generates it in-register
+(_ops.DeviceDraw, cai_noise_src DRAW) and the later ones regenerate it (REPLAY),
+the same values cai_uniform_noise would have written (CAI_FUSED_NOISE=0: the
+separate draw).  Tests inject their own draws (set_noise_source) to compare
+against the CPU oracle.
 
 The bitstream side follows the reference too:
 update() evaluates the pmfs with the reference's torch expressions on the
@@ -35,8 +39,9 @@ import torch.nn as nn
 import scipy.stats
 
 from .. import _coder
-from .._native import F32, Q_DEQUANTIZE, Q_NOISE, Q_SYMBOLS, lib
-from .._ops import BottleneckAuxFn, BottleneckFn, GaussianFn, _check_cuda, _p, _stream, as_rows, dcode, empty_rows_like
+from .._native import F32, NOISE_STATE_WORDS, Q_DEQUANTIZE, Q_NOISE, Q_SYMBOLS, lib
+from .._ops import (BottleneckAuxFn, BottleneckFn, DeviceDraw, GaussianFn, _check_cuda, _p, _stream, as_rows, dcode,
+                    empty_rows_like, noise_src)
 from ..ops import LowerBound
 
 __all__ = ["EntropyModel", "EntropyBottleneck", "GaussianConditional", "set_noise_source", "seed_noise"]
@@ -54,13 +59,16 @@ def set_noise_source(fn: Optional[Callable[[torch.Tensor], torch.Tensor]]):
     _noise_source = fn
 
 
-# on-device generator state per GPU: [seed, draw index, arrival ticket] (uint64 bit patterns).  ONE state per
-# device: draws that use it must be ordered (one stream, or event-ordered) -- two concurrent launches would read
-# the same draw index and mix their arrival tickets.  The models' hyper-branch fork therefore draws z's noise on
-# the caller's stream before forking (models/google.py, _fork_noise).
+# on-device generator state per GPU: [seed, draw index, arrival ticket, ..., the DRAW launches' per-XCD arrival
+# shards] (NOISE_STATE_WORDS uint64 bit patterns, include/cai.h).  ONE state per device: draws that use it must
+# be ordered (one stream, or event-ordered) -- two concurrent launches would read the same draw index and mix
+# their arrival tickets.  The models' hyper-branch fork therefore draws z's noise on the caller's stream before
+# forking (models/google.py, _z_noise).
 _noise_states: dict = {}
-# A/B knob (read once): CAI_TORCH_NOISE=1 draws with torch's generator instead (`uniform_`, as the reference)
+# A/B knobs (read once): CAI_TORCH_NOISE=1 draws with torch's generator instead (`uniform_`, as the reference);
+# CAI_FUSED_NOISE=0 draws into a buffer with cai_uniform_noise instead of inside the consuming kernel
 _TORCH_NOISE = os.environ.get("CAI_TORCH_NOISE", "0") == "1"
+_FUSED_NOISE = os.environ.get("CAI_FUSED_NOISE", "1") == "1"
 
 
 def _as_i64(v: int) -> int:
@@ -77,8 +85,9 @@ def seed_noise(seed: int, device=None) -> None:
         st = [None, None]
         _noise_states[idx] = st
     if st[0] is None:
-        st[0] = torch.zeros(3, dtype=torch.int64, device=torch.device("cuda", idx))
-    st[0].copy_(torch.tensor([_as_i64(seed), 0, 0], dtype=torch.int64))
+        st[0] = torch.zeros(NOISE_STATE_WORDS, dtype=torch.int64, device=torch.device("cuda", idx))
+    st[0].zero_()
+    st[0][0].fill_(_as_i64(seed))
     with torch.cuda.device(idx):
         st[1] = torch.cuda.initial_seed()   # torch's seed at this point: a later manual_seed() re-seeds
 
@@ -115,10 +124,21 @@ def _draw_noise(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def _noise_for(x: torch.Tensor):
+    """Training noise for x, to hand to a noise-mode entropy kernel: a DeviceDraw (drawn inside that kernel),
+    or -- with an injected source, torch's generator, or CAI_FUSED_NOISE=0 -- a tensor from _draw_noise."""
+    if _noise_source is not None or _TORCH_NOISE or not _FUSED_NOISE:
+        return _draw_noise(x)
+    _check_cuda(x)
+    return DeviceDraw(x.shape, _noise_state(x.device))
+
+
 class _QuantizeFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, means, noise, mode: int):
-        _check_cuda(x, means, noise)
+        """noise: None, an fp32 tensor, or a DeviceDraw (NOISE mode)."""
+        draw = isinstance(noise, DeviceDraw)
+        _check_cuda(x, means, None if draw else noise)
         xr, xld, npix, C = as_rows(x)
         m = None
         mld, mpc = 0, 0
@@ -127,11 +147,11 @@ class _QuantizeFn(torch.autograd.Function):
                 m, mld, mpc = means.float().contiguous().reshape(C), 0, 1
             else:
                 m, mld = as_rows(means.float().expand_as(x))[:2]
-        nr, nld = (None, 0) if noise is None else as_rows(noise)[:2]
+        nr, nld = (None, 0) if noise is None or draw else as_rows(noise)[:2]
         odt = torch.int32 if mode == Q_SYMBOLS else x.dtype
         out, obuf = empty_rows_like(x.shape, odt, x.device)
-        lib.cai_quantize(mode, npix, C, _p(xr), dcode(x.dtype), xld, _p(m), mld, mpc, _p(nr), nld, _p(obuf),
-                         dcode(x.dtype) if mode != Q_SYMBOLS else F32, C, _stream())
+        lib.cai_quantize(mode, npix, C, _p(xr), dcode(x.dtype), xld, _p(m), mld, mpc, noise_src(noise, nr, nld),
+                         _p(obuf), dcode(x.dtype) if mode != Q_SYMBOLS else F32, C, _stream())
         ctx.mode = mode
         ctx.has_means = means is not None
         ctx.mshape = None if means is None else means.shape
@@ -194,7 +214,7 @@ class EntropyModel(nn.Module):
         if mode not in ("noise", "dequantize", "symbols"):
             raise ValueError(f'Invalid quantization mode: "{mode}"')
         if mode == "noise":
-            return _QuantizeFn.apply(inputs, None, _draw_noise(inputs), Q_NOISE)
+            return _QuantizeFn.apply(inputs, None, _noise_for(inputs), Q_NOISE)
         if mode == "dequantize":
             return _QuantizeFn.apply(inputs, means, None, Q_DEQUANTIZE)
         return _QuantizeFn.apply(inputs, means, None, Q_SYMBOLS)
@@ -331,7 +351,7 @@ class EntropyBottleneck(EntropyModel):
         if x.dim() < 2 or x.shape[1] != self.channels:
             raise ValueError(f"expected [B, {self.channels}, ...] input, got {tuple(x.shape)}")
         if training and noise is None:
-            noise = _draw_noise(x)
+            noise = _noise_for(x)
         elif training and tuple(noise.shape) != tuple(x.shape):
             raise ValueError(f"noise shape {tuple(noise.shape)} does not match the input's {tuple(x.shape)}")
         elif not training:
@@ -450,7 +470,7 @@ class GaussianConditional(EntropyModel):
         except RuntimeError as e:
             raise ValueError(f"scales / means do not broadcast to the inputs' shape {tuple(inputs.shape)}") from e
         if training and noise is None:
-            noise = _draw_noise(inputs)
+            noise = _noise_for(inputs)
         elif not training:
             noise = None
         sb = self._scale_bound_value

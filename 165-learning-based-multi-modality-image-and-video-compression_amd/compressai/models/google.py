@@ -38,7 +38,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..entropy_models import EntropyBottleneck, GaussianConditional
-from ..entropy_models.entropy_models import _QuantizeFn, _draw_noise
+from ..entropy_models.entropy_models import _QuantizeFn, _draw_noise, _noise_for
 from .._native import Q_DEQUANTIZE, Q_NOISE
 from ..layers import GDN, MaskedConv2d, Sequential
 from .._ops import CatFn, ConvFn, ConvSpec
@@ -71,8 +71,9 @@ def _side_stream(t: torch.Tensor, default: bool):
 
 
 def _quantize_y(y, training):
-    """y_hat = y + U(-1/2, 1/2) (training) / round(y) (eval): GaussianConditional.quantize without means."""
-    noise = _draw_noise(y) if training else None
+    """y_hat = y + U(-1/2, 1/2) (training) / round(y) (eval): GaussianConditional.quantize without means.  The
+    draw is made inside the quantize kernel (a DeviceDraw; the likelihood kernel on the side stream replays it)."""
+    noise = _noise_for(y) if training else None
     return _QuantizeFn.apply(y, None, noise, Q_NOISE if training else Q_DEQUANTIZE), noise
 
 

@@ -19,18 +19,113 @@ static constexpr float kNegInvSqrt2 = -0.70710678118654752440f;   // float(-(2**
 static constexpr float kTwoOverSqrtPi = 1.12837916709551257390f;
 
 // ---------------------------------------------------------------------------
+// training noise U(-1/2, 1/2) (entropy_models.py:170 `empty_like(x).uniform_(-0.5, 0.5)`) generated on the
+// device from a counter in device memory, so a captured graph draws fresh noise on every replay without
+// torch's generator (whose replays re-seed through extra fill launches).  Philox4x32-10 (Salmon et al.,
+// SC'11): key = the 64-bit seed, counter = (element quad, draw index); the draw index lives in
+// state[1] and is advanced by the last block of each launch to finish (state[2] is its arrival ticket,
+// left at 0), so every launch -- and every replay -- uses a new counter range.  24-bit mantissas:
+// u = (r >> 8) * 2^-24 - 1/2 in [-1/2, 1/2).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void philox_round(unsigned (&c)[4], const unsigned (&k)[2]) {
+    const unsigned long long p0 = (unsigned long long)0xD2511F53u * c[0];
+    const unsigned long long p1 = (unsigned long long)0xCD9E8D57u * c[2];
+    const unsigned hi0 = (unsigned)(p0 >> 32), lo0 = (unsigned)p0, hi1 = (unsigned)(p1 >> 32), lo1 = (unsigned)p1;
+    c[0] = hi1 ^ c[1] ^ k[0];
+    c[1] = lo1;
+    c[2] = hi0 ^ c[3] ^ k[1];
+    c[3] = lo0;
+}
+__device__ __forceinline__ void philox4x32_10(unsigned (&c)[4], unsigned k0, unsigned k1) {
+    unsigned k[2] = {k0, k1};
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        philox_round(c, k);
+        k[0] += 0x9E3779B9u;
+        k[1] += 0xBB67AE85u;
+    }
+}
+
+__device__ __forceinline__ float philox_uniform(unsigned long long seed, unsigned long long draw, int64_t i) {
+    const unsigned long long q = (unsigned long long)i >> 2;
+    unsigned c[4] = {(unsigned)q, (unsigned)(q >> 32), (unsigned)draw, (unsigned)(draw >> 32)};
+    philox4x32_10(c, (unsigned)seed, (unsigned)(seed >> 32));
+    const unsigned e = (unsigned)i & 3u;
+    const unsigned r = e == 0 ? c[0] : (e == 1 ? c[1] : (e == 2 ? c[2] : c[3]));
+    return (float)(r >> 8) * 5.9604644775390625e-8f - 0.5f;
+}
+
+// The noise operand inside a kernel (cai_noise_src): a buffer, or the Philox draw {seed, draw} generated per
+// element -- element (p, c) is element p*C + c of cai_uniform_noise's draw, so DRAW / REPLAY reproduce a
+// BUF launch fed by cai_uniform_noise bit for bit.
+struct NoiseView {
+    const float* buf;
+    int ld, gen;
+    unsigned long long seed, draw;
+    __device__ __forceinline__ float at(int64_t p, int c, int C) const {
+        return gen ? philox_uniform(seed, draw, p * C + c) : buf[p * ld + c];
+    }
+};
+
+// Every thread calls this before any early return.  DRAW: thread 0 of each block reads the generator (seed,
+// draw index) and broadcasts it through LDS; block 0 records it in the slot for the REPLAY launches.
+__device__ __forceinline__ NoiseView noise_open(const cai_noise_src& S) {
+    NoiseView v{S.buf, S.ld, S.kind != CAI_NOISE_BUF, 0ull, 0ull};
+    if (S.kind == CAI_NOISE_DRAW) {
+        __shared__ unsigned long long sd[2];
+        if (threadIdx.x == 0 && threadIdx.y == 0) {
+            const unsigned long long seed = __hip_atomic_load(S.state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long draw = __hip_atomic_load(S.state + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sd[0] = seed;
+            sd[1] = draw;
+            if (blockIdx.x == 0 && blockIdx.y == 0) {
+                __hip_atomic_store(S.slot, seed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(S.slot + 1, draw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __syncthreads();
+        v.seed = sd[0];
+        v.draw = sd[1];
+    } else if (S.kind == CAI_NOISE_REPLAY) {
+        v.seed = S.slot[0];
+        v.draw = S.slot[1];
+    }
+    return v;
+}
+
+// DRAW: thread 0 of every block, after its noise_open (its state read is complete: the value went to LDS).
+// The block arrives on its XCD shard's ticket (blocks go round-robin over the 8 XCDs, shard = linear block id
+// mod 8; a fan-in on one word costs ~12 ns per arrival, MI355X_MICROARCH.md 'fanin'); the last arriver of each
+// shard resets it and arrives on state[2]; the last of those advances the draw index and resets state[2].
+// Relaxed: the next launch sees the new index across the kernel boundary.
+__device__ __forceinline__ void noise_close(const cai_noise_src& S, const NoiseView& v) {
+    if (S.kind != CAI_NOISE_DRAW || threadIdx.x != 0 || threadIdx.y != 0) return;
+    const unsigned nb = gridDim.x * gridDim.y;
+    const unsigned b = blockIdx.y * gridDim.x + blockIdx.x;
+    const unsigned k = b & 7u;
+    const unsigned nk = (nb - k + 7u) / 8u;
+    unsigned long long* shard = S.state + CAI_NOISE_SHARD0 + 16 * k;
+    if (__hip_atomic_fetch_add(shard, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != nk - 1) return;
+    __hip_atomic_store(shard, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned ns = nb < 8u ? nb : 8u;
+    if (__hip_atomic_fetch_add(S.state + 2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ns - 1) return;
+    __hip_atomic_store(S.state + 2, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(S.state + 1, v.draw + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---------------------------------------------------------------------------
 // quantize
 // ---------------------------------------------------------------------------
 __global__ void quantize_kernel(int mode, int64_t n, int C, const void* __restrict__ x, int xdt, int xld,
                                 const float* __restrict__ means, int mld, int means_pc,
-                                const float* __restrict__ noise, int nld, void* __restrict__ out, int odt,
-                                int old) {
+                                const cai_noise_src ns, void* __restrict__ out, int odt, int old) {
+    const NoiseView nv = noise_open(ns);
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t p = i / C;
         const int c = (int)(i - p * C);
         const float v = ld_any(x, xdt, p * xld + c);
         if (mode == CAI_Q_NOISE) {
-            st_any(out, odt, p * old + c, v + noise[p * nld + c]);
+            st_any(out, odt, p * old + c, v + nv.at(p, c, C));
             continue;
         }
         float mu = 0.f;
@@ -42,6 +137,7 @@ __global__ void quantize_kernel(int mode, int64_t n, int C, const void* __restri
             st_any(out, odt, p * old + c, means ? r + mu : r);
         }
     }
+    noise_close(ns, nv);
 }
 
 static inline int ew_grid(int64_t n, int nt = 256) {
@@ -65,8 +161,9 @@ __device__ __forceinline__ float std_cum_grad(float t) {
 
 __global__ void gc_fwd_kernel(int mode, int64_t n, int C, const void* __restrict__ x, int xdt, int xld,
                               const void* __restrict__ sc, int sld, const void* __restrict__ mu, int mld, int smdt,
-                              const float* __restrict__ noise, int nld, float sbound, float lbound,
+                              const cai_noise_src ns, float sbound, float lbound,
                               void* __restrict__ q, int qdt, int qld, float* __restrict__ lik, int lld) {
+    const NoiseView nv = noise_open(ns);
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t p = i / C;
         const int c = (int)(i - p * C);
@@ -74,7 +171,7 @@ __global__ void gc_fwd_kernel(int mode, int64_t n, int C, const void* __restrict
         const float m = mu ? ld_any(mu, smdt, p * mld + c) : 0.f;
         float qv;
         if (mode == CAI_Q_NOISE)
-            qv = xv + noise[p * nld + c];
+            qv = xv + nv.at(p, c, C);
         else
             qv = mu ? rintf(xv - m) + m : rintf(xv);
         if (q) st_any(q, qdt, p * qld + c, qv);
@@ -85,20 +182,22 @@ __global__ void gc_fwd_kernel(int mode, int64_t n, int C, const void* __restrict
         const float lo = std_cum((-0.5f - av) / s);
         lik[p * lld + c] = fmaxf(up - lo, lbound);
     }
+    noise_close(ns, nv);
 }
 
 __global__ void gc_bwd_kernel(int mode, int64_t n, int C, const void* __restrict__ x, int xdt, int xld,
                               const void* __restrict__ sc, int sld, const void* __restrict__ mu, int mld, int smdt,
-                              const float* __restrict__ noise, int nld, float sbound, float lbound,
+                              const cai_noise_src ns, float sbound, float lbound,
                               const float* __restrict__ glik, int glld, const void* __restrict__ gq, int gqdt,
                               int gqld, void* __restrict__ dx, int dxld, void* __restrict__ ds, int dsld,
                               void* __restrict__ dm, int dmld) {
+    const NoiseView nv = noise_open(ns);   // BUF or REPLAY
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t p = i / C;
         const int c = (int)(i - p * C);
         const float xv = ld_any(x, xdt, p * xld + c);
         const float m = mu ? ld_any(mu, smdt, p * mld + c) : 0.f;
-        const float qv = (mode == CAI_Q_NOISE) ? xv + noise[p * nld + c] : (mu ? rintf(xv - m) + m : rintf(xv));
+        const float qv = (mode == CAI_Q_NOISE) ? xv + nv.at(p, c, C) : (mu ? rintf(xv - m) + m : rintf(xv));
         const float v = mu ? qv - m : qv;
         const float sraw = ld_any(sc, smdt, p * sld + c);
         const float s = fmaxf(sraw, sbound);
@@ -320,10 +419,11 @@ __device__ __forceinline__ float eb_chain_dx(float d, const float* t, const EbTr
 // fwd: block = 256 threads = 32 channels x 8 pixel rows
 __global__ __launch_bounds__(256) void eb_fwd_kernel(int mode, int64_t npix, int C, cai_eb_params P,
                                                       const void* __restrict__ x, int xdt, int xld,
-                                                      const float* __restrict__ noise, int nld, float lbound,
+                                                      const cai_noise_src ns, float lbound,
                                                       void* __restrict__ q, int qdt, int qld,
                                                       float* __restrict__ lik, int lld) {
     __shared__ float tab[32][EB_NP];
+    const NoiseView nv = noise_open(ns);
     const int cl = threadIdx.x & 31, pr = threadIdx.x >> 5;
     const int c0 = blockIdx.x * 32;
     eb_fill_tables<(32 * EB_NP + 255) / 256>(c0, 32, C, P, &tab[0][0]);
@@ -335,7 +435,7 @@ __global__ __launch_bounds__(256) void eb_fwd_kernel(int mode, int64_t npix, int
         const float xv = ld_any(x, xdt, p * xld + c);
         float v;
         if (mode == CAI_Q_NOISE)
-            v = xv + noise[p * nld + c];
+            v = xv + nv.at(p, c, C);
         else
             v = rintf(xv - t[EB_MED]) + t[EB_MED];
         if (q) st_any(q, qdt, p * qld + c, v);
@@ -346,6 +446,7 @@ __global__ __launch_bounds__(256) void eb_fwd_kernel(int mode, int64_t npix, int
         const float l = fabsf(sigmoid_f(sgn * up) - sigmoid_f(sgn * lo));
         lik[p * lld + c] = fmaxf(l, lbound);
     }
+    noise_close(ns, nv);   // thread 0 (c = c0 < C) always gets here
 }
 
 // bwd: grid (C, S): block (c, s) takes every S-th 256-pixel slice of channel c, one chain pair per thread and
@@ -357,7 +458,7 @@ __global__ __launch_bounds__(256) void eb_fwd_kernel(int mode, int64_t npix, int
 // and applies the chain rule through softplus / tanh into the torch layout.  Deterministic.
 __global__ __launch_bounds__(256) void eb_bwd_kernel(int mode, int64_t npix, int C, cai_eb_params P,
                                                        const void* __restrict__ x, int xdt, int xld,
-                                                       const float* __restrict__ noise, int nld, float lbound,
+                                                       const cai_noise_src ns, float lbound,
                                                        const float* __restrict__ glik, int glld,
                                                        const void* __restrict__ gq, int gqdt, int gqld,
                                                        void* __restrict__ dx, int dxld, cai_eb_grads G,
@@ -366,6 +467,7 @@ __global__ __launch_bounds__(256) void eb_bwd_kernel(int mode, int64_t npix, int
     __shared__ float red[4][EB_NP];
     __shared__ int s_last;
     const int c = blockIdx.x, S = gridDim.y, sp = blockIdx.y;
+    const NoiseView nv = noise_open(ns);   // BUF or REPLAY
     eb_fill_tables<1>(c, 1, C, P, tab);
     __syncthreads();
     const float* t = tab;
@@ -374,7 +476,7 @@ __global__ __launch_bounds__(256) void eb_bwd_kernel(int mode, int64_t npix, int
     for (int k = 0; k < EB_NP; ++k) g[k] = 0.f;
     for (int64_t p = (int64_t)sp * 256 + threadIdx.x; p < npix; p += (int64_t)S * 256) {
         const float xv = ld_any(x, xdt, p * xld + c);
-        const float v = (mode == CAI_Q_NOISE) ? xv + noise[p * nld + c] : rintf(xv - t[EB_MED]) + t[EB_MED];
+        const float v = (mode == CAI_Q_NOISE) ? xv + nv.at(p, c, C) : rintf(xv - t[EB_MED]) + t[EB_MED];
         EbTrace tl, tu;
         const float lo = eb_chain(v - 0.5f, t, &tl);
         const float up = eb_chain(v + 0.5f, t, &tu);
@@ -601,34 +703,6 @@ __global__ void cast_kernel(const void* __restrict__ x, int xdt, void* __restric
         st_any(y, ydt, i, ld_any(x, xdt, i));
 }
 
-// ---------------------------------------------------------------------------
-// training noise U(-1/2, 1/2) (entropy_models.py:170 `empty_like(x).uniform_(-0.5, 0.5)`) generated on the
-// device from a counter in device memory, so a captured graph draws fresh noise on every replay without
-// torch's generator (whose replays re-seed through extra fill launches).  Philox4x32-10 (Salmon et al.,
-// SC'11): key = the 64-bit seed, counter = (element quad, draw index); the draw index lives in
-// state[1] and is advanced by the last block of each launch to finish (state[2] is its arrival ticket,
-// left at 0), so every launch -- and every replay -- uses a new counter range.  24-bit mantissas:
-// u = (r >> 8) * 2^-24 - 1/2 in [-1/2, 1/2).
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void philox_round(unsigned (&c)[4], const unsigned (&k)[2]) {
-    const unsigned long long p0 = (unsigned long long)0xD2511F53u * c[0];
-    const unsigned long long p1 = (unsigned long long)0xCD9E8D57u * c[2];
-    const unsigned hi0 = (unsigned)(p0 >> 32), lo0 = (unsigned)p0, hi1 = (unsigned)(p1 >> 32), lo1 = (unsigned)p1;
-    c[0] = hi1 ^ c[1] ^ k[0];
-    c[1] = lo1;
-    c[2] = hi0 ^ c[3] ^ k[1];
-    c[3] = lo0;
-}
-__device__ __forceinline__ void philox4x32_10(unsigned (&c)[4], unsigned k0, unsigned k1) {
-    unsigned k[2] = {k0, k1};
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        philox_round(c, k);
-        k[0] += 0x9E3779B9u;
-        k[1] += 0xBB67AE85u;
-    }
-}
-
 __global__ __launch_bounds__(256) void uniform_noise_kernel(float* __restrict__ out, int64_t n,
                                                              unsigned long long* __restrict__ state) {
     const unsigned long long seed = __hip_atomic_load(state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -663,6 +737,40 @@ __global__ __launch_bounds__(256) void uniform_noise_kernel(float* __restrict__ 
     }
 }
 
+// DRAW launches take one arrival per block on the sharded tickets: at most this many blocks (grid-stride)
+static constexpr int kDrawBlocks = 1024;
+
+static inline int ew_grid_noise(int64_t n, const cai_noise_src& ns) {
+    const int g = ew_grid(n);
+    return ns.kind == CAI_NOISE_DRAW ? std::min(g, kDrawBlocks) : g;
+}
+
+// the kernels' copy of the noise operand (kind -1: invalid, the error is set); modes other than NOISE get an
+// empty BUF operand the kernels never read
+static cai_noise_src noise_arg(int mode, const cai_noise_src* n, int C, bool may_draw, const char* who) {
+    cai_noise_src s{CAI_NOISE_BUF, 0, nullptr, nullptr, nullptr};
+    if (mode != CAI_Q_NOISE) return s;
+    bool ok = n != nullptr;
+    if (ok) {
+        switch (n->kind) {
+            case CAI_NOISE_BUF: ok = n->buf && n->ld >= C; break;
+            case CAI_NOISE_DRAW:
+                ok = may_draw && n->state && n->slot && (reinterpret_cast<uintptr_t>(n->state) & 7) == 0 &&
+                     (reinterpret_cast<uintptr_t>(n->slot) & 7) == 0;
+                break;
+            case CAI_NOISE_REPLAY: ok = n->slot && (reinterpret_cast<uintptr_t>(n->slot) & 7) == 0; break;
+            default: ok = false;
+        }
+    }
+    if (!ok) {
+        set_error("%s: noise mode needs a valid noise operand (BUF with ld >= C, DRAW%s, REPLAY)", who,
+                  may_draw ? "" : " not allowed here");
+        s.kind = -1;
+        return s;
+    }
+    return *n;
+}
+
 }  // namespace cai
 
 using namespace cai;
@@ -683,63 +791,71 @@ int cai_uniform_noise(float* out, int64_t n, unsigned long long* state, void* st
 }
 
 int cai_quantize(int mode, int64_t npix, int32_t C, const void* x, int x_dtype, int32_t x_ld, const float* means,
-                 int32_t means_ld, int32_t means_per_channel, const float* noise, int32_t noise_ld, void* out,
+                 int32_t means_ld, int32_t means_per_channel, const cai_noise_src* noise, void* out,
                  int out_dtype, int32_t out_ld, void* stream) {
     CAI_CHECK_ARG(mode == CAI_Q_NOISE || mode == CAI_Q_DEQUANTIZE || mode == CAI_Q_SYMBOLS,
                   "quantize: invalid mode %d", mode);
     CAI_CHECK_ARG(C > 0 && npix >= 0 && x_ld >= C && out_ld >= C, "quantize: bad shape");
-    CAI_CHECK_ARG(mode != CAI_Q_NOISE || noise, "quantize: noise mode needs a noise buffer");
+    const cai_noise_src ns = noise_arg(mode, noise, C, true, "quantize");
+    if (ns.kind < 0) return CAI_EINVAL;
     const int64_t n = npix * C;
     if (n == 0) return CAI_OK;
-    hipLaunchKernelGGL(quantize_kernel, dim3(ew_grid(n)), dim3(256), 0, as_stream(stream), mode, n, C, x, x_dtype,
-                       x_ld, means, means_ld, means_per_channel, noise, noise_ld, out, out_dtype, out_ld);
+    hipLaunchKernelGGL(quantize_kernel, dim3(ew_grid_noise(n, ns)), dim3(256), 0, as_stream(stream), mode, n, C, x,
+                       x_dtype, x_ld, means, means_ld, means_per_channel, ns, out, out_dtype, out_ld);
     CAI_LAUNCH_CHECK("quantize");
     return CAI_OK;
 }
 
 int cai_gc_fwd(int mode, int64_t npix, int32_t C, const void* x, int x_dtype, int32_t x_ld, const void* scales,
-               int32_t s_ld, const void* means, int32_t m_ld, int sm_dtype, const float* noise, int32_t noise_ld,
+               int32_t s_ld, const void* means, int32_t m_ld, int sm_dtype, const cai_noise_src* noise,
                float scale_bound, float lik_bound, void* q, int q_dtype, int32_t q_ld, float* lik, int32_t lik_ld,
                void* stream) {
     CAI_CHECK_ARG(mode == CAI_Q_NOISE || mode == CAI_Q_DEQUANTIZE, "gc_fwd: invalid mode %d", mode);
-    CAI_CHECK_ARG(mode != CAI_Q_NOISE || noise, "gc_fwd: noise mode needs a noise buffer");
     CAI_CHECK_ARG(C > 0 && npix >= 0 && lik, "gc_fwd: bad arguments");
+    const cai_noise_src ns = noise_arg(mode, noise, C, true, "gc_fwd");
+    if (ns.kind < 0) return CAI_EINVAL;
     const int64_t n = npix * C;
     if (n == 0) return CAI_OK;
-    hipLaunchKernelGGL(gc_fwd_kernel, dim3(ew_grid(n)), dim3(256), 0, as_stream(stream), mode, n, C, x, x_dtype, x_ld,
-                       scales, s_ld, means, m_ld, sm_dtype, noise, noise_ld, scale_bound, lik_bound, q, q_dtype, q_ld,
-                       lik, lik_ld);
+    hipLaunchKernelGGL(gc_fwd_kernel, dim3(ew_grid_noise(n, ns)), dim3(256), 0, as_stream(stream), mode, n, C, x,
+                       x_dtype, x_ld, scales, s_ld, means, m_ld, sm_dtype, ns, scale_bound, lik_bound, q, q_dtype,
+                       q_ld, lik, lik_ld);
     CAI_LAUNCH_CHECK("gc_fwd");
     return CAI_OK;
 }
 
 int cai_gc_bwd(int mode, int64_t npix, int32_t C, const void* x, int x_dtype, int32_t x_ld, const void* scales,
-               int32_t s_ld, const void* means, int32_t m_ld, int sm_dtype, const float* noise, int32_t noise_ld,
+               int32_t s_ld, const void* means, int32_t m_ld, int sm_dtype, const cai_noise_src* noise,
                float scale_bound, float lik_bound, const float* g_lik, int32_t gl_ld, const void* g_q, int gq_dtype,
                int32_t gq_ld, void* dx, int32_t dx_ld, void* dscales, int32_t ds_ld, void* dmeans, int32_t dm_ld,
                void* stream) {
     CAI_CHECK_ARG(mode == CAI_Q_NOISE || mode == CAI_Q_DEQUANTIZE, "gc_bwd: invalid mode %d", mode);
-    CAI_CHECK_ARG(mode != CAI_Q_NOISE || noise, "gc_bwd: noise mode needs a noise buffer");
+    CAI_CHECK_ARG(C > 0 && npix >= 0, "gc_bwd: bad arguments");
+    const cai_noise_src ns = noise_arg(mode, noise, C, false, "gc_bwd");
+    if (ns.kind < 0) return CAI_EINVAL;
     const int64_t n = npix * C;
     if (n == 0) return CAI_OK;
     hipLaunchKernelGGL(gc_bwd_kernel, dim3(ew_grid(n)), dim3(256), 0, as_stream(stream), mode, n, C, x, x_dtype, x_ld,
-                       scales, s_ld, means, m_ld, sm_dtype, noise, noise_ld, scale_bound, lik_bound, g_lik, gl_ld, g_q,
+                       scales, s_ld, means, m_ld, sm_dtype, ns, scale_bound, lik_bound, g_lik, gl_ld, g_q,
                        gq_dtype, gq_ld, dx, dx_ld, dscales, ds_ld, dmeans, dm_ld);
     CAI_LAUNCH_CHECK("gc_bwd");
     return CAI_OK;
 }
 
 int cai_eb_fwd(int mode, int64_t npix, int32_t C, const cai_eb_params* prm, const void* x, int x_dtype, int32_t x_ld,
-               const float* noise, int32_t noise_ld, float lik_bound, void* q, int q_dtype, int32_t q_ld, float* lik,
+               const cai_noise_src* noise, float lik_bound, void* q, int q_dtype, int32_t q_ld, float* lik,
                int32_t lik_ld, void* stream) {
     CAI_CHECK_ARG(prm, "eb_fwd: null params");
     CAI_CHECK_ARG(mode == CAI_Q_NOISE || mode == CAI_Q_DEQUANTIZE, "eb_fwd: invalid mode %d", mode);
-    CAI_CHECK_ARG(mode != CAI_Q_NOISE || noise, "eb_fwd: noise mode needs a noise buffer");
+    CAI_CHECK_ARG(C > 0 && npix >= 0 && lik, "eb_fwd: bad arguments");
+    const cai_noise_src ns = noise_arg(mode, noise, C, true, "eb_fwd");
+    if (ns.kind < 0) return CAI_EINVAL;
     if (npix * C == 0) return CAI_OK;
+    const int gx = (C + 31) / 32;
     int64_t gy = (npix + 7) / 8;   // one pixel row per thread and pass
     if (gy > 1024) gy = 1024;
-    hipLaunchKernelGGL(eb_fwd_kernel, dim3((C + 31) / 32, (unsigned)gy), dim3(256), 0, as_stream(stream), mode, npix, C,
-                       *prm, x, x_dtype, x_ld, noise, noise_ld, lik_bound, q, q_dtype, q_ld, lik, lik_ld);
+    if (ns.kind == CAI_NOISE_DRAW) gy = std::max<int64_t>(1, std::min<int64_t>(gy, kDrawBlocks / gx));
+    hipLaunchKernelGGL(eb_fwd_kernel, dim3(gx, (unsigned)gy), dim3(256), 0, as_stream(stream), mode, npix, C,
+                       *prm, x, x_dtype, x_ld, ns, lik_bound, q, q_dtype, q_ld, lik, lik_ld);
     CAI_LAUNCH_CHECK("eb_fwd");
     return CAI_OK;
 }
@@ -758,11 +874,14 @@ size_t cai_eb_scratch_bytes(int64_t npix, int32_t C) {
 }
 
 int cai_eb_bwd(int mode, int64_t npix, int32_t C, const cai_eb_params* prm, const void* x, int x_dtype, int32_t x_ld,
-               const float* noise, int32_t noise_ld, float lik_bound, const float* g_lik, int32_t gl_ld,
+               const cai_noise_src* noise, float lik_bound, const float* g_lik, int32_t gl_ld,
                const void* g_q, int gq_dtype, int32_t gq_ld, void* dx, int32_t dx_ld, const cai_eb_grads* grads,
                float* scratch, size_t scratch_bytes, uint32_t* tickets, void* stream) {
     CAI_CHECK_ARG(prm && grads, "eb_bwd: null params/grads");
     CAI_CHECK_ARG(mode == CAI_Q_NOISE || mode == CAI_Q_DEQUANTIZE, "eb_bwd: invalid mode %d", mode);
+    CAI_CHECK_ARG(C >= 0 && npix >= 0, "eb_bwd: bad arguments");
+    const cai_noise_src ns = noise_arg(mode, noise, C > 0 ? C : 1, false, "eb_bwd");
+    if (ns.kind < 0) return CAI_EINVAL;
     for (int i = 0; i < 5; ++i) CAI_CHECK_ARG(grads->matrix[i] && grads->bias[i], "eb_bwd: null grad");
     for (int i = 0; i < 4; ++i) CAI_CHECK_ARG(grads->factor[i], "eb_bwd: null grad");
     if (C == 0) return CAI_OK;
@@ -770,7 +889,7 @@ int cai_eb_bwd(int mode, int64_t npix, int32_t C, const cai_eb_params* prm, cons
     const bool split = scratch && tickets && scratch_bytes >= cai_eb_scratch_bytes(npix, C);
     const int S = split ? eb_bwd_splits(npix) : 1;
     hipLaunchKernelGGL(eb_bwd_kernel, dim3(C, S), dim3(256), 0, as_stream(stream), mode, npix, C, *prm, x,
-                       x_dtype, x_ld, noise, noise_ld, lik_bound, g_lik, gl_ld, g_q, gq_dtype, gq_ld, dx, dx_ld,
+                       x_dtype, x_ld, ns, lik_bound, g_lik, gl_ld, g_q, gq_dtype, gq_ld, dx, dx_ld,
                        *grads, scratch, tickets);
     CAI_LAUNCH_CHECK("eb_bwd");
     return CAI_OK;

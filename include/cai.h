@@ -375,14 +375,37 @@ int cai_gdn_backward_deferred(int dtype, const void* x, int32_t x_ld, const void
  * torch.empty_like(x).uniform_(-0.5, 0.5) (entropy_models.py:170) -- same distribution, its own stream. */
 int cai_uniform_noise(float* out, int64_t n, unsigned long long* state, void* stream);
 
-/* quantize: NOISE  out = x + noise  (noise required, fp32 ld noise_ld)
+/* Noise operand of the NOISE-mode entropy kernels (quantize, gc_fwd/bwd, eb_fwd/bwd):
+ *   BUF     element (p, c) = buf[p*ld + c] (fp32), a draw the caller made (cai_uniform_noise, or injected);
+ *   DRAW    the kernel draws it itself: element (p, c) = element p*C + c of what cai_uniform_noise would write
+ *           into a dense [npix, C] buffer at the generator's current draw index; the kernel records
+ *           {seed, draw index} in slot[0..1] and advances the index once (its last block to arrive, on
+ *           per-XCD sharded tickets in state[CAI_NOISE_SHARD0 + 16 k], k < 8) -- no noise buffer, no draw launch;
+ *   REPLAY  the draw recorded in slot by an earlier DRAW launch (the backward, or a second consumer).
+ * state: the generator's CAI_NOISE_STATE_WORDS uint64 (cai_uniform_noise's state, extended by the shards),
+ * zero past state[1] before the first call; slot: 2 uint64 in device memory.  DRAW launches that share a
+ * state must be ordered (one stream), as cai_uniform_noise calls must. */
+#define CAI_NOISE_BUF 0
+#define CAI_NOISE_DRAW 1
+#define CAI_NOISE_REPLAY 2
+#define CAI_NOISE_SHARD0 16
+#define CAI_NOISE_STATE_WORDS 144
+typedef struct cai_noise_src {
+    int32_t kind;
+    int32_t ld;                   /* BUF: row stride of buf (>= C) */
+    const float* buf;             /* BUF */
+    unsigned long long* state;    /* DRAW */
+    unsigned long long* slot;     /* DRAW (written) / REPLAY (read) */
+} cai_noise_src;
+
+/* quantize: NOISE  out = x + noise  (noise required)
  *           DEQUANTIZE out = rint(x - means) + means  (means nullable)
  *           SYMBOLS    out(int32) = (int)rint(x - means)
  * x_dtype / out_dtype in {CAI_F32, CAI_BF16} (out int32 for SYMBOLS). */
 int cai_quantize(int mode, int64_t npix, int32_t C,
                  const void* x, int x_dtype, int32_t x_ld,
                  const float* means, int32_t means_ld, int32_t means_per_channel,
-                 const float* noise, int32_t noise_ld,
+                 const cai_noise_src* noise,
                  void* out, int out_dtype, int32_t out_ld, void* stream);
 
 /* GaussianConditional forward: q = quantize(x) (NOISE or DEQUANTIZE),
@@ -391,7 +414,7 @@ int cai_quantize(int mode, int64_t npix, int32_t C,
 int cai_gc_fwd(int mode, int64_t npix, int32_t C,
                const void* x, int x_dtype, int32_t x_ld,
                const void* scales, int32_t s_ld, const void* means, int32_t m_ld, int sm_dtype,
-               const float* noise, int32_t noise_ld,
+               const cai_noise_src* noise,
                float scale_bound, float lik_bound,
                void* q, int q_dtype, int32_t q_ld, float* lik, int32_t lik_ld, void* stream);
 /* backward: inputs the gradients wrt lik (fp32, nullable) and wrt q (nullable),
@@ -399,7 +422,7 @@ int cai_gc_fwd(int mode, int64_t npix, int32_t C,
 int cai_gc_bwd(int mode, int64_t npix, int32_t C,
                const void* x, int x_dtype, int32_t x_ld,
                const void* scales, int32_t s_ld, const void* means, int32_t m_ld, int sm_dtype,
-               const float* noise, int32_t noise_ld,
+               const cai_noise_src* noise,
                float scale_bound, float lik_bound,
                const float* g_lik, int32_t gl_ld, const void* g_q, int gq_dtype, int32_t gq_ld,
                void* dx, int32_t dx_ld, void* dscales, int32_t ds_ld, void* dmeans, int32_t dm_ld,
@@ -424,7 +447,7 @@ typedef struct cai_eb_grads {
 
 int cai_eb_fwd(int mode, int64_t npix, int32_t C, const cai_eb_params* prm,
                const void* x, int x_dtype, int32_t x_ld,
-               const float* noise, int32_t noise_ld, float lik_bound,
+               const cai_noise_src* noise, float lik_bound,
                void* q, int q_dtype, int32_t q_ld, float* lik, int32_t lik_ld, void* stream);
 /* Scratch of the split backward / the multi-block aux loss (fp32 partial sums).  Their hand-offs also take
  * caller-owned uint32 tickets -- C for cai_eb_bwd, 1 for cai_eb_aux_loss -- zero before the first call; every
@@ -436,7 +459,7 @@ size_t cai_eb_scratch_bytes(int64_t npix, int32_t C);
  * NULL (or scratch_bytes short) one block per channel. */
 int cai_eb_bwd(int mode, int64_t npix, int32_t C, const cai_eb_params* prm,
                const void* x, int x_dtype, int32_t x_ld,
-               const float* noise, int32_t noise_ld, float lik_bound,
+               const cai_noise_src* noise, float lik_bound,
                const float* g_lik, int32_t gl_ld, const void* g_q, int gq_dtype, int32_t gq_ld,
                void* dx, int32_t dx_ld, const cai_eb_grads* grads,
                float* scratch, size_t scratch_bytes, uint32_t* tickets, void* stream);
