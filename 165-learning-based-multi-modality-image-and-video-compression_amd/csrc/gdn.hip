@@ -29,6 +29,20 @@ namespace cai {
 
 int colsum_any(int dtype, const void* g, int64_t npix, int C, int ld, float* out, int accumulate, void* ws, size_t wsb,
                hipStream_t st);
+// lane-local kernels (gdn_lane.hip)
+bool gdn_lane_fwd_ok(int C, int64_t npix, int x_ld, int y_ld);
+void launch_gdn_fwd_lane(const void* x, int x_ld, int64_t npix, int C, const void* g, const float* b, int inv, void* y,
+                         int y_ld, hipStream_t st);
+bool gdn_lane_bwd_ok(int C, int64_t npix, int x_ld, int dy_ld, int dx_ld);
+int gdn_lane_bwd_blocks(int64_t npix);
+void launch_gdn_bwd_lane(const void* x, int x_ld, const void* dy, int dy_ld, int64_t npix, int C, const void* gop,
+                         const float* beta, int inv, void* dx, int dx_ld, float* part, int nblk, hipStream_t st);
+// A/B knob: CAI_GDN_LANE=0 keeps the LDS-tile kernels (gdn_fwd_kernel, gdn_bwd_fused_kernel); read at every
+// call (host side, a few hundred ns) so the parity tests can compare both kernels in one process
+static bool gdn_lane_on() {
+    const char* e = getenv("CAI_GDN_LANE");
+    return !(e && *e == '0');
+}
 size_t colsum_ws_bytes(int64_t npix, int C);
 
 __device__ __forceinline__ s16x4 ds_tr16(const char* base, int byte_off) {
@@ -1050,6 +1064,11 @@ int cai_gdn_fwd(int dtype, const void* x, int32_t x_ld, int64_t npix, int32_t C,
     CAI_CHECK_ARG(x && gamma_op && beta && y && x_ld >= C && y_ld >= C, "gdn_fwd: bad arguments");
     CAI_CHECK_ARG(x_ld % 8 == 0 && y_ld % 8 == 0, "gdn_fwd: ld must be a multiple of 8");
     if (npix == 0) return CAI_OK;
+    if (dtype == CAI_BF16 && gdn_lane_on() && gdn_lane_fwd_ok(C, npix, x_ld, y_ld)) {
+        launch_gdn_fwd_lane(x, x_ld, npix, C, gamma_op, beta, inverse, y, y_ld, as_stream(stream));
+        CAI_LAUNCH_CHECK("gdn_fwd");
+        return CAI_OK;
+    }
     GDN_DISPATCH(launch_gdn_fwd, x, x_ld, npix, gamma_op, beta, inverse, y, y_ld, as_stream(stream));
     CAI_LAUNCH_CHECK("gdn_fwd");
     return CAI_OK;
@@ -1144,7 +1163,9 @@ static int run_gdn_backward(int dtype, const void* x, int32_t x_ld, const void* 
         return cai_gdn_param_grad(dtype, x, x_ld, ws, npix, C, beta_raw, gamma_raw, beta_min, reparam_offset,
                                   dbeta_raw, dgamma_raw, accumulate, ws + ub, ws_bytes - ub, stream);
     }
-    const int nblk = fused_blocks(npix);
+    const bool lane = gdn_lane_on() && gdn_lane_bwd_ok(C, npix, x_ld, dy_ld, dx_ld);
+    // (the lane kernel's block count never exceeds fused_blocks: the workspace size holds for both)
+    const int nblk = lane ? gdn_lane_bwd_blocks(npix) : fused_blocks(npix);
     float* part = reinterpret_cast<float*>(workspace);
     auto launch = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(nblk), dim3(FNT), 0, st, reinterpret_cast<const bf16*>(x), x_ld,
@@ -1156,6 +1177,9 @@ static int run_gdn_backward(int dtype, const void* x, int32_t x_ld, const void* 
                            reinterpret_cast<const bf16*>(dy), dy_ld, npix, reinterpret_cast<const bf16*>(gamma_op),
                            beta, reinterpret_cast<bf16*>(dx), dx_ld, part);
     };
+    if (lane) {
+        launch_gdn_bwd_lane(x, x_ld, dy, dy_ld, npix, C, gamma_op, beta, inverse, dx, dx_ld, part, nblk, st);
+    } else
 #ifdef CAI_GDN_WIDE128
     if (C == 128) {
         inverse ? launch_wide(gdn_bwd_wide_kernel<128, true>, WideGeo<128>::NT)

@@ -1,7 +1,7 @@
 """Print the kernel sequence of one training step from a rocprofv3 kernel trace.
 
 usage: python tools/prof_step.py <run_kernel_trace.csv> [step_index_from_end]
-Steps are delimited by the optimizer kernel (adam_kernel).
+Steps are delimited by the aux optimizer kernel (adam_small_kernel).
 """
 import csv
 import sys
@@ -10,7 +10,7 @@ import sys
 def main():
     rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
     back = int(sys.argv[2]) if len(sys.argv) > 2 else 2
-    ends = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"]]
+    ends = [i for i, r in enumerate(rows) if "adam_small_kernel" in r["Kernel_Name"]]
     a, b = ends[-back - 1] + 1, ends[-back] + 1
     t0 = int(rows[a]["Start_Timestamp"])
     tot = 0
