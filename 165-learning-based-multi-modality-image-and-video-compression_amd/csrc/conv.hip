@@ -3087,7 +3087,20 @@ using CfgG1 = Cfg2<256, 128, 4, 2>;
 using CfgG2 = Cfg2<128, 192, 2, 4>;
 using CfgG3 = Cfg2<256, 64, 4, 2>;
 using CfgG4 = Cfg2<128, 128, 2, 4>;
-enum { CFG_G1 = 10, CFG_G2, CFG_G3, CFG_G4 };
+using CfgG5 = Cfg2<64, 128, 2, 4>;
+using CfgG6 = Cfg2<64, 192, 2, 4>;
+enum { CFG_G1 = 10, CFG_G2, CFG_G3, CFG_G4, CFG_G5, CFG_G6 };
+
+// 64-row tiles for mid-size maps (cheng2020's attention units at 64x64, B = 4: M = 16384): where the 256 / 128-row
+// grid would split K to fill the chip, the 64-row grid reaches >= 128 tiles without a split (no partial slab, no
+// reduce launch).  A/B knob CAI_GLDS_M64=0.
+static bool glds_m64_off() {
+    static const bool off = [] {
+        const char* e = getenv("CAI_GLDS_M64");
+        return e && *e == '0';
+    }();
+    return off;
+}
 
 static int pick_cfg_glds(int C, int nphase, int& BM, int& BN) {
     if (C <= 64) { BM = 256; BN = 64; return CFG_G3; }
@@ -3137,8 +3150,12 @@ static bool small_off() {
 // M <= 512 rows (4x4 latents), or K <= 2048 with either <= 256 blocks or M <= 1024 (h_a[0] k3 192->128 at
 // 16x16: 16.4 vs 22.8 us; h_s[0] 4->8: 9.3 vs 15.5).  At K = 3200 with M >= 1024 the per-wave K loop is
 // latency-bound and the small tiles re-read the weights too often (g_a[6] 48.9 vs 22.6 us): split-K stays.
-static int pick_small(const Plan& P, int dtype, int mmax, int big_ksplit) {
-    if (small_off() || dtype != CAI_BF16 || P.Cin_pad % 32 != 0 || big_ksplit <= 1 || mmax > 8192) return SMALL_NONE;
+// Also taken where the big-tile grid has fewer than 64 blocks and K is too short to split (cheng2020's attention
+// units at 16x16, B = 4: 1x1 96 <-> 192 on 4 blocks of 256 x 128 ran 16-25 us).
+static int pick_small(const Plan& P, int dtype, int mmax, int big_ksplit, int big_blocks) {
+    if (small_off() || dtype != CAI_BF16 || P.Cin_pad % 32 != 0 || (big_ksplit <= 1 && big_blocks >= 64) ||
+        mmax > 8192)
+        return SMALL_NONE;
     int kmax = 0;
     for (int ph = 0; ph < P.nphase; ++ph) kmax = std::max(kmax, P.ntaps[ph] * P.Cin_pad);
     const int cfg = mmax <= 512 ? SMALL_16x32 : (mmax <= 2048 ? SMALL_32x32 : SMALL_32x64);
@@ -3270,6 +3287,15 @@ static ConvLaunch conv_launch(const cai_conv_geom* g, int dtype, int direction, 
         L.mmax = std::max(L.mmax, g->batch * P.OHg[ph] * P.OWg[ph]);
         kmax = std::max(kmax, P.ntaps[ph] * P.Cin_pad);
     }
+    if (L.glds && !glds_m64_off() && (L.cfg == CFG_G1 || L.cfg == CFG_G2)) {
+        const int nt = (P.kout_c + L.BN - 1) / L.BN;
+        const int big = (L.mmax + L.BM - 1) / L.BM * nt * P.nphase;
+        const int m64 = (L.mmax + 63) / 64 * nt * P.nphase;
+        if (big < 256 && m64 >= 128) {
+            L.cfg = L.cfg == CFG_G1 ? CFG_G5 : CFG_G6;
+            L.BM = 64;
+        }
+    }
     L.mtiles = (L.mmax + L.BM - 1) / L.BM;
     L.ntiles = (P.kout_c + L.BN - 1) / L.BN;
     const int tiles = L.mtiles * L.ntiles * P.nphase;
@@ -3280,7 +3306,7 @@ static ConvLaunch conv_launch(const cai_conv_geom* g, int dtype, int direction, 
     const int target = L.glds ? 256 : 512;    // one 512-thread block per CU vs two 256-thread ones
     if (tiles < 256) ks = std::min({(target + tiles - 1) / tiles, std::max(1, nk / 4), 16});
     L.ksplit = capped(std::max(1, ks));
-    L.small = pick_small(P, dtype, L.mmax, L.ksplit);
+    L.small = pick_small(P, dtype, L.mmax, L.ksplit, tiles * L.ksplit);
     if (L.small) {
         static const int bm[] = {0, 16, 32, 32}, bn[] = {0, 32, 32, 64};
         L.BM = bm[L.small];
@@ -3391,6 +3417,8 @@ static void dispatch_conv(const ConvArgs& a, const ConvLaunch& L, hipStream_t st
             case CFG_G2: launch_conv_glds<CfgG2>(a, L, st); return;
             case CFG_G3: launch_conv_glds<CfgG3>(a, L, st); return;
             case CFG_G4: launch_conv_glds<CfgG4>(a, L, st); return;
+            case CFG_G5: launch_conv_glds<CfgG5>(a, L, st); return;
+            case CFG_G6: launch_conv_glds<CfgG6>(a, L, st); return;
             default: break;
         }
     }
@@ -3627,10 +3655,13 @@ static bool small_wgrad_off() {
     }();
     return off;
 }
+// ... and with at most 2^20 weights: wider outputs (cheng2020 q6 at B = 4: 192->384 k5 and 192->768 k3 at 16x16,
+// 192->768 k3 at 4x4) measured slower than the pixel-split kernel + reduce (134 / 71 / 91 vs 60 / 56 / 54 us,
+// profiles/r03_cheng2020_dispatch_ab.log)
 static bool small_wgrad_ok(const cai_conv_geom* g, int dtype) {
     const WgradPlan W = make_wgrad_plan(g, dtype, true);
     return !small_wgrad_off() && dtype == CAI_BF16 && W.M <= SW_NW * SW_STEPS * 32 && W.Ng % 64 == 0 &&
-           W.Cq_pad % 64 == 0;
+           W.Cq_pad % 64 == 0 && (int64_t)W.Ng * W.ncols <= (1 << 20);
 }
 
 
@@ -3843,6 +3874,8 @@ const char* cai_conv_kernel_name(const cai_conv_geom* g, int dtype, int directio
         case CFG_G2: return "conv_glds_kernel<128x192>";
         case CFG_G3: return "conv_glds_kernel<256x64>";
         case CFG_G4: return "conv_glds_kernel<128x128>";
+        case CFG_G5: return "conv_glds_kernel<64x128>";
+        case CFG_G6: return "conv_glds_kernel<64x192>";
         case CFG_S: return dtype == CAI_BF16 ? "conv_gemm_kernel<bf16,256x16>" : "conv_gemm_kernel<float,256x16>";
         case CFG_M: return dtype == CAI_BF16 ? "conv_gemm_kernel<bf16,128x64>" : "conv_gemm_kernel<float,128x64>";
         case CFG_W: return dtype == CAI_BF16 ? "conv_gemm_kernel<bf16,64x192>" : "conv_gemm_kernel<float,64x192>";

@@ -110,6 +110,11 @@ CONV_CASES = [
     # straddling two taps, the last tile past K, 1x1 and 3x3, both directions, the s^2-phase direction
     ("conv", 4, 96, 96, 64, 64, 3, 1),
     ("conv", 4, 96, 192, 32, 32, 1, 1),
+    # 64-row LDS-DMA tiles (conv_glds_kernel<64x128 / 64x192>: mid-size maps whose 256 / 128-row grid would split
+    # K): cheng2020 attention-unit 1x1 convs at 64x64, B = 4, both directions
+    ("conv", 4, 96, 192, 64, 64, 1, 1),
+    ("conv", 4, 192, 96, 64, 64, 1, 1),
+    ("conv", 2, 192, 192, 64, 80, 3, 1),
     ("conv", 8, 160, 128, 32, 32, 3, 1),
     ("deconv", 4, 96, 64, 32, 32, 5, 2),
     # Spatial_aligner patch embedding / recovery (master.py:708-724): kernel = stride = 2, no padding
