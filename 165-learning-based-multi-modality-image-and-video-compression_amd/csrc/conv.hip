@@ -1170,17 +1170,22 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvArgs a, int
 #endif
 
 
-template <int NA, int NC, int BN_ = 128>
+// HALF: the 256-thread form (4 waves, 8 x 16 tiles, two workgroups per CU): the two waves that share a SIMD
+// belong to different workgroups, so one's barriers, footprint prologue and epilogue overlap the other's MFMAs
+// (the 512-thread form puts both waves of a SIMD behind the same barrier).
+template <int NA, int NC, int BN_ = 128, bool HALF = false>
 struct HaloPhCfg {
-    static constexpr int TH = 8, TW = 32, BM = TH * TW, BN = BN_, WM = 4, WN = 2, CK = 64;
-    // 16-byte weight DMAs per lane per step: 512 lanes stage 128 rows x 64 bytes; BN = 192 issues a second
-    // round (rows 128..255, those past the tile reading the zero page into unread cells)
-    static constexpr int DPS = BN > 128 ? 2 : 1;
+    static constexpr int TH = 8, TW = HALF ? 16 : 32, BM = TH * TW, BN = BN_, WM = 4, WN = HALF ? 1 : 2, CK = 64;
+    static constexpr int NT = HALF ? 256 : 512;
+    // 16-byte weight DMAs per lane per step: NT lanes stage NT / 4 rows x 64 bytes per round; DPS rounds cover
+    // the BN rows (BN = 192 on 512 lanes: rows 128..255 of the second round past the tile read the zero page
+    // into unread cells)
+    static constexpr int DPS = (4 * BN + NT - 1) / NT;
     static constexpr int PH = TH + NA - 1, PW = TW + NC - 1;
     static constexpr int NPOS = PH * PW;
     static constexpr int PLANE = (NPOS + 15) / 16 * 16;       // = 0 (mod 16): conflict-free fragment reads
     static constexpr int PATCH = 8 * PLANE * 16;
-    static constexpr int NPI = (8 * NPOS + 511) / 512;
+    static constexpr int NPI = (8 * NPOS + NT - 1) / NT;
     static constexpr int NTAP = NA * NC, NST = 2 * NTAP;       // steps per chunk: (half, tap)
 #ifndef CAI_HALO_PH_NSTB6
 #define CAI_HALO_PH_NSTB6 0
@@ -1188,7 +1193,7 @@ struct HaloPhCfg {
     // NST % NSTB == 0: a step's stage is t % NSTB.  A 6-stage ring (CAI_HALO_PH_NSTB6=1) measured slower on
     // MI355X (C2 8180 vs 8430 patches/s; the big launch 91.6 vs 88 us): the latency is not in the ring
     static constexpr int NSTB = (CAI_HALO_PH_NSTB6 && NST % 6 == 0) ? 6 : (NST % 3 == 0 ? 3 : 2);
-    static constexpr int BSTAGE = DPS * 128 * 32 * 2;
+    static constexpr int BSTAGE = DPS * NT * 16;
     // BN > 128: register-direct epilogue only (no LDS staging buffer), see conv_epilogue_rows_t
     static constexpr int EPI = BN > 128 ? 0 : BM * (BN + 4) * 4;
     static constexpr int BYTES = (PATCH + NSTB * BSTAGE > EPI) ? PATCH + NSTB * BSTAGE : EPI;
@@ -1199,14 +1204,14 @@ struct HaloPhCfg {
 // NA-1 / NC-1 before dy0 / dx0).  GATHER = true: a stride-1 gather convolution (Conv2d k3 s1 forward): tap
 // (ty, tx) = kernel (kh, kw) reads cell (ty, tx) from the origin dy0 = -pad.  n0: the tile's first output
 // channel (grid y).
-template <int NA, int NC, int BN_ = 128, bool GATHER = false>
+template <int NA, int NC, int BN_ = 128, bool GATHER = false, bool HALF = false>
 __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* smem, int ph, int split, int bid,
                                                      int tiles_x, int tiles_y, int n0 = 0) {
-    using H = HaloPhCfg<NA, NC, BN_>;
-    constexpr int BM = H::BM, BN = H::BN, WM = H::WM, WN = H::WN, DPS = H::DPS;
+    using H = HaloPhCfg<NA, NC, BN_, HALF>;
+    constexpr int BM = H::BM, BN = H::BN, WM = H::WM, WN = H::WN, DPS = H::DPS, NT = H::NT;
     constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
     constexpr int NPI = H::NPI, NTAP = H::NTAP, NST = H::NST, NSTB = H::NSTB;
-    static_assert(WM * WN == 8 && WTM == 2 * H::TW && H::BYTES <= 160 * 1024, "halo phase tile");
+    static_assert(WM * WN == NT / 64 && WTM == 2 * H::TW && H::BYTES <= 160 * 1024, "halo phase tile");
     char* const patch = smem;
     char* const bring = smem + H::PATCH;
 
@@ -1232,7 +1237,7 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
     auto load_cell = [&](int ci, int i) {
         const bool real = ci < nc;
         const int cc = c0 + ci;
-        const int q8 = tid + 512 * i, g = (q8 >> 3) & 7, q = ((q8 >> 6) << 3) | (q8 & 7);
+        const int q8 = tid + NT * i, g = (q8 >> 3) & 7, q = ((q8 >> 6) << 3) | (q8 & 7);
         const int pr = q / H::PW, pc = q - (q / H::PW) * H::PW;
         const int iy = iyb + pr, ix = ixb + pc;
         const bool in = real && q < H::NPOS && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW;
@@ -1251,7 +1256,7 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
     auto store_patch = [&]() {
 #pragma unroll
         for (int i = 0; i < NPI; ++i) {
-            const int q8 = tid + 512 * i, g = (q8 >> 3) & 7, q = ((q8 >> 6) << 3) | (q8 & 7);
+            const int q8 = tid + NT * i, g = (q8 >> 3) & 7, q = ((q8 >> 6) << 3) | (q8 & 7);
             if (q < H::NPOS) *reinterpret_cast<u32x4*>(patch + (g * H::PLANE + q) * 16) = pr_[i];
         }
     };
@@ -1261,8 +1266,8 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
     const char* Wrow = n0 + bn_ < a.Npad
                            ? reinterpret_cast<const char*>(a.w) + (P.w_off + (int64_t)(n0 + bn_) * a.Kp) * 2 + bs_ * 16
                            : nullptr;
-    const char* Wrow2 = (DPS == 2 && n0 + 128 + bn_ < a.Npad)
-                            ? reinterpret_cast<const char*>(a.w) + (P.w_off + (int64_t)(n0 + 128 + bn_) * a.Kp) * 2 +
+    const char* Wrow2 = (DPS == 2 && n0 + NT / 4 + bn_ < a.Npad)
+                            ? reinterpret_cast<const char*>(a.w) + (P.w_off + (int64_t)(n0 + NT / 4 + bn_) * a.Kp) * 2 +
                                   bs_ * 16
                             : nullptr;
     auto issue_b = [&](int ci, int t) {    // step t = (half t / NTAP, tap t % NTAP) of chunk ci into stage t % NSTB
@@ -1272,7 +1277,7 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
         glds16_asm(src, bring + (t % NSTB) * H::BSTAGE + wid * 1024);
         if constexpr (DPS == 2) {
             const void* src2 = (Wrow2 && ci < nc) ? (const void*)(Wrow2 + koff) : (const void*)cai_zero_page;
-            glds16_asm(src2, bring + (t % NSTB) * H::BSTAGE + 8192 + wid * 1024);
+            glds16_asm(src2, bring + (t % NSTB) * H::BSTAGE + NT * 16 + wid * 1024);
         }
     };
 
@@ -1369,11 +1374,11 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
         return (oy < P.OHg && ox < P.OWg) ? b * plane + oy * P.OWg + ox : -1;
     };
     if (CAI_HALO_PH_T || BN > 128)
-        conv_epilogue_rows_t<bf16, BM, BN, WM, WN, 512, decltype(rowm), (BN > 128)>(
+        conv_epilogue_rows_t<bf16, BM, BN, WM, WN, NT, decltype(rowm), (BN > 128)>(
             a, P, plane, n0, reinterpret_cast<float*>(smem), acc, rowm, ph * a.ksplit + split);
     else
-        conv_epilogue_rows<bf16, BM, BN, WM, WN, 512>(a, P, plane, n0, reinterpret_cast<float*>(smem), acc, rowm,
-                                                      ph * a.ksplit + split);
+        conv_epilogue_rows<bf16, BM, BN, WM, WN, NT>(a, P, plane, n0, reinterpret_cast<float*>(smem), acc, rowm,
+                                                     ph * a.ksplit + split);
 }
 
 // grid: x = 4 x the output tiles of one phase, z = split (the split-K slab index of the epilogue).  Block
@@ -1609,6 +1614,29 @@ __global__ __launch_bounds__(512, 1) void conv_halo_phase_kernel(const ConvArgs 
     }
 }
 
+// The 256-thread form of the 128-channel phase kernel (HaloPhCfg HALF: 8 x 16 tiles, two workgroups per CU).
+// grid: x = 4 x the output tiles of one phase (phase-major, tiles XCD-remapped within a phase), z = split.
+__global__ __launch_bounds__(256, 2) void conv_halo_phase_half_kernel(const ConvArgs a, int tiles_x, int tiles_y) {
+    constexpr int BYTES = HaloPhCfg<3, 3, 128, true>::BYTES > HaloPhCfg<2, 2, 128, true>::BYTES
+                              ? HaloPhCfg<3, 3, 128, true>::BYTES
+                              : HaloPhCfg<2, 2, 128, true>::BYTES;
+    static_assert(BYTES >= HaloPhCfg<3, 2, 128, true>::BYTES && BYTES >= HaloPhCfg<2, 3, 128, true>::BYTES &&
+                      2 * BYTES <= 160 * 1024,
+                  "halo phase (half) LDS");
+    __shared__ __attribute__((aligned(16))) char smem[BYTES];
+    const int nt = gridDim.x >> 2;
+    const int ph = blockIdx.x / nt;
+    const int t = blockIdx.x - ph * nt;
+    const int bid = (nt & 7) == 0 ? (t & 7) * (nt >> 3) + (t >> 3) : t;
+    const int split = blockIdx.z;
+    switch (ph) {
+        case 0: conv_halo_phase_body<3, 3, 128, false, true>(a, smem, 0, split, bid, tiles_x, tiles_y); break;
+        case 1: conv_halo_phase_body<3, 2, 128, false, true>(a, smem, 1, split, bid, tiles_x, tiles_y); break;
+        case 2: conv_halo_phase_body<2, 3, 128, false, true>(a, smem, 2, split, bid, tiles_x, tiles_y); break;
+        default: conv_halo_phase_body<2, 2, 128, false, true>(a, smem, 3, split, bid, tiles_x, tiles_y); break;
+    }
+}
+
 // Halo-staged stride-1 k3 p1 convolution (the 3x3 convs of cheng2020's residual / attention blocks and
 // sub-pixel convs, conv3x3 layers/layers.py:38-49 / 86-91): the phase body with one phase of 3x3 taps.
 // GATHER: Conv2d forward (tap = kernel (kh, kw), footprint origin -pad); otherwise the input gradient in the
@@ -1828,11 +1856,13 @@ __device__ __forceinline__ void pack_row(const PackArgs& a, int n, float* S, int
     const int KK = a.k * a.k;
     const int nsrc = a.Creal * KK;
     if (n < a.Nreal) {
-        // four independent loads in flight per thread
-        for (int i0 = threadIdx.x; i0 < nsrc; i0 += 4 * blockDim.x) {
-            float v[4];
+        // PACK_LD independent loads in flight per thread (a 128 x 25-tap row is 3200 floats: one round of 16 per
+        // thread instead of four dependent rounds of 4)
+        constexpr int PACK_LD = 16;
+        for (int i0 = threadIdx.x; i0 < nsrc; i0 += PACK_LD * blockDim.x) {
+            float v[PACK_LD];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < PACK_LD; ++j) {
                 const int i = min(i0 + j * (int)blockDim.x, nsrc - 1);
                 const int c = i / KK, tap = i - c * KK;
                 const int64_t src = a.n_is_d0 ? (int64_t)n * a.D1 * KK + i : ((int64_t)c * a.D1 + n) * KK + tap;
@@ -1840,7 +1870,7 @@ __device__ __forceinline__ void pack_row(const PackArgs& a, int n, float* S, int
                 if (a.mask) v[j] *= a.mask[src];
             }
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < PACK_LD; ++j)
                 if (i0 + j * (int)blockDim.x < nsrc) S[i0 + j * blockDim.x] = v[j];
         }
     }
@@ -3132,6 +3162,7 @@ struct ConvLaunch {
     int halo, tiles_x, tiles_y;    // halo: kernel size of the halo-staged path (0: not taken)
     bool halo_ph;                  // the halo-staged s^2-phase path (k5 s2 p2 transposed direction)
     bool halo_s1;                  // the halo-staged stride-1 k3 path
+    bool ph_half;                  // the halo phase path in its 256-thread form (conv_halo_phase_half_kernel)
     int hbn;                       // output-channel tile of the halo phase / s1 paths (128 / 192)
     int small;                     // conv_small_kernel tile (SMALL_*; 0: not taken)
     size_t ws_bytes;
@@ -3207,6 +3238,17 @@ static bool halo_phase_ok(const cai_conv_geom* g, const Plan& P, bool glds, bool
     return true;
 }
 
+// A/B knob CAI_HALO_PH_HALF=1: the 128-channel halo phase layers on conv_halo_phase_half_kernel.  Measured
+// slower on MI355X (C2 g_s[4] fwd / g_a[2] dgrad 89.0 / 89.4 vs 86.0 / 85.1 us; step -0.1 %,
+// profiles/r03_halo_phase_half_ab.log): separate barriers per SIMD partner do not shorten the step, so it is off.
+static bool halo_ph_half_on() {
+    static const bool on = [] {
+        const char* e = getenv("CAI_HALO_PH_HALF");
+        return e && *e == '1';
+    }();
+    return on;
+}
+
 // the halo-staged stride-1 k3 p1 kernel (both directions), 64-channel input chunks, any output width in
 // BN-channel tiles; A/B knob CAI_HALO_S1_OFF
 static bool halo_s1_off() {
@@ -3251,15 +3293,17 @@ static ConvLaunch conv_launch(const cai_conv_geom* g, int dtype, int direction, 
     if (L.halo_ph || L.halo_s1) {
         const int np = L.halo_ph ? 4 : 1;
         L.hbn = halo_bn(P.kout_c);
-        L.BM = 256;
+        L.ph_half = L.halo_ph && L.hbn == 128 && halo_ph_half_on();
+        L.BM = L.ph_half ? 128 : 256;
         L.BN = L.hbn;
-        L.tiles_x = (P.OWg[0] + 31) / 32;
+        L.tiles_x = L.ph_half ? (P.OWg[0] + 15) / 16 : (P.OWg[0] + 31) / 32;
         L.tiles_y = (P.OHg[0] + 7) / 8;
         for (int ph = 0; ph < np; ++ph) L.mmax = std::max(L.mmax, g->batch * P.OHg[ph] * P.OWg[ph]);
         L.mtiles = g->batch * L.tiles_x * L.tiles_y;
         L.ntiles = (P.kout_c + L.hbn - 1) / L.hbn;
         const int nch = P.Cin_pad / 64, blocks = np * L.mtiles * L.ntiles;
-        L.ksplit = capped(blocks >= 256 ? 1 : std::min(nch, (256 + blocks - 1) / blocks));
+        const int target = L.ph_half ? 512 : 256;   // resident workgroups: two per CU in the 256-thread form
+        L.ksplit = capped(blocks >= target ? 1 : std::min(nch, (target + blocks - 1) / blocks));
         while (L.ksplit > 1 && (L.ksplit - 1) * ((nch + L.ksplit - 1) / L.ksplit) >= nch) --L.ksplit;
         L.ws_ld = L.ntiles * L.hbn;
         L.ws_bytes = L.ksplit > 1 ? (size_t)np * L.ksplit * L.mmax * L.ws_ld * sizeof(float) : 0;
@@ -3361,7 +3405,9 @@ static void launch_conv_halo(const ConvArgs& a, const ConvLaunch& L, hipStream_t
 static void launch_conv_halo_phase(const ConvArgs& a, const ConvLaunch& L, hipStream_t st) {
     const dim3 grid(L.halo_ph ? 4 * L.mtiles : L.mtiles, L.ntiles, a.ksplit);
     if (L.halo_ph) {
-        if (L.hbn == 192)
+        if (L.ph_half)
+            hipLaunchKernelGGL(conv_halo_phase_half_kernel, grid, dim3(256), 0, st, a, L.tiles_x, L.tiles_y);
+        else if (L.hbn == 192)
             hipLaunchKernelGGL(conv_halo_phase_kernel<192>, grid, dim3(512), 0, st, a, L.tiles_x, L.tiles_y);
         else
             hipLaunchKernelGGL(conv_halo_phase_kernel<128>, grid, dim3(512), 0, st, a, L.tiles_x, L.tiles_y);
@@ -3865,7 +3911,9 @@ const char* cai_conv_kernel_name(const cai_conv_geom* g, int dtype, int directio
     }
     const ConvLaunch L = conv_launch(g, dtype, direction, in_abs);
     if (L.halo) return L.halo == 5 ? "conv_halo_kernel<5>" : "conv_halo_kernel<3>";
-    if (L.halo_ph) return L.hbn == 192 ? "conv_halo_phase_kernel<192>" : "conv_halo_phase_kernel";
+    if (L.halo_ph)
+        return L.ph_half ? "conv_halo_phase_half_kernel"
+                         : (L.hbn == 192 ? "conv_halo_phase_kernel<192>" : "conv_halo_phase_kernel");
     if (L.halo_s1) return L.hbn == 192 ? "conv_halo_s1_kernel<192>" : "conv_halo_s1_kernel<128>";
     if (L.small) return L.small == SMALL_16x32 ? "conv_small_kernel<16x32>"
                         : (L.small == SMALL_32x32 ? "conv_small_kernel<32x32>" : "conv_small_kernel<32x64>");

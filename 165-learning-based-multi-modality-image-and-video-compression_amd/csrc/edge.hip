@@ -78,6 +78,13 @@ struct EdgeArgs {
 #endif
 
 __device__ __attribute__((aligned(64))) unsigned edge_zero_page[64];
+// float stride of one superpixel's 16 partial outputs in the d2s cross-wave sum: 17 (not 16) spreads the
+// per-pixel reads of neighbouring threads over the banks (16 put every other pixel on one bank group:
+// SQ_LDS_BANK_CONFLICT 0.60 of the LDS cycles, profiles/r03_pmc_c2_kernels.txt)
+#ifndef CAI_D2S_RS
+#define CAI_D2S_RS 17
+#endif
+constexpr int D2S_RS = CAI_D2S_RS;
 
 typedef const void __attribute__((address_space(1)))* gvoid_ptr;
 typedef void __attribute__((address_space(3)))* lvoid_ptr;
@@ -473,7 +480,7 @@ __device__ __forceinline__ void d2s_row(const EdgeArgs& A, int n, int b0, int a0
 #pragma unroll
         for (int m = 0; m < 4; ++m)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) red[(wave * TB + 16 * m + 4 * g_ + q) * 16 + i16] = acc[SL][m][q];
+            for (int q = 0; q < 4; ++q) red[(wave * TB + 16 * m + 4 * g_ + q) * D2S_RS + i16] = acc[SL][m][q];
         __syncthreads();
         const int64_t W2 = 2 * (int64_t)A.Ws;
         const int xw = min(2 * TB, (int)(W2 - 2 * b0));
@@ -484,7 +491,7 @@ __device__ __forceinline__ void d2s_row(const EdgeArgs& A, int n, int b0, int a0
                 const int c16 = (py * 2 + (x & 1)) * C + co;
                 float s = bC[co];
 #pragma unroll
-                for (int w = 0; w < NW; ++w) s += red[(w * TB + (x >> 1)) * 16 + c16];
+                for (int w = 0; w < NW; ++w) s += red[(w * TB + (x >> 1)) * D2S_RS + c16];
                 if (x < xw) A.out_img[((int64_t)(n * C + co) * (2 * A.Hs) + 2 * a + py) * W2 + 2 * b0 + x] = s;
             }
     }
@@ -495,7 +502,7 @@ __device__ __forceinline__ void d2s_row(const EdgeArgs& A, int n, int b0, int a0
 template <int C, int NW>
 __global__ __launch_bounds__(NW * 64) void edge_d2s_kernel(const EdgeArgs A) {
     constexpr int N = 32 * NW, RS = N * 2 + 16;
-    __shared__ __attribute__((aligned(16))) char smem[TBH * RS + NW * TB * 16 * 4];
+    __shared__ __attribute__((aligned(16))) char smem[TBH * RS + NW * TB * D2S_RS * 4];
     char* Px = smem;
     float* red = reinterpret_cast<float*>(smem + TBH * RS);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;

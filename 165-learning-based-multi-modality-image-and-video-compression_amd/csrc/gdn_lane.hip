@@ -32,6 +32,9 @@ namespace cai {
 
 namespace {
 
+#ifndef CAI_GDN_FWD_NSET
+#define CAI_GDN_FWD_NSET 2   // 16-pixel tiles of loads in flight per wave of the C = 128 forward (A/B: 1 measured 3.7 us slower per C2 step, profiles/r03_gdn_fwd_nset_ab.log)
+#endif
 #ifndef CAI_GDN_PF2
 #define CAI_GDN_PF2 0   // A/B: two steps of x / dy loads in flight per norm wave, dbeta summed by MFMA from bf16 u
 #endif
@@ -103,9 +106,8 @@ __device__ __forceinline__ void afrag_lds(u32x4 (&a)[C / 16][C / 32], const char
 // ---------------------------------------------------------------------------
 // forward: persistent waves, two 16-pixel tiles of loads in flight per wave
 // ---------------------------------------------------------------------------
-// OCC = resident waves per SIMD: 2 keeps one 16-pixel tile of loads in flight per wave (two waves share the SIMD),
-// 1 keeps two
-template <int C, bool INV, int OCC>
+// OCC = resident waves per SIMD; NSET = 16-pixel tiles of loads in flight per wave (register sets)
+template <int C, bool INV, int OCC, int NSET = (OCC == 1 ? 2 : 1)>
 __global__ __launch_bounds__(256, OCC) void gdn_fwd_lane_kernel(const bf16* __restrict__ x, int x_ld,
                                                                              int64_t npix, const bf16* __restrict__ gamma,
                                                                              const float* __restrict__ beta,
@@ -127,7 +129,7 @@ __global__ __launch_bounds__(256, OCC) void gdn_fwd_lane_kernel(const bf16* __re
     const int64_t mine = t < ntiles ? (ntiles - t + nw - 1) / nw : 0;
     u32x4 ra[KB], rb[KB];
     chunk_load<KB>(ra, xr, t * 16 + p, npix, x_ld, g);
-    if constexpr (OCC == 1) chunk_load<KB>(rb, xr, (t + nw) * 16 + p, npix, x_ld, g);
+    if constexpr (NSET == 2) chunk_load<KB>(rb, xr, (t + nw) * 16 + p, npix, x_ld, g);
 
     auto step = [&](u32x4 (&rx)[KB], int64_t cur, int64_t nxt) {
         u32x4 xc[KB], q[KB];
@@ -160,7 +162,7 @@ __global__ __launch_bounds__(256, OCC) void gdn_fwd_lane_kernel(const bf16* __re
         }
         chunk_store<KB>(yv, yr, cur * 16 + p, npix, y_ld, g);
     };
-    if constexpr (OCC == 1) {
+    if constexpr (NSET == 2) {
         for (int64_t it = 0; it < mine / 2; ++it, t += 2 * nw) {
             step(ra, t, t + 2 * nw);
             step(rb, t + nw, t + 3 * nw);
@@ -450,7 +452,7 @@ void launch_gdn_fwd_lane(const void* x, int x_ld, int64_t npix, int C, const voi
     if (C == 64)
         inv ? go(gdn_fwd_lane_kernel<64, true, 2>) : go(gdn_fwd_lane_kernel<64, false, 2>);
     else if (C == 128)
-        inv ? go(gdn_fwd_lane_kernel<128, true, 2>) : go(gdn_fwd_lane_kernel<128, false, 2>);
+        inv ? go(gdn_fwd_lane_kernel<128, true, 2, CAI_GDN_FWD_NSET>) : go(gdn_fwd_lane_kernel<128, false, 2, CAI_GDN_FWD_NSET>);
     else
         inv ? go(gdn_fwd_lane_kernel<192, true, 1>) : go(gdn_fwd_lane_kernel<192, false, 1>);
 }

@@ -55,18 +55,38 @@ __device__ __forceinline__ void wgrad_row_body(const cai_reduce_job& J, int n, f
     const int c4 = ncols >> 2;
     const int64_t slab4 = ((int64_t)Ng * ncols) >> 2;
     const f32x4* src = reinterpret_cast<const f32x4*>(ws) + (int64_t)n * c4;
-    for (int c = threadIdx.x; c < c4; c += 256) {
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-        int sp = 0;
-        for (; sp + 8 <= S; sp += 8) {
-            f32x4 v[8];
+    // RC column chunks per thread at once, RB splits per batch: RC * RB loads in flight per thread (one chunk at
+    // a time left a thread waiting S / 8 + 1 round trips per chunk).  Every chunk still sums its splits in split
+    // order: the same floats as one chunk at a time.
+    constexpr int RC = 4, RB = 4;
+    for (int cb = threadIdx.x; cb < c4; cb += 256 * RC) {
+        bool ok[RC];
+        f32x4 acc[RC];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = src[(int64_t)(sp + j) * slab4 + c];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) acc += v[j];
+        for (int q = 0; q < RC; ++q) {
+            ok[q] = cb + 256 * q < c4;
+            acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
-        for (; sp < S; ++sp) acc += src[(int64_t)sp * slab4 + c];
-        *reinterpret_cast<f32x4*>(row + 4 * c) = acc;
+        int sp = 0;
+        for (; sp + RB <= S; sp += RB) {
+            f32x4 v[RB][RC];
+#pragma unroll
+            for (int j = 0; j < RB; ++j)
+#pragma unroll
+                for (int q = 0; q < RC; ++q)
+                    v[j][q] = ok[q] ? src[(int64_t)(sp + j) * slab4 + cb + 256 * q] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < RB; ++j)
+#pragma unroll
+                for (int q = 0; q < RC; ++q) acc[q] += v[j][q];
+        }
+        for (; sp < S; ++sp)
+#pragma unroll
+            for (int q = 0; q < RC; ++q)
+                if (ok[q]) acc[q] += src[(int64_t)sp * slab4 + cb + 256 * q];
+#pragma unroll
+        for (int q = 0; q < RC; ++q)
+            if (ok[q]) *reinterpret_cast<f32x4*>(row + 4 * (cb + 256 * q)) = acc[q];
     }
     __syncthreads();
     const int kk = k * k, nout = Cq * kk;
