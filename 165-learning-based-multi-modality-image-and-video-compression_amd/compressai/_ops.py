@@ -128,6 +128,7 @@ class _WgradLaunch:
 # immediate path (same kernel).  Off under the per-launch ledger (it replays single calls) and when a weight
 # gradient runs on the side stream.  CAI_DEFER_REDUCE=0 turns it off (A/B).
 _DEFER_REDUCE = os.environ.get("CAI_DEFER_REDUCE", "1") == "1"
+_REDUCE_SPLIT = os.environ.get("CAI_REDUCE_SPLIT", "0") == "1"   # diagnostics: one launch per deferred job
 _JOBS = {}          # device index -> [jobs, their streams, keep-alive tensors]
 
 
@@ -143,8 +144,13 @@ def _flush_jobs(dev):
     for s in {s.cuda_stream: s for s in streams}.values():
         if s.cuda_stream != cur.cuda_stream:
             cur.wait_stream(s)
-    arr = (ReduceJob * len(jobs))(*jobs)
-    lib.cai_reduce_jobs(arr, len(jobs), _VP(cur.cuda_stream))
+    if _REDUCE_SPLIT:   # diagnostics: one launch per job (per-job times in a kernel trace)
+        for j in jobs:
+            one = (ReduceJob * 1)(j)
+            lib.cai_reduce_jobs(one, 1, _VP(cur.cuda_stream))
+    else:
+        arr = (ReduceJob * len(jobs))(*jobs)
+        lib.cai_reduce_jobs(arr, len(jobs), _VP(cur.cuda_stream))
     for t in keep:
         t.record_stream(cur)    # the caching allocator frees them for reuse only after these launches
 

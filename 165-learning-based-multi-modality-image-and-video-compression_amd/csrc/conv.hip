@@ -3204,9 +3204,21 @@ static bool halo_off() {
     }();
     return off;
 }
+// A/B knob CAI_HALO_MIN_TILES (default 0): below this many 8 x 32 output tiles the gather layer goes to the
+// LDS-DMA kernel (64-row tiles, no split-K) instead of the split-K halo kernel + reduce
+static int halo_min_tiles() {
+    static const int v = [] {
+        const char* e = getenv("CAI_HALO_MIN_TILES");
+        return (e && *e) ? atoi(e) : 0;
+    }();
+    return v;
+}
 static int halo_ks(const cai_conv_geom* g, const Plan& P, bool glds) {
     if (!glds || P.phase || halo_off() || g->stride != 2 || (g->kernel != 3 && g->kernel != 5) ||
         g->pad != g->kernel / 2 || P.Cin_pad % 32 != 0 || P.kout_c > 128 || P.OHg[0] < 8 || P.OWg[0] < 32)
+        return 0;
+    if (halo_min_tiles() > 0 &&
+        (int64_t)g->batch * ((P.OWg[0] + 31) / 32) * ((P.OHg[0] + 7) / 8) < halo_min_tiles())
         return 0;
     return g->kernel;
 }
@@ -4044,7 +4056,7 @@ static int run_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int3
     // run now
     cai_reduce_job J{};
     J.kind = CAI_JOB_WGRAD;
-    J.nblocks = wgrad_job_blocks(W.Ng, W.ncols, bws ? (W.nbias + 255) / 256 : 0);
+    J.nblocks = wgrad_job_blocks(W.Ng, W.Cq_pad, g->kernel, bws ? (W.nbias + 255) / 256 : 0);
     J.p[0] = slab; J.p[1] = dw; J.p[2] = bws; J.p[3] = db;
     J.i[0] = W.S; J.i[1] = W.Ng; J.i[2] = W.ncols; J.i[3] = W.Cq; J.i[4] = W.Cq_pad; J.i[5] = g->kernel;
     J.i[6] = accumulate; J.i[7] = W.Sb; J.i[8] = W.nbias;

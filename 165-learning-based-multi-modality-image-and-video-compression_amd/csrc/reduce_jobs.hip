@@ -7,10 +7,10 @@
 // deferred and immediate reduces are bit-identical.
 //
 // Job bodies (the order and arithmetic of every sum is fixed: deterministic):
-//   WGRAD  one block per output row n of the [Ng][ncols] slab: each 16-byte column chunk summed over the S
-//          splits in split order (loads in batches of 8), the row transposed through LDS from [tap][q] to the
-//          torch layout dw[n][q][tap] and stored contiguously (rows wider than 8192 columns: one thread per
-//          chunk, scattered stores); trailing blocks: the bias partials [Sb][nbias] -> db, one thread per channel
+//   WGRAD  one block per (output row n, slice of input channels) of the [Ng][ncols] slab: each 16-byte column
+//          chunk summed over the S splits in split order (loads in batches of 8), the slice transposed through
+//          LDS from [tap][q] to the torch layout dw[n][q][tap] and stored contiguously; trailing blocks: the
+//          bias partials [Sb][nbias] -> db, one thread per channel
 //   EDGE   the image-side layers' weight gradient (edge.hip): unit partials summed in unit order, scattered
 //          into dW / db (and the image-side column sums)
 //   GDN    16 element columns x 16 partial-block groups per block (4 consecutive elements per thread), the
@@ -21,8 +21,17 @@
 
 namespace cai {
 
-// rows of the weight-gradient slab small enough to transpose through LDS (floats)
-constexpr int WG_ROW_LDS = 8192;
+// WGRAD job layout: one block per (output row n, slice of input channels q).  The slab row of n is [tap][Cq_pad]
+// (16-byte chunks of 4 channels); a block takes q4 chunks of every tap (q4 * k*k <= 256 threads, one chunk per
+// thread), sums them over the S splits in split order, transposes the slice through LDS and writes
+// dw[n][q][tap] for its channels -- one contiguous run of the torch layout.  (One block per whole row kept
+// 129-193 blocks per job: ~20 us per C2 halo layer on its own, the batched launch load-imbalanced.)
+__host__ __device__ __forceinline__ int wg_q4(int kk, int cq4) {
+    int q4 = 1;
+    while (q4 * 2 * kk <= 256 && q4 * 2 <= cq4) q4 *= 2;
+    return q4;
+}
+constexpr int WG_TR_FLOATS = 4 * (256 + 64);   // 4 * q4 * (kk + 1) <= 4 * (256 + q4), q4 <= 64
 
 __device__ __forceinline__ void wgrad_bias_body(const cai_reduce_job& J, int bid) {
     const float* __restrict__ bws = static_cast<const float*>(J.p[2]);
@@ -43,115 +52,58 @@ __device__ __forceinline__ void wgrad_bias_body(const cai_reduce_job& J, int bid
     db[n] = accumulate ? db[n] + v : v;
 }
 
-// one output row n per block: the row's ncols = k*k*Cq_pad columns (slab layout [tap][q]) summed over the S
-// splits in split order (16-byte loads, 8 splits in flight), transposed through LDS and written to dw[n][q][tap]
-// (the torch layout is contiguous over (q, tap) for a fixed n): coalesced read-modify-write stores instead of
-// one 4-byte access per k*k-strided element
-__device__ __forceinline__ void wgrad_row_body(const cai_reduce_job& J, int n, float* row) {
+__device__ __forceinline__ void wgrad_slice_body(const cai_reduce_job& J, int bid, float* tr) {
     const float* __restrict__ ws = static_cast<const float*>(J.p[0]);
     float* __restrict__ dw = static_cast<float*>(const_cast<void*>(J.p[1]));
     const int S = J.i[0], Ng = J.i[1], ncols = J.i[2], Cq = J.i[3], Cq_pad = J.i[4], k = J.i[5];
     const int accumulate = J.i[6];
-    const int c4 = ncols >> 2;
+    const int kk = k * k, cq4 = Cq_pad >> 2, c4 = ncols >> 2;
+    const int q4 = wg_q4(kk, cq4), nsl = (cq4 + q4 - 1) / q4;
+    const int n = bid / nsl, c0 = (bid - (bid / nsl) * nsl) * q4;
+    const int t = threadIdx.x / q4, j = threadIdx.x - (threadIdx.x / q4) * q4, c = c0 + j;
+    const bool active = t < kk && c < cq4;
     const int64_t slab4 = ((int64_t)Ng * ncols) >> 2;
-    const f32x4* src = reinterpret_cast<const f32x4*>(ws) + (int64_t)n * c4;
-    // RC column chunks per thread at once, RB splits per batch: RC * RB loads in flight per thread (one chunk at
-    // a time left a thread waiting S / 8 + 1 round trips per chunk).  Every chunk still sums its splits in split
-    // order: the same floats as one chunk at a time.
-    constexpr int RC = 4, RB = 4;
-    for (int cb = threadIdx.x; cb < c4; cb += 256 * RC) {
-        bool ok[RC];
-        f32x4 acc[RC];
-#pragma unroll
-        for (int q = 0; q < RC; ++q) {
-            ok[q] = cb + 256 * q < c4;
-            acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
+    const f32x4* src = reinterpret_cast<const f32x4*>(ws) + (int64_t)n * c4 + t * cq4 + c;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (active) {
         int sp = 0;
-        for (; sp + RB <= S; sp += RB) {
-            f32x4 v[RB][RC];
+        for (; sp + 8 <= S; sp += 8) {
+            f32x4 v[8];
 #pragma unroll
-            for (int j = 0; j < RB; ++j)
+            for (int i = 0; i < 8; ++i) v[i] = src[(int64_t)(sp + i) * slab4];
 #pragma unroll
-                for (int q = 0; q < RC; ++q)
-                    v[j][q] = ok[q] ? src[(int64_t)(sp + j) * slab4 + cb + 256 * q] : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int j = 0; j < RB; ++j)
-#pragma unroll
-                for (int q = 0; q < RC; ++q) acc[q] += v[j][q];
+            for (int i = 0; i < 8; ++i) acc += v[i];
         }
-        for (; sp < S; ++sp)
+        for (; sp < S; ++sp) acc += src[(int64_t)sp * slab4];
 #pragma unroll
-            for (int q = 0; q < RC; ++q)
-                if (ok[q]) acc[q] += src[(int64_t)sp * slab4 + cb + 256 * q];
-#pragma unroll
-        for (int q = 0; q < RC; ++q)
-            if (ok[q]) *reinterpret_cast<f32x4*>(row + 4 * (cb + 256 * q)) = acc[q];
+        for (int e = 0; e < 4; ++e) tr[(4 * j + e) * (kk + 1) + t] = acc[e];
     }
     __syncthreads();
-    const int kk = k * k, nout = Cq * kk;
-    float* d = dw + (int64_t)n * nout;
-    for (int i = threadIdx.x; i < nout; i += 256) {
-        const int q = i / kk, t = i - (i / kk) * kk;
-        const float v = row[t * Cq_pad + q];
+    const int qa = 4 * c0, qb = min(Cq, 4 * (c0 + q4));
+    const int len = (qb - qa) * kk;
+    float* d = dw + ((int64_t)n * Cq + qa) * kk;
+    for (int i = threadIdx.x; i < len; i += 256) {
+        const int ql = i / kk, tt = i - (i / kk) * kk;
+        const float v = tr[ql * (kk + 1) + tt];
         d[i] = accumulate ? d[i] + v : v;
     }
 }
 
-// the same sums for rows too wide for LDS: one thread per 16-byte column chunk, scattered 4-byte stores
-__device__ __forceinline__ void wgrad_scatter_body(const cai_reduce_job& J, int bid) {
-    const float* __restrict__ ws = static_cast<const float*>(J.p[0]);
-    float* __restrict__ dw = static_cast<float*>(const_cast<void*>(J.p[1]));
-    const int S = J.i[0], Ng = J.i[1], ncols = J.i[2], Cq = J.i[3], Cq_pad = J.i[4], k = J.i[5];
-    const int accumulate = J.i[6];
-    const int c4 = ncols >> 2;
-    const int64_t total = (int64_t)Ng * c4;
-    const int64_t i = (int64_t)bid * 256 + threadIdx.x;
-    if (i >= total) return;
-    const int64_t slab4 = ((int64_t)Ng * ncols) >> 2;
-    const f32x4* src = reinterpret_cast<const f32x4*>(ws) + i;
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-    int sp = 0;
-    for (; sp + 8 <= S; sp += 8) {
-        f32x4 v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = src[(int64_t)(sp + j) * slab4];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc += v[j];
-    }
-    for (; sp < S; ++sp) acc += src[(int64_t)sp * slab4];
-    const int n = (int)(i / c4);
-    const int col = (int)(i - (int64_t)n * c4) * 4;
-    const int kk = k * k;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        const int cc = col + e;
-        const int t = cc / Cq_pad, q = cc - (cc / Cq_pad) * Cq_pad;
-        if (q >= Cq) continue;
-        float* d = dw + ((int64_t)n * Cq + q) * kk + t;
-        *d = accumulate ? *d + acc[e] : acc[e];
-    }
-}
-
-// blocks [0, wblocks): the weight rows (LDS-transposed: one row per block; else scattered chunks); then the
-// bias blocks
-__device__ __forceinline__ void wgrad_reduce_body(const cai_reduce_job& J, int bid, float* row) {
-    const int Ng = J.i[1], ncols = J.i[2];
-    const bool lds = ncols <= WG_ROW_LDS;
-    const int wblocks = lds ? Ng : (int)(((int64_t)Ng * (ncols >> 2) + 255) / 256);
+// blocks [0, wblocks): the (row, channel-slice) weight blocks; then the bias blocks
+__device__ __forceinline__ void wgrad_reduce_body(const cai_reduce_job& J, int bid, float* tr) {
+    const int Ng = J.i[1], Cq_pad = J.i[4], k = J.i[5];
+    const int cq4 = Cq_pad >> 2, q4 = wg_q4(k * k, cq4);
+    const int wblocks = Ng * ((cq4 + q4 - 1) / q4);
     if (bid >= wblocks) {
         wgrad_bias_body(J, bid - wblocks);
         return;
     }
-    if (lds)
-        wgrad_row_body(J, bid, row);
-    else
-        wgrad_scatter_body(J, bid);
+    wgrad_slice_body(J, bid, tr);
 }
 
-int wgrad_job_blocks(int Ng, int ncols, int nbias_blocks) {
-    const int wblocks = ncols <= WG_ROW_LDS ? Ng : (int)(((int64_t)Ng * (ncols >> 2) + 255) / 256);
-    return wblocks + nbias_blocks;
+int wgrad_job_blocks(int Ng, int Cq_pad, int k, int nbias_blocks) {
+    const int cq4 = Cq_pad >> 2, q4 = wg_q4(k * k, cq4);
+    return Ng * ((cq4 + q4 - 1) / q4) + nbias_blocks;
 }
 
 __device__ __forceinline__ void gdn_reduce_body(const cai_reduce_job& J, int bid, f32x4 (*red)[17]) {
@@ -279,7 +231,7 @@ __device__ __forceinline__ void edge_reduce_body(const cai_reduce_job& J, int bi
 
 __global__ __launch_bounds__(256) void reduce_jobs_kernel(const ReduceBatch B) {
     __shared__ f32x4 red[16][17];
-    __shared__ __attribute__((aligned(16))) float row[WG_ROW_LDS];
+    __shared__ __attribute__((aligned(16))) float tr[WG_TR_FLOATS];
     __shared__ float ered[16][16];
     __shared__ float etot[16];
     // the job owning this block (block-uniform linear scan over <= CAI_REDUCE_BATCH entries)
@@ -289,7 +241,7 @@ __global__ __launch_bounds__(256) void reduce_jobs_kernel(const ReduceBatch B) {
     const cai_reduce_job& J = B.jobs[j];
     const int bid = b - B.start[j];
     if (J.kind == CAI_JOB_WGRAD)
-        wgrad_reduce_body(J, bid, row);
+        wgrad_reduce_body(J, bid, tr);
     else if (J.kind == CAI_JOB_GDN)
         gdn_reduce_body(J, bid, red);
     else if (J.kind == CAI_JOB_EDGE)

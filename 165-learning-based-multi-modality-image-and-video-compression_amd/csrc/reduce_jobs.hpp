@@ -14,7 +14,7 @@ struct ReduceBatch {
 };
 
 // blocks of a WGRAD job: its weight rows (reduce_jobs.hip's layout choice) + `nbias_blocks` bias blocks
-int wgrad_job_blocks(int Ng, int ncols, int nbias_blocks);
+int wgrad_job_blocks(int Ng, int Cq_pad, int k, int nbias_blocks);
 
 // run `n` jobs (CAI_JOB_NONE entries skipped) in ceil(n / CAI_REDUCE_BATCH) launches
 int launch_reduce_jobs(const cai_reduce_job* jobs, int n, hipStream_t st);
