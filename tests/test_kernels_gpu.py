@@ -110,6 +110,13 @@ CONV_CASES = [
     # straddling two taps, the last tile past K, 1x1 and 3x3, both directions, the s^2-phase direction
     ("conv", 4, 96, 96, 64, 64, 3, 1),
     ("conv", 4, 96, 192, 32, 32, 1, 1),
+    # 32-multiple channel counts at latent size (cheng2020's 96-channel attention units at 16x16, B = 4, 192 -> 288
+    # at 8x8), a ConvTranspose2d with 96 / 160 channels
+    ("conv", 4, 96, 96, 16, 16, 3, 1),
+    ("conv", 4, 192, 96, 16, 16, 1, 1),
+    ("conv", 4, 96, 192, 16, 16, 1, 1),
+    ("conv", 4, 192, 288, 8, 8, 3, 1),
+    ("deconv", 4, 96, 160, 8, 8, 3, 1),
     # 64-row LDS-DMA tiles (conv_glds_kernel<64x128 / 64x192>: mid-size maps whose 256 / 128-row grid would split
     # K): cheng2020 attention-unit 1x1 convs at 64x64, B = 4, both directions
     ("conv", 4, 96, 192, 64, 64, 1, 1),
