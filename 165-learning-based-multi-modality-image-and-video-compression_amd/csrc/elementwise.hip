@@ -142,6 +142,59 @@ __global__ void pixel_shuffle_kernel(const ShuffleArgs s) {
     }
 }
 
+// The same shuffle for bf16 with channel-contiguous sides (xs[3] == ys[3] == 1, 16-byte aligned pixel rows,
+// C % 8 == 0): one thread per (input pixel, 8 output channels) reads the R*R*8 contiguous input channels those
+// outputs come from (R*R 16-byte loads) and writes R*R output pixels x 8 channels (R*R 16-byte stores) -- the
+// scalar kernel above moves 2 bytes per thread with 64-bit divisions per element (20.9 us per cheng2020 launch).
+template <int R>
+__global__ void pixel_shuffle_vec_kernel(const ShuffleArgs s) {
+    const int CG = s.C / 8;
+    const int64_t total = (int64_t)s.B * s.H * s.W * CG;
+    const bf16* src = reinterpret_cast<const bf16*>(s.src);
+    bf16* dst = reinterpret_cast<bf16*>(s.dst);
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int cg = (int)(i % CG);
+        int64_t p = i / CG;
+        const int w = (int)(p % s.W);
+        p /= s.W;
+        const int h = (int)(p % s.H);
+        const int b = (int)(p / s.H);
+        const int64_t xo = b * s.xs[0] + h * s.xs[1] + w * s.xs[2] + (int64_t)cg * 8 * R * R;
+        bf16x8 xv[R * R];    // input channels cg*8*R*R .. +8*R*R: element e = c_local*R*R + ii*R + jj
+        if (!s.inverse) {
+#pragma unroll
+            for (int q = 0; q < R * R; ++q) xv[q] = *reinterpret_cast<const bf16x8*>(src + xo + 8 * q);
+        }
+#pragma unroll
+        for (int ii = 0; ii < R; ++ii)
+#pragma unroll
+            for (int jj = 0; jj < R; ++jj) {
+                const int64_t yo = b * s.ys[0] + (int64_t)(h * R + ii) * s.ys[1] + (int64_t)(w * R + jj) * s.ys[2] +
+                                   cg * 8;
+                if (!s.inverse) {
+                    bf16x8 o;
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) {
+                        const int e = c * R * R + ii * R + jj;
+                        o[c] = xv[e / 8][e % 8];
+                    }
+                    *reinterpret_cast<bf16x8*>(dst + yo) = o;
+                } else {
+                    const bf16x8 v = *reinterpret_cast<const bf16x8*>(src + yo);
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) {
+                        const int e = c * R * R + ii * R + jj;
+                        xv[e / 8][e % 8] = v[c];
+                    }
+                }
+            }
+        if (s.inverse) {
+#pragma unroll
+            for (int q = 0; q < R * R; ++q) *reinterpret_cast<bf16x8*>(dst + xo + 8 * q) = xv[q];
+        }
+    }
+}
+
 // GDN1 (layers/gdn.py:95-121): norm = beta + gamma |x| comes from a 1x1 conv on |x|; this is the
 // remaining  out = x * (1 / norm)  (inverse: x * norm)  and its backward
 template <typename T>
@@ -313,7 +366,18 @@ int cai_pixel_shuffle(int dtype, const void* src, const int64_t* src_strides, vo
     s.B = B; s.H = H; s.W = W; s.C = C; s.r = r; s.inverse = inverse;
     const int64_t n = (int64_t)B * H * r * W * r * C;
     hipStream_t st = as_stream(stream);
-    if (dtype == CAI_BF16)
+    auto al16 = [](const void* p, int64_t off) { return ((reinterpret_cast<uintptr_t>(p) + off * 2) & 15) == 0; };
+    const bool vec = dtype == CAI_BF16 && (r == 2 || r == 4) && C % 8 == 0 && s.xs[3] == 1 && s.ys[3] == 1 &&
+                     s.xs[0] % 8 == 0 && s.xs[1] % 8 == 0 && s.xs[2] % 8 == 0 && s.ys[0] % 8 == 0 &&
+                     s.ys[1] % 8 == 0 && s.ys[2] % 8 == 0 && al16(src, 0) && al16(dst, 0);
+    if (vec) {
+        const int64_t items = (int64_t)B * H * W * (C / 8);
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(16384, (items + 255) / 256));
+        if (r == 2)
+            hipLaunchKernelGGL(pixel_shuffle_vec_kernel<2>, dim3(grid), dim3(256), 0, st, s);
+        else
+            hipLaunchKernelGGL(pixel_shuffle_vec_kernel<4>, dim3(grid), dim3(256), 0, st, s);
+    } else if (dtype == CAI_BF16)
         hipLaunchKernelGGL(pixel_shuffle_kernel<bf16>, dim3(ew_grid2(n)), dim3(256), 0, st, s);
     else
         hipLaunchKernelGGL(pixel_shuffle_kernel<float>, dim3(ew_grid2(n)), dim3(256), 0, st, s);

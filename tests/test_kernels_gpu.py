@@ -522,23 +522,26 @@ def test_rd_loss(cuda):
 
 @pytest.mark.parametrize("bf16", [False, True])
 @pytest.mark.parametrize("pm", [True, False])
-def test_pixel_shuffle(cuda, bf16, pm):
+@pytest.mark.parametrize("r,C", [(2, 16), (2, 24), (4, 8), (2, 12)])
+def test_pixel_shuffle(cuda, bf16, pm, r, C):
+    """Both shuffle kernels (the 16-byte one for bf16 pixel-major sides with C % 8 == 0, r in {2, 4}; the scalar
+    one otherwise), forward and backward, bit-exact against torch."""
     from compressai._ops import PixelShuffleFn, empty_pm
 
     torch.manual_seed(3)
     dt = torch.bfloat16 if bf16 else torch.float32
-    x = torch.randn(2, 64, 5, 7).to(dt)
-    g = torch.randn(2, 16, 10, 14).to(dt)
+    x = torch.randn(2, C * r * r, 5, 7).to(dt)
+    g = torch.randn(2, C, 5 * r, 7 * r).to(dt)
     if pm:
-        xd = empty_pm(2, 64, 5, 7, dt, cuda)
+        xd = empty_pm(2, C * r * r, 5, 7, dt, cuda)
         xd.copy_(x)
     else:
         xd = x.to(cuda).contiguous()
     xd.requires_grad_()
-    y = PixelShuffleFn.apply(xd, 2)
+    y = PixelShuffleFn.apply(xd, r)
     y.backward(g.to(cuda))
-    assert torch.equal(y.cpu(), F.pixel_shuffle(x, 2))
-    assert torch.equal(xd.grad.cpu(), F.pixel_unshuffle(g, 2))
+    assert torch.equal(y.cpu(), F.pixel_shuffle(x, r))
+    assert torch.equal(xd.grad.cpu(), F.pixel_unshuffle(g, r))
 
 
 def _block_pair(kind, cuda):
