@@ -485,9 +485,20 @@ def _edge_bwd(ctx, xs, weight, gy):
     return dx, dw, db, None
 
 
+def residual_fusable(spec: ConvSpec) -> bool:
+    """Whether ConvFn can take a residual input (cai_conv_fwd_res): bf16 pixel-major output of the GEMM kernels,
+    activation in this conv's own backward."""
+    return (compute_dtype() == torch.bfloat16 and not spec.transposed and not spec.out_nchw32
+            and not spec.act_bwd_downstream and not spec.in_abs)
+
+
 class ConvFn(torch.autograd.Function):
+    """y = act(conv(x) + bias [+ res]).  ``res`` (optional, same shape as y) is the residual of ResidualUnit
+    (layers.py:211-226: ``out += identity; relu(out)``) added in the conv epilogue before the activation; its
+    gradient is the activation-masked output gradient."""
+
     @staticmethod
-    def forward(ctx, x, weight, bias, spec: ConvSpec):
+    def forward(ctx, x, weight, bias, spec: ConvSpec, res=None):
         _check_cuda(x, weight, bias)
         dt = compute_dtype()
         vec = _vec(dt)
@@ -500,6 +511,12 @@ class ConvFn(torch.autograd.Function):
         ctx.params = (weight, bias)
         ctx.edge = _edge_mode(ctx, spec, g, dt)
         ctx.small = False
+        ctx.has_res = res is not None
+        if res is not None:
+            if not residual_fusable(spec) or ctx.edge or tuple(res.shape) != (B, cout, g.out_h, g.out_w):
+                raise ValueError(f"conv residual: not fusable for this layer (res {tuple(res.shape)}, "
+                                 f"out {(B, cout, g.out_h, g.out_w)}, dtype {dt})")
+            _check_cuda(res)
         if ctx.edge == 1:   # space-to-depth first layer: reads the NCHW fp32 image directly
             x32 = x.detach().float().contiguous()
             y = empty_pm(B, cout, g.out_h, g.out_w, dt, x.device)
@@ -532,7 +549,21 @@ class ConvFn(torch.autograd.Function):
             ys = (g.out_h * g.out_w * cout, 1, g.out_w * cout, cout)
             ydt = dcode(dt)
         ctx.small = _small_deconv(spec, g, xld, dt)
-        if ctx.small:   # few output channels: per-input-pixel GEMM + col2im (csrc/deconv_small.hip)
+        if res is not None:
+            rpm, rld = to_pm(res, dt, 4)
+            packer = _prepack_active()
+            wp = packer.lookup(weight, dt, 0) if packer is not None else None
+            ctx.wt_packed = packer.lookup(weight, dt, 1) if packer is not None else None
+            if wp is None:
+                wp = _pack_weight(g, dt, 0, weight)
+            ws, wsb = _conv_ws(g, dt, 0, x.device)
+            fl, nb = _ledger.conv_cost(g, _es(dt), 0)
+            nb += B * g.out_h * g.out_w * cout * _es(dt)
+            _ledger.run(lambda: lib.cai_conv_fwd_res(ctypes.byref(g), dcode(dt), _p(xpm), xld, 0, _p(wp), _p(b),
+                                                     spec.act, spec.act_param, _p(rpm), rld, _p(y), ydt, *ys, _p(ws),
+                                                     wsb, _stream()),
+                        "conv_fwd", _conv_kernel(g, dt, 0, False), fl, nb, dt, _ledger.shape_of(g))
+        elif ctx.small:   # few output channels: per-input-pixel GEMM + col2im (csrc/deconv_small.hip)
             ws, wsb = _small_ws(g, dt, x.device)
             w32 = weight.detach().float().contiguous()
             fl, nb = _ledger.conv_cost(g, _es(dt), 0, y_bytes=4)
@@ -563,9 +594,9 @@ class ConvFn(torch.autograd.Function):
         code = dcode(dt)
         st = _stream()
         if ctx.edge:
-            return _edge_bwd(ctx, xpm, weight, gy)
+            return _edge_bwd(ctx, xpm, weight, gy) + (None,)
         if ctx.small:
-            return _small_deconv_bwd(ctx, xpm, weight, gy)
+            return _small_deconv_bwd(ctx, xpm, weight, gy) + (None,)
         gpm, gld = to_pm(gy, dt, vec)
         if spec.act != ACT_NONE and not spec.act_bwd_downstream:
             mode = 1 if spec.act == 1 else 2
@@ -617,7 +648,10 @@ class ConvFn(torch.autograd.Function):
                 dw = db = None
             elif weight.dtype != torch.float32:
                 dw = dw.to(weight.dtype)
-        return dx, dw, db, None
+        dres = None
+        if ctx.has_res and ctx.needs_input_grad[4]:
+            dres = gpm
+        return dx, dw, db, None, dres
 
 
 # ---------------------------------------------------------------------------

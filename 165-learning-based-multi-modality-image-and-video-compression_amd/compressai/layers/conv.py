@@ -43,7 +43,9 @@ class _ConvMixin:
                         out_nchw32=(cout % 8 != 0), in_mask=in_mask, in_mask_param=in_mask_param,
                         act_bwd_downstream=act_bwd_downstream)
 
-    def run(self, x, **kw):
+    def run(self, x, res=None, **kw):
+        if res is not None:   # y = act(conv(x) + bias + res) in the epilogue (ResidualUnit)
+            return ConvFn.apply(x, self.weight, self.bias, self._spec(**kw), res)
         return ConvFn.apply(x, self.weight, self.bias, self._spec(**kw))
 
 

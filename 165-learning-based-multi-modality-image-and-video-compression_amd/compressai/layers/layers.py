@@ -9,16 +9,19 @@ keep the reference's module tree (so state_dict keys match: ``conv1``,
 ``conv2``, ``gdn``, ``skip``, ``subpel_conv.0``, ``upsample.0``,
 ``conv_a.0.conv.2`` ...).  Their forward passes chain the HIP convs with the
 activation in the conv epilogue and its backward mask in the next conv's
-dgrad epilogue; the residual add (+ trailing ReLU), the attention gate and
-the pixel shuffle run on the elementwise kernels (csrc/elementwise.hip).
+dgrad epilogue.  ResidualUnit's ``+ x`` and trailing ReLU run in its last
+conv's epilogue (cai_conv_fwd_res); the other residual adds, the attention
+gate and the pixel shuffle run on the elementwise kernels
+(csrc/elementwise.hip).
 """
+import os
 from typing import Any
 
 import torch
 import torch.nn as nn
 
-from .._native import ACT_LEAKY, ACT_NONE, ACT_RELU, MASK_LEAKY
-from .._ops import AddActFn, GateFn
+from .._native import ACT_LEAKY, ACT_NONE, ACT_RELU, MASK_LEAKY, MASK_POS
+from .._ops import AddActFn, GateFn, residual_fusable
 from .conv import Conv2d, ConvTranspose2d, PixelShuffle, Sequential
 from .gdn import GDN
 
@@ -120,8 +123,17 @@ class ResidualUnit(nn.Module):
                                nn.ReLU(inplace=True), conv1x1(N // 2, N))
         self.relu = nn.ReLU(inplace=True)
 
+    # False: the unfused chain (Sequential, then add + ReLU on the elementwise kernel); CAI_RESIDUAL_FUSE=0 for A/Bs
+    fuse_residual = os.environ.get("CAI_RESIDUAL_FUSE", "1") != "0"
+
     def forward(self, x):
-        return AddActFn.apply(self.conv(x), x, ACT_RELU, 0.0)
+        c = self.conv
+        if not (self.fuse_residual and residual_fusable(c[4]._spec(act=ACT_RELU, in_mask=MASK_POS))):
+            return AddActFn.apply(c(x), x, ACT_RELU, 0.0)
+        # the Sequential's fusion spelled out, with `+ x` and the trailing ReLU in the last conv's epilogue
+        h = c[0].run(x, act=ACT_RELU, act_bwd_downstream=True)
+        h = c[2].run(h, act=ACT_RELU, in_mask=MASK_POS, act_bwd_downstream=True)
+        return c[4].run(h, act=ACT_RELU, in_mask=MASK_POS, res=x)
 
 
 class AttentionBlock(nn.Module):

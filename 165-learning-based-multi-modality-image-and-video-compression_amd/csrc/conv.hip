@@ -66,6 +66,8 @@ struct ConvArgs {
     const void* aux;
     int aux_ld, mask_mode;
     float mask_param;
+    const bf16* res;         // residual input (cai_conv_fwd_res): y = act(conv + bias + res), pixel-major bf16, NULL: none
+    int res_ld;
     int ksplit;              // K splits per phase (grid.z = nphase * ksplit)
     float* ws;               // split-K partials [nphase*ksplit][ws_rows][ws_ld] fp32
     int ws_rows, ws_ld;
@@ -78,6 +80,11 @@ __device__ __forceinline__ float apply_act(float v, int act, float prm) {
     if (act == CAI_ACT_RELU) return v > 0.f ? v : 0.f;
     if (act == CAI_ACT_LEAKY) return v > 0.f ? v : v * prm;
     return v;
+}
+// the activation as the epilogue applies it before the store: deferred to the store when a residual is added
+// first (store_out_chunk / store_out_scalar add res, then activate)
+__device__ __forceinline__ float act_pre(const ConvArgs& a, float v) {
+    return a.res ? v : apply_act(v, a.act, a.act_param);
 }
 __device__ __forceinline__ float mask_val(int mode, float a, float prm) {
     if (mode == CAI_MASK_POS) return a > 0.f ? 1.f : 0.f;
@@ -120,6 +127,12 @@ __device__ __forceinline__ void store_out_chunk(const ConvArgs& a, const PhaseDe
                                                 float (&v)[8], int VO) {
     int b, oy, ox;
     out_pixel<T>(a, P, plane, m, b, oy, ox);
+    if (a.res) {
+        const bf16* R = a.res + (((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.res_ld + n;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            if (e < VO) v[e] = apply_act(v[e] + (float)R[e], a.act, a.act_param);
+    }
     if (a.mask_mode) {
         const T* AUX = reinterpret_cast<const T*>(a.aux);
         const int64_t pa = (((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.aux_ld + n;
@@ -143,6 +156,8 @@ __device__ __forceinline__ void store_out_scalar(const ConvArgs& a, const PhaseD
                                                  float v) {
     int b, oy, ox;
     out_pixel<T>(a, P, plane, m, b, oy, ox);
+    if (a.res)
+        v = apply_act(v + (float)a.res[(((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.res_ld + n], a.act, a.act_param);
     if (a.mask_mode) {
         const T* AUX = reinterpret_cast<const T*>(a.aux);
         v *= mask_val(a.mask_mode, to_f32(AUX[(((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.aux_ld + n]),
@@ -199,7 +214,7 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvArgs& a, const Phas
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = wm * WTM + tm * 16 + (lane >> 4) * 4 + r;
-                E[row * ES + col] = apply_act(acc[tm][tn][r] + bv, a.act, a.act_param);
+                E[row * ES + col] = act_pre(a, acc[tm][tn][r] + bv);
             }
         }
     __syncthreads();
@@ -283,13 +298,16 @@ __device__ __forceinline__ void conv_epilogue_rows_t(const ConvArgs& a, const Ph
             const bf16* AUX = (NOLDS && a.mask_mode) ? reinterpret_cast<const bf16*>(a.aux) +
                                                            (((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.aux_ld
                                                      : nullptr;
+            const bf16* RS = a.res ? a.res + (((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.res_ld : nullptr;
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn) {
                 const int n = n0 + wn * WTN + tn * 16 + 4 * g_;
                 if (n >= a.Cout) continue;
                 f32x4 v;
+                bf16x4 rv = bf16x4{(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+                if (RS) rv = *reinterpret_cast<const bf16x4*>(RS + n);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = apply_act(acc[tm][tn][r] + bv[tn][r], a.act, a.act_param);
+                for (int r = 0; r < 4; ++r) v[r] = apply_act(acc[tm][tn][r] + bv[tn][r] + (float)rv[r], a.act, a.act_param);
                 if (NOLDS && AUX) {
                     const bf16x4 mv = *reinterpret_cast<const bf16x4*>(AUX + n);
 #pragma unroll
@@ -315,7 +333,7 @@ __device__ __forceinline__ void conv_epilogue_rows_t(const ConvArgs& a, const Ph
             for (int r = 0; r < 4; ++r) {
                 const int n = n0 + col + r;
                 const float bvr = (a.bias && n < a.Cout) ? a.bias[n] : 0.f;
-                v[r] = apply_act(acc[tm][tn][r] + bvr, a.act, a.act_param);
+                v[r] = act_pre(a, acc[tm][tn][r] + bvr);
             }
             *reinterpret_cast<f32x4*>(E + row * ES + col) = v;
         }
@@ -848,7 +866,7 @@ __global__ __launch_bounds__(512, 1) void conv_small_kernel(const ConvArgs a) {
         for (int e = 0; e < 8; ++e) {
             const int n = nb + e;
             const float bv = (a.bias && e < VO && n < a.Cout) ? a.bias[n] : 0.f;
-            v[e] = apply_act(v[e] + bv, a.act, a.act_param);
+            v[e] = act_pre(a, v[e] + bv);
         }
         if (a.y_vec) {
             store_out_chunk<bf16>(a, P, plane, m, nb, v, VO);
@@ -1698,7 +1716,7 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce_kernel(const ConvArgs 
         for (int e = 0; e < 8; ++e) {
             const int nn = n + e;
             const float bv = (a.bias && nn < a.Cout) ? a.bias[nn] : 0.f;
-            v[e] = apply_act(v[e] + bv, a.act, a.act_param);
+            v[e] = act_pre(a, v[e] + bv);
         }
         if (a.y_vec) {
             store_out_chunk<T>(a, P, plane, m, n, v, VO);
@@ -3494,7 +3512,8 @@ static void dispatch_conv(const ConvArgs& a, const ConvLaunch& L, hipStream_t st
 static int run_conv(const cai_conv_geom* g, int dtype, int direction, const void* x, int x_ld, int in_abs,
                     const void* w, const float* bias, int act, float act_param, void* y, int y_dtype, int64_t ysb,
                     int64_t ysc, int64_t ysy, int64_t ysx, const void* aux, int aux_ld, int mask_mode,
-                    float mask_param, void* workspace, size_t ws_bytes, void* stream, const char* name) {
+                    float mask_param, void* workspace, size_t ws_bytes, void* stream, const char* name,
+                    const void* res = nullptr, int res_ld = 0) {
     int rc = check_geom(g);
     if (rc) return rc;
     CAI_CHECK_ARG(dtype == CAI_BF16 || dtype == CAI_F32, "%s: bad dtype", name);
@@ -3523,6 +3542,11 @@ static int run_conv(const cai_conv_geom* g, int dtype, int direction, const void
                ((uintptr_t)y & 15) == 0);
     a.bias = bias; a.act = act; a.act_param = act_param;
     a.aux = aux; a.aux_ld = aux_ld; a.mask_mode = mask_mode; a.mask_param = mask_param;
+    // residual (forward only): bf16 pixel-major, 8-byte aligned 4-channel groups, added before the activation
+    CAI_CHECK_ARG(!res || (direction == 0 && dtype == CAI_BF16 && a.y_vec && y_dtype == CAI_BF16 && !mask_mode &&
+                           res_ld >= P.kout_c && res_ld % 4 == 0 && ((uintptr_t)res & 7) == 0),
+                  "%s: residual needs a bf16 pixel-major output and res_ld >= Cout, a multiple of 4", name);
+    a.res = reinterpret_cast<const bf16*>(res); a.res_ld = res_ld;
     if ((L.halo_ph || L.halo_s1) && L.hbn > 128 && L.ksplit == 1 && !epi_t_direct(a))
         L = conv_launch(g, dtype, direction, in_abs, false);    // the 192-channel tiles store from registers only
     CAI_CHECK_ARG(L.ws_bytes == 0 || (workspace && ws_bytes >= L.ws_bytes && ((uintptr_t)workspace & 15) == 0),
@@ -3892,6 +3916,15 @@ int cai_conv_fwd(const cai_conv_geom* g, int dtype, const void* x, int32_t x_ld,
                  int64_t ysy, int64_t ysx, void* workspace, size_t ws_bytes, void* stream) {
     return run_conv(g, dtype, 0, x, x_ld, in_abs, packed_w, bias, act, act_param, y, y_dtype, ysb, ysc, ysy, ysx,
                     nullptr, 0, CAI_MASK_NONE, 0.f, workspace, ws_bytes, stream, "conv_fwd");
+}
+
+int cai_conv_fwd_res(const cai_conv_geom* g, int dtype, const void* x, int32_t x_ld, int32_t in_abs,
+                     const void* packed_w, const float* bias, int32_t act, float act_param, const void* res,
+                     int32_t res_ld, void* y, int y_dtype, int64_t ysb, int64_t ysc, int64_t ysy, int64_t ysx,
+                     void* workspace, size_t ws_bytes, void* stream) {
+    CAI_CHECK_ARG(res, "conv_fwd_res: null residual");
+    return run_conv(g, dtype, 0, x, x_ld, in_abs, packed_w, bias, act, act_param, y, y_dtype, ysb, ysc, ysy, ysx,
+                    nullptr, 0, CAI_MASK_NONE, 0.f, workspace, ws_bytes, stream, "conv_fwd_res", res, res_ld);
 }
 
 int cai_conv_dgrad(const cai_conv_geom* g, int dtype, const void* dy, int32_t dy_ld, const void* packed_wt, void* dx,

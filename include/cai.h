@@ -133,6 +133,18 @@ int cai_conv_fwd(const cai_conv_geom* g, int dtype,
                  void* y, int y_dtype, int64_t ysb, int64_t ysc, int64_t ysy, int64_t ysx,
                  void* workspace, size_t ws_bytes, void* stream);
 
+/* forward with a residual: y = act(conv(x) + bias + res), the ResidualUnit of
+ * cheng2020-attn's attention blocks (CompressAI/compressai/layers/layers.py:
+ * 211-226, `out = self.conv(x); out += identity; out = self.relu(out)`)
+ * in the conv epilogue.  bf16 only; res pixel-major with ld res_ld (>= out_c,
+ * multiple of 4, 8-byte aligned); y pixel-major bf16 (ysc == 1). */
+int cai_conv_fwd_res(const cai_conv_geom* g, int dtype,
+                     const void* x, int32_t x_ld, int32_t in_abs,
+                     const void* packed_w, const float* bias,
+                     int32_t act, float act_param, const void* res, int32_t res_ld,
+                     void* y, int y_dtype, int64_t ysb, int64_t ysc, int64_t ysy, int64_t ysx,
+                     void* workspace, size_t ws_bytes, void* stream);
+
 /* input gradient: dx = mask(aux) * conv_input_grad(dy).  dy pixel-major
  * (ld dy_ld), dx pixel-major (ld dx_ld), aux pixel-major (ld aux_ld) or NULL. */
 int cai_conv_dgrad(const cai_conv_geom* g, int dtype,

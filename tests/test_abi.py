@@ -56,6 +56,15 @@ def test_invalid_geometry_is_einval_with_message(native):
     assert lib.cai_conv_packed_weight_bytes(None, native.BF16, 0) == 0
 
 
+def test_conv_fwd_res_requires_residual(native):
+    lib = native.lib.load()
+    g = native.ConvGeom(2, 16, 8, 8, 16, 8, 8, 1, 1, 0, 0, 0)
+    rc = lib.cai_conv_fwd_res(ctypes.byref(g), native.BF16, None, 16, 0, None, None, 1, 0.0, None, 16, None,
+                              native.BF16, 0, 1, 0, 0, None, 0, None)
+    assert rc == native.CAI_EINVAL
+    assert b"null residual" in lib.cai_last_error()
+
+
 def test_python_shim_raises_valueerror(native):
     g = native.ConvGeom(2, 16, 8, 8, 16, 4, 4, 9, 2, 2, 0, 0)   # kernel 9 unsupported
     with pytest.raises(ValueError, match="unsupported kernel"):
