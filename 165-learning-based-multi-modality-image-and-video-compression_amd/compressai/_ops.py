@@ -616,10 +616,19 @@ class ConvFn(torch.autograd.Function):
             aux = xpm if spec.in_mask != MASK_NONE else None
             ws, wsb = _conv_ws(g, dt, 1, gy.device)
             fl, nb = _ledger.conv_cost(g, _es(dt), 1)
-            _ledger.run(lambda: lib.cai_conv_dgrad(ctypes.byref(g), code, _p(gpm), gld, _p(wt), _p(dx), ldx,
-                                                   spec.in_mask, spec.in_mask_param, _p(aux),
-                                                   ctx.xld if aux is not None else 0, _p(ws), wsb, st),
-                        "conv_dgrad", _conv_kernel(g, dt, 1), fl, nb, dt, _ledger.shape_of(g))
+            dres = getattr(ctx, "dx_res", None)   # ResidualUnitFn: + the residual's gradient, in the epilogue
+            if dres is not None and dt == torch.bfloat16 and aux is None and ldx % 8 == 0:
+                rpm, rld = to_pm(dres, dt, 4)
+                _ledger.run(lambda: lib.cai_conv_dgrad_res(ctypes.byref(g), code, _p(gpm), gld, _p(wt), _p(rpm), rld,
+                                                           _p(dx), ldx, _p(ws), wsb, st),
+                            "conv_dgrad", _conv_kernel(g, dt, 1), fl, nb, dt, _ledger.shape_of(g))
+            else:
+                _ledger.run(lambda: lib.cai_conv_dgrad(ctypes.byref(g), code, _p(gpm), gld, _p(wt), _p(dx), ldx,
+                                                       spec.in_mask, spec.in_mask_param, _p(aux),
+                                                       ctx.xld if aux is not None else 0, _p(ws), wsb, st),
+                            "conv_dgrad", _conv_kernel(g, dt, 1), fl, nb, dt, _ledger.shape_of(g))
+                if dres is not None:
+                    dx = dx + dres
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             nbytes = lib.cai_conv_wgrad_workspace_bytes(ctypes.byref(g), code)
             wparam, bparam = ctx.params
@@ -652,6 +661,48 @@ class ConvFn(torch.autograd.Function):
         if ctx.has_res and ctx.needs_input_grad[4]:
             dres = gpm
         return dx, dw, db, None, dres
+
+
+class _SubCtx:
+    """A stand-in autograd ctx: lets a multi-conv autograd node run ConvFn's forward / backward per layer."""
+
+    def __init__(self, needs):
+        self.needs_input_grad = needs
+        self.saved_tensors = ()
+
+    def save_for_backward(self, *tensors):
+        self.saved_tensors = tensors
+
+
+class ResidualUnitFn(torch.autograd.Function):
+    """ResidualUnit (layers.py:211-226) as one autograd node:
+    y = relu(conv1x1(relu(conv3x3(relu(conv1x1(x))))) + x), every ReLU in a conv epilogue (the residual add in the
+    last conv's, cai_conv_fwd_res), every ReLU mask in the next conv's dgrad epilogue, and x's two gradients (through
+    the convs and through the residual) summed in the first conv's dgrad epilogue (cai_conv_dgrad_res) instead of
+    an autograd gradient-sum launch.  Same kernels and arithmetic as the per-layer ConvFn chain otherwise."""
+
+    @staticmethod
+    def forward(ctx, x, w0, b0, w2, b2, w4, b4, specs):
+        s0, s2, s4 = specs
+        need = ctx.needs_input_grad
+        c0 = _SubCtx((need[0], need[1], need[2], False, False))
+        c2 = _SubCtx((True, need[3], need[4], False, False))
+        c4 = _SubCtx((True, need[5], need[6], False, True))
+        h = ConvFn.forward(c0, x, w0, b0, s0)
+        h = ConvFn.forward(c2, h, w2, b2, s2)
+        y = ConvFn.forward(c4, h, w4, b4, s4, x)
+        ctx.subs = (c0, c2, c4)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        c0, c2, c4 = ctx.subs
+        dh2, dw4, db4, _, g4 = ConvFn.backward(c4, gy)
+        dh1, dw2, db2, _, _ = ConvFn.backward(c2, dh2)
+        c0.dx_res = g4
+        dx, dw0, db0, _, _ = ConvFn.backward(c0, dh1)
+        ctx.subs = None
+        return dx, dw0, db0, dw2, db2, dw4, db4, None
 
 
 # ---------------------------------------------------------------------------
@@ -975,6 +1026,14 @@ def _unit_grad(device) -> torch.Tensor:
         t = torch.ones((), dtype=torch.float32, device=device)
         _UNIT_GRAD[device] = t
     return t
+
+
+def loss_seed(loss: torch.Tensor):
+    """The backward seed dloss/dloss = 1 of a scalar fp32 loss as a persistent device tensor (``loss.backward()``
+    would fill a fresh one: one more launch in every captured step); None (the default seed) otherwise."""
+    if loss.dim() == 0 and loss.dtype == torch.float32 and loss.is_cuda:
+        return _unit_grad(loss.device)
+    return None
 
 
 class BottleneckAuxFn(torch.autograd.Function):

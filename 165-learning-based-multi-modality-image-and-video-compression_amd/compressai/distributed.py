@@ -127,7 +127,10 @@ class OverlappedAllReduce:
             raise RuntimeError("OverlappedAllReduce: the forward did not reach the cut")
         # retain_graph: the engine releases the saved tensors of every node of the graph it was given,
         # including the tail's, which backward_tail still needs
-        torch.autograd.backward(loss, inputs=list(self._ys) + self.head_params, retain_graph=True)
+        from ._ops import loss_seed
+
+        torch.autograd.backward(loss, grad_tensors=loss_seed(loss), inputs=list(self._ys) + self.head_params,
+                                retain_graph=True)
 
     def backward_tail(self):
         ys, self._ys = self._ys, []

@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 
 from .._native import ACT_LEAKY, ACT_NONE, ACT_RELU, MASK_LEAKY, MASK_POS
-from .._ops import AddActFn, GateFn, residual_fusable
+from .._ops import AddActFn, GateFn, ResidualUnitFn, residual_fusable
 from .conv import Conv2d, ConvTranspose2d, PixelShuffle, Sequential
 from .gdn import GDN
 
@@ -130,10 +130,12 @@ class ResidualUnit(nn.Module):
         c = self.conv
         if not (self.fuse_residual and residual_fusable(c[4]._spec(act=ACT_RELU, in_mask=MASK_POS))):
             return AddActFn.apply(c(x), x, ACT_RELU, 0.0)
-        # the Sequential's fusion spelled out, with `+ x` and the trailing ReLU in the last conv's epilogue
-        h = c[0].run(x, act=ACT_RELU, act_bwd_downstream=True)
-        h = c[2].run(h, act=ACT_RELU, in_mask=MASK_POS, act_bwd_downstream=True)
-        return c[4].run(h, act=ACT_RELU, in_mask=MASK_POS, res=x)
+        # the Sequential's fusion as one autograd node, with `+ x` and the trailing ReLU in the last conv's
+        # epilogue and x's two gradients summed in the first conv's dgrad epilogue
+        specs = (c[0]._spec(act=ACT_RELU, act_bwd_downstream=True),
+                 c[2]._spec(act=ACT_RELU, in_mask=MASK_POS, act_bwd_downstream=True),
+                 c[4]._spec(act=ACT_RELU, in_mask=MASK_POS))
+        return ResidualUnitFn.apply(x, c[0].weight, c[0].bias, c[2].weight, c[2].bias, c[4].weight, c[4].bias, specs)
 
 
 class AttentionBlock(nn.Module):

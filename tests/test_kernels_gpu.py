@@ -651,7 +651,7 @@ def test_residual_unit_epilogue(cuda, B, N, H):
 
 
 def test_residual_unit_takes_fused_path(cuda, monkeypatch):
-    """The bf16 ResidualUnit forward launches cai_conv_fwd_res and no add_act kernel."""
+    """The bf16 ResidualUnit launches cai_conv_fwd_res forward, cai_conv_dgrad_res backward, no add_act kernel."""
     import compressai.layers as L
     from compressai import _ops
 
@@ -661,7 +661,7 @@ def test_residual_unit_takes_fused_path(cuda, monkeypatch):
     class Spy:
         def __getattr__(self, name):
             fn = getattr(real, name)
-            if name in ("cai_conv_fwd_res", "cai_add_act"):
+            if name in ("cai_conv_fwd_res", "cai_conv_dgrad_res", "cai_add_act"):
                 def wrapped(*a):
                     calls.append(name)
                     return fn(*a)
@@ -670,11 +670,13 @@ def test_residual_unit_takes_fused_path(cuda, monkeypatch):
 
     monkeypatch.setattr(_ops, "lib", Spy())
     mod = L.layers.ResidualUnit(64).to(cuda)
+    x = torch.randn(2, 64, 16, 16, device=cuda, requires_grad=True)
     with _autocast(True):
-        y = mod(torch.randn(2, 64, 16, 16, device=cuda))
+        y = mod(x)
+    y.float().sum().backward()
     torch.cuda.synchronize()
-    assert calls == ["cai_conv_fwd_res"], calls
-    assert torch.isfinite(y.float()).all()
+    assert calls == ["cai_conv_fwd_res", "cai_conv_dgrad_res"], calls
+    assert torch.isfinite(y.float()).all() and torch.isfinite(x.grad).all()
 
 
 @pytest.mark.parametrize("kind", ["deconv_fwd", "conv_dgrad"])
