@@ -598,7 +598,7 @@ class ConvFn(torch.autograd.Function):
         if ctx.small:
             return _small_deconv_bwd(ctx, xpm, weight, gy) + (None,)
         gpm, gld = to_pm(gy, dt, vec)
-        if spec.act != ACT_NONE and not spec.act_bwd_downstream:
+        if spec.act != ACT_NONE and not spec.act_bwd_downstream and not getattr(ctx, "gy_masked", False):
             mode = 1 if spec.act == 1 else 2
             out = empty_pm(g.batch, g.out_c, g.out_h, g.out_w, dt, gy.device)
             yld = pixel_major_ld(y)
@@ -616,11 +616,15 @@ class ConvFn(torch.autograd.Function):
             aux = xpm if spec.in_mask != MASK_NONE else None
             ws, wsb = _conv_ws(g, dt, 1, gy.device)
             fl, nb = _ledger.conv_cost(g, _es(dt), 1)
-            dres = getattr(ctx, "dx_res", None)   # ResidualUnitFn: + the residual's gradient, in the epilogue
+            # ResidualChainFn: + the residual's gradient in the epilogue (then the previous unit's ReLU mask)
+            dres = getattr(ctx, "dx_res", None)
+            rmask = getattr(ctx, "dx_res_mask", MASK_NONE)
             if dres is not None and dt == torch.bfloat16 and aux is None and ldx % 8 == 0:
                 rpm, rld = to_pm(dres, dt, 4)
+                maux = xpm if rmask != MASK_NONE else None
                 _ledger.run(lambda: lib.cai_conv_dgrad_res(ctypes.byref(g), code, _p(gpm), gld, _p(wt), _p(rpm), rld,
-                                                           _p(dx), ldx, _p(ws), wsb, st),
+                                                           _p(dx), ldx, rmask, 0.0, _p(maux),
+                                                           ctx.xld if maux is not None else 0, _p(ws), wsb, st),
                             "conv_dgrad", _conv_kernel(g, dt, 1), fl, nb, dt, _ledger.shape_of(g))
             else:
                 _ledger.run(lambda: lib.cai_conv_dgrad(ctypes.byref(g), code, _p(gpm), gld, _p(wt), _p(dx), ldx,
@@ -629,6 +633,8 @@ class ConvFn(torch.autograd.Function):
                             "conv_dgrad", _conv_kernel(g, dt, 1), fl, nb, dt, _ledger.shape_of(g))
                 if dres is not None:
                     dx = dx + dres
+                if rmask != MASK_NONE:
+                    raise RuntimeError("conv dgrad: a residual-gradient mask needs the fused bf16 path")
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             nbytes = lib.cai_conv_wgrad_workspace_bytes(ctypes.byref(g), code)
             wparam, bparam = ctx.params
@@ -674,35 +680,51 @@ class _SubCtx:
         self.saved_tensors = tensors
 
 
-class ResidualUnitFn(torch.autograd.Function):
-    """ResidualUnit (layers.py:211-226) as one autograd node:
-    y = relu(conv1x1(relu(conv3x3(relu(conv1x1(x))))) + x), every ReLU in a conv epilogue (the residual add in the
-    last conv's, cai_conv_fwd_res), every ReLU mask in the next conv's dgrad epilogue, and x's two gradients (through
-    the convs and through the residual) summed in the first conv's dgrad epilogue (cai_conv_dgrad_res) instead of
-    an autograd gradient-sum launch.  Same kernels and arithmetic as the per-layer ConvFn chain otherwise."""
+class ResidualChainFn(torch.autograd.Function):
+    """A chain of ResidualUnits (layers.py:211-226; AttentionBlock's conv_a / conv_b, :225-236) as one autograd
+    node.  Unit k: y_k = relu(conv1x1(relu(conv3x3(relu(conv1x1(y_{k-1}))))) + y_{k-1}), every ReLU in a conv
+    epilogue (the residual add in the last conv's, cai_conv_fwd_res), every ReLU mask in the next conv's dgrad
+    epilogue.  Backward: a unit input's two gradients (through the convs and through the residual) are summed in
+    the first conv's dgrad epilogue (cai_conv_dgrad_res), which inside the chain also applies the previous unit's
+    trailing ReLU mask (y_{k-1} > 0) -- so only the chain's last unit runs an activation-backward launch.  Same
+    kernels and arithmetic as the per-layer ConvFn chain otherwise.
+
+    params: (w0, b0, w2, b2, w4, b4) per unit; specs: ((s0, s2, s4), ...) per unit."""
 
     @staticmethod
-    def forward(ctx, x, w0, b0, w2, b2, w4, b4, specs):
-        s0, s2, s4 = specs
+    def forward(ctx, x, specs, *params):
         need = ctx.needs_input_grad
-        c0 = _SubCtx((need[0], need[1], need[2], False, False))
-        c2 = _SubCtx((True, need[3], need[4], False, False))
-        c4 = _SubCtx((True, need[5], need[6], False, True))
-        h = ConvFn.forward(c0, x, w0, b0, s0)
-        h = ConvFn.forward(c2, h, w2, b2, s2)
-        y = ConvFn.forward(c4, h, w4, b4, s4, x)
-        ctx.subs = (c0, c2, c4)
+        subs = []
+        y = x
+        for k, (s0, s2, s4) in enumerate(specs):
+            w0, b0, w2, b2, w4, b4 = params[6 * k:6 * k + 6]
+            pn = need[2 + 6 * k:8 + 6 * k]
+            c0 = _SubCtx((need[0] or k > 0, pn[0], pn[1], False, False))
+            c2 = _SubCtx((True, pn[2], pn[3], False, False))
+            c4 = _SubCtx((True, pn[4], pn[5], False, True))
+            h = ConvFn.forward(c0, y, w0, b0, s0)
+            h = ConvFn.forward(c2, h, w2, b2, s2)
+            y = ConvFn.forward(c4, h, w4, b4, s4, y)
+            if k > 0:   # this unit's input is the previous unit's ReLU output: mask its gradient here
+                c0.dx_res_mask = MASK_POS
+                subs[-1][2].gy_masked = True
+            subs.append((c0, c2, c4))
+        ctx.subs = subs
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        c0, c2, c4 = ctx.subs
-        dh2, dw4, db4, _, g4 = ConvFn.backward(c4, gy)
-        dh1, dw2, db2, _, _ = ConvFn.backward(c2, dh2)
-        c0.dx_res = g4
-        dx, dw0, db0, _, _ = ConvFn.backward(c0, dh1)
+        grads = []
+        g = gy
+        for c0, c2, c4 in reversed(ctx.subs):
+            dh2, dw4, db4, _, g4 = ConvFn.backward(c4, g)
+            dh1, dw2, db2, _, _ = ConvFn.backward(c2, dh2)
+            c0.dx_res = g4
+            g, dw0, db0, _, _ = ConvFn.backward(c0, dh1)
+            grads.append((dw0, db0, dw2, db2, dw4, db4))
         ctx.subs = None
-        return dx, dw0, db0, dw2, db2, dw4, db4, None
+        flat = [t for unit in reversed(grads) for t in unit]
+        return (g, None, *flat)
 
 
 # ---------------------------------------------------------------------------

@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 
 from .._native import ACT_LEAKY, ACT_NONE, ACT_RELU, MASK_LEAKY, MASK_POS
-from .._ops import AddActFn, GateFn, ResidualUnitFn, residual_fusable
+from .._ops import AddActFn, GateFn, ResidualChainFn, residual_fusable
 from .conv import Conv2d, ConvTranspose2d, PixelShuffle, Sequential
 from .gdn import GDN
 
@@ -126,16 +126,36 @@ class ResidualUnit(nn.Module):
     # False: the unfused chain (Sequential, then add + ReLU on the elementwise kernel); CAI_RESIDUAL_FUSE=0 for A/Bs
     fuse_residual = os.environ.get("CAI_RESIDUAL_FUSE", "1") != "0"
 
-    def forward(self, x):
+    def fusable(self) -> bool:
+        return self.fuse_residual and residual_fusable(self.conv[4]._spec(act=ACT_RELU, in_mask=MASK_POS))
+
+    def chain_args(self):
+        """(specs, params) of this unit in ResidualChainFn: the Sequential's fusion, with `+ x` and the trailing
+        ReLU in the last conv's epilogue."""
         c = self.conv
-        if not (self.fuse_residual and residual_fusable(c[4]._spec(act=ACT_RELU, in_mask=MASK_POS))):
-            return AddActFn.apply(c(x), x, ACT_RELU, 0.0)
-        # the Sequential's fusion as one autograd node, with `+ x` and the trailing ReLU in the last conv's
-        # epilogue and x's two gradients summed in the first conv's dgrad epilogue
         specs = (c[0]._spec(act=ACT_RELU, act_bwd_downstream=True),
                  c[2]._spec(act=ACT_RELU, in_mask=MASK_POS, act_bwd_downstream=True),
                  c[4]._spec(act=ACT_RELU, in_mask=MASK_POS))
-        return ResidualUnitFn.apply(x, c[0].weight, c[0].bias, c[2].weight, c[2].bias, c[4].weight, c[4].bias, specs)
+        return specs, (c[0].weight, c[0].bias, c[2].weight, c[2].bias, c[4].weight, c[4].bias)
+
+    def forward(self, x):
+        if not self.fusable():
+            return AddActFn.apply(self.conv(x), x, ACT_RELU, 0.0)
+        return residual_chain([self], x)
+
+
+def residual_chain(units, x):
+    """ResidualUnits applied in sequence, as one ResidualChainFn node when every unit is fusable."""
+    if not all(u.fusable() for u in units):
+        for u in units:
+            x = u(x)
+        return x
+    specs, params = [], []
+    for u in units:
+        sp, pr = u.chain_args()
+        specs.append(sp)
+        params.extend(pr)
+    return ResidualChainFn.apply(x, tuple(specs), *params)
 
 
 class AttentionBlock(nn.Module):
@@ -147,6 +167,7 @@ class AttentionBlock(nn.Module):
         self.conv_b = Sequential(ResidualUnit(N), ResidualUnit(N), ResidualUnit(N), conv1x1(N, N))
 
     def forward(self, x):
-        a = self.conv_a(x)
-        b = self.conv_b(x)
+        # each branch's three ResidualUnits as one chain node (layers.py:225-236)
+        a = residual_chain(list(self.conv_a), x)
+        b = self.conv_b[3](residual_chain(list(self.conv_b)[:3], x))
         return GateFn.apply(a, b, x)

@@ -3543,8 +3543,9 @@ static int run_conv(const cai_conv_geom* g, int dtype, int direction, const void
     a.bias = bias; a.act = act; a.act_param = act_param;
     a.aux = aux; a.aux_ld = aux_ld; a.mask_mode = mask_mode; a.mask_param = mask_param;
     // residual: bf16 pixel-major, 8-byte aligned 4-channel groups, added before the activation (forward) or to
-    // the unmasked input gradient (dgrad)
-    CAI_CHECK_ARG(!res || (direction != 2 && dtype == CAI_BF16 && a.y_vec && y_dtype == CAI_BF16 && !mask_mode &&
+    // the input gradient before its mask (dgrad)
+    CAI_CHECK_ARG(!res || (direction != 2 && dtype == CAI_BF16 && a.y_vec && y_dtype == CAI_BF16 &&
+                           (!mask_mode || direction == 1) &&
                            res_ld >= P.kout_c && res_ld % 4 == 0 && ((uintptr_t)res & 7) == 0),
                   "%s: residual needs a bf16 pixel-major output and res_ld >= Cout, a multiple of 4", name);
     a.res = reinterpret_cast<const bf16*>(res); a.res_ld = res_ld;
@@ -3940,14 +3941,14 @@ int cai_conv_dgrad(const cai_conv_geom* g, int dtype, const void* dy, int32_t dy
 }
 
 int cai_conv_dgrad_res(const cai_conv_geom* g, int dtype, const void* dy, int32_t dy_ld, const void* packed_wt,
-                       const void* res, int32_t res_ld, void* dx, int32_t dx_ld, void* workspace, size_t ws_bytes,
-                       void* stream) {
+                       const void* res, int32_t res_ld, void* dx, int32_t dx_ld, int32_t mask_mode, float mask_param,
+                       const void* aux, int32_t aux_ld, void* workspace, size_t ws_bytes, void* stream) {
     int rc = check_geom(g);
     if (rc) return rc;
     CAI_CHECK_ARG(res, "conv_dgrad_res: null residual");
     const int64_t ld = dx_ld;
     return run_conv(g, dtype, 1, dy, dy_ld, 0, packed_wt, nullptr, CAI_ACT_NONE, 0.f, dx, dtype,
-                    (int64_t)g->in_h * g->in_w * ld, 1, (int64_t)g->in_w * ld, ld, nullptr, 0, CAI_MASK_NONE, 0.f,
+                    (int64_t)g->in_h * g->in_w * ld, 1, (int64_t)g->in_w * ld, ld, aux, aux_ld, mask_mode, mask_param,
                     workspace, ws_bytes, stream, "conv_dgrad_res", res, res_ld);
 }
 

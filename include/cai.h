@@ -153,13 +153,15 @@ int cai_conv_dgrad(const cai_conv_geom* g, int dtype,
                    int32_t mask_mode, float mask_param, const void* aux, int32_t aux_ld,
                    void* workspace, size_t ws_bytes, void* stream);
 
-/* input gradient plus a residual gradient: dx = conv_input_grad(dy) + res (bf16,
- * no mask), the gradient of a ResidualUnit's input (layers.py:211-226: x feeds
- * the first conv and the `out += identity` add) in the first conv's dgrad
- * epilogue instead of a separate sum.  res pixel-major as in cai_conv_fwd_res. */
+/* input gradient plus a residual gradient: dx = mask(aux) * (conv_input_grad(dy)
+ * + res) (bf16), the gradient of a ResidualUnit's input (layers.py:211-226: x
+ * feeds the first conv and the `out += identity` add) in the first conv's dgrad
+ * epilogue instead of a separate sum; the mask (MASK_POS on the unit's input)
+ * is the previous unit's trailing ReLU.  res pixel-major as in cai_conv_fwd_res. */
 int cai_conv_dgrad_res(const cai_conv_geom* g, int dtype,
                        const void* dy, int32_t dy_ld, const void* packed_wt,
                        const void* res, int32_t res_ld, void* dx, int32_t dx_ld,
+                       int32_t mask_mode, float mask_param, const void* aux, int32_t aux_ld,
                        void* workspace, size_t ws_bytes, void* stream);
 
 /* Diagnostics for measurement (bench.py's per-launch roofline):
