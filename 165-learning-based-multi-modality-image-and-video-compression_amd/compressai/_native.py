@@ -118,7 +118,7 @@ SIGNATURES = {
     "cai_gdn1_out_bwd": (_I, [_I, _P, c_int32, _P, c_int32, _P, c_int32, _P, c_int32, _P, c_int32, _I64, c_int32,
                               c_int32, _P]),
     "cai_gate_fwd": (_I, [_I, _P, _P, _P, _P, c_int32, _I64, c_int32, _P]),
-    "cai_gate_bwd": (_I, [_I, _P, _P, _P, c_int32, _P, _P, c_int32, _I64, c_int32, _P]),
+    "cai_gate_bwd": (_I, [_I, _P, _P, _P, c_int32, _P, _P, c_int32, _I64, c_int32, c_int32, _P]),
     "cai_pixel_shuffle": (_I, [_I, _P, POINTER(c_int64), _P, POINTER(c_int64), c_int32, c_int32, c_int32, c_int32,
                                c_int32, c_int32, _P]),
     "cai_layernorm_fwd": (_I, [_I, _P, c_int32, _I64, c_int32, _P, _P, _F, _P, c_int32, _P, _P, _P]),

@@ -689,16 +689,17 @@ class ResidualChainFn(torch.autograd.Function):
     trailing ReLU mask (y_{k-1} > 0) -- so only the chain's last unit runs an activation-backward launch.  Same
     kernels and arithmetic as the per-layer ConvFn chain otherwise.
 
-    params: (w0, b0, w2, b2, w4, b4) per unit; specs: ((s0, s2, s4), ...) per unit."""
+    params: (w0, b0, w2, b2, w4, b4) per unit; specs: ((s0, s2, s4), ...) per unit; out_masked: the chain's
+    consumer applies the last unit's ReLU mask to the gradient it returns."""
 
     @staticmethod
-    def forward(ctx, x, specs, *params):
-        need = ctx.needs_input_grad
+    def forward(ctx, x, specs, out_masked, *params):
+        need = ctx.needs_input_grad   # (x, specs, out_masked, *params)
         subs = []
         y = x
         for k, (s0, s2, s4) in enumerate(specs):
             w0, b0, w2, b2, w4, b4 = params[6 * k:6 * k + 6]
-            pn = need[2 + 6 * k:8 + 6 * k]
+            pn = need[3 + 6 * k:9 + 6 * k]
             c0 = _SubCtx((need[0] or k > 0, pn[0], pn[1], False, False))
             c2 = _SubCtx((True, pn[2], pn[3], False, False))
             c4 = _SubCtx((True, pn[4], pn[5], False, True))
@@ -709,6 +710,8 @@ class ResidualChainFn(torch.autograd.Function):
                 c0.dx_res_mask = MASK_POS
                 subs[-1][2].gy_masked = True
             subs.append((c0, c2, c4))
+        if out_masked:   # the consumer (a MASK_POS dgrad, GateFn relu_a) hands back the masked gradient
+            subs[-1][2].gy_masked = True
         ctx.subs = subs
         return y
 
@@ -724,7 +727,7 @@ class ResidualChainFn(torch.autograd.Function):
             grads.append((dw0, db0, dw2, db2, dw4, db4))
         ctx.subs = None
         flat = [t for unit in reversed(grads) for t in unit]
-        return (g, None, *flat)
+        return (g, None, None, *flat)
 
 
 # ---------------------------------------------------------------------------
@@ -1300,10 +1303,11 @@ class ActFn(torch.autograd.Function):
 
 
 class GateFn(torch.autograd.Function):
-    """AttentionBlock (layers.py:238-243): y = a * sigmoid(b) + x."""
+    """AttentionBlock (layers.py:238-243): y = a * sigmoid(b) + x.  relu_a: a is a ReLU output whose producer
+    (ResidualChainFn with out_masked) expects its gradient already masked: da carries the mask."""
 
     @staticmethod
-    def forward(ctx, a, b, x):
+    def forward(ctx, a, b, x, relu_a: bool = False):
         _check_cuda(a, b, x)
         dt = compute_dtype()
         B, C, H, W = a.shape
@@ -1320,22 +1324,22 @@ class GateFn(torch.autograd.Function):
         y = empty_pm(B, C, H, W, dt, a.device, ld=ld)
         _ledger.run(lambda: lib.cai_gate_fwd(dcode(dt), _p(ap), _p(bp), _p(xp), _p(y), ld, B * H * W, C, _stream()),
                     "gate_fwd", "gate_fwd_kernel", 0, 4 * B * H * W * C * _es(dt), dt)
-        ctx.cfg = (dt, ld)
+        ctx.cfg = (dt, ld, int(relu_a))
         ctx.save_for_backward(ap, bp)
         return y
 
     @staticmethod
     def backward(ctx, g):
         ap, bp = ctx.saved_tensors
-        dt, ld = ctx.cfg
+        dt, ld, relu_a = ctx.cfg
         B, C, H, W = ap.shape
         gp, gld = to_pm(g, dt, _vec(dt))
         da = empty_pm(B, C, H, W, dt, g.device, ld=ld)
         db = empty_pm(B, C, H, W, dt, g.device, ld=ld)
         _ledger.run(lambda: lib.cai_gate_bwd(dcode(dt), _p(ap), _p(bp), _p(gp), gld, _p(da), _p(db), ld, B * H * W, C,
-                                             _stream()),
+                                             relu_a, _stream()),
                     "gate_bwd", "gate_bwd_kernel", 0, 5 * B * H * W * C * _es(dt), dt)
-        return da, db, g
+        return da, db, g, None
 
 
 def _bhwc_strides(t: torch.Tensor):

@@ -144,18 +144,19 @@ class ResidualUnit(nn.Module):
         return residual_chain([self], x)
 
 
-def residual_chain(units, x):
-    """ResidualUnits applied in sequence, as one ResidualChainFn node when every unit is fusable."""
-    if not all(u.fusable() for u in units):
-        for u in units:
-            x = u(x)
-        return x
+def chain_fusable(units) -> bool:
+    return all(u.fusable() for u in units)
+
+
+def residual_chain(units, x, out_masked: bool = False):
+    """ResidualUnits applied in sequence, as one ResidualChainFn node (fusable units only).  out_masked: the
+    caller's consumer applies the last unit's ReLU mask to the gradient (MASK_POS dgrad, GateFn relu_a)."""
     specs, params = [], []
     for u in units:
         sp, pr = u.chain_args()
         specs.append(sp)
         params.extend(pr)
-    return ResidualChainFn.apply(x, tuple(specs), *params)
+    return ResidualChainFn.apply(x, tuple(specs), bool(out_masked), *params)
 
 
 class AttentionBlock(nn.Module):
@@ -167,7 +168,11 @@ class AttentionBlock(nn.Module):
         self.conv_b = Sequential(ResidualUnit(N), ResidualUnit(N), ResidualUnit(N), conv1x1(N, N))
 
     def forward(self, x):
-        # each branch's three ResidualUnits as one chain node (layers.py:225-236)
-        a = residual_chain(list(self.conv_a), x)
-        b = self.conv_b[3](residual_chain(list(self.conv_b)[:3], x))
-        return GateFn.apply(a, b, x)
+        ua, ub = list(self.conv_a), list(self.conv_b)[:3]
+        if not (chain_fusable(ua) and chain_fusable(ub)):
+            return GateFn.apply(self.conv_a(x), self.conv_b(x), x)
+        # each branch's three ResidualUnits as one chain node (layers.py:225-236); the chains' last ReLU masks
+        # in their consumers' backward: conv_b's 1x1 conv dgrad (MASK_POS) and the gate's da
+        a = residual_chain(ua, x, out_masked=True)
+        b = self.conv_b[3].run(residual_chain(ub, x, out_masked=True), in_mask=MASK_POS)
+        return GateFn.apply(a, b, x, True)

@@ -95,15 +95,17 @@ __global__ void gate_fwd_kernel(const T* __restrict__ a, const T* __restrict__ b
 
 template <typename T>
 __global__ void gate_bwd_kernel(const T* __restrict__ a, const T* __restrict__ b, const T* __restrict__ g, int gld,
-                                T* __restrict__ da, T* __restrict__ db, int ld, int npix, int C) {
+                                T* __restrict__ da, T* __restrict__ db, int ld, int npix, int C, int relu_a) {
     const int64_t total = (int64_t)npix * C;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
         const int p = (int)(i / C), c = (int)(i - (int64_t)p * C);
         const int64_t o = (int64_t)p * ld + c;
         const float s = sigmoidf_(to_f32(b[o]));
         const float gv = to_f32(g[(int64_t)p * gld + c]);
-        da[o] = from_f32<T>(gv * s);
-        db[o] = from_f32<T>(gv * to_f32(a[o]) * s * (1.f - s));
+        const float av = to_f32(a[o]);
+        // relu_a: a is a ReLU output (AttentionBlock's conv_a chain): its mask applied here, not in a launch of its own
+        da[o] = from_f32<T>(relu_a && !(av > 0.f) ? 0.f : gv * s);
+        db[o] = from_f32<T>(gv * av * s * (1.f - s));
     }
 }
 
@@ -296,7 +298,7 @@ int cai_gate_fwd(int dtype, const void* a, const void* b, const void* x, void* y
 }
 
 int cai_gate_bwd(int dtype, const void* a, const void* b, const void* g, int32_t g_ld, void* da, void* db, int32_t ld,
-                 int64_t npix, int32_t C, void* stream) {
+                 int64_t npix, int32_t C, int32_t relu_a, void* stream) {
     CAI_CHECK_ARG(dtype == CAI_BF16 || dtype == CAI_F32, "gate_bwd: bad dtype");
     CAI_CHECK_ARG(a && b && g && da && db && ld >= C && g_ld >= C && npix < (1ll << 31), "gate_bwd: bad arguments");
     const int64_t n = npix * C;
@@ -304,10 +306,11 @@ int cai_gate_bwd(int dtype, const void* a, const void* b, const void* g, int32_t
     hipStream_t st = as_stream(stream);
     if (dtype == CAI_BF16)
         hipLaunchKernelGGL(gate_bwd_kernel<bf16>, dim3(ew_grid2(n)), dim3(256), 0, st, (const bf16*)a, (const bf16*)b,
-                           (const bf16*)g, g_ld, (bf16*)da, (bf16*)db, ld, (int)npix, C);
+                           (const bf16*)g, g_ld, (bf16*)da, (bf16*)db, ld, (int)npix, C, (int)relu_a);
     else
         hipLaunchKernelGGL(gate_bwd_kernel<float>, dim3(ew_grid2(n)), dim3(256), 0, st, (const float*)a,
-                           (const float*)b, (const float*)g, g_ld, (float*)da, (float*)db, ld, (int)npix, C);
+                           (const float*)b, (const float*)g, g_ld, (float*)da, (float*)db, ld, (int)npix, C,
+                           (int)relu_a);
     CAI_LAUNCH_CHECK("gate_bwd");
     return CAI_OK;
 }

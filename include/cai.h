@@ -282,8 +282,9 @@ int cai_gdn1_out_bwd(int dtype, const void* x, int32_t x_ld, const void* norm, i
                      int32_t inverse, void* stream);
 int cai_gate_fwd(int dtype, const void* a, const void* b, const void* x, void* y, int32_t ld, int64_t npix, int32_t C,
                  void* stream);
+/* relu_a != 0: a is a ReLU output and da carries its mask (da = g sigmoid(b) [a > 0]) */
 int cai_gate_bwd(int dtype, const void* a, const void* b, const void* g, int32_t g_ld, void* da, void* db, int32_t ld,
-                 int64_t npix, int32_t C, void* stream);
+                 int64_t npix, int32_t C, int32_t relu_a, void* stream);
 /* nn.PixelShuffle(r) of subpel_conv3x3 (layers.py:86-91) between
  * x[B][H][W][C*r*r] and y[B][H*r][W*r][C], each side described by element
  * strides {batch, row, column, channel}; inverse != 0 maps y back to x
