@@ -9,7 +9,16 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 flt = sys.argv[2] if len(sys.argv) > 2 else None
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if "pack_many" in r["Kernel_Name"]]
-step = rows[idx[-2]:idx[-1]]
+# the last complete step: a pack_many-to-pack_many range whose gaps are all short (the tail after the timed steps
+# holds host-side waits and copies)
+step = None
+for k in range(len(idx) - 1, 0, -1):
+    cand = rows[idx[k - 1]:idx[k]]
+    gaps = [int(b["Start_Timestamp"]) - int(a["End_Timestamp"]) for a, b in zip(cand, cand[1:])]
+    if cand and max(gaps, default=0) < 50_000:
+        step = cand
+        break
+step = step or rows[idx[-2]:idx[-1]]
 t0 = int(step[0]["Start_Timestamp"])
 end = t0
 tot = defaultdict(float)
