@@ -141,6 +141,7 @@ SIGNATURES = {
     "cai_gdn_param_grad_workspace_bytes": (_S, [_I64, c_int32, _I]),
     "cai_gdn_param_grad": (_I, [_I, _P, c_int32, _P, _I64, c_int32, _P, _P, _F, _F, _P, _P, c_int32, _P, _S, _P]),
     "cai_gdn_backward_workspace_bytes": (_S, [_I64, c_int32, _I]),
+    "cai_gdn_kernel_name": (c_char_p, [_I, _I64, c_int32, c_int32, c_int32, c_int32]),
     "cai_gdn_backward": (_I, [_I, _P, c_int32, _P, c_int32, _I64, c_int32, _P, _P, c_int32, _P, c_int32, _P, _P, _F, _F,
                               _P, _P, c_int32, _P, _S, _P]),
     "cai_gdn_backward_deferred": (_I, [_I, _P, c_int32, _P, c_int32, _I64, c_int32, _P, _P, c_int32, _P, c_int32, _P,

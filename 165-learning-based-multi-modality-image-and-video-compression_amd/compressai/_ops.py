@@ -21,6 +21,7 @@ from __future__ import annotations
 import ctypes
 import math
 import os
+import warnings
 from typing import Optional, Sequence, Tuple
 
 import torch
@@ -31,7 +32,7 @@ from ._native import (ACT_LEAKY, ACT_NONE, ACT_RELU, BF16, F32, MASK_LEAKY, MASK
                       RdInputs, ReduceJob, lib)
 
 _VP = ctypes.c_void_p
-_GDN_TWO_PASS = os.environ.get("CAI_GDN_TWO_PASS", "0") == "1"   # A/B knobs (tools/gpu_ab.sh)
+_GDN_TWO_PASS = os.environ.get("CAI_GDN_TWO_PASS", "0") == "1"   # A/B knobs (tools/ab_env.sh)
 _RD_UNFUSED = os.environ.get("CAI_RD_UNFUSED", "0") == "1"
 _EDGE_OFF = os.environ.get("CAI_EDGE_OFF", "0") == "1"
 
@@ -129,16 +130,17 @@ class _WgradLaunch:
 # gradient runs on the side stream.  CAI_DEFER_REDUCE=0 turns it off (A/B).
 _DEFER_REDUCE = os.environ.get("CAI_DEFER_REDUCE", "1") == "1"
 _REDUCE_SPLIT = os.environ.get("CAI_REDUCE_SPLIT", "0") == "1"   # diagnostics: one launch per deferred job
-_JOBS = {}          # device index -> [jobs, their streams, keep-alive tensors]
+_JOBS = {}          # (device index, graph task id) -> [jobs, their streams, keep-alive tensors]
 
 
-def _flush_jobs(dev):
-    """Run the queued jobs of `dev` on the current stream (the backward caller's, as DDP's finalize uses it),
-    after it has waited for every other stream a job's partial kernel ran on (the hyper branch's side stream:
-    inside a captured graph this is the join edge)."""
-    pend = _JOBS.pop(dev, None)
+def _flush_jobs(key):
+    """Run the jobs queued under `key` = (device, graph task) on the current stream (the backward caller's, as
+    DDP's finalize uses it), after it has waited for every other stream a job's partial kernel ran on (the
+    hyper branch's side stream: inside a captured graph this is the join edge)."""
+    pend = _JOBS.pop(key, None)
     if not pend or not pend[0]:
         return
+    dev = key[0]
     jobs, streams, keep = pend
     cur = torch.cuda.current_stream(dev)
     for s in {s.cuda_stream: s for s in streams}.values():
@@ -156,18 +158,27 @@ def _flush_jobs(dev):
 
 
 def defer_reduce_ok(direct: bool) -> bool:
-    return _DEFER_REDUCE and direct and _ledger.active() is None and not _WGRAD_STREAM
+    """Deferred only inside a running backward (its final callback runs the jobs)."""
+    return (_DEFER_REDUCE and direct and _ledger.active() is None and not _WGRAD_STREAM
+            and torch._C._current_graph_task_id() >= 0)
 
 
 def defer_job(job: "ReduceJob", device: torch.device, *keep: torch.Tensor):
-    """Queue `job` (filled by a cai_*_deferred call on the current stream) until the end of this backward."""
+    """Queue `job` (filled by a cai_*_deferred call on the current stream) until the end of this backward.
+
+    The queue is keyed on the running graph task, so concurrent backwards (one host thread per replica) keep
+    their own queues and each backward registers its own final callback: a backward that raised before its
+    callback ran leaves only its own (never-run) entry behind, not a queue that later backwards would join
+    without a flush.  Two jobs writing the same gradient (a module called twice in one forward) run in
+    separate launches, in queue order (csrc/reduce_jobs.hip launch_reduce_jobs)."""
     if job.kind == JOB_NONE:
         return
     dev = device.index if device.index is not None else torch.cuda.current_device()
-    pend = _JOBS.get(dev)
+    key = (dev, torch._C._current_graph_task_id())
+    pend = _JOBS.get(key)
     if pend is None:
-        pend = _JOBS[dev] = [[], [], []]
-        torch.autograd.Variable._execution_engine.queue_callback(lambda: _flush_jobs(dev))
+        pend = _JOBS[key] = [[], [], []]
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: _flush_jobs(key))
     pend[0].append(job)
     pend[1].append(torch.cuda.current_stream(dev))
     pend[2].extend(t for t in keep if t is not None)
@@ -175,8 +186,8 @@ def defer_job(job: "ReduceJob", device: torch.device, *keep: torch.Tensor):
 
 def flush_deferred_reduces():
     """Run every queued reduce now (callers that drive the kernels outside autograd)."""
-    for dev in list(_JOBS):
-        _flush_jobs(dev)
+    for key in list(_JOBS):
+        _flush_jobs(key)
 
 
 def _p(t: Optional[torch.Tensor]) -> Optional[_VP]:
@@ -191,14 +202,17 @@ def dcode(dtype: torch.dtype) -> int:
     raise ValueError(f"unsupported dtype {dtype} (bf16 / fp32 only)")
 
 
-_FP16_POLICY = os.environ.get("CAI_FP16_AUTOCAST", "error")   # "error" | "bf16"
+_FP16_POLICY = os.environ.get("CAI_FP16_AUTOCAST", "bf16")   # "bf16" | "error"
+_FP16_WARNED = False
 
 
 def set_fp16_autocast_policy(policy: str):
-    """What fp16 autocast means for this build: "error" (default) raises, "bf16" computes in bf16.
+    """What fp16 autocast means for this build: "bf16" (default) computes the region in bf16, "error" raises.
 
     The reference trains under ``torch.cuda.amp.autocast()`` (fp16, examples/train.py:172,239).  The kernels
-    here have bf16 and fp32 paths only; running an fp16 region in bf16 has to be asked for explicitly."""
+    here have bf16 and fp32 paths only (fp32 MFMA accumulation either way); bf16 keeps fp32's exponent range,
+    so the fp16 GradScaler the reference pairs with autocast (train.py:174-186) works unchanged -- its scaled
+    gradients just never overflow.  A one-time warning says so; "error" restores the strict behaviour."""
     global _FP16_POLICY
     if policy not in ("error", "bf16"):
         raise ValueError(f"fp16 autocast policy must be 'error' or 'bf16', got {policy!r}")
@@ -206,15 +220,20 @@ def set_fp16_autocast_policy(policy: str):
 
 
 def compute_dtype() -> torch.dtype:
-    """bf16 inside torch.autocast('cuda', dtype=torch.bfloat16), exact fp32 outside autocast.
-
-    fp16 autocast raises unless set_fp16_autocast_policy("bf16") (or CAI_FP16_AUTOCAST=bf16) asked for bf16."""
+    """bf16 inside torch.autocast('cuda', dtype=torch.bfloat16) -- and, by default, inside an fp16 autocast
+    region (one warning per process) -- exact fp32 outside autocast."""
+    global _FP16_WARNED
     if not torch.is_autocast_enabled("cuda"):
         return torch.float32
     dt = torch.get_autocast_dtype("cuda")
     if dt == torch.bfloat16:
         return dt
     if dt == torch.float16 and _FP16_POLICY == "bf16":
+        if not _FP16_WARNED:
+            _FP16_WARNED = True
+            warnings.warn("compressai (MI355X build): fp16 autocast regions run the bf16 kernels (fp32 accumulate); "
+                          "compressai.set_fp16_autocast_policy('error') makes this an error", RuntimeWarning,
+                          stacklevel=3)
         return torch.bfloat16
     raise RuntimeError(
         f"autocast dtype {dt} is not supported by the MI355X kernels (bf16 / fp32 only): use "
@@ -712,20 +731,39 @@ class ResidualChainFn(torch.autograd.Function):
             subs.append((c0, c2, c4))
         if out_masked:   # the consumer (a MASK_POS dgrad, GateFn relu_a) hands back the masked gradient
             subs[-1][2].gy_masked = True
-        ctx.subs = subs
+        # every sub-conv's tensors go through save_for_backward (version-counter checks, no y -> grad_fn -> ctx
+        # -> y reference cycle); the stand-in contexts keep only metadata between forward and backward
+        flat, counts = [], []
+        for trio in subs:
+            for c in trio:
+                counts.append(len(c.saved_tensors))
+                flat.extend(c.saved_tensors)
+                c.saved_tensors = ()
+        ctx.save_for_backward(*flat)
+        ctx.subs, ctx.counts = subs, counts
         return y
 
     @staticmethod
     def backward(ctx, gy):
+        saved = ctx.saved_tensors
+        subs = [c for trio in ctx.subs for c in trio]
+        i = 0
+        for c, n in zip(subs, ctx.counts):
+            c.saved_tensors = tuple(saved[i:i + n])
+            i += n
         grads = []
         g = gy
-        for c0, c2, c4 in reversed(ctx.subs):
-            dh2, dw4, db4, _, g4 = ConvFn.backward(c4, g)
-            dh1, dw2, db2, _, _ = ConvFn.backward(c2, dh2)
-            c0.dx_res = g4
-            g, dw0, db0, _, _ = ConvFn.backward(c0, dh1)
-            grads.append((dw0, db0, dw2, db2, dw4, db4))
-        ctx.subs = None
+        try:
+            for c0, c2, c4 in reversed(ctx.subs):
+                dh2, dw4, db4, _, g4 = ConvFn.backward(c4, g)
+                dh1, dw2, db2, _, _ = ConvFn.backward(c2, dh2)
+                c0.dx_res = g4
+                g, dw0, db0, _, _ = ConvFn.backward(c0, dh1)
+                grads.append((dw0, db0, dw2, db2, dw4, db4))
+        finally:
+            for c in subs:     # retain_graph: a second backward restores them from ctx.saved_tensors again
+                c.saved_tensors = ()
+                c.dx_res = None
         flat = [t for unit in reversed(grads) for t in unit]
         return (g, None, None, *flat)
 
@@ -758,7 +796,7 @@ class GdnFn(torch.autograd.Function):
             lib.cai_gdn_reparam(_p(br), _p(gr), C, beta_min, reparam_offset, code, _p(beta), _p(gop), st)
         y = empty_pm(B, C, H, W, dt, x.device)
         _ledger.run(lambda: lib.cai_gdn_fwd(code, _p(xpm), xld, npix, C, _p(gop), _p(beta), int(inverse), _p(y), C, st),
-                    "gdn_fwd", "gdn_fwd_kernel", 2.0 * npix * C * C, 2 * npix * C * _es(dt) + C * C * _es(dt), dt,
+                    "gdn_fwd", lambda: lib.cai_gdn_kernel_name(code, npix, C, xld, C, 0).decode(), 2.0 * npix * C * C, 2 * npix * C * _es(dt) + C * C * _es(dt), dt,
                     f"{'IGDN' if inverse else 'GDN'} C={C} npix={npix}")
         ctx.save_for_backward(xpm, br, gr, beta, gop)
         ctx.cfg = (dt, xld, int(inverse), float(beta_min), float(reparam_offset))
@@ -804,7 +842,8 @@ class GdnFn(torch.autograd.Function):
                                                                       _p(beta), inverse, _p(dx), C, _p(br), _p(gr),
                                                                       beta_min, off, _p(dbr), _p(dgr), int(direct),
                                                                       _p(ws), nbytes, st),
-                        "gdn_bwd", "gdn_bwd (fused / two-pass)", 4.0 * npix * C * C,
+                        "gdn_bwd", lambda: lib.cai_gdn_kernel_name(code, npix, C, max(xld, gld), C, 1).decode(),
+                        4.0 * npix * C * C,
                         3 * npix * C * _es(dt) + 8 * C * C, dt, f"{'IGDN' if inverse else 'GDN'} C={C} npix={npix}")
         if direct:
             dbr = dgr = None
@@ -1014,7 +1053,7 @@ class BottleneckFn(torch.autograd.Function):
         n_el = npix * C
         nsc = lib.cai_eb_scratch_bytes(npix, C)
         scratch = torch.empty(nsc, dtype=torch.uint8, device=xr.device)
-        tickets = _eb_tickets(xr.device, C)
+        tickets = _eb_tickets(ctx.params[0], C)
         _ledger.run(lambda: lib.cai_eb_bwd(mode, npix, C, ctypes.byref(P), _p(xr), dcode(xdtype), xld, nsrc, lb,
                                            _p(gl), glld, _p(gq_r), dcode(gq_r.dtype) if gq_r is not None else F32,
                                            gqld, _p(dxb), C, ctypes.byref(G), _p(scratch), nsc, _p(tickets),
@@ -1027,18 +1066,20 @@ class BottleneckFn(torch.autograd.Function):
 
 
 _UNIT_GRAD = {}
-_EB_TICKETS = {}
+_EB_TICKETS_ATTR = "_cai_eb_tickets"
 _EB_AUX_SLOT = 1 << 12
 
 
-def _eb_tickets(device, C: int = 0, aux: bool = False) -> torch.Tensor:
-    """Zeroed uint32 hand-off tickets of the EntropyBottleneck kernels on `device` (cai_eb_bwd: one per channel;
-    cai_eb_aux_loss: one, in its own slot).  Every launch leaves them at zero, so one buffer per device serves
-    all calls and graph replays (EntropyBottleneck launches on one device never overlap: the forward's side
-    stream ends before its backward, the aux loss runs after the backward)."""
-    t = _EB_TICKETS.get(device)
-    if t is None:
-        t = _EB_TICKETS[device] = torch.zeros(_EB_AUX_SLOT + 64, dtype=torch.int32, device=device)
+def _eb_tickets(quantiles: torch.Tensor, C: int = 0, aux: bool = False) -> torch.Tensor:
+    """Zeroed uint32 hand-off tickets of one EntropyBottleneck's kernels (cai_eb_bwd: one per channel;
+    cai_eb_aux_loss: one, in its own slot), owned by the module's `quantiles` parameter.  Every launch leaves
+    them at zero, so one buffer serves all of the module's calls and graph replays (a module's EntropyBottleneck
+    launches never overlap: the forward's side stream ends before its backward, the aux loss runs after the
+    backward); two models -- e.g. replicas stepped from two host threads -- never share one."""
+    t = getattr(quantiles, _EB_TICKETS_ATTR, None)
+    if t is None or t.device != quantiles.device:
+        t = torch.zeros(_EB_AUX_SLOT + 64, dtype=torch.int32, device=quantiles.device)
+        setattr(quantiles, _EB_TICKETS_ATTR, t)
     if C > _EB_AUX_SLOT:
         raise ValueError(f"EntropyBottleneck with {C} channels: at most {_EB_AUX_SLOT}")
     return t[_EB_AUX_SLOT:] if aux else t
@@ -1081,7 +1122,7 @@ class BottleneckAuxFn(torch.autograd.Function):
         nsc = lib.cai_eb_scratch_bytes(0, C)
         scratch = torch.empty(nsc, dtype=torch.uint8, device=quantiles.device)
         lib.cai_eb_aux_loss(C, ctypes.byref(P), _p(t), _p(loss), _p(_unit_grad(quantiles.device)), _p(dq1), 0,
-                            _p(scratch), nsc, _p(_eb_tickets(quantiles.device, aux=True)), _stream())
+                            _p(scratch), nsc, _p(_eb_tickets(quantiles, aux=True)), _stream())
         ctx.save_for_backward(dq1)
         ctx.qparam = quantiles
         ctx.nparams = len(prm)

@@ -97,12 +97,15 @@ class OverlappedAllReduce:
         self.side = torch.cuda.Stream(device=flat_grad.device)
         self._ys = []
         self._model = None
-        self._handle = None
+        self._handles = []
         if hasattr(tail, "_dp_cut") and hasattr(tail, "dp_tail"):
             self._model = tail
             tail._dp_cut_fn = self._mark
         else:
-            self._handle = tail.register_forward_hook(self._keep)
+            self._handles.append(tail.register_forward_hook(self._keep))
+        # each forward starts a new set of cut tensors: one that never reached backward_tail (a validation
+        # pass, a plain backward) neither leaks into the next step nor keeps its cut tensors alive
+        self._handles.append(tail.register_forward_pre_hook(self._reset))
 
     @classmethod
     def for_model(cls, model: torch.nn.Module, opt):
@@ -112,7 +115,13 @@ class OverlappedAllReduce:
                 if not n.startswith(tail) and not n.endswith(".quantiles")]
         return cls(opt.flat_grad, opt.tail_offset, model, head)
 
+    def _reset(self, module, inputs):
+        self._ys = []
+
     def _mark(self, *ts):
+        # only a forward that can be differentiated marks its cut (no_grad / eval passes go through as is)
+        if not torch.is_grad_enabled() or not any(t.requires_grad for t in ts):
+            return ts
         # boundary nodes: phase 1's capture of a cut tensor's gradient may execute its grad_fn, which for
         # the product convs writes parameter gradients as a side effect; an identity node in between has none
         out = tuple(_Boundary.apply(t) for t in ts)
@@ -153,7 +162,8 @@ class OverlappedAllReduce:
         cur.wait_stream(self.side)
 
     def remove(self):
-        if self._handle is not None:
-            self._handle.remove()
+        for h in self._handles:
+            h.remove()
+        self._handles = []
         if self._model is not None:
             self._model._dp_cut_fn = None

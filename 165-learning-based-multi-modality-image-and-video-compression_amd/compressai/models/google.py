@@ -138,6 +138,15 @@ class CompressionModel(nn.Module):
         raise NotImplementedError()
 
     def __call__(self, *args, **kwargs):
+        if getattr(self, "_is_replica", False):
+            # nn.DataParallel (the reference's CustomDataParallel, examples/train.py:101-108,422-423, taken when
+            # torch.cuda.device_count() > 1) runs replicas in one host thread per GPU over broadcast weight copies;
+            # this build scales one process per GPU instead (compressai.distributed over RCCL)
+            raise RuntimeError(
+                f"{type(self).__name__}: nn.DataParallel replicas are not supported by the MI355X build; run one "
+                "process per GPU (torchrun --nproc-per-node N, gradients exchanged by compressai.distributed: "
+                "OverlappedAllReduce / allreduce_mean_), or make one GPU visible (HIP_VISIBLE_DEVICES=0) so the "
+                "training script does not wrap the model")
         # all conv weights are packed to the MFMA layout in one launch per forward
         # (compressai/_prepack.py); the reference has no counterpart (stock convs)
         from .._prepack import prepacked_forward

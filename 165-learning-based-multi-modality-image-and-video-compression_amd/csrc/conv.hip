@@ -1015,11 +1015,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvArgs a, int
         const int q4 = tid + 512 * i, g = (q4 >> 3) & 3, q = ((q4 >> 5) << 3) | (q4 & 7);
         const int pr = q / H::PW, pc = q - (q / H::PW) * H::PW;
         const int iy = iyb + pr, ix = ixb + pc;
-#ifndef CAI_PROBE_NOCELL    // timing probe only (results invalid): footprint loads from the zero page
         const bool in = real && q < H::NPOS && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW;
-#else
-        const bool in = false && real && iy + ix;
-#endif
         const void* src = in ? (const void*)(X + ((b * a.IH + iy) * a.IW + ix) * ld_b + g * 16 + cc * (H::CK * 2))
                              : (const void*)cai_zero_page;
         pr_[i] = *reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(reinterpret_cast<uintptr_t>(src));
@@ -1109,11 +1105,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvArgs a, int
         for (int t = 0; t < NTAP; ++t) {
             wait_vmcnt_n(halo_younger_sp(t, NSTB, NPI, CSP));
             wait_lgkmcnt0();
-#ifndef CAI_PROBE_NOBAR    // timing probe only (results invalid): no per-step barrier
             __builtin_amdgcn_s_barrier();
-#else
-            if (t == NTAP - 1) __builtin_amdgcn_s_barrier();
-#endif
             if (t == NTAP - 1) {
                 // every wave has read its last fragment of this chunk: stage the next chunk's patch (when the
                 // footprint needs a cell per step of the chunk (k3: NPI == NTAP), the last one is loaded here)
@@ -1137,12 +1129,8 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvArgs a, int
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
                 for (int tn = 0; tn < TN; ++tn) {
-#ifndef CAI_PROBE_NOMFMA    // timing probe only (results invalid): fragments read, no MFMA
                     acc[tm][tn] = CAI_HALO_T ? mma16<bf16>(fb[tn], fa[tm], acc[tm][tn])
                                              : mma16<bf16>(fa[tm], fb[tn], acc[tm][tn]);
-#else
-                    asm volatile("" ::"v"(fa[tm]), "v"(fb[tn]));
-#endif
                 }
             // the next step's reads (separate registers) alternate with this step's first MFMAs (measured:
             // a read burst ahead of the MFMAs, or reads every other MFMA, ran 2-6 % slower)

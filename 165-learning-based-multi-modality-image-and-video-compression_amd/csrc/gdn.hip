@@ -1235,4 +1235,23 @@ int cai_gdn_backward_deferred(int dtype, const void* x, int32_t x_ld, const void
                             ws_bytes, stream, job);
 }
 
+// The kernel cai_gdn_fwd (direction 0) / cai_gdn_backward (direction 1) launches for these arguments, as
+// rocprofv3 names it (the per-launch ledger and the model-level dispatch tests read it); "" for bad arguments.
+const char* cai_gdn_kernel_name(int dtype, int64_t npix, int32_t C, int32_t in_ld, int32_t out_ld, int32_t direction) {
+    static thread_local char buf[48];
+    if (!gdn_c_ok(C, dtype) || npix <= 0 || (direction != 0 && direction != 1)) return "";
+    const char* nm;
+    if (direction == 0)
+        nm = dtype == CAI_BF16 && gdn_lane_on() && gdn_lane_fwd_ok(C, npix, in_ld, out_ld) ? "gdn_fwd_lane_kernel"
+                                                                                          : "gdn_fwd_kernel";
+    else if (!fused_ok(dtype, C))
+        nm = "gdn_bwd_kernel+param_grad";
+    else if (gdn_lane_on() && gdn_lane_bwd_ok(C, npix, in_ld, in_ld, out_ld))
+        nm = "gdn_bwd_lane_kernel";
+    else
+        nm = (C == 192 || C == 160) ? "gdn_bwd_wide_kernel" : "gdn_bwd_fused_kernel";
+    snprintf(buf, sizeof(buf), "%s<%d>", nm, C);
+    return buf;
+}
+
 }  // extern "C"

@@ -248,6 +248,38 @@ __global__ __launch_bounds__(256) void reduce_jobs_kernel(const ReduceBatch B) {
         edge_reduce_body(J, bid, ered, etot);
 }
 
+// The gradient buffers a job writes (read-modify-write when it accumulates).
+static inline void job_dests(const cai_reduce_job& J, const void* d[2]) {
+    d[0] = d[1] = nullptr;
+    if (J.kind == CAI_JOB_WGRAD) {
+        d[0] = J.p[1];
+        d[1] = J.p[3];
+    } else if (J.kind == CAI_JOB_GDN) {
+        d[0] = J.p[3];
+        d[1] = J.p[4];
+    } else if (J.kind == CAI_JOB_EDGE) {
+        d[0] = J.p[2];
+        d[1] = J.p[3];
+    }
+}
+
+static bool shares_dest(const ReduceBatch& B, const cai_reduce_job& J) {
+    const void* a[2];
+    job_dests(J, a);
+    for (int q = 0; q < B.n; ++q) {
+        const void* b[2];
+        job_dests(B.jobs[q], b);
+        for (int u = 0; u < 2; ++u)
+            for (int v = 0; v < 2; ++v)
+                if (a[u] && a[u] == b[v]) return true;
+    }
+    return false;
+}
+
+// Jobs run in list order across launches; within one launch their blocks run concurrently, so two jobs that
+// write the same gradient (a module called twice in one forward, e.g. Channel_aligner's shared trunk,
+// models/master.py:293-304: the second job accumulates onto the first) never share a launch -- the batch is
+// closed before the second and it runs in the next launch, after the first on the stream.
 int launch_reduce_jobs(const cai_reduce_job* jobs, int n, hipStream_t st) {
     for (int j0 = 0; j0 < n;) {
         ReduceBatch B{};
@@ -257,6 +289,7 @@ int launch_reduce_jobs(const cai_reduce_job* jobs, int n, hipStream_t st) {
             if (J.kind == CAI_JOB_NONE || J.nblocks <= 0) continue;
             CAI_CHECK_ARG(J.kind == CAI_JOB_WGRAD || J.kind == CAI_JOB_GDN || J.kind == CAI_JOB_EDGE,
                           "reduce_jobs: unknown job kind %d", J.kind);
+            if (shares_dest(B, J)) break;
             B.jobs[B.n] = J;
             B.start[B.n] = blocks;
             blocks += J.nblocks;

@@ -383,6 +383,10 @@ int cai_gdn_backward(int dtype, const void* x, int32_t x_ld, const void* dy, int
 
 /* cai_gdn_backward with its parameter-gradient reduce left as a job (see cai_reduce_jobs); the fused
  * pass only (bf16, C in {64, 128, 160, 192}), other cases run immediately and return CAI_JOB_NONE. */
+/* The kernel cai_gdn_fwd (direction 0) or cai_gdn_backward (direction 1) launches for these arguments
+ * (in_ld: x / dy leading dimension, out_ld: y / dx), e.g. "gdn_fwd_lane_kernel<128>"; "" for bad arguments.
+ * Diagnostics for the per-launch ledger and the dispatch tests (no reference counterpart). */
+const char* cai_gdn_kernel_name(int dtype, int64_t npix, int32_t C, int32_t in_ld, int32_t out_ld, int32_t direction);
 int cai_gdn_backward_deferred(int dtype, const void* x, int32_t x_ld, const void* dy, int32_t dy_ld, int64_t npix,
                               int32_t C, const void* gamma_op, const float* beta, int32_t inverse, void* dx,
                               int32_t dx_ld, const float* beta_raw, const float* gamma_raw, float beta_min,

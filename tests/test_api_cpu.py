@@ -116,3 +116,18 @@ def test_master_paper_config_parameter_count():
 
     n = sum(p.numel() for p in Master_compresser(width=512, height=640, channel=1).parameters())
     assert 26e6 < n < 29e6
+
+
+def test_dataparallel_replica_rejected():
+    """nn.DataParallel (the reference's CustomDataParallel, examples/train.py:101-108, taken when more than one
+    GPU is visible) runs module replicas from one host thread per GPU; the build scales one process per GPU
+    instead and says so at the replica's forward, before anything is launched."""
+    import pytest
+    import torch
+
+    from compressai.zoo import bmshj2018_hyperprior
+
+    net = bmshj2018_hyperprior(1)
+    replica = net._replicate_for_data_parallel()      # what torch.nn.parallel.replicate builds per device
+    with pytest.raises(RuntimeError, match="one process per GPU"):
+        replica(torch.rand(1, 3, 64, 64))

@@ -11,6 +11,8 @@ run with torch.optim.Adam (the reference's optimizer) and with FusedAdam as a dr
 FusedAdam's checkpoint format (torch.optim.Adam.state_dict, train.py:407,419,475), its handling of gradients a
 caller detached (model.zero_grad()), GradScaler's non-finite skip rule, and the autocast dtype policy.
 """
+import math
+
 import pytest
 import torch
 
@@ -118,28 +120,94 @@ def test_reference_caller_sequence_bf16_autocast(cuda):
 
 
 def test_fp16_autocast_policy(cuda):
-    """fp16 autocast (the reference's torch.cuda.amp.autocast()) raises by default; the bf16 policy runs the
-    region in bf16, identical to an explicit bf16 autocast."""
+    """fp16 autocast (the reference's torch.cuda.amp.autocast()) runs the bf16 kernels by default, identical to
+    an explicit bf16 autocast; the opt-in "error" policy raises."""
     import compressai
     from compressai.entropy_models import set_noise_source
 
     _, net = _pair("bmshj2018-hyperprior", (32, 48), cuda)
     x = torch.rand(1, 3, 64, 64, generator=torch.Generator().manual_seed(1)).to(cuda)
-    with pytest.raises(RuntimeError, match="bf16"):
-        with torch.autocast("cuda", dtype=torch.float16):
-            net(x)
+    compressai.set_fp16_autocast_policy("error")
+    try:
+        with pytest.raises(RuntimeError, match="bf16"):
+            with torch.autocast("cuda", dtype=torch.float16):
+                net(x)
+    finally:
+        compressai.set_fp16_autocast_policy("bf16")
     outs = []
     for dt in (torch.float16, torch.bfloat16):
         noise = [torch.zeros(1, 32, 1, 1, device=cuda), torch.zeros(1, 48, 4, 4, device=cuda)]
         set_noise_source(lambda t: noise.pop(0))
-        compressai.set_fp16_autocast_policy("bf16")
         try:
             with torch.autocast("cuda", dtype=dt):
                 outs.append(net(x)["x_hat"].detach().clone())
         finally:
-            compressai.set_fp16_autocast_policy("error")
             set_noise_source(None)
     assert torch.equal(outs[0], outs[1])
+
+
+def test_train_one_epoch_as_written_fp16(cuda):
+    """examples/train.py:145-206 (train_one_epoch_guided's body) as written: DataLoader batches,
+    torch.cuda.amp.autocast() (fp16) around forward + criterion and around aux_loss, GradScaler scale / unscale_ /
+    clip_grad_norm_ / step / update, torch.optim.Adam from the reference's configure_optimizers (train.py:111-142),
+    on the product ScaleHyperprior.  Runs with no policy call: the fp16 regions compute in bf16 (one warning), the
+    losses stay finite and track the same steps under an explicit bf16 autocast, and the scaler never skips."""
+    import warnings
+
+    from torch.cuda.amp import GradScaler, autocast
+    from torch.utils.data import DataLoader, TensorDataset
+
+    from compressai.entropy_models import set_noise_source
+    from compressai.losses import RateDistortionLoss
+
+    def run(fp16):
+        _, model = _pair("bmshj2018-hyperprior", (64, 96), cuda)
+        optimizer, aux_optimizer = _torch_optimizers(model, 1e-4, 1e-3)
+        scaler = GradScaler()
+        criterion = RateDistortionLoss(1)
+        data = torch.rand(8, 3, 64, 64, generator=torch.Generator().manual_seed(5))
+        loader = DataLoader(TensorDataset(data), batch_size=2, shuffle=False)
+        gen = torch.Generator().manual_seed(6)
+        set_noise_source(lambda t: torch.empty(t.shape).uniform_(-0.5, 0.5, generator=gen).to(cuda))
+        losses, auxes, scales = [], [], []
+        try:
+            model.train()
+            device = next(model.parameters()).device
+            for i, (d,) in enumerate(loader):
+                d = d.to(device)
+                optimizer.zero_grad()
+                aux_optimizer.zero_grad()
+                with (autocast() if fp16 else torch.autocast("cuda", dtype=torch.bfloat16)):
+                    out_net = model(d)
+                    out_criterion = criterion(out_net, d)
+                scaler.scale(out_criterion["loss"]).backward()
+                scaler.unscale_(optimizer)
+                torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+                scaler.step(optimizer)
+                with (autocast() if fp16 else torch.autocast("cuda", dtype=torch.bfloat16)):
+                    aux_loss = model.aux_loss()
+                scaler.scale(aux_loss).backward()
+                scaler.unscale_(aux_optimizer)
+                scaler.step(aux_optimizer)
+                scaler.update()
+                losses.append(out_criterion["loss"].item())
+                auxes.append(aux_loss.item())
+                scales.append(scaler.get_scale())
+        finally:
+            set_noise_source(None)
+        return losses, auxes, scales
+
+    with warnings.catch_warnings(record=True) as caught:
+        warnings.simplefilter("always")
+        l16, a16, s16 = run(True)
+    ours = [w for w in caught if "fp16 autocast regions run the bf16 kernels" in str(w.message)]
+    import compressai._ops as ops
+    assert len(ours) == 1 or ops._FP16_WARNED, [str(w.message) for w in caught]
+    lbf, abf, _ = run(False)
+    assert len(l16) == 4 and all(math.isfinite(v) for v in l16 + a16)
+    assert s16 == sorted(s16) and s16[0] == 65536.0        # no inf / nan step was skipped
+    for a, b in zip(l16, lbf):
+        assert abs(a - b) <= 1e-2 * abs(b), (l16, lbf)
 
 
 def _param_set(dev, seed=9, large=False):

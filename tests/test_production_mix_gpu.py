@@ -4,6 +4,10 @@ conv_halo_phase_kernel<192> >= 512 blocks, so the 64-128 px model tests never di
 
 * C4 cheng2020-attn q6 at 256x256: fp32 parity against the float64 oracle at B=1, and bf16 bounds at the
   per-GPU batch B=4 with conv_halo_s1_kernel<192> asserted in the step's launches;
+* C2 bmshj2018-hyperprior q1 (128, 192) -- the bench's own config -- and C3 mbt2018-mean q1 at 256x256, B=16,
+  bf16, with the kernels that only full-size C2 grids take asserted (lane GDN <128> forward / backward, the
+  halo gather / s^2-phase convs, the halo weight gradient, the image-side edge kernels); C2 also in fp32 at
+  B=2 against the float64 oracle;
 * C2' bmshj2018-hyperprior q6 (192, 320) at 256x256, B=16, bf16, with conv_halo_phase_kernel<192> asserted;
 * C5 at paper resolution (master.py:708-742, 158-210): Spatial_aligner on its three token
   grids (32x40, 64x80, 128x160) against the CPU oracle, Channel_aligner on 512x640 features against the
@@ -87,9 +91,12 @@ def _run(name, args, size, batch, cuda, bf16, quality, seed):
     return ref, net, out_r, out, cr, c, feed.drawn, x, kernels
 
 
-def test_cheng2020_attn_fp32_parity_256(cuda):
-    name, args = "cheng2020-attn", (192,)
-    ref, net, out_r, out, cr, c, drawn, x, _ = _run(name, args, 256, 1, cuda, False, 6, seed=31)
+@pytest.mark.parametrize("name,args,batch,quality,seed", [
+    ("cheng2020-attn", (192,), 1, 6, 31),                 # C4 at 256x256
+    ("bmshj2018-hyperprior", (128, 192), 2, 1, 33),       # C2 (the bench's model) at 256x256
+], ids=["cheng2020-attn-q6-B1", "hyperprior-q1-B2"])
+def test_fp32_parity_256(cuda, name, args, batch, quality, seed):
+    ref, net, out_r, out, cr, c, drawn, x, _ = _run(name, args, 256, batch, cuda, False, quality, seed=seed)
     import copy
 
     r64 = copy.deepcopy(ref).double()
@@ -97,7 +104,7 @@ def test_cheng2020_attn_fp32_parity_256(cuda):
         p.grad = None
     with O.NoiseFeed([n.double() for n in drawn]):
         out64 = r64(x.double())
-    O.RateDistortionLoss(6)(out64, x.double())["loss"].backward()
+    O.RateDistortionLoss(quality)(out64, x.double())["loss"].backward()
 
     def check(a, a32, a64, bar, what):
         e, e32 = relerr(a, a64), relerr(a32, a64)
@@ -122,20 +129,30 @@ def test_cheng2020_attn_fp32_parity_256(cuda):
         el2 = rel_l2(p.grad, p64[n].grad)          # a mask flip: one term of the sum (module docstring)
         assert el2 < 5e-3, (n, e, e32, el2)
         flips.append((n, round(e, 6), round(el2, 6)))
-    print(f"\nfp32 cheng2020-attn 256: mask-flip allowance used by {len(flips)} of {total} tensors: {flips}")
+    print(f"\nfp32 {name} 256 B={batch}: mask-flip allowance used by {len(flips)} of {total} tensors: {flips}")
     assert len(flips) <= 0.02 * total, flips
 
 
 BF16_XHAT, BF16_LIK, BF16_LIK_L2, BF16_LOSS, GRAD_COS, TENSOR_COS = 1e-2, 5e-2, 5e-3, 1e-3, 0.9999, 0.98
 
 
+# the kernels the bench's C2 / C3 step launches at 256x256 B=16 (none of them is taken at the 64-128 px model
+# test sizes: the lane GDN kernels need >= 32768 pixels, the halo / phase / edge kernels full-size grids)
+C2_MIX = ("gdn_fwd_lane_kernel<128>", "gdn_bwd_lane_kernel<128>", "conv_halo_kernel<5>", "conv_halo_phase_kernel",
+          "wgrad_halo_kernel<5>", "edge_s2d_kernel (conv fwd)", "edge_d2s_kernel (deconv fwd)",
+          "edge_wgrad_dma_kernel (+pack, reduce)")
+
+
 @pytest.mark.parametrize("name,args,batch,quality,gated", [
-    ("cheng2020-attn", (192,), 4, 6, "conv_halo_s1_kernel<192>"),                   # C4, per-GPU batch
-    ("bmshj2018-hyperprior", (192, 320), 16, 6, "conv_halo_phase_kernel<192>"),      # C2' at C2's batch
-], ids=["cheng2020-attn-q6-B4", "hyperprior-q6-B16"])
+    ("cheng2020-attn", (192,), 4, 6, ("conv_halo_s1_kernel<192>",)),                 # C4, per-GPU batch
+    ("bmshj2018-hyperprior", (192, 320), 16, 6, ("conv_halo_phase_kernel<192>",)),   # C2' at C2's batch
+    ("bmshj2018-hyperprior", (128, 192), 16, 1, C2_MIX),                             # C2: BASELINE configs[1]
+    ("mbt2018-mean", (128, 192), 16, 1, C2_MIX),                                     # C3: configs[2]
+], ids=["cheng2020-attn-q6-B4", "hyperprior-q6-B16", "hyperprior-q1-B16", "mbt2018-mean-q1-B16"])
 def test_bf16_production_mix_256(cuda, name, args, batch, quality, gated):
     ref, net, out_r, out, cr, c, _, _, kernels = _run(name, args, 256, batch, cuda, True, quality, seed=41)
-    assert gated in kernels, sorted(kernels)
+    missing = [k for k in gated if k not in kernels]
+    assert not missing, (missing, sorted(kernels))
     ex = relerr(out["x_hat"], out_r["x_hat"])
     el = {k: relerr(out["likelihoods"][k], out_r["likelihoods"][k]) for k in out_r["likelihoods"]}
     el2 = {k: rel_l2(out["likelihoods"][k], out_r["likelihoods"][k]) for k in out_r["likelihoods"]}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build lib/libcai_base.so from the last commit (HEAD) for an A/B against the
-# working tree's lib/libcai.so (tools/gpu_ab.sh).  Uncommitted changes are
+# working tree's lib/libcai.so (tools/ab.sh).  Uncommitted changes are
 # stashed around the build and restored.
 set -e
 cd "$(dirname "$0")/.."

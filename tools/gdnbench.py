@@ -1,5 +1,5 @@
 """GDN forward / backward on the hyperprior's largest layer (16 x 128 x 128 x 128 bf16), 30 launches each, for
-rocprofv3 counter passes (profiles/r02_scripts/r02y.sh)."""
+rocprofv3 counter passes (tools/pmc_gdn.sh)."""
 import os
 import sys
 
