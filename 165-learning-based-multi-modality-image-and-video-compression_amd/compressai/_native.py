@@ -92,6 +92,8 @@ SIGNATURES = {
     "cai_conv_dgrad": (_I, [_G, _I, _P, c_int32, _P, _P, c_int32, c_int32, _F, _P, c_int32, _P, _S, _P]),
     "cai_conv_dgrad_res": (_I, [_G, _I, _P, c_int32, _P, _P, c_int32, _P, c_int32, c_int32, _F, _P, c_int32, _P, _S,
                                 _P]),
+    "cai_conv_dgrad_res2": (_I, [_G, _I, _P, c_int32, _P, _P, c_int32, _P, c_int32, _P, c_int32, c_int32, _F, _P,
+                                 c_int32, _P, _S, _P]),
     "cai_conv_wgrad_workspace_bytes": (_S, [_G, _I]),
     "cai_conv_kernel_name": (c_char_p, [_G, _I, _I, c_int32]),
     "cai_conv_split_factor": (c_int32, [_G, _I, _I, c_int32]),

@@ -638,13 +638,24 @@ class ConvFn(torch.autograd.Function):
             # ResidualChainFn: + the residual's gradient in the epilogue (then the previous unit's ReLU mask)
             dres = getattr(ctx, "dx_res", None)
             rmask = getattr(ctx, "dx_res_mask", MASK_NONE)
+            dres2 = getattr(ctx, "dx_res2", None)   # AttentionBlockFn: + the other branch's / the gate's gradient
+            if dres is None and dres2 is not None:
+                dres, dres2 = dres2, None
             if dres is not None and dt == torch.bfloat16 and aux is None and ldx % 8 == 0:
                 rpm, rld = to_pm(dres, dt, 4)
                 maux = xpm if rmask != MASK_NONE else None
-                _ledger.run(lambda: lib.cai_conv_dgrad_res(ctypes.byref(g), code, _p(gpm), gld, _p(wt), _p(rpm), rld,
-                                                           _p(dx), ldx, rmask, 0.0, _p(maux),
-                                                           ctx.xld if maux is not None else 0, _p(ws), wsb, st),
-                            "conv_dgrad", _conv_kernel(g, dt, 1), fl, nb, dt, _ledger.shape_of(g))
+                if dres2 is not None:
+                    r2pm, r2ld = to_pm(dres2, dt, 4)
+                    _ledger.run(lambda: lib.cai_conv_dgrad_res2(ctypes.byref(g), code, _p(gpm), gld, _p(wt), _p(rpm),
+                                                                rld, _p(r2pm), r2ld, _p(dx), ldx, rmask, 0.0,
+                                                                _p(maux), ctx.xld if maux is not None else 0, _p(ws),
+                                                                wsb, st),
+                                "conv_dgrad", _conv_kernel(g, dt, 1), fl, nb, dt, _ledger.shape_of(g))
+                else:
+                    _ledger.run(lambda: lib.cai_conv_dgrad_res(ctypes.byref(g), code, _p(gpm), gld, _p(wt), _p(rpm),
+                                                               rld, _p(dx), ldx, rmask, 0.0, _p(maux),
+                                                               ctx.xld if maux is not None else 0, _p(ws), wsb, st),
+                                "conv_dgrad", _conv_kernel(g, dt, 1), fl, nb, dt, _ledger.shape_of(g))
             else:
                 _ledger.run(lambda: lib.cai_conv_dgrad(ctypes.byref(g), code, _p(gpm), gld, _p(wt), _p(dx), ldx,
                                                        spec.in_mask, spec.in_mask_param, _p(aux),
@@ -652,6 +663,8 @@ class ConvFn(torch.autograd.Function):
                             "conv_dgrad", _conv_kernel(g, dt, 1), fl, nb, dt, _ledger.shape_of(g))
                 if dres is not None:
                     dx = dx + dres
+                if dres2 is not None:
+                    dx = dx + dres2
                 if rmask != MASK_NONE:
                     raise RuntimeError("conv dgrad: a residual-gradient mask needs the fused bf16 path")
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
@@ -714,58 +727,118 @@ class ResidualChainFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, specs, out_masked, *params):
         need = ctx.needs_input_grad   # (x, specs, out_masked, *params)
-        subs = []
-        y = x
-        for k, (s0, s2, s4) in enumerate(specs):
-            w0, b0, w2, b2, w4, b4 = params[6 * k:6 * k + 6]
-            pn = need[3 + 6 * k:9 + 6 * k]
-            c0 = _SubCtx((need[0] or k > 0, pn[0], pn[1], False, False))
-            c2 = _SubCtx((True, pn[2], pn[3], False, False))
-            c4 = _SubCtx((True, pn[4], pn[5], False, True))
-            h = ConvFn.forward(c0, y, w0, b0, s0)
-            h = ConvFn.forward(c2, h, w2, b2, s2)
-            y = ConvFn.forward(c4, h, w4, b4, s4, y)
-            if k > 0:   # this unit's input is the previous unit's ReLU output: mask its gradient here
-                c0.dx_res_mask = MASK_POS
-                subs[-1][2].gy_masked = True
-            subs.append((c0, c2, c4))
-        if out_masked:   # the consumer (a MASK_POS dgrad, GateFn relu_a) hands back the masked gradient
-            subs[-1][2].gy_masked = True
-        # every sub-conv's tensors go through save_for_backward (version-counter checks, no y -> grad_fn -> ctx
-        # -> y reference cycle); the stand-in contexts keep only metadata between forward and backward
-        flat, counts = [], []
-        for trio in subs:
-            for c in trio:
-                counts.append(len(c.saved_tensors))
-                flat.extend(c.saved_tensors)
-                c.saved_tensors = ()
-        ctx.save_for_backward(*flat)
-        ctx.subs, ctx.counts = subs, counts
+        y, ctx.subs = _chain_forward(x, specs, out_masked, params, need[0], need[3:])
+        _stash(ctx, [c for trio in ctx.subs for c in trio])
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        saved = ctx.saved_tensors
-        subs = [c for trio in ctx.subs for c in trio]
-        i = 0
-        for c, n in zip(subs, ctx.counts):
+        with _unstash(ctx):
+            g, flat = _chain_backward(ctx.subs, gy)
+        return (g, None, None, *flat)
+
+
+def _stash(ctx, subs):
+    """Every stand-in context's tensors through ctx.save_for_backward (version-counter checks, no y -> grad_fn ->
+    ctx -> y reference cycle); the stand-ins keep only metadata between forward and backward."""
+    flat, counts = [], []
+    for c in subs:
+        counts.append(len(c.saved_tensors))
+        flat.extend(c.saved_tensors)
+        c.saved_tensors = ()
+    ctx.save_for_backward(*flat)
+    ctx.stash = (subs, counts)
+
+
+class _unstash:
+    """Hand the stand-in contexts their saved tensors for one backward (retain_graph: a second backward restores
+    them from ctx.saved_tensors again)."""
+
+    def __init__(self, ctx):
+        self.subs, counts = ctx.stash
+        saved, i = ctx.saved_tensors, 0
+        for c, n in zip(self.subs, counts):
             c.saved_tensors = tuple(saved[i:i + n])
             i += n
-        grads = []
-        g = gy
-        try:
-            for c0, c2, c4 in reversed(ctx.subs):
-                dh2, dw4, db4, _, g4 = ConvFn.backward(c4, g)
-                dh1, dw2, db2, _, _ = ConvFn.backward(c2, dh2)
-                c0.dx_res = g4
-                g, dw0, db0, _, _ = ConvFn.backward(c0, dh1)
-                grads.append((dw0, db0, dw2, db2, dw4, db4))
-        finally:
-            for c in subs:     # retain_graph: a second backward restores them from ctx.saved_tensors again
-                c.saved_tensors = ()
-                c.dx_res = None
-        flat = [t for unit in reversed(grads) for t in unit]
-        return (g, None, None, *flat)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        for c in self.subs:
+            c.saved_tensors = ()
+            c.dx_res = c.dx_res2 = None
+        return False
+
+
+def _chain_forward(x, specs, out_masked, params, x_need, p_need):
+    subs = []
+    y = x
+    for k, (s0, s2, s4) in enumerate(specs):
+        w0, b0, w2, b2, w4, b4 = params[6 * k:6 * k + 6]
+        pn = p_need[6 * k:6 * k + 6]
+        c0 = _SubCtx((x_need or k > 0, pn[0], pn[1], False, False))
+        c2 = _SubCtx((True, pn[2], pn[3], False, False))
+        c4 = _SubCtx((True, pn[4], pn[5], False, True))
+        h = ConvFn.forward(c0, y, w0, b0, s0)
+        h = ConvFn.forward(c2, h, w2, b2, s2)
+        y = ConvFn.forward(c4, h, w4, b4, s4, y)
+        if k > 0:   # this unit's input is the previous unit's ReLU output: mask its gradient here
+            c0.dx_res_mask = MASK_POS
+            subs[-1][2].gy_masked = True
+        subs.append((c0, c2, c4))
+    if out_masked:   # the consumer (a MASK_POS dgrad, GateFn relu_a) hands back the masked gradient
+        subs[-1][2].gy_masked = True
+    return y, subs
+
+
+def _chain_backward(subs, gy, dx_res2=None):
+    """-> (gradient of the chain input, flat parameter gradients); dx_res2: one more gradient of the chain input,
+    summed in the first unit's dgrad epilogue."""
+    grads = []
+    g = gy
+    for k in range(len(subs) - 1, -1, -1):
+        c0, c2, c4 = subs[k]
+        dh2, dw4, db4, _, g4 = ConvFn.backward(c4, g)
+        dh1, dw2, db2, _, _ = ConvFn.backward(c2, dh2)
+        c0.dx_res = g4
+        if k == 0 and dx_res2 is not None:
+            c0.dx_res2 = dx_res2
+        g, dw0, db0, _, _ = ConvFn.backward(c0, dh1)
+        grads.append((dw0, db0, dw2, db2, dw4, db4))
+    return g, [t for unit in reversed(grads) for t in unit]
+
+
+class AttentionBlockFn(torch.autograd.Function):
+    """AttentionBlock (layers.py:196-244) as one autograd node: y = a * sigmoid(b) + x with a = conv_a(x) and
+    b = conv_b(x) (three ResidualUnits each, as in ResidualChainFn; conv_b's 1x1 conv after its chain).  x's three
+    gradients (both branches and the gate's identity) are summed in the first conv dgrad epilogues (conv_b's first
+    unit: + the gate's; conv_a's first unit: + conv_b's) -- no gradient-sum launch.
+
+    params: conv_a's 18, conv_b's 18 (6 per unit as in ResidualChainFn), then conv_b[3]'s weight and bias."""
+
+    @staticmethod
+    def forward(ctx, x, specs_a, specs_b, spec_b3, *params):
+        need = ctx.needs_input_grad   # (x, specs_a, specs_b, spec_b3, *params)
+        pa, pb, (w3, b3) = params[:18], params[18:36], params[36:38]
+        a, ctx.sub_a = _chain_forward(x, specs_a, True, pa, need[0], need[4:22])
+        hb, ctx.sub_b = _chain_forward(x, specs_b, True, pb, need[0], need[22:40])
+        c3 = _SubCtx((True, need[40], need[41], False, False))
+        bb = ConvFn.forward(c3, hb, w3, b3, spec_b3)
+        cg = _SubCtx((True, True, True, False))
+        y = GateFn.forward(cg, a, bb, x, True)
+        ctx.c3, ctx.cg = c3, cg
+        _stash(ctx, [c for trio in ctx.sub_a + ctx.sub_b for c in trio] + [c3, cg])
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        with _unstash(ctx):
+            da, db, gx, _ = GateFn.backward(ctx.cg, gy)
+            dhb, dw3, db3, _, _ = ConvFn.backward(ctx.c3, db)
+            xb, flat_b = _chain_backward(ctx.sub_b, dhb, dx_res2=gx)
+            dx, flat_a = _chain_backward(ctx.sub_a, da, dx_res2=xb)
+        return (dx, None, None, None, *flat_a, *flat_b, dw3, db3)
 
 
 # ---------------------------------------------------------------------------

@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 
 from .._native import ACT_LEAKY, ACT_NONE, ACT_RELU, MASK_LEAKY, MASK_POS
-from .._ops import AddActFn, GateFn, ResidualChainFn, residual_fusable
+from .._ops import AddActFn, AttentionBlockFn, GateFn, ResidualChainFn, residual_fusable
 from .conv import Conv2d, ConvTranspose2d, PixelShuffle, Sequential
 from .gdn import GDN
 
@@ -151,12 +151,17 @@ def chain_fusable(units) -> bool:
 def residual_chain(units, x, out_masked: bool = False):
     """ResidualUnits applied in sequence, as one ResidualChainFn node (fusable units only).  out_masked: the
     caller's consumer applies the last unit's ReLU mask to the gradient (MASK_POS dgrad, GateFn relu_a)."""
+    specs, params = _chain_specs(units)
+    return ResidualChainFn.apply(x, specs, bool(out_masked), *params)
+
+
+def _chain_specs(units):
     specs, params = [], []
     for u in units:
         sp, pr = u.chain_args()
         specs.append(sp)
         params.extend(pr)
-    return ResidualChainFn.apply(x, tuple(specs), bool(out_masked), *params)
+    return tuple(specs), params
 
 
 class AttentionBlock(nn.Module):
@@ -171,8 +176,10 @@ class AttentionBlock(nn.Module):
         ua, ub = list(self.conv_a), list(self.conv_b)[:3]
         if not (chain_fusable(ua) and chain_fusable(ub)):
             return GateFn.apply(self.conv_a(x), self.conv_b(x), x)
-        # each branch's three ResidualUnits as one chain node (layers.py:225-236); the chains' last ReLU masks
-        # in their consumers' backward: conv_b's 1x1 conv dgrad (MASK_POS) and the gate's da
-        a = residual_chain(ua, x, out_masked=True)
-        b = self.conv_b[3].run(residual_chain(ub, x, out_masked=True), in_mask=MASK_POS)
-        return GateFn.apply(a, b, x, True)
+        # one autograd node: each branch's three ResidualUnits as a chain (layers.py:225-236), the chains' last
+        # ReLU masks in their consumers' backward (conv_b's 1x1 conv dgrad MASK_POS, the gate's da), x's three
+        # gradients summed in the branches' first dgrad epilogues
+        sa, pa = _chain_specs(ua)
+        sb, pb = _chain_specs(ub)
+        c3 = self.conv_b[3]
+        return AttentionBlockFn.apply(x, sa, sb, c3._spec(in_mask=MASK_POS), *pa, *pb, c3.weight, c3.bias)

@@ -68,6 +68,8 @@ struct ConvArgs {
     float mask_param;
     const bf16* res;         // residual input (cai_conv_fwd_res): y = act(conv + bias + res), pixel-major bf16, NULL: none
     int res_ld;
+    const bf16* res2;        // a second residual (dgrad only, cai_conv_dgrad_res2), same layout as res; NULL: none
+    int res2_ld;
     int ksplit;              // K splits per phase (grid.z = nphase * ksplit)
     float* ws;               // split-K partials [nphase*ksplit][ws_rows][ws_ld] fp32
     int ws_rows, ws_ld;
@@ -128,10 +130,12 @@ __device__ __forceinline__ void store_out_chunk(const ConvArgs& a, const PhaseDe
     int b, oy, ox;
     out_pixel<T>(a, P, plane, m, b, oy, ox);
     if (a.res) {
-        const bf16* R = a.res + (((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.res_ld + n;
+        const int64_t px = ((int64_t)b * a.out_h + oy) * a.out_w + ox;
+        const bf16* R = a.res + px * a.res_ld + n;
+        const bf16* R2 = a.res2 ? a.res2 + px * a.res2_ld + n : nullptr;
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-            if (e < VO) v[e] = apply_act(v[e] + (float)R[e], a.act, a.act_param);
+            if (e < VO) v[e] = apply_act(v[e] + (float)R[e] + (R2 ? (float)R2[e] : 0.f), a.act, a.act_param);
     }
     if (a.mask_mode) {
         const T* AUX = reinterpret_cast<const T*>(a.aux);
@@ -156,8 +160,12 @@ __device__ __forceinline__ void store_out_scalar(const ConvArgs& a, const PhaseD
                                                  float v) {
     int b, oy, ox;
     out_pixel<T>(a, P, plane, m, b, oy, ox);
-    if (a.res)
-        v = apply_act(v + (float)a.res[(((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.res_ld + n], a.act, a.act_param);
+    if (a.res) {
+        const int64_t px = ((int64_t)b * a.out_h + oy) * a.out_w + ox;
+        v += (float)a.res[px * a.res_ld + n];
+        if (a.res2) v += (float)a.res2[px * a.res2_ld + n];
+        v = apply_act(v, a.act, a.act_param);
+    }
     if (a.mask_mode) {
         const T* AUX = reinterpret_cast<const T*>(a.aux);
         v *= mask_val(a.mask_mode, to_f32(AUX[(((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.aux_ld + n]),
@@ -298,16 +306,27 @@ __device__ __forceinline__ void conv_epilogue_rows_t(const ConvArgs& a, const Ph
             const bf16* AUX = (NOLDS && a.mask_mode) ? reinterpret_cast<const bf16*>(a.aux) +
                                                            (((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.aux_ld
                                                      : nullptr;
-            const bf16* RS = a.res ? a.res + (((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.res_ld : nullptr;
+            const int64_t rpx = ((int64_t)b * a.out_h + oy) * a.out_w + ox;
+            const bf16* RS = a.res ? a.res + rpx * a.res_ld : nullptr;
+            const bf16* RS2 = a.res2 ? a.res2 + rpx * a.res2_ld : nullptr;
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn) {
                 const int n = n0 + wn * WTN + tn * 16 + 4 * g_;
                 if (n >= a.Cout) continue;
                 f32x4 v;
-                bf16x4 rv = bf16x4{(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
-                if (RS) rv = *reinterpret_cast<const bf16x4*>(RS + n);
+                f32x4 rf = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (RS) {
+                    const bf16x4 rv = *reinterpret_cast<const bf16x4*>(RS + n);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = apply_act(acc[tm][tn][r] + bv[tn][r] + (float)rv[r], a.act, a.act_param);
+                    for (int r = 0; r < 4; ++r) rf[r] = (float)rv[r];
+                    if (RS2) {
+                        const bf16x4 rv2 = *reinterpret_cast<const bf16x4*>(RS2 + n);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) rf[r] += (float)rv2[r];
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = apply_act(acc[tm][tn][r] + bv[tn][r] + rf[r], a.act, a.act_param);
                 if (NOLDS && AUX) {
                     const bf16x4 mv = *reinterpret_cast<const bf16x4*>(AUX + n);
 #pragma unroll
@@ -3501,7 +3520,7 @@ static int run_conv(const cai_conv_geom* g, int dtype, int direction, const void
                     const void* w, const float* bias, int act, float act_param, void* y, int y_dtype, int64_t ysb,
                     int64_t ysc, int64_t ysy, int64_t ysx, const void* aux, int aux_ld, int mask_mode,
                     float mask_param, void* workspace, size_t ws_bytes, void* stream, const char* name,
-                    const void* res = nullptr, int res_ld = 0) {
+                    const void* res = nullptr, int res_ld = 0, const void* res2 = nullptr, int res2_ld = 0) {
     int rc = check_geom(g);
     if (rc) return rc;
     CAI_CHECK_ARG(dtype == CAI_BF16 || dtype == CAI_F32, "%s: bad dtype", name);
@@ -3536,7 +3555,12 @@ static int run_conv(const cai_conv_geom* g, int dtype, int direction, const void
                            (!mask_mode || direction == 1) &&
                            res_ld >= P.kout_c && res_ld % 4 == 0 && ((uintptr_t)res & 7) == 0),
                   "%s: residual needs a bf16 pixel-major output and res_ld >= Cout, a multiple of 4", name);
+    CAI_CHECK_ARG(!res2 || (res && direction == 1 && res2_ld >= P.kout_c && res2_ld % 4 == 0 &&
+                            ((uintptr_t)res2 & 7) == 0),
+                  "%s: a second residual needs the first, the dgrad direction and res2_ld >= Cout, a multiple of 4",
+                  name);
     a.res = reinterpret_cast<const bf16*>(res); a.res_ld = res_ld;
+    a.res2 = reinterpret_cast<const bf16*>(res2); a.res2_ld = res2_ld;
     if ((L.halo_ph || L.halo_s1) && L.hbn > 128 && L.ksplit == 1 && !epi_t_direct(a))
         L = conv_launch(g, dtype, direction, in_abs, false);    // the 192-channel tiles store from registers only
     CAI_CHECK_ARG(L.ws_bytes == 0 || (workspace && ws_bytes >= L.ws_bytes && ((uintptr_t)workspace & 15) == 0),
@@ -3938,6 +3962,19 @@ int cai_conv_dgrad_res(const cai_conv_geom* g, int dtype, const void* dy, int32_
     return run_conv(g, dtype, 1, dy, dy_ld, 0, packed_wt, nullptr, CAI_ACT_NONE, 0.f, dx, dtype,
                     (int64_t)g->in_h * g->in_w * ld, 1, (int64_t)g->in_w * ld, ld, aux, aux_ld, mask_mode, mask_param,
                     workspace, ws_bytes, stream, "conv_dgrad_res", res, res_ld);
+}
+
+int cai_conv_dgrad_res2(const cai_conv_geom* g, int dtype, const void* dy, int32_t dy_ld, const void* packed_wt,
+                        const void* res, int32_t res_ld, const void* res2, int32_t res2_ld, void* dx, int32_t dx_ld,
+                        int32_t mask_mode, float mask_param, const void* aux, int32_t aux_ld, void* workspace,
+                        size_t ws_bytes, void* stream) {
+    int rc = check_geom(g);
+    if (rc) return rc;
+    CAI_CHECK_ARG(res && res2, "conv_dgrad_res2: null residual");
+    const int64_t ld = dx_ld;
+    return run_conv(g, dtype, 1, dy, dy_ld, 0, packed_wt, nullptr, CAI_ACT_NONE, 0.f, dx, dtype,
+                    (int64_t)g->in_h * g->in_w * ld, 1, (int64_t)g->in_w * ld, ld, aux, aux_ld, mask_mode, mask_param,
+                    workspace, ws_bytes, stream, "conv_dgrad_res2", res, res_ld, res2, res2_ld);
 }
 
 const char* cai_conv_kernel_name(const cai_conv_geom* g, int dtype, int direction, int32_t in_abs) {

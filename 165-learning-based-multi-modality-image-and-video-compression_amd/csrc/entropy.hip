@@ -242,7 +242,9 @@ __device__ __forceinline__ float softplus_grad(float v) {   // torch softplus ba
     const float z = expf(v);
     return z / (z + 1.f);
 }
-__device__ __forceinline__ float sigmoid_f(float v) { return 1.f / (1.f + expf(-v)); }
+// the division as v_rcp_f32 (1 ulp): the IEEE divide's scale / fmas / fixup sequence was ~10 instructions, two per
+// chain pair in both EntropyBottleneck kernels
+__device__ __forceinline__ float sigmoid_f(float v) { return __builtin_amdgcn_rcpf(1.f + expf(-v)); }
 
 // Address of the raw parameter behind element k of channel c's table (layout
 // above; k < EB_NP, always a valid address -- the pad slot reads the median).
@@ -300,18 +302,16 @@ __device__ __forceinline__ void eb_fill_tables(int c0, int nch, int C, const cai
 // the libm tanhf with its special-case branches -- the chains evaluate 12 per call and dominated the
 // EntropyBottleneck kernels.  The forward and backward kernels share it, so the backward re-derives exactly the
 // forward's values (sign, LowerBound mask) and reads tanh' = 1 - tanh^2 from the recorded values.
+// Both branches are evaluated and selected (branch-free: a divergent if / else around 12 tanh per chain cost an
+// exec-mask save / restore and a scalar branch each), the large-|x| branch with v_rcp_f32 (1 ulp).
 __device__ __forceinline__ float eb_tanh(float x) {
     const float ax = fabsf(x);
-    float r;
-    if (ax < 0.625f) {
-        const float z = x * x;
-        r = ((((-5.70498872745e-3f * z + 2.06390887954e-2f) * z - 5.37397155531e-2f) * z + 1.33314422036e-1f) * z -
-             3.33332819422e-1f) * z * x + x;
-    } else {
-        const float e = __expf(2.f * fminf(ax, 9.f));
-        r = copysignf(1.f - 2.f / (e + 1.f), x);
-    }
-    return r;
+    const float z = x * x;
+    const float p = ((((-5.70498872745e-3f * z + 2.06390887954e-2f) * z - 5.37397155531e-2f) * z + 1.33314422036e-1f) *
+                         z - 3.33332819422e-1f) * z * x + x;
+    const float e = __expf(2.f * fminf(ax, 9.f));
+    const float q = copysignf(1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f), x);
+    return ax < 0.625f ? p : q;
 }
 
 // forward of one chain; records the tanh of every hidden pre-activation and every hidden output
@@ -416,6 +416,9 @@ __device__ __forceinline__ float eb_chain_dx(float d, const float* t, const EbTr
     return 0.f;
 }
 
+#ifndef EB_FWD_PPL
+#define EB_FWD_PPL 4
+#endif
 // fwd: block = 256 threads = 32 channels x 8 pixel rows
 __global__ __launch_bounds__(256) void eb_fwd_kernel(int mode, int64_t npix, int C, cai_eb_params P,
                                                       const void* __restrict__ x, int xdt, int xld,
@@ -449,6 +452,9 @@ __global__ __launch_bounds__(256) void eb_fwd_kernel(int mode, int64_t npix, int
     noise_close(ns, nv);   // thread 0 (c = c0 < C) always gets here
 }
 
+#ifndef EB_BWD_PPL
+#define EB_BWD_PPL 4
+#endif
 // bwd: grid (C, S): block (c, s) takes every S-th 256-pixel slice of channel c, one chain pair per thread and
 // pass; its 60 per-channel parameter sums reduce in a fixed order (lanes by xor-shuffles, the 4 waves through
 // LDS).  With S > 1 each block stores its 60 sums write-through (sc1) into part[c][s], and the block whose
@@ -502,7 +508,7 @@ __global__ __launch_bounds__(256) void eb_bwd_kernel(int mode, int64_t npix, int
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
     for (int k = 0; k < EB_NP; ++k) {
-        const float v = wave_sum(g[k]);
+        const float v = wave_sum_dpp(g[k]);
         if (lane == 0) red[w][k] = v;
     }
     __syncthreads();
@@ -851,7 +857,8 @@ int cai_eb_fwd(int mode, int64_t npix, int32_t C, const cai_eb_params* prm, cons
     if (ns.kind < 0) return CAI_EINVAL;
     if (npix * C == 0) return CAI_OK;
     const int gx = (C + 31) / 32;
-    int64_t gy = (npix + 7) / 8;   // one pixel row per thread and pass
+    // EB_FWD_PPL pixel rows per thread (one row per block and pass each took its own table fill: 45 us on C1's y)
+    int64_t gy = (npix + 8 * EB_FWD_PPL - 1) / (8 * EB_FWD_PPL);
     if (gy > 1024) gy = 1024;
     if (ns.kind == CAI_NOISE_DRAW) gy = std::max<int64_t>(1, std::min<int64_t>(gy, kDrawBlocks / gx));
     hipLaunchKernelGGL(eb_fwd_kernel, dim3(gx, (unsigned)gy), dim3(256), 0, as_stream(stream), mode, npix, C,
@@ -861,8 +868,11 @@ int cai_eb_fwd(int mode, int64_t npix, int32_t C, const cai_eb_params* prm, cons
 }
 
 static int eb_bwd_splits(int64_t npix) {
-    // one 256-pixel slice per block and pass; blocks of one channel hand their sums to the last arriver
-    return (int)std::max<int64_t>(1, std::min<int64_t>((npix + 255) / 256, 64));
+    // EB_BWD_PPL pixels per thread; the blocks of one channel hand their sums to the last arriver.  (One pixel
+    // per thread, 64 blocks per channel, repeated every block's table fill, 60 wave sums and hand-off for a single
+    // chain pair: C1's backward took 220 us.)
+    const int64_t per_block = 256 * EB_BWD_PPL;
+    return (int)std::max<int64_t>(1, std::min<int64_t>((npix + per_block - 1) / per_block, 64));
 }
 static int eb_aux_blocks(int C) { return (C + EB_AUX_CH - 1) / EB_AUX_CH; }
 

@@ -158,20 +158,37 @@ def replay_time(entry, reps: int) -> float:
     return e0.elapsed_time(e1) / reps
 
 
+def lib_build() -> str:
+    """sha256 prefix of the libcai.so this process runs: PMC records are only valid for the build they measured."""
+    import hashlib
+
+    from compressai._native import LIB_PATH
+
+    with open(LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def pmc_traffic(workload: str, kernel: str, shape: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/pmc_traffic.json, written by
-    tools/pmc_traffic.sh + tools/pmc_traffic_update.py: 2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md 'HBM'); None when no measurement
-    of this exact launch is committed."""
+    """(HBM bytes per launch, note) from the committed rocprofv3 PMC passes (profiles/pmc_traffic.json, written by
+    tools/pmc_traffic.sh + tools/pmc_traffic_update.py: 2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md 'HBM').
+    A record counts only for the libcai.so build it measured (its lib_sha256): bytes None when no record of this
+    exact launch and build is committed."""
     try:
         recs = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
     except (OSError, ValueError):
-        return None
+        return None, "no PMC record committed"
     if isinstance(recs, dict):
         recs = [recs]
+    build = lib_build()
+    stale = None
     for r in recs:
         if r.get("workload") == workload and r.get("kernel") == kernel and r.get("shape") == shape:
-            return r.get("hbm_bytes_per_launch")
-    return None
+            if r.get("lib_sha256") == build:
+                return r.get("hbm_bytes_per_launch"), f"rocprofv3 FETCH/WRITE passes of this launch, build {build}"
+            stale = r.get("lib_sha256")
+    if stale is not None or any(r.get("kernel") == kernel for r in recs):
+        return None, f"PMC record of this launch is for another build ({stale}); this build {build}: re-measure"
+    return None, "no PMC record of this launch"
 
 
 def dominant_roofline(led, workload: str, reps: int = 20, pick=None):
@@ -198,10 +215,11 @@ def dominant_roofline(led, workload: str, reps: int = 20, pick=None):
     kernels = [e.kernel]
     if e.kind == "conv_wgrad" and e.kernel.startswith(("wgrad_halo", "wgrad_glds")):
         kernels.append("reduce_jobs_kernel")
+    traffic, tnote = pmc_traffic(workload, e.kernel, e.shape)
     return {"kernel": e.kernel, "op_kernels": kernels, "launch": f"{e.kind}: {e.shape}", "bound": bound,
             "achieved": round(achieved, 2),
             "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
-            "traffic": pmc_traffic(workload, e.kernel, e.shape),
+            "traffic": traffic, "traffic_note": tnote, "lib_sha256": lib_build(),
             "avg_launch_ms": round(ms, 5), "in_step_ms": round(e.ms, 5),
             "algorithmic_flop_per_launch": e.flops, "algorithmic_bytes_per_launch": e.nbytes,
             "timing": f"HIP events on the launch's stream, {reps} back-to-back replays"}

@@ -164,6 +164,16 @@ int cai_conv_dgrad_res(const cai_conv_geom* g, int dtype,
                        int32_t mask_mode, float mask_param, const void* aux, int32_t aux_ld,
                        void* workspace, size_t ws_bytes, void* stream);
 
+/* as cai_conv_dgrad_res with a second residual gradient: dx = mask(aux) *
+ * (conv_input_grad(dy) + res + res2) -- AttentionBlock's input (layers.py:
+ * 196-244) feeds both residual branches and the gate's `+ identity`. */
+int cai_conv_dgrad_res2(const cai_conv_geom* g, int dtype,
+                        const void* dy, int32_t dy_ld, const void* packed_wt,
+                        const void* res, int32_t res_ld, const void* res2, int32_t res2_ld,
+                        void* dx, int32_t dx_ld,
+                        int32_t mask_mode, float mask_param, const void* aux, int32_t aux_ld,
+                        void* workspace, size_t ws_bytes, void* stream);
+
 /* Diagnostics for measurement (bench.py's per-launch roofline):
  * the kernel a conv call would launch (direction 0 = forward, 1 = input
  * gradient, 2 = weight gradient) as the name rocprofv3 reports, "" for an

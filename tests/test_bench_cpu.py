@@ -92,3 +92,24 @@ def test_dominant_class_sums_launches_of_one_kernel():
     assert d["kernel"] == "conv_small_kernel" and d["launches"] == 10
     assert abs(d["ms_per_step"] - 0.2) < 1e-9 and abs(d["frac"] - 0.05) < 1e-9
     assert abs(d["share_of_instrumented"] - 0.2 / 0.25) < 1e-4
+
+
+def test_pmc_traffic_only_for_the_measured_build(tmp_path, monkeypatch):
+    """bench.py's roofline `traffic` comes from a committed rocprofv3 record only when that record measured the
+    libcai.so this process runs (lib_sha256); a record of another build gives traffic None and says so."""
+    import json
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    monkeypatch.setattr(bench, "lib_build", lambda: "aaaa")
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    rec = {"workload": "w", "kernel": "k", "shape": "s", "hbm_bytes_per_launch": 123, "lib_sha256": "aaaa"}
+    (prof / "pmc_traffic.json").write_text(json.dumps([rec]))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert bench.pmc_traffic("w", "k", "s")[0] == 123
+    monkeypatch.setattr(bench, "lib_build", lambda: "bbbb")
+    t, note = bench.pmc_traffic("w", "k", "s")
+    assert t is None and "another build" in note
+    assert bench.pmc_traffic("w", "k2", "s")[0] is None

@@ -696,14 +696,15 @@ def test_attention_block_residual_chains(cuda, B, N, H):
 
 
 def test_attention_block_chain_launches(cuda, monkeypatch):
-    """One AttentionBlock step: 6 residual-epilogue forwards, 6 residual dgrads, no add_act and no
-    activation-backward launch (the chains' last ReLU masks in the 1x1 conv's dgrad and the gate backward)."""
+    """One AttentionBlock step: 6 residual-epilogue forwards, 6 residual dgrads (the branches' first units with a
+    second residual: x's three gradients summed there), no add_act and no activation-backward launch (the chains'
+    last ReLU masks in the 1x1 conv's dgrad and the gate backward)."""
     import compressai.layers as L
     from compressai import _ops
 
     calls = []
     real = _ops.lib
-    watch = ("cai_conv_fwd_res", "cai_conv_dgrad_res", "cai_add_act", "cai_act_bwd")
+    watch = ("cai_conv_fwd_res", "cai_conv_dgrad_res", "cai_conv_dgrad_res2", "cai_add_act", "cai_act_bwd")
 
     class Spy:
         def __getattr__(self, name):
@@ -722,8 +723,8 @@ def test_attention_block_chain_launches(cuda, monkeypatch):
         y = mod(x)
     y.float().sum().backward()
     torch.cuda.synchronize()
-    assert {n: calls.count(n) for n in watch} == {"cai_conv_fwd_res": 6, "cai_conv_dgrad_res": 6, "cai_add_act": 0,
-                                                  "cai_act_bwd": 0}, calls
+    assert {n: calls.count(n) for n in watch} == {"cai_conv_fwd_res": 6, "cai_conv_dgrad_res": 4,
+                                                  "cai_conv_dgrad_res2": 2, "cai_add_act": 0, "cai_act_bwd": 0}, calls
     assert torch.isfinite(x.grad).all()
 
 

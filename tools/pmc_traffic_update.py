@@ -39,7 +39,8 @@ def main():
         sys.exit(f"no {base} dispatches with counters")
     f_kib, w_kib = sorted(f)[len(f) // 2], sorted(w)[len(w) // 2]
     rd, wr = 2.0 * f_kib * 1024, w_kib * 1024
-    rec = {"workload": rl["workload"], "kernel": kernel, "shape": shape, "dispatches": [len(f), len(w)],
+    rec = {"workload": rl["workload"], "kernel": kernel, "shape": shape, "lib_sha256": rl.get("lib_sha256"),
+           "dispatches": [len(f), len(w)],
            "fetch_size_kib": round(f_kib, 1), "write_size_kib": round(w_kib, 1),
            "read_bytes_per_launch": round(rd), "write_bytes_per_launch": round(wr),
            "hbm_bytes_per_launch": round(rd + wr), "algorithmic_bytes_per_launch": rl["algorithmic_bytes_per_launch"],
@@ -52,6 +53,7 @@ def main():
         recs = []
     if isinstance(recs, dict):
         recs = [recs]
+    # one record per launch: a re-measurement (of a new build) replaces the old one
     recs = [r for r in recs if not (r.get("workload") == rec["workload"] and r.get("kernel") == kernel
                                      and r.get("shape") == shape)]
     recs.append(rec)
