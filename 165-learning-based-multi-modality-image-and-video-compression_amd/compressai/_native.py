@@ -69,6 +69,16 @@ class ReduceJob(Structure):
     _fields_ = [("kind", c_int32), ("nblocks", c_int32), ("i", c_int32 * 10), ("f", c_float * 2), ("p", c_void_p * 6)]
 
 
+class ResunitArgs(Structure):
+    _fields_ = [("batch", c_int32), ("h", c_int32), ("w", c_int32), ("n", c_int32),
+                ("x", c_void_p), ("y", c_void_p), ("wa", c_void_p), ("wb", c_void_p), ("wc", c_void_p),
+                ("ba", c_void_p), ("bb", c_void_p), ("bc", c_void_p), ("h1", c_void_p), ("h2", c_void_p),
+                ("out", c_void_p), ("gc", c_void_p), ("gb", c_void_p), ("ga", c_void_p), ("res2", c_void_p),
+                ("xmask", c_void_p), ("x_ld", c_int32), ("y_ld", c_int32), ("out_ld", c_int32),
+                ("res2_ld", c_int32), ("xmask_ld", c_int32), ("kpa", c_int32), ("kpb", c_int32), ("kpc", c_int32),
+                ("gy_masked", c_int32)]
+
+
 # name -> (restype, argtypes)
 _P, _I, _I64, _F, _S = c_void_p, c_int, c_int64, c_float, c_size_t
 _G = POINTER(ConvGeom)
@@ -95,6 +105,7 @@ SIGNATURES = {
     "cai_conv_dgrad_res2": (_I, [_G, _I, _P, c_int32, _P, _P, c_int32, _P, c_int32, _P, c_int32, c_int32, _F, _P,
                                  c_int32, _P, _S, _P]),
     "cai_conv_wgrad_workspace_bytes": (_S, [_G, _I]),
+    "cai_resunit": (_I, [POINTER(ResunitArgs), c_int32, _P]),
     "cai_conv_kernel_name": (c_char_p, [_G, _I, _I, c_int32]),
     "cai_conv_split_factor": (c_int32, [_G, _I, _I, c_int32]),
     "cai_conv_wgrad": (_I, [_G, _I, _P, c_int32, c_int32, c_int32, _P, c_int32, _P, _P, c_int32, _P, _S, _P]),

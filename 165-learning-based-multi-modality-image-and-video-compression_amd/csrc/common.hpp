@@ -139,5 +139,49 @@ __device__ __forceinline__ void wait_vmcnt() {
     __builtin_amdgcn_s_waitcnt(0x0F70 | (N & 15) | ((N >> 4) << 14));
 }
 __device__ __forceinline__ void wait_lgkmcnt0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
+__device__ __forceinline__ void wait_vmcnt_n(int n) {    // n folds to a constant after unrolling
+    switch (n) {
+        case 0: wait_vmcnt<0>(); break;
+        case 1: wait_vmcnt<1>(); break;
+        case 2: wait_vmcnt<2>(); break;
+        case 3: wait_vmcnt<3>(); break;
+        case 4: wait_vmcnt<4>(); break;
+        case 5: wait_vmcnt<5>(); break;
+        case 6: wait_vmcnt<6>(); break;
+        case 7: wait_vmcnt<7>(); break;
+        case 8: wait_vmcnt<8>(); break;
+        case 9: wait_vmcnt<9>(); break;
+        case 10: wait_vmcnt<10>(); break;
+        case 11: wait_vmcnt<11>(); break;
+        case 12: wait_vmcnt<12>(); break;
+        case 13: wait_vmcnt<13>(); break;
+        case 14: wait_vmcnt<14>(); break;
+        case 15: wait_vmcnt<15>(); break;
+        case 16: wait_vmcnt<16>(); break;
+        case 17: wait_vmcnt<17>(); break;
+        case 18: wait_vmcnt<18>(); break;
+        case 19: wait_vmcnt<19>(); break;
+        case 20: wait_vmcnt<20>(); break;
+        case 21: wait_vmcnt<21>(); break;
+        case 22: wait_vmcnt<22>(); break;
+        case 23: wait_vmcnt<23>(); break;
+        default: wait_vmcnt<24>(); break;
+    }
+}
+
+// The LDS DMA (global_load_lds_dwordx4) issued from inline asm.  The waitcnt pass books the builtin
+// (__builtin_amdgcn_global_load_lds) as an LDS write of unknown order: with one in flight every later fragment
+// read waits for lgkmcnt(0) and vmcnt(0) -- every DMA, prefetches included (the weight-gradient kernels measured
+// 97 -> 81 us once their DMAs moved here).  Issued from asm it is invisible; every ring counts its DMAs with
+// explicit vmcnt waits.  M0 carries the wave's LDS base and is restored after the DMA (the compiler reserves it).
+__device__ __forceinline__ void glds16_asm(const void* g, const char* lds_wave_base) {
+    const unsigned lds = __builtin_amdgcn_readfirstlane((unsigned)reinterpret_cast<uintptr_t>(lds_wave_base));
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(lds)
+                 : "memory");
+}
+
 
 }  // namespace cai

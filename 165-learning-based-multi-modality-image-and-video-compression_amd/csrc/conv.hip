@@ -575,20 +575,6 @@ struct Cfg2 {
 typedef const void __attribute__((address_space(1)))* gvoid_ptr;
 typedef void __attribute__((address_space(3)))* lvoid_ptr;
 
-// The LDS DMA (global_load_lds_dwordx4) issued from inline asm.  The waitcnt pass books the builtin
-// (__builtin_amdgcn_global_load_lds) as an LDS write of unknown order: with one in flight every later fragment
-// read waits for lgkmcnt(0) and vmcnt(0) -- every DMA, prefetches included (the weight-gradient kernels measured
-// 97 -> 81 us once their DMAs moved here).  Issued from asm it is invisible; every ring counts its DMAs with
-// explicit vmcnt waits.  M0 carries the wave's LDS base and is restored after the DMA (the compiler reserves it).
-__device__ __forceinline__ void glds16_asm(const void* g, const char* lds_wave_base) {
-    const unsigned lds = __builtin_amdgcn_readfirstlane((unsigned)reinterpret_cast<uintptr_t>(lds_wave_base));
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(g), "s"(lds)
-                 : "memory");
-}
-
 #define GLDS glds16_asm
 
 template <typename C>
@@ -771,7 +757,8 @@ __global__ __launch_bounds__(512, 1) void conv_small_kernel(const ConvArgs a) {
     const int m0 = blockIdx.x * BM;
     if (m0 >= Mph) return;
     const int n0 = blockIdx.y * BN;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // wave-uniform as a scalar: the K-step bookkeeping below stays on the SALU
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int kq = 8 * (lane >> 4);               // this lane's 8 K elements of a 32-wide step
 
     constexpr unsigned OOB = 0x80000000u;          // beyond every buffer: the load returns 0
@@ -809,14 +796,26 @@ __global__ __launch_bounds__(512, 1) void conv_small_kernel(const ConvArgs a) {
     const int k0 = wave * per, k1 = min(nk, k0 + per);
     const int ngroups = (per + D - 1) / D;
 
+    // the tap / channel position of the next K step to load: loads are issued for consecutive K steps (k0,
+    // k0 + 1, ...), so it advances by one 32-channel step per load instead of being re-derived with two integer
+    // divisions (~50 VALU instructions per load: the kernels were VALU-issue bound, 1,400 VALU per wave for 56
+    // MFMAs on C2's h_a[0])
+    int st_kg = k0 * 32, st_t = st_kg / a.Cin_pad;
+    int st_ci = st_kg - st_t * a.Cin_pad, st_ty = st_t / P.ntx;
+    int st_tx = st_t - st_ty * P.ntx;
     auto load = [&](int ks, u32x4 (&fa)[RT], u32x4 (&fb)[CT]) {
         const bool kok = ks < k1;
-        const int kg = ks * 32;
-        const int t = kg / a.Cin_pad;
-        const int ci0 = kg - t * a.Cin_pad;
-        const int ty = t / P.ntx;
-        const int dy = P.dy0 + a.tap_sy * ty, dx = P.dx0 + a.tap_sx * (t - ty * P.ntx);
-        const int delta = (dy * a.IW + dx) * a.x_ld + ci0;
+        const int kg = st_kg;
+        const int dy = P.dy0 + a.tap_sy * st_ty, dx = P.dx0 + a.tap_sx * st_tx;
+        const int delta = (dy * a.IW + dx) * a.x_ld + st_ci;
+        st_kg += 32;
+        st_ci += 32;
+        const bool w1 = st_ci == a.Cin_pad;
+        st_ci = w1 ? 0 : st_ci;
+        st_tx += w1 ? 1 : 0;
+        const bool w2 = st_tx == P.ntx;
+        st_tx = w2 ? 0 : st_tx;
+        st_ty += w2 ? 1 : 0;
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
             // bitwise tests and an unconditional offset: a short-circuit && here becomes a branch
@@ -933,35 +932,6 @@ __host__ __device__ constexpr int halo_younger_sp(int t, int nstb, int npi, int 
     return nstb - 2 + cells + ((last >= lo && last <= t - 1) ? 4 : 0);
 }
 
-__device__ __forceinline__ void wait_vmcnt_n(int n) {    // n folds to a constant after unrolling
-    switch (n) {
-        case 0: wait_vmcnt<0>(); break;
-        case 1: wait_vmcnt<1>(); break;
-        case 2: wait_vmcnt<2>(); break;
-        case 3: wait_vmcnt<3>(); break;
-        case 4: wait_vmcnt<4>(); break;
-        case 5: wait_vmcnt<5>(); break;
-        case 6: wait_vmcnt<6>(); break;
-        case 7: wait_vmcnt<7>(); break;
-        case 8: wait_vmcnt<8>(); break;
-        case 9: wait_vmcnt<9>(); break;
-        case 10: wait_vmcnt<10>(); break;
-        case 11: wait_vmcnt<11>(); break;
-        case 12: wait_vmcnt<12>(); break;
-        case 13: wait_vmcnt<13>(); break;
-        case 14: wait_vmcnt<14>(); break;
-        case 15: wait_vmcnt<15>(); break;
-        case 16: wait_vmcnt<16>(); break;
-        case 17: wait_vmcnt<17>(); break;
-        case 18: wait_vmcnt<18>(); break;
-        case 19: wait_vmcnt<19>(); break;
-        case 20: wait_vmcnt<20>(); break;
-        case 21: wait_vmcnt<21>(); break;
-        case 22: wait_vmcnt<22>(); break;
-        case 23: wait_vmcnt<23>(); break;
-        default: wait_vmcnt<24>(); break;
-    }
-}
 
 // transposed accumulators + register-direct epilogue (conv_epilogue_rows_t) in the halo kernels: the
 // phase kernel's launches 57.8 vs 59.7 us average in the C2 step (profiles/r02_edge_s2d_ab.log, r02af)
@@ -2218,7 +2188,17 @@ struct SwArgs {
     int bsrc_ld, bnpix, bc;
     float* db;
     int bias_from_g;  // Conv2d: db = column sums of G, taken by the main blocks; else by trailing blocks
+    float inv_plane, inv_wg;   // 1 / (Hg * Wg), 1 / Wg: the per-row pixel decomposition without integer division
 };
+
+// n / d for 0 <= n < 2^23 from a float reciprocal and one correction each way (n * inv is off by at most one);
+// a 32-bit integer division is ~25 VALU instructions
+__device__ __forceinline__ int div_small(int n, int d, float inv) {
+    int q = (int)((float)n * inv);
+    const int r = n - q * d;
+    q += (r >= d ? 1 : 0) - (r < 0 ? 1 : 0);
+    return q;
+}
 
 constexpr int SW_NW = 8, SW_STEPS = 4;   // waves; 32-pixel steps per wave (M <= SW_NW * SW_STEPS * 32)
 // 16-byte slot swizzle of a [32][128 B] tile read by ds_read_b64_tr_b16: the 8 rows one half-wave reads
@@ -2302,9 +2282,9 @@ __global__ __launch_bounds__(512, 1) void wgrad_small_kernel(const SwArgs a) {
             const bool okm = (st < s1) & (m < a.M);
             const unsigned goff = (unsigned)(m * a.g_ld + n0 + slot * 8) * 2u;
             rg[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(gr, okm ? goff : OOB, 0, 0));
-            const int b = m / plane;
+            const int b = div_small(m, plane, a.inv_plane);
             const int r = m - b * plane;
-            const int j = r / a.Wg;
+            const int j = div_small(r, a.Wg, a.inv_wg);
             const int iy = j * a.s - a.p + kh, ix = (r - j * a.Wg) * a.s - a.p + kw;
             const bool okx = okm & ((unsigned)iy < (unsigned)a.Hx) & ((unsigned)ix < (unsigned)a.Wx);
             const unsigned xoff = (unsigned)(((b * a.Hx + iy) * a.Wx + ix) * a.x_ld + q0 + slot * 8) * 2u;
@@ -4077,6 +4057,8 @@ static int run_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int3
         sa.dw = dw; sa.accumulate = accumulate;
         sa.bsrc = dy; sa.bsrc_ld = dy_ld; sa.bnpix = g->batch * g->out_h * g->out_w; sa.bc = g->out_c; sa.db = db;
         sa.bias_from_g = !g->transposed;
+        sa.inv_plane = 1.f / (float)(a.Hg * a.Wg);
+        sa.inv_wg = 1.f / (float)a.Wg;
         CAI_CHECK_ARG((int64_t)sa.bnpix * dy_ld * 2 < (1ll << 31) && (int64_t)a.B * a.Hx * a.Wx * a.x_ld * 2 < (1ll << 31),
                       "conv_wgrad: operand larger than 2 GiB");
         const dim3 grid(sa.ncb + ((db && g->transposed) ? 1 : 0), W.Ng / 64);

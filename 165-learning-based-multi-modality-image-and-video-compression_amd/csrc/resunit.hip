@@ -1,0 +1,361 @@
+// cheng2020's ResidualUnit (compressai/layers/layers.py:211-226: AttentionBlock's conv_a / conv_b units,
+// :225-236) in ONE launch per direction:
+//     h1 = relu(conv1x1_a(x) + ba)        N -> N/2
+//     h2 = relu(conv3x3_b(h1) + bb)       N/2 -> N/2, pad 1
+//     y  = relu(conv1x1_c(h2) + bc + x)   N/2 -> N
+// Unfused, a unit is three conv launches per direction (nine per training step with the weight gradients); at the
+// per-GPU batch of C4 (4 x 64 x 64 and 4 x 16 x 16 latents) each is a small-grid, launch- and latency-bound GEMM.
+//
+// A 512-thread block owns an 8 x 8 tile of output pixels and all channels.  Three MFMA phases, all operands in LDS:
+//   A  1x1 over the tile's 10 x 10 halo (the 3x3's input footprint): the halo's N-channel pixels and the layer's
+//      weights staged in MFMA fragment order (16 x 32 bf16 operands, lane-linear 1 KiB pieces: conflict-free reads;
+//      weights by LDS DMA, activations by register loads);  the N/2-channel result goes to an LDS image, zero
+//      outside the image (the 3x3's zero padding);
+//   B  3x3 over that image: 9 taps x N/2 channels, the tap weights streamed through a 4-deep LDS-DMA ring (one
+//      barrier per tap); result to a second LDS image;
+//   C  1x1 back to N channels, the epilogue adds the residual and stores 8 bytes per lane (transposed MFMA
+//      accumulators: each lane holds 4 consecutive channels of one pixel).
+// The halo costs phase A 100 / 64 of its pixels: 6 % of the unit's MACs at N = 192.
+//
+// Backward (input gradient; the weight gradients stay GEMMs over all pixels, compressai/_ops.py): the same three
+// phases on the transposed weights (direction-1 packs of c, b, a) --
+//     gc = gy * (y > 0)                          (unless the consumer already masked gy)
+//     gb = (gc Wc^T) * (h2 > 0)                  on the halo
+//     ga = conv3x3^T(gb) * (h1 > 0)              taps read (r + 2 - ty, c + 2 - tx) of the halo
+//     dx = (ga Wa^T + gc [+ res2]) [* (xmask > 0)]
+// and writes gc / gb / ga for the weight gradients.  Arithmetic: bf16 operands, fp32 accumulation, bf16 results
+// -- the unfused chain's, with the MFMA K order of this kernel.
+#include "common.hpp"
+#include "mfma.hpp"
+
+#include <algorithm>
+
+namespace cai {
+namespace {
+
+template <int NC>
+struct RuCfg {
+    static constexpr int NH = NC / 2;
+    static constexpr int TH = 8, TW = 8, HW = TW + 2, HPX = (TH + 2) * HW;   // 100 halo pixels
+    static constexpr int MTA = (HPX + 15) / 16;             // 7 M tiles over the halo
+    static constexpr int KA = NC / 32, NTA = NH / 16;       // phase A: K steps, N tiles (also phase B's N tiles)
+    static constexpr int KB = NH / 32;                      // phase B: K steps per tap
+    static constexpr int NTC = NC / 16, KC = NH / 32;       // phase C
+    static constexpr int FRAG = 1024;                       // one 16 x 32 bf16 operand, lane-linear
+    static constexpr int XA = MTA * KA * FRAG, WA = NTA * KA * FRAG;
+    static constexpr int TAPB = NTA * KB * FRAG, NSTB = 4;  // one tap of the 3x3 weights; ring depth
+    static constexpr int R1 = (XA + WA > NSTB * TAPB) ? XA + WA : NSTB * TAPB;
+    // hidden-image row stride: 240 B keeps the tap-shifted 16-byte fragment reads and the 8-byte epilogue stores
+    // at most 2-way on the banks for N/2 = 64 and 96 (a 192-B stride is 8-way on the stores)
+    static constexpr int SH = 240;
+    static constexpr int H1B = MTA * 16 * SH, H2B = 64 * SH;
+    static constexpr int WC = NTC * KC * FRAG;
+    static constexpr int BYTES = R1 + H1B + WC + H2B;
+    static_assert(SH >= 2 * NH && BYTES <= 160 * 1024, "resunit LDS");
+    static_assert(NTA % 2 == 0 && NTC % 2 == 0, "two wave columns");
+};
+
+struct RuArgs {
+    const bf16* x;                   // forward: x; backward: gy
+    const bf16* y;                   // backward: y (its ReLU mask when !gy_masked)
+    const bf16 *wa, *wb, *wc;        // packed: forward a, b, c (direction 0); backward c, b, a (direction 1)
+    const float *ba, *bb, *bc;       // forward biases
+    bf16 *h1, *h2;                   // forward outputs / backward masks (ld N/2)
+    bf16* out;                       // y / dx
+    bf16 *gc, *gb, *ga;              // backward outputs (ld N, N/2, N/2); gc unused when gy_masked
+    const bf16* res2;                // backward: one more gradient of x, added to dx (NULL: none)
+    const bf16* xmask;               // backward: dx *= (xmask > 0) (NULL: none)
+    int x_ld, y_ld, out_ld, res2_ld, xmask_ld;
+    int kpa, kpb, kpc;
+    int B, H, W, tiles_x, tiles_y;
+    int gy_masked;
+};
+
+__device__ __forceinline__ u32x4 keep_pos(u32x4 v, u32x4 m) {   // v where m > 0 (bf16 lanes), else 0
+    const bf16x8 mv = __builtin_bit_cast(bf16x8, m);
+    bf16x8 vv = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) vv[e] = (float)mv[e] > 0.f ? vv[e] : (bf16)0.f;
+    return __builtin_bit_cast(u32x4, vv);
+}
+
+template <int NC, bool BWD>
+__global__ __launch_bounds__(512, 1) void resunit_kernel(const RuArgs a) {
+    using R = RuCfg<NC>;
+    constexpr int NH = R::NH, KA = R::KA, NTA = R::NTA, KB = R::KB, NTC = R::NTC, KC = R::KC, MTA = R::MTA;
+    constexpr int FRAG = R::FRAG, SH = R::SH, NSTB = R::NSTB;
+    constexpr int NJA = NTA / 2, NJC = NTC / 2;
+    __shared__ __attribute__((aligned(16))) char smem[R::BYTES];
+    char* const sXA = smem;
+    char* const sWA = smem + R::XA;
+    char* const ring = smem;                       // phase B reuses phase A's region
+    char* const sH1 = smem + R::R1;
+    char* const sWC = sH1 + R::H1B;
+    char* const sH2 = sWC + R::WC;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int l16 = lane & 15, lg = lane >> 4;
+    const int per_img = a.tiles_x * a.tiles_y;
+    const int b = blockIdx.x / per_img, rt = blockIdx.x - (blockIdx.x / per_img) * per_img;
+    const int y0 = (rt / a.tiles_x) * R::TH, x0 = (rt - (rt / a.tiles_x) * a.tiles_x) * R::TW;
+    auto pix = [&](int yy, int xx) -> int64_t { return ((int64_t)b * a.H + yy) * a.W + xx; };
+    // weight fragment (N tile nt, K elements kofs ..): lane -> packed row nt * 16 + l16, 8 elements from 8 lg
+    auto wsrc = [&](const bf16* w, int kp, int nt, int kofs) -> const void* {
+        return w + (int64_t)(nt * 16 + l16) * kp + kofs + 8 * lg;
+    };
+
+    // ---- staging: phase A weights (DMA), phase A activations (registers -> LDS), phase C weights (DMA) ----
+    for (int f = wave; f < NTA * KA; f += 8) {
+        const int nt = f / KA, ks = f - (f / KA) * KA;
+        glds16_asm(wsrc(a.wa, a.kpa, nt, ks * 32), sWA + f * FRAG);
+    }
+    for (int f = wave; f < MTA * KA; f += 8) {
+        const int mt = f / KA, ks = f - (f / KA) * KA;
+        const int q = mt * 16 + l16, hy = q / R::HW, hx = q - (q / R::HW) * R::HW;
+        const int yy = y0 - 1 + hy, xx = x0 - 1 + hx;
+        const bool in = q < R::HPX && (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
+        u32x4 v = u32x4{0u, 0u, 0u, 0u};
+        if (in) {
+            const int64_t p = pix(yy, xx);
+            v = *reinterpret_cast<const u32x4*>(a.x + p * a.x_ld + ks * 32 + 8 * lg);
+            if (BWD && !a.gy_masked) {
+                v = keep_pos(v, *reinterpret_cast<const u32x4*>(a.y + p * a.y_ld + ks * 32 + 8 * lg));
+                if (hy >= 1 && hy <= R::TH && hx >= 1 && hx <= R::TW)
+                    *reinterpret_cast<u32x4*>(a.gc + p * NC + ks * 32 + 8 * lg) = v;
+            }
+        }
+        *reinterpret_cast<u32x4*>(sXA + f * FRAG + lane * 16) = v;
+    }
+    int nwc = 0;
+    for (int f = wave; f < NTC * KC; f += 8, ++nwc) {
+        const int nt = f / KC, ks = f - (f / KC) * KC;
+        glds16_asm(wsrc(a.wc, a.kpc, nt, ks * 32), sWC + f * FRAG);
+    }
+    wait_vmcnt_n(nwc);      // this wave's phase A weights landed (only its phase C DMAs may be in flight)
+    wait_lgkmcnt0();
+    __builtin_amdgcn_s_barrier();
+
+    // ---- phase A: [112 halo px x N] . [N x N/2]; wave (mg, nh): M tiles mg, mg + 4; N tiles nh * NJA .. ----
+    const int mg = wave & 3, nh = wave >> 2;
+    {
+        f32x4 acc[2][NJA];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < NJA; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const bool two = mg + 4 < MTA;
+#pragma unroll
+        for (int ks = 0; ks < KA; ++ks) {
+            u32x4 fa[2];
+            fa[0] = *reinterpret_cast<const u32x4*>(sXA + (mg * KA + ks) * FRAG + lane * 16);
+            fa[1] = two ? *reinterpret_cast<const u32x4*>(sXA + ((mg + 4) * KA + ks) * FRAG + lane * 16) : fa[0];
+#pragma unroll
+            for (int j = 0; j < NJA; ++j) {
+                const u32x4 fb = *reinterpret_cast<const u32x4*>(sWA + ((nh * NJA + j) * KA + ks) * FRAG + lane * 16);
+                acc[0][j] = mma16<bf16>(fb, fa[0], acc[0][j]);
+                if (two) acc[1][j] = mma16<bf16>(fb, fa[1], acc[1][j]);
+            }
+        }
+        // epilogue A: lane = halo pixel q, channels c0 .. c0 + 3
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            if (i == 1 && !two) break;
+            const int q = (mg + 4 * i) * 16 + l16, hy = q / R::HW, hx = q - (q / R::HW) * R::HW;
+            const int yy = y0 - 1 + hy, xx = x0 - 1 + hx;
+            const bool in = q < R::HPX && (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
+            const bool interior = in && hy >= 1 && hy <= R::TH && hx >= 1 && hx <= R::TW;
+            const int64_t p = in ? pix(yy, xx) : 0;
+#pragma unroll
+            for (int j = 0; j < NJA; ++j) {
+                const int c0 = (nh * NJA + j) * 16 + 4 * lg;
+                bf16x4 hv;
+                if (!BWD) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) hv[r] = (bf16)(in ? fmaxf(acc[i][j][r] + a.ba[c0 + r], 0.f) : 0.f);
+                } else {
+                    bf16x4 m = bf16x4{(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+                    if (in) m = *reinterpret_cast<const bf16x4*>(a.h2 + p * NH + c0);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) hv[r] = (bf16)((float)m[r] > 0.f ? acc[i][j][r] : 0.f);
+                }
+                *reinterpret_cast<bf16x4*>(sH1 + q * SH + c0 * 2) = hv;
+                if (interior) *reinterpret_cast<bf16x4*>((BWD ? a.gb : a.h1) + p * NH + c0) = hv;
+            }
+        }
+    }
+    wait_lgkmcnt0();
+    __builtin_amdgcn_s_barrier();      // the halo image is complete; phase A's operands are dead (ring may refill)
+
+    // ---- phase B: 3x3 over the halo image, tap weights through the DMA ring ----
+    constexpr int FB = NTA * KB;       // weight fragments per tap
+    const int nd = wave < FB ? (FB - 1 - wave) / 8 + 1 : 0;   // this wave's DMAs per tap
+    auto issue_tap = [&](int t) {
+        if (t >= 9) return;
+        for (int f = wave; f < FB; f += 8) {
+            const int nt = f / KB, ks = f - (f / KB) * KB;
+            glds16_asm(wsrc(a.wb, a.kpb, nt, t * NH + ks * 32), ring + (t % NSTB) * R::TAPB + f * FRAG);
+        }
+    };
+    issue_tap(0);
+    issue_tap(1);
+    issue_tap(2);
+    const int mb = mg;                              // output rows 2 mb, 2 mb + 1 of the tile
+    const int orow = 2 * mb + (l16 >> 3), ocol = l16 & 7;
+    f32x4 accb[NJA];
+#pragma unroll
+    for (int j = 0; j < NJA; ++j) accb[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+        // taps t + 1, t + 2 (when they exist) were issued after tap t: everything older has landed
+        wait_vmcnt_n((t + 2 <= 8 ? 2 : 8 - t) * nd);
+        __builtin_amdgcn_s_barrier();   // every wave's tap-t DMAs landed, every wave done with tap t - 1's stage
+        issue_tap(t + 3);               // into stage (t + 3) % 4 = (t - 1) % 4
+        const int ty = t / 3, tx = t - (t / 3) * 3;
+        const int hr = BWD ? orow + 2 - ty : orow + ty, hc = BWD ? ocol + 2 - tx : ocol + tx;
+        const char* arow = sH1 + (hr * R::HW + hc) * SH + 16 * lg;
+        const char* wst = ring + (t % NSTB) * R::TAPB + lane * 16;
+#pragma unroll
+        for (int ks = 0; ks < KB; ++ks) {
+            const u32x4 fa = *reinterpret_cast<const u32x4*>(arow + 64 * ks);
+#pragma unroll
+            for (int j = 0; j < NJA; ++j) {
+                const u32x4 fb = *reinterpret_cast<const u32x4*>(wst + ((nh * NJA + j) * KB + ks) * FRAG);
+                accb[j] = mma16<bf16>(fb, fa, accb[j]);
+            }
+        }
+    }
+    // epilogue B: lane = output pixel (orow, ocol) of the tile
+    const int oy = y0 + orow, ox = x0 + ocol;
+    const bool oin = oy < a.H && ox < a.W;
+    const int64_t op = oin ? pix(oy, ox) : 0;
+#pragma unroll
+    for (int j = 0; j < NJA; ++j) {
+        const int c0 = (nh * NJA + j) * 16 + 4 * lg;
+        bf16x4 hv;
+        if (!BWD) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) hv[r] = (bf16)fmaxf(accb[j][r] + a.bb[c0 + r], 0.f);
+        } else {
+            bf16x4 m = bf16x4{(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+            if (oin) m = *reinterpret_cast<const bf16x4*>(a.h1 + op * NH + c0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) hv[r] = (bf16)((float)m[r] > 0.f ? accb[j][r] : 0.f);
+        }
+        *reinterpret_cast<bf16x4*>(sH2 + (mb * 16 + l16) * SH + c0 * 2) = hv;
+        if (oin) *reinterpret_cast<bf16x4*>((BWD ? a.ga : a.h2) + op * NH + c0) = hv;
+    }
+    wait_lgkmcnt0();
+    __builtin_amdgcn_s_barrier();      // (the last tap's wait drained every DMA, phase C's weights included)
+
+    // ---- phase C: [64 px x N/2] . [N/2 x N] + residual ----
+    f32x4 accc[NJC];
+#pragma unroll
+    for (int j = 0; j < NJC; ++j) accc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const char* arow = sH2 + (mb * 16 + l16) * SH + 16 * lg;
+#pragma unroll
+    for (int ks = 0; ks < KC; ++ks) {
+        const u32x4 fa = *reinterpret_cast<const u32x4*>(arow + 64 * ks);
+#pragma unroll
+        for (int j = 0; j < NJC; ++j) {
+            const u32x4 fb = *reinterpret_cast<const u32x4*>(sWC + ((nh * NJC + j) * KC + ks) * FRAG + lane * 16);
+            accc[j] = mma16<bf16>(fb, fa, accc[j]);
+        }
+    }
+    if (!oin) return;
+#pragma unroll
+    for (int j = 0; j < NJC; ++j) {
+        const int c0 = (nh * NJC + j) * 16 + 4 * lg;
+        const bf16x4 xr = *reinterpret_cast<const bf16x4*>(a.x + op * a.x_ld + c0);
+        bf16x4 ov;
+        if (!BWD) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ov[r] = (bf16)fmaxf(accc[j][r] + a.bc[c0 + r] + (float)xr[r], 0.f);
+        } else {
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = (float)xr[r];
+            if (!a.gy_masked) {
+                const bf16x4 ym = *reinterpret_cast<const bf16x4*>(a.y + op * a.y_ld + c0);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = (float)ym[r] > 0.f ? v[r] : 0.f;
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += accc[j][r];
+            if (a.res2) {
+                const bf16x4 r2 = *reinterpret_cast<const bf16x4*>(a.res2 + op * a.res2_ld + c0);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] += (float)r2[r];
+            }
+            if (a.xmask) {
+                const bf16x4 xm = *reinterpret_cast<const bf16x4*>(a.xmask + op * a.xmask_ld + c0);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = (float)xm[r] > 0.f ? v[r] : 0.f;
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ov[r] = (bf16)v[r];
+        }
+        *reinterpret_cast<bf16x4*>(a.out + op * a.out_ld + c0) = ov;
+    }
+}
+
+}  // namespace
+}  // namespace cai
+
+using namespace cai;
+
+extern "C" int cai_resunit(const cai_resunit_args* p, int32_t direction, void* stream) {
+    CAI_CHECK_ARG(p && (direction == 0 || direction == 1), "resunit: bad arguments");
+    const int n = p->n;
+    CAI_CHECK_ARG(n == 128 || n == 192, "resunit: N = %d (128 or 192 supported)", n);
+    CAI_CHECK_ARG(p->batch > 0 && p->h > 0 && p->w > 0, "resunit: bad sizes");
+    CAI_CHECK_ARG(p->x && p->wa && p->wb && p->wc && p->h1 && p->h2 && p->out, "resunit: null pointer");
+    CAI_CHECK_ARG(p->x_ld >= n && p->x_ld % 8 == 0 && ((uintptr_t)p->x & 15) == 0, "resunit: x needs ld %% 8 == 0");
+    CAI_CHECK_ARG(p->out_ld >= n && p->out_ld % 4 == 0, "resunit: out_ld");
+    CAI_CHECK_ARG(p->kpa >= n && p->kpb >= 9 * (n / 2) && p->kpc >= n / 2 && p->kpa % 8 == 0 &&
+                      p->kpb % 8 == 0 && p->kpc % 8 == 0,
+                  "resunit: packed weight rows");
+    if (direction == 0) {
+        CAI_CHECK_ARG(p->ba && p->bb && p->bc, "resunit: forward needs the biases");
+    } else {
+        CAI_CHECK_ARG(p->ga && p->gb && (p->gy_masked || (p->y && p->gc && p->y_ld >= n && p->y_ld % 8 == 0)),
+                      "resunit: backward outputs / y");
+        CAI_CHECK_ARG(!p->res2 || (p->res2_ld >= n && p->res2_ld % 4 == 0), "resunit: res2_ld");
+        CAI_CHECK_ARG(!p->xmask || (p->xmask_ld >= n && p->xmask_ld % 4 == 0), "resunit: xmask_ld");
+    }
+    const int64_t npix = (int64_t)p->batch * p->h * p->w;
+    CAI_CHECK_ARG(npix * std::max(p->x_ld, p->out_ld) < (1ll << 31), "resunit: tensor too large");
+    RuArgs a{};
+    a.x = static_cast<const bf16*>(p->x);
+    a.y = static_cast<const bf16*>(p->y);
+    a.wa = static_cast<const bf16*>(p->wa);
+    a.wb = static_cast<const bf16*>(p->wb);
+    a.wc = static_cast<const bf16*>(p->wc);
+    a.ba = p->ba; a.bb = p->bb; a.bc = p->bc;
+    a.h1 = static_cast<bf16*>(p->h1);
+    a.h2 = static_cast<bf16*>(p->h2);
+    a.out = static_cast<bf16*>(p->out);
+    a.gc = static_cast<bf16*>(p->gc);
+    a.gb = static_cast<bf16*>(p->gb);
+    a.ga = static_cast<bf16*>(p->ga);
+    a.res2 = static_cast<const bf16*>(p->res2);
+    a.xmask = static_cast<const bf16*>(p->xmask);
+    a.x_ld = p->x_ld; a.y_ld = p->y_ld; a.out_ld = p->out_ld; a.res2_ld = p->res2_ld; a.xmask_ld = p->xmask_ld;
+    a.kpa = p->kpa; a.kpb = p->kpb; a.kpc = p->kpc;
+    a.B = p->batch; a.H = p->h; a.W = p->w;
+    a.tiles_x = (p->w + 7) / 8;
+    a.tiles_y = (p->h + 7) / 8;
+    a.gy_masked = p->gy_masked;
+    const dim3 grid((unsigned)(p->batch * a.tiles_x * a.tiles_y));
+    hipStream_t st = as_stream(stream);
+    if (n == 192 && direction)
+        hipLaunchKernelGGL((resunit_kernel<192, true>), grid, dim3(512), 0, st, a);
+    else if (n == 192)
+        hipLaunchKernelGGL((resunit_kernel<192, false>), grid, dim3(512), 0, st, a);
+    else if (direction)
+        hipLaunchKernelGGL((resunit_kernel<128, true>), grid, dim3(512), 0, st, a);
+    else
+        hipLaunchKernelGGL((resunit_kernel<128, false>), grid, dim3(512), 0, st, a);
+    CAI_LAUNCH_CHECK("resunit");
+    return CAI_OK;
+}

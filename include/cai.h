@@ -174,6 +174,41 @@ int cai_conv_dgrad_res2(const cai_conv_geom* g, int dtype,
                         int32_t mask_mode, float mask_param, const void* aux, int32_t aux_ld,
                         void* workspace, size_t ws_bytes, void* stream);
 
+/* cheng2020's ResidualUnit (layers.py:211-226; AttentionBlock's conv_a / conv_b units, :225-236) in ONE launch
+ * per direction (csrc/resunit.hip): h1 = relu(conv1x1_a(x) + ba), h2 = relu(conv3x3_b(h1) + bb),
+ * y = relu(conv1x1_c(h2) + bc + x); x / y with n in {128, 192} channels, h1 / h2 with n / 2 (ld n / 2), bf16
+ * pixel-major.  Replaces the unit's three cai_conv_fwd(_res) calls (forward) and three cai_conv_dgrad(_res)
+ * calls (backward); the weight gradients stay cai_conv_wgrad calls on the tensors this writes.
+ *   direction 0: x = the unit input; wa / wb / wc = a, b, c packed for direction 0 (cai_conv_pack_weight) with
+ *     row lengths kpa / kpb / kpc; writes h1, h2 and out = y.
+ *   direction 1: x = gy (dLoss/dy; y = the forward output, its ReLU mask applied here unless gy_masked);
+ *     wa / wb / wc = c, b, a packed for direction 1; h1 / h2 = the forward's; writes gc = gy * (y > 0) (when
+ *     !gy_masked), gb = dLoss/d(b's pre-activation), ga = dLoss/d(a's pre-activation) and
+ *     out = dx = (ga . Wa^T + gc [+ res2]) [* (xmask > 0)]. */
+typedef struct cai_resunit_args {
+    int32_t batch, h, w, n;
+    const void* x;
+    const void* y;
+    const void* wa;
+    const void* wb;
+    const void* wc;
+    const float* ba;
+    const float* bb;
+    const float* bc;
+    void* h1;
+    void* h2;
+    void* out;
+    void* gc;
+    void* gb;
+    void* ga;
+    const void* res2;
+    const void* xmask;
+    int32_t x_ld, y_ld, out_ld, res2_ld, xmask_ld;
+    int32_t kpa, kpb, kpc;
+    int32_t gy_masked;
+} cai_resunit_args;
+int cai_resunit(const cai_resunit_args* args, int32_t direction, void* stream);
+
 /* Diagnostics for measurement (bench.py's per-launch roofline):
  * the kernel a conv call would launch (direction 0 = forward, 1 = input
  * gradient, 2 = weight gradient) as the name rocprofv3 reports, "" for an
