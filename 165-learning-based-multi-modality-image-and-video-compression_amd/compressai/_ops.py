@@ -29,7 +29,7 @@ import torch
 from . import _ledger
 from ._native import (ACT_LEAKY, ACT_NONE, ACT_RELU, BF16, F32, MASK_LEAKY, MASK_NONE, MASK_POS, Q_DEQUANTIZE, Q_NOISE,
                       JOB_NONE, NOISE_BUF, NOISE_DRAW, NOISE_REPLAY, ConvGeom, EbGrads, EbParams, NoiseSrc, RdGrads,
-                      RdInputs, ReduceJob, lib)
+                      RdInputs, ReduceJob, ResunitArgs, lib)
 
 _VP = ctypes.c_void_p
 _GDN_TWO_PASS = os.environ.get("CAI_GDN_TWO_PASS", "0") == "1"   # A/B knobs (tools/ab_env.sh)
@@ -668,37 +668,48 @@ class ConvFn(torch.autograd.Function):
                 if rmask != MASK_NONE:
                     raise RuntimeError("conv dgrad: a residual-gradient mask needs the fused bf16 path")
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
-            nbytes = lib.cai_conv_wgrad_workspace_bytes(ctypes.byref(g), code)
             wparam, bparam = ctx.params
-            direct = direct_grad(wparam) and (bparam is None or direct_grad(bparam))
-            if direct:   # accumulate straight into the optimizer's flat gradient buffer
-                dw, db = wparam.grad, (bparam.grad if bparam is not None else None)
-            else:
-                dw = torch.empty(weight.shape, dtype=torch.float32, device=gy.device)
-                db = torch.empty(g.out_c, dtype=torch.float32, device=gy.device) if ctx.has_bias else None
-            fl, nb = _ledger.conv_cost(g, _es(dt), 2)
-            if defer_reduce_ok(direct):
-                wws = torch.empty(nbytes, dtype=torch.uint8, device=gy.device)
-                job = ReduceJob()
-                lib.cai_conv_wgrad_deferred(ctypes.byref(g), code, _p(xpm), ctx.xld, int(spec.in_abs), 0, _p(gpm),
-                                            gld, _p(dw), _p(db), 1, _p(wws), nbytes, st, ctypes.byref(job))
-                defer_job(job, gy.device, wws)
-            else:
-                with _WgradLaunch(gy.device, direct, xpm, gpm):
-                    wws = torch.empty(nbytes, dtype=torch.uint8, device=gy.device)
-                    sw = _stream()
-                    _ledger.run(lambda dw=dw, db=db: lib.cai_conv_wgrad(ctypes.byref(g), code, _p(xpm), ctx.xld,
-                                                                        int(spec.in_abs), 0, _p(gpm), gld, _p(dw),
-                                                                        _p(db), int(direct), _p(wws), nbytes, sw),
-                                "conv_wgrad", _conv_kernel(g, dt, 2, spec.in_abs), fl, nb, dt, _ledger.shape_of(g))
-            if direct:
-                dw = db = None
-            elif weight.dtype != torch.float32:
-                dw = dw.to(weight.dtype)
+            dw, db = conv_wgrad(g, dt, xpm, ctx.xld, int(spec.in_abs), gpm, gld, wparam, bparam, weight,
+                                ctx.has_bias)
         dres = None
         if ctx.has_res and ctx.needs_input_grad[4]:
             dres = gpm
         return dx, dw, db, None, dres
+
+
+def conv_wgrad(g, dt, xpm, xld, in_abs, gpm, gld, wparam, bparam, weight, has_bias):
+    """Weight (+ bias) gradient of one conv from its input xpm and output gradient gpm (pixel-major): straight
+    into the optimizer's flat buffer when the parameters are direct_grad (returns None, None; the final reduce
+    deferred to the end of the backward), else fresh tensors."""
+    code = dcode(dt)
+    dev = gpm.device
+    nbytes = lib.cai_conv_wgrad_workspace_bytes(ctypes.byref(g), code)
+    direct = direct_grad(wparam) and (bparam is None or direct_grad(bparam))
+    if direct:   # accumulate straight into the optimizer's flat gradient buffer
+        dw, db = wparam.grad, (bparam.grad if bparam is not None else None)
+    else:
+        dw = torch.empty(weight.shape, dtype=torch.float32, device=dev)
+        db = torch.empty(g.out_c, dtype=torch.float32, device=dev) if has_bias else None
+    fl, nb = _ledger.conv_cost(g, _es(dt), 2)
+    st = _stream()
+    if defer_reduce_ok(direct):
+        wws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        job = ReduceJob()
+        lib.cai_conv_wgrad_deferred(ctypes.byref(g), code, _p(xpm), xld, int(in_abs), 0, _p(gpm), gld, _p(dw),
+                                    _p(db), 1, _p(wws), nbytes, st, ctypes.byref(job))
+        defer_job(job, dev, wws)
+    else:
+        with _WgradLaunch(dev, direct, xpm, gpm):
+            wws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            sw = _stream()
+            _ledger.run(lambda: lib.cai_conv_wgrad(ctypes.byref(g), code, _p(xpm), xld, int(in_abs), 0, _p(gpm), gld,
+                                                   _p(dw), _p(db), int(direct), _p(wws), nbytes, sw),
+                        "conv_wgrad", _conv_kernel(g, dt, 2, in_abs), fl, nb, dt, _ledger.shape_of(g))
+    if direct:
+        return None, None
+    if weight.dtype != torch.float32:
+        dw = dw.to(weight.dtype)
+    return dw, db
 
 
 class _SubCtx:
@@ -728,7 +739,7 @@ class ResidualChainFn(torch.autograd.Function):
     def forward(ctx, x, specs, out_masked, *params):
         need = ctx.needs_input_grad   # (x, specs, out_masked, *params)
         y, ctx.subs = _chain_forward(x, specs, out_masked, params, need[0], need[3:])
-        _stash(ctx, [c for trio in ctx.subs for c in trio])
+        _stash(ctx, _unit_ctxs(ctx.subs))
         return y
 
     @staticmethod
@@ -771,11 +782,125 @@ class _unstash:
         return False
 
 
+# One launch per ResidualUnit and direction (csrc/resunit.hip) instead of three conv launches: bf16, N in {128, 192}.
+# CAI_RESUNIT_FUSED=0 keeps the per-conv chain (A/B).
+_RESUNIT_FUSED = os.environ.get("CAI_RESUNIT_FUSED", "1") == "1"
+_SPEC_1x1, _SPEC_3x3 = ConvSpec(1, 1, 0), ConvSpec(3, 1, 1)
+
+
+class _FusedUnit:
+    """A ResidualUnit run by cai_resunit: saved tensors (x, h1, h2, y) and what its backward needs."""
+
+    __slots__ = ("saved_tensors", "params", "geoms", "gy_masked", "mask_x", "dx_res2", "dx_res", "need_x")
+
+    def __init__(self, params, geoms, need_x):
+        self.params, self.geoms, self.need_x = params, geoms, need_x
+        self.saved_tensors = ()
+        self.gy_masked = self.mask_x = False
+        self.dx_res2 = self.dx_res = None
+
+
+def _resunit_ok(y, specs, params) -> bool:
+    if not _RESUNIT_FUSED or compute_dtype() != torch.bfloat16 or y.dim() != 4 or not y.is_cuda:
+        return False
+    n = y.shape[1]
+    w0, b0, w2, b2, w4, b4 = params
+    return (n in (128, 192) and b0 is not None and b2 is not None and b4 is not None
+            and tuple(w0.shape) == (n // 2, n, 1, 1) and tuple(w2.shape) == (n // 2, n // 2, 3, 3)
+            and tuple(w4.shape) == (n, n // 2, 1, 1)
+            and (specs[1].k, specs[1].s, specs[1].p) == (3, 1, 1))
+
+
+def _packed_kp(weight, g, dt, direction):
+    """The layer's packed MFMA operand for `direction` (the model's prepacked copy when its forward is active) and
+    its row length."""
+    packer = _prepack_active()
+    wp = packer.lookup(weight, dt, direction) if packer is not None else None
+    if wp is None:
+        wp = _pack_weight(g, dt, direction, weight)
+    kout = g.out_c if direction == 0 else g.in_c
+    return wp, wp.numel() // (2 * ((kout + 15) // 16 * 16))
+
+
+def _resunit_fwd(y, params, need_x):
+    dt = torch.bfloat16
+    xpm, xld = to_pm(y, dt, 8)
+    B, n, H, W = xpm.shape
+    nh = n // 2
+    w0, b0, w2, b2, w4, b4 = params
+    ga = conv_geom(_SPEC_1x1, B, n, H, W, nh)
+    gb = conv_geom(_SPEC_3x3, B, nh, H, W, nh)
+    gc = conv_geom(_SPEC_1x1, B, nh, H, W, n)
+    (wa, kpa), (wb, kpb), (wc, kpc) = (_packed_kp(w0, ga, dt, 0), _packed_kp(w2, gb, dt, 0),
+                                       _packed_kp(w4, gc, dt, 0))
+    h1 = empty_pm(B, nh, H, W, dt, xpm.device)
+    h2 = empty_pm(B, nh, H, W, dt, xpm.device)
+    out = empty_pm(B, n, H, W, dt, xpm.device)
+    bs = [b.detach().float().contiguous() for b in (b0, b2, b4)]
+    A = ResunitArgs(batch=B, h=H, w=W, n=n, x=xpm.data_ptr(), wa=wa.data_ptr(), wb=wb.data_ptr(), wc=wc.data_ptr(),
+                    ba=bs[0].data_ptr(), bb=bs[1].data_ptr(), bc=bs[2].data_ptr(), h1=h1.data_ptr(),
+                    h2=h2.data_ptr(), out=out.data_ptr(), x_ld=xld, out_ld=n, kpa=kpa, kpb=kpb, kpc=kpc)
+    fl = sum(_ledger.conv_cost(g, 2, 0)[0] for g in (ga, gb, gc))
+    _ledger.run(lambda: lib.cai_resunit(ctypes.byref(A), 0, _stream()), "conv_fwd", f"resunit_kernel<{n},fwd>", fl,
+                2 * B * H * W * (2 * n + 2 * nh), dt, f"ResidualUnit N={n} {H}x{W} B={B}")
+    u = _FusedUnit(params, (ga, gb, gc), need_x)
+    u.saved_tensors = (xpm, h1, h2, out)
+    return out, u
+
+
+def _resunit_bwd(u: "_FusedUnit", gy):
+    dt = torch.bfloat16
+    xpm, h1, h2, y = u.saved_tensors
+    ga, gb, gc = u.geoms
+    w0, b0, w2, b2, w4, b4 = u.params
+    B, n, H, W = xpm.shape
+    nh = n // 2
+    gpm, gld = to_pm(gy, dt, 8)
+    (wa, kpa), (wb, kpb), (wc, kpc) = (_packed_kp(w4, gc, dt, 1), _packed_kp(w2, gb, dt, 1),
+                                       _packed_kp(w0, ga, dt, 1))
+    dev = xpm.device
+    g_c = None if u.gy_masked else empty_pm(B, n, H, W, dt, dev)
+    g_b = empty_pm(B, nh, H, W, dt, dev)
+    g_a = empty_pm(B, nh, H, W, dt, dev)
+    dx = empty_pm(B, n, H, W, dt, dev)
+    res2 = None
+    if u.dx_res2 is not None:
+        res2, r2ld = to_pm(u.dx_res2, dt, 4)
+    yld = pixel_major_ld(y)
+    A = ResunitArgs(batch=B, h=H, w=W, n=n, x=gpm.data_ptr(), y=y.data_ptr(), wa=wa.data_ptr(), wb=wb.data_ptr(),
+                    wc=wc.data_ptr(), h1=h1.data_ptr(), h2=h2.data_ptr(), out=dx.data_ptr(),
+                    gc=g_c.data_ptr() if g_c is not None else None, gb=g_b.data_ptr(), ga=g_a.data_ptr(),
+                    res2=res2.data_ptr() if res2 is not None else None,
+                    xmask=xpm.data_ptr() if u.mask_x else None, x_ld=gld, y_ld=yld, out_ld=n,
+                    res2_ld=r2ld if res2 is not None else 0, xmask_ld=pixel_major_ld(xpm) if u.mask_x else 0,
+                    kpa=kpa, kpb=kpb, kpc=kpc, gy_masked=int(u.gy_masked))
+    fl = sum(_ledger.conv_cost(g, 2, 1)[0] for g in (ga, gb, gc))
+    _ledger.run(lambda: lib.cai_resunit(ctypes.byref(A), 1, _stream()), "conv_dgrad", f"resunit_kernel<{n},bwd>", fl,
+                2 * B * H * W * (3 * n + 4 * nh), dt, f"ResidualUnit N={n} {H}x{W} B={B}")
+    gcc, gcld = (gpm, gld) if g_c is None else (g_c, n)
+    dw4, db4 = conv_wgrad(gc, dt, h2, nh, 0, gcc, gcld, w4, b4, w4, True)
+    dw2, db2 = conv_wgrad(gb, dt, h1, nh, 0, g_b, nh, w2, b2, w2, True)
+    dw0, db0 = conv_wgrad(ga, dt, xpm, pixel_major_ld(xpm), 0, g_a, nh, w0, b0, w0, True)
+    return dx, (dw0, db0, dw2, db2, dw4, db4)
+
+
 def _chain_forward(x, specs, out_masked, params, x_need, p_need):
     subs = []
     y = x
     for k, (s0, s2, s4) in enumerate(specs):
-        w0, b0, w2, b2, w4, b4 = params[6 * k:6 * k + 6]
+        pr = params[6 * k:6 * k + 6]
+        if _resunit_ok(y, (s0, s2, s4), pr):
+            y, u = _resunit_fwd(y, pr, x_need or k > 0)
+            if k > 0:   # this unit's input is the previous unit's ReLU output: mask its gradient here
+                u.mask_x = True
+                prev = subs[-1]
+                if isinstance(prev, _FusedUnit):
+                    prev.gy_masked = True
+                else:
+                    prev[2].gy_masked = True
+            subs.append(u)
+            continue
+        w0, b0, w2, b2, w4, b4 = pr
         pn = p_need[6 * k:6 * k + 6]
         c0 = _SubCtx((x_need or k > 0, pn[0], pn[1], False, False))
         c2 = _SubCtx((True, pn[2], pn[3], False, False))
@@ -784,12 +909,30 @@ def _chain_forward(x, specs, out_masked, params, x_need, p_need):
         h = ConvFn.forward(c2, h, w2, b2, s2)
         y = ConvFn.forward(c4, h, w4, b4, s4, y)
         if k > 0:   # this unit's input is the previous unit's ReLU output: mask its gradient here
-            c0.dx_res_mask = MASK_POS
-            subs[-1][2].gy_masked = True
+            prev = subs[-1]
+            if isinstance(prev, _FusedUnit):
+                # a fused unit hands its gradient over unmasked only through dx; the mask goes here
+                c0.dx_res_mask = MASK_POS
+                prev.gy_masked = True
+            else:
+                c0.dx_res_mask = MASK_POS
+                prev[2].gy_masked = True
         subs.append((c0, c2, c4))
     if out_masked:   # the consumer (a MASK_POS dgrad, GateFn relu_a) hands back the masked gradient
-        subs[-1][2].gy_masked = True
+        last = subs[-1]
+        if isinstance(last, _FusedUnit):
+            last.gy_masked = True
+        else:
+            last[2].gy_masked = True
     return y, subs
+
+
+def _unit_ctxs(subs):
+    """Every stand-in context of a chain (a fused unit is one)."""
+    out = []
+    for u in subs:
+        out.extend([u] if isinstance(u, _FusedUnit) else list(u))
+    return out
 
 
 def _chain_backward(subs, gy, dx_res2=None):
@@ -798,7 +941,14 @@ def _chain_backward(subs, gy, dx_res2=None):
     grads = []
     g = gy
     for k in range(len(subs) - 1, -1, -1):
-        c0, c2, c4 = subs[k]
+        u = subs[k]
+        if isinstance(u, _FusedUnit):
+            if k == 0 and dx_res2 is not None:
+                u.dx_res2 = dx_res2
+            g, pg = _resunit_bwd(u, g)
+            grads.append(pg)
+            continue
+        c0, c2, c4 = u
         dh2, dw4, db4, _, g4 = ConvFn.backward(c4, g)
         dh1, dw2, db2, _, _ = ConvFn.backward(c2, dh2)
         c0.dx_res = g4
@@ -828,7 +978,7 @@ class AttentionBlockFn(torch.autograd.Function):
         cg = _SubCtx((True, True, True, False))
         y = GateFn.forward(cg, a, bb, x, True)
         ctx.c3, ctx.cg = c3, cg
-        _stash(ctx, [c for trio in ctx.sub_a + ctx.sub_b for c in trio] + [c3, cg])
+        _stash(ctx, _unit_ctxs(ctx.sub_a + ctx.sub_b) + [c3, cg])
         return y
 
     @staticmethod
