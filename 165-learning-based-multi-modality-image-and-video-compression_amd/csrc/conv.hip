@@ -1163,6 +1163,9 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvArgs a, int
 #ifndef CAI_HALO_PH_MIX
 #define CAI_HALO_PH_MIX 0
 #endif
+#ifndef CAI_HALO_PH_PAIRS
+#define CAI_HALO_PH_PAIRS 0
+#endif
 
 
 // HALF: the 256-thread form (4 waves, 8 x 16 tiles, two workgroups per CU): the two waves that share a SIMD
@@ -1187,13 +1190,31 @@ struct HaloPhCfg {
 #endif
     // NST % NSTB == 0: a step's stage is t % NSTB.  A 6-stage ring (CAI_HALO_PH_NSTB6=1) measured slower on
     // MI355X (C2 8180 vs 8430 patches/s; the big launch 91.6 vs 88 us): the latency is not in the ring
-    static constexpr int NSTB = (CAI_HALO_PH_NSTB6 && NST % 6 == 0) ? 6 : (NST % 3 == 0 ? 3 : 2);
+    // PAIRS (CAI_HALO_PH_PAIRS=1, A/B): one workgroup barrier per two steps.  At an even step t both stages freed
+    // since the last barrier (steps t - 1 and t) refill with steps t + NSTB - 1 and t + NSTB, and the barrier
+    // certifies steps t + 1 and t + 2 -- the operands of both steps until the next one; NSTB = 6 (4 for the
+    // 8-step 2x2 phase) leaves NSTB - 2 steps between a DMA and its barrier.
+    static constexpr bool PAIRS = CAI_HALO_PH_PAIRS && DPS == 1 && !HALF && NST % 2 == 0;
+    static constexpr int NSTB = PAIRS ? (NST % 6 == 0 ? 6 : 4)
+                                      : ((CAI_HALO_PH_NSTB6 && NST % 6 == 0) ? 6 : (NST % 3 == 0 ? 3 : 2));
     static constexpr int BSTAGE = DPS * NT * 16;
     // BN > 128: register-direct epilogue only (no LDS staging buffer), see conv_epilogue_rows_t
     static constexpr int EPI = BN > 128 ? 0 : BM * (BN + 4) * 4;
     static constexpr int BYTES = (PATCH + NSTB * BSTAGE > EPI) ? PATCH + NSTB * BSTAGE : EPI;
-    static_assert(NPI <= NST - NSTB, "the next chunk's footprint must retire before the chunk's last step");
+    static_assert(PAIRS ? (NPI <= NST + 2 - NSTB && NST % NSTB == 0) : NPI <= NST - NSTB,
+                  "the next chunk's footprint must retire before the chunk's last step");
 };
+
+// PAIRS: the loads issued after step t + 2's weight DMA that an even step t's wait leaves in flight -- the DMAs of
+// the even steps after t' = t + 2 - NSTB (two each), the footprint cells issued at steps [t', t - 1] (j < NPI)
+// and the four fence loads after cell NPI - 1
+__host__ __device__ constexpr int halo_younger_pairs(int t, int nstb, int npi) {
+    const int lo = t + 2 - nstb, lo0 = lo > 0 ? lo : 0;
+    const int hi = t - 1 < npi - 1 ? t - 1 : npi - 1;
+    const int cells = hi >= lo0 ? hi - lo0 + 1 : 0;
+    const int fences = (npi - 1 >= lo && npi - 1 <= t - 1) ? 4 : 0;
+    return nstb - 4 + cells + fences;
+}
 
 // GATHER = false: the s^2-phase form (tap (ty, tx) reads footprint cell (NA-1-ty, NC-1-tx) from an origin
 // NA-1 / NC-1 before dy0 / dx0).  GATHER = true: a stride-1 gather convolution (Conv2d k3 s1 forward): tap
@@ -1307,8 +1328,72 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // the step pipeline of conv_halo_kernel, NST steps per chunk
     u32x4 fa[TM], fb[TN];
+    if constexpr (H::PAIRS) {
+        auto issue_s = [&](int ci, int s) {   // step s of chunk ci, s may run into the next chunk
+            if (s < NST)
+                issue_b(ci, s);
+            else
+                issue_b(ci + 1, s - NST);
+        };
+        if (nc > 0) {
+#pragma unroll
+            for (int i = 0; i < NPI; ++i) load_cell(0, i);
+            // the virtual even steps -NSTB .. -2 of the steady state: step -1 is a zero-page DMA into the stage
+            // step NSTB - 1 fills later, then steps 0 .. NSTB - 2
+            glds16_asm(cai_zero_page, bring + (NSTB - 1) * H::BSTAGE + wid * 1024);
+#pragma unroll
+            for (int t = 0; t < NSTB - 1; ++t) issue_b(0, t);
+            store_patch();
+            wait_vmcnt<NSTB - 2>();
+            wait_lgkmcnt0();
+            __builtin_amdgcn_s_barrier();
+            read_frags(0, fa, fb);
+        }
+        for (int ci = 0; ci < nc; ++ci) {
+#pragma unroll
+            for (int t = 0; t < NST; ++t) {
+                if (t % 2 == 0) {
+                    wait_vmcnt_n(halo_younger_pairs(t, NSTB, NPI));
+                    wait_lgkmcnt0();
+                    __builtin_amdgcn_s_barrier();
+                }
+                if (t == NST - 1) {
+                    __builtin_amdgcn_s_barrier();    // every wave has read its last fragment of the old footprint
+                    store_patch();
+                    wait_lgkmcnt0();
+                    __builtin_amdgcn_s_barrier();
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                if (t % 2 == 0) {
+                    issue_s(ci, t + NSTB - 1);
+                    issue_s(ci, t + NSTB);
+                }
+                if (t < NPI) load_cell(ci + 1, t);
+                if (t == NPI - 1) fence_loads();
+                u32x4 na[TM], nb[TN];
+                read_frags(t + 1 == NST ? 0 : t + 1, na, nb);
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn)
+                        acc[tm][tn] = (CAI_HALO_PH_T || BN > 128) ? mma16<bf16>(fb[tn], fa[tm], acc[tm][tn])
+                                                    : mma16<bf16>(fa[tm], fb[tn], acc[tm][tn]);
+#pragma unroll
+                for (int i = 0; i < TM + TN; ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                }
+                __builtin_amdgcn_sched_group_barrier(0x008, TM * TN - (TM + TN), 0);
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm) fa[tm] = na[tm];
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) fb[tn] = nb[tn];
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    } else {
+    // the step pipeline of conv_halo_kernel, NST steps per chunk
     if (nc > 0) {
 #pragma unroll
         for (int i = 0; i < NPI; ++i) load_cell(0, i);
@@ -1360,6 +1445,7 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
             __builtin_amdgcn_sched_barrier(0);
         }
     }
+    }   // !PAIRS
     wait_vmcnt<0>();
     asm volatile("" ::"v"(fence_[0]), "v"(fence_[1]), "v"(fence_[2]), "v"(fence_[3]));
     __syncthreads();
