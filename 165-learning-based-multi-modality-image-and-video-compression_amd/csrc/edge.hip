@@ -55,7 +55,7 @@ struct EdgeArgs {
     int units;
     bf16* sbf;            // packed superpixels [B][Hs][Ws][16] bf16 (wgrad DMA path)
     float* cs_part;       // per-pack-block fp32 column sums of the image side [npack][16]
-    int npack, prow;      // pack blocks, superpixel rows per pack block
+    int npack, ipb;       // pack blocks, superpixels per pack block
 };
 
 // s2d A/B knobs, measured on MI355X (the C2 g_a[0] forward / g_s[6] input gradient, 16 x 128 x 128 x 128
@@ -617,53 +617,59 @@ __global__ __launch_bounds__(NT) void edge_wgrad_kernel(const EdgeArgs A) {
 }
 
 // Image side -> packed bf16 superpixels S[B][Hs][Ws][16] (the constant-1 channel set), and the fp32
-// column sums of the image side per pack block (the deconv's bias gradient), fixed thread/row order.
+// column sums of the image side per pack block (the deconv's bias gradient).  Block b owns the A.ipb
+// consecutive superpixels [b*ipb, (b+1)*ipb) of the flattened (n, a, b) order, one per thread and pass
+// (coalesced float2 reads of the two image rows, 32-byte contiguous writes); fixed order throughout.
 template <int C>
 __global__ __launch_bounds__(256) void edge_pack_s_kernel(const EdgeArgs A) {
     float cs[12];
 #pragma unroll
     for (int e = 0; e < 12; ++e) cs[e] = 0.f;
-    const int64_t rows = (int64_t)A.B * A.Hs;
-    const int64_t r0 = (int64_t)blockIdx.x * A.prow, r1 = min(rows, r0 + A.prow);
+    const int64_t items = (int64_t)A.B * A.Hs * A.Ws;
+    const int64_t i0 = (int64_t)blockIdx.x * A.ipb, i1 = min(items, i0 + A.ipb);
     const int64_t W2 = 2 * (int64_t)A.Ws;
-    for (int64_t row = r0; row < r1; ++row) {
+    for (int64_t it = i0 + threadIdx.x; it < i1; it += 256) {
+        const int64_t row = it / A.Ws;
+        const int sb = (int)(it - row * A.Ws);
         const int n = (int)(row / A.Hs), a = (int)(row - (int64_t)n * A.Hs);
-        for (int sb = threadIdx.x; sb < A.Ws; sb += 256) {
-            float v[16];
+        float v[16];
 #pragma unroll
-            for (int e = 0; e < 16; ++e) v[e] = 0.f;
-            v[ONES] = 1.f;
+        for (int e = 0; e < 16; ++e) v[e] = 0.f;
+        v[ONES] = 1.f;
 #pragma unroll
-            for (int ci = 0; ci < C; ++ci) {
-                const float* base = A.img + ((int64_t)(n * C + ci) * (2 * A.Hs) + 2 * a) * W2 + 2 * sb;
-                const float2 q0 = *reinterpret_cast<const float2*>(base);
-                const float2 q1 = *reinterpret_cast<const float2*>(base + W2);
-                v[0 * C + ci] = q0.x;
-                v[1 * C + ci] = q0.y;
-                v[2 * C + ci] = q1.x;
-                v[3 * C + ci] = q1.y;
-            }
-#pragma unroll
-            for (int e = 0; e < 4 * C; ++e) cs[e] += v[e];
-            bf16x8 lo, hi;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                lo[e] = (bf16)v[e];
-                hi[e] = (bf16)v[8 + e];
-            }
-            bf16* dst = A.sbf + (row * A.Ws + sb) * 16;
-            *reinterpret_cast<u32x4*>(dst) = __builtin_bit_cast(u32x4, lo);
-            *reinterpret_cast<u32x4*>(dst + 8) = __builtin_bit_cast(u32x4, hi);
+        for (int ci = 0; ci < C; ++ci) {
+            const float* base = A.img + ((int64_t)(n * C + ci) * (2 * A.Hs) + 2 * a) * W2 + 2 * sb;
+            const float2 q0 = *reinterpret_cast<const float2*>(base);
+            const float2 q1 = *reinterpret_cast<const float2*>(base + W2);
+            v[0 * C + ci] = q0.x;
+            v[1 * C + ci] = q0.y;
+            v[2 * C + ci] = q1.x;
+            v[3 * C + ci] = q1.y;
         }
-    }
-    __shared__ float red[256 * 12];
 #pragma unroll
-    for (int e = 0; e < 12; ++e) red[threadIdx.x * 12 + e] = cs[e];
+        for (int e = 0; e < 4 * C; ++e) cs[e] += v[e];
+        bf16x8 lo, hi;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            lo[e] = (bf16)v[e];
+            hi[e] = (bf16)v[8 + e];
+        }
+        bf16* dst = A.sbf + it * 16;
+        *reinterpret_cast<u32x4*>(dst) = __builtin_bit_cast(u32x4, lo);
+        *reinterpret_cast<u32x4*>(dst + 8) = __builtin_bit_cast(u32x4, hi);
+    }
+    // wave sums by DPP, then the four waves' partials in order
+    __shared__ float red[4][12];
+    const int wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int e = 0; e < 4 * C; ++e) {
+        const float t = wave_sum_dpp(cs[e]);
+        if ((threadIdx.x & 63) == 0) red[wave][e] = t;
+    }
     __syncthreads();
     if (threadIdx.x < 16) {
         float s = 0.f;
-        if (threadIdx.x < 4 * C)
-            for (int i = 0; i < 256; ++i) s += red[i * 12 + threadIdx.x];
+        if (threadIdx.x < 4 * C) s = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
         A.cs_part[blockIdx.x * 16 + threadIdx.x] = s;
     }
 }
@@ -681,6 +687,10 @@ constexpr int WSR = 132 * 32;             // one packed superpixel row (130 used
 constexpr int WSB = 16 * 1024;            // S region: 3 rows, padded to 16 DMA instructions
 constexpr int WSTAGE = WPB + WSB;
 constexpr int WG = 12;                    // DMA instructions per wave and step
+
+// slot of superpixel j in a packed superpixel row: odd groups of 8 rotated by 4 slots, so the half-wave's
+// ds_read_b64_tr_b16 rows j and j+8 land on disjoint banks (linear slots: 2-way conflicts on every S read)
+__device__ __forceinline__ int sswz(int j) { return j ^ ((j >> 1) & 4); }
 
 __global__ __launch_bounds__(NT, 1) void edge_wgrad_dma_kernel(const EdgeArgs A) {
     __shared__ __attribute__((aligned(16))) char smem[3 * WSTAGE];
@@ -716,8 +726,9 @@ __global__ __launch_bounds__(NT, 1) void edge_wgrad_dma_kernel(const EdgeArgs A)
             const void* src = (const void*)edge_zero_page;
             if (off < 3 * WSR) {
                 const int sr = off / WSR, rem = off - sr * WSR;
-                const int sa = a - 1 + sr, sb = b0 - 1 + rem / 32;
-                if (sa >= 0 && sa < A.Hs && sb >= 0 && sb < A.Ws && rem / 32 < WTB + 2)
+                const int j = sswz(rem / 32);    // the superpixel whose slot this is (sswz is an involution)
+                const int sa = a - 1 + sr, sb = b0 - 1 + j;
+                if (sa >= 0 && sa < A.Hs && sb >= 0 && sb < A.Ws && j < WTB + 2)
                     src = (const void*)(Sg + ((((int64_t)n * A.Hs + sa) * A.Ws + sb) * 16) * 2 + (rem & 31));
             }
             glds16(src, base + WPB + k * 1024);
@@ -727,6 +738,12 @@ __global__ __launch_bounds__(NT, 1) void edge_wgrad_dma_kernel(const EdgeArgs A)
     f32x4 acc[9][2];
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // superpixel-row read offsets for column shift dx and the +4 half (independent of ks: 32*ks leaves bits 0-3)
+    int soff[3][2];
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) soff[dx][h] = sswz(8 * g_ + q_ + dx + 4 * h) * 32 + 8 * p4;
     if (nsteps > 0) issue(0, 0);
     if (nsteps > 1) issue(1, 1);
     for (int st = 0; st < nsteps; ++st) {
@@ -752,8 +769,8 @@ __global__ __launch_bounds__(NT, 1) void edge_wgrad_dma_kernel(const EdgeArgs A)
             }
 #pragma unroll
             for (int t = 0; t < 9; ++t) {
-                const char* sbase = Sst + (t / 3) * WSR + (t % 3) * 32;
-                const u32x4 av = tr_frag(sbase, rr * 32 + 8 * p4, (rr + 4) * 32 + 8 * p4);
+                const char* sbase = Sst + (t / 3) * WSR + ks * 1024;
+                const u32x4 av = tr_frag(sbase, soff[t % 3][0], soff[t % 3][1]);
                 acc[t][0] = mma16<bf16>(av, bv[0], acc[t][0]);
                 acc[t][1] = mma16<bf16>(av, bv[1], acc[t][1]);
             }
@@ -811,15 +828,17 @@ int wgrad_units(const EdgeArgs& A, int* rch) {
 // workspace of the wgrad: [unit partials][packed superpixels (N = 128)][pack column sums]
 struct WgradWs {
     size_t off_sbf, off_cs, total;
-    int npack, prow;
+    int npack, ipb;
 };
 WgradWs wgrad_ws(const EdgeArgs& A) {
     WgradWs W{};
     int rch;
     const int units = wgrad_units(A, &rch);
     const int64_t rows = (int64_t)A.B * A.Hs;
-    W.prow = (int)std::max<int64_t>(1, (rows + 255) / 256);
-    W.npack = (int)((rows + W.prow - 1) / W.prow);
+    // about 1024 pack blocks of 256 threads, one superpixel per thread and pass
+    const int64_t items = rows * A.Ws;
+    W.ipb = (int)(256 * std::max<int64_t>(1, (items + 256 * 1024 - 1) / (256 * 1024)));
+    W.npack = (int)((items + W.ipb - 1) / W.ipb);
     auto up = [](size_t v) { return (v + 255) / 256 * 256; };
     W.off_sbf = up((size_t)units * (9 * 16 * A.N + 16) * sizeof(float));
     W.off_cs = W.off_sbf + (A.N == 128 ? up((size_t)rows * A.Ws * 32) : 0);
@@ -895,7 +914,7 @@ void launch_wgrad(EdgeArgs A, char* ws, float* dw, float* db, int accumulate, hi
         A.sbf = reinterpret_cast<bf16*>(ws + W.off_sbf);
         A.cs_part = reinterpret_cast<float*>(ws + W.off_cs);
         A.npack = W.npack;
-        A.prow = W.prow;
+        A.ipb = W.ipb;
         edge_pack_s_kernel<C><<<W.npack, 256, 0, st>>>(A);
         edge_wgrad_dma_kernel<<<A.units, NT, 0, st>>>(A);
         J->p[1] = A.cs_part; J->i[6] = W.npack; J->i[7] = 16;
