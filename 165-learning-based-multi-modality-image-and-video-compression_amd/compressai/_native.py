@@ -79,6 +79,13 @@ class ResunitArgs(Structure):
                 ("gy_masked", c_int32)]
 
 
+class ResunitWgradArgs(Structure):
+    _fields_ = [("batch", c_int32), ("h", c_int32), ("w", c_int32), ("n", c_int32),
+                ("x", c_void_p), ("h1", c_void_p), ("h2", c_void_p), ("ga", c_void_p), ("gb", c_void_p),
+                ("gc", c_void_p), ("x_ld", c_int32), ("gc_ld", c_int32), ("dwa", c_void_p), ("dba", c_void_p),
+                ("dwb", c_void_p), ("dbb", c_void_p), ("dwc", c_void_p), ("dbc", c_void_p), ("accumulate", c_int32)]
+
+
 # name -> (restype, argtypes)
 _P, _I, _I64, _F, _S = c_void_p, c_int, c_int64, c_float, c_size_t
 _G = POINTER(ConvGeom)
@@ -106,6 +113,8 @@ SIGNATURES = {
                                  c_int32, _P, _S, _P]),
     "cai_conv_wgrad_workspace_bytes": (_S, [_G, _I]),
     "cai_resunit": (_I, [POINTER(ResunitArgs), c_int32, _P]),
+    "cai_resunit_wgrad_workspace_bytes": (_S, [POINTER(ResunitWgradArgs)]),
+    "cai_resunit_wgrad": (_I, [POINTER(ResunitWgradArgs), _P, _S, _P, POINTER(ReduceJob)]),
     "cai_conv_kernel_name": (c_char_p, [_G, _I, _I, c_int32]),
     "cai_conv_split_factor": (c_int32, [_G, _I, _I, c_int32]),
     "cai_conv_wgrad": (_I, [_G, _I, _P, c_int32, c_int32, c_int32, _P, c_int32, _P, _P, c_int32, _P, _S, _P]),

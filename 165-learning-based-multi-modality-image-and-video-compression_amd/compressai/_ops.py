@@ -29,7 +29,7 @@ import torch
 from . import _ledger
 from ._native import (ACT_LEAKY, ACT_NONE, ACT_RELU, BF16, F32, MASK_LEAKY, MASK_NONE, MASK_POS, Q_DEQUANTIZE, Q_NOISE,
                       JOB_NONE, NOISE_BUF, NOISE_DRAW, NOISE_REPLAY, ConvGeom, EbGrads, EbParams, NoiseSrc, RdGrads,
-                      RdInputs, ReduceJob, ResunitArgs, lib)
+                      RdInputs, ReduceJob, ResunitArgs, ResunitWgradArgs, lib)
 
 _VP = ctypes.c_void_p
 _GDN_TWO_PASS = os.environ.get("CAI_GDN_TWO_PASS", "0") == "1"   # A/B knobs (tools/ab_env.sh)
@@ -785,6 +785,7 @@ class _unstash:
 # One launch per ResidualUnit and direction (csrc/resunit.hip) instead of three conv launches: bf16, N in {128, 192}.
 # CAI_RESUNIT_FUSED=0 keeps the per-conv chain (A/B).
 _RESUNIT_FUSED = os.environ.get("CAI_RESUNIT_FUSED", "1") == "1"
+_RESUNIT_WGRAD = os.environ.get("CAI_RESUNIT_WGRAD", "1") == "1"   # one launch for the unit's weight gradients
 _SPEC_1x1, _SPEC_3x3 = ConvSpec(1, 1, 0), ConvSpec(3, 1, 1)
 
 
@@ -878,10 +879,51 @@ def _resunit_bwd(u: "_FusedUnit", gy):
     _ledger.run(lambda: lib.cai_resunit(ctypes.byref(A), 1, _stream()), "conv_dgrad", f"resunit_kernel<{n},bwd>", fl,
                 2 * B * H * W * (3 * n + 4 * nh), dt, f"ResidualUnit N={n} {H}x{W} B={B}")
     gcc, gcld = (gpm, gld) if g_c is None else (g_c, n)
+    if _RESUNIT_WGRAD:
+        grads = _resunit_wgrad(u, xpm, h1, h2, g_a, g_b, gcc, gcld)
+        return dx, grads
     dw4, db4 = conv_wgrad(gc, dt, h2, nh, 0, gcc, gcld, w4, b4, w4, True)
     dw2, db2 = conv_wgrad(gb, dt, h1, nh, 0, g_b, nh, w2, b2, w2, True)
     dw0, db0 = conv_wgrad(ga, dt, xpm, pixel_major_ld(xpm), 0, g_a, nh, w0, b0, w0, True)
     return dx, (dw0, db0, dw2, db2, dw4, db4)
+
+
+def _resunit_wgrad(u: "_FusedUnit", xpm, h1, h2, g_a, g_b, gcc, gcld):
+    """The unit's six parameter gradients in one launch (cai_resunit_wgrad, csrc/resunit.hip) + three WGRAD
+    reduce jobs: deferred to the end of the backward when every parameter writes straight into the optimizer's
+    flat buffer (as conv_wgrad), else run now into fresh tensors."""
+    w0, b0, w2, b2, w4, b4 = u.params
+    B, n, H, W = xpm.shape
+    dev = xpm.device
+    direct = all(direct_grad(p) for p in u.params)
+    if direct:
+        outs = [p.grad for p in u.params]
+    else:
+        outs = [torch.empty(p.shape, dtype=torch.float32, device=dev) for p in u.params]
+    dw0, db0, dw2, db2, dw4, db4 = outs
+    A = ResunitWgradArgs(batch=B, h=H, w=W, n=n, x=xpm.data_ptr(), h1=h1.data_ptr(), h2=h2.data_ptr(),
+                         ga=g_a.data_ptr(), gb=g_b.data_ptr(), gc=gcc.data_ptr(), x_ld=pixel_major_ld(xpm),
+                         gc_ld=gcld, dwa=dw0.data_ptr(), dba=db0.data_ptr(), dwb=dw2.data_ptr(), dbb=db2.data_ptr(),
+                         dwc=dw4.data_ptr(), dbc=db4.data_ptr(), accumulate=int(direct))
+    nbytes = lib.cai_resunit_wgrad_workspace_bytes(ctypes.byref(A))
+    wws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    st = _stream()
+    if defer_reduce_ok(direct):
+        jobs = (ReduceJob * 3)()
+        lib.cai_resunit_wgrad(ctypes.byref(A), _p(wws), nbytes, st, jobs)
+        for j in jobs:
+            defer_job(j, dev, wws)
+    else:
+        nh = n // 2
+        P = B * H * W
+        fl = 2.0 * P * (nh * n * 2 + 9 * nh * nh)
+        nb = 2 * P * (3 * n + 4 * nh)
+        _ledger.run(lambda: lib.cai_resunit_wgrad(ctypes.byref(A), _p(wws), nbytes, st, None), "conv_wgrad",
+                    f"resunit_wgrad_kernel<{n}> (+reduce)", fl, nb, torch.bfloat16,
+                    f"ResidualUnit N={n} {H}x{W} B={B}")
+    if direct:
+        return (None,) * 6
+    return tuple(o if p.dtype == torch.float32 else o.to(p.dtype) for o, p in zip(outs, u.params))
 
 
 def _chain_forward(x, specs, out_masked, params, x_need, p_need):

@@ -3274,6 +3274,14 @@ static bool small_off() {
 // latency-bound and the small tiles re-read the weights too often (g_a[6] 48.9 vs 22.6 us): split-K stays.
 // Also taken where the big-tile grid has fewer than 64 blocks and K is too short to split (cheng2020's attention
 // units at 16x16, B = 4: 1x1 96 <-> 192 on 4 blocks of 256 x 128 ran 16-25 us).
+// A/B knob CAI_SMALL_CONV_KMAX (default 2048): the K bound of the second rule
+static int small_kmax() {
+    static const int v = [] {
+        const char* e = getenv("CAI_SMALL_CONV_KMAX");
+        return (e && *e) ? atoi(e) : 2048;
+    }();
+    return v;
+}
 static int pick_small(const Plan& P, int dtype, int mmax, int big_ksplit, int big_blocks) {
     if (small_off() || dtype != CAI_BF16 || P.Cin_pad % 32 != 0 || (big_ksplit <= 1 && big_blocks >= 64) ||
         mmax > 8192)
@@ -3283,7 +3291,7 @@ static int pick_small(const Plan& P, int dtype, int mmax, int big_ksplit, int bi
     const int cfg = mmax <= 512 ? SMALL_16x32 : (mmax <= 2048 ? SMALL_32x32 : SMALL_32x64);
     static const int bm[] = {0, 16, 32, 32}, bn[] = {0, 32, 32, 64};
     const int blocks = (mmax + bm[cfg] - 1) / bm[cfg] * ((P.kout_c + bn[cfg] - 1) / bn[cfg]) * P.nphase;
-    if (mmax <= 512 || (kmax <= 2048 && (blocks <= 256 || mmax <= 1024))) return cfg;
+    if (mmax <= 512 || (kmax <= small_kmax() && (blocks <= 256 || mmax <= 1024))) return cfg;
     return SMALL_NONE;
 }
 

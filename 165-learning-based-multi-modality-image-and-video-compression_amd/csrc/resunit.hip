@@ -27,8 +27,10 @@
 // -- the unfused chain's, with the MFMA K order of this kernel.
 #include "common.hpp"
 #include "mfma.hpp"
+#include "reduce_jobs.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace cai {
 namespace {
@@ -299,6 +301,240 @@ __global__ __launch_bounds__(512, 1) void resunit_kernel(const RuArgs a) {
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// The unit's three weight (+ bias) gradients in ONE launch (cai_resunit_wgrad), from the tensors the backward
+// kernel leaves behind:
+//     dWa[o][c]         = sum_p ga[p][o] x[p][c]                 (N/2 x N,  bias: sum_p ga)
+//     dWb[o][c][ty][tx] = sum_p gb[p][o] h1[p + (ty-1, tx-1)][c]  (N/2 x N/2 x 9, zero outside the image)
+//     dWc[o][c]         = sum_p gc[p][o] h2[p][c]                 (N x N/2,  bias: sum_p gc)
+// Unfused these are three latency-bound weight-gradient launches per unit (C4's 16 x 16 / 64 x 64 units: 16-25
+// us each for 38 MFLOP - 2.7 GFLOP).  Here the pixels are split S ways and every split has 13 blocks of one
+// (N/2 x N/2) output tile each: the 9 taps of dWb, the two column halves of dWa, the two row halves of dWc.
+// The 13 blocks of a split are consecutive in their XCD's dispatch order (xcd remap), so the split's operand
+// chunks are read from HBM about once and shared through that XCD's L2.  A block walks its split in 64-pixel
+// steps: G and X tiles [64 px][N/2] bf16 by 16-byte buffer loads (pixels past the split or shifted outside the
+// image read 0) into a double-buffered LDS stage (XOR-swizzled slots: conflict-free writes and
+// ds_read_b64_tr_b16 reads, one barrier per step), the next step's loads in flight during the MFMAs.  Wave w
+// takes the 32-pixel half w >> 1 of each step and the column half w & 1 of the tile (all N/2 rows); the two
+// halves are summed in LDS and written as fp32 slabs [S][rows][taps x channels] -- the conv weight-gradient
+// slab format -- so the final sums are ordinary WGRAD reduce jobs (deferred to the end of the backward with the
+// others).  Bias gradients: the column sums of the G tiles, accumulated from the loaded registers by the
+// blocks of tiles 0 (gb), 9 (ga), 11 and 12 (gc), summed in pixel order.  Deterministic throughout.
+// ---------------------------------------------------------------------------
+struct RwArgs {
+    const bf16 *x, *h1, *h2, *ga, *gb, *gc;
+    int x_ld, gc_ld;                 // h1 / h2 / ga / gb: ld N/2
+    int B, H, W, P;                  // P = B * H * W pixels
+    int S, chunk;                    // pixel splits, pixels per split (a multiple of 64)
+    float inv_plane, inv_w;          // 1 / (H * W), 1 / W
+    float *slab_a, *slab_b, *slab_c; // [S][N/2][N], [S][N/2][9 * N/2], [S][N][N/2]
+    float *bias_a, *bias_b, *bias_c; // [S][N/2], [S][N/2], [S][N]
+};
+
+template <int NH>
+struct RwCfg {
+    static constexpr int SLOTS = NH / 8;               // 16-byte slots per pixel row
+    static constexpr int RB = NH * 2;                  // LDS row bytes
+    static constexpr int STEP = 64;                    // pixels per step
+    static constexpr int TILEB = STEP * RB;            // one operand tile
+    static constexpr int LPT = STEP * SLOTS / 256;     // 16-byte loads per thread and operand (3 / 2)
+    static constexpr int TM = NH / 16, TN = NH / 32;   // wave tile: all NH rows x NH / 2 columns
+    static constexpr int EP = NH + 4;                  // epilogue partial row pitch (floats)
+    static constexpr int EPI = NH * EP * 4;
+    static constexpr int RED = 256 * LPT * 8 * 4;      // per-thread bias partials
+    static constexpr int BYTES = (4 * TILEB > EPI + RED) ? 4 * TILEB : EPI + RED;
+    static_assert(STEP * SLOTS % 256 == 0, "whole loads per thread");
+    static_assert(BYTES <= 64 * 1024, "two blocks per CU");
+};
+
+// slot swizzle of a [64][NH] bf16 tile read by ds_read_b64_tr_b16 (rows 8g + q of a half-wave, g in {0, 1})
+template <int NH>
+__device__ __forceinline__ int rw_swz(int row, int slot) {
+    if constexpr (NH == 96)
+        return row * 192 + ((slot ^ (((row >> 3) & 1) << 1)) << 4);
+    else
+        return row * 128 + ((slot ^ ((((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2))) << 4);
+}
+
+__device__ __forceinline__ s16x4 rw_tr16(const char* base, int byte_off) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + byte_off));
+}
+
+// n / d for 0 <= n < 2^23 from a float reciprocal and one correction each way
+__device__ __forceinline__ int rw_div(int n, int d, float inv) {
+    int q = (int)((float)n * inv);
+    const int r = n - q * d;
+    q += (r >= d ? 1 : 0) - (r < 0 ? 1 : 0);
+    return q;
+}
+
+// bijective XCD remap: logical ids [x*q, (x+1)*q) run on XCD x (dispatch is round-robin over 8 XCDs)
+__device__ __forceinline__ int rw_xcd_remap(int wgid, int nwg) {
+    const int xcd = wgid & 7, idx = wgid >> 3;
+    const int q = nwg >> 3, r = nwg & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+template <int NH>
+__global__ __launch_bounds__(256, 2) void resunit_wgrad_kernel(const RwArgs a) {
+    using R = RwCfg<NH>;
+    constexpr int NC = 2 * NH, SLOTS = R::SLOTS, LPT = R::LPT, TM = R::TM, TN = R::TN, EP = R::EP;
+    constexpr unsigned OOB = 0x80000000u;
+    __shared__ __attribute__((aligned(16))) char smem[R::BYTES];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int L = rw_xcd_remap((int)blockIdx.x, (int)gridDim.x);
+    const int s = L / 13, t = L - (L / 13) * 13;
+
+    // this block's GEMM: G (output rows) and X (columns) operands, tap shift, slab placement, bias role
+    const bf16* G;
+    const bf16* X;
+    int g_ld = NH, x_ld = NH, dy = 0, dx = 0;
+    float* slab;
+    float* bias = nullptr;
+    int ng, ncols, row0 = 0, col0 = 0;
+    if (t < 9) {
+        G = a.gb; X = a.h1; dy = t / 3 - 1; dx = t % 3 - 1;
+        slab = a.slab_b; ng = NH; ncols = 9 * NH; col0 = t * NH;
+        if (t == 0) bias = a.bias_b + (int64_t)s * NH;
+    } else if (t < 11) {
+        G = a.ga; X = a.x + (t - 9) * NH; x_ld = a.x_ld;
+        slab = a.slab_a; ng = NH; ncols = NC; col0 = (t - 9) * NH;
+        if (t == 9) bias = a.bias_a + (int64_t)s * NH;
+    } else {
+        row0 = (t - 11) * NH;
+        G = a.gc + row0; g_ld = a.gc_ld; X = a.h2;
+        slab = a.slab_c; ng = NC; ncols = NH;
+        bias = a.bias_c + (int64_t)s * NC + row0;
+    }
+    const __amdgpu_buffer_rsrc_t gr =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(G), (short)0, (int)((int64_t)a.P * g_ld * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(X), (short)0, (int)((int64_t)a.P * x_ld * 2), 0x00020000);
+    const int p0 = s * a.chunk, p1 = min(a.P, p0 + a.chunk);
+    const int nsteps = (p1 - p0 + R::STEP - 1) / R::STEP;
+    const int plane = a.H * a.W;
+    const float gsf = bias ? 1.f : 0.f;
+
+    // per-thread load slots (fixed across steps): chunk e = u * 256 + tid -> pixel row e / SLOTS, slot e % SLOTS
+    int lrow[LPT], lslot[LPT];
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+        const int e = u * 256 + tid;
+        lrow[u] = e / SLOTS;
+        lslot[u] = e - (e / SLOTS) * SLOTS;
+    }
+    u32x4 rg[LPT], rx[LPT];
+    auto load = [&](int st) {
+#pragma unroll
+        for (int u = 0; u < LPT; ++u) {
+            const int m = p0 + st * R::STEP + lrow[u];
+            const bool okm = (st < nsteps) & (m < p1);
+            rg[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  gr, okm ? (unsigned)(m * g_ld + lslot[u] * 8) * 2u : OOB, 0, 0));
+            const int b = rw_div(m, plane, a.inv_plane);
+            const int r = m - b * plane;
+            const int i = rw_div(r, a.W, a.inv_w);
+            const int j = r - i * a.W;
+            const bool okx = okm & ((unsigned)(i + dy) < (unsigned)a.H) & ((unsigned)(j + dx) < (unsigned)a.W);
+            const int xm = m + dy * a.W + dx;
+            rx[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  xr, okx ? (unsigned)(xm * x_ld + lslot[u] * 8) * 2u : OOB, 0, 0));
+        }
+    };
+    float bsum[LPT][8];
+#pragma unroll
+    for (int u = 0; u < LPT; ++u)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bsum[u][e] = 0.f;
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int kh = wave >> 1, wn = wave & 1;
+    const int g_ = lane >> 4, q_ = (lane >> 2) & 3, p4 = lane & 3;
+    const int r0 = 32 * kh + 8 * g_ + q_;
+    load(0);
+    for (int st = 0; st < nsteps; ++st) {
+        char* const Gs = smem + (st & 1) * 2 * R::TILEB;
+        char* const Xs = Gs + R::TILEB;
+#pragma unroll
+        for (int u = 0; u < LPT; ++u) {
+            *reinterpret_cast<u32x4*>(Gs + rw_swz<NH>(lrow[u], lslot[u])) = rg[u];
+            *reinterpret_cast<u32x4*>(Xs + rw_swz<NH>(lrow[u], lslot[u])) = rx[u];
+            const bf16x8 h = __builtin_bit_cast(bf16x8, rg[u]);   // branch-free: scaled by 0 off the bias blocks
+#pragma unroll
+            for (int e = 0; e < 8; ++e) bsum[u][e] += gsf * (float)h[e];
+        }
+        __syncthreads();
+        load(st + 1);    // past the last step: every load reads 0 (no memory touched)
+        u32x4 fb[TN];
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int c = wn * (NH / 2) + tn * 16 + 4 * p4;
+            const s16x4 b0 = rw_tr16(Xs, rw_swz<NH>(r0, c >> 3) + ((c & 7) << 1));
+            const s16x4 b1 = rw_tr16(Xs, rw_swz<NH>(r0 + 4, c >> 3) + ((c & 7) << 1));
+            const s16x8 bv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+            fb[tn] = __builtin_bit_cast(u32x4, bv);
+        }
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+            const int c = tm * 16 + 4 * p4;
+            const s16x4 a0 = rw_tr16(Gs, rw_swz<NH>(r0, c >> 3) + ((c & 7) << 1));
+            const s16x4 a1 = rw_tr16(Gs, rw_swz<NH>(r0 + 4, c >> 3) + ((c & 7) << 1));
+            const s16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+            const u32x4 fa = __builtin_bit_cast(u32x4, av);
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = mma16<bf16>(fa, fb[tn], acc[tm][tn]);
+        }
+    }
+    // the two pixel halves summed through LDS, then the slab rows; bias partials in pixel order
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);
+    float* bred = reinterpret_cast<float*>(smem + R::EPI);
+    if (kh == 1) {
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    red[(tm * 16 + 4 * g_ + r) * EP + wn * (NH / 2) + tn * 16 + (lane & 15)] = acc[tm][tn][r];
+    }
+    if (bias) {
+#pragma unroll
+        for (int u = 0; u < LPT; ++u)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) bred[(tid * LPT + u) * 8 + e] = bsum[u][e];
+    }
+    __syncthreads();
+    if (kh == 0) {
+        float* out = slab + ((int64_t)s * ng + row0) * ncols + col0;
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = tm * 16 + 4 * g_ + r, col = wn * (NH / 2) + tn * 16 + (lane & 15);
+                    out[(int64_t)row * ncols + col] = acc[tm][tn][r] + red[row * EP + col];
+                }
+    }
+    if (bias && tid < NH) {
+        const int sl = tid >> 3, el = tid & 7;
+        float v = 0.f;
+        for (int px = 0; px < R::STEP; ++px) {
+            const int e = px * SLOTS + sl;
+            const int u = e >> 8, th = e & 255;
+            v += bred[(th * LPT + u) * 8 + el];
+        }
+        bias[tid] = v;
+    }
+}
+
 }  // namespace
 }  // namespace cai
 
@@ -358,4 +594,106 @@ extern "C" int cai_resunit(const cai_resunit_args* p, int32_t direction, void* s
         hipLaunchKernelGGL((resunit_kernel<128, false>), grid, dim3(512), 0, st, a);
     CAI_LAUNCH_CHECK("resunit");
     return CAI_OK;
+}
+
+namespace {
+
+// pixel splits of cai_resunit_wgrad: about 400 blocks (13 per split) from 8192 pixels, 4-16 steps per block
+// below; A/B knob CAI_RW_SPLITS (fixed count)
+int rw_splits(int64_t P) {
+    static const int knob = [] {
+        const char* e = std::getenv("CAI_RW_SPLITS");
+        return (e && *e) ? std::max(0, std::atoi(e)) : 0;
+    }();
+    int S = knob > 0 ? knob : (int)std::min<int64_t>(32, std::max<int64_t>(1, P / 256));
+    const int64_t chunk = ((P + S - 1) / S + 63) / 64 * 64;
+    return (int)((P + chunk - 1) / chunk);
+}
+
+struct RwWs {
+    int S, chunk;
+    size_t off_a, off_b, off_c, off_ba, off_bb, off_bc, total;
+};
+bool rw_ws(const cai_resunit_wgrad_args* p, RwWs& w) {
+    if (!p || (p->n != 128 && p->n != 192) || p->batch <= 0 || p->h <= 0 || p->w <= 0) return false;
+    const int64_t P = (int64_t)p->batch * p->h * p->w;
+    const int64_t nh = p->n / 2, n = p->n;
+    w.S = rw_splits(P);
+    w.chunk = (int)(((P + w.S - 1) / w.S + 63) / 64 * 64);
+    auto up = [](size_t v) { return (v + 255) / 256 * 256; };
+    size_t o = 0;
+    w.off_a = o; o += up((size_t)w.S * nh * n * 4);
+    w.off_b = o; o += up((size_t)w.S * nh * 9 * nh * 4);
+    w.off_c = o; o += up((size_t)w.S * n * nh * 4);
+    w.off_ba = o; o += up((size_t)w.S * nh * 4);
+    w.off_bb = o; o += up((size_t)w.S * nh * 4);
+    w.off_bc = o; o += up((size_t)w.S * n * 4);
+    w.total = o;
+    return true;
+}
+
+}  // namespace
+
+extern "C" size_t cai_resunit_wgrad_workspace_bytes(const cai_resunit_wgrad_args* p) {
+    RwWs w;
+    return rw_ws(p, w) ? w.total : 0;
+}
+
+extern "C" int cai_resunit_wgrad(const cai_resunit_wgrad_args* p, void* workspace, size_t ws_bytes, void* stream,
+                                 cai_reduce_job* jobs) {
+    RwWs w;
+    CAI_CHECK_ARG(rw_ws(p, w), "resunit_wgrad: N = %d (128 or 192) and positive sizes", p ? p->n : -1);
+    const int n = p->n, nh = n / 2;
+    CAI_CHECK_ARG(p->x && p->h1 && p->h2 && p->ga && p->gb && p->gc, "resunit_wgrad: null operand");
+    CAI_CHECK_ARG(p->dwa && p->dwb && p->dwc && p->dba && p->dbb && p->dbc, "resunit_wgrad: null gradient");
+    CAI_CHECK_ARG(p->x_ld >= n && p->x_ld % 8 == 0 && p->gc_ld >= n && p->gc_ld % 8 == 0,
+                  "resunit_wgrad: x_ld / gc_ld must be >= N and multiples of 8");
+    for (const void* q : {p->x, p->h1, p->h2, p->ga, p->gb, p->gc})
+        CAI_CHECK_ARG(((uintptr_t)q & 15) == 0, "resunit_wgrad: operands must be 16-byte aligned");
+    CAI_CHECK_ARG(workspace && ws_bytes >= w.total, "resunit_wgrad: workspace %zu < %zu", ws_bytes, w.total);
+    const int64_t P = (int64_t)p->batch * p->h * p->w;
+    CAI_CHECK_ARG(P * std::max(p->x_ld, p->gc_ld) * 2 < (1ll << 31) && P < (1 << 23), "resunit_wgrad: tensor too large");
+    char* ws = static_cast<char*>(workspace);
+    RwArgs a{};
+    a.x = static_cast<const bf16*>(p->x);
+    a.h1 = static_cast<const bf16*>(p->h1);
+    a.h2 = static_cast<const bf16*>(p->h2);
+    a.ga = static_cast<const bf16*>(p->ga);
+    a.gb = static_cast<const bf16*>(p->gb);
+    a.gc = static_cast<const bf16*>(p->gc);
+    a.x_ld = p->x_ld; a.gc_ld = p->gc_ld;
+    a.B = p->batch; a.H = p->h; a.W = p->w; a.P = (int)P;
+    a.S = w.S; a.chunk = w.chunk;
+    a.inv_plane = 1.f / (float)(p->h * p->w);
+    a.inv_w = 1.f / (float)p->w;
+    a.slab_a = reinterpret_cast<float*>(ws + w.off_a);
+    a.slab_b = reinterpret_cast<float*>(ws + w.off_b);
+    a.slab_c = reinterpret_cast<float*>(ws + w.off_c);
+    a.bias_a = reinterpret_cast<float*>(ws + w.off_ba);
+    a.bias_b = reinterpret_cast<float*>(ws + w.off_bb);
+    a.bias_c = reinterpret_cast<float*>(ws + w.off_bc);
+    hipStream_t st = as_stream(stream);
+    const dim3 grid((unsigned)(13 * w.S));
+    if (n == 192)
+        hipLaunchKernelGGL(resunit_wgrad_kernel<96>, grid, dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL(resunit_wgrad_kernel<64>, grid, dim3(256), 0, st, a);
+    CAI_LAUNCH_CHECK("resunit_wgrad");
+    // the final sums: three WGRAD reduce jobs over the slabs (reduce_jobs.hip), returned or run now
+    cai_reduce_job J[3]{};
+    auto fill = [&](cai_reduce_job& j, float* slab, float* dw, float* bws, float* db, int ng, int cq, int k) {
+        j.kind = CAI_JOB_WGRAD;
+        j.nblocks = wgrad_job_blocks(ng, cq, k, (ng + 255) / 256);
+        j.p[0] = slab; j.p[1] = dw; j.p[2] = bws; j.p[3] = db;
+        j.i[0] = w.S; j.i[1] = ng; j.i[2] = k * k * cq; j.i[3] = cq; j.i[4] = cq; j.i[5] = k;
+        j.i[6] = p->accumulate ? 1 : 0; j.i[7] = w.S; j.i[8] = ng;
+    };
+    fill(J[0], a.slab_a, p->dwa, a.bias_a, p->dba, nh, n, 1);
+    fill(J[1], a.slab_b, p->dwb, a.bias_b, p->dbb, nh, nh, 3);
+    fill(J[2], a.slab_c, p->dwc, a.bias_c, p->dbc, n, nh, 1);
+    if (jobs) {
+        for (int i = 0; i < 3; ++i) jobs[i] = J[i];
+        return CAI_OK;
+    }
+    return launch_reduce_jobs(J, 3, st);
 }

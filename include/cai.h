@@ -252,6 +252,34 @@ int cai_conv_wgrad_deferred(const cai_conv_geom* g, int dtype,
                             void* workspace, size_t ws_bytes, void* stream, cai_reduce_job* job);
 int cai_reduce_jobs(const cai_reduce_job* jobs, int32_t n, void* stream);
 
+/* The three weight (+ bias) gradients of a ResidualUnit (layers.py:211-226) in one launch, from the
+ * tensors cai_resunit's backward leaves: x (the unit input, ld x_ld), h1 / h2 (the hidden activations,
+ * ld n/2), ga / gb (the pre-activation gradients of a and b, ld n/2), gc (of c, ld gc_ld), all pixel-major
+ * bf16.  dwa [n/2][n][1][1], dwb [n/2][n/2][3][3], dwc [n][n/2][1][1] and the biases: torch layout fp32,
+ * overwritten or accumulated.  Replaces the three cai_conv_wgrad calls of a unit (compressai/_ops.py
+ * _resunit_bwd).  jobs != NULL: the final slab sums are returned as three CAI_JOB_WGRAD jobs (run later by
+ * cai_reduce_jobs, workspace kept alive until then); NULL: run now.  n in {128, 192}. */
+typedef struct cai_resunit_wgrad_args {
+    int32_t batch, h, w, n;
+    const void* x;
+    const void* h1;
+    const void* h2;
+    const void* ga;
+    const void* gb;
+    const void* gc;
+    int32_t x_ld, gc_ld;
+    float* dwa;
+    float* dba;
+    float* dwb;
+    float* dbb;
+    float* dwc;
+    float* dbc;
+    int32_t accumulate;
+} cai_resunit_wgrad_args;
+size_t cai_resunit_wgrad_workspace_bytes(const cai_resunit_wgrad_args* args);
+int cai_resunit_wgrad(const cai_resunit_wgrad_args* args, void* workspace, size_t ws_bytes, void* stream,
+                      cai_reduce_job* jobs);
+
 /* ConvTranspose2d with out_c <= 16 (the synthesis transform's last layer,
  * models/utils.py:138-146, e.g. deconv(N, 3)): forward as one dense GEMM per
  * input pixel (N = k*k*out_c columns) + col2im, backward as im2col + two 1x1

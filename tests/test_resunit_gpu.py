@@ -60,34 +60,103 @@ def test_resunit_kernel_vs_torch(cuda, n, B, H, W, gy_masked):
     res2 = _pm(torch.randn(B, n, H, W, device=cuda)).to(torch.bfloat16)
     u.dx_res2 = res2
     u.mask_x = True
-    grads = {}
-    real = _ops.conv_wgrad
+    cap = {}
+    real = _ops._resunit_wgrad
 
-    def spy(g, dt, xpm_, xld, in_abs, gpm, gld, wparam, bparam, weight, has_bias):
-        grads[id(wparam)] = (xpm_, gpm)
-        return real(g, dt, xpm_, xld, in_abs, gpm, gld, wparam, bparam, weight, has_bias)
+    def spy(u_, xpm_, h1_, h2_, ga_, gb_, gc_, gcld_):
+        cap.update(ga=ga_, gb=gb_, gc=gc_)
+        return real(u_, xpm_, h1_, h2_, ga_, gb_, gc_, gcld_)
 
-    _ops.conv_wgrad = spy
+    _ops._resunit_wgrad = spy
     try:
         dx, pg = _ops._resunit_bwd(u, gy)
     finally:
-        _ops.conv_wgrad = real
+        _ops._resunit_wgrad = real
     torch.cuda.synchronize()
     gc = gy.float() * (y.float() > 0)
     gbr = F.conv2d(gc, r(wc).transpose(0, 1)) * (h2.float() > 0)
-    gb = grads[id(wb)][1]
+    gb = cap["gb"]
     assert relerr(gb, gbr) < 1e-2
     gar = F.conv_transpose2d(gb.float(), r(wb), padding=1) * (h1.float() > 0)
-    ga = grads[id(wa)][1]
+    ga = cap["ga"]
     assert relerr(ga, gar) < 1e-2
     dxr = (F.conv2d(ga.float(), r(wa).transpose(0, 1)) + gc + res2.float()) * (x.float() > 0)
     assert relerr(dx, dxr) < 1e-2
+    gck = cap["gc"]
     if not gy_masked:
-        assert relerr(grads[id(wc)][1], gc) < 1e-2
-    # the weight gradients come from the kernel's tensors through the conv wgrad path
-    dwa = pg[0]
-    dwar = torch.einsum("bchw,bkhw->kc", x.float(), ga.float()).reshape(wa.shape)
-    assert relerr(dwa, dwar) < 2e-2
+        assert relerr(gck, gc) < 1e-2
+    # the six parameter gradients (cai_resunit_wgrad + its WGRAD reduce jobs) against fp32 sums of the kernel's
+    # own bf16 operands: only the summation order differs
+    dwa, dba, dwb, dbb, dwc, dbc = pg
+    gaf, gbf, gcf = ga.float(), gb.float(), gck.float()
+    assert relerr(dwa, torch.einsum("bchw,bkhw->kc", x.float(), gaf).reshape(wa.shape)) < 1e-3
+    assert relerr(dba, gaf.sum((0, 2, 3))) < 1e-3
+    dwbr = torch.nn.grad.conv2d_weight(h1.float(), wb.shape, gbf, padding=1)
+    assert relerr(dwb, dwbr) < 1e-3
+    assert relerr(dbb, gbf.sum((0, 2, 3))) < 1e-3
+    assert relerr(dwc, torch.einsum("bchw,bkhw->kc", h2.float(), gcf).reshape(wc.shape)) < 1e-3
+    assert relerr(dbc, gcf.sum((0, 2, 3))) < 1e-3
+
+
+@pytest.mark.parametrize("n,H,B", [(192, 64, 2), (192, 16, 4), (128, 32, 2), (128, 13, 1)])
+def test_resunit_wgrad_splits_vs_torch(cuda, n, H, B, monkeypatch):
+    """cai_resunit_wgrad on its own at several pixel counts (1 to 32 splits, ragged last split, 13 x 13 images:
+    the 3x3 taps' zero padding at every border) against fp32 torch on the same bf16 operands."""
+    from compressai import _ops
+    from compressai._native import ResunitWgradArgs
+
+    torch.manual_seed(n * H + B)
+    nh = n // 2
+    t = lambda c: _pm(torch.randn(B, c, H, H, device=cuda)).to(torch.bfloat16)   # noqa: E731
+    x, h1, h2, ga, gb, gc = t(n), t(nh), t(nh), t(nh), t(nh), t(n)
+    out = [torch.full(sh, float("nan"), device=cuda) for sh in
+           ((nh, n, 1, 1), (nh,), (nh, nh, 3, 3), (nh,), (n, nh, 1, 1), (n,))]
+    A = ResunitWgradArgs(batch=B, h=H, w=H, n=n, x=x.data_ptr(), h1=h1.data_ptr(), h2=h2.data_ptr(),
+                         ga=ga.data_ptr(), gb=gb.data_ptr(), gc=gc.data_ptr(), x_ld=n, gc_ld=n,
+                         dwa=out[0].data_ptr(), dba=out[1].data_ptr(), dwb=out[2].data_ptr(), dbb=out[3].data_ptr(),
+                         dwc=out[4].data_ptr(), dbc=out[5].data_ptr(), accumulate=0)
+    import ctypes
+    nbytes = _ops.lib.cai_resunit_wgrad_workspace_bytes(ctypes.byref(A))
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=cuda)
+    assert _ops.lib.cai_resunit_wgrad(ctypes.byref(A), ws.data_ptr(), nbytes,
+                                      torch.cuda.current_stream().cuda_stream, None) == 0
+    torch.cuda.synchronize()
+    f = lambda v: v.float()   # noqa: E731
+    ref = [torch.einsum("bchw,bkhw->kc", f(x), f(ga)).reshape(nh, n, 1, 1), f(ga).sum((0, 2, 3)),
+           torch.nn.grad.conv2d_weight(f(h1), (nh, nh, 3, 3), f(gb), padding=1), f(gb).sum((0, 2, 3)),
+           torch.einsum("bchw,bkhw->kc", f(h2), f(gc)).reshape(n, nh, 1, 1), f(gc).sum((0, 2, 3))]
+    for k, (o, r_) in enumerate(zip(out, ref)):
+        assert torch.isfinite(o).all(), k
+        assert relerr(o, r_) < 1e-3, (k, relerr(o, r_))
+
+
+@pytest.mark.parametrize("n,H", [(192, 64), (128, 16)])
+def test_resunit_wgrad_deferred_bit_identical(cuda, n, H):
+    """The optimizer path (FusedAdam's flat gradient buffer: accumulate, reduce jobs deferred to the end of the
+    backward) gives bit-identical parameter gradients to the plain autograd path (fresh tensors, reduce now)."""
+    import compressai.layers as L
+    from compressai.optim import FusedAdam
+
+    torch.manual_seed(H)
+    mod = L.AttentionBlock(n).to(cuda)
+    x0 = _pm(torch.randn(2, n, H, H, device=cuda))
+    gy = _pm(torch.randn(2, n, H, H, device=cuda))
+
+    def run():
+        x = x0.clone().requires_grad_()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = mod(x)
+        (y.float() * gy).sum().backward()
+        torch.cuda.synchronize()
+        return {k: p.grad.clone() for k, p in mod.named_parameters()}
+
+    plain = run()
+    mod.zero_grad(set_to_none=True)
+    opt = FusedAdam(mod.parameters(), lr=1e-3)
+    opt.zero_grad()
+    direct = run()
+    for k in plain:
+        assert torch.equal(plain[k], direct[k]), k
 
 
 @pytest.mark.parametrize("n,H", [(192, 64), (192, 16), (128, 32)])
@@ -125,8 +194,8 @@ def test_attention_block_fused_units_vs_per_conv(cuda, n, H):
 
 
 def test_resunit_launch_count(cuda, monkeypatch):
-    """One AttentionBlock step on the fused path: 6 cai_resunit forwards and 6 backwards, no per-conv residual
-    launches left."""
+    """One AttentionBlock step on the fused path: 6 cai_resunit forwards and 6 backwards, 6 cai_resunit_wgrad, no
+    per-conv residual launches left."""
     import compressai.layers as L
     from compressai import _ops
 
@@ -136,7 +205,7 @@ def test_resunit_launch_count(cuda, monkeypatch):
     class Spy:
         def __getattr__(self, name):
             fn = getattr(real, name)
-            if not name.startswith(("cai_resunit", "cai_conv_fwd_res", "cai_conv_dgrad_res")):
+            if not name.startswith(("cai_resunit", "cai_conv_fwd_res", "cai_conv_dgrad_res", "cai_conv_wgrad")):
                 return fn
 
             def call(*a):
@@ -155,3 +224,7 @@ def test_resunit_launch_count(cuda, monkeypatch):
     assert names.count("cai_resunit") == 12, calls
     assert sum(1 for c in calls if c[0] == "cai_resunit" and c[1] == 1) == 6
     assert not any(n.startswith("cai_conv_fwd_res") or n.startswith("cai_conv_dgrad_res") for n in names)
+    # the six units' weight gradients: one cai_resunit_wgrad each, no per-conv weight gradient left for them
+    # (the block's final 1x1 conv_b keeps its own)
+    assert names.count("cai_resunit_wgrad") == 6, calls
+    assert sum(1 for n in names if n in ("cai_conv_wgrad", "cai_conv_wgrad_deferred")) == 1, calls
