@@ -801,8 +801,27 @@ class _FusedUnit:
         self.dx_res2 = self.dx_res = None
 
 
+def _gdn_name(code, npix, C, ld, direction) -> str:
+    """The GDN kernel a call launches (ledger label); "gdn" from an older library without the query (A/B)."""
+    try:
+        return lib.cai_gdn_kernel_name(code, npix, C, ld, C, direction).decode()
+    except AttributeError:
+        return "gdn_fwd" if direction == 0 else "gdn_bwd"
+
+
+_HAS = {}
+
+
+def _has_resunit() -> bool:
+    """The library has the fused unit kernels (an older one in an A/B run does not: per-conv chain)."""
+    v = _HAS.get("resunit")
+    if v is None:
+        v = _HAS["resunit"] = hasattr(lib.load(), "cai_resunit")
+    return v
+
+
 def _resunit_ok(y, specs, params) -> bool:
-    if not _RESUNIT_FUSED or compute_dtype() != torch.bfloat16 or y.dim() != 4 or not y.is_cuda:
+    if not _RESUNIT_FUSED or compute_dtype() != torch.bfloat16 or y.dim() != 4 or not y.is_cuda or not _has_resunit():
         return False
     n = y.shape[1]
     w0, b0, w2, b2, w4, b4 = params
@@ -879,7 +898,7 @@ def _resunit_bwd(u: "_FusedUnit", gy):
     _ledger.run(lambda: lib.cai_resunit(ctypes.byref(A), 1, _stream()), "conv_dgrad", f"resunit_kernel<{n},bwd>", fl,
                 2 * B * H * W * (3 * n + 4 * nh), dt, f"ResidualUnit N={n} {H}x{W} B={B}")
     gcc, gcld = (gpm, gld) if g_c is None else (g_c, n)
-    if _RESUNIT_WGRAD:
+    if _RESUNIT_WGRAD and hasattr(lib.load(), "cai_resunit_wgrad"):
         grads = _resunit_wgrad(u, xpm, h1, h2, g_a, g_b, gcc, gcld)
         return dx, grads
     dw4, db4 = conv_wgrad(gc, dt, h2, nh, 0, gcc, gcld, w4, b4, w4, True)
@@ -1061,7 +1080,7 @@ class GdnFn(torch.autograd.Function):
             lib.cai_gdn_reparam(_p(br), _p(gr), C, beta_min, reparam_offset, code, _p(beta), _p(gop), st)
         y = empty_pm(B, C, H, W, dt, x.device)
         _ledger.run(lambda: lib.cai_gdn_fwd(code, _p(xpm), xld, npix, C, _p(gop), _p(beta), int(inverse), _p(y), C, st),
-                    "gdn_fwd", lambda: lib.cai_gdn_kernel_name(code, npix, C, xld, C, 0).decode(), 2.0 * npix * C * C, 2 * npix * C * _es(dt) + C * C * _es(dt), dt,
+                    "gdn_fwd", lambda: _gdn_name(code, npix, C, xld, 0), 2.0 * npix * C * C, 2 * npix * C * _es(dt) + C * C * _es(dt), dt,
                     f"{'IGDN' if inverse else 'GDN'} C={C} npix={npix}")
         ctx.save_for_backward(xpm, br, gr, beta, gop)
         ctx.cfg = (dt, xld, int(inverse), float(beta_min), float(reparam_offset))
@@ -1107,7 +1126,7 @@ class GdnFn(torch.autograd.Function):
                                                                       _p(beta), inverse, _p(dx), C, _p(br), _p(gr),
                                                                       beta_min, off, _p(dbr), _p(dgr), int(direct),
                                                                       _p(ws), nbytes, st),
-                        "gdn_bwd", lambda: lib.cai_gdn_kernel_name(code, npix, C, max(xld, gld), C, 1).decode(),
+                        "gdn_bwd", lambda: _gdn_name(code, npix, C, max(xld, gld), 1),
                         4.0 * npix * C * C,
                         3 * npix * C * _es(dt) + 8 * C * C, dt, f"{'IGDN' if inverse else 'GDN'} C={C} npix={npix}")
         if direct:
