@@ -193,13 +193,6 @@ struct SplitBwdGeo {
     static constexpr int BUF = 4 * IMG;                // x^2, u, t1, x of one step
     static constexpr int IB = NB / 4;                  // dgamma row blocks per dx wave
     static constexpr int LDS = 2 * BUF + C * 4 + 4 * C * 4;   // two buffers, beta, dbeta per norm wave
-    // byte offset of 16-byte chunk `ch` (8 channels) of image row `row`: the chunks of a row are rotated by
-    // (row & 3) + ((row >> 2) & 1).  The dgamma stage's ds_read_b64_tr_b16 (4 rows x 2 chunks per 16 lanes) then
-    // hits 32 distinct banks (2-way on the plain layout: rows 68 dwords apart put chunk c of row r + 1 on chunk
-    // c + 1 of row r), and the 16-byte row stores stay conflict-free.
-    static __device__ __forceinline__ int off(int row, int ch) {
-        return row * RS + ((ch + (row & 3) + ((row >> 2) & 1)) & (C / 8 - 1)) * 16;
-    }
 };
 
 template <int C, bool INV>
@@ -254,8 +247,8 @@ __global__ __launch_bounds__(512, 1) void gdn_bwd_lane_kernel(const bf16* __rest
 #pragma unroll
             for (int kb = 0; kb < KB; ++kb) {
                 q[kb] = sq_chunk<bf16>(rx[kb]);
-                *reinterpret_cast<u32x4*>(Lq + G::off(prow, 4 * kb + g)) = q[kb];
-                *reinterpret_cast<u32x4*>(Lx + G::off(prow, 4 * kb + g)) = rx[kb];
+                *reinterpret_cast<u32x4*>(Lq + prow * G::RS + (32 * kb + 8 * g) * 2) = q[kb];
+                *reinterpret_cast<u32x4*>(Lx + prow * G::RS + (32 * kb + 8 * g) * 2) = rx[kb];
             }
 #pragma unroll
             for (int kx = 0; kx < KB; ++kx) {
@@ -289,8 +282,8 @@ __global__ __launch_bounds__(512, 1) void gdn_bwd_lane_kernel(const bf16* __rest
                         uu[e] = (bf16)uv;
                     }
                 }
-                *reinterpret_cast<bf16x8*>(Lu + G::off(prow, 4 * kx + g)) = uu;
-                *reinterpret_cast<bf16x8*>(Lt + G::off(prow, 4 * kx + g)) = tt;
+                *reinterpret_cast<bf16x8*>(Lu + prow * G::RS + (32 * kx + 8 * g) * 2) = uu;
+                *reinterpret_cast<bf16x8*>(Lt + prow * G::RS + (32 * kx + 8 * g) * 2) = tt;
                 const unsigned off = nok ? (unsigned)(npx * x_ld + 8 * g) * 2u + 64u * kx : LANE_OOB;
                 const unsigned offg = nok ? (unsigned)(npx * dy_ld + 8 * g) * 2u + 64u * kx : LANE_OOB;
                 rx[kx] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
@@ -353,14 +346,14 @@ __global__ __launch_bounds__(512, 1) void gdn_bwd_lane_kernel(const bf16* __rest
             u32x4 uf[KB];
 #pragma unroll
             for (int kb = 0; kb < KB; ++kb)
-                uf[kb] = *reinterpret_cast<const u32x4*>(Lu + G::off(prow, 4 * kb + g));
+                uf[kb] = *reinterpret_cast<const u32x4*>(Lu + prow * G::RS + (32 * kb + 8 * g) * 2);
             // ---- dx^T = gamma^T u^T; dx = t1 + 2 x (gamma^T u), 16 bytes out per K block ----
             const bool ok = pix < npix;
             const unsigned base = (unsigned)(pix * dx_ld + 8 * g) * 2u;
 #pragma unroll
             for (int kx = 0; kx < KB; ++kx) {
-                const bf16x8 xv = *reinterpret_cast<const bf16x8*>(Lx + G::off(prow, 4 * kx + g));
-                const bf16x8 tt = *reinterpret_cast<const bf16x8*>(Lt + G::off(prow, 4 * kx + g));
+                const bf16x8 xv = *reinterpret_cast<const bf16x8*>(Lx + prow * G::RS + (32 * kx + 8 * g) * 2);
+                const bf16x8 tt = *reinterpret_cast<const bf16x8*>(Lt + prow * G::RS + (32 * kx + 8 * g) * 2);
                 bf16x8 dd;
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
@@ -385,9 +378,9 @@ __global__ __launch_bounds__(512, 1) void gdn_bwd_lane_kernel(const bf16* __rest
                 for (int i = 0; i < IB; ++i) {
                     const int col = (d * IB + i) * 16 + 4 * p4;
                     const s16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (__attribute__((address_space(3))) s16x4*)(Lu + G::off(rr, col >> 3) + (col & 7) * 2));
+                        (__attribute__((address_space(3))) s16x4*)(Lu + rr * G::RS + col * 2));
                     const s16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (__attribute__((address_space(3))) s16x4*)(Lu + G::off(rr + 4, col >> 3) + (col & 7) * 2));
+                        (__attribute__((address_space(3))) s16x4*)(Lu + (rr + 4) * G::RS + col * 2));
                     const s16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
                     afr[i] = __builtin_bit_cast(u32x4, av);
 #if CAI_GDN_PF2
@@ -398,9 +391,9 @@ __global__ __launch_bounds__(512, 1) void gdn_bwd_lane_kernel(const bf16* __rest
                 for (int jb = 0; jb < NB; ++jb) {
                     const int col = jb * 16 + 4 * p4;
                     const s16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (__attribute__((address_space(3))) s16x4*)(Lq + G::off(rr, col >> 3) + (col & 7) * 2));
+                        (__attribute__((address_space(3))) s16x4*)(Lq + rr * G::RS + col * 2));
                     const s16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (__attribute__((address_space(3))) s16x4*)(Lq + G::off(rr + 4, col >> 3) + (col & 7) * 2));
+                        (__attribute__((address_space(3))) s16x4*)(Lq + (rr + 4) * G::RS + col * 2));
                     const s16x8 bv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
                     const u32x4 bfr = __builtin_bit_cast(u32x4, bv);
 #pragma unroll
