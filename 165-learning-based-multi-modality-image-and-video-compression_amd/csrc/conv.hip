@@ -2267,7 +2267,8 @@ struct SwArgs {
     int x_ld, Cq, Cq_pad, in_abs, in_sq;
     int B, Hg, Wg, Hx, Wx, k, s, p;
     int M;            // G pixels
-    int ncb;          // 64-wide column blocks: k*k*Cq_pad / 64
+    int ncb;          // 64-wide column blocks: k*k*cbt
+    int cbt;          // column blocks per tap: ceil(Cq_pad / 64) (the last one masked when Cq_pad % 64 == 32)
     float* dw;
     int accumulate;
     const void* bsrc; // bias: column sums of bsrc [bnpix][bc] (ld bsrc_ld) -> db; db == NULL: none
@@ -2340,8 +2341,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_small_kernel(const SwArgs a) {
         return;
     }
     const int n0 = blockIdx.y * 64;
-    const int col0 = blockIdx.x * 64;
-    const int t = col0 / a.Cq_pad, q0 = col0 - t * a.Cq_pad;
+    const int t = (int)blockIdx.x / a.cbt, q0 = ((int)blockIdx.x - t * a.cbt) * 64;
     const int kh = t / a.k, kw = t - kh * a.k;
     const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<void*>(a.g), (short)0, (int)((int64_t)a.M * a.g_ld * 2), 0x00020000);
@@ -2366,13 +2366,16 @@ __global__ __launch_bounds__(512, 1) void wgrad_small_kernel(const SwArgs a) {
             const int row = i * 8 + (lane >> 3);
             const int m = st * 32 + row;
             const bool okm = (st < s1) & (m < a.M);
+            // 32-multiple widths: the channel slots past Ng / Cq_pad of the last row / column block read 0
+            const bool okg = okm & (n0 + slot * 8 < a.Ng);
             const unsigned goff = (unsigned)(m * a.g_ld + n0 + slot * 8) * 2u;
-            rg[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(gr, okm ? goff : OOB, 0, 0));
+            rg[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(gr, okg ? goff : OOB, 0, 0));
             const int b = div_small(m, plane, a.inv_plane);
             const int r = m - b * plane;
             const int j = div_small(r, a.Wg, a.inv_wg);
             const int iy = j * a.s - a.p + kh, ix = (r - j * a.Wg) * a.s - a.p + kw;
-            const bool okx = okm & ((unsigned)iy < (unsigned)a.Hx) & ((unsigned)ix < (unsigned)a.Wx);
+            const bool okx = okm & ((unsigned)iy < (unsigned)a.Hx) & ((unsigned)ix < (unsigned)a.Wx) &
+                             (q0 + slot * 8 < a.Cq_pad);
             const unsigned xoff = (unsigned)(((b * a.Hx + iy) * a.Wx + ix) * a.x_ld + q0 + slot * 8) * 2u;
             rx[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, okx ? xoff : OOB, 0, 0));
         }
@@ -3830,8 +3833,16 @@ static bool small_wgrad_off() {
 // profiles/r03_cheng2020_dispatch_ab.log)
 static bool small_wgrad_ok(const cai_conv_geom* g, int dtype) {
     const WgradPlan W = make_wgrad_plan(g, dtype, true);
-    return !small_wgrad_off() && dtype == CAI_BF16 && W.M <= SW_NW * SW_STEPS * 32 && W.Ng % 64 == 0 &&
-           W.Cq_pad % 64 == 0 && (int64_t)W.Ng * W.ncols <= (1 << 20);
+    // 32-multiple channel counts take partial 64-wide tiles (cheng2020's 96 / 160 / 288-channel latent layers:
+    // 127 us for the 8x8 288 -> 1152 sub-pixel conv's weight gradient on split slabs + reduce)
+    // (A/B knob CAI_SMALL_WGRAD_W64=1: the round-3 rule, 64-multiples and <= 2^20 weights)
+    static const bool w64 = [] {
+        const char* e = getenv("CAI_SMALL_WGRAD_W64");
+        return e && *e == '1';
+    }();
+    const int gran = w64 ? 64 : 32;
+    return !small_wgrad_off() && dtype == CAI_BF16 && W.M <= SW_NW * SW_STEPS * 32 && W.Ng % gran == 0 &&
+           W.Cq_pad % gran == 0 && (int64_t)W.Ng * W.ncols <= (w64 ? (1 << 20) : (1 << 23));
 }
 
 
@@ -4147,7 +4158,7 @@ static int run_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int3
         sa.x = a.x; sa.x_ld = a.x_ld; sa.Cq = W.Cq; sa.Cq_pad = W.Cq_pad; sa.in_abs = a.in_abs; sa.in_sq = a.in_sq;
         sa.B = g->batch; sa.Hg = a.Hg; sa.Wg = a.Wg; sa.Hx = a.Hx; sa.Wx = a.Wx;
         sa.k = g->kernel; sa.s = g->stride; sa.p = g->pad;
-        sa.M = (int)W.M; sa.ncb = W.ncols / 64;
+        sa.M = (int)W.M; sa.cbt = (W.Cq_pad + 63) / 64; sa.ncb = g->kernel * g->kernel * sa.cbt;
         sa.dw = dw; sa.accumulate = accumulate;
         sa.bsrc = dy; sa.bsrc_ld = dy_ld; sa.bnpix = g->batch * g->out_h * g->out_w; sa.bc = g->out_c; sa.db = db;
         sa.bias_from_g = !g->transposed;
@@ -4155,7 +4166,7 @@ static int run_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int3
         sa.inv_wg = 1.f / (float)a.Wg;
         CAI_CHECK_ARG((int64_t)sa.bnpix * dy_ld * 2 < (1ll << 31) && (int64_t)a.B * a.Hx * a.Wx * a.x_ld * 2 < (1ll << 31),
                       "conv_wgrad: operand larger than 2 GiB");
-        const dim3 grid(sa.ncb + ((db && g->transposed) ? 1 : 0), W.Ng / 64);
+        const dim3 grid(sa.ncb + ((db && g->transposed) ? 1 : 0), (W.Ng + 63) / 64);
         if (sa.in_abs)
             hipLaunchKernelGGL(wgrad_small_kernel<1>, grid, dim3(512), 0, st, sa);
         else if (sa.in_sq)

@@ -117,6 +117,13 @@ CONV_CASES = [
     ("conv", 4, 96, 192, 16, 16, 1, 1),
     ("conv", 4, 192, 288, 8, 8, 3, 1),
     ("deconv", 4, 96, 160, 8, 8, 3, 1),
+    # latent-size weight gradients on partial 64-wide tiles (wgrad_small_kernel, 32-multiple widths and outputs
+    # past 2^20 weights): cheng2020 q6 h_s sub-pixel conv 288 -> 1152 at 8x8, context prediction 192 -> 384 k5,
+    # 192 -> 768 at 4x4, a 160 / 96 ConvTranspose2d
+    ("conv", 4, 288, 1152, 8, 8, 3, 1),
+    ("conv", 4, 192, 384, 16, 16, 5, 1),
+    ("conv", 4, 192, 768, 4, 4, 3, 1),
+    ("deconv", 4, 160, 96, 8, 8, 3, 1),
     # 64-row LDS-DMA tiles (conv_glds_kernel<64x128 / 64x192>: mid-size maps whose 256 / 128-row grid would split
     # K): cheng2020 attention-unit 1x1 convs at 64x64, B = 4, both directions
     ("conv", 4, 96, 192, 64, 64, 1, 1),
