@@ -2276,6 +2276,7 @@ struct SwArgs {
     float* db;
     int bias_from_g;  // Conv2d: db = column sums of G, taken by the main blocks; else by trailing blocks
     float inv_plane, inv_wg;   // 1 / (Hg * Wg), 1 / Wg: the per-row pixel decomposition without integer division
+    float* slab;      // non-NULL: dW goes to the [Ng][k*k*Cq_pad] slab (coalesced rows; a WGRAD reduce job transposes it)
 };
 
 // n / d for 0 <= n < 2^23 from a float reciprocal and one correction each way (n * inv is off by at most one);
@@ -2458,6 +2459,22 @@ __global__ __launch_bounds__(512, 1) void wgrad_small_kernel(const SwArgs a) {
             for (int lr = 0; lr < 8; ++lr) v += bred[(w * 64 + lr * 8 + (tid >> 3)) * 8 + (tid & 7)];
         float* d = a.db + n0 + tid;
         *d = a.accumulate ? *d + v : v;
+    }
+    if (a.slab) {
+        // slab row n: [tap][Cq_pad] -- this block's 64 columns are one contiguous 256-byte run per row (the torch
+        // layout's stride-k*k scatter cost one L2 request per element: 819 K requests per C2 h-layer launch)
+        const int ncols = a.k * a.k * a.Cq_pad;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int id = u * 512 + tid;
+            const int nl = id >> 6, ql = id & 63;
+            const int n = n0 + nl, q = q0 + ql;
+            float s_ = 0.f;
+#pragma unroll
+            for (int w = 0; w < SW_NW; ++w) s_ += red[(w * 64 + nl) * 68 + ql];
+            if (n < a.Ng && q < a.Cq_pad) a.slab[(int64_t)n * ncols + t * a.Cq_pad + q] = s_;
+        }
+        return;
     }
     // torch layout dw[n][q][kh][kw]: 8 elements per thread, their old values (accumulate) loaded together
     // before any store -- one dependent round trip instead of eight
@@ -4166,6 +4183,13 @@ static int run_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int3
         sa.inv_wg = 1.f / (float)a.Wg;
         CAI_CHECK_ARG((int64_t)sa.bnpix * dy_ld * 2 < (1ll << 31) && (int64_t)a.B * a.Hx * a.Wx * a.x_ld * 2 < (1ll << 31),
                       "conv_wgrad: operand larger than 2 GiB");
+        // dW through a one-split slab and a WGRAD job (deferred: joins the backward's batched reduce launch);
+        // A/B knob CAI_SMALL_WGRAD_DIRECT=1: straight into the torch layout (scattered stores)
+        static const bool direct_out = [] {
+            const char* e = getenv("CAI_SMALL_WGRAD_DIRECT");
+            return e && *e == '1';
+        }();
+        sa.slab = direct_out ? nullptr : slab;
         const dim3 grid(sa.ncb + ((db && g->transposed) ? 1 : 0), (W.Ng + 63) / 64);
         if (sa.in_abs)
             hipLaunchKernelGGL(wgrad_small_kernel<1>, grid, dim3(512), 0, st, sa);
@@ -4174,7 +4198,18 @@ static int run_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int3
         else
             hipLaunchKernelGGL(wgrad_small_kernel<0>, grid, dim3(512), 0, st, sa);
         CAI_LAUNCH_CHECK("conv_wgrad");
-        return CAI_OK;
+        if (direct_out) return CAI_OK;
+        cai_reduce_job J{};
+        J.kind = CAI_JOB_WGRAD;
+        J.nblocks = wgrad_job_blocks(W.Ng, W.Cq_pad, g->kernel, 0);
+        J.p[0] = slab; J.p[1] = dw;
+        J.i[0] = 1; J.i[1] = W.Ng; J.i[2] = W.ncols; J.i[3] = W.Cq; J.i[4] = W.Cq_pad; J.i[5] = g->kernel;
+        J.i[6] = accumulate;
+        if (job) {
+            *job = J;
+            return CAI_OK;
+        }
+        return launch_reduce_jobs(&J, 1, st);
     }
     float* bws = nullptr;
     if (W.glds) {
