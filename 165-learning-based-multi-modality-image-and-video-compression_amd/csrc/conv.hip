@@ -1166,6 +1166,9 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvArgs a, int
 #ifndef CAI_HALO_PH_PAIRS
 #define CAI_HALO_PH_PAIRS 0
 #endif
+#ifndef CAI_HALO_PH_PP
+#define CAI_HALO_PH_PP 0
+#endif
 
 
 // HALF: the 256-thread form (4 waves, 8 x 16 tiles, two workgroups per CU): the two waves that share a SIMD
@@ -1194,16 +1197,32 @@ struct HaloPhCfg {
     // since the last barrier (steps t - 1 and t) refill with steps t + NSTB - 1 and t + NSTB, and the barrier
     // certifies steps t + 1 and t + 2 -- the operands of both steps until the next one; NSTB = 6 (4 for the
     // 8-step 2x2 phase) leaves NSTB - 2 steps between a DMA and its barrier.
-    static constexpr bool PAIRS = CAI_HALO_PH_PAIRS && DPS == 1 && !HALF && NST % 2 == 0;
-    static constexpr int NSTB = PAIRS ? (NST % 6 == 0 ? 6 : 4)
-                                      : ((CAI_HALO_PH_NSTB6 && NST % 6 == 0) ? 6 : (NST % 3 == 0 ? 3 : 2));
+    // PP (CAI_HALO_PH_PP=1): ping-pong -- waves 4-7 run one barrier behind waves 0-3 (wave w and w + 4 share a
+    // SIMD), so one group's fragment reads and waits overlap the other group's MFMAs.  Waves 0-3 issue every weight
+    // DMA (two per lane and step, PP_D steps ahead) into an NSTB-deep ring (NSTB >= PP_D + 1: the lagging group
+    // still reads the stage a DMA would overwrite otherwise); the footprint is double-buffered, the next chunk's
+    // stored at step NST - 3 (the lagging group's stores retire one barrier before the leading group's first read).
+    static constexpr bool PP = CAI_HALO_PH_PP && DPS == 1 && !HALF;
+    static constexpr int PP_D = 3;
+    static constexpr bool PAIRS = CAI_HALO_PH_PAIRS && DPS == 1 && !HALF && NST % 2 == 0 && !PP;
+    static constexpr int NSTB = PP ? (NST % 6 == 0 ? 6 : 4)
+                                   : PAIRS ? (NST % 6 == 0 ? 6 : 4)
+                                           : ((CAI_HALO_PH_NSTB6 && NST % 6 == 0) ? 6 : (NST % 3 == 0 ? 3 : 2));
+    static constexpr int NPATCH = PP ? 2 : 1;
     static constexpr int BSTAGE = DPS * NT * 16;
     // BN > 128: register-direct epilogue only (no LDS staging buffer), see conv_epilogue_rows_t
     static constexpr int EPI = BN > 128 ? 0 : BM * (BN + 4) * 4;
-    static constexpr int BYTES = (PATCH + NSTB * BSTAGE > EPI) ? PATCH + NSTB * BSTAGE : EPI;
-    static_assert(PAIRS ? (NPI <= NST + 2 - NSTB && NST % NSTB == 0) : NPI <= NST - NSTB,
+    static constexpr int BYTES = (NPATCH * PATCH + NSTB * BSTAGE > EPI) ? NPATCH * PATCH + NSTB * BSTAGE : EPI;
+    static_assert(PP ? (NPI <= NST - 3 && NST % NSTB == 0 && NSTB >= PP_D + 1)
+                     : PAIRS ? (NPI <= NST + 2 - NSTB && NST % NSTB == 0) : NPI <= NST - NSTB,
                   "the next chunk's footprint must retire before the chunk's last step");
 };
+
+// PP: the loads group A issued after the weight DMA of step t + 1 (issued at step t + 1 - PP_D = t - 2): the two
+// DMAs of step t - 1 and the footprint cells of steps t - 2 and t - 1 (one per step below npi)
+__host__ __device__ constexpr int halo_younger_pp(int t, int npi) {
+    return 2 + ((t >= 2 && t - 2 < npi) ? 1 : 0) + ((t >= 1 && t - 1 < npi) ? 1 : 0);
+}
 
 // PAIRS: the loads issued after step t + 2's weight DMA that an even step t's wait leaves in flight -- the DMAs of
 // the even steps after t' = t + 2 - NSTB (two each), the footprint cells issued at steps [t', t - 1] (j < NPI)
@@ -1229,7 +1248,7 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
     constexpr int NPI = H::NPI, NTAP = H::NTAP, NST = H::NST, NSTB = H::NSTB;
     static_assert(WM * WN == NT / 64 && WTM == 2 * H::TW && H::BYTES <= 160 * 1024, "halo phase tile");
     char* const patch = smem;
-    char* const bring = smem + H::PATCH;
+    char* const bring = smem + H::NPATCH * H::PATCH;
 
     const PhaseDesc& P = a.ph[ph];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1308,7 +1327,7 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
         const int n = wn * WTN + tn * 16 + i16;
-        bpos[tn] = H::PATCH + (4 * n + (g_ ^ (((n >> 3) & 1) * 3))) * 16;
+        bpos[tn] = H::NPATCH * H::PATCH + (4 * n + (g_ ^ (((n >> 3) & 1) * 3))) * 16;
     }
     auto read_frags = [&](int t, u32x4 (&fa)[TM], u32x4 (&fb)[TN]) {
         const int hf = t / NTAP, tap = t - hf * NTAP;
@@ -1329,7 +1348,105 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     u32x4 fa[TM], fb[TN];
-    if constexpr (H::PAIRS) {
+    if constexpr (H::PP) {
+        constexpr int D = H::PP_D;
+        const int wv = __builtin_amdgcn_readfirstlane(wid);
+        const bool grpA = wv < 4;
+        // group A lane la stages weight rows la >> 2 and (la >> 2) + 64 (16-byte slots as in the one-DMA layout)
+        const int la = (wv & 3) * 64 + lane;
+        const int bna = la >> 2, bsa = (la & 3) ^ (((bna >> 3) & 1) * 3);
+        const char* WrA0 = n0 + bna < a.Npad
+                               ? reinterpret_cast<const char*>(a.w) + (P.w_off + (int64_t)(n0 + bna) * a.Kp) * 2 + bsa * 16
+                               : nullptr;
+        const char* WrA1 = n0 + bna + 64 < a.Npad ? reinterpret_cast<const char*>(a.w) +
+                                                        (P.w_off + (int64_t)(n0 + bna + 64) * a.Kp) * 2 + bsa * 16
+                                                  : nullptr;
+        auto issue_pp = [&](int ci, int t) {   // weight step t of chunk ci (t >= NST: the next chunk's)
+            if (t >= NST) {
+                ci += 1;
+                t -= NST;
+            }
+            const int hf = t / NTAP, tap = t - hf * NTAP;
+            const int koff = (tap * a.Cin_pad + (c0 + ci) * H::CK + hf * 32) * 2;
+            const bool live = ci < nc;
+            char* const dst = bring + (t % NSTB) * H::BSTAGE + (wv & 3) * 1024;
+            glds16_asm((WrA0 && live) ? (const void*)(WrA0 + koff) : (const void*)cai_zero_page, dst);
+            glds16_asm((WrA1 && live) ? (const void*)(WrA1 + koff) : (const void*)cai_zero_page, dst + 4 * 1024);
+        };
+        auto read_pp = [&](int t, int pb, u32x4 (&ra)[TM], u32x4 (&rb)[TN]) {
+            const int hf = t / NTAP, tap = t - hf * NTAP;
+            const int ty = tap / NC, tx = tap - (tap / NC) * NC;
+            const int toff = GATHER ? (hf * 4 * H::PLANE + ty * H::PW + tx) * 16
+                                    : (hf * 4 * H::PLANE + (NA - 1 - ty) * H::PW + (NC - 1 - tx)) * 16;
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm) ra[tm] = *reinterpret_cast<const u32x4*>(smem + pb + apos[tm] + toff);
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn)
+                rb[tn] = *reinterpret_cast<const u32x4*>(smem + bpos[tn] + (t % NSTB) * H::BSTAGE);
+        };
+        auto store_pp = [&](int pb) {
+#pragma unroll
+            for (int i = 0; i < NPI; ++i) {
+                const int q8 = tid + NT * i, g = (q8 >> 3) & 7, q = ((q8 >> 6) << 3) | (q8 & 7);
+                if (q < H::NPOS) *reinterpret_cast<u32x4*>(smem + pb + (g * H::PLANE + q) * 16) = pr_[i];
+            }
+        };
+        if (nc > 0) {
+#pragma unroll
+            for (int i = 0; i < NPI; ++i) load_cell(0, i);
+            if (grpA) {
+#pragma unroll
+                for (int t = 0; t < D; ++t) issue_pp(0, t);
+            }
+            wait_vmcnt<0>();
+            store_pp(0);
+            wait_lgkmcnt0();
+            __builtin_amdgcn_s_barrier();
+            read_pp(0, 0, fa, fb);
+            if (!grpA) __builtin_amdgcn_s_barrier();   // group B runs one barrier behind from here on
+        }
+        for (int ci = 0; ci < nc; ++ci) {
+            const int pb = (ci & 1) * H::PATCH, pbn = pb ^ H::PATCH;
+#pragma unroll
+            for (int t = 0; t < NST; ++t) {
+                if (grpA) wait_vmcnt_n(halo_younger_pp(t, NPI));   // this group's DMA of step t + 1 has landed
+                wait_lgkmcnt0();
+                __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_sched_barrier(0);
+                if (grpA) issue_pp(ci, t + D);
+                if (t < NPI) load_cell(ci + 1, t);
+                if (t == NST - 3) {   // the next chunk's footprint into the other buffer
+                    if (grpA)
+                        wait_vmcnt_n(2 * (t - NPI + 1));   // the DMAs of steps NPI .. t came after the last cell
+                    else
+                        wait_vmcnt<0>();
+                    store_pp(pbn);
+                }
+                u32x4 na[TM], nb[TN];
+                read_pp(t + 1 == NST ? 0 : t + 1, t + 1 == NST ? pbn : pb, na, nb);
+                __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn)
+                        acc[tm][tn] = (CAI_HALO_PH_T || BN > 128) ? mma16<bf16>(fb[tn], fa[tm], acc[tm][tn])
+                                                    : mma16<bf16>(fa[tm], fb[tn], acc[tm][tn]);
+#pragma unroll
+                for (int i = 0; i < TM + TN; ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                }
+                __builtin_amdgcn_sched_group_barrier(0x008, TM * TN - (TM + TN), 0);
+                __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm) fa[tm] = na[tm];
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) fb[tn] = nb[tn];
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        if (nc > 0 && grpA) __builtin_amdgcn_s_barrier();   // pairs group B's extra barrier
+    } else if constexpr (H::PAIRS) {
         auto issue_s = [&](int ci, int s) {   // step s of chunk ci, s may run into the next chunk
             if (s < NST)
                 issue_b(ci, s);
