@@ -3419,6 +3419,14 @@ static int small_kmax() {
     }();
     return v;
 }
+// A/B knob CAI_SMALL_CONV_MMAX (default 1024): the row bound that lifts the 256-block limit of the second rule
+static int small_mmax() {
+    static const int v = [] {
+        const char* e = getenv("CAI_SMALL_CONV_MMAX");
+        return (e && *e) ? atoi(e) : 1024;
+    }();
+    return v;
+}
 static int pick_small(const Plan& P, int dtype, int mmax, int big_ksplit, int big_blocks) {
     if (small_off() || dtype != CAI_BF16 || P.Cin_pad % 32 != 0 || (big_ksplit <= 1 && big_blocks >= 64) ||
         mmax > 8192)
@@ -3428,7 +3436,7 @@ static int pick_small(const Plan& P, int dtype, int mmax, int big_ksplit, int bi
     const int cfg = mmax <= 512 ? SMALL_16x32 : (mmax <= 2048 ? SMALL_32x32 : SMALL_32x64);
     static const int bm[] = {0, 16, 32, 32}, bn[] = {0, 32, 32, 64};
     const int blocks = (mmax + bm[cfg] - 1) / bm[cfg] * ((P.kout_c + bn[cfg] - 1) / bn[cfg]) * P.nphase;
-    if (mmax <= 512 || (kmax <= small_kmax() && (blocks <= 256 || mmax <= 1024))) return cfg;
+    if (mmax <= 512 || (kmax <= small_kmax() && (blocks <= 256 || mmax <= small_mmax()))) return cfg;
     return SMALL_NONE;
 }
 
