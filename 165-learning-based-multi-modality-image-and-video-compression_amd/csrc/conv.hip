@@ -2412,7 +2412,8 @@ __device__ __forceinline__ int swz_sw(int row, int slot) {
     return row * 128 + ((slot ^ ((((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2))) << 4);
 }
 
-template <int XT>   // X transform on load: 0 none, 1 |x| (h_a's first conv), 2 x^2 (GDN's gamma gradient)
+// LONG: more than SW_STEPS steps per wave (M up to small_wgrad_mmax()): the step pairs in a loop
+template <int XT, bool LONG = false>   // X transform on load: 0 none, 1 |x| (h_a's first conv), 2 x^2 (GDN's gamma gradient)
 __global__ __launch_bounds__(512, 1) void wgrad_small_kernel(const SwArgs a) {
     // 8 x (64 x 68 fp32) partial tiles (the loop's staging uses the first 64 KB) + 512 x 8 bias partials
     __shared__ __attribute__((aligned(16))) char smem[SW_NW * 64 * 68 * 4 + 512 * 8 * 4];
@@ -2546,10 +2547,19 @@ __global__ __launch_bounds__(512, 1) void wgrad_small_kernel(const SwArgs a) {
     // M <= 1024 (host check): at most SW_STEPS steps per wave, straight-line code (no loop-carried
     // register sets, whose back-edge copies would wait for the prefetch); steps past s1 multiply zeros
     static_assert(SW_STEPS % 2 == 0, "pairs");
+    if constexpr (LONG) {
+        // the two register sets keep fixed roles in the pair body: no back-edge copies
+        const int npairs = s1 > s0 ? (s1 - s0 + 1) / 2 : 0;
+        for (int it = 0; it < npairs; ++it) {
+            step(s0 + 2 * it, rga, rxa);
+            step(s0 + 2 * it + 1, rgb, rxb);
+        }
+    } else {
 #pragma unroll
-    for (int it = 0; it < SW_STEPS / 2; ++it) {
-        step(s0 + 2 * it, rga, rxa);
-        step(s0 + 2 * it + 1, rgb, rxb);
+        for (int it = 0; it < SW_STEPS / 2; ++it) {
+            step(s0 + 2 * it, rga, rxa);
+            step(s0 + 2 * it + 1, rgb, rxb);
+        }
     }
     // partial tiles: wave w -> fp32 [64][68] at w * 17 KB (the staging regions are dead past this barrier)
     __syncthreads();
@@ -3973,6 +3983,15 @@ static bool small_wgrad_off() {
 // ... and with at most 2^20 weights: wider outputs (cheng2020 q6 at B = 4: 192->384 k5 and 192->768 k3 at 16x16,
 // 192->768 k3 at 4x4) measured slower than the pixel-split kernel + reduce (134 / 71 / 91 vs 60 / 56 / 54 us,
 // profiles/r03_cheng2020_dispatch_ab.log)
+// G pixels up to which the latent-size weight gradient is taken: SW_NW * SW_STEPS * 32 = 1024 (straight-line
+// steps); A/B knob CAI_SMALL_WGRAD_MMAX (e.g. 4096: C2's g_a[6] / g_s[0], 16 x 16 x 16 pixels, on the looped form)
+static int64_t small_wgrad_mmax() {
+    static const int64_t v = [] {
+        const char* e = getenv("CAI_SMALL_WGRAD_MMAX");
+        return (e && *e) ? (int64_t)atoi(e) : (int64_t)(SW_NW * SW_STEPS * 32);
+    }();
+    return v;
+}
 static bool small_wgrad_ok(const cai_conv_geom* g, int dtype) {
     const WgradPlan W = make_wgrad_plan(g, dtype, true);
     // 32-multiple channel counts take partial 64-wide tiles (cheng2020's 96 / 160 / 288-channel latent layers:
@@ -3983,7 +4002,7 @@ static bool small_wgrad_ok(const cai_conv_geom* g, int dtype) {
         return e && *e == '1';
     }();
     const int gran = w64 ? 64 : 32;
-    return !small_wgrad_off() && dtype == CAI_BF16 && W.M <= SW_NW * SW_STEPS * 32 && W.Ng % gran == 0 &&
+    return !small_wgrad_off() && dtype == CAI_BF16 && W.M <= small_wgrad_mmax() && W.Ng % gran == 0 &&
            W.Cq_pad % gran == 0 && (int64_t)W.Ng * W.ncols <= (w64 ? (1 << 20) : (1 << 23));
 }
 
@@ -4316,12 +4335,19 @@ static int run_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int3
         }();
         sa.slab = direct_out ? nullptr : slab;
         const dim3 grid(sa.ncb + ((db && g->transposed) ? 1 : 0), (W.Ng + 63) / 64);
-        if (sa.in_abs)
-            hipLaunchKernelGGL(wgrad_small_kernel<1>, grid, dim3(512), 0, st, sa);
+        const bool lng = W.M > SW_NW * SW_STEPS * 32;
+        if (sa.in_abs && lng)
+            hipLaunchKernelGGL((wgrad_small_kernel<1, true>), grid, dim3(512), 0, st, sa);
+        else if (sa.in_abs)
+            hipLaunchKernelGGL((wgrad_small_kernel<1, false>), grid, dim3(512), 0, st, sa);
+        else if (sa.in_sq && lng)
+            hipLaunchKernelGGL((wgrad_small_kernel<2, true>), grid, dim3(512), 0, st, sa);
         else if (sa.in_sq)
-            hipLaunchKernelGGL(wgrad_small_kernel<2>, grid, dim3(512), 0, st, sa);
+            hipLaunchKernelGGL((wgrad_small_kernel<2, false>), grid, dim3(512), 0, st, sa);
+        else if (lng)
+            hipLaunchKernelGGL((wgrad_small_kernel<0, true>), grid, dim3(512), 0, st, sa);
         else
-            hipLaunchKernelGGL(wgrad_small_kernel<0>, grid, dim3(512), 0, st, sa);
+            hipLaunchKernelGGL((wgrad_small_kernel<0, false>), grid, dim3(512), 0, st, sa);
         CAI_LAUNCH_CHECK("conv_wgrad");
         if (direct_out) return CAI_OK;
         cai_reduce_job J{};
