@@ -19,8 +19,6 @@
 #include "common.hpp"
 #include "reduce_jobs.hpp"
 
-#include <cstdlib>
-
 namespace cai {
 
 // WGRAD job layout: one block per (output row n, slice of input channels q).  The slab row of n is [tap][Cq_pad]
@@ -91,80 +89,9 @@ __device__ __forceinline__ void wgrad_slice_body(const cai_reduce_job& J, int bi
     }
 }
 
-// Row mode: one block per output row n when the row's transpose fits the LDS buffer.  Each split's row is one
-// contiguous run of the slab (ncols floats: 12.8 KB for a 128 x 25-tap row), read by the whole block in 16-byte
-// chunks -- the slice mode's 128-byte pieces of 25 taps x S splits were scattered reads (~4 TB/s over the C2
-// backward's ~400 MB).  Chunk c of the row is thread c % 256's, summed over the splits in split order (4 splits'
-// loads in flight), transposed through LDS and written contiguously as dw[n][q][tap].
-constexpr int WG_ROW_FLOATS = 8192;   // LDS floats of the row-mode transpose (32 KB): Cq_pad * (k*k + 1)
-__host__ __device__ __forceinline__ bool wg_row_mode(int Cq_pad, int k) {
-    return Cq_pad * (k * k + 1) <= WG_ROW_FLOATS && (Cq_pad * k * k) / 4 <= 4 * 256;
-}
-
-__device__ __forceinline__ void wgrad_row_body(const cai_reduce_job& J, int n, float* tr) {
-    const float* __restrict__ ws = static_cast<const float*>(J.p[0]);
-    float* __restrict__ dw = static_cast<float*>(const_cast<void*>(J.p[1]));
-    const int S = J.i[0], Ng = J.i[1], ncols = J.i[2], Cq = J.i[3], Cq_pad = J.i[4], k = J.i[5];
-    const int accumulate = J.i[6];
-    const int kk = k * k, c4 = ncols >> 2;
-    const int64_t slab4 = ((int64_t)Ng * ncols) >> 2;
-    const f32x4* src = reinterpret_cast<const f32x4*>(ws) + (int64_t)n * c4;
-    f32x4 acc[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int tid = threadIdx.x;
-    int sp = 0;
-    for (; sp + 4 <= S; sp += 4) {
-        f32x4 v[4][4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int c = tid + 256 * u;
-                v[j][u] = c < c4 ? src[(int64_t)(sp + j) * slab4 + c] : f32x4{0.f, 0.f, 0.f, 0.f};
-            }
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int u = 0; u < 4; ++u) acc[u] += v[j][u];
-    }
-    for (; sp < S; ++sp)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int c = tid + 256 * u;
-            if (c < c4) acc[u] += src[(int64_t)sp * slab4 + c];
-        }
-    // chunk c = 4 consecutive channels q of tap t (Cq_pad % 4 == 0): tr[q][t], row pitch kk + 1
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int c = tid + 256 * u;
-        if (c < c4) {
-            const int e0 = 4 * c, t = e0 / Cq_pad, q = e0 - t * Cq_pad;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) tr[(q + e) * (kk + 1) + t] = acc[u][e];
-        }
-    }
-    __syncthreads();
-    const int len = Cq * kk;
-    float* d = dw + (int64_t)n * len;
-    for (int i = tid; i < len; i += 256) {
-        const int q = i / kk, t = i - (i / kk) * kk;
-        const float v = tr[q * (kk + 1) + t];
-        d[i] = accumulate ? d[i] + v : v;
-    }
-}
-
-// blocks [0, wblocks): the weight blocks (rows, or (row, channel-slice) pieces); then the bias blocks
+// blocks [0, wblocks): the (row, channel-slice) weight blocks; then the bias blocks
 __device__ __forceinline__ void wgrad_reduce_body(const cai_reduce_job& J, int bid, float* tr) {
     const int Ng = J.i[1], Cq_pad = J.i[4], k = J.i[5];
-    if (J.i[9]) {   // row mode (set by launch_reduce_jobs)
-        if (bid >= Ng) {
-            wgrad_bias_body(J, bid - Ng);
-            return;
-        }
-        wgrad_row_body(J, bid, tr);
-        return;
-    }
     const int cq4 = Cq_pad >> 2, q4 = wg_q4(k * k, cq4);
     const int wblocks = Ng * ((cq4 + q4 - 1) / q4);
     if (bid >= wblocks) {
@@ -177,24 +104,6 @@ __device__ __forceinline__ void wgrad_reduce_body(const cai_reduce_job& J, int b
 int wgrad_job_blocks(int Ng, int Cq_pad, int k, int nbias_blocks) {
     const int cq4 = Cq_pad >> 2, q4 = wg_q4(k * k, cq4);
     return Ng * ((cq4 + q4 - 1) / q4) + nbias_blocks;
-}
-
-// A/B knob CAI_REDUCE_ROWS=0: the (row, channel-slice) form for every WGRAD job
-static bool reduce_rows_on() {
-    static const bool on = [] {
-        const char* e = std::getenv("CAI_REDUCE_ROWS");
-        return !(e && *e == '0');
-    }();
-    return on;
-}
-
-// the form a WGRAD job runs in (i[9]) and its block count, whatever the producer filled in
-static cai_reduce_job wgrad_job_form(cai_reduce_job J) {
-    const int Ng = J.i[1], Cq_pad = J.i[4], k = J.i[5];
-    const int nbias_blocks = J.p[2] ? (J.i[8] + 255) / 256 : 0;
-    J.i[9] = reduce_rows_on() && wg_row_mode(Cq_pad, k) ? 1 : 0;
-    J.nblocks = J.i[9] ? Ng + nbias_blocks : wgrad_job_blocks(Ng, Cq_pad, k, nbias_blocks);
-    return J;
 }
 
 __device__ __forceinline__ void gdn_reduce_body(const cai_reduce_job& J, int bid, f32x4 (*red)[17]) {
@@ -321,14 +230,10 @@ __device__ __forceinline__ void edge_reduce_body(const cai_reduce_job& J, int bi
 }
 
 __global__ __launch_bounds__(256) void reduce_jobs_kernel(const ReduceBatch B) {
-    // one body per block: the bodies' LDS arrays alias one buffer
-    __shared__ __attribute__((aligned(16))) float lds[WG_ROW_FLOATS];
-    static_assert(WG_TR_FLOATS <= WG_ROW_FLOATS && 16 * 17 * 4 <= WG_ROW_FLOATS && 16 * 16 + 16 <= WG_ROW_FLOATS,
-                  "reduce_jobs LDS");
-    float* const tr = lds;
-    f32x4 (*red)[17] = reinterpret_cast<f32x4 (*)[17]>(lds);
-    float (*ered)[16] = reinterpret_cast<float (*)[16]>(lds);
-    float* const etot = lds + 16 * 16;
+    __shared__ f32x4 red[16][17];
+    __shared__ __attribute__((aligned(16))) float tr[WG_TR_FLOATS];
+    __shared__ float ered[16][16];
+    __shared__ float etot[16];
     // the job owning this block (block-uniform linear scan over <= CAI_REDUCE_BATCH entries)
     const int b = blockIdx.x;
     int j = 0;
@@ -385,9 +290,9 @@ int launch_reduce_jobs(const cai_reduce_job* jobs, int n, hipStream_t st) {
             CAI_CHECK_ARG(J.kind == CAI_JOB_WGRAD || J.kind == CAI_JOB_GDN || J.kind == CAI_JOB_EDGE,
                           "reduce_jobs: unknown job kind %d", J.kind);
             if (shares_dest(B, J)) break;
-            B.jobs[B.n] = J.kind == CAI_JOB_WGRAD ? wgrad_job_form(J) : J;
+            B.jobs[B.n] = J;
             B.start[B.n] = blocks;
-            blocks += B.jobs[B.n].nblocks;
+            blocks += J.nblocks;
             ++B.n;
         }
         if (B.n == 0) continue;
