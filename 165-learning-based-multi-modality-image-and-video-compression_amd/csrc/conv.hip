@@ -1169,6 +1169,9 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvArgs a, int
 #ifndef CAI_HALO_PH_PP
 #define CAI_HALO_PH_PP 0
 #endif
+#ifndef CAI_HALO_PH_PP_PRIO
+#define CAI_HALO_PH_PP_PRIO 1
+#endif
 
 
 // HALF: the 256-thread form (4 waves, 8 x 16 tiles, two workgroups per CU): the two waves that share a SIMD
@@ -1424,7 +1427,7 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
                 }
                 u32x4 na[TM], nb[TN];
                 read_pp(t + 1 == NST ? 0 : t + 1, t + 1 == NST ? pbn : pb, na, nb);
-                __builtin_amdgcn_s_setprio(1);
+                if (CAI_HALO_PH_PP_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
                 for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
@@ -1437,7 +1440,7 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
                     __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                 }
                 __builtin_amdgcn_sched_group_barrier(0x008, TM * TN - (TM + TN), 0);
-                __builtin_amdgcn_s_setprio(0);
+                if (CAI_HALO_PH_PP_PRIO) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
                 for (int tm = 0; tm < TM; ++tm) fa[tm] = na[tm];
 #pragma unroll
