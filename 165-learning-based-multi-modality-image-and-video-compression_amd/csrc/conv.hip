@@ -1205,10 +1205,13 @@ struct HaloPhCfg {
     // DMA (two per lane and step, PP_D steps ahead) into an NSTB-deep ring (NSTB >= PP_D + 1: the lagging group
     // still reads the stage a DMA would overwrite otherwise); the footprint is double-buffered, the next chunk's
     // stored at step NST - 3 (the lagging group's stores retire one barrier before the leading group's first read).
+    // PP2 (CAI_HALO_PH_PP=2): both groups issue their own rows' DMAs (one per lane and step, as the lockstep form),
+    // PP_D = 4 steps ahead (the lagging group retires its half two steps after issue) into a 6 / 8-deep ring
     static constexpr bool PP = CAI_HALO_PH_PP && DPS == 1 && !HALF;
-    static constexpr int PP_D = 3;
+    static constexpr bool PP2 = PP && CAI_HALO_PH_PP == 2;
+    static constexpr int PP_D = PP2 ? 4 : 3;
     static constexpr bool PAIRS = CAI_HALO_PH_PAIRS && DPS == 1 && !HALF && NST % 2 == 0 && !PP;
-    static constexpr int NSTB = PP ? (NST % 6 == 0 ? 6 : 4)
+    static constexpr int NSTB = PP ? (NST % 6 == 0 ? 6 : (PP2 ? 8 : 4))
                                    : PAIRS ? (NST % 6 == 0 ? 6 : 4)
                                            : ((CAI_HALO_PH_NSTB6 && NST % 6 == 0) ? 6 : (NST % 3 == 0 ? 3 : 2));
     static constexpr int NPATCH = PP ? 2 : 1;
@@ -1226,6 +1229,17 @@ struct HaloPhCfg {
 __host__ __device__ constexpr int halo_younger_pp(int t, int npi) {
     return 2 + ((t >= 2 && t - 2 < npi) ? 1 : 0) + ((t >= 1 && t - 1 < npi) ? 1 : 0);
 }
+__host__ __device__ constexpr int halo_cells_in(int lo, int hi, int npi) {   // cells issued at steps lo .. hi
+    int n = 0;
+    for (int j = lo; j <= hi; ++j) n += (j >= 0 && j < npi) ? 1 : 0;
+    return n;
+}
+// PP2, leading group at step t: its DMA of step t + 1 (issued at step t - 3); younger: its DMAs of steps t - 2,
+// t - 1 and the cells of steps t - 3 .. t - 1
+__host__ __device__ constexpr int halo_younger_pp2a(int t, int npi) { return 2 + halo_cells_in(t - 3, t - 1, npi); }
+// PP2, lagging group at step t: its DMA of step t + 2 (the leading group reads it after the next barrier; issued
+// at step t - 2); younger: its DMA of step t - 1 and the cells of steps t - 2, t - 1
+__host__ __device__ constexpr int halo_younger_pp2b(int t, int npi) { return 1 + halo_cells_in(t - 2, t - 1, npi); }
 
 // PAIRS: the loads issued after step t + 2's weight DMA that an even step t's wait leaves in flight -- the DMAs of
 // the even steps after t' = t + 2 - NSTB (two each), the footprint cells issued at steps [t', t - 1] (j < NPI)
@@ -1397,7 +1411,10 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
         if (nc > 0) {
 #pragma unroll
             for (int i = 0; i < NPI; ++i) load_cell(0, i);
-            if (grpA) {
+            if constexpr (H::PP2) {
+#pragma unroll
+                for (int t = 0; t < D; ++t) issue_b(0, t);
+            } else if (grpA) {
 #pragma unroll
                 for (int t = 0; t < D; ++t) issue_pp(0, t);
             }
@@ -1412,14 +1429,30 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
             const int pb = (ci & 1) * H::PATCH, pbn = pb ^ H::PATCH;
 #pragma unroll
             for (int t = 0; t < NST; ++t) {
-                if (grpA) wait_vmcnt_n(halo_younger_pp(t, NPI));   // this group's DMA of step t + 1 has landed
+                if constexpr (H::PP2) {
+                    if (grpA)
+                        wait_vmcnt_n(halo_younger_pp2a(t, NPI));
+                    else
+                        wait_vmcnt_n(halo_younger_pp2b(t, NPI));
+                } else if (grpA) {
+                    wait_vmcnt_n(halo_younger_pp(t, NPI));   // this group's DMA of step t + 1 has landed
+                }
                 wait_lgkmcnt0();
                 __builtin_amdgcn_s_barrier();
                 __builtin_amdgcn_sched_barrier(0);
-                if (grpA) issue_pp(ci, t + D);
+                if constexpr (H::PP2) {
+                    if (t + D < NST)
+                        issue_b(ci, t + D);
+                    else
+                        issue_b(ci + 1, t + D - NST);
+                } else if (grpA) {
+                    issue_pp(ci, t + D);
+                }
                 if (t < NPI) load_cell(ci + 1, t);
                 if (t == NST - 3) {   // the next chunk's footprint into the other buffer
-                    if (grpA)
+                    if constexpr (H::PP2)
+                        wait_vmcnt_n(t - NPI + 1);         // the DMAs of steps NPI .. t came after the last cell
+                    else if (grpA)
                         wait_vmcnt_n(2 * (t - NPI + 1));   // the DMAs of steps NPI .. t came after the last cell
                     else
                         wait_vmcnt<0>();
