@@ -1961,7 +1961,8 @@ struct PackArgs {
     int items_pp;          // pack_many: 8-element items per phase (Npad * Kp / 8)
     int64_t row_begin;     // pack_many: first global row of this descriptor (row-mode conv descriptors)
     int64_t rows_total;    // pack_many: rows of the whole table (the same in every descriptor)
-    int rowmode;           // 1: packed one output row (all phases) per block from an LDS copy of its sources
+    int rowmode;           // 1: packed output rows (all phases) per block from an LDS copy of their sources
+    int rpu;               // row mode: consecutive rows per work unit (as many as the LDS copy holds, <= 8)
     int edge;              // 1: edge-layer MFMA fragments (edge_frag.hpp), one item per fragment
     EdgeFragSpec es;
     int gdn;               // 1: GDN reparametrisation (w = gamma_raw, mask = beta_raw, out = gamma_op, D1 = C)
@@ -2004,6 +2005,10 @@ __global__ void pack_weight_kernel(const PackArgs a) {
 #define CAI_PACK_ROW_MAX 6144   // 24 KB: A/B 12288 / 6144 / 4096 / item-only -> 47 / 33 / 35 / 47 us (C2)
 #endif
 constexpr int PACK_ROW_MAX = CAI_PACK_ROW_MAX;   // source floats per row that fit the LDS copy
+#ifndef CAI_PACK_ROWS_PER_UNIT
+#define CAI_PACK_ROWS_PER_UNIT 8   // A/B: 1 = one row per work unit (the round-3 form)
+#endif
+constexpr int PACK_ROWS_PER_UNIT = CAI_PACK_ROWS_PER_UNIT;
 
 template <typename T>
 __device__ __forceinline__ void pack_item(const PackArgs* __restrict__ descs, int n, int64_t gi) {
@@ -2083,29 +2088,33 @@ __device__ __forceinline__ void pack_item(const PackArgs* __restrict__ descs, in
     }
 }
 
-// TO[ph * 64 + t]: the source tap (kernel offset kh * k + kw) of packed tap t of phase ph, filled once per row
-// (k <= 7: <= 49 taps) so the packing loop reads S without an integer division per element
+// TO[ph * 64 + t]: the source tap (kernel offset kh * k + kw) of packed tap t of phase ph, filled once per unit
+// (k <= 7: <= 49 taps) so the packing loop reads S without an integer division per element.  A unit is `cnt`
+// consecutive output rows n0 .. n0 + cnt - 1 (a.rpu of them): their sources go to LDS in one round of loads and
+// one barrier -- a unit per row left cheng2020's 1728-float rows latency-bound (267 us per C4 step).
 template <typename T>
-__device__ __forceinline__ void pack_row(const PackArgs& a, int n, float* S, int* TO) {
+__device__ __forceinline__ void pack_rows(const PackArgs& a, int n0, int cnt, float* S, int* TO) {
     const int KK = a.k * a.k;
     const int nsrc = a.Creal * KK;
-    if (n < a.Nreal) {
-        // PACK_LD independent loads in flight per thread (a 128 x 25-tap row is 3200 floats: one round of 16 per
-        // thread instead of four dependent rounds of 4)
+    const int tot = cnt * nsrc;
+    {
+        // PACK_LD independent loads in flight per thread
         constexpr int PACK_LD = 16;
-        for (int i0 = threadIdx.x; i0 < nsrc; i0 += PACK_LD * blockDim.x) {
+        for (int i0 = threadIdx.x; i0 < tot; i0 += PACK_LD * blockDim.x) {
             float v[PACK_LD];
 #pragma unroll
             for (int j = 0; j < PACK_LD; ++j) {
-                const int i = min(i0 + j * (int)blockDim.x, nsrc - 1);
-                const int c = i / KK, tap = i - c * KK;
-                const int64_t src = a.n_is_d0 ? (int64_t)n * a.D1 * KK + i : ((int64_t)c * a.D1 + n) * KK + tap;
-                v[j] = a.w[src];
-                if (a.mask) v[j] *= a.mask[src];
+                const int i = min(i0 + j * (int)blockDim.x, tot - 1);
+                const int r = i / nsrc, ii = i - r * nsrc;
+                const int n = n0 + r;
+                const int c = ii / KK, tap = ii - c * KK;
+                const int64_t src = a.n_is_d0 ? (int64_t)n * a.D1 * KK + ii : ((int64_t)c * a.D1 + n) * KK + tap;
+                v[j] = n < a.Nreal ? a.w[src] : 0.f;
+                if (a.mask && n < a.Nreal) v[j] *= a.mask[src];
             }
 #pragma unroll
             for (int j = 0; j < PACK_LD; ++j)
-                if (i0 + j * (int)blockDim.x < nsrc) S[i0 + j * blockDim.x] = v[j];
+                if (i0 + j * (int)blockDim.x < tot) S[i0 + j * blockDim.x] = v[j];
         }
     }
     for (int idx = threadIdx.x; idx < a.nphase * 64; idx += blockDim.x) {
@@ -2121,16 +2130,19 @@ __device__ __forceinline__ void pack_row(const PackArgs& a, int n, float* S, int
     for (int ph = 0; ph < a.nphase; ++ph) {
         const int ntaps = ph == 0 ? a.ntaps[0] : (ph == 1 ? a.ntaps[1] : (ph == 2 ? a.ntaps[2] : a.ntaps[3]));
         const int64_t off = ph == 0 ? a.off[0] : (ph == 1 ? a.off[1] : (ph == 2 ? a.off[2] : a.off[3]));
-        T* out = reinterpret_cast<T*>(a.out) + off + (int64_t)n * a.Kp;
         const int* TOp = TO + ph * 64;
-        for (int ch = threadIdx.x; ch < nch; ch += blockDim.x) {
+        for (int idx = threadIdx.x; idx < cnt * nch; idx += blockDim.x) {
+            const int r = idx / nch, ch = idx - r * nch;
+            const int n = n0 + r;
+            T* out = reinterpret_cast<T*>(a.out) + off + (int64_t)n * a.Kp;
+            const float* Sr = S + r * nsrc;
             const int e0 = ch * 8;
             int t = e0 / a.Cpad, c = e0 - t * a.Cpad;   // fp32 (Cpad % 4 == 0): the 8 may span two taps
             float v[8];
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 float x = 0.f;
-                if (n < a.Nreal && c < a.Creal && t < ntaps) x = S[c * KK + TOp[t]];
+                if (n < a.Nreal && c < a.Creal && t < ntaps) x = Sr[c * KK + TOp[t]];
                 v[e] = x;
                 if (++c == a.Cpad) { c = 0; ++t; }
             }
@@ -2145,7 +2157,7 @@ __device__ __forceinline__ void pack_row(const PackArgs& a, int n, float* S, int
             }
         }
     }
-    __syncthreads();   // the next row reuses S
+    __syncthreads();   // the next unit reuses S
 }
 
 template <typename T>
@@ -2162,7 +2174,9 @@ __global__ __launch_bounds__(256) void pack_many_kernel(const PackArgs* __restri
                 const int mid = (lo + hi + 1) >> 1;
                 if (descs[mid].row_begin <= u) lo = mid; else hi = mid - 1;
             }
-            pack_row<T>(descs[lo], (int)(u - descs[lo].row_begin), S, TO);
+            const PackArgs& d = descs[lo];
+            const int n0 = (int)(u - d.row_begin) * d.rpu;
+            pack_rows<T>(d, n0, min(d.rpu, d.Npad - n0), S, TO);
         } else {
             const int64_t gi = (u - R) * 256 + threadIdx.x;
             if (gi < I) pack_item<T>(descs, n, gi);
@@ -4158,10 +4172,12 @@ int64_t cai_conv_pack_finalize(void* descs, int32_t n) {
     for (int i = 0; i < n; ++i) {
         d[i].items_pp = (int)((int64_t)d[i].Npad * d[i].Kp / 8);
         d[i].rowmode = !d[i].edge && !d[i].gdn && d[i].Creal * d[i].k * d[i].k <= PACK_ROW_MAX;
+        d[i].rpu = d[i].rowmode ? std::max(1, std::min(PACK_ROWS_PER_UNIT, PACK_ROW_MAX / (d[i].Creal * d[i].k * d[i].k)))
+                                : 1;
         d[i].item_begin = items;
         d[i].row_begin = rows;
         if (d[i].rowmode)
-            rows += d[i].Npad;
+            rows += (d[i].Npad + d[i].rpu - 1) / d[i].rpu;
         else
             items += (int64_t)d[i].items_pp * d[i].nphase;
     }

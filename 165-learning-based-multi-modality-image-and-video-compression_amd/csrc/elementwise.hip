@@ -13,6 +13,7 @@
 #include "common.hpp"
 
 #include <algorithm>
+#include <initializer_list>
 
 namespace cai {
 
@@ -107,6 +108,53 @@ __global__ void gate_bwd_kernel(const T* __restrict__ a, const T* __restrict__ b
         da[o] = from_f32<T>(relu_a && !(av > 0.f) ? 0.f : gv * s);
         db[o] = from_f32<T>(gv * av * s * (1.f - s));
     }
+}
+
+// bf16 forms with one 8-channel chunk (16 bytes) per thread: C % 8 == 0, ld % 8 == 0, 16-byte aligned rows
+__global__ void gate_fwd_vec_kernel(const bf16* __restrict__ a, const bf16* __restrict__ b, const bf16* __restrict__ x,
+                                    bf16* __restrict__ y, int ld, int64_t npix, int nch) {
+    const int64_t total = npix * nch;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t p = i / nch;
+        const int64_t o = p * ld + (int)(i - p * nch) * 8;
+        const bf16x8 va = *reinterpret_cast<const bf16x8*>(a + o), vb = *reinterpret_cast<const bf16x8*>(b + o),
+                     vx = *reinterpret_cast<const bf16x8*>(x + o);
+        bf16x8 vy;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) vy[e] = (bf16)((float)va[e] * sigmoidf_((float)vb[e]) + (float)vx[e]);
+        *reinterpret_cast<bf16x8*>(y + o) = vy;
+    }
+}
+
+__global__ void gate_bwd_vec_kernel(const bf16* __restrict__ a, const bf16* __restrict__ b, const bf16* __restrict__ g,
+                                    int gld, bf16* __restrict__ da, bf16* __restrict__ db, int ld, int64_t npix, int nch,
+                                    int relu_a) {
+    const int64_t total = npix * nch;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t p = i / nch;
+        const int c0 = (int)(i - p * nch) * 8;
+        const int64_t o = p * ld + c0;
+        const bf16x8 va = *reinterpret_cast<const bf16x8*>(a + o), vb = *reinterpret_cast<const bf16x8*>(b + o),
+                     vg = *reinterpret_cast<const bf16x8*>(g + p * gld + c0);
+        bf16x8 oa, ob;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float sg = sigmoidf_((float)vb[e]), gv = (float)vg[e], av = (float)va[e];
+            oa[e] = (bf16)(relu_a && !(av > 0.f) ? 0.f : gv * sg);
+            ob[e] = (bf16)(gv * av * sg * (1.f - sg));
+        }
+        *reinterpret_cast<bf16x8*>(da + o) = oa;
+        *reinterpret_cast<bf16x8*>(db + o) = ob;
+    }
+}
+
+__host__ __forceinline__ bool vec8_ok(int C, std::initializer_list<int> lds, std::initializer_list<const void*> ptrs) {
+    if (C % 8) return false;
+    for (int l : lds)
+        if (l % 8) return false;
+    for (const void* q : ptrs)
+        if (reinterpret_cast<uintptr_t>(q) & 15) return false;
+    return true;
 }
 
 // Pixel shuffle between x [B][H][W][C*r*r] (channel n = c*r*r + i*r + j) and
@@ -287,7 +335,10 @@ int cai_gate_fwd(int dtype, const void* a, const void* b, const void* x, void* y
     const int64_t n = npix * C;
     if (n == 0) return CAI_OK;
     hipStream_t st = as_stream(stream);
-    if (dtype == CAI_BF16)
+    if (dtype == CAI_BF16 && vec8_ok(C, {ld}, {a, b, x, y}))
+        hipLaunchKernelGGL(gate_fwd_vec_kernel, dim3(ew_grid2(n / 8)), dim3(256), 0, st, (const bf16*)a, (const bf16*)b,
+                           (const bf16*)x, (bf16*)y, ld, npix, C / 8);
+    else if (dtype == CAI_BF16)
         hipLaunchKernelGGL(gate_fwd_kernel<bf16>, dim3(ew_grid2(n)), dim3(256), 0, st, (const bf16*)a, (const bf16*)b,
                            (const bf16*)x, (bf16*)y, ld, (int)npix, C);
     else
@@ -304,7 +355,10 @@ int cai_gate_bwd(int dtype, const void* a, const void* b, const void* g, int32_t
     const int64_t n = npix * C;
     if (n == 0) return CAI_OK;
     hipStream_t st = as_stream(stream);
-    if (dtype == CAI_BF16)
+    if (dtype == CAI_BF16 && vec8_ok(C, {ld, g_ld}, {a, b, g, da, db}))
+        hipLaunchKernelGGL(gate_bwd_vec_kernel, dim3(ew_grid2(n / 8)), dim3(256), 0, st, (const bf16*)a,
+                           (const bf16*)b, (const bf16*)g, g_ld, (bf16*)da, (bf16*)db, ld, npix, C / 8, (int)relu_a);
+    else if (dtype == CAI_BF16)
         hipLaunchKernelGGL(gate_bwd_kernel<bf16>, dim3(ew_grid2(n)), dim3(256), 0, st, (const bf16*)a, (const bf16*)b,
                            (const bf16*)g, g_ld, (bf16*)da, (bf16*)db, ld, (int)npix, C, (int)relu_a);
     else

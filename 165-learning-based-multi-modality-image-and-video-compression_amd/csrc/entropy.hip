@@ -704,6 +704,30 @@ __global__ void act_bwd_kernel(int mode, float prm, const void* __restrict__ y, 
     }
 }
 
+// bf16, C % 8 == 0, 16-byte rows: one 8-channel chunk per thread (the element form above is a scalar load /
+// store per element and an int64 division: 1.9 TB/s on cheng2020's 128 x 128 x 192 maps)
+__global__ void act_bwd_vec_kernel(int mode, float prm, const bf16* __restrict__ y, int yld, const bf16* __restrict__ g,
+                                   int gld, bf16* __restrict__ out, int old, int64_t npix, int nch) {
+    const int64_t total = npix * nch;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t p = i / nch;
+        const int c0 = (int)(i - p * nch) * 8;
+        const bf16x8 yv = *reinterpret_cast<const bf16x8*>(y + p * yld + c0);
+        const bf16x8 gv = *reinterpret_cast<const bf16x8*>(g + p * gld + c0);
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float yy = (float)yv[e];
+            float m = 1.f;
+            if (mode == CAI_MASK_POS) m = yy > 0.f ? 1.f : 0.f;
+            else if (mode == CAI_MASK_LEAKY) m = yy > 0.f ? 1.f : prm;
+            else if (mode == CAI_MASK_SIGN) m = yy > 0.f ? 1.f : (yy < 0.f ? -1.f : 0.f);
+            o[e] = (bf16)((float)gv[e] * m);
+        }
+        *reinterpret_cast<bf16x8*>(out + p * old + c0) = o;
+    }
+}
+
 __global__ void cast_kernel(const void* __restrict__ x, int xdt, void* __restrict__ y, int ydt, int64_t n) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         st_any(y, ydt, i, ld_any(x, xdt, i));
@@ -1073,8 +1097,17 @@ int cai_act_bwd(int mask_mode, float param, const void* y, int32_t y_ld, const v
                 int32_t out_ld, int64_t npix, int32_t C, int dtype, void* stream) {
     const int64_t n = npix * C;
     if (n == 0) return CAI_OK;
-    hipLaunchKernelGGL(act_bwd_kernel, dim3(ew_grid(n)), dim3(256), 0, as_stream(stream), mask_mode, param, y, y_ld, g,
-                       g_ld, out, out_ld, n, C, dtype);
+    const bool a16 = ((reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(out)) &
+                      15) == 0;
+    if (dtype == CAI_BF16 && C % 8 == 0 && y_ld % 8 == 0 && g_ld % 8 == 0 && out_ld % 8 == 0 && a16) {
+        const int nch = C / 8;
+        hipLaunchKernelGGL(act_bwd_vec_kernel, dim3(ew_grid(npix * nch)), dim3(256), 0, as_stream(stream), mask_mode,
+                           param, static_cast<const bf16*>(y), y_ld, static_cast<const bf16*>(g), g_ld,
+                           static_cast<bf16*>(out), out_ld, npix, nch);
+    } else {
+        hipLaunchKernelGGL(act_bwd_kernel, dim3(ew_grid(n)), dim3(256), 0, as_stream(stream), mask_mode, param, y, y_ld,
+                           g, g_ld, out, out_ld, n, C, dtype);
+    }
     CAI_LAUNCH_CHECK("act_bwd");
     return CAI_OK;
 }
