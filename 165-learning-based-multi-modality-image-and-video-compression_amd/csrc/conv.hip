@@ -1169,6 +1169,9 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvArgs a, int
 #ifndef CAI_HALO_PH_PP
 #define CAI_HALO_PH_PP 0
 #endif
+#ifndef CAI_PH_PROBE
+#define CAI_PH_PROBE 0
+#endif
 #ifndef CAI_HALO_PH_PP_PRIO
 #define CAI_HALO_PH_PP_PRIO 1
 #endif
@@ -1364,6 +1367,11 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+#if CAI_PH_PROBE
+    // diagnostics (-DCAI_PH_PROBE=1, printf from sampled blocks): s_memtime totals per wave of the prologue, the
+    // counted vmcnt waits, the lgkmcnt waits, the barrier waits and the step bodies (lockstep form)
+    unsigned long long pr_t0 = __builtin_amdgcn_s_memtime(), pr_vm = 0, pr_lg = 0, pr_bar = 0, pr_body = 0, pr_pro = 0;
+#endif
     u32x4 fa[TM], fb[TN];
     if constexpr (H::PP) {
         constexpr int D = H::PP_D;
@@ -1558,13 +1566,33 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
         __builtin_amdgcn_s_barrier();
         read_frags(0, fa, fb);
     }
+#if CAI_PH_PROBE
+    unsigned long long pr_s = __builtin_amdgcn_s_memtime();
+    pr_pro = pr_s - pr_t0;
+#endif
     for (int ci = 0; ci < nc; ++ci) {
 #pragma unroll
         for (int t = 0; t < NST; ++t) {
+#if CAI_PH_PROBE
+            const unsigned long long q0 = __builtin_amdgcn_s_memtime();
+            pr_body += q0 - pr_s;
+#endif
             // halo_younger counts one DMA per younger step; DPS DMAs per step add (DPS - 1) per younger tap
             wait_vmcnt_n(halo_younger(t, NSTB, NPI) + (DPS - 1) * (NSTB - 2));
+#if CAI_PH_PROBE
+            const unsigned long long q1 = __builtin_amdgcn_s_memtime();
+#endif
             wait_lgkmcnt0();
+#if CAI_PH_PROBE
+            const unsigned long long q2 = __builtin_amdgcn_s_memtime();
+#endif
             __builtin_amdgcn_s_barrier();
+#if CAI_PH_PROBE
+            pr_s = __builtin_amdgcn_s_memtime();
+            pr_vm += q1 - q0;
+            pr_lg += q2 - q1;
+            pr_bar += pr_s - q2;
+#endif
             if (t == NST - 1) {
                 store_patch();
                 wait_lgkmcnt0();
@@ -1598,6 +1626,9 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
             __builtin_amdgcn_sched_barrier(0);
         }
     }
+#if CAI_PH_PROBE
+    pr_body += __builtin_amdgcn_s_memtime() - pr_s;
+#endif
     }   // !PAIRS
     wait_vmcnt<0>();
     asm volatile("" ::"v"(fence_[0]), "v"(fence_[1]), "v"(fence_[2]), "v"(fence_[3]));
@@ -1613,6 +1644,14 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
     else
         conv_epilogue_rows<bf16, BM, BN, WM, WN, NT>(a, P, plane, n0, reinterpret_cast<float*>(smem), acc, rowm,
                                                      ph * a.ksplit + split);
+#if CAI_PH_PROBE
+    if constexpr (!H::PP && !H::PAIRS && !GATHER && BN == 128) {
+        if ((blockIdx.x & 127) == 5 && (threadIdx.x & 63) == 0)
+            printf("PHPROBE ph=%d wave=%d nc=%d total=%llu pro=%llu vm=%llu lg=%llu bar=%llu body=%llu\n", ph,
+                   (int)(threadIdx.x >> 6), nc, __builtin_amdgcn_s_memtime() - pr_t0, pr_pro, pr_vm, pr_lg, pr_bar,
+                   pr_body);
+    }
+#endif
 }
 
 // grid: x = 4 x the output tiles of one phase, z = split (the split-K slab index of the epilogue).  Block
