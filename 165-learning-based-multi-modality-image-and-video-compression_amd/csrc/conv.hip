@@ -1630,9 +1630,18 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
     pr_body += __builtin_amdgcn_s_memtime() - pr_s;
 #endif
     }   // !PAIRS
+#if CAI_PH_PROBE
+    const unsigned long long pe0 = __builtin_amdgcn_s_memtime();
+#endif
     wait_vmcnt<0>();
     asm volatile("" ::"v"(fence_[0]), "v"(fence_[1]), "v"(fence_[2]), "v"(fence_[3]));
+#if CAI_PH_PROBE
+    const unsigned long long pe1 = __builtin_amdgcn_s_memtime();
+#endif
     __syncthreads();
+#if CAI_PH_PROBE
+    const unsigned long long pe2 = __builtin_amdgcn_s_memtime();
+#endif
     const int plane = P.OHg * P.OWg;
     auto rowm = [=](int row) {
         const int oy = ty0 + row / H::TW, ox = tx0 + row % H::TW;
@@ -1646,10 +1655,13 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
                                                      ph * a.ksplit + split);
 #if CAI_PH_PROBE
     if constexpr (!H::PP && !H::PAIRS && !GATHER && BN == 128) {
+        const unsigned long long pe3 = __builtin_amdgcn_s_memtime();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned long long pe4 = __builtin_amdgcn_s_memtime();
         if ((blockIdx.x & 127) == 5 && (threadIdx.x & 63) == 0)
-            printf("PHPROBE ph=%d wave=%d nc=%d total=%llu pro=%llu vm=%llu lg=%llu bar=%llu body=%llu\n", ph,
-                   (int)(threadIdx.x >> 6), nc, __builtin_amdgcn_s_memtime() - pr_t0, pr_pro, pr_vm, pr_lg, pr_bar,
-                   pr_body);
+            printf("PHPROBE ph=%d wave=%d nc=%d total=%llu pro=%llu vm=%llu lg=%llu bar=%llu body=%llu ewait=%llu "
+                   "esync=%llu epi=%llu edrain=%llu\n", ph, (int)(threadIdx.x >> 6), nc, pe3 - pr_t0, pr_pro, pr_vm,
+                   pr_lg, pr_bar, pr_body, pe1 - pe0, pe2 - pe1, pe3 - pe2, pe4 - pe3);
     }
 #endif
 }
