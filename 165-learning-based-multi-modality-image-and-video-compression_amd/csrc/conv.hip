@@ -251,6 +251,9 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvArgs& a, const Phas
     }
 }
 
+#ifndef CAI_EPI_T_LDS
+#define CAI_EPI_T_LDS 0
+#endif
 // Epilogue for TRANSPOSED accumulators (weights as the MFMA's A operand): lane (i16, g_) of tile (tm, tn)
 // holds output channels wn*WTN + tn*16 + 4*g_ + 0..3 of tile row wm*WTM + tm*16 + i16, so the common cases
 // store straight from registers: split-K partials as 16-byte fp32 stores into the slab, bf16 outputs
@@ -287,7 +290,9 @@ __device__ __forceinline__ void conv_epilogue_rows_t(const ConvArgs& a, const Ph
         return;
     }
     // (the mask variant only in the NOLDS tiles: in the 128-channel halo kernels its registers spill the loop)
-    if (NOLDS ? epi_t_direct(a) : (a.y_vec && a.y_dtype == CAI_BF16 && !a.mask_mode && (a.Cout & 3) == 0)) {
+    // A/B -DCAI_EPI_T_LDS=1: the LDS-staged form (16-byte stores of whole pixel rows) for the 128-channel tiles too
+    if (NOLDS ? epi_t_direct(a)
+              : (!CAI_EPI_T_LDS && a.y_vec && a.y_dtype == CAI_BF16 && !a.mask_mode && (a.Cout & 3) == 0)) {
         f32x4 bv[TN];
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn) {
