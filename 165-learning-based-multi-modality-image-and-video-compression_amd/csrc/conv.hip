@@ -124,12 +124,15 @@ __device__ __forceinline__ void out_pixel(const ConvArgs& a, const PhaseDesc& P,
     ox = P.ox0 + a.out_step * (r - j * P.OWg);
 }
 
-template <typename T>
+// EXTRA = false: the caller has checked that there is no residual and no mask (no loads at all: a load here sits
+// behind the earlier iterations' stores on the shared vmcnt, and its wait serialized a whole epilogue's stores --
+// 38 % of the phase kernel's block time)
+template <typename T, bool EXTRA = true>
 __device__ __forceinline__ void store_out_chunk(const ConvArgs& a, const PhaseDesc& P, int plane, int m, int n,
                                                 float (&v)[8], int VO) {
     int b, oy, ox;
     out_pixel<T>(a, P, plane, m, b, oy, ox);
-    if (a.res) {
+    if (EXTRA && a.res) {
         const int64_t px = ((int64_t)b * a.out_h + oy) * a.out_w + ox;
         const bf16* R = a.res + px * a.res_ld + n;
         const bf16* R2 = a.res2 ? a.res2 + px * a.res2_ld + n : nullptr;
@@ -137,7 +140,7 @@ __device__ __forceinline__ void store_out_chunk(const ConvArgs& a, const PhaseDe
         for (int e = 0; e < 8; ++e)
             if (e < VO) v[e] = apply_act(v[e] + (float)R[e] + (R2 ? (float)R2[e] : 0.f), a.act, a.act_param);
     }
-    if (a.mask_mode) {
+    if (EXTRA && a.mask_mode) {
         const T* AUX = reinterpret_cast<const T*>(a.aux);
         const int64_t pa = (((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.aux_ld + n;
 #pragma unroll
@@ -229,18 +232,24 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvArgs& a, const Phas
     if (a.y_vec) {
         const int VO = a.y_dtype == CAI_BF16 ? 8 : 4;
         const int cpr = BN / VO;
-        for (int id = tid; id < BM * cpr; id += NTH) {
-            const int row = id / cpr, cc = id - (id / cpr) * cpr;
-            const int m = rowm(row), n = n0 + cc * VO;
-            if (m < 0 || n >= a.Cout) continue;
-            float v[8];
-            const f32x4 lo = *reinterpret_cast<const f32x4*>(E + row * ES + cc * VO);
-            f32x4 hi = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (VO == 8) hi = *reinterpret_cast<const f32x4*>(E + row * ES + cc * VO + 4);
-            v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
-            v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
-            store_out_chunk<T>(a, P, plane, m, n, v, VO);
-        }
+        auto run = [&](auto extra) {
+            for (int id = tid; id < BM * cpr; id += NTH) {
+                const int row = id / cpr, cc = id - (id / cpr) * cpr;
+                const int m = rowm(row), n = n0 + cc * VO;
+                if (m < 0 || n >= a.Cout) continue;
+                float v[8];
+                const f32x4 lo = *reinterpret_cast<const f32x4*>(E + row * ES + cc * VO);
+                f32x4 hi = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (VO == 8) hi = *reinterpret_cast<const f32x4*>(E + row * ES + cc * VO + 4);
+                v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+                v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+                store_out_chunk<T, decltype(extra)::value>(a, P, plane, m, n, v, VO);
+            }
+        };
+        if (a.res || a.mask_mode)
+            run(std::true_type{});
+        else
+            run(std::false_type{});
     } else {
         for (int id = tid; id < BM * BN; id += NTH) {
             const int col = id / BM, row = id - (id / BM) * BM;
@@ -299,6 +308,45 @@ __device__ __forceinline__ void conv_epilogue_rows_t(const ConvArgs& a, const Ph
             const int n = n0 + wn * WTN + tn * 16 + 4 * g_;
 #pragma unroll
             for (int r = 0; r < 4; ++r) bv[tn][r] = (a.bias && n + r < a.Cout) ? a.bias[n + r] : 0.f;
+        }
+        if (!a.res && !(NOLDS && a.mask_mode)) {
+            // no residual, no mask: stores only.  The bias loads are retired here once: a wait at their first use
+            // inside the store loop (the compiler's, behind divergent control flow) was a vmcnt(0) that also
+            // drained every store issued before it -- the epilogue ran at ~1.3 TB/s, 38 % of the phase kernel's
+            // block time (CAI_PH_PROBE).  The activation is resolved outside the loop (no per-element switch).
+            wait_vmcnt<0>();
+            auto stores = [&](auto actc) {
+                constexpr int ACT = decltype(actc)::value;
+                const float prm = a.act_param;
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm) {
+                    const int m = rowm(wm * WTM + tm * 16 + i16);
+                    int b, oy, ox;
+                    out_pixel<T>(a, P, plane, m < 0 ? 0 : m, b, oy, ox);
+                    bf16* Y =
+                        reinterpret_cast<bf16*>(a.y) + (int64_t)b * a.ysb + (int64_t)oy * a.ysy + (int64_t)ox * a.ysx;
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn) {
+                        const int n = n0 + wn * WTN + tn * 16 + 4 * g_;
+                        bf16x4 h;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            float v = acc[tm][tn][r] + bv[tn][r];
+                            if constexpr (ACT == CAI_ACT_RELU) v = v > 0.f ? v : 0.f;
+                            if constexpr (ACT == CAI_ACT_LEAKY) v = v > 0.f ? v : v * prm;
+                            h[r] = (bf16)v;
+                        }
+                        if (m >= 0 && n < a.Cout) *reinterpret_cast<bf16x4*>(Y + n) = h;
+                    }
+                }
+            };
+            if (a.act == CAI_ACT_RELU)
+                stores(std::integral_constant<int, CAI_ACT_RELU>{});
+            else if (a.act == CAI_ACT_LEAKY)
+                stores(std::integral_constant<int, CAI_ACT_LEAKY>{});
+            else
+                stores(std::integral_constant<int, CAI_ACT_NONE>{});
+            return;
         }
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) {
@@ -365,18 +413,24 @@ __device__ __forceinline__ void conv_epilogue_rows_t(const ConvArgs& a, const Ph
     if (a.y_vec) {
         const int VO = a.y_dtype == CAI_BF16 ? 8 : 4;
         const int cpr = BN / VO;
-        for (int id = tid; id < BM * cpr; id += NTH) {
-            const int row = id / cpr, cc = id - (id / cpr) * cpr;
-            const int m = rowm(row), n = n0 + cc * VO;
-            if (m < 0 || n >= a.Cout) continue;
-            float v[8];
-            const f32x4 lo = *reinterpret_cast<const f32x4*>(E + row * ES + cc * VO);
-            f32x4 hi = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (VO == 8) hi = *reinterpret_cast<const f32x4*>(E + row * ES + cc * VO + 4);
-            v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
-            v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
-            store_out_chunk<T>(a, P, plane, m, n, v, VO);
-        }
+        auto run = [&](auto extra) {
+            for (int id = tid; id < BM * cpr; id += NTH) {
+                const int row = id / cpr, cc = id - (id / cpr) * cpr;
+                const int m = rowm(row), n = n0 + cc * VO;
+                if (m < 0 || n >= a.Cout) continue;
+                float v[8];
+                const f32x4 lo = *reinterpret_cast<const f32x4*>(E + row * ES + cc * VO);
+                f32x4 hi = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (VO == 8) hi = *reinterpret_cast<const f32x4*>(E + row * ES + cc * VO + 4);
+                v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+                v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+                store_out_chunk<T, decltype(extra)::value>(a, P, plane, m, n, v, VO);
+            }
+        };
+        if (a.res || a.mask_mode)
+            run(std::true_type{});
+        else
+            run(std::false_type{});
     } else {
         for (int id = tid; id < BM * BN; id += NTH) {
             const int col = id / BM, row = id - (id / BM) * BM;
@@ -891,7 +945,9 @@ __global__ __launch_bounds__(512, 1) void conv_small_kernel(const ConvArgs a) {
             const float bv = (a.bias && e < VO && n < a.Cout) ? a.bias[n] : 0.f;
             v[e] = act_pre(a, v[e] + bv);
         }
-        if (a.y_vec) {
+        if (a.y_vec && !a.res && !a.mask_mode) {
+            store_out_chunk<bf16, false>(a, P, plane, m, nb, v, VO);
+        } else if (a.y_vec) {
             store_out_chunk<bf16>(a, P, plane, m, nb, v, VO);
         } else {
 #pragma unroll
@@ -1990,7 +2046,9 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce_kernel(const ConvArgs 
             const float bv = (a.bias && nn < a.Cout) ? a.bias[nn] : 0.f;
             v[e] = act_pre(a, v[e] + bv);
         }
-        if (a.y_vec) {
+        if (a.y_vec && !a.res && !a.mask_mode) {
+            store_out_chunk<T, false>(a, P, plane, m, n, v, VO);
+        } else if (a.y_vec) {
             store_out_chunk<T>(a, P, plane, m, n, v, VO);
         } else {
 #pragma unroll
