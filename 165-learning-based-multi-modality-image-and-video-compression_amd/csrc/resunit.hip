@@ -159,27 +159,52 @@ __global__ __launch_bounds__(512, 1) void resunit_kernel(const RuArgs a) {
                 if (two) acc[1][j] = mma16<bf16>(fb, fa[1], acc[1][j]);
             }
         }
-        // epilogue A: lane = halo pixel q, channels c0 .. c0 + 3
+        // epilogue A: lane = halo pixel q, channels c0 .. c0 + 3.  Every load (bias / mask) is issued before the
+        // first store: a load behind a store waits for it on the shared vmcnt, and the per-j load -> store chain
+        // serialized the epilogues (the same for B and C below)
+        int qv[2], pv[2];
+        bool inv[2], intv[2];
+        f32x4 bA[NJA];
+        bf16x4 mA[2][NJA];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int q = (mg + 4 * i) * 16 + l16, hy = q / R::HW, hx = q - (q / R::HW) * R::HW;
+            const int yy = y0 - 1 + hy, xx = x0 - 1 + hx;
+            inv[i] = (i == 0 || two) && q < R::HPX && (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
+            intv[i] = inv[i] && hy >= 1 && hy <= R::TH && hx >= 1 && hx <= R::TW;
+            qv[i] = q;
+            pv[i] = inv[i] ? (int)pix(yy, xx) : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < NJA; ++j) {
+            const int c0 = (nh * NJA + j) * 16 + 4 * lg;
+            if (!BWD) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) bA[j][r] = a.ba[c0 + r];
+            } else {
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    mA[i][j] = bf16x4{(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+                    if (inv[i]) mA[i][j] = *reinterpret_cast<const bf16x4*>(a.h2 + (int64_t)pv[i] * NH + c0);
+                }
+            }
+        }
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             if (i == 1 && !two) break;
-            const int q = (mg + 4 * i) * 16 + l16, hy = q / R::HW, hx = q - (q / R::HW) * R::HW;
-            const int yy = y0 - 1 + hy, xx = x0 - 1 + hx;
-            const bool in = q < R::HPX && (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
-            const bool interior = in && hy >= 1 && hy <= R::TH && hx >= 1 && hx <= R::TW;
-            const int64_t p = in ? pix(yy, xx) : 0;
+            const int q = qv[i];
+            const bool in = inv[i], interior = intv[i];
+            const int64_t p = pv[i];
 #pragma unroll
             for (int j = 0; j < NJA; ++j) {
                 const int c0 = (nh * NJA + j) * 16 + 4 * lg;
                 bf16x4 hv;
                 if (!BWD) {
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) hv[r] = (bf16)(in ? fmaxf(acc[i][j][r] + a.ba[c0 + r], 0.f) : 0.f);
+                    for (int r = 0; r < 4; ++r) hv[r] = (bf16)(in ? fmaxf(acc[i][j][r] + bA[j][r], 0.f) : 0.f);
                 } else {
-                    bf16x4 m = bf16x4{(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
-                    if (in) m = *reinterpret_cast<const bf16x4*>(a.h2 + p * NH + c0);
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) hv[r] = (bf16)((float)m[r] > 0.f ? acc[i][j][r] : 0.f);
+                    for (int r = 0; r < 4; ++r) hv[r] = (bf16)((float)mA[i][j][r] > 0.f ? acc[i][j][r] : 0.f);
                 }
                 *reinterpret_cast<bf16x4*>(sH1 + q * SH + c0 * 2) = hv;
                 if (interior) *reinterpret_cast<bf16x4*>((BWD ? a.gb : a.h1) + p * NH + c0) = hv;
@@ -231,18 +256,29 @@ __global__ __launch_bounds__(512, 1) void resunit_kernel(const RuArgs a) {
     const int oy = y0 + orow, ox = x0 + ocol;
     const bool oin = oy < a.H && ox < a.W;
     const int64_t op = oin ? pix(oy, ox) : 0;
+    f32x4 bB[NJA];
+    bf16x4 mB[NJA];
+#pragma unroll
+    for (int j = 0; j < NJA; ++j) {   // loads first (see epilogue A)
+        const int c0 = (nh * NJA + j) * 16 + 4 * lg;
+        if (!BWD) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bB[j][r] = a.bb[c0 + r];
+        } else {
+            mB[j] = bf16x4{(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+            if (oin) mB[j] = *reinterpret_cast<const bf16x4*>(a.h1 + op * NH + c0);
+        }
+    }
 #pragma unroll
     for (int j = 0; j < NJA; ++j) {
         const int c0 = (nh * NJA + j) * 16 + 4 * lg;
         bf16x4 hv;
         if (!BWD) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) hv[r] = (bf16)fmaxf(accb[j][r] + a.bb[c0 + r], 0.f);
+            for (int r = 0; r < 4; ++r) hv[r] = (bf16)fmaxf(accb[j][r] + bB[j][r], 0.f);
         } else {
-            bf16x4 m = bf16x4{(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
-            if (oin) m = *reinterpret_cast<const bf16x4*>(a.h1 + op * NH + c0);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) hv[r] = (bf16)((float)m[r] > 0.f ? accb[j][r] : 0.f);
+            for (int r = 0; r < 4; ++r) hv[r] = (bf16)((float)mB[j][r] > 0.f ? accb[j][r] : 0.f);
         }
         *reinterpret_cast<bf16x4*>(sH2 + (mb * 16 + l16) * SH + c0 * 2) = hv;
         if (oin) *reinterpret_cast<bf16x4*>((BWD ? a.ga : a.h2) + op * NH + c0) = hv;
@@ -265,34 +301,48 @@ __global__ __launch_bounds__(512, 1) void resunit_kernel(const RuArgs a) {
         }
     }
     if (!oin) return;
+    // every load of the epilogue before its first store (see epilogue A)
+    bf16x4 xrC[NJC], ymC[NJC], r2C[NJC], xmC[NJC];
+    f32x4 bC[NJC];
+    const bf16x4 z4 = bf16x4{(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
 #pragma unroll
     for (int j = 0; j < NJC; ++j) {
         const int c0 = (nh * NJC + j) * 16 + 4 * lg;
-        const bf16x4 xr = *reinterpret_cast<const bf16x4*>(a.x + op * a.x_ld + c0);
+        xrC[j] = *reinterpret_cast<const bf16x4*>(a.x + op * a.x_ld + c0);
+        if (!BWD) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bC[j][r] = a.bc[c0 + r];
+        } else {
+            ymC[j] = !a.gy_masked ? *reinterpret_cast<const bf16x4*>(a.y + op * a.y_ld + c0) : z4;
+            r2C[j] = a.res2 ? *reinterpret_cast<const bf16x4*>(a.res2 + op * a.res2_ld + c0) : z4;
+            xmC[j] = a.xmask ? *reinterpret_cast<const bf16x4*>(a.xmask + op * a.xmask_ld + c0) : z4;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NJC; ++j) {
+        const int c0 = (nh * NJC + j) * 16 + 4 * lg;
+        const bf16x4 xr = xrC[j];
         bf16x4 ov;
         if (!BWD) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) ov[r] = (bf16)fmaxf(accc[j][r] + a.bc[c0 + r] + (float)xr[r], 0.f);
+            for (int r = 0; r < 4; ++r) ov[r] = (bf16)fmaxf(accc[j][r] + bC[j][r] + (float)xr[r], 0.f);
         } else {
             float v[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = (float)xr[r];
             if (!a.gy_masked) {
-                const bf16x4 ym = *reinterpret_cast<const bf16x4*>(a.y + op * a.y_ld + c0);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = (float)ym[r] > 0.f ? v[r] : 0.f;
+                for (int r = 0; r < 4; ++r) v[r] = (float)ymC[j][r] > 0.f ? v[r] : 0.f;
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] += accc[j][r];
             if (a.res2) {
-                const bf16x4 r2 = *reinterpret_cast<const bf16x4*>(a.res2 + op * a.res2_ld + c0);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] += (float)r2[r];
+                for (int r = 0; r < 4; ++r) v[r] += (float)r2C[j][r];
             }
             if (a.xmask) {
-                const bf16x4 xm = *reinterpret_cast<const bf16x4*>(a.xmask + op * a.xmask_ld + c0);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = (float)xm[r] > 0.f ? v[r] : 0.f;
+                for (int r = 0; r < 4; ++r) v[r] = (float)xmC[j][r] > 0.f ? v[r] : 0.f;
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) ov[r] = (bf16)v[r];
