@@ -111,21 +111,36 @@ __device__ __forceinline__ void adam_range(float* __restrict__ p, float* __restr
                                            float* __restrict__ v, int64_t n, int64_t i0, int64_t stride, float scale,
                                            float b1, float b2, float eps, float step_size, float bc2s, bool zero_g) {
     const int64_t n4 = n / 4;
-    for (int64_t i = i0; i < n4; i += stride) {
-        f32x4 gv = reinterpret_cast<const f32x4*>(g)[i] * scale;
-        if (zero_g) reinterpret_cast<f32x4*>(g)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-        f32x4 mv = reinterpret_cast<f32x4*>(m)[i];
-        f32x4 vv = reinterpret_cast<f32x4*>(v)[i];
-        f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
+    // U chunks per thread and round, all loaded before any store: a load issued behind a store waits for it (one
+    // vmcnt for both), so the one-chunk loop was a chain of dependent round trips (14 per thread on C4)
+    constexpr int U = 4;
+    for (int64_t ib = i0; ib < n4; ib += U * stride) {
+        f32x4 gv[U], mv[U], vv[U], pv[U];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            mv[e] = b1 * mv[e] + (1.f - b1) * gv[e];
-            vv[e] = b2 * vv[e] + (1.f - b2) * gv[e] * gv[e];
-            pv[e] -= step_size * mv[e] / (sqrtf(vv[e]) / bc2s + eps);
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = ib + u * stride;
+            if (i < n4) {
+                gv[u] = reinterpret_cast<const f32x4*>(g)[i] * scale;
+                mv[u] = reinterpret_cast<f32x4*>(m)[i];
+                vv[u] = reinterpret_cast<f32x4*>(v)[i];
+                pv[u] = reinterpret_cast<f32x4*>(p)[i];
+            }
         }
-        reinterpret_cast<f32x4*>(m)[i] = mv;
-        reinterpret_cast<f32x4*>(v)[i] = vv;
-        reinterpret_cast<f32x4*>(p)[i] = pv;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = ib + u * stride;
+            if (i >= n4) continue;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                mv[u][e] = b1 * mv[u][e] + (1.f - b1) * gv[u][e];
+                vv[u][e] = b2 * vv[u][e] + (1.f - b2) * gv[u][e] * gv[u][e];
+                pv[u][e] -= step_size * mv[u][e] / (sqrtf(vv[u][e]) / bc2s + eps);
+            }
+            if (zero_g) reinterpret_cast<f32x4*>(g)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            reinterpret_cast<f32x4*>(m)[i] = mv[u];
+            reinterpret_cast<f32x4*>(v)[i] = vv[u];
+            reinterpret_cast<f32x4*>(p)[i] = pv[u];
+        }
     }
     for (int64_t i = n4 * 4 + i0; i < n; i += stride) {
         const float gv = g[i] * scale;
