@@ -313,39 +313,29 @@ __device__ __forceinline__ void conv_epilogue_rows_t(const ConvArgs& a, const Ph
             // no residual, no mask: stores only.  The bias loads are retired here once: a wait at their first use
             // inside the store loop (the compiler's, behind divergent control flow) was a vmcnt(0) that also
             // drained every store issued before it -- the epilogue ran at ~1.3 TB/s, 38 % of the phase kernel's
-            // block time (CAI_PH_PROBE).  The activation is resolved outside the loop (no per-element switch).
+            // block time (CAI_PH_PROBE).
             wait_vmcnt<0>();
-            auto stores = [&](auto actc) {
-                constexpr int ACT = decltype(actc)::value;
-                const float prm = a.act_param;
+            // the activation as one branch-free select: v > 0 ? v : v * neg (neg = 0 / slope / 1; the ReLU's
+            // negative side stays +0)
+            const float neg = a.act == CAI_ACT_RELU ? 0.f : (a.act == CAI_ACT_LEAKY ? a.act_param : 1.f);
 #pragma unroll
-                for (int tm = 0; tm < TM; ++tm) {
-                    const int m = rowm(wm * WTM + tm * 16 + i16);
-                    int b, oy, ox;
-                    out_pixel<T>(a, P, plane, m < 0 ? 0 : m, b, oy, ox);
-                    bf16* Y =
-                        reinterpret_cast<bf16*>(a.y) + (int64_t)b * a.ysb + (int64_t)oy * a.ysy + (int64_t)ox * a.ysx;
+            for (int tm = 0; tm < TM; ++tm) {
+                const int m = rowm(wm * WTM + tm * 16 + i16);
+                int b, oy, ox;
+                out_pixel<T>(a, P, plane, m < 0 ? 0 : m, b, oy, ox);
+                bf16* Y = reinterpret_cast<bf16*>(a.y) + (int64_t)b * a.ysb + (int64_t)oy * a.ysy + (int64_t)ox * a.ysx;
 #pragma unroll
-                    for (int tn = 0; tn < TN; ++tn) {
-                        const int n = n0 + wn * WTN + tn * 16 + 4 * g_;
-                        bf16x4 h;
+                for (int tn = 0; tn < TN; ++tn) {
+                    const int n = n0 + wn * WTN + tn * 16 + 4 * g_;
+                    bf16x4 h;
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            float v = acc[tm][tn][r] + bv[tn][r];
-                            if constexpr (ACT == CAI_ACT_RELU) v = v > 0.f ? v : 0.f;
-                            if constexpr (ACT == CAI_ACT_LEAKY) v = v > 0.f ? v : v * prm;
-                            h[r] = (bf16)v;
-                        }
-                        if (m >= 0 && n < a.Cout) *reinterpret_cast<bf16x4*>(Y + n) = h;
+                    for (int r = 0; r < 4; ++r) {
+                        const float v = acc[tm][tn][r] + bv[tn][r];
+                        h[r] = (bf16)(v > 0.f ? v : (neg == 0.f ? 0.f : v * neg));
                     }
+                    if (m >= 0 && n < a.Cout) *reinterpret_cast<bf16x4*>(Y + n) = h;
                 }
-            };
-            if (a.act == CAI_ACT_RELU)
-                stores(std::integral_constant<int, CAI_ACT_RELU>{});
-            else if (a.act == CAI_ACT_LEAKY)
-                stores(std::integral_constant<int, CAI_ACT_LEAKY>{});
-            else
-                stores(std::integral_constant<int, CAI_ACT_NONE>{});
+            }
             return;
         }
 #pragma unroll
