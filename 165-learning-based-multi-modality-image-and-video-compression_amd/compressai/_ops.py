@@ -792,11 +792,12 @@ _SPEC_1x1, _SPEC_3x3 = ConvSpec(1, 1, 0), ConvSpec(3, 1, 1)
 class _FusedUnit:
     """A ResidualUnit run by cai_resunit: saved tensors (x, h1, h2, y) and what its backward needs."""
 
-    __slots__ = ("saved_tensors", "params", "geoms", "gy_masked", "mask_x", "dx_res2", "dx_res", "need_x")
+    __slots__ = ("saved_tensors", "params", "geoms", "gy_masked", "mask_x", "dx_res2", "dx_res", "need_x", "wt_packed")
 
     def __init__(self, params, geoms, need_x):
         self.params, self.geoms, self.need_x = params, geoms, need_x
         self.saved_tensors = ()
+        self.wt_packed = None
         self.gy_masked = self.mask_x = False
         self.dx_res2 = self.dx_res = None
 
@@ -865,6 +866,10 @@ def _resunit_fwd(y, params, need_x):
                 2 * B * H * W * (2 * n + 2 * nh), dt, f"ResidualUnit N={n} {H}x{W} B={B}")
     u = _FusedUnit(params, (ga, gb, gc), need_x)
     u.saved_tensors = (xpm, h1, h2, out)
+    if _prepack_active() is not None:
+        # the input-gradient operands from this forward's pack_many launch: the backward runs after the forward's
+        # prepack context has closed, where a lookup would miss and pack each of them in a launch of its own
+        u.wt_packed = (_packed_kp(w4, gc, dt, 1), _packed_kp(w2, gb, dt, 1), _packed_kp(w0, ga, dt, 1))
     return out, u
 
 
@@ -876,8 +881,9 @@ def _resunit_bwd(u: "_FusedUnit", gy):
     B, n, H, W = xpm.shape
     nh = n // 2
     gpm, gld = to_pm(gy, dt, 8)
-    (wa, kpa), (wb, kpb), (wc, kpc) = (_packed_kp(w4, gc, dt, 1), _packed_kp(w2, gb, dt, 1),
-                                       _packed_kp(w0, ga, dt, 1))
+    wt = getattr(u, "wt_packed", None)
+    (wa, kpa), (wb, kpb), (wc, kpc) = wt if wt is not None else (_packed_kp(w4, gc, dt, 1), _packed_kp(w2, gb, dt, 1),
+                                                                 _packed_kp(w0, ga, dt, 1))
     dev = xpm.device
     g_c = None if u.gy_masked else empty_pm(B, n, H, W, dt, dev)
     g_b = empty_pm(B, nh, H, W, dt, dev)

@@ -90,8 +90,22 @@ static int sq_parts(int64_t n) {
 __global__ __launch_bounds__(256) void sq_part_kernel(const float* __restrict__ g, int64_t n, float* __restrict__ part,
                                                       float* __restrict__ step) {
     __shared__ float red[4];
-    float acc = 0.f;
-    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) acc += g[i] * g[i];
+    // 16-byte loads, U of them in flight per thread (the one-float loop ran at ~1.9 TB/s on C4's 26M gradients)
+    constexpr int U = 4;
+    const int64_t n4 = n / 4, stride = (int64_t)gridDim.x * 256;
+    f32x4 a4 = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t ib = blockIdx.x * 256 + threadIdx.x; ib < n4; ib += U * stride) {
+        f32x4 gv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = ib + u * stride;
+            gv[u] = i < n4 ? reinterpret_cast<const f32x4*>(g)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) a4 += gv[u] * gv[u];
+    }
+    float acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+    for (int64_t i = n4 * 4 + blockIdx.x * 256 + threadIdx.x; i < n; i += stride) acc += g[i] * g[i];
     const float r = block_sum<256>(acc, red);
     if (threadIdx.x == 0) {
         part[blockIdx.x] = r;

@@ -228,3 +228,35 @@ def test_resunit_launch_count(cuda, monkeypatch):
     # (the block's final 1x1 conv_b keeps its own)
     assert names.count("cai_resunit_wgrad") == 6, calls
     assert sum(1 for n in names if n in ("cai_conv_wgrad", "cai_conv_wgrad_deferred")) == 1, calls
+
+
+def test_resunit_backward_uses_prepacked_weights(cuda, monkeypatch):
+    """Under a model forward's pack_many context the fused units' backward takes its input-gradient operands from
+    that launch: no per-layer cai_conv_pack_weight launch in the backward (there were 72 per cheng2020 step)."""
+    import compressai.layers as L
+    from compressai import _ops
+    from compressai._prepack import prepacked_forward
+
+    calls = []
+    real = _ops.lib
+
+    class Spy:
+        def __getattr__(self, name):
+            fn = getattr(real, name)
+            if name != "cai_conv_pack_weight":
+                return fn
+
+            def call(*a):
+                calls.append(name)
+                return fn(*a)
+            return call
+
+    monkeypatch.setattr(_ops, "lib", Spy())
+    mod = L.AttentionBlock(192).to(cuda)
+    x = _pm(torch.randn(1, 192, 16, 16, device=cuda)).requires_grad_()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        with prepacked_forward(mod):
+            y = mod(x)
+    y.float().sum().backward()
+    torch.cuda.synchronize()
+    assert calls == [], calls
