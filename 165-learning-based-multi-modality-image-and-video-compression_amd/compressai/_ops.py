@@ -1026,6 +1026,33 @@ def _chain_backward(subs, gy, dx_res2=None):
     return g, [t for unit in reversed(grads) for t in unit]
 
 
+class ResidualBlockFn(torch.autograd.Function):
+    """ResidualBlock with an identity skip (layers.py:162-193): y = leaky(conv2(leaky(conv1(x)))) + x as one
+    autograd node.  x's two gradients (through the convs and through the skip) are summed in conv1's dgrad
+    epilogue (cai_conv_dgrad_res) instead of an autograd gradient-sum launch; the forward runs the same kernels as
+    the per-module chain (conv1 with its LeakyReLU epilogue, conv2 applying that mask in its dgrad, the add)."""
+
+    @staticmethod
+    def forward(ctx, x, spec1, spec2, w1, b1, w2, b2):
+        need = ctx.needs_input_grad   # (x, spec1, spec2, w1, b1, w2, b2)
+        c1 = _SubCtx((need[0], need[3], need[4], False, False))
+        c2 = _SubCtx((True, need[5], need[6], False, False))
+        h = ConvFn.forward(c1, x, w1, b1, spec1)
+        o = ConvFn.forward(c2, h, w2, b2, spec2)
+        y = AddActFn.forward(_SubCtx((True, True, False, False)), o, x, ACT_NONE, 0.0)
+        ctx.c1, ctx.c2 = c1, c2
+        _stash(ctx, [c1, c2])
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        with _unstash(ctx):
+            dh, dw2, db2, _, _ = ConvFn.backward(ctx.c2, gy)
+            ctx.c1.dx_res = gy   # the skip's gradient (the add has no activation)
+            dx, dw1, db1, _, _ = ConvFn.backward(ctx.c1, dh)
+        return dx, None, None, dw1, db1, dw2, db2
+
+
 class AttentionBlockFn(torch.autograd.Function):
     """AttentionBlock (layers.py:196-244) as one autograd node: y = a * sigmoid(b) + x with a = conv_a(x) and
     b = conv_b(x) (three ResidualUnits each, as in ResidualChainFn; conv_b's 1x1 conv after its chain).  x's three

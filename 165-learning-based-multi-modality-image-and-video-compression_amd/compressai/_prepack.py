@@ -120,11 +120,13 @@ class Prepacker:
         host = ctypes.create_string_buffer(b"".join(descs), len(descs) * dsz)
         total = lib.cai_conv_pack_finalize(host, len(descs))
         blob = torch.frombuffer(bytearray(host.raw), dtype=torch.uint8).to(dev)
-        # algorithmic bytes of one pack launch (ledger): every packed buffer written once, and its fp32 source
-        # read once per descriptor (approximated as 2x a bf16 buffer / 1x an fp32 one)
+        # algorithmic bytes of one pack launch (ledger): every packed buffer written once, and every fp32 source
+        # (weight, mask, GDN parameters) read once -- a weight's two directions share the source tiles
         written = sum(b.numel() * b.element_size() for b in buffers)
+        read = sum(4 * (m.weight.numel() + (k.numel() if k is not None else 0)) for m, k in self._convs())
+        read += sum(4 * (m.beta.numel() + m.gamma.numel()) for m in gdns)
         return {"sig": self._signature(), "table": table, "buffers": buffers, "descs": blob, "n": len(descs),
-                "total": total, "bytes": written * (3 if dtype == torch.bfloat16 else 2)}
+                "total": total, "bytes": written + read}
 
     # -------------------------------------------------------------------- use
     def refresh(self):

@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 
 from .._native import ACT_LEAKY, ACT_NONE, ACT_RELU, MASK_LEAKY, MASK_POS
-from .._ops import AddActFn, AttentionBlockFn, GateFn, ResidualChainFn, residual_fusable
+from .._ops import AddActFn, AttentionBlockFn, GateFn, ResidualBlockFn, ResidualChainFn, residual_fusable
 from .conv import Conv2d, ConvTranspose2d, PixelShuffle, Sequential
 from .gdn import GDN
 
@@ -107,7 +107,15 @@ class ResidualBlock(nn.Module):
         self.conv2 = conv3x3(out_ch, out_ch)
         self.skip = conv1x1(in_ch, out_ch) if in_ch != out_ch else None
 
+    # False: the per-module chain (autograd sums x's two gradients); CAI_RESIDUAL_FUSE=0 for A/Bs
+    fuse_residual = os.environ.get("CAI_RESIDUAL_FUSE", "1") != "0"
+
     def forward(self, x):
+        s1 = self.conv1._spec(act=ACT_LEAKY, act_param=_SLOPE, act_bwd_downstream=True)
+        s2 = self.conv2._spec(act=ACT_LEAKY, act_param=_SLOPE, in_mask=MASK_LEAKY, in_mask_param=_SLOPE)
+        if self.skip is None and self.fuse_residual:
+            return ResidualBlockFn.apply(x, s1, s2, self.conv1.weight, self.conv1.bias, self.conv2.weight,
+                                         self.conv2.bias)
         out = self.conv1.run(x, act=ACT_LEAKY, act_param=_SLOPE, act_bwd_downstream=True)
         out = self.conv2.run(out, act=ACT_LEAKY, act_param=_SLOPE, in_mask=MASK_LEAKY, in_mask_param=_SLOPE)
         identity = self.skip(x) if self.skip is not None else x

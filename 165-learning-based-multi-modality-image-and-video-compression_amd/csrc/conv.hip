@@ -2072,6 +2072,16 @@ struct PackArgs {
     int gdn;               // 1: GDN reparametrisation (w = gamma_raw, mask = beta_raw, out = gamma_op, D1 = C)
     float* gdn_beta;       //    beta output (C floats)
     float gdn_bb, gdn_gb, gdn_ped;
+    // pack_many tile mode: 1 = this descriptor owns source tiles (and, pair = 1, also writes the next descriptor:
+    // the other direction of the same weight, from the same LDS tile); 2 = written by the previous one's tiles
+    int tilemode, pair;
+    int td0, td1, tdp;     // tile: source dim-0 x dim-1 entries (k*k taps each); LDS row pitch (floats)
+    int tstride;           // LDS floats per tap plane: td0 * tdp + 4 (planes start on different banks)
+    int d0real, d1real;    // source extents (torch dims 0 / 1)
+    int tn1;               // tiles along dim 1
+    uint32_t mrl, mkk;     // ceil(2^32 / (td1 * k * k)), ceil(2^32 / (k * k)) (k > 1): divisions by multiply-high
+    int64_t tile_begin;    // first global tile of this descriptor (non-decreasing over the table)
+    int64_t tiles_total;   // tiles of the whole table (the same in every descriptor)
 };
 
 template <typename T>
@@ -2113,6 +2123,10 @@ constexpr int PACK_ROW_MAX = CAI_PACK_ROW_MAX;   // source floats per row that f
 #define CAI_PACK_ROWS_PER_UNIT 8   // A/B: 1 = one row per work unit (the round-3 form)
 #endif
 constexpr int PACK_ROWS_PER_UNIT = CAI_PACK_ROWS_PER_UNIT;
+#ifndef CAI_PACK_TILES
+#define CAI_PACK_TILES 1   // A/B: 0 = row / item modes only (each direction reads its fp32 source itself)
+#endif
+constexpr bool PACK_TILES = CAI_PACK_TILES != 0;
 
 template <typename T>
 __device__ __forceinline__ void pack_item(const PackArgs* __restrict__ descs, int n, int64_t gi) {
@@ -2264,14 +2278,200 @@ __device__ __forceinline__ void pack_rows(const PackArgs& a, int n0, int cnt, fl
     __syncthreads();   // the next unit reuses S
 }
 
+// Tile mode (round 4): a unit is a td0 x td1 tile of the SOURCE [D0][D1][k*k], loaded once with coalesced runs
+// of td1*k*k floats (16-byte loads where the rows allow) and kept in LDS tap-major, S[tap][a][b] (row pitch
+// tdp = td1 + 4, plane stride td0 * tdp + 4).  Both packed directions of the
+// weight are written from it: the one whose rows are dim 0 (rows a, 16-byte channel chunks read as vectors along
+// b) and the one whose rows are dim 1 (rows b, chunks gathered along a).  Every packed element of a tile's rows
+// and channels is written, padding included: rows < Npad, and each row as ceil(Kp / Cpad) slots of Cpad channels
+// (slot t < ntaps[ph] holds source tap TO[ph][t]; the rest, and channels >= Creal, are zero).  The row mode read
+// the source once per direction, a unit of <= 8 rows at a time (a third of cheng2020's step in the pack launch
+// ran at 1.8 TB/s).
+constexpr int PACK_TILE_FLOATS = 10404;   // 41.6 KB: 32 x 32 tiles of 3x3, 16 x 16 of 5x5, 128 x 64 of 1x1
+constexpr int PACK_LDS_FLOATS = PACK_TILE_FLOATS > PACK_ROW_MAX ? PACK_TILE_FLOATS : PACK_ROW_MAX;
+
+__device__ __forceinline__ void pack_taps(const PackArgs& a, int* TO) {
+    for (int idx = threadIdx.x; idx < a.nphase * 64; idx += blockDim.x) {
+        const int ph = idx >> 6, t = idx & 63;
+        const int ntx = ph == 0 ? a.ntx[0] : (ph == 1 ? a.ntx[1] : (ph == 2 ? a.ntx[2] : a.ntx[3]));
+        const int kh0 = ph == 0 ? a.kh0[0] : (ph == 1 ? a.kh0[1] : (ph == 2 ? a.kh0[2] : a.kh0[3]));
+        const int kw0 = ph == 0 ? a.kw0[0] : (ph == 1 ? a.kw0[1] : (ph == 2 ? a.kw0[2] : a.kw0[3]));
+        const int ty = t / ntx;
+        TO[idx] = (kh0 + a.step * ty) * a.k + kw0 + a.step * (t - ty * ntx);
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void pack_tile_store(const PackArgs& X, int ph, int n, int e0, const float (&v)[16 / sizeof(T)]) {
+    const int64_t off = ph == 0 ? X.off[0] : (ph == 1 ? X.off[1] : (ph == 2 ? X.off[2] : X.off[3]));
+    T* out = reinterpret_cast<T*>(X.out) + off + (int64_t)n * X.Kp + e0;
+    if constexpr (sizeof(T) == 2) {
+        bf16x8 h;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) h[e] = (bf16)v[e];
+        *reinterpret_cast<bf16x8*>(out) = h;
+    } else {
+        *reinterpret_cast<f32x4*>(out) = f32x4{v[0], v[1], v[2], v[3]};
+    }
+}
+
+// rows = source dim 0 (n = d0, channel c = d1): chunk reads are 16-byte LDS vectors along b
+template <typename T>
+__device__ __forceinline__ void pack_tile_rows0(const PackArgs& X, int d0_0, int d1_0, const PackArgs& G, const float* S,
+                                                const int* TO) {
+    constexpr int VW = 16 / sizeof(T);
+    const int td0 = G.td0, tdp = G.tdp, nch = G.td1 / VW;
+    const int nslot = (X.Kp + X.Cpad - 1) / X.Cpad;
+    const int cnt = X.nphase * td0 * nslot * nch;
+    for (int w = threadIdx.x; w < cnt; w += blockDim.x) {
+        const int ch = w % nch, r1 = w / nch, t = r1 % nslot, r2 = r1 / nslot, a = r2 % td0, ph = r2 / td0;
+        const int n = d0_0 + a, c0 = d1_0 + ch * VW, e0 = t * X.Cpad + c0;
+        if (n >= X.Npad || c0 >= X.Cpad || e0 >= X.Kp) continue;
+        const int ntaps = ph == 0 ? X.ntaps[0] : (ph == 1 ? X.ntaps[1] : (ph == 2 ? X.ntaps[2] : X.ntaps[3]));
+        float v[VW];
+#pragma unroll
+        for (int e = 0; e < VW; ++e) v[e] = 0.f;
+        if (n < X.Nreal && t < ntaps) {
+            const float* s = S + TO[ph * 64 + t] * G.tstride + a * tdp + ch * VW;
+#pragma unroll
+            for (int q = 0; q < VW / 4; ++q) {
+                const f32x4 f = *reinterpret_cast<const f32x4*>(s + 4 * q);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[4 * q + e] = c0 + 4 * q + e < X.Creal ? f[e] : 0.f;
+            }
+        }
+        pack_tile_store<T>(X, ph, n, e0, v);
+    }
+}
+
+// rows = source dim 1 (n = d1, channel c = d0): consecutive lanes take a row's consecutive chunks, then rows
+template <typename T>
+__device__ __forceinline__ void pack_tile_rows1(const PackArgs& X, int d0_0, int d1_0, const PackArgs& G, const float* S,
+                                                const int* TO) {
+    constexpr int VW = 16 / sizeof(T);
+    const int td0 = G.td0, td1 = G.td1, tdp = G.tdp, nch = td0 / VW;
+    const int nslot = (X.Kp + X.Cpad - 1) / X.Cpad;
+    const int cnt = X.nphase * nslot * td1 * nch;
+    for (int w = threadIdx.x; w < cnt; w += blockDim.x) {
+        const int ch = w % nch, r1 = w / nch, b = r1 % td1, r2 = r1 / td1, t = r2 % nslot, ph = r2 / nslot;
+        const int n = d1_0 + b, c0 = d0_0 + ch * VW, e0 = t * X.Cpad + c0;
+        if (n >= X.Npad || c0 >= X.Cpad || e0 >= X.Kp) continue;
+        const int ntaps = ph == 0 ? X.ntaps[0] : (ph == 1 ? X.ntaps[1] : (ph == 2 ? X.ntaps[2] : X.ntaps[3]));
+        float v[VW];
+#pragma unroll
+        for (int e = 0; e < VW; ++e) v[e] = 0.f;
+        if (n < X.Nreal && t < ntaps) {
+            const float* s = S + TO[ph * 64 + t] * G.tstride + ch * VW * tdp + b;
+#pragma unroll
+            for (int e = 0; e < VW; ++e) v[e] = c0 + e < X.Creal ? s[e * tdp] : 0.f;
+        }
+        pack_tile_store<T>(X, ph, n, e0, v);
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void pack_tile(const PackArgs* __restrict__ descs, int lo, int64_t tl, float* S, int* TO) {
+    const PackArgs& A = descs[lo];
+    const int i0 = (int)(tl / A.tn1), i1 = (int)(tl - (int64_t)i0 * A.tn1);
+    const int td0 = A.td0, td1 = A.td1, tdp = A.tdp;
+    const int d0_0 = i0 * td0, d1_0 = i1 * td1;
+    const int KK = A.k * A.k, RL = td1 * KK, tot = td0 * RL;
+    pack_taps(A, TO);
+    if (A.pair) pack_taps(descs[lo + 1], TO + 256);
+    const int TS = A.tstride;
+    const int lim = (A.d1real - d1_0) * KK;   // valid source floats of a tile row
+    if (((A.D1 * KK) & 3) == 0 && (((uintptr_t)A.w | (uintptr_t)A.mask) & 15) == 0) {
+        // 16-byte loads: a tile row is td1*k*k floats (a multiple of 4) starting 16-byte aligned
+        constexpr int LD = 8;   // independent 16-byte loads in flight per thread
+        const int tot4 = tot >> 2;
+        for (int q0 = threadIdx.x; q0 < tot4; q0 += LD * blockDim.x) {
+            f32x4 v[LD];
+            int aa[LD], rr[LD];
+#pragma unroll
+            for (int j = 0; j < LD; ++j) {
+                const int q = q0 + j * (int)blockDim.x, l = 4 * q;
+                const int a = (int)__umulhi((unsigned)l, A.mrl), r = l - a * RL;
+                aa[j] = q < tot4 ? a : -1;
+                rr[j] = r;
+                v[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (q >= tot4 || d0_0 + a >= A.d0real) continue;
+                const int64_t src = ((int64_t)(d0_0 + a) * A.D1 + d1_0) * KK + r;
+                if (r + 4 <= lim) {
+                    v[j] = *reinterpret_cast<const f32x4*>(A.w + src);
+                    if (A.mask) v[j] *= *reinterpret_cast<const f32x4*>(A.mask + src);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (r + e < lim) v[j][e] = A.mask ? A.w[src + e] * A.mask[src + e] : A.w[src + e];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < LD; ++j) {
+                if (aa[j] < 0) continue;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int r = rr[j] + e;
+                    const int b = KK == 1 ? r : (int)__umulhi((unsigned)r, A.mkk), tap = r - b * KK;
+                    S[tap * TS + aa[j] * tdp + b] = v[j][e];
+                }
+            }
+        }
+    } else {
+        constexpr int LD = 8;   // independent loads in flight per thread
+        for (int l0 = threadIdx.x; l0 < tot; l0 += LD * blockDim.x) {
+            float v[LD];
+            int dst[LD];
+#pragma unroll
+            for (int j = 0; j < LD; ++j) {
+                const int l = l0 + j * (int)blockDim.x;
+                const int a = (int)__umulhi((unsigned)l, A.mrl), r = l - a * RL;
+                const int b = KK == 1 ? r : (int)__umulhi((unsigned)r, A.mkk), tap = r - b * KK;   // 2^32 / 1 overflows
+                const bool ok = l < tot && d0_0 + a < A.d0real && r < lim;
+                const int64_t src = ((int64_t)(d0_0 + a) * A.D1 + d1_0) * KK + r;
+                float x = ok ? A.w[src] : 0.f;
+                if (A.mask && ok) x *= A.mask[src];
+                v[j] = x;
+                dst[j] = l < tot ? tap * TS + a * tdp + b : -1;
+            }
+#pragma unroll
+            for (int j = 0; j < LD; ++j)
+                if (dst[j] >= 0) S[dst[j]] = v[j];
+        }
+    }
+    __syncthreads();
+    if (A.n_is_d0)
+        pack_tile_rows0<T>(A, d0_0, d1_0, A, S, TO);
+    else
+        pack_tile_rows1<T>(A, d0_0, d1_0, A, S, TO);
+    if (A.pair) {
+        const PackArgs& B = descs[lo + 1];
+        if (B.n_is_d0)
+            pack_tile_rows0<T>(B, d0_0, d1_0, A, S, TO + 256);
+        else
+            pack_tile_rows1<T>(B, d0_0, d1_0, A, S, TO + 256);
+    }
+    __syncthreads();   // the next unit reuses S and TO
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void pack_many_kernel(const PackArgs* __restrict__ descs, int n, int64_t total) {
-    __shared__ float S[PACK_ROW_MAX];
-    __shared__ int TO[4 * 64];
+    __shared__ __attribute__((aligned(16))) float S[PACK_LDS_FLOATS];
+    __shared__ int TO[2 * 4 * 64];
+    const int64_t Tt = descs[0].tiles_total;
     const int64_t R = descs[0].rows_total;
-    const int64_t I = total - R;
-    const int64_t units = R + (I + 255) / 256;
-    for (int64_t u = blockIdx.x; u < units; u += gridDim.x) {
+    const int64_t I = total - Tt - R;
+    const int64_t units = Tt + R + (I + 255) / 256;
+    for (int64_t u0 = blockIdx.x; u0 < units; u0 += gridDim.x) {
+        if (u0 < Tt) {
+            int lo = 0, hi = n - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (descs[mid].tile_begin <= u0) lo = mid; else hi = mid - 1;
+            }
+            pack_tile<T>(descs, lo, u0 - descs[lo].tile_begin, S, TO);
+            continue;
+        }
+        const int64_t u = u0 - Tt;
         if (u < R) {
             int lo = 0, hi = n - 1;
             while (lo < hi) {
@@ -3068,6 +3268,10 @@ struct WhCfg {
     static constexpr int TN = WCOL / 16;
 };
 
+#ifndef CAI_WH_PF
+#define CAI_WH_PF 0   // A/B: 1 = fragment reads one K-half ahead (no gain: the kernel waits on its DMA, r04_wgrad_halo_pf_ab.log)
+#endif
+
 __device__ __forceinline__ int wh_h(int cell) { return ((cell >> 1) & 1) | (((cell >> 3) & 1) << 1); }
 
 // keep a per-lane value opaque to the optimiser: it stays one materialised VGPR instead of being
@@ -3213,50 +3417,110 @@ __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
         }
     }
 
-    auto step = [&](auto ustage) {
-        constexpr int U = decltype(ustage)::value;
+    // fragment reads of one K-half (ks) of a ring stage, and the MFMAs (+ bias sums) on them
+    auto rd = [&](auto ustage, auto kc, u32x4 (&fa)[4], u32x4 (&fb)[W::TN]) {
+        constexpr int U = decltype(ustage)::value, ks = decltype(kc)::value;
         const char* Gs = smem + U * W::GIMG;
         const char* Xs = smem + U * W::XSTRIDE;      // boff carries XBASE
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            u32x4 fb[W::TN];
+        for (int t = 0; t < W::TN; ++t) {
+            s16x4 b0 = ds_tr16(Xs, boff[ks][t][0]);
+            s16x4 b1 = ds_tr16(Xs, boff[ks][t][1]);
+            s16x8 bv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+            fb[t] = __builtin_bit_cast(u32x4, bv);
+        }
 #pragma unroll
-            for (int t = 0; t < W::TN; ++t) {
-                s16x4 b0 = ds_tr16(Xs, boff[ks][t][0]);
-                s16x4 b1 = ds_tr16(Xs, boff[ks][t][1]);
-                s16x8 bv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
-                fb[t] = __builtin_bit_cast(u32x4, bv);
-            }
-#pragma unroll
-            for (int tm = 0; tm < 4; ++tm) {
-                s16x4 a0 = ds_tr16(Gs, aoff[ks][tm][0]);
-                s16x4 a1 = ds_tr16(Gs, aoff[ks][tm][1]);
-                s16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-                const u32x4 fa = __builtin_bit_cast(u32x4, av);
-                if constexpr ((FLAGS & WG_BIAS) != 0) {
-                    if (do_bias && tm == wc) {
-                        const bf16x8 h = __builtin_bit_cast(bf16x8, fa);
-                        float sacc = 0.f;
-#pragma unroll
-                        for (int e = 0; e < 8; ++e) sacc += (float)h[e];
-                        bsum[tm] += sacc;
-                    }
-                }
-#pragma unroll
-                for (int tn = 0; tn < W::TN; ++tn) acc[tm][tn] = mma16<bf16>(fa, fb[tn], acc[tm][tn]);
-            }
-            // transposed bias sums after the MFMAs: inside the read loop they made each B read wait
-            if constexpr ((FLAGS & WG_TBIAS) != 0) {
-#pragma unroll
-                for (int t = 0; t < W::TN; ++t)
-                    if (tsel[t] >= 0) tsum[t] += sum8_bf16(fb[t]);
-            }
+        for (int tm = 0; tm < 4; ++tm) {
+            s16x4 a0 = ds_tr16(Gs, aoff[ks][tm][0]);
+            s16x4 a1 = ds_tr16(Gs, aoff[ks][tm][1]);
+            s16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+            fa[tm] = __builtin_bit_cast(u32x4, av);
         }
     };
+    auto mm = [&](const u32x4 (&fa)[4], const u32x4 (&fb)[W::TN]) {
+#pragma unroll
+        for (int tm = 0; tm < 4; ++tm) {
+            if constexpr ((FLAGS & WG_BIAS) != 0) {
+                if (do_bias && tm == wc) {
+                    const bf16x8 h = __builtin_bit_cast(bf16x8, fa[tm]);
+                    float sacc = 0.f;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) sacc += (float)h[e];
+                    bsum[tm] += sacc;
+                }
+            }
+#pragma unroll
+            for (int tn = 0; tn < W::TN; ++tn) acc[tm][tn] = mma16<bf16>(fa[tm], fb[tn], acc[tm][tn]);
+        }
+        // transposed bias sums after the MFMAs: inside the read loop they made each B read wait
+        if constexpr ((FLAGS & WG_TBIAS) != 0) {
+#pragma unroll
+            for (int t = 0; t < W::TN; ++t)
+                if (tsel[t] >= 0) tsum[t] += sum8_bf16(fb[t]);
+        }
+    };
+    using K0 = std::integral_constant<int, 0>;
+    using K1 = std::integral_constant<int, 1>;
 
 #pragma unroll
     for (int s = 0; s < W::NST - 1; ++s)
         if (s < nsteps) issue(s);
+#if CAI_WH_PF
+    // Software-pipelined: the fragments of the next K-half are read while the MFMAs of the current one run --
+    // the second half of a strip during the first, and the first half of the NEXT strip during the second.
+    // So a step's wait covers the next strip as well (2 strips in flight instead of 3), and the one barrier
+    // per step still separates every read of a stage from the DMA that refills it (issued a step later).
+    u32x4 fca[4], fcb[W::TN], fna[4], fnb[W::TN];
+    if (nsteps > 0) {
+        if (nsteps >= 3)
+            wait_vmcnt<2 * W::NLOAD>();
+        else if (nsteps == 2)
+            wait_vmcnt<W::NLOAD>();
+        else
+            wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        rd(K0(), K0(), fca, fcb);
+    }
+    for (int st0 = 0; st0 < nsteps; st0 += W::NST) {
+        auto one = [&](auto ustage) {
+            constexpr int U = decltype(ustage)::value;
+            const int st = st0 + U;
+            if (st >= nsteps) return;
+            if (st + 2 < nsteps)   // strips 0 .. st + 1 landed (st + 2 may stay in flight)
+                wait_vmcnt<W::NLOAD>();
+            else
+                wait_vmcnt<0>();
+            wait_lgkmcnt0();
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            if (st + W::NST - 1 < nsteps) issue((U + W::NST - 1) % W::NST);
+            rd(ustage, K1(), fna, fnb);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_setprio(1);
+            mm(fca, fcb);
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) fca[i] = fna[i];
+#pragma unroll
+            for (int i = 0; i < W::TN; ++i) fcb[i] = fnb[i];
+            if (st + 1 < nsteps) rd(std::integral_constant<int, (U + 1) % W::NST>(), K0(), fna, fnb);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_setprio(1);
+            mm(fca, fcb);
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) fca[i] = fna[i];
+#pragma unroll
+            for (int i = 0; i < W::TN; ++i) fcb[i] = fnb[i];
+        };
+        one(std::integral_constant<int, 0>());
+        one(std::integral_constant<int, 1>());
+        one(std::integral_constant<int, 2>());
+        one(std::integral_constant<int, 3>());
+    }
+#else
     // the ring position is a compile-time constant: the loop runs NST strips per trip
     for (int st0 = 0; st0 < nsteps; st0 += W::NST) {
         auto one = [&](auto ustage) {
@@ -3274,7 +3538,11 @@ __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
             if (st + W::NST - 1 < nsteps) issue((U + W::NST - 1) % W::NST);
-            step(ustage);
+            u32x4 fa[4], fb[W::TN];
+            rd(ustage, K0(), fa, fb);
+            mm(fa, fb);
+            rd(ustage, K1(), fa, fb);
+            mm(fa, fb);
             __builtin_amdgcn_sched_barrier(0);
         };
         one(std::integral_constant<int, 0>());
@@ -3282,6 +3550,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
         one(std::integral_constant<int, 2>());
         one(std::integral_constant<int, 3>());
     }
+#endif
     if constexpr ((FLAGS & WG_BIAS) != 0) {
         if (do_bias) {
             float v = bsum[0] + bsum[1] + bsum[2] + bsum[3];
@@ -4270,23 +4539,76 @@ int cai_gdn_reparam_describe(const float* beta_raw, const float* gamma_raw, int3
 int64_t cai_conv_pack_finalize(void* descs, int32_t n) {
     if (!descs || n <= 0) return -1;
     PackArgs* d = reinterpret_cast<PackArgs*>(descs);
-    // row mode for conv descriptors whose source row fits the LDS copy; zero-size entries in the other
-    // numbering keep both begin arrays non-decreasing (a unit's descriptor is the LAST one at or below it)
-    int64_t items = 0, rows = 0;
+    // tile mode for conv descriptors with k*k <= 25 (the two directions of one weight, consecutive in the table,
+    // share their tiles), row mode for the other conv descriptors whose source row fits the LDS copy; zero-size
+    // entries in the other numberings keep every begin array non-decreasing (a unit's descriptor is the LAST one
+    // at or below it)
+    int64_t items = 0, rows = 0, tiles = 0;
+    auto conv_desc = [&](int i) { return !d[i].edge && !d[i].gdn; };
+    auto src_ext = [&](const PackArgs& x, int& e0, int& e1) {   // source entries the tiles cover (padding included)
+        e0 = x.n_is_d0 ? x.Npad : x.Cpad;
+        e1 = x.n_is_d0 ? x.Cpad : x.Npad;
+    };
+    for (int i = 0; i < n; ++i) {
+        d[i].tilemode = d[i].pair = 0;
+        d[i].tile_begin = tiles;
+        if (!conv_desc(i) || d[i].k * d[i].k > 25 || !PACK_TILES) continue;
+        if (i > 0 && d[i - 1].tilemode == 1 && d[i - 1].pair) {
+            d[i].tilemode = 2;
+            continue;
+        }
+        PackArgs& x = d[i];
+        const int kk = x.k * x.k;
+        static const int cand[][2] = {{128, 64}, {64, 64}, {32, 64}, {32, 32}, {16, 32}, {16, 16}, {8, 16}, {8, 8}};
+        x.td0 = x.td1 = 0;
+        for (const auto& c : cand)
+            if ((int64_t)kk * (c[0] * (c[1] + 4) + 4) <= PACK_TILE_FLOATS) {
+                x.td0 = c[0];
+                x.td1 = c[1];
+                break;
+            }
+        x.tdp = x.td1 + 4;
+        x.tstride = x.td0 * x.tdp + 4;
+        x.d0real = x.n_is_d0 ? x.Nreal : x.Creal;
+        x.d1real = x.n_is_d0 ? x.Creal : x.Nreal;
+        x.mrl = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)(x.td1 * kk) - 1) / (uint64_t)(x.td1 * kk));
+        x.mkk = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)kk - 1) / (uint64_t)kk);
+        int e0, e1;
+        src_ext(x, e0, e1);
+        if (i + 1 < n && conv_desc(i + 1)) {
+            const PackArgs& y = d[i + 1];
+            if (y.w == x.w && y.mask == x.mask && y.k == x.k && y.D1 == x.D1 && y.n_is_d0 != x.n_is_d0 &&
+                (y.n_is_d0 ? y.Nreal : y.Creal) == x.d0real && (y.n_is_d0 ? y.Creal : y.Nreal) == x.d1real) {
+                int f0, f1;
+                src_ext(y, f0, f1);
+                e0 = std::max(e0, f0);
+                e1 = std::max(e1, f1);
+                x.pair = 1;
+            }
+        }
+        x.tilemode = 1;
+        x.tn1 = (e1 + x.td1 - 1) / x.td1;
+        tiles += (int64_t)((e0 + x.td0 - 1) / x.td0) * x.tn1;
+    }
     for (int i = 0; i < n; ++i) {
         d[i].items_pp = (int)((int64_t)d[i].Npad * d[i].Kp / 8);
-        d[i].rowmode = !d[i].edge && !d[i].gdn && d[i].Creal * d[i].k * d[i].k <= PACK_ROW_MAX;
+        d[i].rowmode = !d[i].tilemode && !d[i].edge && !d[i].gdn && d[i].Creal * d[i].k * d[i].k <= PACK_ROW_MAX;
         d[i].rpu = d[i].rowmode ? std::max(1, std::min(PACK_ROWS_PER_UNIT, PACK_ROW_MAX / (d[i].Creal * d[i].k * d[i].k)))
                                 : 1;
         d[i].item_begin = items;
         d[i].row_begin = rows;
+        if (d[i].tilemode)
+            continue;
         if (d[i].rowmode)
             rows += (d[i].Npad + d[i].rpu - 1) / d[i].rpu;
         else
             items += (int64_t)d[i].items_pp * d[i].nphase;
     }
-    for (int i = 0; i < n; ++i) d[i].rows_total = rows;
-    return rows + items;
+    for (int i = 0; i < n; ++i) {
+        d[i].rows_total = rows;
+        d[i].tiles_total = tiles;
+    }
+    return tiles + rows + items;
 }
 
 int cai_conv_pack_many(const void* descs, int32_t n, int dtype, int64_t total_items, void* stream) {

@@ -21,17 +21,20 @@
 
 namespace cai {
 
-// WGRAD job layout: one block per (output row n, slice of input channels q).  The slab row of n is [tap][Cq_pad]
-// (16-byte chunks of 4 channels); a block takes q4 chunks of every tap (q4 * k*k <= 256 threads, one chunk per
-// thread), sums them over the S splits in split order, transposes the slice through LDS and writes
-// dw[n][q][tap] for its channels -- one contiguous run of the torch layout.  (One block per whole row kept
-// 129-193 blocks per job: ~20 us per C2 halo layer on its own, the batched launch load-imbalanced.)
-__host__ __device__ __forceinline__ int wg_q4(int kk, int cq4) {
-    int q4 = 1;
-    while (q4 * 2 * kk <= 256 && q4 * 2 <= cq4) q4 *= 2;
-    return q4;
+// WGRAD job layout: one block per (rpb output rows n .. n + rpb - 1, slice of input channels q).  The slab row of n
+// is [tap][Cq_pad] (16-byte chunks of 4 channels); a block takes q4 chunks of every tap of each of its rows
+// (rpb * q4 * k*k <= 256 threads, one chunk per thread), sums them over the S splits in split order (loads in
+// batches of 16), transposes the slice through LDS from [tap][q] to the torch layout dw[n][q][tap] and writes it
+// -- contiguous runs of the torch layout.  (One block per whole row kept 129-193 blocks per job: ~20 us per C2
+// halo layer on its own, the batched launch load-imbalanced; power-of-two slices left 44 % of a 3x3 block's
+// threads and most of a 1x1 block's idle.)
+__host__ __device__ __forceinline__ void wg_shape(int kk, int cq4, int& q4, int& rpb) {
+    q4 = cq4 < 256 / kk ? cq4 : 256 / kk;
+    if (q4 < 1) q4 = 1;
+    rpb = 256 / (q4 * kk);
+    if (rpb < 1) rpb = 1;
 }
-constexpr int WG_TR_FLOATS = 4 * (256 + 64);   // 4 * q4 * (kk + 1) <= 4 * (256 + q4), q4 <= 64
+constexpr int WG_TR_FLOATS = 2048;   // rpb * 4 * q4 * (kk + 1) <= 4 * (256 + 256)
 
 __device__ __forceinline__ void wgrad_bias_body(const cai_reduce_job& J, int bid) {
     const float* __restrict__ bws = static_cast<const float*>(J.p[2]);
@@ -58,42 +61,56 @@ __device__ __forceinline__ void wgrad_slice_body(const cai_reduce_job& J, int bi
     const int S = J.i[0], Ng = J.i[1], ncols = J.i[2], Cq = J.i[3], Cq_pad = J.i[4], k = J.i[5];
     const int accumulate = J.i[6];
     const int kk = k * k, cq4 = Cq_pad >> 2, c4 = ncols >> 2;
-    const int q4 = wg_q4(kk, cq4), nsl = (cq4 + q4 - 1) / q4;
-    const int n = bid / nsl, c0 = (bid - (bid / nsl) * nsl) * q4;
-    const int t = threadIdx.x / q4, j = threadIdx.x - (threadIdx.x / q4) * q4, c = c0 + j;
-    const bool active = t < kk && c < cq4;
+    int q4, rpb;
+    wg_shape(kk, cq4, q4, rpb);
+    const int nsl = (cq4 + q4 - 1) / q4;
+    const int nb = bid / nsl, c0 = (bid - nb * nsl) * q4, n0 = nb * rpb;
+    const int per = q4 * kk, r = threadIdx.x / per, rem = threadIdx.x - r * per;
+    const int t = rem / q4, j = rem - t * q4, c = c0 + j, n = n0 + r;
+    const bool active = r < rpb && n < Ng && c < cq4;
     const int64_t slab4 = ((int64_t)Ng * ncols) >> 2;
-    const f32x4* src = reinterpret_cast<const f32x4*>(ws) + (int64_t)n * c4 + t * cq4 + c;
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int rpitch = 4 * q4 * (kk + 1);
     if (active) {
+        const f32x4* src = reinterpret_cast<const f32x4*>(ws) + (int64_t)n * c4 + t * cq4 + c;
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
         int sp = 0;
-        for (; sp + 8 <= S; sp += 8) {
-            f32x4 v[8];
+        for (; sp + 16 <= S; sp += 16) {
+            f32x4 v[16];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) v[i] = src[(int64_t)(sp + i) * slab4];
+            for (int i = 0; i < 16; ++i) v[i] = src[(int64_t)(sp + i) * slab4];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) acc += v[i];
+            for (int i = 0; i < 16; ++i) acc += v[i];
+        }
+        for (; sp + 4 <= S; sp += 4) {
+            f32x4 v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = src[(int64_t)(sp + i) * slab4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc += v[i];
         }
         for (; sp < S; ++sp) acc += src[(int64_t)sp * slab4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) tr[(4 * j + e) * (kk + 1) + t] = acc[e];
+        for (int e = 0; e < 4; ++e) tr[r * rpitch + (4 * j + e) * (kk + 1) + t] = acc[e];
     }
     __syncthreads();
     const int qa = 4 * c0, qb = min(Cq, 4 * (c0 + q4));
     const int len = (qb - qa) * kk;
-    float* d = dw + ((int64_t)n * Cq + qa) * kk;
-    for (int i = threadIdx.x; i < len; i += 256) {
-        const int ql = i / kk, tt = i - (i / kk) * kk;
-        const float v = tr[ql * (kk + 1) + tt];
-        d[i] = accumulate ? d[i] + v : v;
+    const int rows = min(rpb, Ng - n0);
+    for (int i = threadIdx.x; i < rows * len; i += 256) {
+        const int rr = i / len, ii = i - rr * len;
+        const int ql = ii / kk, tt = ii - ql * kk;
+        const float v = tr[rr * rpitch + ql * (kk + 1) + tt];
+        float* d = dw + ((int64_t)(n0 + rr) * Cq + qa) * kk + ii;
+        *d = accumulate ? *d + v : v;
     }
 }
 
-// blocks [0, wblocks): the (row, channel-slice) weight blocks; then the bias blocks
+// blocks [0, wblocks): the (rows, channel-slice) weight blocks; then the bias blocks
 __device__ __forceinline__ void wgrad_reduce_body(const cai_reduce_job& J, int bid, float* tr) {
     const int Ng = J.i[1], Cq_pad = J.i[4], k = J.i[5];
-    const int cq4 = Cq_pad >> 2, q4 = wg_q4(k * k, cq4);
-    const int wblocks = Ng * ((cq4 + q4 - 1) / q4);
+    int q4, rpb;
+    wg_shape(k * k, Cq_pad >> 2, q4, rpb);
+    const int wblocks = (Ng + rpb - 1) / rpb * ((Cq_pad / 4 + q4 - 1) / q4);
     if (bid >= wblocks) {
         wgrad_bias_body(J, bid - wblocks);
         return;
@@ -102,8 +119,9 @@ __device__ __forceinline__ void wgrad_reduce_body(const cai_reduce_job& J, int b
 }
 
 int wgrad_job_blocks(int Ng, int Cq_pad, int k, int nbias_blocks) {
-    const int cq4 = Cq_pad >> 2, q4 = wg_q4(k * k, cq4);
-    return Ng * ((cq4 + q4 - 1) / q4) + nbias_blocks;
+    int q4, rpb;
+    wg_shape(k * k, Cq_pad >> 2, q4, rpb);
+    return (Ng + rpb - 1) / rpb * ((Cq_pad / 4 + q4 - 1) / q4) + nbias_blocks;
 }
 
 __device__ __forceinline__ void gdn_reduce_body(const cai_reduce_job& J, int bid, f32x4 (*red)[17]) {

@@ -967,3 +967,51 @@ def test_deferred_reduce_jobs_bit_identical(cuda, batch):
            for i, ((a0, a1), (b0, b1)) in enumerate(zip(outs_def, outs_imm))
            if not (torch.equal(a0, b0) and torch.equal(a1, b1))]
     assert not bad, bad
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_pack_many_matches_pack_weight(cuda, dtype):
+    """The model-wide pack launch (Prepacker -> cai_conv_pack_many: source tiles shared by a weight's two
+    directions, row and item modes for the rest) writes every packed operand bit for bit as the per-layer
+    cai_conv_pack_weight does, padding included: stride-1 / stride-2 convs, 1x1s, phase-decomposed deconvs,
+    a masked 5x5, channel counts off the tile and padding grids."""
+    import ctypes
+
+    from compressai._native import lib
+    from compressai._ops import _p, _stream, conv_geom, dcode
+    from compressai._prepack import Prepacker
+    from compressai.layers.conv import Conv2d, ConvTranspose2d
+    from compressai.layers.layers import MaskedConv2d
+
+    torch.manual_seed(11)
+    mods = torch.nn.ModuleList([
+        Conv2d(3, 192, 3, 1, 1), Conv2d(192, 192, 3, 1, 1), Conv2d(192, 96, 1), Conv2d(96, 192, 1),
+        Conv2d(128, 128, 5, 2, 2), Conv2d(12, 200, 3, 2, 1), Conv2d(288, 1152, 3, 1, 1), Conv2d(40, 24, 7, 1, 3),
+        ConvTranspose2d(192, 128, 5, 2, 2, output_padding=1), ConvTranspose2d(128, 72, 3, 2, 1, output_padding=1),
+        MaskedConv2d(192, 384, 5, 1, 2),
+    ]).to(cuda)
+    for m in mods:
+        m.weight.data.uniform_(-1, 1)
+    packer = Prepacker(mods)
+    plan = packer._build(dtype)
+    assert plan is not None
+    packer._plans[dtype] = plan
+    lib.cai_conv_pack_many(_p(plan["descs"]), plan["n"], dcode(dtype), plan["total"], _stream())
+    torch.cuda.synchronize()
+    checked = 0
+    for m in mods:
+        spec = m._spec()
+        g = conv_geom(spec, 1, m.in_channels, 16, 16, m.out_channels)
+        mask = m.mask if isinstance(m, MaskedConv2d) else None
+        for direction in (0, 1):
+            got = packer.lookup(m.weight, dtype, direction)
+            if got is None:
+                continue
+            ref = torch.full_like(got, 0x5A)
+            rc = lib.cai_conv_pack_weight(ctypes.byref(g), dcode(dtype), direction, _p(m.weight.detach()),
+                                          _p(mask) if mask is not None else None, _p(ref), _stream())
+            assert rc == 0
+            torch.cuda.synchronize()
+            assert torch.equal(got, ref), (type(m).__name__, m.weight.shape, direction)
+            checked += 1
+    assert checked >= 2 * len(mods) - 2

@@ -260,3 +260,30 @@ def test_resunit_backward_uses_prepacked_weights(cuda, monkeypatch):
     y.float().sum().backward()
     torch.cuda.synchronize()
     assert calls == [], calls
+
+
+def test_residual_block_fused_backward_matches_chain(cuda, monkeypatch):
+    """ResidualBlock (identity skip) as one ResidualBlockFn node: the same forward bits as the per-module chain,
+    and x's two gradients summed in conv1's dgrad epilogue (one bf16 rounding instead of two) within bf16
+    tolerance of the chain's autograd sum; parameter gradients identical in kind."""
+    import compressai.layers as L
+    from compressai.layers.layers import ResidualBlock
+
+    torch.manual_seed(5)
+    mod = L.ResidualBlock(192, 192).to(cuda)
+    x0 = _pm(torch.randn(2, 192, 32, 32, device=cuda))
+    g = torch.randn(2, 192, 32, 32, device=cuda)
+    outs = {}
+    for fuse in (True, False):
+        monkeypatch.setattr(ResidualBlock, "fuse_residual", fuse)
+        mod.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = mod(x)
+        y.float().backward(g)
+        torch.cuda.synchronize()
+        outs[fuse] = (y.detach().float(), x.grad.float(), {k: p.grad.clone() for k, p in mod.named_parameters()})
+    assert torch.equal(outs[True][0], outs[False][0])
+    assert relerr(outs[True][1], outs[False][1]) < 1e-2
+    for k in outs[True][2]:
+        assert relerr(outs[True][2][k], outs[False][2][k]) < 1e-2, k
