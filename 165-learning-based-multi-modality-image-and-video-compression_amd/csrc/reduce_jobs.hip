@@ -29,8 +29,10 @@ namespace cai {
 // halo layer on its own, the batched launch load-imbalanced; power-of-two slices left 44 % of a 3x3 block's
 // threads and most of a 1x1 block's idle.)
 __host__ __device__ __forceinline__ void wg_shape(int kk, int cq4, int& q4, int& rpb) {
-    q4 = cq4 < 256 / kk ? cq4 : 256 / kk;
-    if (q4 < 1) q4 = 1;
+    int qmax = 256 / kk;
+    if (qmax < 1) qmax = 1;
+    const int nsl = (cq4 + qmax - 1) / qmax;
+    q4 = (cq4 + nsl - 1) / nsl;   // equal slices: 5x5 at 128 channels 8 + 8 + 8 + 8, not 10 + 10 + 10 + 2
     rpb = 256 / (q4 * kk);
     if (rpb < 1) rpb = 1;
 }
