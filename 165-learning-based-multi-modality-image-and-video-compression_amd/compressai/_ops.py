@@ -1002,12 +1002,17 @@ def _unit_ctxs(subs):
     return out
 
 
-def _chain_backward(subs, gy, dx_res2=None):
+def _chain_backward(subs, gy, dx_res2=None, before_first=None):
     """-> (gradient of the chain input, flat parameter gradients); dx_res2: one more gradient of the chain input,
-    summed in the first unit's dgrad epilogue."""
+    summed in the first unit's dgrad epilogue (a callable: evaluated right before that unit, after
+    `before_first()`, so another stream's producer can run under the later units)."""
     grads = []
     g = gy
     for k in range(len(subs) - 1, -1, -1):
+        if k == 0 and before_first is not None:
+            before_first()
+        if k == 0 and callable(dx_res2):
+            dx_res2 = dx_res2()
         u = subs[k]
         if isinstance(u, _FusedUnit):
             if k == 0 and dx_res2 is not None:
@@ -1053,6 +1058,25 @@ class ResidualBlockFn(torch.autograd.Function):
         return dx, None, None, dw1, db1, dw2, db2
 
 
+# AttentionBlock branches on two streams when their launches are small (<= CAI_AB_STREAM_PX pixels: C4's 16 x 16
+# latents at B = 4 run the units on 16 blocks); CAI_AB_STREAM=0 keeps them serial (A/B)
+_AB_STREAM = os.environ.get("CAI_AB_STREAM", "1") == "1"
+_AB_STREAM_PX = int(os.environ.get("CAI_AB_STREAM_PX", "8192"))
+_AB_SIDE = {}
+
+
+def _ab_side(x):
+    if not (_AB_STREAM and x.is_cuda and _ledger.active() is None):
+        return None
+    B, _, H, W = x.shape
+    if B * H * W > _AB_STREAM_PX:
+        return None
+    s = _AB_SIDE.get(x.device)
+    if s is None:
+        s = _AB_SIDE[x.device] = torch.cuda.Stream(device=x.device)
+    return s
+
+
 class AttentionBlockFn(torch.autograd.Function):
     """AttentionBlock (layers.py:196-244) as one autograd node: y = a * sigmoid(b) + x with a = conv_a(x) and
     b = conv_b(x) (three ResidualUnits each, as in ResidualChainFn; conv_b's 1x1 conv after its chain).  x's three
@@ -1065,10 +1089,26 @@ class AttentionBlockFn(torch.autograd.Function):
     def forward(ctx, x, specs_a, specs_b, spec_b3, *params):
         need = ctx.needs_input_grad   # (x, specs_a, specs_b, spec_b3, *params)
         pa, pb, (w3, b3) = params[:18], params[18:36], params[36:38]
-        a, ctx.sub_a = _chain_forward(x, specs_a, True, pa, need[0], need[4:22])
-        hb, ctx.sub_b = _chain_forward(x, specs_b, True, pb, need[0], need[22:40])
         c3 = _SubCtx((True, need[40], need[41], False, False))
-        bb = ConvFn.forward(c3, hb, w3, b3, spec_b3)
+        side = _ab_side(x)
+        ctx.side = side
+        if side is None:
+            a, ctx.sub_a = _chain_forward(x, specs_a, True, pa, need[0], need[4:22])
+            hb, ctx.sub_b = _chain_forward(x, specs_b, True, pb, need[0], need[22:40])
+            bb = ConvFn.forward(c3, hb, w3, b3, spec_b3)
+        else:
+            # small maps: the two branches' launches fill a fraction of the GPU each -- branch b on the side stream
+            main = torch.cuda.current_stream(x.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                hb, ctx.sub_b = _chain_forward(x, specs_b, True, pb, need[0], need[22:40])
+                bb = ConvFn.forward(c3, hb, w3, b3, spec_b3)
+            a, ctx.sub_a = _chain_forward(x, specs_a, True, pa, need[0], need[4:22])
+            main.wait_stream(side)
+            x.record_stream(side)
+            for t in [hb, bb] + [t for c in _unit_ctxs(ctx.sub_b) + [c3] for t in c.saved_tensors]:
+                if isinstance(t, torch.Tensor):
+                    t.record_stream(main)
         cg = _SubCtx((True, True, True, False))
         y = GateFn.forward(cg, a, bb, x, True)
         ctx.c3, ctx.cg = c3, cg
@@ -1079,9 +1119,25 @@ class AttentionBlockFn(torch.autograd.Function):
     def backward(ctx, gy):
         with _unstash(ctx):
             da, db, gx, _ = GateFn.backward(ctx.cg, gy)
-            dhb, dw3, db3, _, _ = ConvFn.backward(ctx.c3, db)
-            xb, flat_b = _chain_backward(ctx.sub_b, dhb, dx_res2=gx)
-            dx, flat_a = _chain_backward(ctx.sub_a, da, dx_res2=xb)
+            side = ctx.side
+            if side is None or _ledger.active() is not None:
+                dhb, dw3, db3, _, _ = ConvFn.backward(ctx.c3, db)
+                xb, flat_b = _chain_backward(ctx.sub_b, dhb, dx_res2=gx)
+                dx, flat_a = _chain_backward(ctx.sub_a, da, dx_res2=xb)
+            else:
+                # branch b on the side stream under branch a's later units; a's first unit waits for it (its dgrad
+                # epilogue adds b's input gradient)
+                main = torch.cuda.current_stream(gy.device)
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    dhb, dw3, db3, _, _ = ConvFn.backward(ctx.c3, db)
+                    xb, flat_b = _chain_backward(ctx.sub_b, dhb, dx_res2=gx)
+                db.record_stream(side)
+                gx.record_stream(side)
+                for t in [xb, dw3, db3, *flat_b]:
+                    if isinstance(t, torch.Tensor):
+                        t.record_stream(main)
+                dx, flat_a = _chain_backward(ctx.sub_a, da, dx_res2=xb, before_first=lambda: main.wait_stream(side))
         return (dx, None, None, None, *flat_a, *flat_b, dw3, db3)
 
 

@@ -287,3 +287,31 @@ def test_residual_block_fused_backward_matches_chain(cuda, monkeypatch):
     assert relerr(outs[True][1], outs[False][1]) < 1e-2
     for k in outs[True][2]:
         assert relerr(outs[True][2][k], outs[False][2][k]) < 1e-2, k
+
+
+@pytest.mark.parametrize("H", [8, 16])
+def test_attention_block_two_streams_bit_identical(cuda, monkeypatch, H):
+    """Small-map AttentionBlocks run branch b on a side stream (forward, and its backward under branch a's later
+    units): the same kernels on the same data, so output and every gradient are bit-identical to the serial
+    order."""
+    import compressai.layers as L
+    from compressai import _ops
+
+    torch.manual_seed(9)
+    mod = L.AttentionBlock(192).to(cuda)
+    x0 = _pm(torch.randn(4, 192, H, H, device=cuda))
+    g = torch.randn(4, 192, H, H, device=cuda)
+    outs = {}
+    for on in (True, False):
+        monkeypatch.setattr(_ops, "_AB_STREAM", on)
+        mod.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = mod(x)
+        y.float().backward(g)
+        torch.cuda.synchronize()
+        outs[on] = (y.detach().float(), x.grad.float(), {k: p.grad.clone() for k, p in mod.named_parameters()})
+    assert torch.equal(outs[True][0], outs[False][0])
+    assert torch.equal(outs[True][1], outs[False][1])
+    for k in outs[True][2]:
+        assert torch.equal(outs[True][2][k], outs[False][2][k]), k
