@@ -1058,10 +1058,11 @@ class ResidualBlockFn(torch.autograd.Function):
         return dx, None, None, dw1, db1, dw2, db2
 
 
-# AttentionBlock branches on two streams when their launches are small (<= CAI_AB_STREAM_PX pixels: C4's 16 x 16
-# latents at B = 4 run the units on 16 blocks); CAI_AB_STREAM=0 keeps them serial (A/B)
+# AttentionBlock branches (and the skip branches of ResidualBlockWithStride / ResidualBlockUpsample) on two streams
+# when their launches are small (<= CAI_AB_STREAM_PX input pixels: C4's 16 x 16 latents at B = 4 run the units on 16
+# blocks, its 64 x 64 maps on 256; profiles/r04_attention_two_streams_ab.log); CAI_AB_STREAM=0 keeps them serial
 _AB_STREAM = os.environ.get("CAI_AB_STREAM", "1") == "1"
-_AB_STREAM_PX = int(os.environ.get("CAI_AB_STREAM_PX", "8192"))
+_AB_STREAM_PX = int(os.environ.get("CAI_AB_STREAM_PX", "16384"))
 _AB_SIDE = {}
 
 

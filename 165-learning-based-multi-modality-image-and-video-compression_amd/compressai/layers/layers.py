@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 
 from .._native import ACT_LEAKY, ACT_NONE, ACT_RELU, MASK_LEAKY, MASK_POS
-from .._ops import AddActFn, AttentionBlockFn, GateFn, ResidualBlockFn, ResidualChainFn, residual_fusable
+from .._ops import AddActFn, AttentionBlockFn, GateFn, ResidualBlockFn, ResidualChainFn, _ab_side, residual_fusable
 from .conv import Conv2d, ConvTranspose2d, PixelShuffle, Sequential
 from .gdn import GDN
 
@@ -59,6 +59,13 @@ def subpel_conv3x3(in_ch: int, out_ch: int, r: int = 1) -> nn.Module:
     return Sequential(Conv2d(in_ch, out_ch * r ** 2, kernel_size=3, padding=1), PixelShuffle(r))
 
 
+def _join(main, side, x, identity):
+    """The side branch joins the caller's stream; caching-allocator bookkeeping of the tensors that crossed."""
+    main.wait_stream(side)
+    x.record_stream(side)
+    identity.record_stream(main)
+
+
 class ResidualBlockWithStride(nn.Module):
     """layers.py:97-129: conv3x3(s) -> LeakyReLU -> conv3x3 -> GDN, + skip (conv1x1(s) or identity)."""
 
@@ -71,10 +78,19 @@ class ResidualBlockWithStride(nn.Module):
         self.skip = conv1x1(in_ch, out_ch, stride=stride) if (stride != 1 or in_ch != out_ch) else None
 
     def forward(self, x):
+        side = _ab_side(x) if self.skip is not None else None
+        if side is not None:   # the skip conv on the side stream (autograd runs its backward there too)
+            main = torch.cuda.current_stream(x.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                identity = self.skip(x)
         out = self.conv1.run(x, act=ACT_LEAKY, act_param=_SLOPE, act_bwd_downstream=True)
         out = self.conv2.run(out, in_mask=MASK_LEAKY, in_mask_param=_SLOPE)
         out = self.gdn(out)
-        identity = self.skip(x) if self.skip is not None else x
+        if side is not None:
+            _join(main, side, x, identity)
+        else:
+            identity = self.skip(x) if self.skip is not None else x
         return AddActFn.apply(out, identity, ACT_NONE, 0.0)
 
 
@@ -90,10 +106,19 @@ class ResidualBlockUpsample(nn.Module):
         self.upsample = subpel_conv3x3(in_ch, out_ch, upsample)
 
     def forward(self, x):
+        side = _ab_side(x)
+        if side is not None:   # the upsampling branch on the side stream (autograd runs its backward there too)
+            main = torch.cuda.current_stream(x.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                identity = self.upsample(x)
         out = self.subpel_conv(x, act=ACT_LEAKY, act_param=_SLOPE, act_bwd_downstream=True)
         out = self.conv.run(out, in_mask=MASK_LEAKY, in_mask_param=_SLOPE)
         out = self.igdn(out)
-        identity = self.upsample(x)
+        if side is not None:
+            _join(main, side, x, identity)
+        else:
+            identity = self.upsample(x)
         return AddActFn.apply(out, identity, ACT_NONE, 0.0)
 
 

@@ -315,3 +315,29 @@ def test_attention_block_two_streams_bit_identical(cuda, monkeypatch, H):
     assert torch.equal(outs[True][1], outs[False][1])
     for k in outs[True][2]:
         assert torch.equal(outs[True][2][k], outs[False][2][k]), k
+
+
+@pytest.mark.parametrize("kind", ["stride", "upsample"])
+def test_residual_skip_branch_side_stream_bit_identical(cuda, monkeypatch, kind):
+    """ResidualBlockWithStride's skip conv / ResidualBlockUpsample's upsampling branch on the side stream (small
+    maps): output and every gradient bit-identical to the serial order."""
+    import compressai.layers as L
+    from compressai import _ops
+
+    torch.manual_seed(13)
+    mod = (L.ResidualBlockWithStride(192, 192, 2) if kind == "stride" else L.ResidualBlockUpsample(192, 192, 2)).to(cuda)
+    x0 = _pm(torch.randn(4, 192, 16, 16, device=cuda))
+    outs = {}
+    for on in (True, False):
+        monkeypatch.setattr(_ops, "_AB_STREAM", on)
+        mod.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = mod(x)
+        y.float().backward(torch.sin(torch.arange(y.numel(), device=cuda, dtype=torch.float32)).view_as(y))
+        torch.cuda.synchronize()
+        outs[on] = (y.detach().float(), x.grad.float(), {k: p.grad.clone() for k, p in mod.named_parameters()})
+    assert torch.equal(outs[True][0], outs[False][0])
+    assert torch.equal(outs[True][1], outs[False][1])
+    for k in outs[True][2]:
+        assert torch.equal(outs[True][2][k], outs[False][2][k]), k
