@@ -118,6 +118,38 @@ class _WgradLaunch:
         return False
 
 
+# Deferred weight-gradient partial kernels of SMALL layers (<= CAI_WGRAD_SIDE_PX G pixels) on the side stream: they
+# touch only their slabs until the deferred reduce (which waits for the side stream), so they can run under the
+# input-gradient chain; 0 = off.
+_WGRAD_SIDE_PX = int(os.environ.get("CAI_WGRAD_SIDE_PX", "0"))
+
+
+class _SideDeferred:
+    def __init__(self, device, npix: int, *inputs):
+        self.side = None
+        if not (_WGRAD_SIDE_PX and npix <= _WGRAD_SIDE_PX and _ledger.active() is None):
+            return
+        side = _WSIDE.get(device)
+        if side is None:
+            side = _WSIDE[device] = torch.cuda.Stream(device=device)
+        self.side, self.inputs = side, inputs
+
+    def __enter__(self):
+        if self.side is not None:
+            self.side.wait_stream(torch.cuda.current_stream(self.side.device))
+            self._ctx = torch.cuda.stream(self.side)
+            self._ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.side is not None:
+            self._ctx.__exit__(*exc)
+            for t in self.inputs:
+                if t is not None:
+                    t.record_stream(self.side)
+        return False
+
+
 # ---------------------------------------------------------------------------
 # deferred parameter-gradient reduces (cai_reduce_jobs, csrc/reduce_jobs.hip)
 # ---------------------------------------------------------------------------
@@ -693,11 +725,13 @@ def conv_wgrad(g, dt, xpm, xld, in_abs, gpm, gld, wparam, bparam, weight, has_bi
     fl, nb = _ledger.conv_cost(g, _es(dt), 2)
     st = _stream()
     if defer_reduce_ok(direct):
-        wws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        job = ReduceJob()
-        lib.cai_conv_wgrad_deferred(ctypes.byref(g), code, _p(xpm), xld, int(in_abs), 0, _p(gpm), gld, _p(dw),
-                                    _p(db), 1, _p(wws), nbytes, st, ctypes.byref(job))
-        defer_job(job, dev, wws)
+        npix = g.batch * (g.in_h * g.in_w if g.transposed else g.out_h * g.out_w)
+        with _SideDeferred(dev, npix, xpm, gpm):
+            wws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            job = ReduceJob()
+            lib.cai_conv_wgrad_deferred(ctypes.byref(g), code, _p(xpm), xld, int(in_abs), 0, _p(gpm), gld, _p(dw),
+                                        _p(db), 1, _p(wws), nbytes, _stream(), ctypes.byref(job))
+            defer_job(job, dev, wws)
     else:
         with _WgradLaunch(dev, direct, xpm, gpm):
             wws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
@@ -931,14 +965,16 @@ def _resunit_wgrad(u: "_FusedUnit", xpm, h1, h2, g_a, g_b, gcc, gcld):
                          gc_ld=gcld, dwa=dw0.data_ptr(), dba=db0.data_ptr(), dwb=dw2.data_ptr(), dbb=db2.data_ptr(),
                          dwc=dw4.data_ptr(), dbc=db4.data_ptr(), accumulate=int(direct))
     nbytes = lib.cai_resunit_wgrad_workspace_bytes(ctypes.byref(A))
-    wws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     st = _stream()
     if defer_reduce_ok(direct):
-        jobs = (ReduceJob * 3)()
-        lib.cai_resunit_wgrad(ctypes.byref(A), _p(wws), nbytes, st, jobs)
-        for j in jobs:
-            defer_job(j, dev, wws)
+        with _SideDeferred(dev, B * H * W, xpm, h1, h2, g_a, g_b, gcc):
+            wws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            jobs = (ReduceJob * 3)()
+            lib.cai_resunit_wgrad(ctypes.byref(A), _p(wws), nbytes, _stream(), jobs)
+            for j in jobs:
+                defer_job(j, dev, wws)
     else:
+        wws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
         nh = n // 2
         P = B * H * W
         fl = 2.0 * P * (nh * n * 2 + 9 * nh * nh)
