@@ -1211,30 +1211,14 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvArgs a, int
 // cells) in LDS once and runs the NA*NC taps x two 32-channel halves out of it.  The weights stream through
 // the same hand-ordered LDS-DMA ring as conv_halo_kernel (one 16-byte DMA per lane per step, NSTB-1 steps
 // ahead); the next chunk's footprint is loaded into registers while the current one is consumed.
-#ifndef CAI_HALO_PH_MIX
-#define CAI_HALO_PH_MIX 0
-#endif
-#ifndef CAI_HALO_PH_PAIRS
-#define CAI_HALO_PH_PAIRS 0
-#endif
-#ifndef CAI_HALO_PH_PP
-#define CAI_HALO_PH_PP 0
-#endif
-#ifndef CAI_PH_PROBE
-#define CAI_PH_PROBE 0
-#endif
-#ifndef CAI_HALO_PH_PP_PRIO
-#define CAI_HALO_PH_PP_PRIO 1
-#endif
-
-
-// HALF: the 256-thread form (4 waves, 8 x 16 tiles, two workgroups per CU): the two waves that share a SIMD
-// belong to different workgroups, so one's barriers, footprint prologue and epilogue overlap the other's MFMAs
-// (the 512-thread form puts both waves of a SIMD behind the same barrier).
-template <int NA, int NC, int BN_ = 128, bool HALF = false>
+// (Variants measured slower and removed in round 5 -- one barrier per two steps, a ping-pong wave schedule,
+// the four phases of a tile interleaved on one XCD, the 256-thread form, a 6-stage ring: DESIGN.md section 8,
+// the round-4 tree of this file.)  conv_halo_quad_kernel (conv_quad.hip) runs all four phases of a tile from
+// one staged footprint for the large 128-channel layers.
+template <int NA, int NC, int BN_ = 128>
 struct HaloPhCfg {
-    static constexpr int TH = 8, TW = HALF ? 16 : 32, BM = TH * TW, BN = BN_, WM = 4, WN = HALF ? 1 : 2, CK = 64;
-    static constexpr int NT = HALF ? 256 : 512;
+    static constexpr int TH = 8, TW = 32, BM = TH * TW, BN = BN_, WM = 4, WN = 2, CK = 64;
+    static constexpr int NT = 512;
     // 16-byte weight DMAs per lane per step: NT lanes stage NT / 4 rows x 64 bytes per round; DPS rounds cover
     // the BN rows (BN = 192 on 512 lanes: rows 128..255 of the second round past the tile read the zero page
     // into unread cells)
@@ -1245,81 +1229,30 @@ struct HaloPhCfg {
     static constexpr int PATCH = 8 * PLANE * 16;
     static constexpr int NPI = (8 * NPOS + NT - 1) / NT;
     static constexpr int NTAP = NA * NC, NST = 2 * NTAP;       // steps per chunk: (half, tap)
-#ifndef CAI_HALO_PH_NSTB6
-#define CAI_HALO_PH_NSTB6 0
-#endif
-    // NST % NSTB == 0: a step's stage is t % NSTB.  A 6-stage ring (CAI_HALO_PH_NSTB6=1) measured slower on
-    // MI355X (C2 8180 vs 8430 patches/s; the big launch 91.6 vs 88 us): the latency is not in the ring
-    // PAIRS (CAI_HALO_PH_PAIRS=1, A/B): one workgroup barrier per two steps.  At an even step t both stages freed
-    // since the last barrier (steps t - 1 and t) refill with steps t + NSTB - 1 and t + NSTB, and the barrier
-    // certifies steps t + 1 and t + 2 -- the operands of both steps until the next one; NSTB = 6 (4 for the
-    // 8-step 2x2 phase) leaves NSTB - 2 steps between a DMA and its barrier.
-    // PP (CAI_HALO_PH_PP=1): ping-pong -- waves 4-7 run one barrier behind waves 0-3 (wave w and w + 4 share a
-    // SIMD), so one group's fragment reads and waits overlap the other group's MFMAs.  Waves 0-3 issue every weight
-    // DMA (two per lane and step, PP_D steps ahead) into an NSTB-deep ring (NSTB >= PP_D + 1: the lagging group
-    // still reads the stage a DMA would overwrite otherwise); the footprint is double-buffered, the next chunk's
-    // stored at step NST - 3 (the lagging group's stores retire one barrier before the leading group's first read).
-    // PP2 (CAI_HALO_PH_PP=2): both groups issue their own rows' DMAs (one per lane and step, as the lockstep form),
-    // PP_D = 4 steps ahead (the lagging group retires its half two steps after issue) into a 6 / 8-deep ring
-    static constexpr bool PP = CAI_HALO_PH_PP && DPS == 1 && !HALF;
-    static constexpr bool PP2 = PP && CAI_HALO_PH_PP == 2;
-    static constexpr int PP_D = PP2 ? 4 : 3;
-    static constexpr bool PAIRS = CAI_HALO_PH_PAIRS && DPS == 1 && !HALF && NST % 2 == 0 && !PP;
-    static constexpr int NSTB = PP ? (NST % 6 == 0 ? 6 : (PP2 ? 8 : 4))
-                                   : PAIRS ? (NST % 6 == 0 ? 6 : 4)
-                                           : ((CAI_HALO_PH_NSTB6 && NST % 6 == 0) ? 6 : (NST % 3 == 0 ? 3 : 2));
-    static constexpr int NPATCH = PP ? 2 : 1;
+    // NST % NSTB == 0: a step's stage is t % NSTB (a 6-stage ring measured slower: C2 8180 vs 8430 patches/s)
+    static constexpr int NSTB = NST % 3 == 0 ? 3 : 2;
     static constexpr int BSTAGE = DPS * NT * 16;
     // BN > 128: register-direct epilogue only (no LDS staging buffer), see conv_epilogue_rows_t
     static constexpr int EPI = BN > 128 ? 0 : BM * (BN + 4) * 4;
-    static constexpr int BYTES = (NPATCH * PATCH + NSTB * BSTAGE > EPI) ? NPATCH * PATCH + NSTB * BSTAGE : EPI;
-    static_assert(PP ? (NPI <= NST - 3 && NST % NSTB == 0 && NSTB >= PP_D + 1)
-                     : PAIRS ? (NPI <= NST + 2 - NSTB && NST % NSTB == 0) : NPI <= NST - NSTB,
-                  "the next chunk's footprint must retire before the chunk's last step");
+    static constexpr int BYTES = (PATCH + NSTB * BSTAGE > EPI) ? PATCH + NSTB * BSTAGE : EPI;
+    static_assert(NPI <= NST - NSTB, "the next chunk's footprint must retire before the chunk's last step");
 };
 
-// PP: the loads group A issued after the weight DMA of step t + 1 (issued at step t + 1 - PP_D = t - 2): the two
-// DMAs of step t - 1 and the footprint cells of steps t - 2 and t - 1 (one per step below npi)
-__host__ __device__ constexpr int halo_younger_pp(int t, int npi) {
-    return 2 + ((t >= 2 && t - 2 < npi) ? 1 : 0) + ((t >= 1 && t - 1 < npi) ? 1 : 0);
-}
-__host__ __device__ constexpr int halo_cells_in(int lo, int hi, int npi) {   // cells issued at steps lo .. hi
-    int n = 0;
-    for (int j = lo; j <= hi; ++j) n += (j >= 0 && j < npi) ? 1 : 0;
-    return n;
-}
-// PP2, leading group at step t: its DMA of step t + 1 (issued at step t - 3); younger: its DMAs of steps t - 2,
-// t - 1 and the cells of steps t - 3 .. t - 1
-__host__ __device__ constexpr int halo_younger_pp2a(int t, int npi) { return 2 + halo_cells_in(t - 3, t - 1, npi); }
-// PP2, lagging group at step t: its DMA of step t + 2 (the leading group reads it after the next barrier; issued
-// at step t - 2); younger: its DMA of step t - 1 and the cells of steps t - 2, t - 1
-__host__ __device__ constexpr int halo_younger_pp2b(int t, int npi) { return 1 + halo_cells_in(t - 2, t - 1, npi); }
-
-// PAIRS: the loads issued after step t + 2's weight DMA that an even step t's wait leaves in flight -- the DMAs of
-// the even steps after t' = t + 2 - NSTB (two each), the footprint cells issued at steps [t', t - 1] (j < NPI)
-// and the four fence loads after cell NPI - 1
-__host__ __device__ constexpr int halo_younger_pairs(int t, int nstb, int npi) {
-    const int lo = t + 2 - nstb, lo0 = lo > 0 ? lo : 0;
-    const int hi = t - 1 < npi - 1 ? t - 1 : npi - 1;
-    const int cells = hi >= lo0 ? hi - lo0 + 1 : 0;
-    const int fences = (npi - 1 >= lo && npi - 1 <= t - 1) ? 4 : 0;
-    return nstb - 4 + cells + fences;
-}
 
 // GATHER = false: the s^2-phase form (tap (ty, tx) reads footprint cell (NA-1-ty, NC-1-tx) from an origin
 // NA-1 / NC-1 before dy0 / dx0).  GATHER = true: a stride-1 gather convolution (Conv2d k3 s1 forward): tap
 // (ty, tx) = kernel (kh, kw) reads cell (ty, tx) from the origin dy0 = -pad.  n0: the tile's first output
 // channel (grid y).
-template <int NA, int NC, int BN_ = 128, bool GATHER = false, bool HALF = false>
+template <int NA, int NC, int BN_ = 128, bool GATHER = false>
 __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* smem, int ph, int split, int bid,
                                                      int tiles_x, int tiles_y, int n0 = 0) {
-    using H = HaloPhCfg<NA, NC, BN_, HALF>;
+    using H = HaloPhCfg<NA, NC, BN_>;
     constexpr int BM = H::BM, BN = H::BN, WM = H::WM, WN = H::WN, DPS = H::DPS, NT = H::NT;
     constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
     constexpr int NPI = H::NPI, NTAP = H::NTAP, NST = H::NST, NSTB = H::NSTB;
     static_assert(WM * WN == NT / 64 && WTM == 2 * H::TW && H::BYTES <= 160 * 1024, "halo phase tile");
     char* const patch = smem;
-    char* const bring = smem + H::NPATCH * H::PATCH;
+    char* const bring = smem + H::PATCH;
 
     const PhaseDesc& P = a.ph[ph];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1398,7 +1331,7 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
         const int n = wn * WTN + tn * 16 + i16;
-        bpos[tn] = H::NPATCH * H::PATCH + (4 * n + (g_ ^ (((n >> 3) & 1) * 3))) * 16;
+        bpos[tn] = H::PATCH + (4 * n + (g_ ^ (((n >> 3) & 1) * 3))) * 16;
     }
     auto read_frags = [&](int t, u32x4 (&fa)[TM], u32x4 (&fb)[TN]) {
         const int hf = t / NTAP, tap = t - hf * NTAP;
@@ -1417,194 +1350,7 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-#if CAI_PH_PROBE
-    // diagnostics (-DCAI_PH_PROBE=1, printf from sampled blocks): s_memtime totals per wave of the prologue, the
-    // counted vmcnt waits, the lgkmcnt waits, the barrier waits and the step bodies (lockstep form)
-    unsigned long long pr_t0 = __builtin_amdgcn_s_memtime(), pr_vm = 0, pr_lg = 0, pr_bar = 0, pr_body = 0, pr_pro = 0;
-#endif
     u32x4 fa[TM], fb[TN];
-    if constexpr (H::PP) {
-        constexpr int D = H::PP_D;
-        const int wv = __builtin_amdgcn_readfirstlane(wid);
-        const bool grpA = wv < 4;
-        // group A lane la stages weight rows la >> 2 and (la >> 2) + 64 (16-byte slots as in the one-DMA layout)
-        const int la = (wv & 3) * 64 + lane;
-        const int bna = la >> 2, bsa = (la & 3) ^ (((bna >> 3) & 1) * 3);
-        const char* WrA0 = n0 + bna < a.Npad
-                               ? reinterpret_cast<const char*>(a.w) + (P.w_off + (int64_t)(n0 + bna) * a.Kp) * 2 + bsa * 16
-                               : nullptr;
-        const char* WrA1 = n0 + bna + 64 < a.Npad ? reinterpret_cast<const char*>(a.w) +
-                                                        (P.w_off + (int64_t)(n0 + bna + 64) * a.Kp) * 2 + bsa * 16
-                                                  : nullptr;
-        auto issue_pp = [&](int ci, int t) {   // weight step t of chunk ci (t >= NST: the next chunk's)
-            if (t >= NST) {
-                ci += 1;
-                t -= NST;
-            }
-            const int hf = t / NTAP, tap = t - hf * NTAP;
-            const int koff = (tap * a.Cin_pad + (c0 + ci) * H::CK + hf * 32) * 2;
-            const bool live = ci < nc;
-            char* const dst = bring + (t % NSTB) * H::BSTAGE + (wv & 3) * 1024;
-            glds16_asm((WrA0 && live) ? (const void*)(WrA0 + koff) : (const void*)cai_zero_page, dst);
-            glds16_asm((WrA1 && live) ? (const void*)(WrA1 + koff) : (const void*)cai_zero_page, dst + 4 * 1024);
-        };
-        auto read_pp = [&](int t, int pb, u32x4 (&ra)[TM], u32x4 (&rb)[TN]) {
-            const int hf = t / NTAP, tap = t - hf * NTAP;
-            const int ty = tap / NC, tx = tap - (tap / NC) * NC;
-            const int toff = GATHER ? (hf * 4 * H::PLANE + ty * H::PW + tx) * 16
-                                    : (hf * 4 * H::PLANE + (NA - 1 - ty) * H::PW + (NC - 1 - tx)) * 16;
-#pragma unroll
-            for (int tm = 0; tm < TM; ++tm) ra[tm] = *reinterpret_cast<const u32x4*>(smem + pb + apos[tm] + toff);
-#pragma unroll
-            for (int tn = 0; tn < TN; ++tn)
-                rb[tn] = *reinterpret_cast<const u32x4*>(smem + bpos[tn] + (t % NSTB) * H::BSTAGE);
-        };
-        auto store_pp = [&](int pb) {
-#pragma unroll
-            for (int i = 0; i < NPI; ++i) {
-                const int q8 = tid + NT * i, g = (q8 >> 3) & 7, q = ((q8 >> 6) << 3) | (q8 & 7);
-                if (q < H::NPOS) *reinterpret_cast<u32x4*>(smem + pb + (g * H::PLANE + q) * 16) = pr_[i];
-            }
-        };
-        if (nc > 0) {
-#pragma unroll
-            for (int i = 0; i < NPI; ++i) load_cell(0, i);
-            if constexpr (H::PP2) {
-#pragma unroll
-                for (int t = 0; t < D; ++t) issue_b(0, t);
-            } else if (grpA) {
-#pragma unroll
-                for (int t = 0; t < D; ++t) issue_pp(0, t);
-            }
-            wait_vmcnt<0>();
-            store_pp(0);
-            wait_lgkmcnt0();
-            __builtin_amdgcn_s_barrier();
-            read_pp(0, 0, fa, fb);
-            if (!grpA) __builtin_amdgcn_s_barrier();   // group B runs one barrier behind from here on
-        }
-        for (int ci = 0; ci < nc; ++ci) {
-            const int pb = (ci & 1) * H::PATCH, pbn = pb ^ H::PATCH;
-#pragma unroll
-            for (int t = 0; t < NST; ++t) {
-                if constexpr (H::PP2) {
-                    if (grpA)
-                        wait_vmcnt_n(halo_younger_pp2a(t, NPI));
-                    else
-                        wait_vmcnt_n(halo_younger_pp2b(t, NPI));
-                } else if (grpA) {
-                    wait_vmcnt_n(halo_younger_pp(t, NPI));   // this group's DMA of step t + 1 has landed
-                }
-                wait_lgkmcnt0();
-                __builtin_amdgcn_s_barrier();
-                __builtin_amdgcn_sched_barrier(0);
-                if constexpr (H::PP2) {
-                    if (t + D < NST)
-                        issue_b(ci, t + D);
-                    else
-                        issue_b(ci + 1, t + D - NST);
-                } else if (grpA) {
-                    issue_pp(ci, t + D);
-                }
-                if (t < NPI) load_cell(ci + 1, t);
-                if (t == NST - 3) {   // the next chunk's footprint into the other buffer
-                    if constexpr (H::PP2)
-                        wait_vmcnt_n(t - NPI + 1);         // the DMAs of steps NPI .. t came after the last cell
-                    else if (grpA)
-                        wait_vmcnt_n(2 * (t - NPI + 1));   // the DMAs of steps NPI .. t came after the last cell
-                    else
-                        wait_vmcnt<0>();
-                    store_pp(pbn);
-                }
-                u32x4 na[TM], nb[TN];
-                read_pp(t + 1 == NST ? 0 : t + 1, t + 1 == NST ? pbn : pb, na, nb);
-                if (CAI_HALO_PH_PP_PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-                for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-                    for (int tn = 0; tn < TN; ++tn)
-                        acc[tm][tn] = (CAI_HALO_PH_T || BN > 128) ? mma16<bf16>(fb[tn], fa[tm], acc[tm][tn])
-                                                    : mma16<bf16>(fa[tm], fb[tn], acc[tm][tn]);
-#pragma unroll
-                for (int i = 0; i < TM + TN; ++i) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                }
-                __builtin_amdgcn_sched_group_barrier(0x008, TM * TN - (TM + TN), 0);
-                if (CAI_HALO_PH_PP_PRIO) __builtin_amdgcn_s_setprio(0);
-#pragma unroll
-                for (int tm = 0; tm < TM; ++tm) fa[tm] = na[tm];
-#pragma unroll
-                for (int tn = 0; tn < TN; ++tn) fb[tn] = nb[tn];
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-        if (nc > 0 && grpA) __builtin_amdgcn_s_barrier();   // pairs group B's extra barrier
-    } else if constexpr (H::PAIRS) {
-        auto issue_s = [&](int ci, int s) {   // step s of chunk ci, s may run into the next chunk
-            if (s < NST)
-                issue_b(ci, s);
-            else
-                issue_b(ci + 1, s - NST);
-        };
-        if (nc > 0) {
-#pragma unroll
-            for (int i = 0; i < NPI; ++i) load_cell(0, i);
-            // the virtual even steps -NSTB .. -2 of the steady state: step -1 is a zero-page DMA into the stage
-            // step NSTB - 1 fills later, then steps 0 .. NSTB - 2
-            glds16_asm(cai_zero_page, bring + (NSTB - 1) * H::BSTAGE + wid * 1024);
-#pragma unroll
-            for (int t = 0; t < NSTB - 1; ++t) issue_b(0, t);
-            store_patch();
-            wait_vmcnt<NSTB - 2>();
-            wait_lgkmcnt0();
-            __builtin_amdgcn_s_barrier();
-            read_frags(0, fa, fb);
-        }
-        for (int ci = 0; ci < nc; ++ci) {
-#pragma unroll
-            for (int t = 0; t < NST; ++t) {
-                if (t % 2 == 0) {
-                    wait_vmcnt_n(halo_younger_pairs(t, NSTB, NPI));
-                    wait_lgkmcnt0();
-                    __builtin_amdgcn_s_barrier();
-                }
-                if (t == NST - 1) {
-                    __builtin_amdgcn_s_barrier();    // every wave has read its last fragment of the old footprint
-                    store_patch();
-                    wait_lgkmcnt0();
-                    __builtin_amdgcn_s_barrier();
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                if (t % 2 == 0) {
-                    issue_s(ci, t + NSTB - 1);
-                    issue_s(ci, t + NSTB);
-                }
-                if (t < NPI) load_cell(ci + 1, t);
-                if (t == NPI - 1) fence_loads();
-                u32x4 na[TM], nb[TN];
-                read_frags(t + 1 == NST ? 0 : t + 1, na, nb);
-#pragma unroll
-                for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-                    for (int tn = 0; tn < TN; ++tn)
-                        acc[tm][tn] = (CAI_HALO_PH_T || BN > 128) ? mma16<bf16>(fb[tn], fa[tm], acc[tm][tn])
-                                                    : mma16<bf16>(fa[tm], fb[tn], acc[tm][tn]);
-#pragma unroll
-                for (int i = 0; i < TM + TN; ++i) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                }
-                __builtin_amdgcn_sched_group_barrier(0x008, TM * TN - (TM + TN), 0);
-#pragma unroll
-                for (int tm = 0; tm < TM; ++tm) fa[tm] = na[tm];
-#pragma unroll
-                for (int tn = 0; tn < TN; ++tn) fb[tn] = nb[tn];
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-    } else {
     // the step pipeline of conv_halo_kernel, NST steps per chunk
     if (nc > 0) {
 #pragma unroll
@@ -1617,33 +1363,13 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
         __builtin_amdgcn_s_barrier();
         read_frags(0, fa, fb);
     }
-#if CAI_PH_PROBE
-    unsigned long long pr_s = __builtin_amdgcn_s_memtime();
-    pr_pro = pr_s - pr_t0;
-#endif
     for (int ci = 0; ci < nc; ++ci) {
 #pragma unroll
         for (int t = 0; t < NST; ++t) {
-#if CAI_PH_PROBE
-            const unsigned long long q0 = __builtin_amdgcn_s_memtime();
-            pr_body += q0 - pr_s;
-#endif
             // halo_younger counts one DMA per younger step; DPS DMAs per step add (DPS - 1) per younger tap
             wait_vmcnt_n(halo_younger(t, NSTB, NPI) + (DPS - 1) * (NSTB - 2));
-#if CAI_PH_PROBE
-            const unsigned long long q1 = __builtin_amdgcn_s_memtime();
-#endif
             wait_lgkmcnt0();
-#if CAI_PH_PROBE
-            const unsigned long long q2 = __builtin_amdgcn_s_memtime();
-#endif
             __builtin_amdgcn_s_barrier();
-#if CAI_PH_PROBE
-            pr_s = __builtin_amdgcn_s_memtime();
-            pr_vm += q1 - q0;
-            pr_lg += q2 - q1;
-            pr_bar += pr_s - q2;
-#endif
             if (t == NST - 1) {
                 store_patch();
                 wait_lgkmcnt0();
@@ -1677,22 +1403,9 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
             __builtin_amdgcn_sched_barrier(0);
         }
     }
-#if CAI_PH_PROBE
-    pr_body += __builtin_amdgcn_s_memtime() - pr_s;
-#endif
-    }   // !PAIRS
-#if CAI_PH_PROBE
-    const unsigned long long pe0 = __builtin_amdgcn_s_memtime();
-#endif
     wait_vmcnt<0>();
     asm volatile("" ::"v"(fence_[0]), "v"(fence_[1]), "v"(fence_[2]), "v"(fence_[3]));
-#if CAI_PH_PROBE
-    const unsigned long long pe1 = __builtin_amdgcn_s_memtime();
-#endif
     __syncthreads();
-#if CAI_PH_PROBE
-    const unsigned long long pe2 = __builtin_amdgcn_s_memtime();
-#endif
     const int plane = P.OHg * P.OWg;
     auto rowm = [=](int row) {
         const int oy = ty0 + row / H::TW, ox = tx0 + row % H::TW;
@@ -1704,24 +1417,11 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
     else
         conv_epilogue_rows<bf16, BM, BN, WM, WN, NT>(a, P, plane, n0, reinterpret_cast<float*>(smem), acc, rowm,
                                                      ph * a.ksplit + split);
-#if CAI_PH_PROBE
-    if constexpr (!H::PP && !H::PAIRS && !GATHER && BN == 128) {
-        const unsigned long long pe3 = __builtin_amdgcn_s_memtime();
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned long long pe4 = __builtin_amdgcn_s_memtime();
-        if ((blockIdx.x & 127) == 5 && (threadIdx.x & 63) == 0)
-            printf("PHPROBE ph=%d wave=%d nc=%d total=%llu pro=%llu vm=%llu lg=%llu bar=%llu body=%llu ewait=%llu "
-                   "esync=%llu epi=%llu edrain=%llu\n", ph, (int)(threadIdx.x >> 6), nc, pe3 - pr_t0, pr_pro, pr_vm,
-                   pr_lg, pr_bar, pr_body, pe1 - pe0, pe2 - pe1, pe3 - pe2, pe4 - pe3);
-    }
-#endif
 }
 
+
 // grid: x = 4 x the output tiles of one phase, z = split (the split-K slab index of the epilogue).  Block
-// order: phase-major (tiles XCD-remapped within a phase).  CAI_HALO_PH_MIX=1 makes the four phases of one
-// output tile consecutive logical blocks on one XCD (shared input footprint from its L2, every round mixing
-// 9-, 6- and 4-tap blocks): measured on MI355X the big launch unchanged (88-90 us) and the C2 step 2 %
-// slower (8316 vs 8465 patches/s), so it is off.
+// order: phase-major, tiles XCD-remapped within a phase.
 // 256 x 192 tiles of the halo phase / stride-1 kernels (192-, 384-, 768-channel layers).  The 96 accumulator
 // registers leave no room for register-staged footprint cells or a second B fragment set, so:
 //  * the next chunk's footprint goes global -> LDS by DMA into the other half of a double-buffered patch
@@ -1919,19 +1619,10 @@ __global__ __launch_bounds__(512, 1) void conv_halo_phase_kernel(const ConvArgs 
                   "halo phase LDS");
     __shared__ __attribute__((aligned(16))) char smem[BYTES];
     const int n0 = blockIdx.y * BN;
-    const int nb = gridDim.x;
-    const int lid = CAI_HALO_PH_MIX ? ((nb & 7) == 0 ? (blockIdx.x & 7) * (nb >> 3) + (blockIdx.x >> 3) : blockIdx.x)
-                                    : blockIdx.x;
-    const int nt = nb >> 2;
-    int ph, bid;
-    if (CAI_HALO_PH_MIX) {
-        ph = lid & 3;
-        bid = lid >> 2;
-    } else {   // the previous order: phase-major, tiles XCD-remapped within a phase
-        ph = blockIdx.x / nt;
-        const int t = blockIdx.x - ph * nt;
-        bid = (nt & 7) == 0 ? (t & 7) * (nt >> 3) + (t >> 3) : t;
-    }
+    const int nt = gridDim.x >> 2;
+    const int ph = blockIdx.x / nt;
+    const int t = blockIdx.x - ph * nt;
+    const int bid = (nt & 7) == 0 ? (t & 7) * (nt >> 3) + (t >> 3) : t;
     const int split = blockIdx.z;
     if constexpr (DMA) {
         switch (ph) {
@@ -1950,28 +1641,6 @@ __global__ __launch_bounds__(512, 1) void conv_halo_phase_kernel(const ConvArgs 
     }
 }
 
-// The 256-thread form of the 128-channel phase kernel (HaloPhCfg HALF: 8 x 16 tiles, two workgroups per CU).
-// grid: x = 4 x the output tiles of one phase (phase-major, tiles XCD-remapped within a phase), z = split.
-__global__ __launch_bounds__(256, 2) void conv_halo_phase_half_kernel(const ConvArgs a, int tiles_x, int tiles_y) {
-    constexpr int BYTES = HaloPhCfg<3, 3, 128, true>::BYTES > HaloPhCfg<2, 2, 128, true>::BYTES
-                              ? HaloPhCfg<3, 3, 128, true>::BYTES
-                              : HaloPhCfg<2, 2, 128, true>::BYTES;
-    static_assert(BYTES >= HaloPhCfg<3, 2, 128, true>::BYTES && BYTES >= HaloPhCfg<2, 3, 128, true>::BYTES &&
-                      2 * BYTES <= 160 * 1024,
-                  "halo phase (half) LDS");
-    __shared__ __attribute__((aligned(16))) char smem[BYTES];
-    const int nt = gridDim.x >> 2;
-    const int ph = blockIdx.x / nt;
-    const int t = blockIdx.x - ph * nt;
-    const int bid = (nt & 7) == 0 ? (t & 7) * (nt >> 3) + (t >> 3) : t;
-    const int split = blockIdx.z;
-    switch (ph) {
-        case 0: conv_halo_phase_body<3, 3, 128, false, true>(a, smem, 0, split, bid, tiles_x, tiles_y); break;
-        case 1: conv_halo_phase_body<3, 2, 128, false, true>(a, smem, 1, split, bid, tiles_x, tiles_y); break;
-        case 2: conv_halo_phase_body<2, 3, 128, false, true>(a, smem, 2, split, bid, tiles_x, tiles_y); break;
-        default: conv_halo_phase_body<2, 2, 128, false, true>(a, smem, 3, split, bid, tiles_x, tiles_y); break;
-    }
-}
 
 // Halo-staged stride-1 k3 p1 convolution (the 3x3 convs of cheng2020's residual / attention blocks and
 // sub-pixel convs, conv3x3 layers/layers.py:38-49 / 86-91): the phase body with one phase of 3x3 taps.
@@ -3823,7 +3492,6 @@ struct ConvLaunch {
     int halo, tiles_x, tiles_y;    // halo: kernel size of the halo-staged path (0: not taken)
     bool halo_ph;                  // the halo-staged s^2-phase path (k5 s2 p2 transposed direction)
     bool halo_s1;                  // the halo-staged stride-1 k3 path
-    bool ph_half;                  // the halo phase path in its 256-thread form (conv_halo_phase_half_kernel)
     int hbn;                       // output-channel tile of the halo phase / s1 paths (128 / 192)
     int small;                     // conv_small_kernel tile (SMALL_*; 0: not taken)
     size_t ws_bytes;
@@ -3927,17 +3595,6 @@ static bool halo_phase_ok(const cai_conv_geom* g, const Plan& P, bool glds, bool
     return true;
 }
 
-// A/B knob CAI_HALO_PH_HALF=1: the 128-channel halo phase layers on conv_halo_phase_half_kernel.  Measured
-// slower on MI355X (C2 g_s[4] fwd / g_a[2] dgrad 89.0 / 89.4 vs 86.0 / 85.1 us; step -0.1 %,
-// profiles/r03_halo_phase_half_ab.log): separate barriers per SIMD partner do not shorten the step, so it is off.
-static bool halo_ph_half_on() {
-    static const bool on = [] {
-        const char* e = getenv("CAI_HALO_PH_HALF");
-        return e && *e == '1';
-    }();
-    return on;
-}
-
 // the halo-staged stride-1 k3 p1 kernel (both directions), 64-channel input chunks, any output width in
 // BN-channel tiles; A/B knob CAI_HALO_S1_OFF
 static bool halo_s1_off() {
@@ -3982,17 +3639,15 @@ static ConvLaunch conv_launch(const cai_conv_geom* g, int dtype, int direction, 
     if (L.halo_ph || L.halo_s1) {
         const int np = L.halo_ph ? 4 : 1;
         L.hbn = halo_bn(P.kout_c);
-        L.ph_half = L.halo_ph && L.hbn == 128 && halo_ph_half_on();
-        L.BM = L.ph_half ? 128 : 256;
+        L.BM = 256;
         L.BN = L.hbn;
-        L.tiles_x = L.ph_half ? (P.OWg[0] + 15) / 16 : (P.OWg[0] + 31) / 32;
+        L.tiles_x = (P.OWg[0] + 31) / 32;
         L.tiles_y = (P.OHg[0] + 7) / 8;
         for (int ph = 0; ph < np; ++ph) L.mmax = std::max(L.mmax, g->batch * P.OHg[ph] * P.OWg[ph]);
         L.mtiles = g->batch * L.tiles_x * L.tiles_y;
         L.ntiles = (P.kout_c + L.hbn - 1) / L.hbn;
         const int nch = P.Cin_pad / 64, blocks = np * L.mtiles * L.ntiles;
-        const int target = L.ph_half ? 512 : 256;   // resident workgroups: two per CU in the 256-thread form
-        L.ksplit = capped(blocks >= target ? 1 : std::min(nch, (target + blocks - 1) / blocks));
+        L.ksplit = capped(blocks >= 256 ? 1 : std::min(nch, (256 + blocks - 1) / blocks));
         while (L.ksplit > 1 && (L.ksplit - 1) * ((nch + L.ksplit - 1) / L.ksplit) >= nch) --L.ksplit;
         L.ws_ld = L.ntiles * L.hbn;
         L.ws_bytes = L.ksplit > 1 ? (size_t)np * L.ksplit * L.mmax * L.ws_ld * sizeof(float) : 0;
@@ -4094,9 +3749,7 @@ static void launch_conv_halo(const ConvArgs& a, const ConvLaunch& L, hipStream_t
 static void launch_conv_halo_phase(const ConvArgs& a, const ConvLaunch& L, hipStream_t st) {
     const dim3 grid(L.halo_ph ? 4 * L.mtiles : L.mtiles, L.ntiles, a.ksplit);
     if (L.halo_ph) {
-        if (L.ph_half)
-            hipLaunchKernelGGL(conv_halo_phase_half_kernel, grid, dim3(256), 0, st, a, L.tiles_x, L.tiles_y);
-        else if (L.hbn == 192)
+        if (L.hbn == 192)
             hipLaunchKernelGGL(conv_halo_phase_kernel<192>, grid, dim3(512), 0, st, a, L.tiles_x, L.tiles_y);
         else
             hipLaunchKernelGGL(conv_halo_phase_kernel<128>, grid, dim3(512), 0, st, a, L.tiles_x, L.tiles_y);
@@ -4720,8 +4373,7 @@ const char* cai_conv_kernel_name(const cai_conv_geom* g, int dtype, int directio
     const ConvLaunch L = conv_launch(g, dtype, direction, in_abs);
     if (L.halo) return L.halo == 5 ? "conv_halo_kernel<5>" : "conv_halo_kernel<3>";
     if (L.halo_ph)
-        return L.ph_half ? "conv_halo_phase_half_kernel"
-                         : (L.hbn == 192 ? "conv_halo_phase_kernel<192>" : "conv_halo_phase_kernel");
+        return L.hbn == 192 ? "conv_halo_phase_kernel<192>" : "conv_halo_phase_kernel";
     if (L.halo_s1) return L.hbn == 192 ? "conv_halo_s1_kernel<192>" : "conv_halo_s1_kernel<128>";
     if (L.small) return L.small == SMALL_16x32 ? "conv_small_kernel<16x32>"
                         : (L.small == SMALL_32x32 ? "conv_small_kernel<32x32>" : "conv_small_kernel<32x64>");
