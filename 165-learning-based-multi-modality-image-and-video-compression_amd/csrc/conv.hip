@@ -30,6 +30,7 @@
 #include "edge_frag.hpp"
 #include "mfma.hpp"
 #include "reduce_jobs.hpp"
+#include "conv_args.hpp"
 
 #include <algorithm>
 #include <vector>
@@ -38,43 +39,6 @@ namespace cai {
 
 constexpr int NT = 256;
 
-struct PhaseDesc {
-    int oy0, ox0;     // output offset of this phase
-    int OHg, OWg;     // GEMM row grid of this phase
-    int ntaps, ntx;   // taps, taps per kernel row
-    int dy0, dx0;     // input offset of tap 0
-    int K;            // ntaps * Cin_pad
-    int pad_;
-    int64_t w_off;    // element offset of this phase's packed weights
-};
-
-struct ConvArgs {
-    const void* x;
-    int B, IH, IW, x_ld, Cin_pad, in_abs;
-    const void* w;
-    int Kp, Npad;
-    int nphase;
-    int tap_sy, tap_sx;
-    int row_stride, out_step;
-    int out_h, out_w, Cout;
-    void* y;
-    int y_dtype, y_vec;
-    int64_t ysb, ysc, ysy, ysx;
-    const float* bias;
-    int act;
-    float act_param;
-    const void* aux;
-    int aux_ld, mask_mode;
-    float mask_param;
-    const bf16* res;         // residual input (cai_conv_fwd_res): y = act(conv + bias + res), pixel-major bf16, NULL: none
-    int res_ld;
-    const bf16* res2;        // a second residual (dgrad only, cai_conv_dgrad_res2), same layout as res; NULL: none
-    int res2_ld;
-    int ksplit;              // K splits per phase (grid.z = nphase * ksplit)
-    float* ws;               // split-K partials [nphase*ksplit][ws_rows][ws_ld] fp32
-    int ws_rows, ws_ld;
-    PhaseDesc ph[4];
-};
 
 __device__ __forceinline__ int swz(int row, int slot) { return slot ^ ((row >> 1) & 7); }
 
@@ -3746,10 +3710,15 @@ static void launch_conv_halo(const ConvArgs& a, const ConvLaunch& L, hipStream_t
     }
 }
 
+// the four-phase kernel (conv_quad.hip) where every block of it gets a CU: >= 256 tiles, no split
+static bool quad_grid(const ConvLaunch& L) { return L.halo_ph && L.hbn == 128 && L.ksplit == 1 && L.mtiles >= 256; }
+
 static void launch_conv_halo_phase(const ConvArgs& a, const ConvLaunch& L, hipStream_t st) {
     const dim3 grid(L.halo_ph ? 4 * L.mtiles : L.mtiles, L.ntiles, a.ksplit);
     if (L.halo_ph) {
-        if (L.hbn == 192)
+        if (quad_grid(L) && conv_quad_ok(a))
+            launch_conv_halo_quad(a, L.tiles_x, L.tiles_y, L.mtiles, st);
+        else if (L.hbn == 192)
             hipLaunchKernelGGL(conv_halo_phase_kernel<192>, grid, dim3(512), 0, st, a, L.tiles_x, L.tiles_y);
         else
             hipLaunchKernelGGL(conv_halo_phase_kernel<128>, grid, dim3(512), 0, st, a, L.tiles_x, L.tiles_y);
@@ -4372,8 +4341,22 @@ const char* cai_conv_kernel_name(const cai_conv_geom* g, int dtype, int directio
     }
     const ConvLaunch L = conv_launch(g, dtype, direction, in_abs);
     if (L.halo) return L.halo == 5 ? "conv_halo_kernel<5>" : "conv_halo_kernel<3>";
-    if (L.halo_ph)
+    if (L.halo_ph) {
+        if (quad_grid(L) && dtype == CAI_BF16) {
+            // the four-phase kernel when the output takes the register-direct epilogue (bf16, no mask / residual)
+            const Plan P = make_plan(g, dtype, direction);
+            ConvArgs a{};
+            a.nphase = P.nphase; a.Cin_pad = P.Cin_pad; a.Cout = P.kout_c; a.Npad = P.Npad; a.ksplit = L.ksplit;
+            a.out_step = P.phase ? g->stride : 1; a.in_abs = in_abs; a.y_vec = 1; a.y_dtype = CAI_BF16;
+            a.x_ld = P.Cin_pad;
+            for (int ph = 0; ph < P.nphase; ++ph) {
+                a.ph[ph].ntaps = P.ntaps[ph]; a.ph[ph].ntx = P.ntx[ph]; a.ph[ph].dy0 = P.dy0[ph];
+                a.ph[ph].dx0 = P.dx0[ph]; a.ph[ph].oy0 = P.oy0[ph]; a.ph[ph].ox0 = P.ox0[ph];
+            }
+            if (conv_quad_ok(a)) return "conv_halo_quad_kernel";
+        }
         return L.hbn == 192 ? "conv_halo_phase_kernel<192>" : "conv_halo_phase_kernel";
+    }
     if (L.halo_s1) return L.hbn == 192 ? "conv_halo_s1_kernel<192>" : "conv_halo_s1_kernel<128>";
     if (L.small) return L.small == SMALL_16x32 ? "conv_small_kernel<16x32>"
                         : (L.small == SMALL_32x32 ? "conv_small_kernel<32x32>" : "conv_small_kernel<32x64>");

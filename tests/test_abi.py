@@ -152,7 +152,12 @@ def test_halo_kernel_selection(native):
     assert name(G(8, 64, 64, 64, 192, 128, 128, 5, 2, 2, 1, 1), 0) == "conv_halo_phase_kernel<192>"
     assert name(G(8, 192, 128, 128, 64, 64, 64, 5, 2, 2, 0, 0), 1) == "conv_halo_phase_kernel<192>"
     assert "halo" not in name(G(16, 192, 32, 32, 192, 64, 64, 5, 2, 2, 1, 1), 0)    # 256 blocks
-    assert name(G(16, 128, 64, 64, 128, 128, 128, 5, 2, 2, 1, 1), 0) == "conv_halo_phase_kernel"
+    # 128 channels: the four-phase kernel from 256 tiles (one block per CU), the per-phase kernel below
+    assert name(G(16, 128, 64, 64, 128, 128, 128, 5, 2, 2, 1, 1), 0) == "conv_halo_quad_kernel"
+    assert name(G(16, 128, 128, 128, 128, 64, 64, 5, 2, 2, 0, 0), 1) == "conv_halo_quad_kernel"
+    assert name(G(8, 128, 64, 64, 128, 128, 128, 5, 2, 2, 1, 1), 0) == "conv_halo_phase_kernel"
+    assert name(G(16, 128, 32, 32, 128, 64, 64, 5, 2, 2, 1, 1), 0) == "conv_halo_phase_kernel"
+    assert name(G(16, 192, 64, 64, 128, 128, 128, 5, 2, 2, 1, 1), 0) == "conv_halo_phase_kernel"   # Cin 192
     # weight gradient: the halo-staged kernel's stride-1 form for 64-multiple G widths
     if os.environ.get("CAI_HALO_WGRAD_S1_OFF", "0") in ("", "0"):
         assert name(G(4, 192, 128, 128, 192, 128, 128, 3, 1, 1, 0, 0), 2) == "wgrad_halo_kernel<3,s1>"

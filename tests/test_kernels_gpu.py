@@ -794,6 +794,58 @@ def test_multiphase_conv(cuda, kind):
         assert relerr(x.grad, xr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("kind,act", [("deconv_fwd", 0), ("deconv_fwd", 1), ("deconv_fwd", 2), ("conv_dgrad", 0)])
+def test_quad_kernel_bit_identical_to_phase_kernel(cuda, kind, act):
+    """conv_halo_quad_kernel (all four s^2 phases of a tile from one staged footprint; B = 16: 256 tiles) against
+    conv_halo_phase_kernel (one block per phase and tile; taken for each B = 8 half: 128 tiles): the same
+    accumulation order per output, so the outputs are bit-identical.  Covers the C2 g_s[4] forward
+    (ConvTranspose2d 128->128 k5 s2 op1, 64^2 -> 128^2) with bias and no / ReLU / LeakyReLU activation, and the
+    g_a[2] input gradient (Conv2d 128->128 k5 s2, 64^2 -> 128^2 in the phase form), through the C ABI."""
+    import ctypes
+
+    from compressai import _native as native
+    from compressai._ops import _p, _stream
+
+    raw = native.lib.load()
+    torch.manual_seed(11 + act)
+    G = native.ConvGeom
+    if kind == "deconv_fwd":
+        geo = lambda b: G(b, 128, 64, 64, 128, 128, 128, 5, 2, 2, 1, 1)   # noqa: E731
+        direction = 0
+    else:
+        geo = lambda b: G(b, 128, 128, 128, 128, 64, 64, 5, 2, 2, 0, 0)   # noqa: E731
+        direction = 1
+    g16, g8 = geo(16), geo(8)
+    assert raw.cai_conv_kernel_name(ctypes.byref(g16), native.BF16, direction, 0).decode() == "conv_halo_quad_kernel"
+    assert raw.cai_conv_kernel_name(ctypes.byref(g8), native.BF16, direction, 0).decode() == "conv_halo_phase_kernel"
+    assert native.lib.cai_conv_workspace_bytes(ctypes.byref(g16), native.BF16, direction) == 0
+    w = (torch.randn(128, 128, 5, 5, device=cuda) * 0.05).contiguous()
+    bias = torch.randn(128, device=cuda) if kind == "deconv_fwd" else None
+    wp = torch.empty(native.lib.cai_conv_packed_weight_bytes(ctypes.byref(g16), native.BF16, direction),
+                     dtype=torch.uint8, device=cuda)
+    native.lib.cai_conv_pack_weight(ctypes.byref(g16), native.BF16, direction, _p(w), None, _p(wp), _stream())
+    x = torch.randn(16, 64, 64, 128, device=cuda).bfloat16().contiguous()       # pixel-major, 64^2 either way
+
+    def run(g, xin):
+        bsz = xin.shape[0]
+        y = torch.full((bsz, 128, 128, 128), float("nan"), device=cuda).bfloat16()
+        if direction == 0:
+            native.lib.cai_conv_fwd(ctypes.byref(g), native.BF16, _p(xin), 128, 0, _p(wp), _p(bias), act, 0.01,
+                                    _p(y), native.BF16, 128 * 128 * 128, 1, 128 * 128, 128, None, 0, _stream())
+        else:
+            native.lib.cai_conv_dgrad(ctypes.byref(g), native.BF16, _p(xin), 128, _p(wp), _p(y), 128,
+                                      native.MASK_NONE, 0.0, None, 0, None, 0, _stream())
+        return y
+
+    y16 = run(g16, x)
+    y8 = torch.cat([run(g8, x[:8].contiguous()), run(g8, x[8:].contiguous())])
+    torch.cuda.synchronize()
+    assert torch.isfinite(y16.float()).all()
+    if act == 1:
+        assert (y16.float() >= 0).all() and (y16.view(torch.int16) != -32768).all()   # ReLU: +0, never -0
+    assert torch.equal(y16.view(torch.int16), y8.view(torch.int16))
+
+
 @pytest.mark.parametrize("B", [16, 14])
 def test_halo_conv_full(cuda, B):
     """Full-size stride-2 GEMMs on the halo-staged kernels: the C2 g_a[2] forward (Conv2d 128->128 k5 s2,

@@ -139,6 +139,7 @@ BF16_XHAT, BF16_LIK, BF16_LIK_L2, BF16_LOSS, GRAD_COS, TENSOR_COS = 1e-2, 5e-2, 
 # the kernels the bench's C2 / C3 step launches at 256x256 B=16 (none of them is taken at the 64-128 px model
 # test sizes: the lane GDN kernels need >= 32768 pixels, the halo / phase / edge kernels full-size grids)
 C2_MIX = ("gdn_fwd_lane_kernel<128>", "gdn_bwd_lane_kernel<128>", "conv_halo_kernel<5>", "conv_halo_phase_kernel",
+          "conv_halo_quad_kernel",
           "wgrad_halo_kernel<5>", "edge_s2d_kernel (conv fwd)", "edge_d2s_kernel (deconv fwd)",
           "edge_wgrad_dma_kernel (+pack, reduce)")
 
