@@ -896,8 +896,10 @@ def _resunit_fwd(y, params, need_x):
                     ba=bs[0].data_ptr(), bb=bs[1].data_ptr(), bc=bs[2].data_ptr(), h1=h1.data_ptr(),
                     h2=h2.data_ptr(), out=out.data_ptr(), x_ld=xld, out_ld=n, kpa=kpa, kpb=kpb, kpc=kpc)
     fl = sum(_ledger.conv_cost(g, 2, 0)[0] for g in (ga, gb, gc))
-    _ledger.run(lambda: lib.cai_resunit(ctypes.byref(A), 0, _stream()), "conv_fwd", f"resunit_kernel<{n},fwd>", fl,
-                2 * B * H * W * (2 * n + 2 * nh), dt, f"ResidualUnit N={n} {H}x{W} B={B}")
+    # the closure owns every buffer A points at: the ledger may replay it after the step (bench.py --replay)
+    _ledger.run(lambda keep=(A, xpm, wa, wb, wc, h1, h2, out, bs): lib.cai_resunit(ctypes.byref(keep[0]), 0, _stream()),
+                "conv_fwd", f"resunit_kernel<{n},fwd>", fl, 2 * B * H * W * (2 * n + 2 * nh), dt,
+                f"ResidualUnit N={n} {H}x{W} B={B}")
     u = _FusedUnit(params, (ga, gb, gc), need_x)
     u.saved_tensors = (xpm, h1, h2, out)
     if _prepack_active() is not None:
@@ -935,7 +937,8 @@ def _resunit_bwd(u: "_FusedUnit", gy):
                     res2_ld=r2ld if res2 is not None else 0, xmask_ld=pixel_major_ld(xpm) if u.mask_x else 0,
                     kpa=kpa, kpb=kpb, kpc=kpc, gy_masked=int(u.gy_masked))
     fl = sum(_ledger.conv_cost(g, 2, 1)[0] for g in (ga, gb, gc))
-    _ledger.run(lambda: lib.cai_resunit(ctypes.byref(A), 1, _stream()), "conv_dgrad", f"resunit_kernel<{n},bwd>", fl,
+    _ledger.run(lambda keep=(A, gpm, y, wa, wb, wc, h1, h2, dx, g_c, g_b, g_a, res2, xpm):
+                lib.cai_resunit(ctypes.byref(keep[0]), 1, _stream()), "conv_dgrad", f"resunit_kernel<{n},bwd>", fl,
                 2 * B * H * W * (3 * n + 4 * nh), dt, f"ResidualUnit N={n} {H}x{W} B={B}")
     gcc, gcld = (gpm, gld) if g_c is None else (g_c, n)
     if _RESUNIT_WGRAD and hasattr(lib.load(), "cai_resunit_wgrad"):
@@ -979,7 +982,8 @@ def _resunit_wgrad(u: "_FusedUnit", xpm, h1, h2, g_a, g_b, gcc, gcld):
         P = B * H * W
         fl = 2.0 * P * (nh * n * 2 + 9 * nh * nh)
         nb = 2 * P * (3 * n + 4 * nh)
-        _ledger.run(lambda: lib.cai_resunit_wgrad(ctypes.byref(A), _p(wws), nbytes, st, None), "conv_wgrad",
+        _ledger.run(lambda keep=(A, wws, xpm, h1, h2, g_a, g_b, gcc, outs):
+                    lib.cai_resunit_wgrad(ctypes.byref(keep[0]), _p(keep[1]), nbytes, st, None), "conv_wgrad",
                     f"resunit_wgrad_kernel<{n}> (+reduce)", fl, nb, torch.bfloat16,
                     f"ResidualUnit N={n} {H}x{W} B={B}")
     if direct:

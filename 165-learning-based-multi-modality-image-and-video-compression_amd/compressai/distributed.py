@@ -73,93 +73,144 @@ class _Boundary(torch.autograd.Function):
 
 
 class OverlappedAllReduce:
-    """Two-bucket gradient all-reduce overlapped with the backward of the model's tail.
+    """Bucketed gradient all-reduce overlapped with the backward.
 
-    The backward runs in two phases: ``backward_head(loss)`` differentiates down to the cut tensors and
-    into every other parameter (``torch.autograd.backward(loss, inputs=[*cut, *head_params])``), so
-    flat_grad[:split] -- every gradient but the tail's (FusedAdam layout from
-    configure_optimizers(..., tail=model.dp_tail)) -- is final; ``reduce_head()`` all-reduces it on a side
-    stream while ``backward_tail()`` runs the tail's backward on the compute stream; ``finish()``
-    all-reduces flat_grad[split:] and joins the streams.  Each phase can be captured in its own HIP
-    graph; the collectives stay outside the graphs (stream order only, no events).
+    The flat gradient buffer of FusedAdam (configure_optimizers(..., tail=model.dp_tail,
+    tail_cuts=model.dp_tail_cuts)) holds the buckets in the order the backward finishes them: the head
+    (everything but the tail), then the tail's pieces from the loss side down to the input.  The backward
+    runs in one phase per bucket: ``backward_head(loss)`` differentiates down to the model's cut
+    (``torch.autograd.backward(loss, inputs=[*cut, *head_params])``), so bucket 0 is final;
+    ``backward_phase(i)`` continues from cut i-1 down to cut i (the input of the tail child named by
+    dp_tail_cuts[i-1]) or, for the last one, to the input.  ``reduce_bucket(i)`` all-reduces bucket i on a
+    side stream while the next phase runs on the compute stream; ``finish()`` all-reduces the last bucket and
+    joins the streams.  Each phase can be captured in its own HIP graph; the collectives stay outside the
+    graphs (stream order only, no events).  ``reduce_head()`` / ``backward_tail()`` are the eager two-call
+    form (every tail phase, each bucket all-reduced once the phase after it is queued).
 
     `tail`: a model with a ``_dp_cut`` marker (CompressionModel: the cut the model itself declares), or any
     module whose output is a cut (a forward hook marks it: e.g. ``net.g_a`` of the zoo models).
 
-    Memory: backward_head keeps the graph (retain_graph) because backward_tail still needs the tail's saved
-    tensors; the head's saved tensors are released when the caller drops its loss tensor (bench.py's step
-    drops it on return) -- the serial backward's peak otherwise."""
+    Cut tensors accumulate over the grad-enabled forwards of a step (micro-batches summed into one loss) and
+    are released by ``finish()``; a plain ``loss.backward()`` outside the phases (no exchange) releases the
+    ones it differentiated through, so they never leak into the next step.
 
-    def __init__(self, flat_grad: torch.Tensor, split: int, tail: torch.nn.Module, head_params):
-        self.head = flat_grad[:split]
-        self.tail = flat_grad[split:]
+    Memory: each phase keeps the graph (retain_graph) because the later phases still need the tail's saved
+    tensors; they are released when the caller drops its loss tensor (bench.py's step drops it on return) --
+    the serial backward's peak otherwise."""
+
+    def __init__(self, flat_grad: torch.Tensor, split, tail: torch.nn.Module, head_params,
+                 cut_modules=(), stage_params=None):
+        bounds = list(split) if isinstance(split, (list, tuple)) else [0, int(split), flat_grad.numel()]
+        if len(bounds) != len(cut_modules) + 3 and not (len(bounds) == 2 and not cut_modules):
+            raise ValueError("OverlappedAllReduce: one bucket per cut piece expected "
+                             f"({len(cut_modules) + 2} buckets for {len(cut_modules)} tail cuts, bounds {bounds})")
+        self.buckets = [flat_grad[bounds[i]:bounds[i + 1]] for i in range(len(bounds) - 1)]
+        self.head, self.tail = self.buckets[0], flat_grad[bounds[1]:] if len(bounds) > 2 else flat_grad[:0]
         self.head_params = [p for p in head_params if p.requires_grad]
-        self.side = torch.cuda.Stream(device=flat_grad.device)
-        self._ys = []
+        self.stage_params = [[p for p in ps if p.requires_grad] for ps in (stage_params or [])]
+        # (a CPU buffer -- the gloo tests of the phase logic -- reduces synchronously, no side stream)
+        self.side = torch.cuda.Stream(device=flat_grad.device) if flat_grad.is_cuda else None
+        self._cuts = [[] for _ in range(max(1, len(self.buckets) - 1))]   # cut tensors of each tail phase
+        self._in_phase = False
         self._model = None
         self._handles = []
         if hasattr(tail, "_dp_cut") and hasattr(tail, "dp_tail"):
             self._model = tail
-            tail._dp_cut_fn = self._mark
+            tail._dp_cut_fn = lambda *ts: self._mark(0, *ts)
         else:
-            self._handles.append(tail.register_forward_hook(self._keep))
-        # each forward starts a new set of cut tensors: one that never reached backward_tail (a validation
-        # pass, a plain backward) neither leaks into the next step nor keeps its cut tensors alive
-        self._handles.append(tail.register_forward_pre_hook(self._reset))
+            self._handles.append(tail.register_forward_hook(lambda m, i, o: self._mark(0, o)[0]))
+        for k, m in enumerate(cut_modules):
+            self._handles.append(m.register_forward_pre_hook(
+                lambda mod, inputs, k=k: (self._mark(k + 1, inputs[0]),) + tuple(inputs[1:])))
 
     @classmethod
     def for_model(cls, model: torch.nn.Module, opt):
-        """The exchange of `model` over FusedAdam `opt` built by configure_optimizers(model, tail=model.dp_tail)."""
+        """The exchange of `model` over FusedAdam `opt` built by configure_optimizers(model,
+        tail=model.dp_tail, tail_cuts=model.dp_tail_cuts); a buffer built without the cuts gets two buckets."""
+        from .optim import dp_stage
+
         tail = tuple(model.dp_tail)
-        head = [p for n, p in model.named_parameters()
-                if not n.startswith(tail) and not n.endswith(".quantiles")]
-        return cls(opt.flat_grad, opt.tail_offset, model, head)
+        bounds = list(getattr(opt, "bucket_bounds", [0, opt.tail_offset, opt.numel]))
+        cuts = tuple(getattr(model, "dp_tail_cuts", ())) if len(bounds) > 3 else ()
+        main = [(n, p) for n, p in model.named_parameters() if not n.endswith(".quantiles")]
+        head = [p for n, p in main if dp_stage(n, tail, cuts) == 0]
+        stages = [[p for n, p in main if dp_stage(n, tail, cuts) == s] for s in range(1, len(cuts) + 2)]
+        return cls(opt.flat_grad, bounds, model, head, [model.get_submodule(c) for c in cuts], stages)
 
-    def _reset(self, module, inputs):
-        self._ys = []
+    @property
+    def nphases(self) -> int:
+        return len(self.buckets)
 
-    def _mark(self, *ts):
+    def _mark(self, k, *ts):
         # only a forward that can be differentiated marks its cut (no_grad / eval passes go through as is)
         if not torch.is_grad_enabled() or not any(t.requires_grad for t in ts):
-            return ts
-        # boundary nodes: phase 1's capture of a cut tensor's gradient may execute its grad_fn, which for
+            return ts[0] if k else ts
+        # boundary nodes: a phase's capture of a cut tensor's gradient may execute its grad_fn, which for
         # the product convs writes parameter gradients as a side effect; an identity node in between has none
         out = tuple(_Boundary.apply(t) for t in ts)
-        self._ys.extend(out)
-        return out
+        for t in out:
+            # a backward outside the phases (a plain loss.backward()) releases the cut (by id: a reference in the
+            # hook would keep the tensor, and with it its graph, alive until the cycle collector runs)
+            t.register_hook(lambda g, tid=id(t), k=k: self._release(k, tid))
+        self._cuts[k].extend(out)
+        return out[0] if k else out
 
-    def _keep(self, module, inputs, output):
-        return self._mark(output)[0]
+    def _release(self, k, tid):
+        if not self._in_phase:
+            self._cuts[k] = [c for c in self._cuts[k] if id(c) != tid]
+        return None
+
+    def _backward(self, roots, grads, inputs):
+        self._in_phase = True
+        try:
+            torch.autograd.backward(roots, grad_tensors=grads, inputs=inputs or None, retain_graph=bool(inputs))
+        finally:
+            self._in_phase = False
 
     def backward_head(self, loss: torch.Tensor):
-        if not self._ys:
+        if not self._cuts[0]:
             raise RuntimeError("OverlappedAllReduce: the forward did not reach the cut")
-        # retain_graph: the engine releases the saved tensors of every node of the graph it was given,
-        # including the tail's, which backward_tail still needs
         from ._ops import loss_seed
 
-        torch.autograd.backward(loss, grad_tensors=loss_seed(loss), inputs=list(self._ys) + self.head_params,
-                                retain_graph=True)
+        # retain_graph: the engine releases the saved tensors of every node of the graph it was given,
+        # including the tail's, which the later phases still need
+        self._backward(loss, loss_seed(loss), list(self._cuts[0]) + self.head_params)
 
-    def backward_tail(self):
-        ys, self._ys = self._ys, []
-        used = [y for y in ys if y.grad is not None]
-        torch.autograd.backward(used, grad_tensors=[y.grad for y in used])
+    def backward_phase(self, i: int):
+        """Tail phase i (1 .. nphases - 1): from cut i - 1's gradients down to cut i (all of it for the last)."""
+        ys = [y for y in self._cuts[i - 1] if y.grad is not None]
+        last = i == self.nphases - 1
+        inputs = [] if last else list(self._cuts[i]) + self.stage_params[i - 1]
+        if ys:
+            self._backward(ys, [y.grad for y in ys], inputs)
 
-    def reduce_head(self):
+    def reduce_bucket(self, i: int):
+        """All-reduce bucket i on the side stream, after everything queued on the compute stream."""
+        if self.side is None:
+            if self.buckets[i].numel():
+                allreduce_mean_(self.buckets[i])
+            return
         self.side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self.side):
-            if self.head.numel():
-                allreduce_mean_(self.head)
+            if self.buckets[i].numel():
+                allreduce_mean_(self.buckets[i])
+
+    def reduce_head(self):
+        self.reduce_bucket(0)
+
+    def backward_tail(self):
+        """Every tail phase, eagerly: bucket i is all-reduced while phase i + 1 runs (the last by finish())."""
+        for i in range(1, self.nphases):
+            self.backward_phase(i)
+            if i < self.nphases - 1:
+                self.reduce_bucket(i)
 
     def finish(self):
-        """All-reduce the tail bucket after the whole backward, then join the side stream."""
-        cur = torch.cuda.current_stream()
-        self.side.wait_stream(cur)
-        with torch.cuda.stream(self.side):
-            if self.tail.numel():
-                allreduce_mean_(self.tail)
-        cur.wait_stream(self.side)
+        """All-reduce the last bucket after the whole backward, join the side stream, release the cuts."""
+        self.reduce_bucket(self.nphases - 1)
+        if self.side is not None:
+            torch.cuda.current_stream().wait_stream(self.side)
+        self._cuts = [[] for _ in self._cuts]
 
     def remove(self):
         for h in self._handles:

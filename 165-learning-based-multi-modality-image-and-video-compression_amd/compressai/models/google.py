@@ -107,8 +107,12 @@ def get_scale_table(min=SCALES_MIN, max=SCALES_MAX, levels=SCALES_LEVELS):
 
 class CompressionModel(nn.Module):
     # data parallelism (compressai.distributed.OverlappedAllReduce): the parameters upstream of the cut the
-    # forward marks with _dp_cut (name prefixes), exchanged in the second bucket
+    # forward marks with _dp_cut (name prefixes) form the tail; dp_tail_cuts (children of the tail Sequential,
+    # outermost first) cut it further at their inputs, one gradient bucket per piece, each all-reduced while
+    # the pieces below it run their backward.  _analysis: g_a[4:], g_a[2:4], g_a[:2] (the last, exposed one
+    # is conv(3, N) + GDN: 26 K parameters at N = 128)
     dp_tail = ("g_a.",)
+    dp_tail_cuts = ("g_a.4", "g_a.2")
     _dp_cut_fn = None
 
     def _dp_cut(self, *ts):

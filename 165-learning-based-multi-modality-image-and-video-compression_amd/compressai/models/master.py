@@ -381,6 +381,7 @@ class Master_compresser(_ARCoding, MeanScaleHyperprior):
     # so the cut is {x_feature, guided_align}, not g_a's output); the inherited g_s is never used (its
     # gradients stay zero, as in the reference, master.py:839)
     dp_tail = ("fencoder1.", "fencoder2.", "ch_aligner.")
+    dp_tail_cuts = ()     # one tail bucket (10.6 MB against a ~57 ms pair step)
 
     def __init__(self, width=256, height=256, channel=3, N=192, M=192):
         super().__init__(M, M)

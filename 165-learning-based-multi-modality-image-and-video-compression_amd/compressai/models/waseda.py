@@ -18,6 +18,10 @@ __all__ = ["Cheng2020Anchor", "Cheng2020Attention"]
 class Cheng2020Anchor(JointAutoregressiveHierarchicalPriors):
     """waseda.py:48-123."""
 
+    # gradient buckets of g_a (compressai.distributed): g_a[4:], g_a[2:4], g_a[1], g_a[0] (the exposed last
+    # bucket: ResidualBlockWithStride(3, N), 0.37 M parameters at N = 192)
+    dp_tail_cuts = ("g_a.4", "g_a.2", "g_a.1")
+
     def __init__(self, N=192, channel=3, **kwargs):
         super().__init__(N=N, M=N, **kwargs)
         self.g_a = Sequential(
@@ -48,6 +52,9 @@ class Cheng2020Anchor(JointAutoregressiveHierarchicalPriors):
 
 class Cheng2020Attention(Cheng2020Anchor):
     """waseda.py:126-158."""
+
+    # g_a[5:] (10.0 MB of fp32 gradients at N = 192), g_a[2:5] (8.6 MB), g_a[1] (2.7 MB), g_a[0] (1.5 MB, exposed)
+    dp_tail_cuts = ("g_a.5", "g_a.2", "g_a.1")
 
     def __init__(self, N=192, channel=3, **kwargs):
         super().__init__(N=N, **kwargs)

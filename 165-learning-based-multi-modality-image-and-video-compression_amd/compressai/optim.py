@@ -239,18 +239,42 @@ def parameter_groups(net):
     return main, aux
 
 
+def dp_stage(name: str, tail: Tuple[str, ...], cuts: Tuple[str, ...] = ()) -> int:
+    """Gradient bucket of parameter `name` (compressai.distributed.OverlappedAllReduce): 0 outside the tail;
+    in the tail 1 + the number of `cuts` ("g_a.4": the input of child 4 of the tail Sequential g_a) the
+    parameter lies below, i.e. the order in which the backward finishes the buckets."""
+    if not any(name.startswith(t) for t in tail):
+        return 0
+    below = 0
+    for c in cuts:
+        parent, idx = c.rsplit(".", 1)
+        if name.startswith(parent + "."):
+            child = name[len(parent) + 1:].split(".", 1)[0]
+            if child.isdigit() and int(child) < int(idx):
+                below += 1
+    return 1 + below
+
+
 def configure_optimizers(net, lr: float = 1e-4, aux_lr: float = 1e-3, tail: Tuple[str, ...] = (),
-                         zero_grad_in_step: bool = False):
+                         zero_grad_in_step: bool = False, tail_cuts: Tuple[str, ...] = ()):
     """train.py:111-142: main Adam on all but `.quantiles`, aux Adam on `.quantiles` (sorted by name).
 
-    tail: name prefixes whose parameters go last in the main flat buffers (FusedAdam layout); the
-    optimizer's ``tail_offset`` is where they start (distributed.OverlappedAllReduce).
+    tail: name prefixes whose parameters go last in the main flat buffers (FusedAdam layout); tail_cuts split
+    the tail further (dp_stage): the buffer holds the buckets in backward order, head first.  The optimizer's
+    ``bucket_bounds`` are the buckets' element offsets ([0, ..., numel]); ``tail_offset`` is where the tail
+    starts (distributed.OverlappedAllReduce).
     zero_grad_in_step: see FusedAdam (both optimizers)."""
     named = dict(net.named_parameters())
     main, aux = parameter_groups(net)
-    is_tail = [any(n.startswith(t) for t in tail) for n in main]
-    layout = [i for i, t in enumerate(is_tail) if not t] + [i for i, t in enumerate(is_tail) if t]
+    stage = [dp_stage(n, tail, tail_cuts) for n in main]
+    nst = 1 + len(tail_cuts) + 1 if tail else 1
+    layout = [i for s in range(nst) for i, t in enumerate(stage) if t == s]
     opt = FusedAdam((named[n] for n in main), lr=lr, layout=layout, zero_grad_in_step=zero_grad_in_step)
-    tails = [opt.offsets[i] for i, t in enumerate(is_tail) if t]
-    opt.tail_offset = min(tails) if tails else opt.numel
+    bounds = [0]
+    for s in range(1, nst):
+        offs = [opt.offsets[i] for i, t in enumerate(stage) if t >= s]
+        bounds.append(min(offs) if offs else opt.numel)
+    bounds.append(opt.numel)
+    opt.bucket_bounds = bounds
+    opt.tail_offset = bounds[1] if len(bounds) > 2 else opt.numel
     return opt, FusedAdam((named[n] for n in aux), lr=aux_lr, zero_grad_in_step=zero_grad_in_step)

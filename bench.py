@@ -357,13 +357,14 @@ def main():
         x = torch.rand(args.batch, 3, args.size, args.size, generator=gen).to(dev)
     broadcast_parameters_(net)
     torch.cuda.manual_seed(1000 + rank)      # per-rank training noise
-    # N > 1: the gradient exchange in two buckets, the first overlapped with the backward of the model's tail
-    # (compressai.distributed.OverlappedAllReduce: g_a for the zoo models; the feature encoders + channel
-    # aligner for Master_compresser)
+    # N > 1: the gradient exchange in buckets, each all-reduced while the backward below it runs
+    # (compressai.distributed.OverlappedAllReduce: the head, then g_a in pieces for the zoo models; the head,
+    # then the feature encoders + channel aligner for Master_compresser)
     overlap = world > 1 and not args.serial_allreduce
     # the reference loop order (zero_grad, forward, backward, step): the Adam kernels consume the gradients
     # and zero_grad() launches nothing (FusedAdam zero_grad_in_step)
-    opt, aux_opt = configure_optimizers(net, tail=net.dp_tail if overlap else (), zero_grad_in_step=not args.keep_grads)
+    opt, aux_opt = configure_optimizers(net, tail=net.dp_tail if overlap else (), zero_grad_in_step=not args.keep_grads,
+                                        tail_cuts=tuple(getattr(net, "dp_tail_cuts", ())) if overlap else ())
     sync = OverlappedAllReduce.for_model(net, opt) if overlap else None
     criterion = RateDistortionLoss(args.quality)
     state = {}
@@ -440,11 +441,12 @@ def main():
             with torch.cuda.graph(gA):
                 fwd_bwd()
         else:
-            gT = torch.cuda.CUDAGraph()             # g_a's backward: the second phase
+            gT = [torch.cuda.CUDAGraph() for _ in range(1, sync.nphases)]   # the tail's backward phases
             with torch.cuda.graph(gA):
                 fwd(two_phase=True)
-            with torch.cuda.graph(gT, pool=gA.pool()):
-                sync.backward_tail()
+            for i, g in enumerate(gT, 1):
+                with torch.cuda.graph(g, pool=gA.pool()):
+                    sync.backward_phase(i)
         with torch.cuda.graph(gB, pool=gA.pool()):
             opt_part()
 
@@ -453,8 +455,9 @@ def main():
             if sync is None:
                 allreduce_mean_(opt.flat_grad)
             else:
-                sync.reduce_head()                  # overlaps gT on the compute stream
-                gT.replay()
+                for i, g in enumerate(gT, 1):
+                    sync.reduce_bucket(i - 1)       # side stream, overlapped with phase i on the compute stream
+                    g.replay()
                 sync.finish()
             gB.replay()
 
@@ -504,8 +507,10 @@ def main():
                        "model": args.model, "quality": args.quality, "global_batch": args.batch * world,
                        "per_gpu_batch": args.batch, "seq_len": None,
                        "patch": list(MM_IR) if multimodal else args.size, "parallelism": f"dp{world}",
-                       "grad_exchange": (f"2-bucket all-reduce, head overlapped with the {'+'.join(p.rstrip('.') for p in net.dp_tail)} "
-                                         "backward (2-phase backward)" if sync else
+                       "grad_exchange": (f"{sync.nphases}-bucket all-reduce (head, then "
+                                         f"{'+'.join(p.rstrip('.') for p in net.dp_tail)} in {sync.nphases - 1} "
+                                         f"pieces), bucket i overlapped with backward phase i+1; exposed: the last "
+                                         f"({4 * sync.buckets[-1].numel() / 1e6:.2f} MB)" if sync else
                                          "1 all-reduce after backward") if world > 1 else None},
             "final_loss": round(loss, 5),
             "roofline": roof, "dominant_class": dom_class, "step_roofline": step_roof, "cpu_baseline": cpu,

@@ -5,7 +5,7 @@ ScaleHyperprior(32, 48), "cheng2020-attn" = Cheng2020Attention(192), "multimodal
 guided by a replicated, frozen Guided_compresser(RGB) run under no_grad in training mode, train.py:208-246),
 FusedAdam, a HIP-graph-captured forward + RD loss + backward with the injected noise read from static device
 buffers, then the gradient exchange bench.py runs: one all-reduce of the flat gradient (serial) or the
-two-bucket OverlappedAllReduce at the model's cut (overlap / overlap-eager).
+bucketed OverlappedAllReduce at the model's cuts (overlap / overlap-eager).
 Writes the averaged flat gradient (rank 0) to $CAI_DIST_OUT.
 """
 import os
@@ -60,7 +60,8 @@ def main():
         broadcast_parameters_(guide)                 # replicated, frozen: never exchanged
     mode = os.environ.get("CAI_DIST_MODE", "serial")
     overlap = mode.startswith("overlap")
-    opt, aux_opt = configure_optimizers(net, tail=net.dp_tail if overlap else ())
+    opt, aux_opt = configure_optimizers(net, tail=net.dp_tail if overlap else (),
+                                        tail_cuts=tuple(net.dp_tail_cuts) if overlap else ())
     sync = OverlappedAllReduce.for_model(net, opt) if overlap else None
     b = inp["x"].shape[0] // world
     sl = slice(rank * b, (rank + 1) * b)
@@ -98,10 +99,12 @@ def main():
         if sync is None:
             allreduce_mean_(opt.flat_grad)
             return
-        sync.reduce_head()
         if replayed:
-            gT.replay()
+            for i, g in enumerate(gT, 1):
+                sync.reduce_bucket(i - 1)
+                g.replay()
         else:
+            sync.reduce_head()
             sync.backward_tail()
         sync.finish()
 
@@ -122,9 +125,10 @@ def main():
         with torch.cuda.graph(graph):
             fwd_bwd()
         if sync is not None:
-            gT = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gT, pool=graph.pool()):
-                sync.backward_tail()
+            gT = [torch.cuda.CUDAGraph() for _ in range(1, sync.nphases)]
+            for i, g in enumerate(gT, 1):
+                with torch.cuda.graph(g, pool=graph.pool()):
+                    sync.backward_phase(i)
         opt.flat_grad.fill_(123.0)           # the replay must overwrite this
         graph.replay()
         exchange(True)
@@ -133,7 +137,9 @@ def main():
     if rank == 0:
         main_names, _ = parameter_groups(net)
         torch.save({"flat_grad": opt.flat_grad.cpu(), "offsets": list(opt.offsets), "names": main_names,
-                    "numels": [p.numel() for p in opt.params], "tail_offset": int(opt.tail_offset)},
+                    "numels": [p.numel() for p in opt.params], "tail_offset": int(opt.tail_offset),
+                    "bounds": [int(b) for b in opt.bucket_bounds],
+                    "nphases": sync.nphases if sync is not None else 1},
                    os.environ["CAI_DIST_OUT"])
     dist.barrier()
     dist.destroy_process_group()

@@ -72,9 +72,12 @@ def _oracle_case(kind):
                                        ("multimodal", "serial"), ("multimodal", "overlap"),
                                        ("multimodal", "overlap-eager")])
 def test_world2_allreduced_flat_grad_matches_oracle(cuda, tmp_path, kind, mode):
-    """serial: one all-reduce after the graph replay (bench.py --serial-allreduce); overlap: the two-bucket
-    exchange of compressai.distributed.OverlappedAllReduce (head bucket all-reduced on a side stream while the
-    captured tail-backward graph replays); overlap-eager: the same without graphs."""
+    """serial: one all-reduce after the graph replay (bench.py --serial-allreduce); overlap: the bucketed
+    exchange of compressai.distributed.OverlappedAllReduce (bucket i all-reduced on a side stream while the
+    captured graph of backward phase i + 1 replays: head, then g_a in 3 / 4 pieces for C2 / cheng2020-attn, the
+    feature encoders + channel aligner for C5); overlap-eager: the same without graphs."""
+    from compressai.optim import dp_stage
+
     ref, case = _oracle_case(kind)
     inp, outp = tmp_path / "in.pt", tmp_path / "out.pt"
     torch.save(case, inp)
@@ -99,11 +102,16 @@ def test_world2_allreduced_flat_grad_matches_oracle(cuda, tmp_path, kind, mode):
     flat = res["flat_grad"]
     gmax = max(p.grad.abs().max().item() for p in ref.parameters() if p.grad is not None)
     tail = tuple(("g_a.",) if kind != "multimodal" else ("fencoder1.", "fencoder2.", "ch_aligner."))
+    cuts = {"c2": ("g_a.4", "g_a.2"), "cheng2020-attn": ("g_a.5", "g_a.2", "g_a.1"), "multimodal": ()}[kind]
     n_tail = 0
+    if mode.startswith("overlap"):
+        assert res["nphases"] == len(cuts) + 2 == len(res["bounds"]) - 1, (res["nphases"], res["bounds"])
     for name, off, n in zip(res["names"], res["offsets"], res["numels"]):
         g = flat[off:off + n]
         if mode.startswith("overlap"):
             assert (off >= res["tail_offset"]) == name.startswith(tail), name   # the bucket layout
+            st = dp_stage(name, tail, cuts)
+            assert res["bounds"][st] <= off and off + n <= res["bounds"][st + 1], (name, st, off, res["bounds"])
             n_tail += name.startswith(tail)
         gr = pr[name].grad
         if gr is None:

@@ -341,3 +341,41 @@ def test_residual_skip_branch_side_stream_bit_identical(cuda, monkeypatch, kind)
     assert torch.equal(outs[True][1], outs[False][1])
     for k in outs[True][2]:
         assert torch.equal(outs[True][2][k], outs[False][2][k]), k
+
+
+def test_resunit_ledger_replay_owns_buffers(cuda):
+    """bench.py's per-launch ledger replays recorded launches after the step (dominant_roofline, --replay): the
+    fused ResidualUnit entries must own every buffer their argument block points at.  Record one AttentionBlock
+    step, drop the caller's references, churn the caching allocator, then replay each resunit entry: the forward's
+    output is rewritten bit for bit and nothing faults."""
+    import gc
+
+    import compressai.layers as L
+    from compressai import _ledger
+
+    torch.manual_seed(7)
+    mod = L.AttentionBlock(128).to(cuda)
+    x = _pm(torch.randn(2, 128, 16, 16, device=cuda)).requires_grad_()
+    with _ledger.recording() as led:
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = mod(x)
+        y.float().sum().backward()
+    led.finish()
+    ents = [e for e in led.entries if e.kernel.startswith("resunit")]
+    assert any(e.kind == "conv_fwd" for e in ents) and any(e.kind == "conv_dgrad" for e in ents)
+    del y, x, mod
+    gc.collect()
+    torch.cuda.empty_cache()
+    junk = [torch.full((1 << 20,), 7.0, device=cuda) for _ in range(16)]      # reuse of any freed block
+    for e in ents:
+        if e.kind == "conv_fwd":
+            out = e.replay.__defaults__[0][7]
+            ref = out.clone()
+            out.zero_()
+            e.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(out.view(torch.int16), ref.view(torch.int16))
+        else:
+            e.replay()
+    torch.cuda.synchronize()
+    assert all(bool((j == 7.0).all()) for j in junk)
