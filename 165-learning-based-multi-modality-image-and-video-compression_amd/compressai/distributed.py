@@ -72,6 +72,18 @@ class _Boundary(torch.autograd.Function):
         return g
 
 
+def _cut_site(model: torch.nn.Module, name: str):
+    """Where the cut at the input of child `name` ("g_a.4") is marked: the parent's cut slot for a product
+    Sequential (compressai.layers.Sequential), else the child's forward pre-hook."""
+    from .layers.conv import Sequential
+
+    parent, idx = name.rsplit(".", 1)
+    pm = model.get_submodule(parent)
+    if isinstance(pm, Sequential):
+        return (pm, int(idx))
+    return model.get_submodule(name)
+
+
 class OverlappedAllReduce:
     """Bucketed gradient all-reduce overlapped with the backward.
 
@@ -114,14 +126,23 @@ class OverlappedAllReduce:
         self._in_phase = False
         self._model = None
         self._handles = []
+        self._slots = []
         if hasattr(tail, "_dp_cut") and hasattr(tail, "dp_tail"):
             self._model = tail
             tail._dp_cut_fn = lambda *ts: self._mark(0, *ts)
         else:
             self._handles.append(tail.register_forward_hook(lambda m, i, o: self._mark(0, o)[0]))
         for k, m in enumerate(cut_modules):
-            self._handles.append(m.register_forward_pre_hook(
-                lambda mod, inputs, k=k: (self._mark(k + 1, inputs[0]),) + tuple(inputs[1:])))
+            if isinstance(m, tuple):
+                # (parent Sequential, child index): the product Sequential runs its children through .run()
+                # (conv + activation epilogue fusion), so the cut goes into its own cut slots
+                parent, idx = m
+                slots = parent.__dict__.setdefault("_cut_fns", {})
+                slots[idx] = lambda x, k=k: self._mark(k + 1, x)
+                self._slots.append((parent, idx))
+            else:
+                self._handles.append(m.register_forward_pre_hook(
+                    lambda mod, inputs, k=k: (self._mark(k + 1, inputs[0]),) + tuple(inputs[1:])))
 
     @classmethod
     def for_model(cls, model: torch.nn.Module, opt):
@@ -135,7 +156,7 @@ class OverlappedAllReduce:
         main = [(n, p) for n, p in model.named_parameters() if not n.endswith(".quantiles")]
         head = [p for n, p in main if dp_stage(n, tail, cuts) == 0]
         stages = [[p for n, p in main if dp_stage(n, tail, cuts) == s] for s in range(1, len(cuts) + 2)]
-        return cls(opt.flat_grad, bounds, model, head, [model.get_submodule(c) for c in cuts], stages)
+        return cls(opt.flat_grad, bounds, model, head, [_cut_site(model, c) for c in cuts], stages)
 
     @property
     def nphases(self) -> int:
@@ -216,5 +237,8 @@ class OverlappedAllReduce:
         for h in self._handles:
             h.remove()
         self._handles = []
+        for parent, idx in self._slots:
+            parent.__dict__.get("_cut_fns", {}).pop(idx, None)
+        self._slots = []
         if self._model is not None:
             self._model._dp_cut_fn = None

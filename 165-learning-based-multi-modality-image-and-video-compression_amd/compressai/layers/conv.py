@@ -101,8 +101,13 @@ class Sequential(nn.Sequential):
         i = 0
         pending = (MASK_SIGN, 0.0) if input_abs else (in_mask, in_mask_param)
         first = True
+        cuts = self.__dict__.get("_cut_fns")
         while i < n:
             m = mods[i]
+            if cuts and i in cuts:
+                # a gradient-bucket cut at this child's input (compressai.distributed): children are called
+                # through .run(), which bypasses forward pre-hooks
+                x = cuts[i](x)
             convlike = isinstance(m, _CONVS) or _is_subpel(m)
             if convlike:
                 a, prm = _act_of(mods[i + 1]) if i + 1 < n else (ACT_NONE, 0.0)
@@ -132,6 +137,18 @@ class Sequential(nn.Sequential):
                 pending = (MASK_NONE, 0.0)
                 i += 1
             first = False
+        if cuts:
+            # every cut must fall on a child this loop starts (not inside a fused conv + activation pair)
+            visited = set()
+            j = 0
+            while j < n:
+                visited.add(j)
+                mm = mods[j]
+                fused = (isinstance(mm, _CONVS) or _is_subpel(mm)) and j + 1 < n and _act_of(mods[j + 1])[0] != ACT_NONE
+                j += 2 if fused else 1
+            bad = [c for c in cuts if c not in visited]
+            if bad:
+                raise ValueError(f"Sequential: gradient-bucket cut at child {bad} falls inside a fused conv + activation")
         if act != ACT_NONE and not (n and (isinstance(mods[-1], _CONVS) or _is_subpel(mods[-1])
                                            or isinstance(mods[-1], nn.PixelShuffle))):
             x = ActFn.apply(x, act, act_param)

@@ -65,10 +65,12 @@ constexpr int Q_BYTES = Q_BIASO + 128 * 4;
 constexpr int Q_TOTAL = 100;                                              // steps per tile
 constexpr int Q_STORE1 = Q_PAIRS ? 15 : 16;                               // chunk 1's footprint -> LDS
 constexpr int Q_NSTORE = Q_TM * Q_TN / 2;                                 // 16-byte stores per wave and phase
-// CAI_QUAD_SPREAD = d > 0: phases 0..2 issue their output stores one every d steps under the next phase's steps
-// (their bf16 results wait in registers); 0: at the phase's end, all at once.  Phase 3's go out at the end.
+// CAI_QUAD_SPREAD = d > 0 (A/B): phases 0..2 issue their output stores one every d steps under the next phase's
+// steps (their bf16 results wait in registers); 0 (default): at the phase's end, all at once.  Phase 3's go out
+// at the end.  Measured equal within 1 % (d = 1, 2 with 4-, 6- and 8-stage rings: 49.0 - 50.1 us per launch,
+// profiles/r05_quad_variants.log); the ring depth (3 - 8) and one barrier per two steps were equal too.
 #ifndef CAI_QUAD_SPREAD
-#define CAI_QUAD_SPREAD 2
+#define CAI_QUAD_SPREAD 0
 #endif
 constexpr int Q_SPREAD = CAI_QUAD_SPREAD;
 static_assert(Q_BYTES <= 160 * 1024 && Q_NPI + Q_NSTB <= Q_STORE1 + (Q_PAIRS ? 2 : 0) && Q_STORE1 < 17, "quad tile");

@@ -84,7 +84,7 @@ class NoiseFeed:
 def _noise_like(x: torch.Tensor) -> torch.Tensor:
     # entropy_models.py:163-167 draws uniform_(-0.5, 0.5) of x's shape
     if NoiseFeed.active is not None:
-        return NoiseFeed.active.pop(x.shape).to(x.dtype)
+        return NoiseFeed.active.pop(x.shape).to(device=x.device, dtype=x.dtype)
     return torch.empty_like(x).uniform_(-0.5, 0.5)
 
 
@@ -324,7 +324,7 @@ class EntropyBottleneck(EntropyModel):
         if training:
             # noise is injected in the logical (input) layout so both paths see the same values
             if NoiseFeed.active is not None:
-                n = NoiseFeed.active.pop(x.shape).to(x.dtype)
+                n = NoiseFeed.active.pop(x.shape).to(device=x.device, dtype=x.dtype)
                 n = n.permute(*perm).contiguous().reshape(values.shape)
                 outputs = values + n
             else:
