@@ -1106,11 +1106,17 @@ _AB_STREAM_PX = int(os.environ.get("CAI_AB_STREAM_PX", "16384"))
 _AB_SIDE = {}
 
 
-def _ab_side(x):
+def _ab_side(x, params=()):
+    """The side stream for a small branch, or None.  `params`: the parameters of a branch that is its own autograd
+    node (a module called on the side stream): its gradients must go straight into FusedAdam's buffer (direct
+    grads) -- a gradient returned to an AccumulateGrad node of the caller's stream would cross streams (torch
+    syncs it, warns, and such a step could not be graph-captured)."""
     if not (_AB_STREAM and x.is_cuda and _ledger.active() is None):
         return None
     B, _, H, W = x.shape
     if B * H * W > _AB_STREAM_PX:
+        return None
+    if torch.is_grad_enabled() and any(p.requires_grad and not direct_grad(p) for p in params):
         return None
     s = _AB_SIDE.get(x.device)
     if s is None:

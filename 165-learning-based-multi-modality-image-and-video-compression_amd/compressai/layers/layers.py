@@ -78,7 +78,7 @@ class ResidualBlockWithStride(nn.Module):
         self.skip = conv1x1(in_ch, out_ch, stride=stride) if (stride != 1 or in_ch != out_ch) else None
 
     def forward(self, x):
-        side = _ab_side(x) if self.skip is not None else None
+        side = _ab_side(x, self.skip.parameters()) if self.skip is not None else None
         if side is not None:   # the skip conv on the side stream (autograd runs its backward there too)
             main = torch.cuda.current_stream(x.device)
             side.wait_stream(main)
@@ -106,7 +106,7 @@ class ResidualBlockUpsample(nn.Module):
         self.upsample = subpel_conv3x3(in_ch, out_ch, upsample)
 
     def forward(self, x):
-        side = _ab_side(x)
+        side = _ab_side(x, self.upsample.parameters())
         if side is not None:   # the upsampling branch on the side stream (autograd runs its backward there too)
             main = torch.cuda.current_stream(x.device)
             side.wait_stream(main)

@@ -151,7 +151,10 @@ def test_train_one_epoch_as_written_fp16(cuda):
     torch.cuda.amp.autocast() (fp16) around forward + criterion and around aux_loss, GradScaler scale / unscale_ /
     clip_grad_norm_ / step / update, torch.optim.Adam from the reference's configure_optimizers (train.py:111-142),
     on the product ScaleHyperprior.  Runs with no policy call: the fp16 regions compute in bf16 (one warning), the
-    losses stay finite and track the same steps under an explicit bf16 autocast, and the scaler never skips."""
+    losses stay finite and track the same steps under an explicit bf16 autocast, and the scaler never skips.
+    Parity caveat (INTEGRATION.md): the reference's fp16 autocast carries 11 mantissa bits, this path bf16's 8;
+    no reference-held fixture pins either.  The first step's loss (before any update) is checked against the
+    fp32 CPU oracle on the same weights, batch and quantisation noise within the bf16 model-level bound."""
     import warnings
 
     from torch.cuda.amp import GradScaler, autocast
@@ -160,15 +163,25 @@ def test_train_one_epoch_as_written_fp16(cuda):
     from compressai.entropy_models import set_noise_source
     from compressai.losses import RateDistortionLoss
 
+    first = {}
+
     def run(fp16):
-        _, model = _pair("bmshj2018-hyperprior", (64, 96), cuda)
+        ref, model = _pair("bmshj2018-hyperprior", (64, 96), cuda)
+        first.setdefault("ref", ref)
         optimizer, aux_optimizer = _torch_optimizers(model, 1e-4, 1e-3)
         scaler = GradScaler()
         criterion = RateDistortionLoss(1)
         data = torch.rand(8, 3, 64, 64, generator=torch.Generator().manual_seed(5))
         loader = DataLoader(TensorDataset(data), batch_size=2, shuffle=False)
         gen = torch.Generator().manual_seed(6)
-        set_noise_source(lambda t: torch.empty(t.shape).uniform_(-0.5, 0.5, generator=gen).to(cuda))
+        drawn = []
+
+        def source(t):
+            n = torch.empty(t.shape).uniform_(-0.5, 0.5, generator=gen)
+            drawn.append(n)
+            return n.to(cuda)
+
+        set_noise_source(source)
         losses, auxes, scales = [], [], []
         try:
             model.train()
@@ -192,6 +205,9 @@ def test_train_one_epoch_as_written_fp16(cuda):
                 scaler.update()
                 losses.append(out_criterion["loss"].item())
                 auxes.append(aux_loss.item())
+                if i == 0:
+                    first.setdefault("noise", list(drawn))
+                    first.setdefault("x", d.cpu())
                 scales.append(scaler.get_scale())
         finally:
             set_noise_source(None)
@@ -208,6 +224,11 @@ def test_train_one_epoch_as_written_fp16(cuda):
     assert s16 == sorted(s16) and s16[0] == 65536.0        # no inf / nan step was skipped
     for a, b in zip(l16, lbf):
         assert abs(a - b) <= 1e-2 * abs(b), (l16, lbf)
+    # step 0 against the fp32 oracle (same initial weights, batch and noise): the bf16 model-level loss bound
+    with O.NoiseFeed(list(first["noise"])):
+        out_r = first["ref"](first["x"])
+    l_ref = O.RateDistortionLoss(1)(out_r, first["x"])["loss"].item()
+    assert abs(l16[0] - l_ref) <= 1e-2 * abs(l_ref), (l16[0], l_ref)
 
 
 def _param_set(dev, seed=9, large=False):

@@ -320,22 +320,45 @@ def test_attention_block_two_streams_bit_identical(cuda, monkeypatch, H):
 @pytest.mark.parametrize("kind", ["stride", "upsample"])
 def test_residual_skip_branch_side_stream_bit_identical(cuda, monkeypatch, kind):
     """ResidualBlockWithStride's skip conv / ResidualBlockUpsample's upsampling branch on the side stream (small
-    maps): output and every gradient bit-identical to the serial order."""
+    maps): output and every gradient bit-identical to the serial order.  The branch is its own autograd node, so
+    it takes the side stream only with its gradients written straight into FusedAdam's buffer (the training
+    path); with gradients returned to autograd's accumulators it stays on the caller's stream."""
     import compressai.layers as L
     from compressai import _ops
+    from compressai.optim import FusedAdam
 
     torch.manual_seed(13)
     mod = (L.ResidualBlockWithStride(192, 192, 2) if kind == "stride" else L.ResidualBlockUpsample(192, 192, 2)).to(cuda)
     x0 = _pm(torch.randn(4, 192, 16, 16, device=cuda))
+    branch = mod.skip if kind == "stride" else mod.upsample
+    taken = []
+    real_side = _ops._ab_side
+
+    def spy(x, params=()):
+        params = list(params)
+        s = real_side(x, params)
+        if params:
+            taken.append(s is not None)
+        return s
+
+    monkeypatch.setattr(L.layers, "_ab_side", spy)
+    # plain autograd accumulators: the branch stays serial (no cross-stream AccumulateGrad)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        mod(x0.clone().requires_grad_()).float().sum().backward()
+    assert taken == [False]
+    opt = FusedAdam(mod.parameters(), lr=1e-4)       # direct gradients: the training path
+    assert all(_ops.direct_grad(p) for p in branch.parameters())
     outs = {}
     for on in (True, False):
         monkeypatch.setattr(_ops, "_AB_STREAM", on)
-        mod.zero_grad(set_to_none=True)
+        opt.zero_grad()
+        taken.clear()
         x = x0.clone().requires_grad_()
         with torch.autocast("cuda", dtype=torch.bfloat16):
             y = mod(x)
         y.float().backward(torch.sin(torch.arange(y.numel(), device=cuda, dtype=torch.float32)).view_as(y))
         torch.cuda.synchronize()
+        assert taken == [on]
         outs[on] = (y.detach().float(), x.grad.float(), {k: p.grad.clone() for k, p in mod.named_parameters()})
     assert torch.equal(outs[True][0], outs[False][0])
     assert torch.equal(outs[True][1], outs[False][1])
