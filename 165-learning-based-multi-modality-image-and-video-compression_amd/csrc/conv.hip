@@ -4397,7 +4397,6 @@ static int run_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int3
     if (rc) return rc;
     CAI_CHECK_ARG(x && dy && dw, "conv_wgrad: null pointer");
     const WgradPlan W = make_wgrad_plan(g, dtype, true, in_abs || in_sq);
-    CAI_CHECK_ARG(W.Cq_pad <= 1024, "conv_wgrad: %d input-side channels (the slab reduce takes <= 1024)", W.Cq);
     CAI_CHECK_ARG(workspace && ws_bytes >= W.ws_slab + W.ws_bias + W.ws_col + 256, "conv_wgrad: workspace too small");
     const int VEC = dtype == CAI_BF16 ? 8 : 4;
     WgradArgs a{};
