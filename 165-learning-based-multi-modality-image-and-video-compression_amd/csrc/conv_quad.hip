@@ -42,38 +42,20 @@ constexpr int Q_PW = Q_TW + 2, Q_NPOS = (Q_TH + 2) * Q_PW;                 // 10
 constexpr int Q_PLANE = (Q_NPOS + 15) / 16 * 16;                          // = 0 (mod 16): conflict-free reads
 constexpr int Q_PATCH = 8 * Q_PLANE * 16;                                 // one 64-channel chunk
 constexpr int Q_NPI = (8 * Q_NPOS + Q_NT - 1) / Q_NT;                     // footprint cells per thread and chunk
-// CAI_QUAD_PAIRS=1 (A/B): one barrier per two steps -- at an even step both stages freed since the last barrier
-// refill (steps s + NSTB - 1 and s + NSTB) and the barrier certifies the stages of steps s + 1 and s + 2
-#ifndef CAI_QUAD_PAIRS
-#define CAI_QUAD_PAIRS 0
-#endif
+// ring depth: 3 .. 8 stages and one barrier per two steps measured equal (profiles/r05_quad_variants.log)
 #ifndef CAI_QUAD_NSTB
-#define CAI_QUAD_NSTB (CAI_QUAD_PAIRS ? 6 : 4)
+#define CAI_QUAD_NSTB 4
 #endif
-// CAI_QUAD_DIAG (timing ablations only -- the results are wrong): bit 1 no step barrier, 2 no weight DMAs in
-// the loop, 4 no output stores, 8 no fragment reads in the loop
-#ifndef CAI_QUAD_DIAG
-#define CAI_QUAD_DIAG 0
-#endif
-constexpr int Q_DIAG = CAI_QUAD_DIAG;
-constexpr bool Q_PAIRS = CAI_QUAD_PAIRS;
 constexpr int Q_NSTB = CAI_QUAD_NSTB;                                     // weight ring depth
-static_assert(!Q_PAIRS || (Q_NSTB % 2 == 0 && Q_NSTB >= 4), "pairs: an even ring of >= 4 stages");
 constexpr int Q_BSTAGE = Q_NT * 16;                                       // 128 rows x 64 bytes
 constexpr int Q_RING = 2 * Q_PATCH, Q_BIASO = Q_RING + Q_NSTB * Q_BSTAGE;
 constexpr int Q_BYTES = Q_BIASO + 128 * 4;
 constexpr int Q_TOTAL = 100;                                              // steps per tile
-constexpr int Q_STORE1 = Q_PAIRS ? 15 : 16;                               // chunk 1's footprint -> LDS
+constexpr int Q_STORE1 = 16;                                              // chunk 1's footprint -> LDS
 constexpr int Q_NSTORE = Q_TM * Q_TN / 2;                                 // 16-byte stores per wave and phase
-// CAI_QUAD_SPREAD = d > 0 (A/B): phases 0..2 issue their output stores one every d steps under the next phase's
-// steps (their bf16 results wait in registers); 0 (default): at the phase's end, all at once.  Phase 3's go out
-// at the end.  Measured equal within 1 % (d = 1, 2 with 4-, 6- and 8-stage rings: 49.0 - 50.1 us per launch,
-// profiles/r05_quad_variants.log); the ring depth (3 - 8) and one barrier per two steps were equal too.
-#ifndef CAI_QUAD_SPREAD
-#define CAI_QUAD_SPREAD 0
-#endif
-constexpr int Q_SPREAD = CAI_QUAD_SPREAD;
-static_assert(Q_BYTES <= 160 * 1024 && Q_NPI + Q_NSTB <= Q_STORE1 + (Q_PAIRS ? 2 : 0) && Q_STORE1 < 17, "quad tile");
+// a phase's 8 output stores per wave go out at the end of its last step, all at once (spreading them over the next
+// phase's steps, one every 1 or 2 steps, measured equal: profiles/r05_quad_variants.log)
+static_assert(Q_BYTES <= 160 * 1024 && Q_NPI + Q_NSTB <= Q_STORE1 && Q_STORE1 < 17, "quad tile");
 
 __host__ __device__ constexpr int q_start(int p) { return p <= 0 ? 0 : p == 1 ? 36 : p == 2 ? 60 : p == 3 ? 84 : 100; }
 __host__ __device__ constexpr int q_phase(int s) { return s < 36 ? 0 : s < 60 ? 1 : s < 84 ? 2 : 3; }
@@ -96,30 +78,13 @@ __host__ __device__ constexpr int q_toff(int s) {
 // vector-memory operations a wave issues inside step j after that step's weight DMA: the next chunk's
 // footprint cell (steps < NPI), the four fence loads behind the last one, and a finished phase's output
 // stores (issued at the end of the phase's last step)
-// store k of the previous phase issued in step j (spread mode), -1: none
-__host__ __device__ constexpr int q_spread_k(int j) {
-    if (Q_SPREAD <= 0 || q_phase(j) == 0) return -1;
-    const int d = j - q_start(q_phase(j));
-    return (d % Q_SPREAD == 0 && d / Q_SPREAD < Q_NSTORE) ? d / Q_SPREAD : -1;
-}
-__host__ __device__ constexpr int q_stores(int j) {
-    if (Q_DIAG & 4) return 0;
-    if (Q_SPREAD > 0) return (q_spread_k(j) >= 0 ? 1 : 0) + (j == Q_TOTAL - 1 ? Q_NSTORE : 0);
-    return q_last(j) ? Q_NSTORE : 0;
-}
 __host__ __device__ constexpr int q_after_dma(int j) {
-    return (j < Q_NPI ? 1 : 0) + (j == Q_NPI - 1 ? 4 : 0) + q_stores(j);
+    return (j < Q_NPI ? 1 : 0) + (j == Q_NPI - 1 ? 4 : 0) + (q_last(j) ? Q_NSTORE : 0);
 }
-// weight DMAs of step j: lockstep, step j + NSTB; pairs, at even j steps j + NSTB - 1 and j + NSTB
-__host__ __device__ constexpr int q_dmas(int j) {
-    return (Q_DIAG & 2) ? 0 : Q_PAIRS ? ((j % 2 == 0) ? (j + Q_NSTB - 1 < Q_TOTAL ? 1 : 0) + (j + Q_NSTB < Q_TOTAL ? 1 : 0) : 0)
-                   : (j + Q_NSTB < Q_TOTAL ? 1 : 0);
-}
-__host__ __device__ constexpr int q_ops(int j) { return q_dmas(j) + q_after_dma(j); }
-// operations issued after the weight DMA that step s's wait retires (lockstep: step s + 1's; pairs, at even s:
-// step s + 2's, issued right after step s + 1's), when step s starts (the prologue drained everything)
+__host__ __device__ constexpr int q_ops(int j) { return (j + Q_NSTB < Q_TOTAL ? 1 : 0) + q_after_dma(j); }
+// operations issued after step s + 1's weight DMA when step s starts (the prologue drained everything)
 __host__ __device__ constexpr int q_younger(int s) {
-    const int i = Q_PAIRS ? s + 2 - Q_NSTB : s + 1 - Q_NSTB;   // the step that issued that DMA
+    const int i = s + 1 - Q_NSTB;   // the step that issued step s + 1's DMA
     int n = 0;
     if (i >= 0) n += q_after_dma(i);
     for (int j = (i >= 0 ? i + 1 : 0); j < s; ++j) n += q_ops(j);
@@ -278,14 +243,14 @@ __global__ __launch_bounds__(512, 1) void conv_halo_quad_kernel(const ConvArgs a
         const bool ok = qy < P.OHg && qx < P.OWg && n < a.Cout;
         bf16* Y = reinterpret_cast<bf16*>(a.y) + (int64_t)b * a.ysb + (int64_t)(P.oy0 + 2 * qy) * a.ysy +
                   (int64_t)(P.ox0 + 2 * qx) * a.ysx + n;
-        if ((Q_DIAG & 4) ? a.ysb == -12345 : ok)   // (diag: results kept live, never stored)
+        if (ok)
             *reinterpret_cast<u32x4*>(Y) = u32x4{pend[tm][2 * pp][0], pend[tm][2 * pp][1], pend[tm][2 * pp + 1][0],
                                                  pend[tm][2 * pp + 1][1]};
     };
 
     // prologue: the first weight stages (lockstep NSTB, pairs NSTB - 1), the bias, chunk 0's footprint; everything
     // drained once
-    q_for<0, Q_PAIRS ? Q_NSTB - 1 : Q_NSTB>([&](auto sc) { issue_b(sc); });
+    q_for<0, Q_NSTB>([&](auto sc) { issue_b(sc); });
     const int nb = tid & 127;
     const float* bsrc = (a.bias && nb < a.Cout) ? a.bias + nb : reinterpret_cast<const float*>(quad_zero_page);
     const float bval = *reinterpret_cast<const __attribute__((address_space(1))) float*>(reinterpret_cast<uintptr_t>(bsrc));
@@ -303,33 +268,17 @@ __global__ __launch_bounds__(512, 1) void conv_halo_quad_kernel(const ConvArgs a
         constexpr int s = decltype(sc)::value;
         constexpr int yg = q_younger(s);
         static_assert(yg >= 0 && yg < 64, "vmcnt range");
-        if constexpr (!Q_PAIRS || s % 2 == 0) {
-            wait_vmcnt<yg>();    // step s + 1's (pairs: and s + 2's) weights have landed (this wave's share)
-            wait_lgkmcnt0();
-            if constexpr (!(Q_DIAG & 1)) __builtin_amdgcn_s_barrier();   // ... every wave's share; stage s % NSTB
-        }                                                                  // (pairs: and (s-1) % NSTB) is free
+        wait_vmcnt<yg>();    // step s + 1's weights have landed (this wave's share)
+        wait_lgkmcnt0();
+        __builtin_amdgcn_s_barrier();   // ... every wave's share; stage s % NSTB is free
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (Q_DIAG & 2) {
-        } else if constexpr (Q_PAIRS) {
-            if constexpr (s % 2 == 0 && s + Q_NSTB - 1 < Q_TOTAL) issue_b(std::integral_constant<int, s + Q_NSTB - 1>{});
-            if constexpr (s % 2 == 0 && s + Q_NSTB < Q_TOTAL) issue_b(std::integral_constant<int, s + Q_NSTB>{});
-        } else if constexpr (s + Q_NSTB < Q_TOTAL) {
-            issue_b(std::integral_constant<int, s + Q_NSTB>{});
-        }
+        if constexpr (s + Q_NSTB < Q_TOTAL) issue_b(std::integral_constant<int, s + Q_NSTB>{});
         if constexpr (s < Q_NPI) load_cell(1, s);
         if constexpr (s == Q_NPI - 1) fence_loads();
         // read from step 18 on (its fragments are read in step 17, after the next barrier)
         if constexpr (s == Q_STORE1) store_patch(1);
-        if constexpr (q_spread_k(s) >= 0 && !(Q_DIAG & 4))
-            store_k(std::integral_constant<int, q_phase(s) - 1>{}, q_spread_k(s));
         u32x4 na[Q_TM], nb2[Q_TN];
-        if constexpr (s + 1 < Q_TOTAL && !(Q_DIAG & 8)) read_frags(std::integral_constant<int, s + 1>{}, na, nb2);
-        if constexpr (Q_DIAG & 8) {
-#pragma unroll
-            for (int i = 0; i < Q_TM; ++i) na[i] = fa[i] + 1u;
-#pragma unroll
-            for (int i = 0; i < Q_TN; ++i) nb2[i] = fb[i] + 1u;
-        }
+        if constexpr (s + 1 < Q_TOTAL) read_frags(std::integral_constant<int, s + 1>{}, na, nb2);
 #pragma unroll
         for (int tm = 0; tm < Q_TM; ++tm)
 #pragma unroll
@@ -350,10 +299,8 @@ __global__ __launch_bounds__(512, 1) void conv_halo_quad_kernel(const ConvArgs a
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (q_last(s)) {
             finish();
-            if constexpr (Q_SPREAD <= 0 || s == Q_TOTAL - 1 || (Q_DIAG & 4)) {
 #pragma unroll
-                for (int k = 0; k < Q_NSTORE; ++k) store_k(std::integral_constant<int, q_phase(s)>{}, k);
-            }
+            for (int k = 0; k < Q_NSTORE; ++k) store_k(std::integral_constant<int, q_phase(s)>{}, k);
         }
     });
     asm volatile("" ::"v"(fence_[0]), "v"(fence_[1]), "v"(fence_[2]), "v"(fence_[3]));
