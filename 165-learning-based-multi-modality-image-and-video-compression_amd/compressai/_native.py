@@ -18,6 +18,7 @@ CAI_OK, CAI_EINVAL, CAI_EDEVICE, CAI_EWORKSPACE = 0, 1, 2, 3
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_LEAKY = 0, 1, 2
 MASK_NONE, MASK_POS, MASK_LEAKY, MASK_SIGN = 0, 1, 2, 3
+MASK_BEFORE_RES = 16   # flag: the dgrad mask scales the conv's input gradient only (cai.h CAI_MASK_BEFORE_RES)
 Q_NOISE, Q_DEQUANTIZE, Q_SYMBOLS = 0, 1, 2
 ADAM_CLIP, ADAM_SKIP_NONFINITE, ADAM_ZERO_GRAD = 1, 2, 4          # cai_adam_step flags (include/cai.h)
 ADAM_SMALL_N = 1 << 16                         # cai_adam_step: one-block path at or below this many parameters
@@ -135,6 +136,7 @@ SIGNATURES = {
     "cai_edge_wgrad": (_I, [_G, _P, _P, c_int32, _P, _P, c_int32, _P, _S, _P]),
     "cai_edge_wgrad_deferred": (_I, [_G, _P, _P, c_int32, _P, _P, c_int32, _P, _S, _P, POINTER(ReduceJob)]),
     "cai_add_act": (_I, [_I, _P, c_int32, _P, c_int32, _P, c_int32, _I64, c_int32, c_int32, _F, _P]),
+    "cai_axpy_dev": (_I, [_I64, _P, _P, _P, _P]),
     "cai_act": (_I, [_I, _P, c_int32, _P, c_int32, _I64, c_int32, c_int32, _F, _P]),
     "cai_gdn1_out": (_I, [_I, _P, c_int32, _P, c_int32, _P, c_int32, _I64, c_int32, c_int32, _P]),
     "cai_gdn1_out_bwd": (_I, [_I, _P, c_int32, _P, c_int32, _P, c_int32, _P, c_int32, _P, c_int32, _I64, c_int32,

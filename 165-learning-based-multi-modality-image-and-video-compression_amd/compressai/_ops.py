@@ -27,7 +27,8 @@ from typing import Optional, Sequence, Tuple
 import torch
 
 from . import _ledger
-from ._native import (ACT_LEAKY, ACT_NONE, ACT_RELU, BF16, F32, MASK_LEAKY, MASK_NONE, MASK_POS, Q_DEQUANTIZE, Q_NOISE,
+from ._native import (ACT_LEAKY, ACT_NONE, ACT_RELU, BF16, F32, MASK_BEFORE_RES, MASK_LEAKY, MASK_NONE, MASK_POS,
+                      Q_DEQUANTIZE, Q_NOISE,
                       JOB_NONE, NOISE_BUF, NOISE_DRAW, NOISE_REPLAY, ConvGeom, EbGrads, EbParams, NoiseSrc, RdGrads,
                       RdInputs, ReduceJob, ResunitArgs, ResunitWgradArgs, lib)
 
@@ -563,6 +564,7 @@ class ConvFn(torch.autograd.Function):
         ctx.edge = _edge_mode(ctx, spec, g, dt)
         ctx.small = False
         ctx.has_res = res is not None
+        ctx.fan = _fan_role(x, "take")
         if res is not None:
             if not residual_fusable(spec) or ctx.edge or tuple(res.shape) != (B, cout, g.out_h, g.out_w):
                 raise ValueError(f"conv residual: not fusable for this layer (res {tuple(res.shape)}, "
@@ -673,7 +675,25 @@ class ConvFn(torch.autograd.Function):
             dres2 = getattr(ctx, "dx_res2", None)   # AttentionBlockFn: + the other branch's / the gate's gradient
             if dres is None and dres2 is not None:
                 dres, dres2 = dres2, None
-            if dres is not None and dt == torch.bfloat16 and aux is None and ldx % 8 == 0:
+            fan, done = getattr(ctx, "fan", None), False
+            if fan is not None and fan.pending is not None and dres is None and dt == torch.bfloat16 and ldx % 8 == 0:
+                # FanOutFn: the input's other consumer has run its backward -- its gradient joins this dgrad's
+                # epilogue (after the input mask: dx = mask(x) * conv_input_grad + other) instead of a separate add
+                post = fan.pending
+                if aux is None:
+                    dres, fan.pending = post, None
+                elif "halo" not in _conv_kernel(g, dt, 1)():
+                    ppm, pld = to_pm(post, dt, 4)
+                    mode = spec.in_mask | MASK_BEFORE_RES
+                    _ledger.run(lambda ppm=ppm, dx=dx, wt=wt, gpm=gpm, ws=ws: lib.cai_conv_dgrad_res(
+                                    ctypes.byref(g), code, _p(gpm), gld, _p(wt), _p(ppm), pld, _p(dx), ldx, mode,
+                                    spec.in_mask_param, _p(xpm), ctx.xld, _p(ws), wsb, st),
+                                "conv_dgrad", _conv_kernel(g, dt, 1), fl, nb + post.numel() * _es(dt), dt,
+                                _ledger.shape_of(g))
+                    fan.pending, done = None, True
+            if done:
+                pass
+            elif dres is not None and dt == torch.bfloat16 and aux is None and ldx % 8 == 0:
                 rpm, rld = to_pm(dres, dt, 4)
                 maux = xpm if rmask != MASK_NONE else None
                 if dres2 is not None:
@@ -755,6 +775,78 @@ class _SubCtx:
 
     def save_for_backward(self, *tensors):
         self.saved_tensors = tensors
+
+
+class _FanIn:
+    """The gradient hand-off of FanOutFn: the giving consumer's backward leaves its input gradient here; the taking
+    consumer's backward, when it runs later, adds it in its own dgrad epilogue; FanOutFn adds what is left."""
+
+    __slots__ = ("pending",)
+
+    def __init__(self):
+        self.pending = None
+
+
+_FAN_ATTR = "_cai_fan"
+
+
+def _fan_role(x, role):
+    f = getattr(x, _FAN_ATTR, None)
+    return f[0] if f is not None and f[1] == role else None
+
+
+class FanOutFn(torch.autograd.Function):
+    """x -> (x_take, x_give): two aliases of one tensor read by two consumers (the hyperprior models' y: h_a's
+    first conv and the GaussianConditional), so that their gradients meet in a kernel rather than in autograd's
+    input buffer (an ATen add per step).  The GaussianConditional (giver) hands its x gradient over instead of
+    returning it; the conv (taker), whose backward runs after it (h_a's gradient arrives through the scales),
+    adds it in its dgrad epilogue (cai_conv_dgrad_res: CAI_MASK_BEFORE_RES under h_a's abs mask).  Whatever is
+    not absorbed -- another order, a layout the epilogue cannot take -- is added here.  Values are autograd's:
+    dx = dx_take + dx_give."""
+
+    @staticmethod
+    def forward(ctx, x, box):
+        ctx.set_materialize_grads(False)
+        ctx.box = box
+        return x.view_as(x), x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, ga, gb):
+        box = ctx.box
+        extra, box.pending = box.pending, None
+        gs = [t for t in (ga, gb, extra) if t is not None]
+        if not gs:
+            return None, None
+        total = gs[0]
+        for t in gs[1:]:
+            total = _add_grads(total, t)
+        return total, None
+
+
+def _add_grads(a, b):
+    """a + b for two gradients of one tensor: the native add for bf16 pixel-major, else torch."""
+    if a.dtype == b.dtype == torch.bfloat16 and a.is_cuda and a.dim() == 4 and a.shape == b.shape:
+        ap, ald = to_pm(a, torch.bfloat16, 4)
+        bp, bld = to_pm(b, torch.bfloat16, 4)
+        y, yld = _out_pm_like(a, torch.bfloat16)
+        B, C, H, W = a.shape
+        _ledger.run(lambda ap=ap, bp=bp, y=y: lib.cai_add_act(BF16, _p(ap), ald, _p(bp), bld, _p(y), yld, B * H * W,
+                                                             C, ACT_NONE, 0.0, _stream()),
+                    "add_act", "add_act_kernel", 0, 3 * B * H * W * C * 2, torch.bfloat16)
+        return y
+    return a + b
+
+
+def fan_out(x):
+    """(x_take, x_give) for a tensor read by a conv (x_take) and a GaussianConditional (x_give); (x, x) when x
+    does not require a gradient."""
+    if not (torch.is_grad_enabled() and x.requires_grad):
+        return x, x
+    box = _FanIn()
+    a, b = FanOutFn.apply(x, box)
+    setattr(a, _FAN_ATTR, (box, "take"))
+    setattr(b, _FAN_ATTR, (box, "give"))
+    return a, b
 
 
 class ResidualChainFn(torch.autograd.Function):
@@ -1374,6 +1466,7 @@ class GaussianFn(torch.autograd.Function):
                             + (4 if nr is not None else 0)), torch.float32, f"{n_el} elements")
         ctx.save_for_backward(xr, sr, mr, nr)
         ctx.draw = draw
+        ctx.give = _fan_role(x, "give")
         ctx.cfg = (mode, scale_bound, lik_bound, xld, sld, mld, nld, npix, C, x.shape, x.dtype, scales.shape,
                    scales.dtype, means is not None)
         return q, lik
@@ -1402,6 +1495,8 @@ class GaussianFn(torch.autograd.Function):
                     n_el * (2 * es_x + (4 if mr is not None else 2) * es_s + (4 if nr is not None else 0)
                             + (4 if gl is not None else 0) + (es_x if gq_r is not None else 0)),
                     torch.float32, f"{n_el} elements")
+        if ctx.give is not None:    # FanOutFn: x's other consumer adds it (in its dgrad epilogue)
+            ctx.give.pending, dx = dx, None
         return dx, ds, dm, None, None, None, None
 
 
@@ -1527,7 +1622,8 @@ class BottleneckAuxFn(torch.autograd.Function):
 
     The loss is |F(quantiles) - target| summed, so d loss / d quantiles is linear in the upstream gradient:
     the forward launch also produces it for an upstream gradient of 1, and the backward only scales it
-    (one elementwise op instead of a second pass through the 5-layer CDF chains)."""
+    (one elementwise launch, cai_axpy_dev into a direct gradient, instead of a second pass through the 5-layer
+    CDF chains)."""
 
     @staticmethod
     def forward(ctx, quantiles, target, *params):
@@ -1553,7 +1649,12 @@ class BottleneckAuxFn(torch.autograd.Function):
         (dq1,) = ctx.saved_tensors
         gl = g.float().reshape(())
         if direct_grad(ctx.qparam):
-            ctx.qparam.grad.view_as(dq1).addcmul_(dq1, gl)
+            gq = ctx.qparam.grad
+            if not gq.is_contiguous() or gq.numel() != dq1.numel():
+                raise RuntimeError("BottleneckAuxFn: a direct gradient must be a contiguous view of the flat buffer")
+            _ledger.run(lambda dq1=dq1, gl=gl, gq=gq: lib.cai_axpy_dev(dq1.numel(), _p(dq1), _p(gl), _p(gq),
+                                                                       _stream()),
+                        "eb_aux_bwd", "axpy_dev_kernel", 0, 12 * dq1.numel(), torch.float32)
             return (None, None, *([None] * ctx.nparams))
         return ((dq1 * gl).view_as(ctx.qparam), None, *([None] * ctx.nparams))
 

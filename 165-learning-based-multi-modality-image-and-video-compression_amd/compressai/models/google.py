@@ -41,7 +41,7 @@ from ..entropy_models import EntropyBottleneck, GaussianConditional
 from ..entropy_models.entropy_models import _QuantizeFn, _draw_noise, _noise_for
 from .._native import Q_DEQUANTIZE, Q_NOISE
 from ..layers import GDN, MaskedConv2d, Sequential
-from .._ops import CatFn, ConvFn, ConvSpec
+from .._ops import CatFn, ConvFn, ConvSpec, fan_out
 from .._prepack import prepacked_forward
 from ..ans import BufferedRansEncoder, RansDecoder
 from ..layers.conv import Conv2d
@@ -243,10 +243,11 @@ class ScaleHyperprior(CompressionModel):
         y = self._dp_cut(self.g_a(x))
         side = _side_stream(y, False)
         if side is None:
-            z = self.h_a(y, input_abs=True)          # h_a(|y|)
+            y_ha, y_gc = fan_out(y)                  # y's two gradients meet in h_a's first dgrad epilogue
+            z = self.h_a(y_ha, input_abs=True)       # h_a(|y|)
             z_hat, z_likelihoods = self.entropy_bottleneck(z)
             scales_hat = self.h_s(z_hat)
-            y_hat, y_likelihoods = self.gaussian_conditional(y, scales_hat)
+            y_hat, y_likelihoods = self.gaussian_conditional(y_gc, scales_hat)
             x_hat = self.g_s(y_hat)
             return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods, "z": z_likelihoods}}
         main = torch.cuda.current_stream()
@@ -323,10 +324,11 @@ class MeanScaleHyperprior(ScaleHyperprior):
         y = self._dp_cut(self.g_a(x))
         side = _side_stream(y, False) if self.training else None   # eval: y_hat = round(y - means) + means
         if side is None:
-            z = self.h_a(y)
+            y_ha, y_gc = fan_out(y)
+            z = self.h_a(y_ha)
             z_hat, z_likelihoods = self.entropy_bottleneck(z)
             scales_hat, means_hat = self.h_s(z_hat).chunk(2, 1)
-            y_hat, y_likelihoods = self.gaussian_conditional(y, scales_hat, means=means_hat)
+            y_hat, y_likelihoods = self.gaussian_conditional(y_gc, scales_hat, means=means_hat)
             x_hat = self.g_s(y_hat)
             return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods, "z": z_likelihoods}}
         main = torch.cuda.current_stream()

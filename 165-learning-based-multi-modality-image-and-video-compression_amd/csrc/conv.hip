@@ -90,12 +90,21 @@ __device__ __forceinline__ void out_pixel(const ConvArgs& a, const PhaseDesc& P,
 
 // EXTRA = false: the caller has checked that there is no residual and no mask (no loads at all: a load here sits
 // behind the earlier iterations' stores on the shared vmcnt, and its wait serialized a whole epilogue's stores --
-// 38 % of the phase kernel's block time)
-template <typename T, bool EXTRA = true>
+// 38 % of the phase kernel's block time).  POST = false: a.res_post is not supported (the halo kernels: its
+// registers spill their main loops; the host rejects it there)
+template <typename T, bool EXTRA = true, bool POST = true>
 __device__ __forceinline__ void store_out_chunk(const ConvArgs& a, const PhaseDesc& P, int plane, int m, int n,
                                                 float (&v)[8], int VO) {
     int b, oy, ox;
     out_pixel<T>(a, P, plane, m, b, oy, ox);
+    auto mask = [&]() {
+        const T* AUX = reinterpret_cast<const T*>(a.aux);
+        const int64_t pa = (((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.aux_ld + n;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            if (e < VO) v[e] *= mask_val(a.mask_mode, to_f32(AUX[pa + e]), a.mask_param);
+    };
+    if (EXTRA && POST && a.mask_mode && a.res_post) mask();
     if (EXTRA && a.res) {
         const int64_t px = ((int64_t)b * a.out_h + oy) * a.out_w + ox;
         const bf16* R = a.res + px * a.res_ld + n;
@@ -104,13 +113,7 @@ __device__ __forceinline__ void store_out_chunk(const ConvArgs& a, const PhaseDe
         for (int e = 0; e < 8; ++e)
             if (e < VO) v[e] = apply_act(v[e] + (float)R[e] + (R2 ? (float)R2[e] : 0.f), a.act, a.act_param);
     }
-    if (EXTRA && a.mask_mode) {
-        const T* AUX = reinterpret_cast<const T*>(a.aux);
-        const int64_t pa = (((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.aux_ld + n;
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-            if (e < VO) v[e] *= mask_val(a.mask_mode, to_f32(AUX[pa + e]), a.mask_param);
-    }
+    if (EXTRA && a.mask_mode && !(POST && a.res_post)) mask();
     const int64_t off = (int64_t)b * a.ysb + (int64_t)oy * a.ysy + (int64_t)ox * a.ysx + n;
     if (a.y_dtype == CAI_BF16) {
         bf16x8 h;
@@ -122,22 +125,23 @@ __device__ __forceinline__ void store_out_chunk(const ConvArgs& a, const PhaseDe
     }
 }
 
-template <typename T>
+template <typename T, bool POST = true>
 __device__ __forceinline__ void store_out_scalar(const ConvArgs& a, const PhaseDesc& P, int plane, int m, int n,
                                                  float v) {
     int b, oy, ox;
     out_pixel<T>(a, P, plane, m, b, oy, ox);
+    const float mk = a.mask_mode ? mask_val(a.mask_mode, to_f32(reinterpret_cast<const T*>(a.aux)[
+                                                 (((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.aux_ld + n]),
+                                             a.mask_param)
+                                 : 1.f;
+    if (POST && a.res_post) v *= mk;
     if (a.res) {
         const int64_t px = ((int64_t)b * a.out_h + oy) * a.out_w + ox;
         v += (float)a.res[px * a.res_ld + n];
         if (a.res2) v += (float)a.res2[px * a.res2_ld + n];
         v = apply_act(v, a.act, a.act_param);
     }
-    if (a.mask_mode) {
-        const T* AUX = reinterpret_cast<const T*>(a.aux);
-        v *= mask_val(a.mask_mode, to_f32(AUX[(((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.aux_ld + n]),
-                      a.mask_param);
-    }
+    if (!(POST && a.res_post)) v *= mk;
     st_any(a.y, a.y_dtype, (int64_t)b * a.ysb + (int64_t)n * a.ysc + (int64_t)oy * a.ysy + (int64_t)ox * a.ysx, v);
 }
 
@@ -148,7 +152,7 @@ __device__ __forceinline__ void store_out_scalar(const ConvArgs& a, const PhaseD
 // rowm(row): the GEMM row m of tile row `row`, or -1 outside the phase
 // slab: the split-K partial slab this block writes (-1: blockIdx.z, the phase * ksplit + split of the
 // phase-major grids)
-template <typename T, int BM, int BN, int WM, int WN, int NTH, class RowMap>
+template <typename T, int BM, int BN, int WM, int WN, int NTH, class RowMap, bool POST = true>
 __device__ __forceinline__ void conv_epilogue_rows(const ConvArgs& a, const PhaseDesc& P, int plane, int n0, float* E,
                                                    const f32x4 (&acc)[BM / WM / 16][BN / WN / 16], RowMap rowm,
                                                    int slab = -1) {
@@ -207,7 +211,7 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvArgs& a, const Phas
                 if (VO == 8) hi = *reinterpret_cast<const f32x4*>(E + row * ES + cc * VO + 4);
                 v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
                 v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
-                store_out_chunk<T, decltype(extra)::value>(a, P, plane, m, n, v, VO);
+                store_out_chunk<T, decltype(extra)::value, POST>(a, P, plane, m, n, v, VO);
             }
         };
         if (a.res || a.mask_mode)
@@ -219,7 +223,7 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvArgs& a, const Phas
             const int col = id / BM, row = id - (id / BM) * BM;
             const int m = rowm(row), n = n0 + col;
             if (m < 0 || n >= a.Cout) continue;
-            store_out_scalar<T>(a, P, plane, m, n, E[row * ES + col]);
+            store_out_scalar<T, POST>(a, P, plane, m, n, E[row * ES + col]);
         }
     }
 }
@@ -238,7 +242,7 @@ __host__ __device__ __forceinline__ bool epi_t_direct(const ConvArgs& a) {
            (!a.mask_mode || ((a.aux_ld & 3) == 0 && (reinterpret_cast<uintptr_t>(a.aux) & 7) == 0));
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int NTH, class RowMap, bool NOLDS = false>
+template <typename T, int BM, int BN, int WM, int WN, int NTH, class RowMap, bool NOLDS = false, bool POST = true>
 __device__ __forceinline__ void conv_epilogue_rows_t(const ConvArgs& a, const PhaseDesc& P, int plane, int n0,
                                                      float* E, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
                                                      RowMap rowm, int slab) {
@@ -332,13 +336,17 @@ __device__ __forceinline__ void conv_epilogue_rows_t(const ConvArgs& a, const Ph
                         for (int r = 0; r < 4; ++r) rf[r] += (float)rv2[r];
                     }
                 }
-#pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = apply_act(acc[tm][tn][r] + bv[tn][r] + rf[r], a.act, a.act_param);
+                f32x4 mk = f32x4{1.f, 1.f, 1.f, 1.f};
                 if (NOLDS && AUX) {
                     const bf16x4 mv = *reinterpret_cast<const bf16x4*>(AUX + n);
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] *= mask_val(a.mask_mode, (float)mv[r], a.mask_param);
+                    for (int r = 0; r < 4; ++r) mk[r] = mask_val(a.mask_mode, (float)mv[r], a.mask_param);
                 }
+                // res_post (dgrad): mask(aux) * (conv input gradient) + res; else mask(aux) * act(... + res)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    v[r] = (POST && a.res_post) ? (acc[tm][tn][r] + bv[tn][r]) * mk[r] + rf[r]
+                                      : apply_act(acc[tm][tn][r] + bv[tn][r] + rf[r], a.act, a.act_param) * mk[r];
                 bf16x4 h;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) h[r] = (bf16)v[r];
@@ -378,7 +386,7 @@ __device__ __forceinline__ void conv_epilogue_rows_t(const ConvArgs& a, const Ph
                 if (VO == 8) hi = *reinterpret_cast<const f32x4*>(E + row * ES + cc * VO + 4);
                 v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
                 v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
-                store_out_chunk<T, decltype(extra)::value>(a, P, plane, m, n, v, VO);
+                store_out_chunk<T, decltype(extra)::value, POST>(a, P, plane, m, n, v, VO);
             }
         };
         if (a.res || a.mask_mode)
@@ -390,7 +398,7 @@ __device__ __forceinline__ void conv_epilogue_rows_t(const ConvArgs& a, const Ph
             const int col = id / BM, row = id - (id / BM) * BM;
             const int m = rowm(row), n = n0 + col;
             if (m < 0 || n >= a.Cout) continue;
-            store_out_scalar<T>(a, P, plane, m, n, E[row * ES + col]);
+            store_out_scalar<T, POST>(a, P, plane, m, n, E[row * ES + col]);
         }
     }
     }
@@ -1160,10 +1168,11 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvArgs a, int
         return (oy < P.OHg && ox < P.OWg) ? b * plane + oy * P.OWg + ox : -1;
     };
     if (CAI_HALO_T)
-        conv_epilogue_rows_t<bf16, BM, BN, WM, WN, 512>(a, P, plane, 0, reinterpret_cast<float*>(smem), acc, rowm,
-                                                        (int)blockIdx.z);
+        conv_epilogue_rows_t<bf16, BM, BN, WM, WN, 512, decltype(rowm), false, false>(
+            a, P, plane, 0, reinterpret_cast<float*>(smem), acc, rowm, (int)blockIdx.z);
     else
-        conv_epilogue_rows<bf16, BM, BN, WM, WN, 512>(a, P, plane, 0, reinterpret_cast<float*>(smem), acc, rowm);
+        conv_epilogue_rows<bf16, BM, BN, WM, WN, 512, decltype(rowm), false>(a, P, plane, 0,
+                                                                             reinterpret_cast<float*>(smem), acc, rowm);
 }
 
 // Halo-staged s^2-phase implicit GEMM for the stride-2 k5 transposed convolutions (ConvTranspose2d k5 s2 p2
@@ -1376,11 +1385,11 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
         return (oy < P.OHg && ox < P.OWg) ? b * plane + oy * P.OWg + ox : -1;
     };
     if (CAI_HALO_PH_T || BN > 128)
-        conv_epilogue_rows_t<bf16, BM, BN, WM, WN, NT, decltype(rowm), (BN > 128)>(
+        conv_epilogue_rows_t<bf16, BM, BN, WM, WN, NT, decltype(rowm), (BN > 128), false>(
             a, P, plane, n0, reinterpret_cast<float*>(smem), acc, rowm, ph * a.ksplit + split);
     else
-        conv_epilogue_rows<bf16, BM, BN, WM, WN, NT>(a, P, plane, n0, reinterpret_cast<float*>(smem), acc, rowm,
-                                                     ph * a.ksplit + split);
+        conv_epilogue_rows<bf16, BM, BN, WM, WN, NT, decltype(rowm), false>(
+            a, P, plane, n0, reinterpret_cast<float*>(smem), acc, rowm, ph * a.ksplit + split);
 }
 
 
@@ -1561,7 +1570,7 @@ __device__ __forceinline__ void conv_halo_wide_body(const ConvArgs& a, char* sme
         const int oy = ty0 + row / H::TW, ox = tx0 + row % H::TW;
         return (oy < P.OHg && ox < P.OWg) ? b * plane + oy * P.OWg + ox : -1;
     };
-    conv_epilogue_rows_t<bf16, BM, BN, WM, WN, 512, decltype(rowm), (BN > 128)>(
+    conv_epilogue_rows_t<bf16, BM, BN, WM, WN, 512, decltype(rowm), (BN > 128), false>(
         a, P, plane, n0, reinterpret_cast<float*>(smem), acc, rowm, ph * a.ksplit + split);
 }
 
@@ -3807,6 +3816,11 @@ static int run_conv(const cai_conv_geom* g, int dtype, int direction, const void
     CAI_CHECK_ARG(((uintptr_t)x & 15) == 0, "%s: input not 16-byte aligned", name);
     CAI_CHECK_ARG((int64_t)g->batch * P.in_h * P.in_w * x_ld * dtype_size(dtype) < (1ll << 31),
                   "%s: input larger than 2 GiB", name);
+    const int res_post = (mask_mode & CAI_MASK_BEFORE_RES) != 0;
+    mask_mode &= ~CAI_MASK_BEFORE_RES;
+    CAI_CHECK_ARG(mask_mode >= CAI_MASK_NONE && mask_mode <= CAI_MASK_SIGN, "%s: bad mask mode", name);
+    CAI_CHECK_ARG(!res_post || (res && direction == 1 && mask_mode != CAI_MASK_NONE),
+                  "%s: CAI_MASK_BEFORE_RES needs a residual, a mask and the dgrad direction", name);
     CAI_CHECK_ARG(!mask_mode || (aux && aux_ld >= P.kout_c), "%s: mask needs aux", name);
     CAI_CHECK_ARG(L.ws_bytes == 0 || (workspace && ws_bytes >= L.ws_bytes && ((uintptr_t)workspace & 15) == 0),
                   "%s: workspace of %zu bytes required", name, L.ws_bytes);
@@ -3835,8 +3849,12 @@ static int run_conv(const cai_conv_geom* g, int dtype, int direction, const void
                   name);
     a.res = reinterpret_cast<const bf16*>(res); a.res_ld = res_ld;
     a.res2 = reinterpret_cast<const bf16*>(res2); a.res2_ld = res2_ld;
+    a.res_post = res_post;
     if ((L.halo_ph || L.halo_s1) && L.hbn > 128 && L.ksplit == 1 && !epi_t_direct(a))
         L = conv_launch(g, dtype, direction, in_abs, false);    // the 192-channel tiles store from registers only
+    CAI_CHECK_ARG(!res_post || !(L.halo || L.halo_ph || L.halo_s1),
+                  "%s: CAI_MASK_BEFORE_RES is not supported by the halo-staged tiles (%s)", name,
+                  "check cai_conv_kernel_name first");
     CAI_CHECK_ARG(L.ws_bytes == 0 || (workspace && ws_bytes >= L.ws_bytes && ((uintptr_t)workspace & 15) == 0),
                   "%s: workspace of %zu bytes required", name, L.ws_bytes);
     a.ksplit = L.ksplit; a.ws = reinterpret_cast<float*>(workspace); a.ws_rows = L.mmax; a.ws_ld = L.ws_ld;

@@ -37,6 +37,7 @@ struct ConvArgs {
     int res_ld;
     const bf16* res2;        // a second residual (dgrad only, cai_conv_dgrad_res2), same layout as res; NULL: none
     int res2_ld;
+    int res_post;            // dgrad: the mask scales the conv's input gradient only, the residuals are added after it
     int ksplit;              // K splits per phase (grid.z = nphase * ksplit)
     float* ws;               // split-K partials [nphase*ksplit][ws_rows][ws_ld] fp32
     int ws_rows, ws_ld;

@@ -281,6 +281,14 @@ __global__ void gdn1_out_bwd_kernel(const T* __restrict__ x, int xld, const T* _
     }
 }
 
+// y += x * g[0] with g a device scalar: the aux loss's parameter gradient scaled by its upstream gradient,
+// accumulated into the optimizer's flat buffer (BottleneckAuxFn.backward)
+__global__ void axpy_dev_kernel(int64_t n, const float* __restrict__ x, const float* __restrict__ g,
+                                float* __restrict__ y) {
+    const float s = g[0];
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) y[i] += x[i] * s;
+}
+
 static int ew_grid2(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(16384, (n + 255) / 256)); }
 
 }  // namespace cai
@@ -306,6 +314,14 @@ int cai_add_act(int dtype, const void* a, int32_t a_ld, const void* b, int32_t b
         hipLaunchKernelGGL(add_act_kernel<float>, dim3(ew_grid2(n)), dim3(256), 0, st, (const float*)a, a_ld,
                            (const float*)b, b_ld, (float*)y, y_ld, (int)npix, C, act, act_param);
     CAI_LAUNCH_CHECK("add_act");
+    return CAI_OK;
+}
+
+int cai_axpy_dev(int64_t n, const float* x, const float* g, float* y, void* stream) {
+    CAI_CHECK_ARG(n >= 0 && (n == 0 || (x && g && y)), "axpy_dev: bad arguments");
+    if (n == 0) return CAI_OK;
+    hipLaunchKernelGGL(axpy_dev_kernel, dim3(ew_grid2(n)), dim3(256), 0, as_stream(stream), n, x, g, y);
+    CAI_LAUNCH_CHECK("axpy_dev");
     return CAI_OK;
 }
 

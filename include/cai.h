@@ -55,6 +55,10 @@ extern "C" {
 #define CAI_MASK_POS 1    /* dgrad epilogue: out *= (aux > 0)          (ReLU backward)      */
 #define CAI_MASK_LEAKY 2  /* dgrad epilogue: out *= aux > 0 ? 1 : slope (LeakyReLU backward) */
 #define CAI_MASK_SIGN 3   /* dgrad epilogue: out *= sign(aux)           (abs backward)       */
+/* flag OR-ed into the mask mode of cai_conv_dgrad_res / _res2: the mask scales the conv's input gradient
+ * only and the residual gradients are added after it -- dx = mask(aux) * conv_input_grad(dy) + res (+ res2):
+ * a tensor read by a masked first layer (h_a's abs, google.py) and by a second consumer */
+#define CAI_MASK_BEFORE_RES 16
 
 /* ---- quantisation modes (entropy_models.py:157-182) -------------------- */
 #define CAI_Q_NOISE 0
@@ -344,6 +348,9 @@ int cai_add_act(int dtype, const void* a, int32_t a_ld, const void* b, int32_t b
 /* y = act(x) for a ReLU / LeakyReLU that no conv epilogue can absorb. */
 int cai_act(int dtype, const void* x, int32_t x_ld, void* y, int32_t y_ld, int64_t npix, int32_t C, int32_t act,
             float act_param, void* stream);
+/* y[i] += x[i] * g[0] (fp32, g a device scalar): a gradient accumulated with its upstream gradient read on
+ * the device (EntropyBottleneck.loss's backward into an optimizer's flat buffer, compressai/_ops.py). */
+int cai_axpy_dev(int64_t n, const float* x, const float* g, float* y, void* stream);
 /* AttentionBlock gate (layers.py:238-243): y = a * sigmoid(b) + x;
  * backward da = g * s(b), db = g * a * s(b) * (1 - s(b)) (dx = g). */
 /* GDN1 (layers/gdn.py:95-121): y = x / norm (inverse: x * norm), norm from a 1x1 conv of |x|

@@ -1067,3 +1067,108 @@ def test_pack_many_matches_pack_weight(cuda, dtype):
             assert torch.equal(got, ref), (type(m).__name__, m.weight.shape, direction)
             checked += 1
     assert checked >= 2 * len(mods) - 2
+
+
+@pytest.mark.parametrize("B,H,cin,cout", [(16, 16, 192, 128), (2, 8, 192, 128), (4, 16, 128, 128)],
+                         ids=["C2-h_a0-B16", "B2-8x8", "B4-128ch"])
+def test_dgrad_mask_before_residual(cuda, B, H, cin, cout):
+    """cai_conv_dgrad_res with CAI_MASK_SIGN | CAI_MASK_BEFORE_RES: dx = sign(x) * conv_input_grad(dy) + res --
+    the hyperprior's y gradient (h_a's first conv under abs, plus the GaussianConditional's gradient, FanOutFn).
+    x holds exact zeros (|x|'s gradient is 0 there: dx = res).  Reference: torch fp32 on the GPU over the same
+    bf16 operands; relative max error <= 1e-2.  The halo-staged tiles reject the flag (checked by name)."""
+    import ctypes
+
+    from compressai import _native as native
+    from compressai._ops import _p, _stream
+
+    raw = native.lib.load()
+    torch.manual_seed(B * 100 + cin)
+    g = native.ConvGeom(B, cin, H, H, cout, H, H, 3, 1, 1, 0, 0)
+    name = raw.cai_conv_kernel_name(ctypes.byref(g), native.BF16, 1, 0).decode()
+    w = (torch.randn(cout, cin, 3, 3, device=cuda) * 0.05).contiguous()
+    wp = torch.empty(native.lib.cai_conv_packed_weight_bytes(ctypes.byref(g), native.BF16, 1), dtype=torch.uint8,
+                     device=cuda)
+    native.lib.cai_conv_pack_weight(ctypes.byref(g), native.BF16, 1, _p(w), None, _p(wp), _stream())
+    dy = torch.randn(B, H, H, cout, device=cuda).bfloat16()                  # pixel-major
+    x = torch.randn(B, H, H, cin, device=cuda)
+    x[x.abs() < 0.2] = 0.0                                                    # ~16 % exact zeros
+    x = x.bfloat16()
+    res = torch.randn(B, H, H, cin, device=cuda).bfloat16()
+    dx = torch.full((B, H, H, cin), float("nan"), device=cuda).bfloat16()
+    nws = native.lib.cai_conv_workspace_bytes(ctypes.byref(g), native.BF16, 1)
+    ws = torch.empty(max(nws, 16), dtype=torch.uint8, device=cuda)
+    mode = native.MASK_SIGN | native.MASK_BEFORE_RES
+
+    def call():
+        native.lib.cai_conv_dgrad_res(ctypes.byref(g), native.BF16, _p(dy), cout, _p(wp), _p(res), cin, _p(dx), cin,
+                                      mode, 0.0, _p(x), cin, _p(ws), nws, _stream())
+
+    if "halo" in name:
+        with pytest.raises(ValueError, match="BEFORE_RES"):
+            call()
+        return
+    call()
+    torch.cuda.synchronize()
+    dyn = dy.float().permute(0, 3, 1, 2)
+    ref = F.conv_transpose2d(dyn, w.bfloat16().float(), padding=1)           # conv2d's input gradient
+    ref = torch.sign(x.float().permute(0, 3, 1, 2)) * ref + res.float().permute(0, 3, 1, 2)
+    out = dx.float().permute(0, 3, 1, 2)
+    assert torch.isfinite(out).all(), name
+    assert relerr(out, ref) < 1e-2, name
+    zero = (x == 0).permute(0, 3, 1, 2)
+    assert torch.equal(out[zero], res.float().permute(0, 3, 1, 2)[zero]), name      # dx = res exactly at x = 0
+
+
+def test_hyperprior_y_gradients_meet_in_dgrad(cuda, monkeypatch):
+    """bmshj2018-hyperprior (q1, 128/192 channels, B=4, 128^2, bf16 autocast): y's two gradients (h_a's first
+    conv under abs, the GaussianConditional) are summed in that conv's dgrad epilogue -- one cai_conv_dgrad_res
+    with CAI_MASK_BEFORE_RES, no add -- and every parameter gradient matches the unfused sum (FanOutFn off:
+    autograd's add) within bf16 rounding: per-tensor cosine >= 0.9999, relative max error <= 2e-2."""
+    from compressai import _native as native
+    from compressai import _ops
+    from compressai.entropy_models.entropy_models import seed_noise
+    from compressai.losses import RateDistortionLoss
+    from compressai.models import google
+    from compressai.zoo import image_models
+
+    torch.manual_seed(7)
+    net = image_models["bmshj2018-hyperprior"](1).to(cuda).train()
+    x = torch.rand(4, 3, 128, 128, device=cuda)
+    crit = RateDistortionLoss(1)
+
+    def grads():
+        net.zero_grad(set_to_none=True)
+        seed_noise(3, cuda)                  # the same training noise in both runs
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = crit(net(x), x)["loss"]
+        loss.backward()
+        return {n: p.grad.detach().clone() for n, p in net.named_parameters() if p.grad is not None}
+
+    real = _ops.lib
+    modes = []
+
+    class Spy:
+        def __getattr__(self, name):
+            fn = getattr(real, name)
+            if name != "cai_conv_dgrad_res":
+                return fn
+
+            def call(*a):
+                modes.append(a[9])
+                return fn(*a)
+            return call
+
+    monkeypatch.setattr(_ops, "lib", Spy())
+    fused = grads()
+    assert native.MASK_SIGN | native.MASK_BEFORE_RES in modes, modes
+    monkeypatch.setattr(google, "fan_out", lambda y: (y, y))
+    modes.clear()
+    plain = grads()
+    assert native.MASK_SIGN | native.MASK_BEFORE_RES not in modes
+    assert fused.keys() == plain.keys()
+    for n in fused:
+        a, b = fused[n].double().flatten(), plain[n].double().flatten()
+        if torch.equal(a, b):        # e.g. the quantiles (no aux loss here: zero in both)
+            continue
+        cos = float(F.cosine_similarity(a, b, dim=0))
+        assert cos > 0.9999 and relerr(a, b) < 2e-2, (n, cos, relerr(a, b))

@@ -445,3 +445,46 @@ def test_master_guided_paper_resolution_vs_oracle(cuda):
         assert total > 0 and len(flips) <= 0.02 * total, flips
     finally:
         torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32, torch.backends.cudnn.enabled = prev
+
+
+def test_c2_step_launches_no_aten_kernels(cuda):
+    """The C2 training step (bmshj2018-hyperprior q1, B=16, 256^2, bf16 autocast; bench.py's step: FusedAdam with
+    zero_grad_in_step, the persistent loss seeds, clip + Adam + aux loss) launches only libcai kernels: no ATen
+    elementwise / fill / reduce kernel (y's two gradients meet in h_a's first dgrad epilogue, the aux loss's
+    quantile gradient accumulates through cai_axpy_dev).  Device kernels of the third eager step, from
+    torch.profiler."""
+    from torch.profiler import ProfilerActivity, profile
+
+    from compressai._ops import loss_seed
+    from compressai.losses import RateDistortionLoss
+    from compressai.optim import configure_optimizers
+    from compressai.zoo import image_models
+
+    torch.manual_seed(0)
+    net = image_models["bmshj2018-hyperprior"](1).to(cuda).train()
+    x = torch.rand(16, 3, 256, 256, device=cuda)
+    opt, aux_opt = configure_optimizers(net, zero_grad_in_step=True)
+    crit = RateDistortionLoss(1)
+
+    def step():
+        opt.zero_grad()
+        aux_opt.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = crit(net(x), x)["loss"]
+        loss.backward(loss_seed(loss))
+        opt.step(max_norm=1.0)
+        aux = net.aux_loss()
+        aux.backward(loss_seed(aux))
+        aux_opt.step()
+
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        step()
+        torch.cuda.synchronize()
+    names = sorted({e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA})
+    print(f"\nC2 step: {len(names)} distinct device kernels / copies")
+    assert len(names) > 20, names               # the profiler saw the step's kernels
+    aten = [n for n in names if "at::" in n or "aten::" in n]
+    assert not aten, aten
