@@ -70,6 +70,13 @@ class ReduceJob(Structure):
     _fields_ = [("kind", c_int32), ("nblocks", c_int32), ("i", c_int32 * 10), ("f", c_float * 2), ("p", c_void_p * 6)]
 
 
+class WgradCall(Structure):
+    """cai_wgrad_call: one weight-gradient call of cai_conv_wgrad_batch."""
+    _fields_ = [("geom", ConvGeom), ("dtype", c_int32), ("x", c_void_p), ("x_ld", c_int32), ("in_abs", c_int32),
+                ("in_sq", c_int32), ("dy", c_void_p), ("dy_ld", c_int32), ("dw", c_void_p), ("db", c_void_p),
+                ("accumulate", c_int32), ("workspace", c_void_p), ("ws_bytes", c_size_t)]
+
+
 class ResunitArgs(Structure):
     _fields_ = [("batch", c_int32), ("h", c_int32), ("w", c_int32), ("n", c_int32),
                 ("x", c_void_p), ("y", c_void_p), ("wa", c_void_p), ("wb", c_void_p), ("wc", c_void_p),
@@ -122,6 +129,7 @@ SIGNATURES = {
     "cai_conv_wgrad_deferred": (_I, [_G, _I, _P, c_int32, c_int32, c_int32, _P, c_int32, _P, _P, c_int32, _P, _S, _P,
                                      POINTER(ReduceJob)]),
     "cai_reduce_jobs": (_I, [POINTER(ReduceJob), c_int32, _P]),
+    "cai_conv_wgrad_batch": (_I, [POINTER(WgradCall), c_int32, _P, POINTER(ReduceJob)]),
     "cai_deconv_small_workspace_bytes": (_S, [_G, _I]),
     "cai_deconv_small_fwd": (_I, [_G, _I, _P, c_int32, _P, _P, _P, _P, _S, _P]),
     "cai_deconv_small_bwd": (_I, [_G, _I, _P, c_int32, _P, _P, _P, c_int32, _P, _P, c_int32, _P, _S, _P]),

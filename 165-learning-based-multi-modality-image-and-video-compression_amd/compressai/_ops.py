@@ -30,7 +30,7 @@ from . import _ledger
 from ._native import (ACT_LEAKY, ACT_NONE, ACT_RELU, BF16, F32, MASK_BEFORE_RES, MASK_LEAKY, MASK_NONE, MASK_POS,
                       Q_DEQUANTIZE, Q_NOISE,
                       JOB_NONE, NOISE_BUF, NOISE_DRAW, NOISE_REPLAY, ConvGeom, EbGrads, EbParams, NoiseSrc, RdGrads,
-                      RdInputs, ReduceJob, ResunitArgs, ResunitWgradArgs, lib)
+                      RdInputs, ReduceJob, ResunitArgs, ResunitWgradArgs, WgradCall, lib)
 
 _VP = ctypes.c_void_p
 _GDN_TWO_PASS = os.environ.get("CAI_GDN_TWO_PASS", "0") == "1"   # A/B knobs (tools/ab_env.sh)
@@ -163,7 +163,11 @@ class _SideDeferred:
 # gradient runs on the side stream.  CAI_DEFER_REDUCE=0 turns it off (A/B).
 _DEFER_REDUCE = os.environ.get("CAI_DEFER_REDUCE", "1") == "1"
 _REDUCE_SPLIT = os.environ.get("CAI_REDUCE_SPLIT", "0") == "1"   # diagnostics: one launch per deferred job
-_JOBS = {}          # (device index, graph task id) -> [jobs, their streams, keep-alive tensors]
+_JOBS = {}          # (device index, graph task id) -> [jobs, their streams, keep-alive tensors, wgrad calls]
+# The latent layers' weight gradients (wgrad_small_kernel: <= 1024 G pixels) are deferred the same way, as whole
+# calls: the flush runs them in one launch (cai_conv_wgrad_batch) ahead of the reduce launch, instead of one
+# launch per layer in the backward's chain.  CAI_WGRAD_BATCH=0 launches them in place (A/B).
+_WGRAD_BATCH = os.environ.get("CAI_WGRAD_BATCH", "1") == "1"
 
 
 def _flush_jobs(key):
@@ -171,14 +175,23 @@ def _flush_jobs(key):
     DDP's finalize uses it), after it has waited for every other stream a job's partial kernel ran on (the
     hyper branch's side stream: inside a captured graph this is the join edge)."""
     pend = _JOBS.pop(key, None)
-    if not pend or not pend[0]:
+    if not pend or not (pend[0] or pend[3]):
         return
     dev = key[0]
-    jobs, streams, keep = pend
+    jobs, streams, keep, calls = pend[:4]
     cur = torch.cuda.current_stream(dev)
     for s in {s.cuda_stream: s for s in streams}.values():
         if s.cuda_stream != cur.cuda_stream:
             cur.wait_stream(s)
+    if calls:
+        arr = (WgradCall * len(calls))(*calls)
+        out = (ReduceJob * len(calls))()
+        lib.cai_conv_wgrad_batch(arr, len(calls), _VP(cur.cuda_stream), out)
+        jobs = jobs + [j for j in out if j.kind != JOB_NONE]
+    if not jobs:
+        for t in keep:
+            t.record_stream(cur)
+        return
     if _REDUCE_SPLIT:   # diagnostics: one launch per job (per-job times in a kernel trace)
         for j in jobs:
             one = (ReduceJob * 1)(j)
@@ -206,14 +219,27 @@ def defer_job(job: "ReduceJob", device: torch.device, *keep: torch.Tensor):
     separate launches, in queue order (csrc/reduce_jobs.hip launch_reduce_jobs)."""
     if job.kind == JOB_NONE:
         return
+    pend = _pending(device)
+    pend[0].append(job)
+    pend[1].append(torch.cuda.current_stream(pend[4]))
+    pend[2].extend(t for t in keep if t is not None)
+
+
+def _pending(device: torch.device):
     dev = device.index if device.index is not None else torch.cuda.current_device()
     key = (dev, torch._C._current_graph_task_id())
     pend = _JOBS.get(key)
     if pend is None:
-        pend = _JOBS[key] = [[], [], []]
+        pend = _JOBS[key] = [[], [], [], [], dev]
         torch.autograd.Variable._execution_engine.queue_callback(lambda: _flush_jobs(key))
-    pend[0].append(job)
-    pend[1].append(torch.cuda.current_stream(dev))
+    return pend
+
+
+def defer_wgrad_call(call: "WgradCall", device: torch.device, *keep: torch.Tensor):
+    """Queue a whole weight-gradient call (its operands and workspace kept alive) for this backward's flush."""
+    pend = _pending(device)
+    pend[3].append(call)
+    pend[1].append(torch.cuda.current_stream(pend[4]))
     pend[2].extend(t for t in keep if t is not None)
 
 
@@ -729,6 +755,18 @@ class ConvFn(torch.autograd.Function):
         return dx, dw, db, None, dres
 
 
+_SMALL_WGRAD = {}
+
+
+def _small_wgrad(g, code, in_abs) -> bool:
+    """Whether this weight gradient takes the latent-size kernel (batched when deferred)."""
+    key = (tuple(getattr(g, f) for f, _ in ConvGeom._fields_), code, int(in_abs))
+    v = _SMALL_WGRAD.get(key)
+    if v is None:
+        v = _SMALL_WGRAD[key] = lib.cai_conv_kernel_name(ctypes.byref(g), code, 2, int(in_abs)) == b"wgrad_small_kernel"
+    return v
+
+
 def conv_wgrad(g, dt, xpm, xld, in_abs, gpm, gld, wparam, bparam, weight, has_bias):
     """Weight (+ bias) gradient of one conv from its input xpm and output gradient gpm (pixel-major): straight
     into the optimizer's flat buffer when the parameters are direct_grad (returns None, None; the final reduce
@@ -744,7 +782,11 @@ def conv_wgrad(g, dt, xpm, xld, in_abs, gpm, gld, wparam, bparam, weight, has_bi
         db = torch.empty(g.out_c, dtype=torch.float32, device=dev) if has_bias else None
     fl, nb = _ledger.conv_cost(g, _es(dt), 2)
     st = _stream()
-    if defer_reduce_ok(direct):
+    if defer_reduce_ok(direct) and _WGRAD_BATCH and not _WGRAD_SIDE_PX and _small_wgrad(g, code, in_abs):
+        wws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        call = WgradCall(g, code, _p(xpm), xld, int(in_abs), 0, _p(gpm), gld, _p(dw), _p(db), 1, _p(wws), nbytes)
+        defer_wgrad_call(call, dev, xpm, gpm, wws)
+    elif defer_reduce_ok(direct):
         npix = g.batch * (g.in_h * g.in_w if g.transposed else g.out_h * g.out_w)
         with _SideDeferred(dev, npix, xpm, gpm):
             wws = torch.empty(nbytes, dtype=torch.uint8, device=dev)

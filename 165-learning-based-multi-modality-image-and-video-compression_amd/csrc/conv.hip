@@ -2408,20 +2408,22 @@ __device__ __forceinline__ int swz_sw(int row, int slot) {
     return row * 128 + ((slot ^ ((((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2))) << 4);
 }
 
+// 8 x (64 x 68 fp32) partial tiles (the loop's staging uses the first 64 KB) + 512 x 8 bias partials
+constexpr int SW_SMEM = SW_NW * 64 * 68 * 4 + 512 * 8 * 4;
+
+// One block of the latent-size weight gradient: block (bx, by) of a (ncb [+ 1]) x gy grid.
 // LONG: more than SW_STEPS steps per wave (M up to small_wgrad_mmax()): the step pairs in a loop
-template <int XT, bool LONG = false>   // X transform on load: 0 none, 1 |x| (h_a's first conv), 2 x^2 (GDN's gamma gradient)
-__global__ __launch_bounds__(512, 1) void wgrad_small_kernel(const SwArgs a) {
-    // 8 x (64 x 68 fp32) partial tiles (the loop's staging uses the first 64 KB) + 512 x 8 bias partials
-    __shared__ __attribute__((aligned(16))) char smem[SW_NW * 64 * 68 * 4 + 512 * 8 * 4];
+template <int XT, bool LONG>   // X transform on load: 0 none, 1 |x| (h_a's first conv), 2 x^2 (GDN's gamma gradient)
+__device__ __forceinline__ void wgrad_small_block(const SwArgs& a, int bx, int by, int gy, char* smem) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr unsigned OOB = 0x80000000u;
-    if ((int)blockIdx.x == a.ncb) {
+    if (bx == a.ncb) {
         // bias: 64 channels per block, pixels over 64 row groups of 8 threads (8 channels each)
         if (!a.db || a.bias_from_g) return;
         float* red = reinterpret_cast<float*>(smem);
         const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<void*>(a.bsrc), (short)0, (int)((int64_t)a.bnpix * a.bsrc_ld * 2), 0x00020000);
-        for (int c0 = blockIdx.y * 64; c0 < a.bc; c0 += gridDim.y * 64) {
+        for (int c0 = by * 64; c0 < a.bc; c0 += gy * 64) {
             const int slot = tid & 7, r = tid >> 3;
             const int c = c0 + slot * 8;
             float sacc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -2455,8 +2457,8 @@ __global__ __launch_bounds__(512, 1) void wgrad_small_kernel(const SwArgs a) {
         }
         return;
     }
-    const int n0 = blockIdx.y * 64;
-    const int t = (int)blockIdx.x / a.cbt, q0 = ((int)blockIdx.x - t * a.cbt) * 64;
+    const int n0 = by * 64;
+    const int t = bx / a.cbt, q0 = (bx - t * a.cbt) * 64;
     const int kh = t / a.k, kw = t - kh * a.k;
     const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<void*>(a.g), (short)0, (int)((int64_t)a.M * a.g_ld * 2), 0x00020000);
@@ -2627,6 +2629,34 @@ __global__ __launch_bounds__(512, 1) void wgrad_small_kernel(const SwArgs a) {
 #pragma unroll
     for (int u = 0; u < 8; ++u)
         if (ok[u]) *d[u] = v[u];
+}
+
+template <int XT, bool LONG = false>
+__global__ __launch_bounds__(512, 1) void wgrad_small_kernel(const SwArgs a) {
+    __shared__ __attribute__((aligned(16))) char smem[SW_SMEM];
+    wgrad_small_block<XT, LONG>(a, (int)blockIdx.x, (int)blockIdx.y, (int)gridDim.y, smem);
+}
+
+// Several latent-size weight gradients in ONE launch (cai_conv_wgrad_batch): job j owns blocks
+// [start[j], start[j + 1]) of a 1-D grid, laid out as its own gx x gy grid.  They are independent (each writes
+// its own slab; bias gradients written in place never repeat within a batch: host check), so a batch costs one
+// launch and fills the chip with blocks that one layer alone leaves idle.
+constexpr int SW_BATCH_MAX = 16;
+struct SwBatch {
+    SwArgs job[SW_BATCH_MAX];
+    int start[SW_BATCH_MAX + 1];
+    int gx[SW_BATCH_MAX], gy[SW_BATCH_MAX];
+    int n;
+};
+
+template <int XT, bool LONG>
+__global__ __launch_bounds__(512, 1) void wgrad_small_batch_kernel(const SwBatch b) {
+    __shared__ __attribute__((aligned(16))) char smem[SW_SMEM];
+    const int L = (int)blockIdx.x;
+    int j = 0;
+    while (j + 1 < b.n && L >= b.start[j + 1]) ++j;
+    const int l = L - b.start[j], gx = b.gx[j];
+    wgrad_small_block<XT, LONG>(b.job[j], l % gx, l / gx, b.gy[j], smem);
 }
 
 // dw[n][q][kh][kw] (+)= sum_s ws[s][n][(kh*k+kw)*Cq_pad + q]
@@ -4407,17 +4437,80 @@ size_t cai_conv_wgrad_workspace_bytes(const cai_conv_geom* g, int dtype) {
                      W2.ws_slab + W2.ws_bias + W2.ws_col}) + 256;
 }
 
-static int run_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_ld, int32_t in_abs,
-                          int32_t in_sq, const void* dy, int32_t dy_ld, float* dw, float* db, int32_t accumulate,
-                          void* workspace, size_t ws_bytes, void* stream, cai_reduce_job* job) {
-    if (job) *job = cai_reduce_job{};
+// The latent-size weight gradient's arguments, grid and (slab -> torch layout) reduce job; `a` carries the
+// operand roles run_conv_wgrad set up (Conv2d: G = dy, X = x; ConvTranspose2d: the other way round).
+static int small_wgrad_setup(const cai_conv_geom* g, const WgradPlan& W, const WgradArgs& a, const void* dy,
+                             int32_t dy_ld, float* dw, float* db, int32_t accumulate, float* slab, SwArgs& sa,
+                             dim3& grid, cai_reduce_job& J) {
+    sa = SwArgs{};
+    sa.g = a.g; sa.g_ld = a.g_ld; sa.Ng = W.Ng;
+    sa.x = a.x; sa.x_ld = a.x_ld; sa.Cq = W.Cq; sa.Cq_pad = W.Cq_pad; sa.in_abs = a.in_abs; sa.in_sq = a.in_sq;
+    sa.B = g->batch; sa.Hg = a.Hg; sa.Wg = a.Wg; sa.Hx = a.Hx; sa.Wx = a.Wx;
+    sa.k = g->kernel; sa.s = g->stride; sa.p = g->pad;
+    sa.M = (int)W.M; sa.cbt = (W.Cq_pad + 63) / 64; sa.ncb = g->kernel * g->kernel * sa.cbt;
+    sa.dw = dw; sa.accumulate = accumulate;
+    sa.bsrc = dy; sa.bsrc_ld = dy_ld; sa.bnpix = g->batch * g->out_h * g->out_w; sa.bc = g->out_c; sa.db = db;
+    sa.bias_from_g = !g->transposed;
+    sa.inv_plane = 1.f / (float)(a.Hg * a.Wg);
+    sa.inv_wg = 1.f / (float)a.Wg;
+    CAI_CHECK_ARG((int64_t)sa.bnpix * dy_ld * 2 < (1ll << 31) && (int64_t)a.B * a.Hx * a.Wx * a.x_ld * 2 < (1ll << 31),
+                  "conv_wgrad: operand larger than 2 GiB");
+    // dW through a one-split slab and a WGRAD job (deferred: joins the backward's batched reduce launch);
+    // A/B knob CAI_SMALL_WGRAD_DIRECT=1: straight into the torch layout (scattered stores)
+    static const bool direct_out = [] {
+        const char* e = getenv("CAI_SMALL_WGRAD_DIRECT");
+        return e && *e == '1';
+    }();
+    sa.slab = direct_out ? nullptr : slab;
+    grid = dim3(sa.ncb + ((db && g->transposed) ? 1 : 0), (W.Ng + 63) / 64);
+    J = cai_reduce_job{};
+    if (direct_out) return CAI_OK;
+    J.kind = CAI_JOB_WGRAD;
+    J.nblocks = wgrad_job_blocks(W.Ng, W.Cq_pad, g->kernel, 0);
+    J.p[0] = slab; J.p[1] = dw;
+    J.i[0] = 1; J.i[1] = W.Ng; J.i[2] = W.ncols; J.i[3] = W.Cq; J.i[4] = W.Cq_pad; J.i[5] = g->kernel;
+    J.i[6] = accumulate;
+    return CAI_OK;
+}
+
+static void launch_wgrad_small(const SwArgs& sa, dim3 grid, bool lng, hipStream_t st) {
+    if (sa.in_abs && lng)
+        hipLaunchKernelGGL((wgrad_small_kernel<1, true>), grid, dim3(512), 0, st, sa);
+    else if (sa.in_abs)
+        hipLaunchKernelGGL((wgrad_small_kernel<1, false>), grid, dim3(512), 0, st, sa);
+    else if (sa.in_sq && lng)
+        hipLaunchKernelGGL((wgrad_small_kernel<2, true>), grid, dim3(512), 0, st, sa);
+    else if (sa.in_sq)
+        hipLaunchKernelGGL((wgrad_small_kernel<2, false>), grid, dim3(512), 0, st, sa);
+    else if (lng)
+        hipLaunchKernelGGL((wgrad_small_kernel<0, true>), grid, dim3(512), 0, st, sa);
+    else
+        hipLaunchKernelGGL((wgrad_small_kernel<0, false>), grid, dim3(512), 0, st, sa);
+}
+
+static void launch_wgrad_small_batch(const SwBatch& b, int cls, hipStream_t st) {
+    const dim3 grid(b.start[b.n]);
+    switch (cls) {
+        case 1: hipLaunchKernelGGL((wgrad_small_batch_kernel<1, false>), grid, dim3(512), 0, st, b); break;
+        case 2: hipLaunchKernelGGL((wgrad_small_batch_kernel<2, false>), grid, dim3(512), 0, st, b); break;
+        case 3: hipLaunchKernelGGL((wgrad_small_batch_kernel<0, true>), grid, dim3(512), 0, st, b); break;
+        case 4: hipLaunchKernelGGL((wgrad_small_batch_kernel<1, true>), grid, dim3(512), 0, st, b); break;
+        case 5: hipLaunchKernelGGL((wgrad_small_batch_kernel<2, true>), grid, dim3(512), 0, st, b); break;
+        default: hipLaunchKernelGGL((wgrad_small_batch_kernel<0, false>), grid, dim3(512), 0, st, b); break;
+    }
+}
+
+// the argument checks and operand roles of a weight-gradient call (run_conv_wgrad, cai_conv_wgrad_batch)
+static int wgrad_prepare(const cai_conv_geom* g, int dtype, const void* x, int32_t x_ld, int32_t in_abs,
+                         int32_t in_sq, const void* dy, int32_t dy_ld, const float* dw, const float* db,
+                         const void* workspace, size_t ws_bytes, WgradPlan& W, WgradArgs& a) {
     int rc = check_geom(g);
     if (rc) return rc;
     CAI_CHECK_ARG(x && dy && dw, "conv_wgrad: null pointer");
-    const WgradPlan W = make_wgrad_plan(g, dtype, true, in_abs || in_sq);
+    W = make_wgrad_plan(g, dtype, true, in_abs || in_sq);
     CAI_CHECK_ARG(workspace && ws_bytes >= W.ws_slab + W.ws_bias + W.ws_col + 256, "conv_wgrad: workspace too small");
     const int VEC = dtype == CAI_BF16 ? 8 : 4;
-    WgradArgs a{};
+    a = WgradArgs{};
     if (!g->transposed) {
         a.g = dy; a.g_ld = dy_ld; a.x = x; a.x_ld = x_ld;
         a.Hg = g->out_h; a.Wg = g->out_w; a.Hx = g->in_h; a.Wx = g->in_w;
@@ -4436,8 +4529,19 @@ static int run_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int3
     CAI_CHECK_ARG(!db || (dy_ld % VEC == 0 && g->out_c <= COLSUM_MAXC), "conv_wgrad: bad bias-gradient layout");
     a.Ng = W.Ng; a.Cq_pad = W.Cq_pad; a.B = g->batch;
     a.k = g->kernel; a.s = g->stride; a.p = g->pad; a.ncols = W.ncols; a.M = W.M; a.split_len = W.split_len;
-    float* slab = reinterpret_cast<float*>(workspace);
-    a.ws = slab;
+    a.ws = reinterpret_cast<float*>(const_cast<void*>(workspace));
+    return CAI_OK;
+}
+
+static int run_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_ld, int32_t in_abs,
+                          int32_t in_sq, const void* dy, int32_t dy_ld, float* dw, float* db, int32_t accumulate,
+                          void* workspace, size_t ws_bytes, void* stream, cai_reduce_job* job) {
+    if (job) *job = cai_reduce_job{};
+    WgradPlan W;
+    WgradArgs a;
+    int rc = wgrad_prepare(g, dtype, x, x_ld, in_abs, in_sq, dy, dy_ld, dw, db, workspace, ws_bytes, W, a);
+    if (rc) return rc;
+    float* slab = a.ws;
     a.ctiles = (W.ncols + 127) / 128;
     a.rtiles = (W.Ng + 127) / 128;
     a.nsub = W.nsub;
@@ -4445,48 +4549,14 @@ static int run_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int3
     a.chunk = W.px_chunk;
     hipStream_t st = as_stream(stream);
     if (small_wgrad_ok(g, dtype)) {
-        SwArgs sa{};
-        sa.g = a.g; sa.g_ld = a.g_ld; sa.Ng = W.Ng;
-        sa.x = a.x; sa.x_ld = a.x_ld; sa.Cq = W.Cq; sa.Cq_pad = W.Cq_pad; sa.in_abs = a.in_abs; sa.in_sq = a.in_sq;
-        sa.B = g->batch; sa.Hg = a.Hg; sa.Wg = a.Wg; sa.Hx = a.Hx; sa.Wx = a.Wx;
-        sa.k = g->kernel; sa.s = g->stride; sa.p = g->pad;
-        sa.M = (int)W.M; sa.cbt = (W.Cq_pad + 63) / 64; sa.ncb = g->kernel * g->kernel * sa.cbt;
-        sa.dw = dw; sa.accumulate = accumulate;
-        sa.bsrc = dy; sa.bsrc_ld = dy_ld; sa.bnpix = g->batch * g->out_h * g->out_w; sa.bc = g->out_c; sa.db = db;
-        sa.bias_from_g = !g->transposed;
-        sa.inv_plane = 1.f / (float)(a.Hg * a.Wg);
-        sa.inv_wg = 1.f / (float)a.Wg;
-        CAI_CHECK_ARG((int64_t)sa.bnpix * dy_ld * 2 < (1ll << 31) && (int64_t)a.B * a.Hx * a.Wx * a.x_ld * 2 < (1ll << 31),
-                      "conv_wgrad: operand larger than 2 GiB");
-        // dW through a one-split slab and a WGRAD job (deferred: joins the backward's batched reduce launch);
-        // A/B knob CAI_SMALL_WGRAD_DIRECT=1: straight into the torch layout (scattered stores)
-        static const bool direct_out = [] {
-            const char* e = getenv("CAI_SMALL_WGRAD_DIRECT");
-            return e && *e == '1';
-        }();
-        sa.slab = direct_out ? nullptr : slab;
-        const dim3 grid(sa.ncb + ((db && g->transposed) ? 1 : 0), (W.Ng + 63) / 64);
-        const bool lng = W.M > SW_NW * SW_STEPS * 32;
-        if (sa.in_abs && lng)
-            hipLaunchKernelGGL((wgrad_small_kernel<1, true>), grid, dim3(512), 0, st, sa);
-        else if (sa.in_abs)
-            hipLaunchKernelGGL((wgrad_small_kernel<1, false>), grid, dim3(512), 0, st, sa);
-        else if (sa.in_sq && lng)
-            hipLaunchKernelGGL((wgrad_small_kernel<2, true>), grid, dim3(512), 0, st, sa);
-        else if (sa.in_sq)
-            hipLaunchKernelGGL((wgrad_small_kernel<2, false>), grid, dim3(512), 0, st, sa);
-        else if (lng)
-            hipLaunchKernelGGL((wgrad_small_kernel<0, true>), grid, dim3(512), 0, st, sa);
-        else
-            hipLaunchKernelGGL((wgrad_small_kernel<0, false>), grid, dim3(512), 0, st, sa);
+        SwArgs sa;
+        dim3 grid;
+        cai_reduce_job J;
+        rc = small_wgrad_setup(g, W, a, dy, dy_ld, dw, db, accumulate, slab, sa, grid, J);
+        if (rc) return rc;
+        launch_wgrad_small(sa, grid, W.M > SW_NW * SW_STEPS * 32, st);
         CAI_LAUNCH_CHECK("conv_wgrad");
-        if (direct_out) return CAI_OK;
-        cai_reduce_job J{};
-        J.kind = CAI_JOB_WGRAD;
-        J.nblocks = wgrad_job_blocks(W.Ng, W.Cq_pad, g->kernel, 0);
-        J.p[0] = slab; J.p[1] = dw;
-        J.i[0] = 1; J.i[1] = W.Ng; J.i[2] = W.ncols; J.i[3] = W.Cq; J.i[4] = W.Cq_pad; J.i[5] = g->kernel;
-        J.i[6] = accumulate;
+        if (J.kind == CAI_JOB_NONE) return CAI_OK;
         if (job) {
             *job = J;
             return CAI_OK;
@@ -4567,6 +4637,53 @@ int cai_conv_wgrad_deferred(const cai_conv_geom* g, int dtype, const void* x, in
     CAI_CHECK_ARG(job, "conv_wgrad_deferred: null job");
     return run_conv_wgrad(g, dtype, x, x_ld, in_abs, in_sq, dy, dy_ld, dw, db, accumulate, workspace, ws_bytes, stream,
                           job);
+}
+
+int cai_conv_wgrad_batch(const cai_wgrad_call* calls, int32_t n, void* stream, cai_reduce_job* jobs) {
+    CAI_CHECK_ARG(n >= 0 && (n == 0 || (calls && jobs)), "conv_wgrad_batch: bad arguments");
+    hipStream_t st = as_stream(stream);
+    // the latent-size calls, grouped by kernel variant (input transform, long form): one launch per group of up to
+    // SW_BATCH_MAX calls; a call whose bias gradient (written in place) another call of the open group also
+    // writes starts a new group, so no launch holds two writers of one bias
+    SwBatch b[6];
+    for (int c = 0; c < 6; ++c) b[c].n = 0, b[c].start[0] = 0;
+    for (int i = 0; i < n; ++i) {
+        const cai_wgrad_call& c = calls[i];
+        jobs[i] = cai_reduce_job{};
+        if (!small_wgrad_ok(&c.geom, c.dtype)) {
+            int rc = run_conv_wgrad(&c.geom, c.dtype, c.x, c.x_ld, c.in_abs, c.in_sq, c.dy, c.dy_ld, c.dw, c.db,
+                                    c.accumulate, c.workspace, c.ws_bytes, stream, &jobs[i]);
+            if (rc) return rc;
+            continue;
+        }
+        WgradPlan W;
+        WgradArgs a;
+        int rc = wgrad_prepare(&c.geom, c.dtype, c.x, c.x_ld, c.in_abs, c.in_sq, c.dy, c.dy_ld, c.dw, c.db,
+                               c.workspace, c.ws_bytes, W, a);
+        if (rc) return rc;
+        SwArgs sa;
+        dim3 grid;
+        rc = small_wgrad_setup(&c.geom, W, a, c.dy, c.dy_ld, c.dw, c.db, c.accumulate, a.ws, sa, grid, jobs[i]);
+        if (rc) return rc;
+        const bool lng = W.M > SW_NW * SW_STEPS * 32;
+        const int cls = (sa.in_abs ? 1 : (sa.in_sq ? 2 : 0)) + (lng ? 3 : 0);
+        SwBatch& B = b[cls];
+        bool clash = false;
+        for (int j = 0; j < B.n; ++j) clash |= sa.db && B.job[j].db == sa.db;
+        if (clash || B.n == SW_BATCH_MAX) {
+            launch_wgrad_small_batch(B, cls, st);
+            B.n = 0;
+        }
+        B.job[B.n] = sa;
+        B.gx[B.n] = (int)grid.x;
+        B.gy[B.n] = (int)grid.y;
+        B.start[B.n + 1] = B.start[B.n] + (int)(grid.x * grid.y);
+        ++B.n;
+    }
+    for (int c = 0; c < 6; ++c)
+        if (b[c].n) launch_wgrad_small_batch(b[c], c, st);
+    CAI_LAUNCH_CHECK("conv_wgrad_batch");
+    return CAI_OK;
 }
 
 }  // extern "C"

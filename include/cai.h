@@ -255,6 +255,26 @@ int cai_conv_wgrad_deferred(const cai_conv_geom* g, int dtype,
                             float* dw, float* db, int32_t accumulate,
                             void* workspace, size_t ws_bytes, void* stream, cai_reduce_job* job);
 int cai_reduce_jobs(const cai_reduce_job* jobs, int32_t n, void* stream);
+/* n weight-gradient calls, each as cai_conv_wgrad_deferred makes it (jobs[i]: call i's reduce job), with the
+ * latent-size ones (the wgrad_small_kernel path, cai_conv_kernel_name(direction 2) == "wgrad_small_kernel")
+ * batched: one launch per input transform for up to 16 such calls (two calls that write one bias gradient
+ * go to separate launches, in call order); the others run one by one.  Replaces a backward's per-layer
+ * launches of the latent layers' weight gradients, deferred to its end (compressai/_ops.py conv_wgrad).
+ * Operands as cai_conv_wgrad_deferred; every call's buffers must stay valid until its reduce job has run. */
+typedef struct cai_wgrad_call {
+    cai_conv_geom geom;
+    int32_t dtype;
+    const void* x;
+    int32_t x_ld, in_abs, in_sq;
+    const void* dy;
+    int32_t dy_ld;
+    float* dw;
+    float* db;
+    int32_t accumulate;
+    void* workspace;
+    size_t ws_bytes;
+} cai_wgrad_call;
+int cai_conv_wgrad_batch(const cai_wgrad_call* calls, int32_t n, void* stream, cai_reduce_job* jobs);
 
 /* The three weight (+ bias) gradients of a ResidualUnit (layers.py:211-226) in one launch, from the
  * tensors cai_resunit's backward leaves: x (the unit input, ld x_ld), h1 / h2 (the hidden activations,

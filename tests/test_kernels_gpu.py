@@ -1172,3 +1172,80 @@ def test_hyperprior_y_gradients_meet_in_dgrad(cuda, monkeypatch):
             continue
         cos = float(F.cosine_similarity(a, b, dim=0))
         assert cos > 0.9999 and relerr(a, b) < 2e-2, (n, cos, relerr(a, b))
+
+
+def test_wgrad_batch_bit_identical_to_single_calls(cuda):
+    """cai_conv_wgrad_batch (the latent layers' weight gradients of a backward in one launch per input transform,
+    deferred to its end) against one cai_conv_wgrad call per layer: bit-identical weight and bias gradients.
+    Calls: C2's h_a[2] / h_a[4] (Conv2d k5 s2 at 16x16 / 8x8, B = 16), h_s[0] / h_s[2] (ConvTranspose2d k5 s2
+    at 4x4 / 8x8: bias from trailing blocks), an |x| input (k3 s1 at 8x8), two calls accumulating into ONE bias
+    gradient (separate launches), and a 16x16 k3 layer too large for the latent kernel (run as usual)."""
+    import ctypes
+
+    from compressai import _native as native
+    from compressai._ops import _p, _stream
+
+    raw = native.lib.load()
+    G = native.ConvGeom
+    torch.manual_seed(21)
+    specs = [  # geom, in_abs
+        (G(16, 128, 16, 16, 128, 8, 8, 5, 2, 2, 0, 0), 0),
+        (G(16, 128, 8, 8, 128, 4, 4, 5, 2, 2, 0, 0), 0),
+        (G(16, 128, 4, 4, 128, 8, 8, 5, 2, 2, 1, 1), 0),
+        (G(16, 128, 8, 8, 128, 16, 16, 5, 2, 2, 1, 1), 0),
+        (G(16, 192, 8, 8, 128, 8, 8, 3, 1, 1, 0, 0), 1),
+        (G(16, 128, 8, 8, 128, 4, 4, 5, 2, 2, 0, 0), 0),             # shares call 1's bias gradient
+        (G(16, 192, 16, 16, 128, 16, 16, 3, 1, 1, 0, 0), 0),          # 4096 pixels: wgrad_glds + slab reduce
+    ]
+    names = [raw.cai_conv_kernel_name(ctypes.byref(g), native.BF16, 2, a).decode() for g, a in specs]
+    assert names[:6] == ["wgrad_small_kernel"] * 6 and names[6] != "wgrad_small_kernel", names
+    calls = []
+    for i, (g, in_abs) in enumerate(specs):
+        x = torch.randn(g.batch, g.in_h, g.in_w, g.in_c, device=cuda).bfloat16()
+        dy = torch.randn(g.batch, g.out_h, g.out_w, g.out_c, device=cuda).bfloat16()
+        wshape = (g.in_c, g.out_c, 5, 5) if g.transposed else (g.out_c, g.in_c, g.kernel, g.kernel)
+        nws = native.lib.cai_conv_wgrad_workspace_bytes(ctypes.byref(g), native.BF16)
+        calls.append(dict(g=g, in_abs=in_abs, x=x, dy=dy, dw0=torch.randn(wshape, device=cuda),
+                          db0=torch.randn(g.out_c, device=cuda), nws=nws))
+    calls[5]["shared"] = 1
+
+    def single():
+        dws, dbs = [], []
+        for i, c in enumerate(calls):
+            dw = c["dw0"].clone()
+            db = dbs[c["shared"]] if "shared" in c else c["db0"].clone()
+            ws = torch.empty(c["nws"], dtype=torch.uint8, device=cuda)
+            native.lib.cai_conv_wgrad(ctypes.byref(c["g"]), native.BF16, _p(c["x"]), c["g"].in_c, c["in_abs"], 0,
+                                      _p(c["dy"]), c["g"].out_c, _p(dw), _p(db), 1, _p(ws), c["nws"], _stream())
+            torch.cuda.synchronize()
+            dws.append(dw)
+            dbs.append(db)
+        return dws, dbs
+
+    def batched():
+        dws, dbs, wss = [], [], []
+        arr = (native.WgradCall * len(calls))()
+        for i, c in enumerate(calls):
+            dw = c["dw0"].clone()
+            db = dbs[c["shared"]] if "shared" in c else c["db0"].clone()
+            ws = torch.empty(c["nws"], dtype=torch.uint8, device=cuda)
+            arr[i] = native.WgradCall(c["g"], native.BF16, _p(c["x"]), c["g"].in_c, c["in_abs"], 0, _p(c["dy"]),
+                                      c["g"].out_c, _p(dw), _p(db), 1, _p(ws), c["nws"])
+            dws.append(dw)
+            dbs.append(db)
+            wss.append(ws)
+        jobs = (native.ReduceJob * len(calls))()
+        native.lib.cai_conv_wgrad_batch(arr, len(calls), _stream(), jobs)
+        live = [j for j in jobs if j.kind != native.JOB_NONE]
+        assert len(live) == len(calls)
+        for j in live:          # one launch each, in call order (as the single calls ran them)
+            native.lib.cai_reduce_jobs((native.ReduceJob * 1)(j), 1, _stream())
+        torch.cuda.synchronize()
+        return dws, dbs
+
+    sw, sb = single()
+    bw, bb = batched()
+    for i in range(len(calls)):
+        assert torch.isfinite(bw[i]).all(), i
+        assert torch.equal(sw[i], bw[i]), (i, names[i], (sw[i] - bw[i]).abs().max().item())
+        assert torch.equal(sb[i], bb[i]), (i, names[i], (sb[i] - bb[i]).abs().max().item())
