@@ -130,6 +130,8 @@ SIGNATURES = {
                                      POINTER(ReduceJob)]),
     "cai_reduce_jobs": (_I, [POINTER(ReduceJob), c_int32, _P]),
     "cai_conv_wgrad_batch": (_I, [POINTER(WgradCall), c_int32, _P, POINTER(ReduceJob)]),
+    "cai_resunit_wgrad_batch": (_I, [POINTER(ResunitWgradArgs), POINTER(c_void_p), POINTER(c_size_t), c_int32, _P,
+                                    POINTER(ReduceJob)]),
     "cai_deconv_small_workspace_bytes": (_S, [_G, _I]),
     "cai_deconv_small_fwd": (_I, [_G, _I, _P, c_int32, _P, _P, _P, _P, _S, _P]),
     "cai_deconv_small_bwd": (_I, [_G, _I, _P, c_int32, _P, _P, _P, c_int32, _P, _P, c_int32, _P, _S, _P]),

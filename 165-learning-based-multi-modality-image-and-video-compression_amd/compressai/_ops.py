@@ -163,10 +163,11 @@ class _SideDeferred:
 # gradient runs on the side stream.  CAI_DEFER_REDUCE=0 turns it off (A/B).
 _DEFER_REDUCE = os.environ.get("CAI_DEFER_REDUCE", "1") == "1"
 _REDUCE_SPLIT = os.environ.get("CAI_REDUCE_SPLIT", "0") == "1"   # diagnostics: one launch per deferred job
-_JOBS = {}          # (device index, graph task id) -> [jobs, their streams, keep-alive tensors, wgrad calls]
+_JOBS = {}          # (device, graph task id) -> [jobs, streams, keep-alive tensors, wgrad calls, device, unit calls]
 # The latent layers' weight gradients (wgrad_small_kernel: <= 1024 G pixels) are deferred the same way, as whole
 # calls: the flush runs them in one launch (cai_conv_wgrad_batch) ahead of the reduce launch, instead of one
-# launch per layer in the backward's chain.  CAI_WGRAD_BATCH=0 launches them in place (A/B).
+# launch per layer in the backward's chain; so are the ResidualUnits' weight gradients (cai_resunit_wgrad_batch: one
+# launch for a backward's units).  CAI_WGRAD_BATCH=0 launches both in place (A/B).
 _WGRAD_BATCH = os.environ.get("CAI_WGRAD_BATCH", "1") == "1"
 
 
@@ -175,7 +176,7 @@ def _flush_jobs(key):
     DDP's finalize uses it), after it has waited for every other stream a job's partial kernel ran on (the
     hyper branch's side stream: inside a captured graph this is the join edge)."""
     pend = _JOBS.pop(key, None)
-    if not pend or not (pend[0] or pend[3]):
+    if not pend or not (pend[0] or pend[3] or pend[5]):
         return
     dev = key[0]
     jobs, streams, keep, calls = pend[:4]
@@ -187,6 +188,14 @@ def _flush_jobs(key):
         arr = (WgradCall * len(calls))(*calls)
         out = (ReduceJob * len(calls))()
         lib.cai_conv_wgrad_batch(arr, len(calls), _VP(cur.cuda_stream), out)
+        jobs = jobs + [j for j in out if j.kind != JOB_NONE]
+    units = pend[5]
+    if units:
+        args = (ResunitWgradArgs * len(units))(*[u[0] for u in units])
+        wss = (ctypes.c_void_p * len(units))(*[u[1] for u in units])
+        nbs = (ctypes.c_size_t * len(units))(*[u[2] for u in units])
+        out = (ReduceJob * (3 * len(units)))()
+        lib.cai_resunit_wgrad_batch(args, wss, nbs, len(units), _VP(cur.cuda_stream), out)
         jobs = jobs + [j for j in out if j.kind != JOB_NONE]
     if not jobs:
         for t in keep:
@@ -230,7 +239,7 @@ def _pending(device: torch.device):
     key = (dev, torch._C._current_graph_task_id())
     pend = _JOBS.get(key)
     if pend is None:
-        pend = _JOBS[key] = [[], [], [], [], dev]
+        pend = _JOBS[key] = [[], [], [], [], dev, []]
         torch.autograd.Variable._execution_engine.queue_callback(lambda: _flush_jobs(key))
     return pend
 
@@ -1103,7 +1112,13 @@ def _resunit_wgrad(u: "_FusedUnit", xpm, h1, h2, g_a, g_b, gcc, gcld):
                          dwc=dw4.data_ptr(), dbc=db4.data_ptr(), accumulate=int(direct))
     nbytes = lib.cai_resunit_wgrad_workspace_bytes(ctypes.byref(A))
     st = _stream()
-    if defer_reduce_ok(direct):
+    if defer_reduce_ok(direct) and _WGRAD_BATCH and not _WGRAD_SIDE_PX:
+        wws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        pend = _pending(dev)
+        pend[5].append((A, wws.data_ptr(), nbytes))
+        pend[1].append(torch.cuda.current_stream(pend[4]))
+        pend[2].extend((xpm, h1, h2, g_a, g_b, gcc, wws))
+    elif defer_reduce_ok(direct):
         with _SideDeferred(dev, B * H * W, xpm, h1, h2, g_a, g_b, gcc):
             wws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
             jobs = (ReduceJob * 3)()

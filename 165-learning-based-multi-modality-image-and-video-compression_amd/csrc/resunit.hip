@@ -426,15 +426,15 @@ __device__ __forceinline__ int rw_xcd_remap(int wgid, int nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
+// block wgid of a 13 x S grid of nwg blocks (wgid's XCD: wgid & 7, as the hardware dispatches a grid)
 template <int NH>
-__global__ __launch_bounds__(256, 2) void resunit_wgrad_kernel(const RwArgs a) {
+__device__ __forceinline__ void resunit_wgrad_block(const RwArgs& a, int wgid, int nwg, char* smem) {
     using R = RwCfg<NH>;
     constexpr int NC = 2 * NH, SLOTS = R::SLOTS, LPT = R::LPT, TM = R::TM, TN = R::TN, EP = R::EP;
     constexpr unsigned OOB = 0x80000000u;
-    __shared__ __attribute__((aligned(16))) char smem[R::BYTES];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int L = rw_xcd_remap((int)blockIdx.x, (int)gridDim.x);
+    const int L = rw_xcd_remap(wgid, nwg);
     const int s = L / 13, t = L - (L / 13) * 13;
 
     // this block's GEMM: G (output rows) and X (columns) operands, tap shift, slab placement, bias role
@@ -585,6 +585,33 @@ __global__ __launch_bounds__(256, 2) void resunit_wgrad_kernel(const RwArgs a) {
     }
 }
 
+template <int NH>
+__global__ __launch_bounds__(256, 2) void resunit_wgrad_kernel(const RwArgs a) {
+    __shared__ __attribute__((aligned(16))) char smem[RwCfg<NH>::BYTES];
+    resunit_wgrad_block<NH>(a, (int)blockIdx.x, (int)gridDim.x, smem);
+}
+
+// Several units' weight gradients in one launch (cai_resunit_wgrad_batch): job j owns blocks [start[j], start[j + 1])
+// of a 1-D grid, its 13 * S blocks first (starts are multiples of 8, so a block's XCD is its local id's, as in a
+// launch of its own), then padding blocks that exit.  Each job writes only its own slabs.
+constexpr int RW_BATCH_MAX = 24;
+struct RwBatch {
+    RwArgs job[RW_BATCH_MAX];
+    int start[RW_BATCH_MAX + 1];
+    int n;
+};
+
+template <int NH>
+__global__ __launch_bounds__(256, 2) void resunit_wgrad_batch_kernel(const RwBatch b) {
+    __shared__ __attribute__((aligned(16))) char smem[RwCfg<NH>::BYTES];
+    const int L = (int)blockIdx.x;
+    int j = 0;
+    while (j + 1 < b.n && L >= b.start[j + 1]) ++j;
+    const int l = L - b.start[j], nwg = 13 * b.job[j].S;
+    if (l >= nwg) return;
+    resunit_wgrad_block<NH>(b.job[j], l, nwg, smem);
+}
+
 }  // namespace
 }  // namespace cai
 
@@ -689,8 +716,9 @@ extern "C" size_t cai_resunit_wgrad_workspace_bytes(const cai_resunit_wgrad_args
     return rw_ws(p, w) ? w.total : 0;
 }
 
-extern "C" int cai_resunit_wgrad(const cai_resunit_wgrad_args* p, void* workspace, size_t ws_bytes, void* stream,
-                                 cai_reduce_job* jobs) {
+// the checks, kernel arguments and the three WGRAD reduce jobs of one call
+static int rw_prepare(const cai_resunit_wgrad_args* p, void* workspace, size_t ws_bytes, RwArgs& a,
+                      cai_reduce_job (&J)[3]) {
     RwWs w;
     CAI_CHECK_ARG(rw_ws(p, w), "resunit_wgrad: N = %d (128 or 192) and positive sizes", p ? p->n : -1);
     const int n = p->n, nh = n / 2;
@@ -704,7 +732,7 @@ extern "C" int cai_resunit_wgrad(const cai_resunit_wgrad_args* p, void* workspac
     const int64_t P = (int64_t)p->batch * p->h * p->w;
     CAI_CHECK_ARG(P * std::max(p->x_ld, p->gc_ld) * 2 < (1ll << 31) && P < (1 << 23), "resunit_wgrad: tensor too large");
     char* ws = static_cast<char*>(workspace);
-    RwArgs a{};
+    a = RwArgs{};
     a.x = static_cast<const bf16*>(p->x);
     a.h1 = static_cast<const bf16*>(p->h1);
     a.h2 = static_cast<const bf16*>(p->h2);
@@ -722,15 +750,8 @@ extern "C" int cai_resunit_wgrad(const cai_resunit_wgrad_args* p, void* workspac
     a.bias_a = reinterpret_cast<float*>(ws + w.off_ba);
     a.bias_b = reinterpret_cast<float*>(ws + w.off_bb);
     a.bias_c = reinterpret_cast<float*>(ws + w.off_bc);
-    hipStream_t st = as_stream(stream);
-    const dim3 grid((unsigned)(13 * w.S));
-    if (n == 192)
-        hipLaunchKernelGGL(resunit_wgrad_kernel<96>, grid, dim3(256), 0, st, a);
-    else
-        hipLaunchKernelGGL(resunit_wgrad_kernel<64>, grid, dim3(256), 0, st, a);
-    CAI_LAUNCH_CHECK("resunit_wgrad");
-    // the final sums: three WGRAD reduce jobs over the slabs (reduce_jobs.hip), returned or run now
-    cai_reduce_job J[3]{};
+    // the final sums: three WGRAD reduce jobs over the slabs (reduce_jobs.hip)
+    for (auto& j : J) j = cai_reduce_job{};
     auto fill = [&](cai_reduce_job& j, float* slab, float* dw, float* bws, float* db, int ng, int cq, int k) {
         j.kind = CAI_JOB_WGRAD;
         j.nblocks = wgrad_job_blocks(ng, cq, k, (ng + 255) / 256);
@@ -741,9 +762,60 @@ extern "C" int cai_resunit_wgrad(const cai_resunit_wgrad_args* p, void* workspac
     fill(J[0], a.slab_a, p->dwa, a.bias_a, p->dba, nh, n, 1);
     fill(J[1], a.slab_b, p->dwb, a.bias_b, p->dbb, nh, nh, 3);
     fill(J[2], a.slab_c, p->dwc, a.bias_c, p->dbc, n, nh, 1);
+    return CAI_OK;
+}
+
+extern "C" int cai_resunit_wgrad(const cai_resunit_wgrad_args* p, void* workspace, size_t ws_bytes, void* stream,
+                                 cai_reduce_job* jobs) {
+    RwArgs a;
+    cai_reduce_job J[3];
+    const int rc = rw_prepare(p, workspace, ws_bytes, a, J);
+    if (rc) return rc;
+    hipStream_t st = as_stream(stream);
+    const dim3 grid((unsigned)(13 * a.S));
+    if (p->n == 192)
+        hipLaunchKernelGGL(resunit_wgrad_kernel<96>, grid, dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL(resunit_wgrad_kernel<64>, grid, dim3(256), 0, st, a);
+    CAI_LAUNCH_CHECK("resunit_wgrad");
     if (jobs) {
         for (int i = 0; i < 3; ++i) jobs[i] = J[i];
         return CAI_OK;
     }
     return launch_reduce_jobs(J, 3, st);
+}
+
+extern "C" int cai_resunit_wgrad_batch(const cai_resunit_wgrad_args* args, void* const* workspaces,
+                                       const size_t* ws_bytes, int32_t n, void* stream, cai_reduce_job* jobs) {
+    CAI_CHECK_ARG(n >= 0 && (n == 0 || (args && workspaces && ws_bytes && jobs)), "resunit_wgrad_batch: bad arguments");
+    hipStream_t st = as_stream(stream);
+    RwBatch b[2];     // N = 192 (NH 96), N = 128 (NH 64)
+    b[0].n = b[1].n = 0;
+    b[0].start[0] = b[1].start[0] = 0;
+    auto flush = [&](int c) {
+        if (!b[c].n) return;
+        const dim3 grid((unsigned)b[c].start[b[c].n]);
+        if (c == 0)
+            hipLaunchKernelGGL(resunit_wgrad_batch_kernel<96>, grid, dim3(256), 0, st, b[c]);
+        else
+            hipLaunchKernelGGL(resunit_wgrad_batch_kernel<64>, grid, dim3(256), 0, st, b[c]);
+        b[c].n = 0;
+    };
+    for (int i = 0; i < n; ++i) {
+        RwArgs a;
+        cai_reduce_job J[3];
+        const int rc = rw_prepare(&args[i], workspaces[i], ws_bytes[i], a, J);
+        if (rc) return rc;
+        for (int k = 0; k < 3; ++k) jobs[3 * i + k] = J[k];
+        const int c = args[i].n == 192 ? 0 : 1;
+        if (b[c].n == RW_BATCH_MAX) flush(c);
+        RwBatch& B = b[c];
+        B.job[B.n] = a;
+        B.start[B.n + 1] = B.start[B.n] + (13 * a.S + 7) / 8 * 8;
+        ++B.n;
+    }
+    flush(0);
+    flush(1);
+    CAI_LAUNCH_CHECK("resunit_wgrad_batch");
+    return CAI_OK;
 }

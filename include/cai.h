@@ -301,6 +301,12 @@ typedef struct cai_resunit_wgrad_args {
     int32_t accumulate;
 } cai_resunit_wgrad_args;
 size_t cai_resunit_wgrad_workspace_bytes(const cai_resunit_wgrad_args* args);
+/* n cai_resunit_wgrad calls (each with its own workspace, kept valid until its jobs have run) in one launch per
+ * width; jobs: 3 per call, in call order.  The backward's ResidualUnit weight gradients, deferred to its end
+ * (compressai/_ops.py _resunit_wgrad): one launch instead of one per unit, the small units' grids filling the
+ * chip together. */
+int cai_resunit_wgrad_batch(const cai_resunit_wgrad_args* args, void* const* workspaces, const size_t* ws_bytes,
+                            int32_t n, void* stream, cai_reduce_job* jobs);
 int cai_resunit_wgrad(const cai_resunit_wgrad_args* args, void* workspace, size_t ws_bytes, void* stream,
                       cai_reduce_job* jobs);
 

@@ -402,3 +402,62 @@ def test_resunit_ledger_replay_owns_buffers(cuda):
             e.replay()
     torch.cuda.synchronize()
     assert all(bool((j == 7.0).all()) for j in junk)
+
+
+def test_resunit_wgrad_batch_bit_identical(cuda):
+    """cai_resunit_wgrad_batch against one cai_resunit_wgrad per unit: 27 units of both widths (N = 192 / 128) and
+    several sizes (1 to 32 pixel splits: 16x16 / 8x8 at B = 1..4, one 64x64) -- more than one launch's 24 jobs
+    per width -- with accumulate on: bit-identical parameter gradients after the same reduce jobs."""
+    import ctypes
+
+    from compressai import _ops
+    from compressai._native import ReduceJob, ResunitWgradArgs
+
+    torch.manual_seed(5)
+    specs = [(192 if i % 3 else 128, (16, 8)[i % 2], 1 + i % 4) for i in range(26)] + [(192, 64, 2)]
+    units = []
+    for n, H, B in specs:
+        nh = n // 2
+        t = lambda c: _pm(torch.randn(B, c, H, H, device=cuda)).to(torch.bfloat16)   # noqa: E731,B023
+        ops = [t(n), t(nh), t(nh), t(nh), t(nh), t(n)]
+        init = [torch.randn(sh, device=cuda) for sh in
+                ((nh, n, 1, 1), (nh,), (nh, nh, 3, 3), (nh,), (n, nh, 1, 1), (n,))]
+        units.append((n, H, B, ops, init))
+
+    def args(u, outs):
+        n, H, B, (x, h1, h2, ga, gb, gc), _ = u
+        return ResunitWgradArgs(batch=B, h=H, w=H, n=n, x=x.data_ptr(), h1=h1.data_ptr(), h2=h2.data_ptr(),
+                                ga=ga.data_ptr(), gb=gb.data_ptr(), gc=gc.data_ptr(), x_ld=n, gc_ld=n,
+                                dwa=outs[0].data_ptr(), dba=outs[1].data_ptr(), dwb=outs[2].data_ptr(),
+                                dbb=outs[3].data_ptr(), dwc=outs[4].data_ptr(), dbc=outs[5].data_ptr(), accumulate=1)
+
+    st = torch.cuda.current_stream().cuda_stream
+    single = []
+    for u in units:
+        outs = [v.clone() for v in u[4]]
+        A = args(u, outs)
+        nb = _ops.lib.cai_resunit_wgrad_workspace_bytes(ctypes.byref(A))
+        ws = torch.empty(nb, dtype=torch.uint8, device=cuda)
+        _ops.lib.cai_resunit_wgrad(ctypes.byref(A), ws.data_ptr(), nb, st, None)
+        torch.cuda.synchronize()
+        single.append(outs)
+    batched, keep = [], []
+    arr = (ResunitWgradArgs * len(units))()
+    wss = (ctypes.c_void_p * len(units))()
+    nbs = (ctypes.c_size_t * len(units))()
+    for i, u in enumerate(units):
+        outs = [v.clone() for v in u[4]]
+        arr[i] = args(u, outs)
+        nbs[i] = _ops.lib.cai_resunit_wgrad_workspace_bytes(ctypes.byref(arr[i]))
+        ws = torch.empty(nbs[i], dtype=torch.uint8, device=cuda)
+        wss[i] = ws.data_ptr()
+        keep.append(ws)
+        batched.append(outs)
+    jobs = (ReduceJob * (3 * len(units)))()
+    _ops.lib.cai_resunit_wgrad_batch(arr, wss, nbs, len(units), st, jobs)
+    _ops.lib.cai_reduce_jobs(jobs, len(jobs), st)
+    torch.cuda.synchronize()
+    for i, (a, b) in enumerate(zip(single, batched)):
+        for k in range(6):
+            assert torch.isfinite(b[k]).all(), (i, k)
+            assert torch.equal(a[k], b[k]), (i, specs[i], k, (a[k] - b[k]).abs().max().item())
