@@ -764,15 +764,22 @@ class ConvFn(torch.autograd.Function):
         return dx, dw, db, None, dres
 
 
-_SMALL_WGRAD = {}
+_BATCHED_WGRAD = {}
+# the weight-gradient kernels whose calls are deferred to the backward's flush and batched there (one launch per
+# kernel variant, cai_conv_wgrad_batch): the latent-size kernel and the pixel-split kernels of the mid-size and
+# stride-1 3x3 layers (cheng2020: 12 + 15 launches per step).  The stride-2 halo weight gradients of the big maps
+# stay in place: each already fills the chip, and right after its input gradient its operands are cache-warm.
+_BATCHED_WGRAD_KERNELS = (b"wgrad_small_kernel", b"wgrad_glds_kernel<256>", b"wgrad_glds_kernel<128>",
+                          b"wgrad_halo_kernel<3,s1>")
 
 
 def _small_wgrad(g, code, in_abs) -> bool:
-    """Whether this weight gradient takes the latent-size kernel (batched when deferred)."""
+    """Whether this weight gradient's call is deferred and batched (_BATCHED_WGRAD_KERNELS)."""
     key = (tuple(getattr(g, f) for f, _ in ConvGeom._fields_), code, int(in_abs))
-    v = _SMALL_WGRAD.get(key)
+    v = _BATCHED_WGRAD.get(key)
     if v is None:
-        v = _SMALL_WGRAD[key] = lib.cai_conv_kernel_name(ctypes.byref(g), code, 2, int(in_abs)) == b"wgrad_small_kernel"
+        name = lib.cai_conv_kernel_name(ctypes.byref(g), code, 2, int(in_abs))
+        v = _BATCHED_WGRAD[key] = name in _BATCHED_WGRAD_KERNELS
     return v
 
 

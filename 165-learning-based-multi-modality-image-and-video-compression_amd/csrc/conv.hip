@@ -2690,19 +2690,22 @@ __device__ __forceinline__ int tbias_sel(const WgradArgs& a, int kh, int kw) {
     return ((unsigned)dh < (unsigned)a.tb_s && (unsigned)dw < (unsigned)a.tb_s) ? dh * a.tb_s + dw : -1;
 }
 
+template <int CT>
+constexpr int wgrad_glds_smem() { return 3 * (1 + CT / 128) * 64 * 256; }
+
+// block wgid of an nwg-block grid (its XCD: wgid & 7, as the hardware dispatches a grid of its own)
 template <int CT, int FLAGS>
-__global__ __launch_bounds__(512, 1) void wgrad_glds_kernel(const WgradArgs a) {
+__device__ __forceinline__ void wgrad_glds_block(const WgradArgs& a, int wgid, int nwg, char* smem) {
     constexpr int OPB = 64 * 256;                 // one [64][256 B] image
     constexpr int NX = CT / 128;                  // X images (128 columns each)
     constexpr int STAGE = (1 + NX) * OPB;         // G, X_0 [, X_1]
     constexpr int WCOL = CT / 4;                  // columns per wave
     constexpr int TN = WCOL / 16;
     constexpr int G = 2 * (1 + NX);               // DMA instructions per thread per step
-    __shared__ __attribute__((aligned(16))) char smem[3 * STAGE];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wr = wid >> 2, wc = wid & 3;        // 2 (rows) x 4 (cols) waves
     const int ntile = a.ctiles * a.rtiles;
-    const int L = xcd_remap((int)blockIdx.x, (int)gridDim.x);
+    const int L = xcd_remap(wgid, nwg);
     const int split = L / ntile;
     const int tl = L - split * ntile;
     const int ctile = tl % a.ctiles, rtile = tl / a.ctiles;
@@ -2898,6 +2901,37 @@ __global__ __launch_bounds__(512, 1) void wgrad_glds_kernel(const WgradArgs a) {
         }
 }
 
+template <int CT, int FLAGS>
+__global__ __launch_bounds__(512, 1) void wgrad_glds_kernel(const WgradArgs a) {
+    __shared__ __attribute__((aligned(16))) char smem[wgrad_glds_smem<CT>()];
+    wgrad_glds_block<CT, FLAGS>(a, (int)blockIdx.x, (int)gridDim.x, smem);
+}
+
+// Several pixel-split weight gradients of one kernel variant in one launch (cai_conv_wgrad_batch): job j owns
+// blocks [start[j], start[j + 1]) of a 1-D grid -- its nwg[j] blocks, then padding blocks that exit; starts are
+// multiples of 8, so every block keeps the XCD of its launch-of-its-own index.  Each job writes only its slabs.
+constexpr int WG_BATCH_MAX = 16;
+struct WgBatch {
+    WgradArgs job[WG_BATCH_MAX];
+    int start[WG_BATCH_MAX + 1];
+    int nwg[WG_BATCH_MAX];
+    int n;
+};
+static_assert(sizeof(WgBatch) <= 4096, "kernel argument block");
+
+__device__ __forceinline__ int wg_batch_job(const WgBatch& b, int L) {
+    int j = 0;
+    while (j + 1 < b.n && L >= b.start[j + 1]) ++j;
+    return j;
+}
+
+template <int CT, int FLAGS>
+__global__ __launch_bounds__(512, 1) void wgrad_glds_batch_kernel(const WgBatch b) {
+    __shared__ __attribute__((aligned(16))) char smem[wgrad_glds_smem<CT>()];
+    const int L = (int)blockIdx.x, j = wg_batch_job(b, L), l = L - b.start[j];
+    if (l < b.nwg[j]) wgrad_glds_block<CT, FLAGS>(b.job[j], l, b.nwg[j], smem);
+}
+
 // ---------------------------------------------------------------------------
 // Halo-staged weight gradient of the stride-2 gather convolutions (Conv2d k3/k5 s2 p=k/2, and the
 // ConvTranspose2d of that geometry, whose wgrad gathers its output gradient the same way), bf16, for
@@ -2954,15 +2988,14 @@ __device__ __forceinline__ int opaque(int v) {
 }
 
 // S = 1: the stride-1 k3 p1 Conv2d (cheng2020's 3x3 convs): one footprint plane, tap kw at cell p + kw.
-template <int KS, int S, int FLAGS, int R = 1>
-__global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
+template <int KS, int S, int FLAGS, int R>
+__device__ __forceinline__ void wgrad_halo_block(const WgradArgs& a, int wgid, int nwg, char* smem) {
     using W = WhCfg<KS, S, R>;
-    __shared__ __attribute__((aligned(16))) char smem[W::BYTES];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wr = wid >> 2, wc = wid & 3;            // 2 (rows) x 4 (cols) waves
     const int nqc = a.Cq_pad / 64;
     const int ntile = KS * nqc * a.rtiles;
-    const int L = xcd_remap((int)blockIdx.x, (int)gridDim.x);
+    const int L = xcd_remap(wgid, nwg);
     const int split = L / ntile;
     const int tl = L - split * ntile;
     const int ctile = tl % (KS * nqc), rtile = tl / (KS * nqc);
@@ -3257,6 +3290,19 @@ __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
     }
 }
 
+template <int KS, int S, int FLAGS, int R = 1>
+__global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
+    __shared__ __attribute__((aligned(16))) char smem[WhCfg<KS, S, R>::BYTES];
+    wgrad_halo_block<KS, S, FLAGS, R>(a, (int)blockIdx.x, (int)gridDim.x, smem);
+}
+
+template <int KS, int S, int FLAGS, int R = 1>
+__global__ __launch_bounds__(512, 1) void wgrad_halo_batch_kernel(const WgBatch b) {
+    __shared__ __attribute__((aligned(16))) char smem[WhCfg<KS, S, R>::BYTES];
+    const int L = (int)blockIdx.x, j = wg_batch_job(b, L), l = L - b.start[j];
+    if (l < b.nwg[j]) wgrad_halo_block<KS, S, FLAGS, R>(b.job[j], l, b.nwg[j], smem);
+}
+
 template <int KS, int S, int R = 1>
 static void launch_wgrad_halo(const WgradArgs& a, int nblocks, int bias, hipStream_t st) {
     if (bias == WG_BIAS)
@@ -3265,6 +3311,35 @@ static void launch_wgrad_halo(const WgradArgs& a, int nblocks, int bias, hipStre
         hipLaunchKernelGGL((wgrad_halo_kernel<KS, S, WG_TBIAS, R>), dim3(nblocks), dim3(512), 0, st, a);
     else
         hipLaunchKernelGGL((wgrad_halo_kernel<KS, S, 0, R>), dim3(nblocks), dim3(512), 0, st, a);
+}
+
+template <int KS, int S, int R = 1>
+static void launch_wgrad_halo_batch(const WgBatch& b, int bias, hipStream_t st) {
+    const dim3 grid(b.start[b.n]);
+    if (bias == WG_BIAS)
+        hipLaunchKernelGGL((wgrad_halo_batch_kernel<KS, S, WG_BIAS, R>), grid, dim3(512), 0, st, b);
+    else if (S == 2 && bias == WG_TBIAS)
+        hipLaunchKernelGGL((wgrad_halo_batch_kernel<KS, S, WG_TBIAS, R>), grid, dim3(512), 0, st, b);
+    else
+        hipLaunchKernelGGL((wgrad_halo_batch_kernel<KS, S, 0, R>), grid, dim3(512), 0, st, b);
+}
+
+template <int CT>
+static void launch_wgrad_glds_batch(const WgBatch& b, int f, hipStream_t st) {
+    const dim3 grid(b.start[b.n]);
+    switch (f) {
+        case WG_TBIAS: hipLaunchKernelGGL((wgrad_glds_batch_kernel<CT, WG_TBIAS>), grid, dim3(512), 0, st, b); break;
+        case 0: hipLaunchKernelGGL((wgrad_glds_batch_kernel<CT, 0>), grid, dim3(512), 0, st, b); break;
+        case WG_ABS: hipLaunchKernelGGL((wgrad_glds_batch_kernel<CT, WG_ABS>), grid, dim3(512), 0, st, b); break;
+        case WG_SQ: hipLaunchKernelGGL((wgrad_glds_batch_kernel<CT, WG_SQ>), grid, dim3(512), 0, st, b); break;
+        case WG_BIAS: hipLaunchKernelGGL((wgrad_glds_batch_kernel<CT, WG_BIAS>), grid, dim3(512), 0, st, b); break;
+        case WG_ABS | WG_BIAS:
+            hipLaunchKernelGGL((wgrad_glds_batch_kernel<CT, WG_ABS | WG_BIAS>), grid, dim3(512), 0, st, b);
+            break;
+        default:
+            hipLaunchKernelGGL((wgrad_glds_batch_kernel<CT, WG_SQ | WG_BIAS>), grid, dim3(512), 0, st, b);
+            break;
+    }
 }
 
 template <int CT>
@@ -4533,6 +4608,83 @@ static int wgrad_prepare(const cai_conv_geom* g, int dtype, const void* x, int32
     return CAI_OK;
 }
 
+// The pixel-split weight gradient (LDS-DMA glds / halo kernels): the remaining kernel arguments, the kernel variant
+// (key: halo KS, S, R and bias flag, or glds CT and input / bias flags) and the block count.
+static void wgrad_split_setup(const cai_conv_geom* g, const WgradPlan& W, WgradArgs& a, void* workspace, float* db,
+                              int in_abs, int in_sq, int& key, int& nblocks) {
+    a.ctiles = (W.ncols + W.ct - 1) / W.ct;
+    a.rtiles = (W.Ng + 127) / 128;
+    a.nsub = W.nsub; a.grp_len = W.grp_len; a.chunk = W.px_chunk;
+    a.split_len = W.split_len;
+    a.nsplit = W.S;
+    float* bws = nullptr;
+    if ((W.fused_bias || W.tbias) && db) bws = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + W.ws_slab);
+    a.bws = bws;
+    a.tb_kh0 = W.tb_kh0; a.tb_kw0 = W.tb_kw0; a.tb_s = g->stride; a.nbias = W.nbias;
+    const int bflag = !bws ? 0 : (W.tbias ? WG_TBIAS : WG_BIAS);
+    nblocks = W.S * W.tiles;
+    if (W.halo) {
+        a.nsplit = W.strips_per_split;
+        a.rtiles = (W.Ng + 127) / 128;
+        key = (((W.halo * 10 + g->stride) * 10 + halo_wgrad_rows(g)) << 4) | bflag;
+    } else {
+        key = (1 << 20) | (W.ct << 4) | (in_abs ? WG_ABS : 0) | (in_sq ? WG_SQ : 0) | bflag;
+    }
+}
+
+// the fixed-order slab reduce of a pixel-split weight gradient (slab a.ws, bias partials a.bws) into torch layout
+static cai_reduce_job wgrad_split_job(const cai_conv_geom* g, const WgradPlan& W, const WgradArgs& a, float* dw,
+                                      float* db, int accumulate) {
+    cai_reduce_job J{};
+    J.kind = CAI_JOB_WGRAD;
+    J.nblocks = wgrad_job_blocks(W.Ng, W.Cq_pad, g->kernel, a.bws ? (W.nbias + 255) / 256 : 0);
+    J.p[0] = a.ws; J.p[1] = dw; J.p[2] = a.bws; J.p[3] = db;
+    J.i[0] = W.S; J.i[1] = W.Ng; J.i[2] = W.ncols; J.i[3] = W.Cq; J.i[4] = W.Cq_pad; J.i[5] = g->kernel;
+    J.i[6] = accumulate; J.i[7] = W.Sb; J.i[8] = W.nbias;
+    return J;
+}
+
+static void launch_wgrad_split(const WgradArgs& a, int key, int nblocks, hipStream_t st) {
+    const int f = key & 15;
+    if (key >> 20) {
+        const int in_abs = (f & WG_ABS) != 0, in_sq = (f & WG_SQ) != 0, bflag = f & (WG_BIAS | WG_TBIAS);
+        if (((key >> 4) & 0xffff) == 256)
+            launch_wgrad_glds<256>(a, nblocks, in_abs, in_sq, bflag, st);
+        else
+            launch_wgrad_glds<128>(a, nblocks, in_abs, in_sq, bflag, st);
+        return;
+    }
+    switch (key >> 4) {
+        case 521: launch_wgrad_halo<5, 2>(a, nblocks, f, st); break;
+        case 522: launch_wgrad_halo<5, 2, 2>(a, nblocks, f, st); break;
+        case 524: launch_wgrad_halo<5, 2, 4>(a, nblocks, f, st); break;
+        case 322: launch_wgrad_halo<3, 2, 2>(a, nblocks, f, st); break;
+        case 324: launch_wgrad_halo<3, 2, 4>(a, nblocks, f, st); break;
+        case 311: launch_wgrad_halo<3, 1>(a, nblocks, f, st); break;
+        default: launch_wgrad_halo<3, 2>(a, nblocks, f, st); break;
+    }
+}
+
+static void launch_wgrad_split_batch(const WgBatch& b, int key, hipStream_t st) {
+    const int f = key & 15;
+    if (key >> 20) {
+        if (((key >> 4) & 0xffff) == 256)
+            launch_wgrad_glds_batch<256>(b, f, st);
+        else
+            launch_wgrad_glds_batch<128>(b, f, st);
+        return;
+    }
+    switch (key >> 4) {
+        case 521: launch_wgrad_halo_batch<5, 2>(b, f, st); break;
+        case 522: launch_wgrad_halo_batch<5, 2, 2>(b, f, st); break;
+        case 524: launch_wgrad_halo_batch<5, 2, 4>(b, f, st); break;
+        case 322: launch_wgrad_halo_batch<3, 2, 2>(b, f, st); break;
+        case 324: launch_wgrad_halo_batch<3, 2, 4>(b, f, st); break;
+        case 311: launch_wgrad_halo_batch<3, 1>(b, f, st); break;
+        default: launch_wgrad_halo_batch<3, 2>(b, f, st); break;
+    }
+}
+
 static int run_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int32_t x_ld, int32_t in_abs,
                           int32_t in_sq, const void* dy, int32_t dy_ld, float* dw, float* db, int32_t accumulate,
                           void* workspace, size_t ws_bytes, void* stream, cai_reduce_job* job) {
@@ -4565,32 +4717,10 @@ static int run_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int3
     }
     float* bws = nullptr;
     if (W.glds) {
-        a.ctiles = (W.ncols + W.ct - 1) / W.ct;
-        a.split_len = W.split_len;
-        a.nsplit = W.S;
-        if ((W.fused_bias || W.tbias) && db) bws = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + W.ws_slab);
-        a.bws = bws;
-        a.tb_kh0 = W.tb_kh0; a.tb_kw0 = W.tb_kw0; a.tb_s = g->stride; a.nbias = W.nbias;
-        const int bflag = !bws ? 0 : (W.tbias ? WG_TBIAS : WG_BIAS);
-        if (W.halo) {
-            a.nsplit = W.strips_per_split;
-            a.rtiles = (W.Ng + 127) / 128;
-            const int R = halo_wgrad_rows(g);
-            if (W.halo == 5)
-                R == 1 ? launch_wgrad_halo<5, 2>(a, W.S * W.tiles, bflag, st)
-                       : (R == 2 ? launch_wgrad_halo<5, 2, 2>(a, W.S * W.tiles, bflag, st)
-                                 : launch_wgrad_halo<5, 2, 4>(a, W.S * W.tiles, bflag, st));
-            else if (g->stride == 2 && R > 1)
-                R == 2 ? launch_wgrad_halo<3, 2, 2>(a, W.S * W.tiles, bflag, st)
-                       : launch_wgrad_halo<3, 2, 4>(a, W.S * W.tiles, bflag, st);
-            else if (g->stride == 1)
-                launch_wgrad_halo<3, 1>(a, W.S * W.tiles, bflag, st);
-            else
-                launch_wgrad_halo<3, 2>(a, W.S * W.tiles, bflag, st);
-        } else if (W.ct == 256)
-            launch_wgrad_glds<256>(a, W.S * W.tiles, in_abs, in_sq, bflag, st);
-        else
-            launch_wgrad_glds<128>(a, W.S * W.tiles, in_abs, in_sq, bflag, st);
+        int key, nblocks;
+        wgrad_split_setup(g, W, a, workspace, db, in_abs, in_sq, key, nblocks);
+        bws = a.bws;
+        launch_wgrad_split(a, key, nblocks, st);
     } else {
         dim3 grid(8 * a.ctiles * a.rtiles * a.nsub);
         if (dtype == CAI_BF16)
@@ -4600,12 +4730,9 @@ static int run_conv_wgrad(const cai_conv_geom* g, int dtype, const void* x, int3
     }
     // the fixed-order slab reduce into torch layout: a job (reduce_jobs.hip), returned to a deferring caller or
     // run now
-    cai_reduce_job J{};
-    J.kind = CAI_JOB_WGRAD;
-    J.nblocks = wgrad_job_blocks(W.Ng, W.Cq_pad, g->kernel, bws ? (W.nbias + 255) / 256 : 0);
-    J.p[0] = slab; J.p[1] = dw; J.p[2] = bws; J.p[3] = db;
-    J.i[0] = W.S; J.i[1] = W.Ng; J.i[2] = W.ncols; J.i[3] = W.Cq; J.i[4] = W.Cq_pad; J.i[5] = g->kernel;
-    J.i[6] = accumulate; J.i[7] = W.Sb; J.i[8] = W.nbias;
+    a.bws = bws;
+    const cai_reduce_job J = wgrad_split_job(g, W, a, dw, db, accumulate);
+    (void)slab;
     if (job) {
         *job = J;
     } else {
@@ -4647,13 +4774,43 @@ int cai_conv_wgrad_batch(const cai_wgrad_call* calls, int32_t n, void* stream, c
     // writes starts a new group, so no launch holds two writers of one bias
     SwBatch b[6];
     for (int c = 0; c < 6; ++c) b[c].n = 0, b[c].start[0] = 0;
+    // the pixel-split calls (glds / halo kernels) grouped by kernel variant, up to WG_BATCH_MAX per launch
+    std::vector<std::pair<int, WgBatch>> groups;
     for (int i = 0; i < n; ++i) {
         const cai_wgrad_call& c = calls[i];
         jobs[i] = cai_reduce_job{};
         if (!small_wgrad_ok(&c.geom, c.dtype)) {
-            int rc = run_conv_wgrad(&c.geom, c.dtype, c.x, c.x_ld, c.in_abs, c.in_sq, c.dy, c.dy_ld, c.dw, c.db,
-                                    c.accumulate, c.workspace, c.ws_bytes, stream, &jobs[i]);
+            WgradPlan W;
+            WgradArgs a;
+            int rc = wgrad_prepare(&c.geom, c.dtype, c.x, c.x_ld, c.in_abs, c.in_sq, c.dy, c.dy_ld, c.dw, c.db,
+                                   c.workspace, c.ws_bytes, W, a);
             if (rc) return rc;
+            const bool fused_bias = !c.db || ((W.fused_bias || W.tbias));
+            if (!W.glds || !fused_bias) {   // other kernels, or a bias gradient by separate column sums: as usual
+                rc = run_conv_wgrad(&c.geom, c.dtype, c.x, c.x_ld, c.in_abs, c.in_sq, c.dy, c.dy_ld, c.dw, c.db,
+                                    c.accumulate, c.workspace, c.ws_bytes, stream, &jobs[i]);
+                if (rc) return rc;
+                continue;
+            }
+            int key, nblocks;
+            wgrad_split_setup(&c.geom, W, a, c.workspace, c.db, c.in_abs, c.in_sq, key, nblocks);
+            jobs[i] = wgrad_split_job(&c.geom, W, a, c.dw, c.db, c.accumulate);
+            size_t gi = 0;
+            while (gi < groups.size() && groups[gi].first != key) ++gi;
+            if (gi == groups.size()) {
+                groups.emplace_back(key, WgBatch{});
+                groups[gi].second.n = 0;
+                groups[gi].second.start[0] = 0;
+            }
+            WgBatch& B = groups[gi].second;
+            if (B.n == WG_BATCH_MAX) {
+                launch_wgrad_split_batch(B, key, st);
+                B.n = 0;
+            }
+            B.job[B.n] = a;
+            B.nwg[B.n] = nblocks;
+            B.start[B.n + 1] = B.start[B.n] + (nblocks + 7) / 8 * 8;
+            ++B.n;
             continue;
         }
         WgradPlan W;
@@ -4682,6 +4839,8 @@ int cai_conv_wgrad_batch(const cai_wgrad_call* calls, int32_t n, void* stream, c
     }
     for (int c = 0; c < 6; ++c)
         if (b[c].n) launch_wgrad_small_batch(b[c], c, st);
+    for (auto& kv : groups)
+        if (kv.second.n) launch_wgrad_split_batch(kv.second, kv.first, st);
     CAI_LAUNCH_CHECK("conv_wgrad_batch");
     return CAI_OK;
 }

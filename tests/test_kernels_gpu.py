@@ -1179,7 +1179,8 @@ def test_wgrad_batch_bit_identical_to_single_calls(cuda):
     deferred to its end) against one cai_conv_wgrad call per layer: bit-identical weight and bias gradients.
     Calls: C2's h_a[2] / h_a[4] (Conv2d k5 s2 at 16x16 / 8x8, B = 16), h_s[0] / h_s[2] (ConvTranspose2d k5 s2
     at 4x4 / 8x8: bias from trailing blocks), an |x| input (k3 s1 at 8x8), two calls accumulating into ONE bias
-    gradient (separate launches), and a 16x16 k3 layer too large for the latent kernel (run as usual)."""
+    gradient (separate launches), and pixel-split calls grouped by kernel variant: 16x16 k3 layers on the LDS-DMA
+    kernel (one with |x|) and two 64x64 stride-1 3x3 layers on the halo kernel (cheng2020's)."""
     import ctypes
 
     from compressai import _native as native
@@ -1196,9 +1197,14 @@ def test_wgrad_batch_bit_identical_to_single_calls(cuda):
         (G(16, 192, 8, 8, 128, 8, 8, 3, 1, 1, 0, 0), 1),
         (G(16, 128, 8, 8, 128, 4, 4, 5, 2, 2, 0, 0), 0),             # shares call 1's bias gradient
         (G(16, 192, 16, 16, 128, 16, 16, 3, 1, 1, 0, 0), 0),          # 4096 pixels: wgrad_glds + slab reduce
+        (G(16, 192, 16, 16, 128, 16, 16, 3, 1, 1, 0, 0), 1),          # the same variant with |x|: its own launch
+        (G(16, 128, 16, 16, 192, 16, 16, 3, 1, 1, 0, 0), 0),          # a second glds call of call 6's variant
+        (G(4, 192, 64, 64, 192, 64, 64, 3, 1, 1, 0, 0), 0),           # cheng2020's stride-1 3x3 (halo, s1) ...
+        (G(4, 192, 64, 64, 192, 64, 64, 3, 1, 1, 0, 0), 0),           # ... twice: one batched launch
     ]
     names = [raw.cai_conv_kernel_name(ctypes.byref(g), native.BF16, 2, a).decode() for g, a in specs]
     assert names[:6] == ["wgrad_small_kernel"] * 6 and names[6] != "wgrad_small_kernel", names
+    assert names[9] == names[10] == "wgrad_halo_kernel<3,s1>", names
     calls = []
     for i, (g, in_abs) in enumerate(specs):
         x = torch.randn(g.batch, g.in_h, g.in_w, g.in_c, device=cuda).bfloat16()
