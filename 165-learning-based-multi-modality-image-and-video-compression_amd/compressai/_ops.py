@@ -863,22 +863,22 @@ class FanOutFn(torch.autograd.Function):
     dx = dx_take + dx_give."""
 
     @staticmethod
-    def forward(ctx, x, box):
+    def forward(ctx, x, box, n: int):
         ctx.set_materialize_grads(False)
         ctx.box = box
-        return x.view_as(x), x.view_as(x)
+        return tuple(x.view_as(x) for _ in range(n))
 
     @staticmethod
-    def backward(ctx, ga, gb):
+    def backward(ctx, *grads):
         box = ctx.box
         extra, box.pending = box.pending, None
-        gs = [t for t in (ga, gb, extra) if t is not None]
+        gs = [t for t in (*grads, extra) if t is not None]
         if not gs:
-            return None, None
+            return None, None, None
         total = gs[0]
         for t in gs[1:]:
             total = _add_grads(total, t)
-        return total, None
+        return total, None, None
 
 
 def _add_grads(a, b):
@@ -895,16 +895,23 @@ def _add_grads(a, b):
     return a + b
 
 
-def fan_out(x):
-    """(x_take, x_give) for a tensor read by a conv (x_take) and a GaussianConditional (x_give); (x, x) when x
-    does not require a gradient."""
-    if not (torch.is_grad_enabled() and x.requires_grad):
-        return x, x
+_FANOUT = os.environ.get("CAI_FANOUT", "1") == "1"   # 0: autograd sums the gradients (A/B)
+
+
+def fan_out(x, n: int = 2, absorb: bool = True):
+    """n aliases of x for its n consumers (x itself n times when x does not require a gradient); their gradients
+    are summed by the native add instead of autograd's ATen add.  absorb (n == 2): the first alias is read by a
+    conv (taker), the second by a GaussianConditional (giver), whose gradient the conv adds in its dgrad epilogue.
+    absorb=False keeps the sum order-independent (one native add of the two gradients, whichever stream or order
+    produced them: bit-identical to autograd's sum)."""
+    if not (_FANOUT and torch.is_grad_enabled() and x.requires_grad):
+        return (x,) * n
     box = _FanIn()
-    a, b = FanOutFn.apply(x, box)
-    setattr(a, _FAN_ATTR, (box, "take"))
-    setattr(b, _FAN_ATTR, (box, "give"))
-    return a, b
+    outs = FanOutFn.apply(x, box, n)
+    if absorb and n == 2:
+        setattr(outs[0], _FAN_ATTR, (box, "take"))
+        setattr(outs[1], _FAN_ATTR, (box, "give"))
+    return outs
 
 
 class ResidualChainFn(torch.autograd.Function):

@@ -21,7 +21,8 @@ import torch
 import torch.nn as nn
 
 from .._native import ACT_LEAKY, ACT_NONE, ACT_RELU, MASK_LEAKY, MASK_POS
-from .._ops import AddActFn, AttentionBlockFn, GateFn, ResidualBlockFn, ResidualChainFn, _ab_side, residual_fusable
+from .._ops import (AddActFn, AttentionBlockFn, GateFn, ResidualBlockFn, ResidualChainFn, _ab_side, fan_out,
+                    residual_fusable)
 from .conv import Conv2d, ConvTranspose2d, PixelShuffle, Sequential
 from .gdn import GDN
 
@@ -79,18 +80,19 @@ class ResidualBlockWithStride(nn.Module):
 
     def forward(self, x):
         side = _ab_side(x, self.skip.parameters()) if self.skip is not None else None
+        xm, xs = fan_out(x, absorb=False)   # x's two gradients: one native add, not autograd's ATen add
         if side is not None:   # the skip conv on the side stream (autograd runs its backward there too)
             main = torch.cuda.current_stream(x.device)
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                identity = self.skip(x)
-        out = self.conv1.run(x, act=ACT_LEAKY, act_param=_SLOPE, act_bwd_downstream=True)
+                identity = self.skip(xs)
+        out = self.conv1.run(xm, act=ACT_LEAKY, act_param=_SLOPE, act_bwd_downstream=True)
         out = self.conv2.run(out, in_mask=MASK_LEAKY, in_mask_param=_SLOPE)
         out = self.gdn(out)
         if side is not None:
             _join(main, side, x, identity)
         else:
-            identity = self.skip(x) if self.skip is not None else x
+            identity = self.skip(xs) if self.skip is not None else xs
         return AddActFn.apply(out, identity, ACT_NONE, 0.0)
 
 
@@ -107,18 +109,19 @@ class ResidualBlockUpsample(nn.Module):
 
     def forward(self, x):
         side = _ab_side(x, self.upsample.parameters())
+        xm, xu = fan_out(x, absorb=False)
         if side is not None:   # the upsampling branch on the side stream (autograd runs its backward there too)
             main = torch.cuda.current_stream(x.device)
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                identity = self.upsample(x)
-        out = self.subpel_conv(x, act=ACT_LEAKY, act_param=_SLOPE, act_bwd_downstream=True)
+                identity = self.upsample(xu)
+        out = self.subpel_conv(xm, act=ACT_LEAKY, act_param=_SLOPE, act_bwd_downstream=True)
         out = self.conv.run(out, in_mask=MASK_LEAKY, in_mask_param=_SLOPE)
         out = self.igdn(out)
         if side is not None:
             _join(main, side, x, identity)
         else:
-            identity = self.upsample(x)
+            identity = self.upsample(xu)
         return AddActFn.apply(out, identity, ACT_NONE, 0.0)
 
 
@@ -141,9 +144,10 @@ class ResidualBlock(nn.Module):
         if self.skip is None and self.fuse_residual:
             return ResidualBlockFn.apply(x, s1, s2, self.conv1.weight, self.conv1.bias, self.conv2.weight,
                                          self.conv2.bias)
-        out = self.conv1.run(x, act=ACT_LEAKY, act_param=_SLOPE, act_bwd_downstream=True)
+        xm, xs = fan_out(x, absorb=False)
+        out = self.conv1.run(xm, act=ACT_LEAKY, act_param=_SLOPE, act_bwd_downstream=True)
         out = self.conv2.run(out, act=ACT_LEAKY, act_param=_SLOPE, in_mask=MASK_LEAKY, in_mask_param=_SLOPE)
-        identity = self.skip(x) if self.skip is not None else x
+        identity = self.skip(xs) if self.skip is not None else xs
         return AddActFn.apply(out, identity, ACT_NONE, 0.0)
 
 

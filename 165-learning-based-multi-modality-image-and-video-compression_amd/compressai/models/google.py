@@ -477,35 +477,39 @@ class JointAutoregressiveHierarchicalPriors(_ARCoding, MeanScaleHyperprior):
         y = self._dp_cut(self.g_a(x))
         side = _side_stream(y, True)
         if side is None:
-            z = self.h_a(y)
+            y_ha, y_q, y_gc = fan_out(y, 3, absorb=False)
+            z = self.h_a(y_ha)
             z_hat, z_likelihoods = self.entropy_bottleneck(z)
             params = self.h_s(z_hat)
-            y_hat = self.gaussian_conditional.quantize(y, "noise" if self.training else "dequantize")
-            ctx_params = self.context_prediction(y_hat)
+            y_hat = self.gaussian_conditional.quantize(y_q, "noise" if self.training else "dequantize")
+            y_ctx, y_gs = fan_out(y_hat, absorb=False)
+            ctx_params = self.context_prediction(y_ctx)
             gaussian_params = self.entropy_parameters(torch.cat((params, ctx_params), dim=1))
             scales_hat, means_hat = gaussian_params.chunk(2, 1)
-            _, y_likelihoods = self.gaussian_conditional(y, scales_hat, means=means_hat)
-            x_hat = self.g_s(y_hat)
+            _, y_likelihoods = self.gaussian_conditional(y_gc, scales_hat, means=means_hat)
+            x_hat = self.g_s(y_gs)
             return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods, "z": z_likelihoods}}
         main = torch.cuda.current_stream()
         z_noise = _z_noise(self, y)
+        y_ha, y_q, y_gc = fan_out(y, 3, absorb=False)   # y's three gradients: native adds, not ATen's
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            z = self.h_a(y)
+            z = self.h_a(y_ha)
             z_hat, z_likelihoods = self.entropy_bottleneck(z, noise=z_noise)
             params = self.h_s(z_hat)
         # the reference's draws in its order (z, then y_hat's, then the likelihood's)
-        y_hat, noise = _quantize_y(y, self.training)
+        y_hat, noise = _quantize_y(y_q, self.training)
         noise2 = _draw_noise(y) if self.training else None
+        y_gs, y_ctx = fan_out(y_hat, absorb=False)
         ready = torch.cuda.Event()
         ready.record(main)
-        x_hat = self.g_s(y_hat)
+        x_hat = self.g_s(y_gs)
         with torch.cuda.stream(side):
             side.wait_event(ready)
-            ctx_params = self.context_prediction(y_hat)
+            ctx_params = self.context_prediction(y_ctx)
             gaussian_params = self.entropy_parameters(torch.cat((params, ctx_params), dim=1))
             scales_hat, means_hat = gaussian_params.chunk(2, 1)
-            _, y_likelihoods = self.gaussian_conditional(y, scales_hat, means=means_hat, noise=noise2)
+            _, y_likelihoods = self.gaussian_conditional(y_gc, scales_hat, means=means_hat, noise=noise2)
         main.wait_stream(side)
         y_hat.record_stream(side)
         if noise2 is not None:

@@ -447,12 +447,19 @@ def test_master_guided_paper_resolution_vs_oracle(cuda):
         torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32, torch.backends.cudnn.enabled = prev
 
 
-def test_c2_step_launches_no_aten_kernels(cuda):
-    """The C2 training step (bmshj2018-hyperprior q1, B=16, 256^2, bf16 autocast; bench.py's step: FusedAdam with
-    zero_grad_in_step, the persistent loss seeds, clip + Adam + aux loss) launches only libcai kernels: no ATen
-    elementwise / fill / reduce kernel (y's two gradients meet in h_a's first dgrad epilogue, the aux loss's
-    quantile gradient accumulates through cai_axpy_dev).  Device kernels of the third eager step, from
-    torch.profiler."""
+@pytest.mark.parametrize("name,quality,batch,only", [
+    ("bmshj2018-hyperprior", 1, 16, None),
+    ("cheng2020-attn", 6, 4, "Functor_add"),
+], ids=["C2", "C4"])
+def test_step_launches_no_aten_kernels(cuda, name, quality, batch, only):
+    """The training step (C2: bmshj2018-hyperprior q1, B=16; C4: cheng2020-attn q6, B=4; 256^2, bf16 autocast;
+    bench.py's step: FusedAdam with zero_grad_in_step, the persistent loss seeds, clip + Adam + aux loss).
+    C2 launches only libcai kernels: no ATen elementwise / fill / reduce kernel -- y's two gradients meet in h_a's
+    first dgrad epilogue, the aux loss's quantile gradient accumulates through cai_axpy_dev.  C4 launches no ATen
+    gradient sum (`only`): the residual blocks' inputs and the context model's y / y_hat are read through FanOutFn,
+    whose native add sums their gradients.  C4 still has four ATen launches: the context model's torch.cat, the
+    masked conv's in-place weight mask (the reference's `weight.data *= mask`), one layout copy and one fill.
+    Device kernels of the third eager step, from torch.profiler."""
     from torch.profiler import ProfilerActivity, profile
 
     from compressai._ops import loss_seed
@@ -461,10 +468,10 @@ def test_c2_step_launches_no_aten_kernels(cuda):
     from compressai.zoo import image_models
 
     torch.manual_seed(0)
-    net = image_models["bmshj2018-hyperprior"](1).to(cuda).train()
-    x = torch.rand(16, 3, 256, 256, device=cuda)
+    net = image_models[name](quality).to(cuda).train()
+    x = torch.rand(batch, 3, 256, 256, device=cuda)
     opt, aux_opt = configure_optimizers(net, zero_grad_in_step=True)
-    crit = RateDistortionLoss(1)
+    crit = RateDistortionLoss(quality)
 
     def step():
         opt.zero_grad()
@@ -484,7 +491,7 @@ def test_c2_step_launches_no_aten_kernels(cuda):
         step()
         torch.cuda.synchronize()
     names = sorted({e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA})
-    print(f"\nC2 step: {len(names)} distinct device kernels / copies")
+    print(f"\n{name} step: {len(names)} distinct device kernels / copies")
     assert len(names) > 20, names               # the profiler saw the step's kernels
-    aten = [n for n in names if "at::" in n or "aten::" in n]
+    aten = [n for n in names if ("at::" in n or "aten::" in n) and (only is None or only in n)]
     assert not aten, aten
