@@ -2974,9 +2974,6 @@ struct WhCfg {
     static constexpr int TN = WCOL / 16;
 };
 
-#ifndef CAI_WH_PF
-#define CAI_WH_PF 0   // A/B: 1 = fragment reads one K-half ahead (no gain: the kernel waits on its DMA, r04_wgrad_halo_pf_ab.log)
-#endif
 
 __device__ __forceinline__ int wh_h(int cell) { return ((cell >> 1) & 1) | (((cell >> 3) & 1) << 1); }
 
@@ -2988,8 +2985,11 @@ __device__ __forceinline__ int opaque(int v) {
 }
 
 // S = 1: the stride-1 k3 p1 Conv2d (cheng2020's 3x3 convs): one footprint plane, tap kw at cell p + kw.
-template <int KS, int S, int FLAGS, int R>
+// TMR: row fragments per wave -- 4 (128-row tiles) or 2 (64-row tiles, for Ng a multiple of 64 but not of 128:
+// cheng2020's 192-channel layers, C2's g_a[6] / g_s[0]; the 128-row tiles left a third of their rows empty)
+template <int KS, int S, int FLAGS, int R, int TMR>
 __device__ __forceinline__ void wgrad_halo_block(const WgradArgs& a, int wgid, int nwg, char* smem) {
+    static_assert(TMR == 4 || TMR == 2, "128- or 64-row tiles");
     using W = WhCfg<KS, S, R>;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wr = wid >> 2, wc = wid & 3;            // 2 (rows) x 4 (cols) waves
@@ -2999,7 +2999,7 @@ __device__ __forceinline__ void wgrad_halo_block(const WgradArgs& a, int wgid, i
     const int split = L / ntile;
     const int tl = L - split * ntile;
     const int ctile = tl % (KS * nqc), rtile = tl / (KS * nqc);
-    const int kh = ctile / nqc, q0 = (ctile - kh * nqc) * 64, r0 = rtile * 128;
+    const int kh = ctile / nqc, q0 = (ctile - kh * nqc) * 64, r0 = rtile * (32 * TMR);
     const int nsr = R == 1 ? a.Wg / 64 : 1;           // strips per G row (R > 1: one strip spans R rows)
     const int nrg = a.Hg / R;                         // strip rows per image
     const int nstrip = a.B * nrg * nsr;
@@ -3013,7 +3013,7 @@ __device__ __forceinline__ void wgrad_halo_block(const WgradArgs& a, int wgid, i
     const char* Gp = reinterpret_cast<const char*>(a.g);
     const char* Xp = reinterpret_cast<const char*>(a.x);
     const int gch = r0 + sl * 8;
-    const bool gvalid = gch < a.Ng;
+    const bool gvalid = gch < a.Ng && (TMR == 4 || sl < 8);   // 64-row tiles: the strip's first 64 channels
     // X DMA: this lane's footprint piece of each instruction (x offset t, channel byte offset), or the sink
     int xt[W::NXI];
     int xr[W::NXI];                                   // strip row of the piece (R > 1)
@@ -3075,15 +3075,17 @@ __device__ __forceinline__ void wgrad_halo_block(const WgradArgs& a, int wgid, i
         }
     };
 
-    f32x4 acc[4][W::TN];
+    f32x4 acc[TMR][W::TN];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < TMR; ++i)
 #pragma unroll
         for (int j = 0; j < W::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const int g_ = lane >> 4, i16 = lane & 15, q_ = i16 >> 2, p4 = i16 & 3;
     const bool do_bias = (FLAGS & WG_BIAS) && ctile == 0;
-    float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+    float bsum[TMR];
+#pragma unroll
+    for (int i = 0; i < TMR; ++i) bsum[i] = 0.f;
     const int wcol = wc * W::WCOL;
     int tsel[W::TN];
     float tsum[W::TN];
@@ -3099,7 +3101,7 @@ __device__ __forceinline__ void wgrad_halo_block(const WgradArgs& a, int wgid, i
     // LDS byte offsets of every fragment read, fixed for the launch (stage 0; the other stages add a
     // compile-time immediate): B (footprint) per (ks, column block, pixel half) -- the tap's plane / cell
     // shift and the block's swizzled 32-B group -- and A (G strip)
-    int boff[2][W::TN][2], aoff[2][4][2];
+    int boff[2][W::TN][2], aoff[2][TMR][2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
         const int rr = 32 * ks + 8 * g_ + q_;
@@ -3114,8 +3116,8 @@ __device__ __forceinline__ void wgrad_halo_block(const WgradArgs& a, int wgid, i
             }
         }
 #pragma unroll
-        for (int tm = 0; tm < 4; ++tm) {
-            const int colA = wr * 64 + tm * 16 + 4 * p4;
+        for (int tm = 0; tm < TMR; ++tm) {
+            const int colA = wr * (16 * TMR) + tm * 16 + 4 * p4;
 #pragma unroll
             for (int h = 0; h < 2; ++h)
                 aoff[ks][tm][h] = opaque(trswz(rr + 4 * h, colA >> 3) + ((colA & 7) << 1));
@@ -3123,7 +3125,7 @@ __device__ __forceinline__ void wgrad_halo_block(const WgradArgs& a, int wgid, i
     }
 
     // fragment reads of one K-half (ks) of a ring stage, and the MFMAs (+ bias sums) on them
-    auto rd = [&](auto ustage, auto kc, u32x4 (&fa)[4], u32x4 (&fb)[W::TN]) {
+    auto rd = [&](auto ustage, auto kc, u32x4 (&fa)[TMR], u32x4 (&fb)[W::TN]) {
         constexpr int U = decltype(ustage)::value, ks = decltype(kc)::value;
         const char* Gs = smem + U * W::GIMG;
         const char* Xs = smem + U * W::XSTRIDE;      // boff carries XBASE
@@ -3135,16 +3137,16 @@ __device__ __forceinline__ void wgrad_halo_block(const WgradArgs& a, int wgid, i
             fb[t] = __builtin_bit_cast(u32x4, bv);
         }
 #pragma unroll
-        for (int tm = 0; tm < 4; ++tm) {
+        for (int tm = 0; tm < TMR; ++tm) {
             s16x4 a0 = ds_tr16(Gs, aoff[ks][tm][0]);
             s16x4 a1 = ds_tr16(Gs, aoff[ks][tm][1]);
             s16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
             fa[tm] = __builtin_bit_cast(u32x4, av);
         }
     };
-    auto mm = [&](const u32x4 (&fa)[4], const u32x4 (&fb)[W::TN]) {
+    auto mm = [&](const u32x4 (&fa)[TMR], const u32x4 (&fb)[W::TN]) {
 #pragma unroll
-        for (int tm = 0; tm < 4; ++tm) {
+        for (int tm = 0; tm < TMR; ++tm) {
             if constexpr ((FLAGS & WG_BIAS) != 0) {
                 if (do_bias && tm == wc) {
                     const bf16x8 h = __builtin_bit_cast(bf16x8, fa[tm]);
@@ -3170,62 +3172,6 @@ __device__ __forceinline__ void wgrad_halo_block(const WgradArgs& a, int wgid, i
 #pragma unroll
     for (int s = 0; s < W::NST - 1; ++s)
         if (s < nsteps) issue(s);
-#if CAI_WH_PF
-    // Software-pipelined: the fragments of the next K-half are read while the MFMAs of the current one run --
-    // the second half of a strip during the first, and the first half of the NEXT strip during the second.
-    // So a step's wait covers the next strip as well (2 strips in flight instead of 3), and the one barrier
-    // per step still separates every read of a stage from the DMA that refills it (issued a step later).
-    u32x4 fca[4], fcb[W::TN], fna[4], fnb[W::TN];
-    if (nsteps > 0) {
-        if (nsteps >= 3)
-            wait_vmcnt<2 * W::NLOAD>();
-        else if (nsteps == 2)
-            wait_vmcnt<W::NLOAD>();
-        else
-            wait_vmcnt<0>();
-        __builtin_amdgcn_s_barrier();
-        rd(K0(), K0(), fca, fcb);
-    }
-    for (int st0 = 0; st0 < nsteps; st0 += W::NST) {
-        auto one = [&](auto ustage) {
-            constexpr int U = decltype(ustage)::value;
-            const int st = st0 + U;
-            if (st >= nsteps) return;
-            if (st + 2 < nsteps)   // strips 0 .. st + 1 landed (st + 2 may stay in flight)
-                wait_vmcnt<W::NLOAD>();
-            else
-                wait_vmcnt<0>();
-            wait_lgkmcnt0();
-            __builtin_amdgcn_s_barrier();
-            __builtin_amdgcn_sched_barrier(0);
-            if (st + W::NST - 1 < nsteps) issue((U + W::NST - 1) % W::NST);
-            rd(ustage, K1(), fna, fnb);
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_setprio(1);
-            mm(fca, fcb);
-            __builtin_amdgcn_s_setprio(0);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) fca[i] = fna[i];
-#pragma unroll
-            for (int i = 0; i < W::TN; ++i) fcb[i] = fnb[i];
-            if (st + 1 < nsteps) rd(std::integral_constant<int, (U + 1) % W::NST>(), K0(), fna, fnb);
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_setprio(1);
-            mm(fca, fcb);
-            __builtin_amdgcn_s_setprio(0);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) fca[i] = fna[i];
-#pragma unroll
-            for (int i = 0; i < W::TN; ++i) fcb[i] = fnb[i];
-        };
-        one(std::integral_constant<int, 0>());
-        one(std::integral_constant<int, 1>());
-        one(std::integral_constant<int, 2>());
-        one(std::integral_constant<int, 3>());
-    }
-#else
     // the ring position is a compile-time constant: the loop runs NST strips per trip
     for (int st0 = 0; st0 < nsteps; st0 += W::NST) {
         auto one = [&](auto ustage) {
@@ -3243,7 +3189,7 @@ __device__ __forceinline__ void wgrad_halo_block(const WgradArgs& a, int wgid, i
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
             if (st + W::NST - 1 < nsteps) issue((U + W::NST - 1) % W::NST);
-            u32x4 fa[4], fb[W::TN];
+            u32x4 fa[TMR], fb[W::TN];
             rd(ustage, K0(), fa, fb);
             mm(fa, fb);
             rd(ustage, K1(), fa, fb);
@@ -3255,13 +3201,14 @@ __device__ __forceinline__ void wgrad_halo_block(const WgradArgs& a, int wgid, i
         one(std::integral_constant<int, 2>());
         one(std::integral_constant<int, 3>());
     }
-#endif
     if constexpr ((FLAGS & WG_BIAS) != 0) {
-        if (do_bias) {
-            float v = bsum[0] + bsum[1] + bsum[2] + bsum[3];
+        if (do_bias && wc < TMR) {   // wave (wr, wc) summed fragment wc of its rows
+            float v = 0.f;
+#pragma unroll
+            for (int i = 0; i < TMR; ++i) v += bsum[i];
             v += __shfl_xor(v, 16);
             v += __shfl_xor(v, 32);
-            const int n = r0 + wr * 64 + wc * 16 + lane;
+            const int n = r0 + wr * (16 * TMR) + wc * 16 + lane;
             if (lane < 16 && n < a.Ng) a.bws[(int64_t)split * a.Ng + n] = v;
         }
     }
@@ -3281,47 +3228,47 @@ __device__ __forceinline__ void wgrad_halo_block(const WgradArgs& a, int wgid, i
         const int col = wcol + tn * 16 + (lane & 15), kw = col / 64;
         const int gcol = (kh * KS + kw) * a.Cq_pad + q0 + col % 64;
 #pragma unroll
-        for (int tm = 0; tm < 4; ++tm)
+        for (int tm = 0; tm < TMR; ++tm)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int row = r0 + wr * 64 + tm * 16 + (lane >> 4) * 4 + r;
+                const int row = r0 + wr * (16 * TMR) + tm * 16 + (lane >> 4) * 4 + r;
                 if (row < a.Ng) out[(int64_t)row * a.ncols + gcol] = acc[tm][tn][r];
             }
     }
 }
 
-template <int KS, int S, int FLAGS, int R = 1>
+template <int KS, int S, int FLAGS, int R = 1, int TMR = 4>
 __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
     __shared__ __attribute__((aligned(16))) char smem[WhCfg<KS, S, R>::BYTES];
-    wgrad_halo_block<KS, S, FLAGS, R>(a, (int)blockIdx.x, (int)gridDim.x, smem);
+    wgrad_halo_block<KS, S, FLAGS, R, TMR>(a, (int)blockIdx.x, (int)gridDim.x, smem);
 }
 
-template <int KS, int S, int FLAGS, int R = 1>
+template <int KS, int S, int FLAGS, int R = 1, int TMR = 4>
 __global__ __launch_bounds__(512, 1) void wgrad_halo_batch_kernel(const WgBatch b) {
     __shared__ __attribute__((aligned(16))) char smem[WhCfg<KS, S, R>::BYTES];
     const int L = (int)blockIdx.x, j = wg_batch_job(b, L), l = L - b.start[j];
-    if (l < b.nwg[j]) wgrad_halo_block<KS, S, FLAGS, R>(b.job[j], l, b.nwg[j], smem);
+    if (l < b.nwg[j]) wgrad_halo_block<KS, S, FLAGS, R, TMR>(b.job[j], l, b.nwg[j], smem);
 }
 
-template <int KS, int S, int R = 1>
+template <int KS, int S, int R = 1, int TMR = 4>
 static void launch_wgrad_halo(const WgradArgs& a, int nblocks, int bias, hipStream_t st) {
     if (bias == WG_BIAS)
-        hipLaunchKernelGGL((wgrad_halo_kernel<KS, S, WG_BIAS, R>), dim3(nblocks), dim3(512), 0, st, a);
+        hipLaunchKernelGGL((wgrad_halo_kernel<KS, S, WG_BIAS, R, TMR>), dim3(nblocks), dim3(512), 0, st, a);
     else if (S == 2 && bias == WG_TBIAS)
-        hipLaunchKernelGGL((wgrad_halo_kernel<KS, S, WG_TBIAS, R>), dim3(nblocks), dim3(512), 0, st, a);
+        hipLaunchKernelGGL((wgrad_halo_kernel<KS, S, WG_TBIAS, R, TMR>), dim3(nblocks), dim3(512), 0, st, a);
     else
-        hipLaunchKernelGGL((wgrad_halo_kernel<KS, S, 0, R>), dim3(nblocks), dim3(512), 0, st, a);
+        hipLaunchKernelGGL((wgrad_halo_kernel<KS, S, 0, R, TMR>), dim3(nblocks), dim3(512), 0, st, a);
 }
 
-template <int KS, int S, int R = 1>
+template <int KS, int S, int R = 1, int TMR = 4>
 static void launch_wgrad_halo_batch(const WgBatch& b, int bias, hipStream_t st) {
     const dim3 grid(b.start[b.n]);
     if (bias == WG_BIAS)
-        hipLaunchKernelGGL((wgrad_halo_batch_kernel<KS, S, WG_BIAS, R>), grid, dim3(512), 0, st, b);
+        hipLaunchKernelGGL((wgrad_halo_batch_kernel<KS, S, WG_BIAS, R, TMR>), grid, dim3(512), 0, st, b);
     else if (S == 2 && bias == WG_TBIAS)
-        hipLaunchKernelGGL((wgrad_halo_batch_kernel<KS, S, WG_TBIAS, R>), grid, dim3(512), 0, st, b);
+        hipLaunchKernelGGL((wgrad_halo_batch_kernel<KS, S, WG_TBIAS, R, TMR>), grid, dim3(512), 0, st, b);
     else
-        hipLaunchKernelGGL((wgrad_halo_batch_kernel<KS, S, 0, R>), grid, dim3(512), 0, st, b);
+        hipLaunchKernelGGL((wgrad_halo_batch_kernel<KS, S, 0, R, TMR>), grid, dim3(512), 0, st, b);
 }
 
 template <int CT>
@@ -3984,6 +3931,7 @@ struct WgradPlan {
     int tbias, tb_kh0, tb_kw0;   // ConvTranspose2d bias from the X operand's tap set (WG_TBIAS)
     int Sb, nbias;               // bias partial slabs and their length
     int strips_per_split;
+    int hrows;                   // halo kernel: rows (output channels) per tile, 128 or 64
     bool glds, fused_bias;
     int ct;
     size_t ws_bias;
@@ -4119,7 +4067,16 @@ static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype, bool glds, b
         const int Wg = g->transposed ? g->in_w : g->out_w;
         const int Hg = g->transposed ? g->in_h : g->out_h;
         const int64_t nstrip = (int64_t)g->batch * Hg * Wg / 64;    // 64-pixel strips (R rows each)
-        W.tiles = W.halo * (W.Cq_pad / 64) * ((W.Ng + 127) / 128);
+        // 64-row tiles where 128 would leave rows empty (Ng = 192: a third of the MFMA work) -- for the k5 kernel
+        // only: C2's g_a[6] / g_s[0] weight gradients 10198 -> 10265 patches/s, while cheng2020's k3 layers lost
+        // 0.9 % (688 -> 682: half the MFMA work per step against the same per-step DMA and barrier, and more steps
+        // per block; profiles/r05_halo_wgrad_64_rows_ab.log).  A/B knob CAI_HALO_WGRAD_ROWS128=1 keeps 128.
+        static const bool rows128 = [] {
+            const char* e = getenv("CAI_HALO_WGRAD_ROWS128");
+            return e && *e == '1';
+        }();
+        W.hrows = (!rows128 && W.halo == 5 && W.Ng % 128 != 0 && W.Ng % 64 == 0) ? 64 : 128;
+        W.tiles = W.halo * (W.Cq_pad / 64) * ((W.Ng + W.hrows - 1) / W.hrows);
         int S = std::max(1, wg_blocks() / W.tiles);
         S = (int)std::max<int64_t>(1, std::min<int64_t>(S, nstrip / wg_min_strips()));   // >= 4 strips per split
         W.strips_per_split = (int)((nstrip + S - 1) / S);
@@ -4625,8 +4582,8 @@ static void wgrad_split_setup(const cai_conv_geom* g, const WgradPlan& W, WgradA
     nblocks = W.S * W.tiles;
     if (W.halo) {
         a.nsplit = W.strips_per_split;
-        a.rtiles = (W.Ng + 127) / 128;
-        key = (((W.halo * 10 + g->stride) * 10 + halo_wgrad_rows(g)) << 4) | bflag;
+        a.rtiles = (W.Ng + W.hrows - 1) / W.hrows;
+        key = (((((W.halo * 10 + g->stride) * 10 + halo_wgrad_rows(g)) << 1) | (W.hrows == 64 ? 1 : 0)) << 4) | bflag;
     } else {
         key = (1 << 20) | (W.ct << 4) | (in_abs ? WG_ABS : 0) | (in_sq ? WG_SQ : 0) | bflag;
     }
@@ -4654,14 +4611,15 @@ static void launch_wgrad_split(const WgradArgs& a, int key, int nblocks, hipStre
             launch_wgrad_glds<128>(a, nblocks, in_abs, in_sq, bflag, st);
         return;
     }
-    switch (key >> 4) {
-        case 521: launch_wgrad_halo<5, 2>(a, nblocks, f, st); break;
-        case 522: launch_wgrad_halo<5, 2, 2>(a, nblocks, f, st); break;
-        case 524: launch_wgrad_halo<5, 2, 4>(a, nblocks, f, st); break;
-        case 322: launch_wgrad_halo<3, 2, 2>(a, nblocks, f, st); break;
-        case 324: launch_wgrad_halo<3, 2, 4>(a, nblocks, f, st); break;
-        case 311: launch_wgrad_halo<3, 1>(a, nblocks, f, st); break;
-        default: launch_wgrad_halo<3, 2>(a, nblocks, f, st); break;
+    const bool r64 = (key >> 4) & 1;
+    switch (key >> 5) {
+        case 521: r64 ? launch_wgrad_halo<5, 2, 1, 2>(a, nblocks, f, st) : launch_wgrad_halo<5, 2>(a, nblocks, f, st); break;
+        case 522: r64 ? launch_wgrad_halo<5, 2, 2, 2>(a, nblocks, f, st) : launch_wgrad_halo<5, 2, 2>(a, nblocks, f, st); break;
+        case 524: r64 ? launch_wgrad_halo<5, 2, 4, 2>(a, nblocks, f, st) : launch_wgrad_halo<5, 2, 4>(a, nblocks, f, st); break;
+        case 322: r64 ? launch_wgrad_halo<3, 2, 2, 2>(a, nblocks, f, st) : launch_wgrad_halo<3, 2, 2>(a, nblocks, f, st); break;
+        case 324: r64 ? launch_wgrad_halo<3, 2, 4, 2>(a, nblocks, f, st) : launch_wgrad_halo<3, 2, 4>(a, nblocks, f, st); break;
+        case 311: r64 ? launch_wgrad_halo<3, 1, 1, 2>(a, nblocks, f, st) : launch_wgrad_halo<3, 1>(a, nblocks, f, st); break;
+        default: r64 ? launch_wgrad_halo<3, 2, 1, 2>(a, nblocks, f, st) : launch_wgrad_halo<3, 2>(a, nblocks, f, st); break;
     }
 }
 
@@ -4674,14 +4632,15 @@ static void launch_wgrad_split_batch(const WgBatch& b, int key, hipStream_t st) 
             launch_wgrad_glds_batch<128>(b, f, st);
         return;
     }
-    switch (key >> 4) {
-        case 521: launch_wgrad_halo_batch<5, 2>(b, f, st); break;
-        case 522: launch_wgrad_halo_batch<5, 2, 2>(b, f, st); break;
-        case 524: launch_wgrad_halo_batch<5, 2, 4>(b, f, st); break;
-        case 322: launch_wgrad_halo_batch<3, 2, 2>(b, f, st); break;
-        case 324: launch_wgrad_halo_batch<3, 2, 4>(b, f, st); break;
-        case 311: launch_wgrad_halo_batch<3, 1>(b, f, st); break;
-        default: launch_wgrad_halo_batch<3, 2>(b, f, st); break;
+    const bool r64 = (key >> 4) & 1;
+    switch (key >> 5) {
+        case 521: r64 ? launch_wgrad_halo_batch<5, 2, 1, 2>(b, f, st) : launch_wgrad_halo_batch<5, 2>(b, f, st); break;
+        case 522: r64 ? launch_wgrad_halo_batch<5, 2, 2, 2>(b, f, st) : launch_wgrad_halo_batch<5, 2, 2>(b, f, st); break;
+        case 524: r64 ? launch_wgrad_halo_batch<5, 2, 4, 2>(b, f, st) : launch_wgrad_halo_batch<5, 2, 4>(b, f, st); break;
+        case 322: r64 ? launch_wgrad_halo_batch<3, 2, 2, 2>(b, f, st) : launch_wgrad_halo_batch<3, 2, 2>(b, f, st); break;
+        case 324: r64 ? launch_wgrad_halo_batch<3, 2, 4, 2>(b, f, st) : launch_wgrad_halo_batch<3, 2, 4>(b, f, st); break;
+        case 311: r64 ? launch_wgrad_halo_batch<3, 1, 1, 2>(b, f, st) : launch_wgrad_halo_batch<3, 1>(b, f, st); break;
+        default: r64 ? launch_wgrad_halo_batch<3, 2, 1, 2>(b, f, st) : launch_wgrad_halo_batch<3, 2>(b, f, st); break;
     }
 }
 

@@ -1255,3 +1255,45 @@ def test_wgrad_batch_bit_identical_to_single_calls(cuda):
         assert torch.isfinite(bw[i]).all(), i
         assert torch.equal(sw[i], bw[i]), (i, names[i], (sw[i] - bw[i]).abs().max().item())
         assert torch.equal(sb[i], bb[i]), (i, names[i], (sb[i] - bb[i]).abs().max().item())
+
+
+@pytest.mark.parametrize("kind,B,cin,cout,H,k,s", [
+    ("conv", 4, 192, 192, 64, 3, 1),      # cheng2020's 3x3 at 64x64 (stride-1 halo kernel)
+    ("conv", 4, 192, 192, 64, 3, 2),      # ResidualBlockWithStride's conv1 (stride-2 k3)
+    ("conv", 16, 128, 192, 32, 5, 2),     # C2's g_a[6] (k5, 16-wide G rows: 4 rows per strip)
+    ("deconv", 16, 192, 128, 16, 5, 2),   # C2's g_s[0] (ConvTranspose2d: G = x, 192 rows)
+], ids=["s1-192", "s2k3-192", "ga6", "gs0"])
+def test_halo_wgrad_64_row_tiles(cuda, kind, B, cin, cout, H, k, s):
+    """The halo-staged weight gradient at Ng = 192 -- 64-row tiles on the k5 kernel (C2's g_a[6] / g_s[0]; 128-row
+    tiles left a third of the rows empty), 128-row tiles on the k3 ones (cheng2020's) -- against torch fp32 on the
+    same bf16-rounded operands: weight and bias gradients within 1e-2 (relative max)."""
+    import ctypes
+
+    from compressai import _native as native
+    from compressai.layers import Conv2d, ConvTranspose2d
+
+    torch.manual_seed(H + cin + k)
+    raw = native.lib.load()
+    if kind == "conv":
+        mod = Conv2d(cin, cout, k, stride=s, padding=k // 2).to(cuda)
+        Ho = (H + 2 * (k // 2) - k) // s + 1
+        g = native.ConvGeom(B, cin, H, H, cout, Ho, Ho, k, s, k // 2, 0, 0)
+    else:
+        mod = ConvTranspose2d(cin, cout, k, stride=s, padding=k // 2, output_padding=s - 1).to(cuda)
+        Ho = H * s
+        g = native.ConvGeom(B, cin, H, H, cout, Ho, Ho, k, s, k // 2, s - 1, 1)
+    assert raw.cai_conv_kernel_name(ctypes.byref(g), native.BF16, 2, 0).decode().startswith("wgrad_halo_kernel")
+    x = torch.randn(B, cin, H, H, device=cuda).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(B, cout, Ho, Ho, device=cuda)
+    with _autocast(True):
+        y = mod(x)
+    y.backward(gy)
+    wr = mod.weight.detach().bfloat16().float().requires_grad_()
+    br = mod.bias.detach().clone().requires_grad_()
+    xr = x.detach().bfloat16().float()
+    if kind == "conv":
+        F.conv2d(xr, wr, br, stride=s, padding=k // 2).backward(gy.bfloat16().float())
+    else:
+        F.conv_transpose2d(xr, wr, br, stride=s, padding=k // 2, output_padding=s - 1).backward(gy.bfloat16().float())
+    assert relerr(mod.weight.grad, wr.grad) < 1e-2, relerr(mod.weight.grad, wr.grad)
+    assert relerr(mod.bias.grad, br.grad) < 1e-2, relerr(mod.bias.grad, br.grad)
