@@ -228,9 +228,6 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvArgs& a, const Phas
     }
 }
 
-#ifndef CAI_EPI_T_LDS
-#define CAI_EPI_T_LDS 0
-#endif
 // Epilogue for TRANSPOSED accumulators (weights as the MFMA's A operand): lane (i16, g_) of tile (tm, tn)
 // holds output channels wn*WTN + tn*16 + 4*g_ + 0..3 of tile row wm*WTM + tm*16 + i16, so the common cases
 // store straight from registers: split-K partials as 16-byte fp32 stores into the slab, bf16 outputs
@@ -267,9 +264,8 @@ __device__ __forceinline__ void conv_epilogue_rows_t(const ConvArgs& a, const Ph
         return;
     }
     // (the mask variant only in the NOLDS tiles: in the 128-channel halo kernels its registers spill the loop)
-    // A/B -DCAI_EPI_T_LDS=1: the LDS-staged form (16-byte stores of whole pixel rows) for the 128-channel tiles too
     if (NOLDS ? epi_t_direct(a)
-              : (!CAI_EPI_T_LDS && a.y_vec && a.y_dtype == CAI_BF16 && !a.mask_mode && (a.Cout & 3) == 0)) {
+              : (a.y_vec && a.y_dtype == CAI_BF16 && !a.mask_mode && (a.Cout & 3) == 0)) {
         f32x4 bv[TN];
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn) {
@@ -958,12 +954,6 @@ __host__ __device__ constexpr int halo_younger_sp(int t, int nstb, int npi, int 
 
 // transposed accumulators + register-direct epilogue (conv_epilogue_rows_t) in the halo kernels: the
 // phase kernel's launches 57.8 vs 59.7 us average in the C2 step (profiles/r02_edge_s2d_ab.log, r02af)
-#ifndef CAI_HALO_T
-#define CAI_HALO_T 1
-#endif
-#ifndef CAI_HALO_PH_T
-#define CAI_HALO_PH_T 1
-#endif
 
 template <int KS>
 struct HaloCfg {
@@ -1141,8 +1131,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvArgs a, int
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
                 for (int tn = 0; tn < TN; ++tn) {
-                    acc[tm][tn] = CAI_HALO_T ? mma16<bf16>(fb[tn], fa[tm], acc[tm][tn])
-                                             : mma16<bf16>(fa[tm], fb[tn], acc[tm][tn]);
+                    acc[tm][tn] = mma16<bf16>(fb[tn], fa[tm], acc[tm][tn]);   // transposed accumulators
                 }
             // the next step's reads (separate registers) alternate with this step's first MFMAs (measured:
             // a read burst ahead of the MFMAs, or reads every other MFMA, ran 2-6 % slower)
@@ -1167,12 +1156,8 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvArgs a, int
         const int oy = ty0 + row / H::TW, ox = tx0 + row % H::TW;
         return (oy < P.OHg && ox < P.OWg) ? b * plane + oy * P.OWg + ox : -1;
     };
-    if (CAI_HALO_T)
-        conv_epilogue_rows_t<bf16, BM, BN, WM, WN, 512, decltype(rowm), false, false>(
-            a, P, plane, 0, reinterpret_cast<float*>(smem), acc, rowm, (int)blockIdx.z);
-    else
-        conv_epilogue_rows<bf16, BM, BN, WM, WN, 512, decltype(rowm), false>(a, P, plane, 0,
-                                                                             reinterpret_cast<float*>(smem), acc, rowm);
+    conv_epilogue_rows_t<bf16, BM, BN, WM, WN, 512, decltype(rowm), false, false>(
+        a, P, plane, 0, reinterpret_cast<float*>(smem), acc, rowm, (int)blockIdx.z);
 }
 
 // Halo-staged s^2-phase implicit GEMM for the stride-2 k5 transposed convolutions (ConvTranspose2d k5 s2 p2
@@ -1361,8 +1346,7 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
                 for (int tn = 0; tn < TN; ++tn)
-                    acc[tm][tn] = (CAI_HALO_PH_T || BN > 128) ? mma16<bf16>(fb[tn], fa[tm], acc[tm][tn])
-                                                : mma16<bf16>(fa[tm], fb[tn], acc[tm][tn]);
+                    acc[tm][tn] = mma16<bf16>(fb[tn], fa[tm], acc[tm][tn]);   // transposed accumulators
 #pragma unroll
             for (int i = 0; i < TM + TN; ++i) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -1384,12 +1368,8 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
         const int oy = ty0 + row / H::TW, ox = tx0 + row % H::TW;
         return (oy < P.OHg && ox < P.OWg) ? b * plane + oy * P.OWg + ox : -1;
     };
-    if (CAI_HALO_PH_T || BN > 128)
-        conv_epilogue_rows_t<bf16, BM, BN, WM, WN, NT, decltype(rowm), (BN > 128), false>(
-            a, P, plane, n0, reinterpret_cast<float*>(smem), acc, rowm, ph * a.ksplit + split);
-    else
-        conv_epilogue_rows<bf16, BM, BN, WM, WN, NT, decltype(rowm), false>(
-            a, P, plane, n0, reinterpret_cast<float*>(smem), acc, rowm, ph * a.ksplit + split);
+    conv_epilogue_rows_t<bf16, BM, BN, WM, WN, NT, decltype(rowm), (BN > 128), false>(
+        a, P, plane, n0, reinterpret_cast<float*>(smem), acc, rowm, ph * a.ksplit + split);
 }
 
 
@@ -1574,15 +1554,11 @@ __device__ __forceinline__ void conv_halo_wide_body(const ConvArgs& a, char* sme
         a, P, plane, n0, reinterpret_cast<float*>(smem), acc, rowm, ph * a.ksplit + split);
 }
 
-// CAI_HALO_DMA=1: the 128-channel phase / stride-1 kernels on the DMA-footprint body as well (A/B)
-#ifndef CAI_HALO_DMA
-#define CAI_HALO_DMA 0
-#endif
 
 // grid y: output-channel tiles of BN (192-channel layers: BN = 192, one tile per 192 channels).
 template <int BN>
 __global__ __launch_bounds__(512, 1) void conv_halo_phase_kernel(const ConvArgs a, int tiles_x, int tiles_y) {
-    constexpr bool DMA = BN > 128 || CAI_HALO_DMA;
+    constexpr bool DMA = BN > 128;
     constexpr int BYTES =
         DMA ? HaloWideCfg<3, 3, BN>::BYTES
             : (HaloPhCfg<3, 3>::BYTES > HaloPhCfg<2, 2>::BYTES ? HaloPhCfg<3, 3>::BYTES : HaloPhCfg<2, 2>::BYTES);
@@ -1622,7 +1598,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_phase_kernel(const ConvArgs 
 // z = split.
 template <int BN, bool GATHER>
 __global__ __launch_bounds__(512, 1) void conv_halo_s1_kernel(const ConvArgs a, int tiles_x, int tiles_y) {
-    constexpr bool DMA = BN > 128 || CAI_HALO_DMA;
+    constexpr bool DMA = BN > 128;
     __shared__ __attribute__((aligned(16))) char smem[DMA ? HaloWideCfg<3, 3, BN>::BYTES : HaloPhCfg<3, 3>::BYTES];
     const int nt = gridDim.x, t = blockIdx.x;
     const int bid = (nt & 7) == 0 ? (t & 7) * (nt >> 3) + (t >> 3) : t;

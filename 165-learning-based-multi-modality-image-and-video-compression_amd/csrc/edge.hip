@@ -64,9 +64,6 @@ struct EdgeArgs {
 // (the default); prefetch distance 2 23.4; nt stores 28.5 / 26.9 (grid-stride).  Timing probes (results
 // invalid): stores skipped at run time 12.9, no in-loop image loads 18.8 -- the kernel is issue-bound
 // (MFMA + VALU per tile) with the stores on top, against 11.3 us for a torch fill of the same bytes.
-#ifndef CAI_EDGE_PROBE
-#define CAI_EDGE_PROBE 0      // timing probes: 1 stores skipped at run time, 2 no in-loop image loads
-#endif
 #ifndef CAI_EDGE_S2D_PD
 #define CAI_EDGE_S2D_PD 1     // prefetch distance in tiles (1 or 2)
 #endif
@@ -351,7 +348,7 @@ __global__ __launch_bounds__(NT) void edge_s2d_kernel(const EdgeArgs A) {
         __syncthreads();
         const int tn = n, ta = a, tb0 = b0;
         decode(t + PD * TS, n, a, b0);
-        if (!(CAI_EDGE_PROBE & 2)) s_load_b<C>(A, ir, n, a, b0, P);
+        s_load_b<C>(A, ir, n, a, b0, P);
         f32x4 acc[4][NPW];
 #pragma unroll
         for (int m = 0; m < 4; ++m)
@@ -370,7 +367,6 @@ __global__ __launch_bounds__(NT) void edge_s2d_kernel(const EdgeArgs A) {
                 for (int j = 0; j < NPW; ++j) acc[m][j] = mma16<bf16>(bw[ks][j], av, acc[m][j]);
             }
         }
-        if ((CAI_EDGE_PROBE & 1) && A.Hs > 0) return;   // probe: stores skipped at run time, code kept
         const int rowoff = ((tn * A.Hs + ta) * A.Ws + tb0) * A.out_ld;
 #pragma unroll
         for (int m = 0; m < 4; ++m) {

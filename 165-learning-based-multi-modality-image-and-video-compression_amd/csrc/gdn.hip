@@ -1180,12 +1180,6 @@ static int run_gdn_backward(int dtype, const void* x, int32_t x_ld, const void* 
     if (lane) {
         launch_gdn_bwd_lane(x, x_ld, dy, dy_ld, npix, C, gamma_op, beta, inverse, dx, dx_ld, part, nblk, st);
     } else
-#ifdef CAI_GDN_WIDE128
-    if (C == 128) {
-        inverse ? launch_wide(gdn_bwd_wide_kernel<128, true>, WideGeo<128>::NT)
-                : launch_wide(gdn_bwd_wide_kernel<128, false>, WideGeo<128>::NT);
-    } else
-#endif
     if (C == 192)
         inverse ? launch_wide(gdn_bwd_wide_kernel<192, true>, WideGeo<192>::NT)
                 : launch_wide(gdn_bwd_wide_kernel<192, false>, WideGeo<192>::NT);

@@ -35,9 +35,6 @@ namespace {
 #ifndef CAI_GDN_FWD_NSET
 #define CAI_GDN_FWD_NSET 2   // 16-pixel tiles of loads in flight per wave of the C = 128 forward (A/B: 1 measured 3.7 us slower per C2 step, profiles/r03_gdn_fwd_nset_ab.log)
 #endif
-#ifndef CAI_GDN_PF2
-#define CAI_GDN_PF2 0   // A/B: two steps of x / dy loads in flight per norm wave, dbeta summed by MFMA from bf16 u
-#endif
 
 constexpr unsigned LANE_OOB = 0x80000000u;   // beyond every buffer: loads return 0, stores are dropped
 
@@ -227,13 +224,11 @@ __global__ __launch_bounds__(512, 1) void gdn_bwd_lane_kernel(const bf16* __rest
 
     if (norm_role) {
         const __amdgpu_buffer_rsrc_t xr = rsrc(x, npix * x_ld * 2), gr = rsrc(dy, npix * dy_ld * 2);
-#if !CAI_GDN_PF2
         float dbeta[KB][8];
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
             for (int e = 0; e < 8; ++e) dbeta[kb][e] = 0.f;
-#endif
         // one step: consume (rx, rg) = step s; as each chunk retires, that chunk of step `pf` goes out into its
         // registers (pf = the next step, or the one after it with two register sets in flight)
         auto nstep = [&](u32x4 (&rx)[KB], u32x4 (&rg)[KB], int64_t it, int64_t pf) {
@@ -275,9 +270,7 @@ __global__ __launch_bounds__(512, 1) void gdn_bwd_lane_kernel(const bf16* __rest
                             tv = gv_ * rs;
                             uv = -0.5f * gv_ * xf * rs * rs * rs;
                         }
-#if !CAI_GDN_PF2
                         dbeta[kx][e] += uv;
-#endif
                         tt[e] = (bf16)tv;   // t1 rounded to bf16 as in the fused kernel
                         uu[e] = (bf16)uv;
                     }
@@ -296,17 +289,6 @@ __global__ __launch_bounds__(512, 1) void gdn_bwd_lane_kernel(const bf16* __rest
         u32x4 rx[KB], rg[KB];
         chunk_load<KB>(rx, xr, s0 * G::BP + prow, npix, x_ld, g);
         chunk_load<KB>(rg, gr, s0 * G::BP + prow, npix, dy_ld, g);
-#if CAI_GDN_PF2
-        u32x4 rx2[KB], rg2[KB];
-        chunk_load<KB>(rx2, xr, (s0 + stride) * G::BP + prow, npix, x_ld, g);
-        chunk_load<KB>(rg2, gr, (s0 + stride) * G::BP + prow, npix, dy_ld, g);
-        int64_t s = s0, it = 0;
-        for (; it + 1 < mine; it += 2, s += 2 * stride) {
-            nstep(rx, rg, it, s + 2 * stride);
-            nstep(rx2, rg2, it + 1, s + 3 * stride);
-        }
-        if (it < mine) nstep(rx, rg, it, s + 2 * stride);
-#else
         int64_t s = s0;
         for (int64_t it = 0; it < mine; ++it, s += stride) nstep(rx, rg, it, s + stride);
         // dbeta: the 16 pixel lanes of each channel, then the four norm waves in order
@@ -319,7 +301,6 @@ __global__ __launch_bounds__(512, 1) void gdn_bwd_lane_kernel(const bf16* __rest
                 for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
                 if (p == 0) Ldb[d * C + 32 * kb + 8 * g + e] = v;
             }
-#endif
     } else {
         const __amdgpu_buffer_rsrc_t dr = rsrc(dx, npix * dx_ld * 2);
         const int q_ = p >> 2, p4 = p & 3;
@@ -328,12 +309,6 @@ __global__ __launch_bounds__(512, 1) void gdn_bwd_lane_kernel(const bf16* __rest
         for (int i = 0; i < IB; ++i)
 #pragma unroll
             for (int j = 0; j < NB; ++j) dg[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#if CAI_GDN_PF2
-        f32x4 db[IB];   // dbeta rows of this wave: u^T . 1 (every column of the MFMA output holds the sum)
-#pragma unroll
-        for (int i = 0; i < IB; ++i) db[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const u32x4 ones = u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
-#endif
         int64_t s = s0;
         for (int64_t it = 0; it < mine; ++it, s += stride) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -383,9 +358,6 @@ __global__ __launch_bounds__(512, 1) void gdn_bwd_lane_kernel(const bf16* __rest
                         (__attribute__((address_space(3))) s16x4*)(Lu + (rr + 4) * G::RS + col * 2));
                     const s16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
                     afr[i] = __builtin_bit_cast(u32x4, av);
-#if CAI_GDN_PF2
-                    db[i] = mma16<bf16>(afr[i], ones, db[i]);
-#endif
                 }
 #pragma unroll
                 for (int jb = 0; jb < NB; ++jb) {
@@ -411,19 +383,9 @@ __global__ __launch_bounds__(512, 1) void gdn_bwd_lane_kernel(const bf16* __rest
                     const int row = (d * IB + i) * 16 + 4 * g + r, col = jb * 16 + p;
                     pb[(int64_t)row * C + col] = dg[i][jb][r];
                 }
-#if CAI_GDN_PF2
-        if (p == 0) {
-#pragma unroll
-            for (int i = 0; i < IB; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) pb[(int64_t)C * C + (d * IB + i) * 16 + 4 * g + r] = db[i][r];
-        }
-#endif
     }
-#if !CAI_GDN_PF2
     __syncthreads();
     for (int c = threadIdx.x; c < C; c += 512) pb[(int64_t)C * C + c] = ((Ldb[c] + Ldb[C + c]) + Ldb[2 * C + c]) + Ldb[3 * C + c];
-#endif
 }
 
 // ---------------------------------------------------------------------------
