@@ -4102,9 +4102,16 @@ static bool small_wgrad_ok(const cai_conv_geom* g, int dtype) {
         const char* e = getenv("CAI_SMALL_WGRAD_W64");
         return e && *e == '1';
     }();
+    // at most 2^20 weights (A/B knob CAI_SMALL_WGRAD_WMAX = log2 of the bound): cheng2020's 288 -> 1152 k3 at 8x8
+    // (3 M weights, 810 blocks of one K step per wave) ran faster on the pixel-split kernel, both deferred and
+    // batched (C4 676.7 -> 680.4 patches/s, profiles/r05_small_wgrad_wmax_ab.log)
+    static const int wmax = [] {
+        const char* e = getenv("CAI_SMALL_WGRAD_WMAX");
+        return (e && *e) ? atoi(e) : 20;
+    }();
     const int gran = w64 ? 64 : 32;
     return !small_wgrad_off() && dtype == CAI_BF16 && W.M <= small_wgrad_mmax() && W.Ng % gran == 0 &&
-           W.Cq_pad % gran == 0 && (int64_t)W.Ng * W.ncols <= (w64 ? (1 << 20) : (1 << 23));
+           W.Cq_pad % gran == 0 && (int64_t)W.Ng * W.ncols <= ((int64_t)1 << wmax);
 }
 
 
