@@ -156,7 +156,7 @@ class _SideDeferred:
 # ---------------------------------------------------------------------------
 # The weight gradients that land straight in the optimizer's flat buffer (direct_grad) are read by nothing
 # before the optimizer, so their final fixed-order reduces (conv weight-gradient slabs, fused-GDN partials)
-# are queued per stream during the backward pass and run in ONE launch (per 16 jobs) from an autograd final
+# are queued per stream during the backward pass and run in ONE launch (per 32 jobs) from an autograd final
 # callback -- before backward() returns, so .grad reads after backward see the finished values -- instead of
 # one launch after every layer.  The job's workspace is kept alive until that launch.  Bit-identical to the
 # immediate path (same kernel).  Off under the per-launch ledger (it replays single calls) and when a weight
