@@ -2930,7 +2930,8 @@ __global__ __launch_bounds__(512, 1) void wgrad_glds_batch_kernel(const WgBatch 
 // ---------------------------------------------------------------------------
 // R > 1 (G width 64 / R = 32 or 16): a strip is R whole G rows of 64 / R pixels (still 64 consecutive G
 // pixels); each row has its own footprint row image of NCR cells (even / odd planes), rows stacked.
-template <int KS, int S = 2, int R = 1>
+// GR = 192 (192-row tiles): the G strip is three [64 px][64 ch] images of 128-byte rows (swz_sw slots), 24 KB.
+template <int KS, int S = 2, int R = 1, int GR = 128>
 struct WhCfg {
     static constexpr int WR = 64 / R;                 // pixels per strip row
     static constexpr int NCR = S * (WR - 1) + KS;     // footprint cells of one strip row
@@ -2940,11 +2941,12 @@ struct WhCfg {
     static constexpr int XGRP = (XSLOTS + 63) / 64;   // wave-instructions that fill it
     static constexpr int NXI = (XGRP + 7) / 8;        // per thread (8 waves); spare instructions hit a sink
     static constexpr int NST = 4;                     // ring stages (3 strips in flight)
-    static constexpr int GIMG = 64 * 256;             // G strip [64 px][128 ch]; the 4 G images first ...
-    static constexpr int XBASE = NST * GIMG;          // ... then the 4 footprints: every stage offset < 64 KB
+    static constexpr int GIMG = 64 * 2 * GR;          // G strip [64 px][128 ch]; the 4 G images first ...
+    static constexpr int XBASE = NST * GIMG;          // ... then the 4 footprints (GR = 128: every stage offset < 64 KB)
     static constexpr int XSTRIDE = XGRP * 1024 + 1024;   // footprint + a 1 KB sink for the spare DMAs
     static constexpr int BYTES = XBASE + NST * XSTRIDE;
-    static constexpr int NLOAD = 2 + NXI;             // DMA instructions per thread per step
+    static_assert(BYTES <= 160 * 1024, "LDS");
+    static constexpr int NLOAD = (GR == 192 ? 3 : 2) + NXI;   // DMA instructions per thread per step
     static constexpr int CT = KS * 64;                // tile columns
     static constexpr int WCOL = CT / 4;               // columns per column-wave
     static constexpr int TN = WCOL / 16;
@@ -2961,12 +2963,14 @@ __device__ __forceinline__ int opaque(int v) {
 }
 
 // S = 1: the stride-1 k3 p1 Conv2d (cheng2020's 3x3 convs): one footprint plane, tap kw at cell p + kw.
-// TMR: row fragments per wave -- 4 (128-row tiles) or 2 (64-row tiles, for Ng a multiple of 64 but not of 128:
-// cheng2020's 192-channel layers, C2's g_a[6] / g_s[0]; the 128-row tiles left a third of their rows empty)
+// TMR: row fragments per wave -- 4 (128-row tiles), 2 (64-row tiles, for Ng a multiple of 64 but not of 128:
+// C2's g_a[6] / g_s[0]; the 128-row tiles left a third of their rows empty) or 6 (192-row tiles, stride-1 k3 with
+// Ng = 192: cheng2020's 3x3 convs -- X read once per tile and no empty rows, against 64-row tiles' three passes
+// over X and half the MFMA work per step)
 template <int KS, int S, int FLAGS, int R, int TMR>
 __device__ __forceinline__ void wgrad_halo_block(const WgradArgs& a, int wgid, int nwg, char* smem) {
-    static_assert(TMR == 4 || TMR == 2, "128- or 64-row tiles");
-    using W = WhCfg<KS, S, R>;
+    static_assert(TMR == 4 || TMR == 2 || TMR == 6, "128-, 64- or 192-row tiles");
+    using W = WhCfg<KS, S, R, TMR == 6 ? 192 : 128>;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wr = wid >> 2, wc = wid & 3;            // 2 (rows) x 4 (cols) waves
     const int nqc = a.Cq_pad / 64;
@@ -2990,6 +2994,10 @@ __device__ __forceinline__ void wgrad_halo_block(const WgradArgs& a, int wgid, i
     const char* Xp = reinterpret_cast<const char*>(a.x);
     const int gch = r0 + sl * 8;
     const bool gvalid = gch < a.Ng && (TMR == 4 || sl < 8);   // 64-row tiles: the strip's first 64 channels
+    // 192-row tiles: wave w fills rows 8w .. 8w + 7 of each 64-channel image, one instruction per image; a lane's
+    // source slot is the swz_sw slot of its lane-linear LDS position
+    const int grow6 = wid * 8 + (lane >> 3);
+    const int gsl6 = (lane & 7) ^ ((((grow6 >> 1) & 1) << 1) | (((grow6 >> 3) & 1) << 2));
     // X DMA: this lane's footprint piece of each instruction (x offset t, channel byte offset), or the sink
     int xt[W::NXI];
     int xr[W::NXI];                                   // strip row of the piece (R > 1)
@@ -3011,16 +3019,24 @@ __device__ __forceinline__ void wgrad_halo_block(const WgradArgs& a, int wgid, i
     // strip coordinates (column block, row, image) of the next strip to issue: strips are issued in order,
     // so they advance by carries instead of integer divisions per step
     int cib = sbeg % nsr, cj = ((sbeg / nsr) % nrg) * R, cb = (sbeg / nsr) / nrg;
-    const char* gsrc = Gp + ((int64_t)(sbeg * 64 + prow0) * a.g_ld + gch) * 2;   // strips are 64 G pixels
+    const char* gsrc = TMR == 6 ? Gp + ((int64_t)(sbeg * 64 + grow6) * a.g_ld + r0 + gsl6 * 8) * 2
+                                : Gp + ((int64_t)(sbeg * 64 + prow0) * a.g_ld + gch) * 2;   // strips are 64 G pixels
     const int64_t gstep = (int64_t)64 * a.g_ld * 2, ghalf = (int64_t)32 * a.g_ld * 2;
 
     auto issue = [&](int stage) {
         char* gb = smem + stage * W::GIMG;
         char* xb = smem + W::XBASE + stage * W::XSTRIDE;
+        if constexpr (TMR == 6) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-            glds16_asm(gvalid ? (const void*)(gsrc + i * ghalf) : (const void*)cai_zero_page,
-                   gb + wid * 4 * 256 + i * 32 * 256);
+            for (int i = 0; i < 3; ++i)
+                glds16_asm(r0 + i * 64 + gsl6 * 8 < a.Ng ? (const void*)(gsrc + i * 128) : (const void*)cai_zero_page,
+                           gb + i * 8192 + wid * 1024);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                glds16_asm(gvalid ? (const void*)(gsrc + i * ghalf) : (const void*)cai_zero_page,
+                       gb + wid * 4 * 256 + i * 32 * 256);
+        }
         gsrc += gstep;
         const int y = cj * S - a.p + kh;
         const int x0 = cib * (64 * S) - a.p;
@@ -3096,7 +3112,8 @@ __device__ __forceinline__ void wgrad_halo_block(const WgradArgs& a, int wgid, i
             const int colA = wr * (16 * TMR) + tm * 16 + 4 * p4;
 #pragma unroll
             for (int h = 0; h < 2; ++h)
-                aoff[ks][tm][h] = opaque(trswz(rr + 4 * h, colA >> 3) + ((colA & 7) << 1));
+                aoff[ks][tm][h] = opaque(TMR == 6 ? (colA >> 6) * 8192 + swz_sw(rr + 4 * h, (colA & 63) >> 3) + ((colA & 7) << 1)
+                                                  : trswz(rr + 4 * h, colA >> 3) + ((colA & 7) << 1));
         }
     }
 
@@ -3124,7 +3141,7 @@ __device__ __forceinline__ void wgrad_halo_block(const WgradArgs& a, int wgid, i
 #pragma unroll
         for (int tm = 0; tm < TMR; ++tm) {
             if constexpr ((FLAGS & WG_BIAS) != 0) {
-                if (do_bias && tm == wc) {
+                if (do_bias && (tm & 3) == wc) {   // fragment tm's sums: column-wave tm % 4
                     const bf16x8 h = __builtin_bit_cast(bf16x8, fa[tm]);
                     float sacc = 0.f;
 #pragma unroll
@@ -3178,14 +3195,16 @@ __device__ __forceinline__ void wgrad_halo_block(const WgradArgs& a, int wgid, i
         one(std::integral_constant<int, 3>());
     }
     if constexpr ((FLAGS & WG_BIAS) != 0) {
-        if (do_bias && wc < TMR) {   // wave (wr, wc) summed fragment wc of its rows
-            float v = 0.f;
+        if (do_bias) {   // wave (wr, wc) summed fragments wc, wc + 4 of its rows
 #pragma unroll
-            for (int i = 0; i < TMR; ++i) v += bsum[i];
-            v += __shfl_xor(v, 16);
-            v += __shfl_xor(v, 32);
-            const int n = r0 + wr * (16 * TMR) + wc * 16 + lane;
-            if (lane < 16 && n < a.Ng) a.bws[(int64_t)split * a.Ng + n] = v;
+            for (int tm = 0; tm < TMR; ++tm) {
+                if ((tm & 3) != wc) continue;
+                float v = bsum[tm];
+                v += __shfl_xor(v, 16);
+                v += __shfl_xor(v, 32);
+                const int n = r0 + wr * (16 * TMR) + tm * 16 + lane;
+                if (lane < 16 && n < a.Ng) a.bws[(int64_t)split * a.Ng + n] = v;
+            }
         }
     }
     if constexpr ((FLAGS & WG_TBIAS) != 0) {
@@ -3215,13 +3234,13 @@ __device__ __forceinline__ void wgrad_halo_block(const WgradArgs& a, int wgid, i
 
 template <int KS, int S, int FLAGS, int R = 1, int TMR = 4>
 __global__ __launch_bounds__(512, 1) void wgrad_halo_kernel(const WgradArgs a) {
-    __shared__ __attribute__((aligned(16))) char smem[WhCfg<KS, S, R>::BYTES];
+    __shared__ __attribute__((aligned(16))) char smem[WhCfg<KS, S, R, TMR == 6 ? 192 : 128>::BYTES];
     wgrad_halo_block<KS, S, FLAGS, R, TMR>(a, (int)blockIdx.x, (int)gridDim.x, smem);
 }
 
 template <int KS, int S, int FLAGS, int R = 1, int TMR = 4>
 __global__ __launch_bounds__(512, 1) void wgrad_halo_batch_kernel(const WgBatch b) {
-    __shared__ __attribute__((aligned(16))) char smem[WhCfg<KS, S, R>::BYTES];
+    __shared__ __attribute__((aligned(16))) char smem[WhCfg<KS, S, R, TMR == 6 ? 192 : 128>::BYTES];
     const int L = (int)blockIdx.x, j = wg_batch_job(b, L), l = L - b.start[j];
     if (l < b.nwg[j]) wgrad_halo_block<KS, S, FLAGS, R, TMR>(b.job[j], l, b.nwg[j], smem);
 }
@@ -3907,7 +3926,7 @@ struct WgradPlan {
     int tbias, tb_kh0, tb_kw0;   // ConvTranspose2d bias from the X operand's tap set (WG_TBIAS)
     int Sb, nbias;               // bias partial slabs and their length
     int strips_per_split;
-    int hrows;                   // halo kernel: rows (output channels) per tile, 128 or 64
+    int hrows;                   // halo kernel: rows (output channels) per tile, 128, 64 or 192
     bool glds, fused_bias;
     int ct;
     size_t ws_bias;
@@ -4052,6 +4071,15 @@ static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype, bool glds, b
             return e && *e == '1';
         }();
         W.hrows = (!rows128 && W.halo == 5 && W.Ng % 128 != 0 && W.Ng % 64 == 0) ? 64 : 128;
+        // 192-row tiles for the stride-1 k3 kernel at Ng = 192 k (cheng2020's 3x3 convs).  A/B knob
+        // CAI_HALO_WGRAD_ROWS192=0 keeps 128.
+        static const bool rows192 = [] {
+            const char* e = getenv("CAI_HALO_WGRAD_ROWS192");
+            return !(e && *e == '0');
+        }();
+        if (rows192 && !rows128 && W.halo == 3 && g->stride == 1 && halo_wgrad_rows(g) == 1 && W.Ng % 192 == 0 &&
+            W.Ng % 128 != 0)
+            W.hrows = 192;
         W.tiles = W.halo * (W.Cq_pad / 64) * ((W.Ng + W.hrows - 1) / W.hrows);
         int S = std::max(1, wg_blocks() / W.tiles);
         S = (int)std::max<int64_t>(1, std::min<int64_t>(S, nstrip / wg_min_strips()));   // >= 4 strips per split
@@ -4566,7 +4594,8 @@ static void wgrad_split_setup(const cai_conv_geom* g, const WgradPlan& W, WgradA
     if (W.halo) {
         a.nsplit = W.strips_per_split;
         a.rtiles = (W.Ng + W.hrows - 1) / W.hrows;
-        key = (((((W.halo * 10 + g->stride) * 10 + halo_wgrad_rows(g)) << 1) | (W.hrows == 64 ? 1 : 0)) << 4) | bflag;
+        // row mode (bits 4-5): 0 = 128-row tiles, 1 = 64, 2 = 192
+        key = (((((W.halo * 10 + g->stride) * 10 + halo_wgrad_rows(g)) << 2) | (W.hrows == 64 ? 1 : W.hrows == 192 ? 2 : 0)) << 4) | bflag;
     } else {
         key = (1 << 20) | (W.ct << 4) | (in_abs ? WG_ABS : 0) | (in_sq ? WG_SQ : 0) | bflag;
     }
@@ -4594,14 +4623,18 @@ static void launch_wgrad_split(const WgradArgs& a, int key, int nblocks, hipStre
             launch_wgrad_glds<128>(a, nblocks, in_abs, in_sq, bflag, st);
         return;
     }
-    const bool r64 = (key >> 4) & 1;
-    switch (key >> 5) {
+    const int rmode = (key >> 4) & 3;
+    const bool r64 = rmode == 1;
+    switch (key >> 6) {
         case 521: r64 ? launch_wgrad_halo<5, 2, 1, 2>(a, nblocks, f, st) : launch_wgrad_halo<5, 2>(a, nblocks, f, st); break;
         case 522: r64 ? launch_wgrad_halo<5, 2, 2, 2>(a, nblocks, f, st) : launch_wgrad_halo<5, 2, 2>(a, nblocks, f, st); break;
         case 524: r64 ? launch_wgrad_halo<5, 2, 4, 2>(a, nblocks, f, st) : launch_wgrad_halo<5, 2, 4>(a, nblocks, f, st); break;
         case 322: r64 ? launch_wgrad_halo<3, 2, 2, 2>(a, nblocks, f, st) : launch_wgrad_halo<3, 2, 2>(a, nblocks, f, st); break;
         case 324: r64 ? launch_wgrad_halo<3, 2, 4, 2>(a, nblocks, f, st) : launch_wgrad_halo<3, 2, 4>(a, nblocks, f, st); break;
-        case 311: r64 ? launch_wgrad_halo<3, 1, 1, 2>(a, nblocks, f, st) : launch_wgrad_halo<3, 1>(a, nblocks, f, st); break;
+        case 311:
+            if (rmode == 2) launch_wgrad_halo<3, 1, 1, 6>(a, nblocks, f, st);
+            else r64 ? launch_wgrad_halo<3, 1, 1, 2>(a, nblocks, f, st) : launch_wgrad_halo<3, 1>(a, nblocks, f, st);
+            break;
         default: r64 ? launch_wgrad_halo<3, 2, 1, 2>(a, nblocks, f, st) : launch_wgrad_halo<3, 2>(a, nblocks, f, st); break;
     }
 }
@@ -4615,14 +4648,18 @@ static void launch_wgrad_split_batch(const WgBatch& b, int key, hipStream_t st) 
             launch_wgrad_glds_batch<128>(b, f, st);
         return;
     }
-    const bool r64 = (key >> 4) & 1;
-    switch (key >> 5) {
+    const int rmode = (key >> 4) & 3;
+    const bool r64 = rmode == 1;
+    switch (key >> 6) {
         case 521: r64 ? launch_wgrad_halo_batch<5, 2, 1, 2>(b, f, st) : launch_wgrad_halo_batch<5, 2>(b, f, st); break;
         case 522: r64 ? launch_wgrad_halo_batch<5, 2, 2, 2>(b, f, st) : launch_wgrad_halo_batch<5, 2, 2>(b, f, st); break;
         case 524: r64 ? launch_wgrad_halo_batch<5, 2, 4, 2>(b, f, st) : launch_wgrad_halo_batch<5, 2, 4>(b, f, st); break;
         case 322: r64 ? launch_wgrad_halo_batch<3, 2, 2, 2>(b, f, st) : launch_wgrad_halo_batch<3, 2, 2>(b, f, st); break;
         case 324: r64 ? launch_wgrad_halo_batch<3, 2, 4, 2>(b, f, st) : launch_wgrad_halo_batch<3, 2, 4>(b, f, st); break;
-        case 311: r64 ? launch_wgrad_halo_batch<3, 1, 1, 2>(b, f, st) : launch_wgrad_halo_batch<3, 1>(b, f, st); break;
+        case 311:
+            if (rmode == 2) launch_wgrad_halo_batch<3, 1, 1, 6>(b, f, st);
+            else r64 ? launch_wgrad_halo_batch<3, 1, 1, 2>(b, f, st) : launch_wgrad_halo_batch<3, 1>(b, f, st);
+            break;
         default: r64 ? launch_wgrad_halo_batch<3, 2, 1, 2>(b, f, st) : launch_wgrad_halo_batch<3, 2>(b, f, st); break;
     }
 }

@@ -1297,3 +1297,36 @@ def test_halo_wgrad_64_row_tiles(cuda, kind, B, cin, cout, H, k, s):
         F.conv_transpose2d(xr, wr, br, stride=s, padding=k // 2, output_padding=s - 1).backward(gy.bfloat16().float())
     assert relerr(mod.weight.grad, wr.grad) < 1e-2, relerr(mod.weight.grad, wr.grad)
     assert relerr(mod.bias.grad, br.grad) < 1e-2, relerr(mod.bias.grad, br.grad)
+
+
+@pytest.mark.parametrize("B,cin,cout,H,bias", [
+    (2, 192, 192, 128, True),    # cheng2020's 3x3 convs at 128x128
+    (2, 192, 576, 64, True),     # three 192-row tiles
+    (2, 128, 192, 64, True),     # 128 input channels (two 64-channel column blocks per tap)
+    (2, 192, 192, 64, False),    # no bias partials
+], ids=["128px", "ng576", "cq128", "nobias"])
+def test_halo_wgrad_192_row_tiles(cuda, B, cin, cout, H, bias):
+    """The stride-1 k3 halo weight gradient with 192-row tiles (Ng a multiple of 192 but not of 128: one tile holds
+    all of cheng2020's 192 output channels; the G strip staged as three 64-channel LDS images) against torch fp32 on
+    the same bf16-rounded operands: weight and bias gradients within 1e-2 (relative max)."""
+    import ctypes
+
+    from compressai import _native as native
+    from compressai.layers import Conv2d
+
+    torch.manual_seed(H + cin + cout)
+    raw = native.lib.load()
+    mod = Conv2d(cin, cout, 3, stride=1, padding=1, bias=bias).to(cuda)
+    g = native.ConvGeom(B, cin, H, H, cout, H, H, 3, 1, 1, 0, 0)
+    assert raw.cai_conv_kernel_name(ctypes.byref(g), native.BF16, 2, 0).decode() == "wgrad_halo_kernel<3,s1>"
+    x = torch.randn(B, cin, H, H, device=cuda).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(B, cout, H, H, device=cuda)
+    with _autocast(True):
+        y = mod(x)
+    y.backward(gy)
+    wr = mod.weight.detach().bfloat16().float().requires_grad_()
+    br = mod.bias.detach().clone().requires_grad_() if bias else None
+    F.conv2d(x.detach().bfloat16().float(), wr, br, stride=1, padding=1).backward(gy.bfloat16().float())
+    assert relerr(mod.weight.grad, wr.grad) < 1e-2, relerr(mod.weight.grad, wr.grad)
+    if bias:
+        assert relerr(mod.bias.grad, br.grad) < 1e-2, relerr(mod.bias.grad, br.grad)
