@@ -3628,12 +3628,24 @@ static bool halo_s1_off() {
 // conv_glds_kernel (192->192 64x64: 43 vs 38 us, 32x32: 31 vs 24 us; 128x128: 58 vs 73 us fwd, 71 vs 94 dgrad),
 // and with > 64 output channels: 64-channel outputs fill half the 128-channel tile (multimodal 64->64 at
 // 512x640 input gradient 200 vs 157 us on conv_glds_kernel<256x64>)
+// Also taken with >= 64 tiles when the input is wide (Cin_pad >= CAI_HALO_S1_SPLIT_CIN, default 512; 0 = off): K
+// splits at least four ways into chunks as long as a 192-channel layer's whole K, so the split blocks run the
+// forward's per-block work (cheng2020's sub-pixel conv 192 -> 768 at 64x64, B = 4: its input gradient, K = 6912,
+// ran 256 blocks of conv_glds_kernel<64x192> at 102 us)
+static int halo_s1_split_cin() {
+    static const int v = [] {
+        const char* e = getenv("CAI_HALO_S1_SPLIT_CIN");
+        return (e && *e) ? atoi(e) : 512;
+    }();
+    return v;
+}
 static bool halo_s1_ok(const cai_conv_geom* g, const Plan& P, bool glds, bool wide) {
     const int bn = halo_bn(P.kout_c);
     const int64_t tiles = (int64_t)g->batch * ((P.OWg[0] + 31) / 32) * ((P.OHg[0] + 7) / 8) * ((P.kout_c + bn - 1) / bn);
+    const bool split_wide = halo_s1_split_cin() > 0 && P.Cin_pad >= halo_s1_split_cin() && tiles >= 64;
     return glds && !halo_off() && !halo_s1_off() && g->stride == 1 && g->kernel == 3 && g->pad == 1 &&
            P.nphase == 1 && P.ntaps[0] == 9 && P.Cin_pad % 64 == 0 && (bn == 128 || wide) && P.OHg[0] >= 8 &&
-           P.OWg[0] >= 32 && tiles >= 128 && P.kout_c > 64;
+           P.OWg[0] >= 32 && (tiles >= 128 || split_wide) && P.kout_c > 64;
 }
 
 

@@ -143,6 +143,8 @@ def test_halo_kernel_selection(native):
     assert name(G(4, 192, 128, 128, 192, 128, 128, 3, 1, 1, 0, 0), 0) == "conv_halo_s1_kernel<192>"
     assert name(G(4, 192, 128, 128, 192, 128, 128, 3, 1, 1, 0, 0), 1) == "conv_halo_s1_kernel<192>"
     assert name(G(4, 192, 64, 64, 768, 64, 64, 3, 1, 1, 0, 0), 0) == "conv_halo_s1_kernel<192>"
+    # its input gradient (768 -> 192, 64 tiles): K split four ways on the halo kernel
+    assert name(G(4, 192, 64, 64, 768, 64, 64, 3, 1, 1, 0, 0), 1) == "conv_halo_s1_kernel<192>"
     assert name(G(4, 128, 64, 128, 96, 64, 128, 3, 1, 1, 0, 0), 0) == "conv_halo_s1_kernel<128>"
     assert name(G(4, 128, 64, 64, 256, 64, 64, 3, 1, 1, 0, 0), 0) == "conv_halo_s1_kernel<128>"
     assert name(G(4, 96, 64, 128, 128, 64, 128, 3, 1, 1, 0, 0), 0) != "conv_halo_s1_kernel<128>"   # Cin % 64

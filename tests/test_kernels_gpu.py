@@ -1299,6 +1299,30 @@ def test_halo_wgrad_64_row_tiles(cuda, kind, B, cin, cout, H, k, s):
     assert relerr(mod.bias.grad, br.grad) < 1e-2, relerr(mod.bias.grad, br.grad)
 
 
+def test_halo_s1_split_k_input_gradient(cuda):
+    """cheng2020's sub-pixel conv 192 -> 768 (k3 s1) at 64x64, B = 4: its input gradient (a 768 -> 192 conv on 64
+    halo tiles) on conv_halo_s1_kernel<192> with K split four ways + the split-K reduce, against torch fp32 on the
+    same bf16-rounded operands (relative max 1e-2)."""
+    import ctypes
+
+    from compressai import _native as native
+    from compressai.layers import Conv2d
+
+    torch.manual_seed(5)
+    raw = native.lib.load()
+    g = native.ConvGeom(4, 192, 64, 64, 768, 64, 64, 3, 1, 1, 0, 0)
+    assert raw.cai_conv_kernel_name(ctypes.byref(g), native.BF16, 1, 0).decode() == "conv_halo_s1_kernel<192>"
+    mod = Conv2d(192, 768, 3, stride=1, padding=1).to(cuda)
+    x = torch.randn(4, 192, 64, 64, device=cuda).contiguous(memory_format=torch.channels_last).requires_grad_()
+    gy = torch.randn(4, 768, 64, 64, device=cuda)
+    with _autocast(True):
+        y = mod(x)
+    y.backward(gy)
+    xr = x.detach().bfloat16().float().requires_grad_()
+    F.conv2d(xr, mod.weight.detach().bfloat16().float(), None, padding=1).backward(gy.bfloat16().float())
+    assert relerr(x.grad.float(), xr.grad) < 1e-2, relerr(x.grad.float(), xr.grad)
+
+
 @pytest.mark.parametrize("B,cin,cout,H,bias", [
     (2, 192, 192, 128, True),    # cheng2020's 3x3 convs at 128x128
     (2, 192, 576, 64, True),     # three 192-row tiles
