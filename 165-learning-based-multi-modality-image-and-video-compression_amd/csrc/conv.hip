@@ -4093,7 +4093,11 @@ static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype, bool glds, b
             W.Ng % 128 != 0)
             W.hrows = 192;
         W.tiles = W.halo * (W.Cq_pad / 64) * ((W.Ng + W.hrows - 1) / W.hrows);
-        int S = std::max(1, wg_blocks() / W.tiles);
+        // 192-row tiles: half the 256-block target by default (CAI_WG_BLOCKS_R192) -- the same pixel splits as the
+        // 128-row tiles had, so the fp32 slab the reduce reads back does not double (cheng2020's 192-channel layers:
+        // 9 tiles, 14 splits of 18.6 MB instead of 28 of 37 MB)
+        static const int blocks192 = env_int("CAI_WG_BLOCKS_R192", 128);
+        int S = std::max(1, (W.hrows == 192 ? blocks192 : wg_blocks()) / W.tiles);
         S = (int)std::max<int64_t>(1, std::min<int64_t>(S, nstrip / wg_min_strips()));   // >= 4 strips per split
         W.strips_per_split = (int)((nstrip + S - 1) / S);
         W.S = (int)((nstrip + W.strips_per_split - 1) / W.strips_per_split);
