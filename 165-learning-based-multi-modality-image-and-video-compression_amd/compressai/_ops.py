@@ -1540,6 +1540,9 @@ class GaussianFn(torch.autograd.Function):
         ctx.give = _fan_role(x, "give")
         ctx.cfg = (mode, scale_bound, lik_bound, xld, sld, mld, nld, npix, C, x.shape, x.dtype, scales.shape,
                    scales.dtype, means is not None)
+        # scales / means as ChunkFn's halves of one [pixels][2C] buffer: their gradients go to one such buffer too
+        ctx.paired = (means is not None and scales.dim() == 4 and sld == 2 * C and mld == 2 * C
+                      and means.data_ptr() == scales.data_ptr() + C * scales.element_size())
         return q, lik
 
     @staticmethod
@@ -1554,14 +1557,21 @@ class GaussianFn(torch.autograd.Function):
         if gq is not None:
             gq_r, gqld = as_rows(gq)[:2]
         dx, dxb = empty_rows_like(xshape, xdtype, xr.device)
-        ds, dsb = empty_rows_like(sshape, sdtype, xr.device)
-        dm, dmb = empty_rows_like(sshape, sdtype, xr.device) if has_m else (None, None)
+        dld = C
+        if ctx.paired:    # both gradients in one [pixels][2C] buffer: ChunkFn's backward hands it back whole
+            pair, _ = empty_rows_like((sshape[0], 2 * C, *sshape[2:]), sdtype, xr.device)
+            ds = dsb = pair[:, :C]
+            dm = dmb = pair[:, C:]
+            dld = 2 * C
+        else:
+            ds, dsb = empty_rows_like(sshape, sdtype, xr.device)
+            dm, dmb = empty_rows_like(sshape, sdtype, xr.device) if has_m else (None, None)
         n_el = npix * C
         es_x, es_s = xr.element_size(), sr.element_size()
         _ledger.run(lambda: lib.cai_gc_bwd(mode, npix, C, _p(xr), dcode(xdtype), xld, _p(sr), sld, _p(mr), mld,
                                            dcode(sdtype), nsrc, sb, lb, _p(gl), glld, _p(gq_r),
                                            dcode(gq_r.dtype) if gq_r is not None else F32, gqld, _p(dxb), C, _p(dsb),
-                                           C, _p(dmb), C, _stream()),
+                                           dld, _p(dmb), dld, _stream()),
                     "gc_bwd", "gc_bwd_kernel", 0,
                     n_el * (2 * es_x + (4 if mr is not None else 2) * es_s + (4 if nr is not None else 0)
                             + (4 if gl is not None else 0) + (es_x if gq_r is not None else 0)),
@@ -2049,6 +2059,37 @@ class CatFn(torch.autograd.Function):
             outs.append(g[:, off:off + c])
             off += c
         return tuple(outs)
+
+
+class ChunkFn(torch.autograd.Function):
+    """t.chunk(2, 1) for the entropy parameters' (scales, means) pair (models/google.py): channel views forward.
+    Backward: when GaussianFn wrote both gradients into one [pixels][2C] buffer (the pair's halves, adjacent), that
+    buffer IS t's gradient -- handed back as it is, no concatenation; otherwise the halves are copied natively into
+    one pixel-major buffer (torch's chunk backward is an ATen cat)."""
+
+    @staticmethod
+    def forward(ctx, t):
+        C = t.shape[1] // 2
+        ctx.cfg = (C, tuple(t.shape))
+        return t[:, :C], t[:, C:]
+
+    @staticmethod
+    def backward(ctx, gs, gm):
+        C, shape = ctx.cfg
+        if (gs is not None and gm is not None and gs.dtype == gm.dtype and gs.stride() == gm.stride()
+                and pixel_major_ld(gs) == 2 * C and gm.data_ptr() == gs.data_ptr() + C * gs.element_size()):
+            return gs.as_strided(shape, gs.stride())
+        ref = gs if gs is not None else gm
+        dt = ref.dtype
+        B, _, H, W = shape
+        out = empty_pm(B, 2 * C, H, W, dt, ref.device, ld=2 * C)
+        for k, g in enumerate((gs, gm)):
+            if g is None:
+                g = torch.zeros((B, C, H, W), dtype=dt, device=ref.device)
+            gp, gld = to_pm(g.to(dt), dt, _vec(dt))
+            dst = _VP(out.data_ptr() + k * C * out.element_size())
+            lib.cai_act(dcode(dt), _p(gp), gld, dst, 2 * C, B * H * W, C, ACT_NONE, 0.0, _stream())
+        return out
 
 
 class LayerNormFn(torch.autograd.Function):

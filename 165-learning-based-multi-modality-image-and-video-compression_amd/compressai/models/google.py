@@ -41,7 +41,7 @@ from ..entropy_models import EntropyBottleneck, GaussianConditional
 from ..entropy_models.entropy_models import _QuantizeFn, _draw_noise, _noise_for
 from .._native import Q_DEQUANTIZE, Q_NOISE
 from ..layers import GDN, MaskedConv2d, Sequential
-from .._ops import CatFn, ConvFn, ConvSpec, fan_out
+from .._ops import CatFn, ChunkFn, ConvFn, ConvSpec, fan_out
 from .._prepack import prepacked_forward
 from ..ans import BufferedRansEncoder, RansDecoder
 from ..layers.conv import Conv2d
@@ -327,7 +327,7 @@ class MeanScaleHyperprior(ScaleHyperprior):
             y_ha, y_gc = fan_out(y)
             z = self.h_a(y_ha)
             z_hat, z_likelihoods = self.entropy_bottleneck(z)
-            scales_hat, means_hat = self.h_s(z_hat).chunk(2, 1)
+            scales_hat, means_hat = ChunkFn.apply(self.h_s(z_hat))
             y_hat, y_likelihoods = self.gaussian_conditional(y_gc, scales_hat, means=means_hat)
             x_hat = self.g_s(y_hat)
             return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods, "z": z_likelihoods}}
@@ -337,7 +337,7 @@ class MeanScaleHyperprior(ScaleHyperprior):
         with torch.cuda.stream(side):
             z = self.h_a(y)
             z_hat, z_likelihoods = self.entropy_bottleneck(z, noise=z_noise)
-            scales_hat, means_hat = self.h_s(z_hat).chunk(2, 1)
+            scales_hat, means_hat = ChunkFn.apply(self.h_s(z_hat))
         y_hat, noise = _quantize_y(y, True)         # noise mode ignores the means
         ready = torch.cuda.Event()
         ready.record(main)
@@ -357,7 +357,7 @@ class MeanScaleHyperprior(ScaleHyperprior):
             z = self.h_a(y)
             z_strings = self.entropy_bottleneck.compress(z)
             z_hat = self.entropy_bottleneck.decompress(z_strings, z.size()[-2:])
-            scales_hat, means_hat = self.h_s(z_hat).chunk(2, 1)
+            scales_hat, means_hat = ChunkFn.apply(self.h_s(z_hat))
             indexes = self.gaussian_conditional.build_indexes(scales_hat)
             y_strings = self.gaussian_conditional.compress(y, indexes, means=means_hat)
         return {"strings": [y_strings, z_strings], "shape": z.size()[-2:]}
@@ -368,7 +368,7 @@ class MeanScaleHyperprior(ScaleHyperprior):
         assert isinstance(strings, list) and len(strings) == 2
         with prepacked_forward(self):
             z_hat = self.entropy_bottleneck.decompress(strings[1], shape)
-            scales_hat, means_hat = self.h_s(z_hat).chunk(2, 1)
+            scales_hat, means_hat = ChunkFn.apply(self.h_s(z_hat))
             indexes = self.gaussian_conditional.build_indexes(scales_hat)
             y_hat = self.gaussian_conditional.decompress(strings[0], indexes, means=means_hat)
             x_hat = self.g_s(y_hat).clamp_(0, 1)
@@ -390,7 +390,7 @@ class _ARCoding:
             _ARCoding._AR_SPEC = ConvSpec(5, 1, 0)
         cp = self.context_prediction
         ctx_p = ConvFn.apply(y_crop, cp.weight, cp.bias, _ARCoding._AR_SPEC)
-        return self.entropy_parameters(CatFn.apply(p, ctx_p)).chunk(2, 1)
+        return ChunkFn.apply(self.entropy_parameters(CatFn.apply(p, ctx_p)))
 
     def _gc_tables(self):
         gc = self.gaussian_conditional
@@ -484,8 +484,8 @@ class JointAutoregressiveHierarchicalPriors(_ARCoding, MeanScaleHyperprior):
             y_hat = self.gaussian_conditional.quantize(y_q, "noise" if self.training else "dequantize")
             y_ctx, y_gs = fan_out(y_hat, absorb=False)
             ctx_params = self.context_prediction(y_ctx)
-            gaussian_params = self.entropy_parameters(torch.cat((params, ctx_params), dim=1))
-            scales_hat, means_hat = gaussian_params.chunk(2, 1)
+            gaussian_params = self.entropy_parameters(CatFn.apply(params, ctx_params))
+            scales_hat, means_hat = ChunkFn.apply(gaussian_params)
             _, y_likelihoods = self.gaussian_conditional(y_gc, scales_hat, means=means_hat)
             x_hat = self.g_s(y_gs)
             return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods, "z": z_likelihoods}}
@@ -507,8 +507,8 @@ class JointAutoregressiveHierarchicalPriors(_ARCoding, MeanScaleHyperprior):
         with torch.cuda.stream(side):
             side.wait_event(ready)
             ctx_params = self.context_prediction(y_ctx)
-            gaussian_params = self.entropy_parameters(torch.cat((params, ctx_params), dim=1))
-            scales_hat, means_hat = gaussian_params.chunk(2, 1)
+            gaussian_params = self.entropy_parameters(CatFn.apply(params, ctx_params))
+            scales_hat, means_hat = ChunkFn.apply(gaussian_params)
             _, y_likelihoods = self.gaussian_conditional(y_gc, scales_hat, means=means_hat, noise=noise2)
         main.wait_stream(side)
         y_hat.record_stream(side)
