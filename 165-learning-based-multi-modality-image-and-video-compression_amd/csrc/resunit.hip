@@ -81,16 +81,6 @@ __device__ __forceinline__ u32x4 keep_pos(u32x4 v, u32x4 m) {   // v where m > 0
     return __builtin_bit_cast(u32x4, vv);
 }
 
-#ifdef CAI_RU_PROBE
-// diagnostic builds only (tools/quick_variant.sh ... -DCAI_RU_PROBE, tools/ru_probe.py): per-block wall-clock stamps
-// (100 MHz) of the last launch of each direction -- start, staged, phase A done, taps done, epilogue B done, phase C
-// MFMAs done, end
-__device__ unsigned long long ru_probe[2][4096][8];
-#define RU_STAMP(k) tp[k] = __builtin_amdgcn_s_memrealtime()
-#else
-#define RU_STAMP(k)
-#endif
-
 template <int NC, bool BWD>
 __global__ __launch_bounds__(512, 1) void resunit_kernel(const RuArgs a) {
     using R = RuCfg<NC>;
@@ -106,10 +96,6 @@ __global__ __launch_bounds__(512, 1) void resunit_kernel(const RuArgs a) {
     char* const sH2 = sWC + R::WC;
 
     const int tid = threadIdx.x, lane = tid & 63;
-#ifdef CAI_RU_PROBE
-    unsigned long long tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#endif
-    RU_STAMP(0);
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int l16 = lane & 15, lg = lane >> 4;
     const int per_img = a.tiles_x * a.tiles_y;
@@ -151,7 +137,6 @@ __global__ __launch_bounds__(512, 1) void resunit_kernel(const RuArgs a) {
     wait_vmcnt_n(nwc);      // this wave's phase A weights landed (only its phase C DMAs may be in flight)
     wait_lgkmcnt0();
     __builtin_amdgcn_s_barrier();
-    RU_STAMP(1);
 
     // ---- phase A: [112 halo px x N] . [N x N/2]; wave (mg, nh): M tiles mg, mg + 4; N tiles nh * NJA .. ----
     const int mg = wave & 3, nh = wave >> 2;
@@ -228,7 +213,6 @@ __global__ __launch_bounds__(512, 1) void resunit_kernel(const RuArgs a) {
     }
     wait_lgkmcnt0();
     __builtin_amdgcn_s_barrier();      // the halo image is complete; phase A's operands are dead (ring may refill)
-    RU_STAMP(2);
 
     // ---- phase B: 3x3 over the halo image, tap weights through the DMA ring ----
     constexpr int FB = NTA * KB;       // weight fragments per tap
@@ -268,7 +252,6 @@ __global__ __launch_bounds__(512, 1) void resunit_kernel(const RuArgs a) {
             }
         }
     }
-    RU_STAMP(3);
     // epilogue B: lane = output pixel (orow, ocol) of the tile
     const int oy = y0 + orow, ox = x0 + ocol;
     const bool oin = oy < a.H && ox < a.W;
@@ -302,7 +285,6 @@ __global__ __launch_bounds__(512, 1) void resunit_kernel(const RuArgs a) {
     }
     wait_lgkmcnt0();
     __builtin_amdgcn_s_barrier();      // (the last tap's wait drained every DMA, phase C's weights included)
-    RU_STAMP(4);
 
     // ---- phase C: [64 px x N/2] . [N/2 x N] + residual ----
     f32x4 accc[NJC];
@@ -318,7 +300,6 @@ __global__ __launch_bounds__(512, 1) void resunit_kernel(const RuArgs a) {
             accc[j] = mma16<bf16>(fb, fa, accc[j]);
         }
     }
-    RU_STAMP(5);
     if (!oin) return;
     // every load of the epilogue before its first store (see epilogue A)
     bf16x4 xrC[NJC], ymC[NJC], r2C[NJC], xmC[NJC];
@@ -368,15 +349,6 @@ __global__ __launch_bounds__(512, 1) void resunit_kernel(const RuArgs a) {
         }
         *reinterpret_cast<bf16x4*>(a.out + op * a.out_ld + c0) = ov;
     }
-#ifdef CAI_RU_PROBE
-    RU_STAMP(6);
-    if (tid < 7) {   // lane-dependent values: vector stores
-        unsigned long long v = tp[0];
-#pragma unroll
-        for (int k = 1; k < 7; ++k) v = tid == k ? tp[k] : v;
-        ru_probe[BWD][blockIdx.x & 4095][tid] = v;
-    }
-#endif
 }
 
 
@@ -848,11 +820,3 @@ extern "C" int cai_resunit_wgrad_batch(const cai_resunit_wgrad_args* args, void*
     return CAI_OK;
 }
 
-#ifdef CAI_RU_PROBE
-// diagnostic builds only: copy the stamps of direction `bwd` (nblk blocks x 8) to host memory
-extern "C" int cai_ru_probe_read(int32_t bwd, unsigned long long* out, int32_t nblk) {
-    if (nblk > 4096 || bwd < 0 || bwd > 1) return -1;
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(cai::ru_probe), sizeof(unsigned long long) * 8 * nblk,
-                                    sizeof(unsigned long long) * 8 * 4096 * bwd, hipMemcpyDeviceToHost);
-}
-#endif

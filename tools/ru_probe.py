@@ -1,6 +1,8 @@
-"""Phase timing of the fused ResidualUnit kernel from a diagnostic build (tools/quick_variant.sh ruprobe resunit.hip
--DCAI_RU_PROBE; run with CAI_LIB=<that lib> CAI_AB_STREAM=0): one AttentionBlock(192) step at B=4 per map size, then
-the per-block stamps of the last launch of each direction -- median / max of every phase in microseconds.
+"""Phase timing of the fused ResidualUnit kernel from a diagnostic build: the stamps (RU_STAMP, cai_ru_probe_read)
+are not in the product source -- re-apply commit 53c4b80's csrc/resunit.hip hunks, build with
+tools/quick_variant.sh ruprobe resunit.hip -DCAI_RU_PROBE and run with CAI_LIB=<that lib> CAI_AB_STREAM=0.  One
+AttentionBlock(192) step at B=4 per map size, then the per-block stamps of the last launch of each direction --
+median / max of every phase in microseconds (profiles/r05_resunit_phase_probe.log).
 usage: python tools/ru_probe.py"""
 import ctypes
 import os
