@@ -104,7 +104,10 @@ class OverlappedAllReduce:
 
     Cut tensors accumulate over the grad-enabled forwards of a step (micro-batches summed into one loss) and
     are released by ``finish()``; a plain ``loss.backward()`` outside the phases (no exchange) releases the
-    ones it differentiated through, so they never leak into the next step.
+    ones it differentiated through, so they never leak into the next step.  The cuts of a grad-enabled
+    forward the step's loss does not depend on (one computed for logging, never backpropagated) are dropped
+    by ``backward_head`` (a reachability walk from the loss, only when more than one forward marked a cut).
+    Cut lists must come in backward order (``optim.check_tail_cuts``).
 
     Memory: each phase keeps the graph (retain_graph) because the later phases still need the tail's saved
     tensors; they are released when the caller drops its loss tensor (bench.py's step drops it on return) --
@@ -124,6 +127,7 @@ class OverlappedAllReduce:
         self.side = torch.cuda.Stream(device=flat_grad.device) if flat_grad.is_cuda else None
         self._cuts = [[] for _ in range(max(1, len(self.buckets) - 1))]   # cut tensors of each tail phase
         self._in_phase = False
+        self._nfwd = 0                  # grad-enabled forwards that marked cut 0 since the last step
         self._model = None
         self._handles = []
         self._slots = []
@@ -148,11 +152,11 @@ class OverlappedAllReduce:
     def for_model(cls, model: torch.nn.Module, opt):
         """The exchange of `model` over FusedAdam `opt` built by configure_optimizers(model,
         tail=model.dp_tail, tail_cuts=model.dp_tail_cuts); a buffer built without the cuts gets two buckets."""
-        from .optim import dp_stage
+        from .optim import check_tail_cuts, dp_stage
 
         tail = tuple(model.dp_tail)
         bounds = list(getattr(opt, "bucket_bounds", [0, opt.tail_offset, opt.numel]))
-        cuts = tuple(getattr(model, "dp_tail_cuts", ())) if len(bounds) > 3 else ()
+        cuts = check_tail_cuts(getattr(model, "dp_tail_cuts", ())) if len(bounds) > 3 else ()
         main = [(n, p) for n, p in model.named_parameters() if not n.endswith(".quantiles")]
         head = [p for n, p in main if dp_stage(n, tail, cuts) == 0]
         stages = [[p for n, p in main if dp_stage(n, tail, cuts) == s] for s in range(1, len(cuts) + 2)]
@@ -169,6 +173,8 @@ class OverlappedAllReduce:
         # boundary nodes: a phase's capture of a cut tensor's gradient may execute its grad_fn, which for
         # the product convs writes parameter gradients as a side effect; an identity node in between has none
         out = tuple(_Boundary.apply(t) for t in ts)
+        if k == 0:
+            self._nfwd += 1
         for t in out:
             # a backward outside the phases (a plain loss.backward()) releases the cut (by id: a reference in the
             # hook would keep the tensor, and with it its graph, alive until the cycle collector runs)
@@ -179,7 +185,25 @@ class OverlappedAllReduce:
     def _release(self, k, tid):
         if not self._in_phase:
             self._cuts[k] = [c for c in self._cuts[k] if id(c) != tid]
+            if k == 0 and not self._cuts[0]:
+                self._nfwd = 0
         return None
+
+    def _prune(self, loss: torch.Tensor):
+        """Drop the cut tensors of grad-enabled forwards this loss does not depend on (a forward computed for
+        logging and never backpropagated): they would keep their graphs alive for the step and be passed to
+        the phases as inputs.  Only needed when more than one forward marked its cut since the last step."""
+        if self._nfwd <= 1:
+            return
+        seen, stack = set(), [loss.grad_fn]
+        while stack:
+            n = stack.pop()
+            if n is None or n in seen:
+                continue
+            seen.add(n)
+            stack.extend(f for f, _ in n.next_functions)
+        self._cuts = [[t for t in c if t.grad_fn in seen] for c in self._cuts]
+        self._nfwd = 1
 
     def _backward(self, roots, grads, inputs):
         self._in_phase = True
@@ -189,6 +213,7 @@ class OverlappedAllReduce:
             self._in_phase = False
 
     def backward_head(self, loss: torch.Tensor):
+        self._prune(loss)
         if not self._cuts[0]:
             raise RuntimeError("OverlappedAllReduce: the forward did not reach the cut")
         from ._ops import loss_seed
@@ -232,6 +257,7 @@ class OverlappedAllReduce:
         if self.side is not None:
             torch.cuda.current_stream().wait_stream(self.side)
         self._cuts = [[] for _ in self._cuts]
+        self._nfwd = 0
 
     def remove(self):
         for h in self._handles:

@@ -239,6 +239,24 @@ def parameter_groups(net):
     return main, aux
 
 
+def check_tail_cuts(cuts: Tuple[str, ...]) -> Tuple[str, ...]:
+    """Cuts must be listed in the order the backward reaches them: cuts of one parent in strictly
+    descending child index ("g_a.4", "g_a.2").  OverlappedAllReduce.backward_phase(i) stops at cuts[i]; an
+    ascending list would run phase 1 through the lower cut and leave the later phases nothing to propagate
+    (silently zero gradients), so it is rejected."""
+    cuts = tuple(cuts)
+    last = {}
+    for c in cuts:
+        parent, sep, idx = c.rpartition(".")
+        if not sep or not idx.isdigit():
+            raise ValueError(f"tail cut {c!r}: expected '<parent>.<child index>'")
+        if parent in last and int(idx) >= last[parent]:
+            raise ValueError(f"tail cuts {cuts}: cuts of {parent!r} must be listed in strictly descending child "
+                             f"order (the order the backward reaches them); {c!r} follows {parent}.{last[parent]}")
+        last[parent] = int(idx)
+    return cuts
+
+
 def dp_stage(name: str, tail: Tuple[str, ...], cuts: Tuple[str, ...] = ()) -> int:
     """Gradient bucket of parameter `name` (compressai.distributed.OverlappedAllReduce): 0 outside the tail;
     in the tail 1 + the number of `cuts` ("g_a.4": the input of child 4 of the tail Sequential g_a) the
@@ -266,6 +284,7 @@ def configure_optimizers(net, lr: float = 1e-4, aux_lr: float = 1e-3, tail: Tupl
     zero_grad_in_step: see FusedAdam (both optimizers)."""
     named = dict(net.named_parameters())
     main, aux = parameter_groups(net)
+    tail_cuts = check_tail_cuts(tail_cuts)
     stage = [dp_stage(n, tail, tail_cuts) for n in main]
     nst = 1 + len(tail_cuts) + 1 if tail else 1
     layout = [i for s in range(nst) for i, t in enumerate(stage) if t == s]

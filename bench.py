@@ -481,6 +481,7 @@ def main():
     if not math.isfinite(loss):
         raise RuntimeError(f"non-finite loss {loss}")
     ms_per_step = dt / args.steps * 1e3
+    peak_gb = torch.cuda.max_memory_allocated(dev) / 1e9   # the timed steps' (and their graphs') peak
 
     roof = step_roof = dom_class = None
     if rank == 0 and not args.no_profile:
@@ -512,7 +513,7 @@ def main():
                                          f"pieces), bucket i overlapped with backward phase i+1; exposed: the last "
                                          f"({4 * sync.buckets[-1].numel() / 1e6:.2f} MB)" if sync else
                                          "1 all-reduce after backward") if world > 1 else None},
-            "final_loss": round(loss, 5),
+            "final_loss": round(loss, 5), "max_memory_allocated_gb": round(peak_gb, 3),
             "roofline": roof, "dominant_class": dom_class, "step_roofline": step_roof, "cpu_baseline": cpu,
         }
         if cpu:

@@ -255,11 +255,13 @@ int cai_conv_wgrad_deferred(const cai_conv_geom* g, int dtype,
                             float* dw, float* db, int32_t accumulate,
                             void* workspace, size_t ws_bytes, void* stream, cai_reduce_job* job);
 int cai_reduce_jobs(const cai_reduce_job* jobs, int32_t n, void* stream);
-/* n weight-gradient calls, each as cai_conv_wgrad_deferred makes it (jobs[i]: call i's reduce job), with the
- * latent-size ones (the wgrad_small_kernel path, cai_conv_kernel_name(direction 2) == "wgrad_small_kernel")
- * batched: one launch per input transform for up to 16 such calls (two calls that write one bias gradient
- * go to separate launches, in call order); the others run one by one.  Replaces a backward's per-layer
- * launches of the latent layers' weight gradients, deferred to its end (compressai/_ops.py conv_wgrad).
+/* n weight-gradient calls, each as cai_conv_wgrad_deferred makes it (jobs[i]: call i's reduce job), grouped
+ * into batched launches: the latent-size ones (the wgrad_small_kernel path, cai_conv_kernel_name(direction 2)
+ * == "wgrad_small_kernel") one launch per input transform, and the pixel-split ones (wgrad_glds_kernel<128 /
+ * 256>, wgrad_halo_kernel variants) one launch per kernel variant, up to 16 (WG_BATCH_MAX) calls per launch;
+ * two calls that write one bias gradient go to separate launches, in call order, and a pixel-split call whose
+ * bias gradient is not fused into its kernel runs on its own.  Replaces a backward's per-layer launches of
+ * those weight gradients, deferred to its end (compressai/_ops.py conv_wgrad).
  * Operands as cai_conv_wgrad_deferred; every call's buffers must stay valid until its reduce job has run. */
 typedef struct cai_wgrad_call {
     cai_conv_geom geom;

@@ -183,3 +183,71 @@ def test_bucketed_phases_world2(tmp_path, micro):
     for r in range(world):
         for i, d in enumerate(res[r]["done"]):
             assert torch.allclose(d, res[r]["ref_local"][b[i]:b[i + 1]], rtol=1e-5, atol=1e-7), (r, i)
+
+
+def _toy_sync(net):
+    from compressai.distributed import OverlappedAllReduce
+    from compressai.optim import dp_stage, parameter_groups
+
+    main, _ = parameter_groups(net)
+    named = dict(net.named_parameters())
+    stage = [dp_stage(n, net.dp_tail, net.dp_tail_cuts) for n in main]
+    order = [i for s in range(4) for i, t in enumerate(stage) if t == s]
+    sizes = [named[main[i]].numel() for i in order]
+    offs = [sum(sizes[:k]) for k in range(len(sizes))]
+    bounds = [0] + [min([o for o, i in zip(offs, order) if stage[i] >= s] or [sum(sizes)]) for s in (1, 2, 3)]
+    bounds.append(sum(sizes))
+    flat = torch.zeros(sum(sizes))
+    for o, i, n in zip(offs, order, sizes):
+        named[main[i]].grad = flat[o:o + n].view_as(named[main[i]])
+    head = [named[main[i]] for i in order if stage[i] == 0]
+    stages = [[named[main[i]] for i in order if stage[i] == s] for s in (1, 2, 3)]
+    sync = OverlappedAllReduce(flat, bounds, net, head, [net.get_submodule(c) for c in net.dp_tail_cuts], stages)
+    return sync, flat, [named[main[i]] for i in order]
+
+
+def test_forward_without_backward_is_pruned():
+    """a grad-enabled forward that is never backpropagated (a logging forward) must not keep its
+    cuts (and graph) for the step, nor feed them to the phases: the phased gradient equals the plain one."""
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "165-learning-based-multi-modality-image-and-video-compression_amd"))
+    torch.manual_seed(0)
+    net = _toy_model()
+    sync, flat, params = _toy_sync(net)
+    x = torch.rand(2, 3, 16, 16, generator=torch.Generator().manual_seed(1))
+    ref = torch.cat([g.flatten() for g in torch.autograd.grad(net(x), params)])
+    sync._cuts = [[] for _ in sync._cuts]
+    sync._nfwd = 0
+    flat.zero_()
+    _ = net(torch.rand(2, 3, 16, 16))          # logging forward, no backward
+    loss = net(x)
+    assert [len(c) for c in sync._cuts] == [2, 2, 2]
+    sync.backward_head(loss)
+    assert [len(c) for c in sync._cuts] == [1, 1, 1]
+    for i in range(1, sync.nphases):
+        sync.backward_phase(i)
+    sync.finish()
+    assert torch.allclose(flat, ref, rtol=1e-5, atol=1e-7)
+    sync.remove()
+
+
+def test_tail_cuts_must_descend():
+    """cuts of one parent listed in ascending order would leave the lower buckets zero; rejected."""
+    import sys
+
+    import pytest
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "165-learning-based-multi-modality-image-and-video-compression_amd"))
+    from compressai.optim import check_tail_cuts, configure_optimizers
+
+    assert check_tail_cuts(("g_a.4", "g_a.2")) == ("g_a.4", "g_a.2")
+    assert check_tail_cuts(("g_a.5", "g_a.2", "g_a.1", "h.3")) == ("g_a.5", "g_a.2", "g_a.1", "h.3")
+    for bad in (("g_a.2", "g_a.4"), ("g_a.2", "g_a.2"), ("g_a",)):
+        with pytest.raises(ValueError):
+            check_tail_cuts(bad)
+    net = _toy_model()
+    with pytest.raises(ValueError):
+        configure_optimizers(net, tail=("g_a.",), tail_cuts=("g_a.2", "g_a.4"))

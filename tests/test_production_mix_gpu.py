@@ -496,3 +496,8 @@ def test_step_launches_no_aten_kernels(cuda, name, quality, batch, only):
     assert len(names) > 20, names               # the profiler saw the step's kernels
     aten = [n for n in names if ("at::" in n or "aten::" in n) and (only is None or any(o in n for o in only))]
     assert not aten, aten
+    if only is None:
+        # nor runtime copies / fills (HIP's blit kernels: __amd_rocclr_copyBuffer / fillBuffer, which carry no
+        # ATen name; the profiler lists them as Memcpy / Memset)
+        blits = [n for n in names if any(k in n for k in ("Memcpy", "Memset", "copyBuffer", "fillBuffer"))]
+        assert not blits, blits
