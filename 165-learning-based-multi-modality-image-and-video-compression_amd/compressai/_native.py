@@ -129,6 +129,7 @@ SIGNATURES = {
     "cai_conv_wgrad_deferred": (_I, [_G, _I, _P, c_int32, c_int32, c_int32, _P, c_int32, _P, _P, c_int32, _P, _S, _P,
                                      POINTER(ReduceJob)]),
     "cai_reduce_jobs": (_I, [POINTER(ReduceJob), c_int32, _P]),
+    "cai_reduce_jobs_grid": (_I, [POINTER(ReduceJob), c_int32, c_int32, _P]),
     "cai_conv_wgrad_batch": (_I, [POINTER(WgradCall), c_int32, _P, POINTER(ReduceJob)]),
     "cai_resunit_wgrad_batch": (_I, [POINTER(ResunitWgradArgs), POINTER(c_void_p), POINTER(c_size_t), c_int32, _P,
                                     POINTER(ReduceJob)]),

@@ -29,7 +29,7 @@ import torch
 from . import _ledger
 from ._native import (ACT_LEAKY, ACT_NONE, ACT_RELU, BF16, F32, MASK_BEFORE_RES, MASK_LEAKY, MASK_NONE, MASK_POS,
                       Q_DEQUANTIZE, Q_NOISE,
-                      JOB_NONE, NOISE_BUF, NOISE_DRAW, NOISE_REPLAY, ConvGeom, EbGrads, EbParams, NoiseSrc, RdGrads,
+                      JOB_EDGE, JOB_GDN, JOB_NONE, JOB_WGRAD, NOISE_BUF, NOISE_DRAW, NOISE_REPLAY, ConvGeom, EbGrads, EbParams, NoiseSrc, RdGrads,
                       RdInputs, ReduceJob, ResunitArgs, ResunitWgradArgs, WgradCall, lib)
 
 _VP = ctypes.c_void_p
@@ -163,12 +163,55 @@ class _SideDeferred:
 # gradient runs on the side stream.  CAI_DEFER_REDUCE=0 turns it off (A/B).
 _DEFER_REDUCE = os.environ.get("CAI_DEFER_REDUCE", "1") == "1"
 _REDUCE_SPLIT = os.environ.get("CAI_REDUCE_SPLIT", "0") == "1"   # diagnostics: one launch per deferred job
-_JOBS = {}          # (device, graph task id) -> [jobs, streams, keep-alive tensors, wgrad calls, device, unit calls]
+_JOBS = {}          # (device, graph task id) -> [jobs, streams, keep-alive tensors, wgrad calls, device, unit calls,
+                    #                            early-reduce stream, bytes queued since the last early reduce]
 # The latent layers' weight gradients (wgrad_small_kernel: <= 1024 G pixels) are deferred the same way, as whole
 # calls: the flush runs them in one launch (cai_conv_wgrad_batch) ahead of the reduce launch, instead of one
 # launch per layer in the backward's chain; so are the ResidualUnits' weight gradients (cai_resunit_wgrad_batch: one
 # launch for a backward's units).  CAI_WGRAD_BATCH=0 launches both in place (A/B).
 _WGRAD_BATCH = os.environ.get("CAI_WGRAD_BATCH", "1") == "1"
+# Early reduces: once the queued jobs' partials pass CAI_EARLY_REDUCE_MB, they are reduced on a per-device side
+# stream (forked from the backward's stream after their partial kernels) while the backward goes on -- the
+# loss-side layers' slabs (C2: g_s's weight-gradient slabs and GDN partials, ~150 MB) under the latent chain's
+# small launches -- and the final flush joins that stream before its own launch.  Safe because a gradient with a
+# deferred job has no immediate writer in the same backward (every direct-grad path defers); two jobs that write
+# one gradient stay ordered (the side stream's launches in queue order, the final flush after the join).  0 = off.
+_EARLY_BYTES = float(os.environ.get("CAI_EARLY_REDUCE_MB", "0")) * 1e6
+_EARLY_BLOCKS = int(os.environ.get("CAI_EARLY_REDUCE_BLOCKS", "0"))   # grid cap of the early launches (0: none)
+_EARLY_MAX = int(os.environ.get("CAI_EARLY_REDUCE_MAX", "1"))          # early launches per backward
+_RSIDE = {}
+
+
+def _job_bytes(j) -> float:
+    """Partial bytes a reduce job reads (its slab / per-block partials)."""
+    if j.kind == JOB_WGRAD:
+        return 4.0 * j.i[0] * j.i[1] * j.i[2]
+    if j.kind == JOB_GDN:
+        return 4.0 * j.i[0] * (j.i[1] * j.i[1] + j.i[1])
+    if j.kind == JOB_EDGE:
+        return 4.0 * j.i[1] * (9 * 16 * j.i[0] + 16)
+    return 0.0
+
+
+def _early_flush(pend):
+    """Reduce the jobs queued so far on the side stream (after every stream their partial kernels ran on)."""
+    dev = pend[4]
+    side = _RSIDE.get(dev)
+    if side is None:
+        side = _RSIDE[dev] = torch.cuda.Stream(device=dev)
+    cur = torch.cuda.current_stream(dev)
+    side.wait_stream(cur)
+    for s in {s.cuda_stream: s for s in pend[1]}.values():
+        if s.cuda_stream != cur.cuda_stream:
+            side.wait_stream(s)
+    jobs = pend[0]
+    arr = (ReduceJob * len(jobs))(*jobs)
+    lib.cai_reduce_jobs_grid(arr, len(jobs), _EARLY_BLOCKS, _VP(side.cuda_stream))
+    for t in pend[2]:
+        t.record_stream(side)
+    pend[0] = []
+    pend[6] = side
+    pend[7] = 0.0
 
 
 def _flush_jobs(key):
@@ -176,11 +219,15 @@ def _flush_jobs(key):
     DDP's finalize uses it), after it has waited for every other stream a job's partial kernel ran on (the
     hyper branch's side stream: inside a captured graph this is the join edge)."""
     pend = _JOBS.pop(key, None)
-    if not pend or not (pend[0] or pend[3] or pend[5]):
+    if not pend:
         return
     dev = key[0]
-    jobs, streams, keep, calls = pend[:4]
     cur = torch.cuda.current_stream(dev)
+    if pend[6] is not None:
+        cur.wait_stream(pend[6])        # join the early reduces
+    if not (pend[0] or pend[3] or pend[5]):
+        return
+    jobs, streams, keep, calls = pend[:4]
     for s in {s.cuda_stream: s for s in streams}.values():
         if s.cuda_stream != cur.cuda_stream:
             cur.wait_stream(s)
@@ -232,6 +279,11 @@ def defer_job(job: "ReduceJob", device: torch.device, *keep: torch.Tensor):
     pend[0].append(job)
     pend[1].append(torch.cuda.current_stream(pend[4]))
     pend[2].extend(t for t in keep if t is not None)
+    if _EARLY_BYTES > 0 and pend[8] < _EARLY_MAX:
+        pend[7] += _job_bytes(job)
+        if pend[7] >= _EARLY_BYTES:
+            _early_flush(pend)
+            pend[8] += 1
 
 
 def _pending(device: torch.device):
@@ -239,7 +291,9 @@ def _pending(device: torch.device):
     key = (dev, torch._C._current_graph_task_id())
     pend = _JOBS.get(key)
     if pend is None:
-        pend = _JOBS[key] = [[], [], [], [], dev, []]
+        # [jobs, streams, keep-alive tensors, wgrad calls, device, unit calls, early-reduce stream, queued bytes,
+        #  early launches so far]
+        pend = _JOBS[key] = [[], [], [], [], dev, [], None, 0.0, 0]
         torch.autograd.Variable._execution_engine.queue_callback(lambda: _flush_jobs(key))
     return pend
 

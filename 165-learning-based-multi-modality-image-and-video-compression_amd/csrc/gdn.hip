@@ -948,9 +948,24 @@ __global__ __launch_bounds__(WideGeo<C>::NT, 1) void gdn_bwd_wide_kernel(const b
         }
 }
 
+// Blocks of the fused / lane backward.  Each block writes one (C*C + C) fp32 partial (66 KB at C = 128) that the
+// reduce job reads back: at 64 pixels per block a 32 x 32 x 16 layer's 256 partials (16.9 MB) outweigh its x / dy /
+// dx (12.6 MB).  CAI_GDN_BWD_MIN_PX (A/B knob, 0 = off) caps the blocks at ceil(npix / MIN_PX).
+static int64_t gdn_bwd_min_px() {
+    static const int64_t v = [] {
+        const char* e = getenv("CAI_GDN_BWD_MIN_PX");
+        return (int64_t)((e && *e) ? std::max(0, atoi(e)) : 0);
+    }();
+    return v;
+}
+static int gdn_bwd_cap(int64_t npix, int64_t blocks) {
+    const int64_t m = gdn_bwd_min_px();
+    if (m > 0) blocks = std::min<int64_t>(blocks, (npix + m - 1) / m);
+    return (int)std::max<int64_t>(1, blocks);
+}
 static int fused_blocks(int64_t npix) {
     const int64_t tiles = (npix + GBM - 1) / GBM;
-    return (int)std::max<int64_t>(1, std::min<int64_t>(256, tiles));
+    return gdn_bwd_cap(npix, std::min<int64_t>(256, tiles));
 }
 
 __global__ void gdn_reparam_kernel(const float* __restrict__ beta_raw, const float* __restrict__ gamma_raw, int C,
@@ -1165,7 +1180,7 @@ static int run_gdn_backward(int dtype, const void* x, int32_t x_ld, const void* 
     }
     const bool lane = gdn_lane_on() && gdn_lane_bwd_ok(C, npix, x_ld, dy_ld, dx_ld);
     // (the lane kernel's block count never exceeds fused_blocks: the workspace size holds for both)
-    const int nblk = lane ? gdn_lane_bwd_blocks(npix) : fused_blocks(npix);
+    const int nblk = lane ? gdn_bwd_cap(npix, gdn_lane_bwd_blocks(npix)) : fused_blocks(npix);
     float* part = reinterpret_cast<float*>(workspace);
     auto launch = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(nblk), dim3(FNT), 0, st, reinterpret_cast<const bf16*>(x), x_ld,

@@ -222,7 +222,7 @@ extern "C" {
 
 const char* cai_last_error(void) { return g_err; }
 int cai_version(void) { return 1; }
-int cai_abi_count(void) { return 91; }
+int cai_abi_count(void) { return 92; }
 
 int cai_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float eps,
              float* step, const float* sqnorm, float max_norm, void* stream) {

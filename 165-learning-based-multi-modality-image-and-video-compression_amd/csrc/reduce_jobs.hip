@@ -249,14 +249,9 @@ __device__ __forceinline__ void edge_reduce_body(const cai_reduce_job& J, int bi
     if (dst >= 0) dw[dst] = accumulate ? dw[dst] + s : s;
 }
 
-__global__ __launch_bounds__(256) void reduce_jobs_kernel(const ReduceBatch B) {
-    __shared__ f32x4 red[16][17];
-    __shared__ __attribute__((aligned(16))) float tr[WG_TR_FLOATS];
-    __shared__ float ered[16][16];
-    __shared__ float etot[16];
-    // the job owning this block (block-uniform linear scan over <= CAI_REDUCE_BATCH entries)
-    const int b = blockIdx.x;
-    int j = 0;
+__device__ __forceinline__ void reduce_block(const ReduceBatch& B, int b, int& j, f32x4 (*red)[17], float* tr,
+                                             float (*ered)[16], float* etot) {
+    // the job owning block b (block-uniform linear scan over <= CAI_REDUCE_BATCH entries, from job j on)
     while (j + 1 < B.n && b >= B.start[j + 1]) ++j;
     const cai_reduce_job& J = B.jobs[j];
     const int bid = b - B.start[j];
@@ -266,6 +261,25 @@ __global__ __launch_bounds__(256) void reduce_jobs_kernel(const ReduceBatch B) {
         gdn_reduce_body(J, bid, red);
     else if (J.kind == CAI_JOB_EDGE)
         edge_reduce_body(J, bid, ered, etot);
+}
+
+// LOOP: a capped grid walks the batch's blocks in order (cai_reduce_jobs_grid: a reduce that runs beside other
+// work on a side stream holds at most that many CUs' worth of blocks); each block's arithmetic is the same
+template <bool LOOP>
+__global__ __launch_bounds__(256) void reduce_jobs_kernel(const ReduceBatch B) {
+    __shared__ f32x4 red[16][17];
+    __shared__ __attribute__((aligned(16))) float tr[WG_TR_FLOATS];
+    __shared__ float ered[16][16];
+    __shared__ float etot[16];
+    int j = 0;
+    if constexpr (!LOOP) {
+        reduce_block(B, (int)blockIdx.x, j, red, tr, ered, etot);
+    } else {
+        for (int b = (int)blockIdx.x; b < B.total; b += (int)gridDim.x) {
+            __syncthreads();    // the previous block's LDS readers are done
+            reduce_block(B, b, j, red, tr, ered, etot);
+        }
+    }
 }
 
 // The gradient buffers a job writes (read-modify-write when it accumulates).
@@ -300,7 +314,7 @@ static bool shares_dest(const ReduceBatch& B, const cai_reduce_job& J) {
 // write the same gradient (a module called twice in one forward, e.g. Channel_aligner's shared trunk,
 // models/master.py:293-304: the second job accumulates onto the first) never share a launch -- the batch is
 // closed before the second and it runs in the next launch, after the first on the stream.
-int launch_reduce_jobs(const cai_reduce_job* jobs, int n, hipStream_t st) {
+int launch_reduce_jobs(const cai_reduce_job* jobs, int n, hipStream_t st, int max_grid) {
     for (int j0 = 0; j0 < n;) {
         ReduceBatch B{};
         int blocks = 0;
@@ -316,7 +330,11 @@ int launch_reduce_jobs(const cai_reduce_job* jobs, int n, hipStream_t st) {
             ++B.n;
         }
         if (B.n == 0) continue;
-        hipLaunchKernelGGL(reduce_jobs_kernel, dim3((unsigned)blocks), dim3(256), 0, st, B);
+        B.total = blocks;
+        if (max_grid > 0 && blocks > max_grid)
+            hipLaunchKernelGGL(reduce_jobs_kernel<true>, dim3((unsigned)max_grid), dim3(256), 0, st, B);
+        else
+            hipLaunchKernelGGL(reduce_jobs_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, B);
         CAI_LAUNCH_CHECK("reduce_jobs");
     }
     return CAI_OK;
@@ -326,5 +344,10 @@ int launch_reduce_jobs(const cai_reduce_job* jobs, int n, hipStream_t st) {
 
 extern "C" int cai_reduce_jobs(const cai_reduce_job* jobs, int32_t n, void* stream) {
     CAI_CHECK_ARG(n >= 0 && (n == 0 || jobs), "reduce_jobs: bad arguments");
-    return cai::launch_reduce_jobs(jobs, n, cai::as_stream(stream));
+    return cai::launch_reduce_jobs(jobs, n, cai::as_stream(stream), 0);
+}
+
+extern "C" int cai_reduce_jobs_grid(const cai_reduce_job* jobs, int32_t n, int32_t max_blocks, void* stream) {
+    CAI_CHECK_ARG(n >= 0 && (n == 0 || jobs) && max_blocks >= 0, "reduce_jobs_grid: bad arguments");
+    return cai::launch_reduce_jobs(jobs, n, cai::as_stream(stream), max_blocks);
 }

@@ -14,6 +14,7 @@ constexpr int CAI_REDUCE_BATCH = CAI_REDUCE_BATCH_MAX;
 
 struct ReduceBatch {
     int n;
+    int total;                         // blocks of the batch (the capped-grid kernel walks them)
     int start[CAI_REDUCE_BATCH];       // first block of each job
     cai_reduce_job jobs[CAI_REDUCE_BATCH];
 };
@@ -23,6 +24,6 @@ static_assert(sizeof(ReduceBatch) <= 4096, "kernel argument block");
 int wgrad_job_blocks(int Ng, int Cq_pad, int k, int nbias_blocks);
 
 // run `n` jobs (CAI_JOB_NONE entries skipped) in ceil(n / CAI_REDUCE_BATCH) launches
-int launch_reduce_jobs(const cai_reduce_job* jobs, int n, hipStream_t st);
+int launch_reduce_jobs(const cai_reduce_job* jobs, int n, hipStream_t st, int max_grid = 0);
 
 }  // namespace cai

@@ -255,6 +255,10 @@ int cai_conv_wgrad_deferred(const cai_conv_geom* g, int dtype,
                             float* dw, float* db, int32_t accumulate,
                             void* workspace, size_t ws_bytes, void* stream, cai_reduce_job* job);
 int cai_reduce_jobs(const cai_reduce_job* jobs, int32_t n, void* stream);
+/* cai_reduce_jobs with the grid capped at max_blocks (0 = uncapped): each block walks the batch's blocks in order,
+ * same arithmetic per output (bit-identical).  For a reduce launched on a side stream beside the backward's chain
+ * (compressai/_ops.py early reduces), so it holds a bounded share of the CUs. */
+int cai_reduce_jobs_grid(const cai_reduce_job* jobs, int32_t n, int32_t max_blocks, void* stream);
 /* n weight-gradient calls, each as cai_conv_wgrad_deferred makes it (jobs[i]: call i's reduce job), grouped
  * into batched launches: the latent-size ones (the wgrad_small_kernel path, cai_conv_kernel_name(direction 2)
  * == "wgrad_small_kernel") one launch per input transform, and the pixel-split ones (wgrad_glds_kernel<128 /
