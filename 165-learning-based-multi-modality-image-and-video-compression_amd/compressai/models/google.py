@@ -113,13 +113,84 @@ class CompressionModel(nn.Module):
     # is conv(3, N) + GDN: 26 K parameters at N = 128)
     dp_tail = ("g_a.",)
     dp_tail_cuts = ("g_a.4", "g_a.2")
+    # dp_phases(): the head split too -- g_s first (its gradients are final first: the loss reaches x_hat
+    # before anything else), in pieces at the inputs of dp_gs_cuts (children of g_s, outermost first), then the
+    # entropy path: dp_head_splits, each (param prefixes, the cut it stops at besides y), then what is left
+    dp_split_head = False     # the forward marks gs_in / the likelihoods (google.py, waseda.py models)
+    dp_gs_cuts = ()
+    dp_head_splits = ()
     _dp_cut_fn = None
+    _dp_mark_fn = None
+
+    def _dp_mark(self, name, *ts):
+        """Identity, unless a bucketed exchange is attached (compressai.distributed.OverlappedAllReduce): then
+        boundary nodes at this named point of the graph (a cut of its phase plan)."""
+        if self._dp_mark_fn is not None:
+            ts = self._dp_mark_fn(name, *ts)
+        return ts[0] if len(ts) == 1 else ts
 
     def _dp_cut(self, *ts):
-        """Identity, unless a two-bucket exchange is attached: then boundary nodes for its two-phase backward."""
-        if self._dp_cut_fn is not None:
+        """The cut between the head and the tail (dp_tail): y = g_a(x) for the zoo models."""
+        if self._dp_cut_fn is not None:      # an exchange built from dp_tail / dp_tail_cuts alone
             ts = self._dp_cut_fn(*ts)
-        return ts[0] if len(ts) == 1 else ts
+            return ts[0] if len(ts) == 1 else ts
+        return self._dp_mark("y", *ts)
+
+    # the cuts the synthesis / entropy path marks in forward (dp_phases): g_s's input, each likelihood tensor
+    _dp_synth = "g_s"
+    _dp_synth_in = "gs_in"
+    _dp_liks = ("lik_y", "lik_z")
+
+    def dp_phases(self):
+        """The bucketed gradient exchange's backward phases, in backward order (compressai.distributed,
+        configure_optimizers(phases=...)): (parameter-name prefixes of the phase's bucket (None: all the rest),
+        root cuts, input cuts).  Synthesis pieces first, then the entropy path (dp_head_splits), then the tail
+        (dp_tail) in the pieces dp_tail_cuts makes."""
+        from ..optim import check_tail_cuts
+
+        if not self.dp_split_head:      # a forward that marks only y: one head bucket
+            return [(None, ["loss"], ["y"])] + self._dp_tail_phases()
+        syn = self._dp_synth
+        gs_cuts = check_tail_cuts(self.dp_gs_cuts)
+        liks = list(self._dp_liks)
+        ph = []
+        prev, hi = ["loss"], len(self.get_submodule(syn))
+        for c in gs_cuts:                                   # g_s[k:] pieces, outermost first
+            k = int(c.rsplit(".", 1)[1])
+            ph.append(([f"{syn}.{j}." for j in range(k, hi)], prev, [c] + (liks if prev == ["loss"] else [])))
+            prev, hi = [c], k
+        ph.append(([f"{syn}.{j}." for j in range(hi)], prev,
+                   [self._dp_synth_in] + (liks if prev == ["loss"] else [])))
+        roots = [self._dp_synth_in] + liks[:1]
+        pending = liks[1:]
+        for prefixes, cut in self.dp_head_splits:           # e.g. the context / entropy-parameter stack
+            # it stops at its cut AND at "yq" -- y as its other consumers (quantize, GaussianConditional)
+            # read it -- not at y itself: the hyper path below the cut also leads to y, and an input reachable
+            # from another input of one phase would pull that path into the phase
+            ph.append((list(prefixes), roots, [cut, "yq"]))
+            roots = [cut] + pending
+            pending = []
+        ph.append((None, roots + pending, ["y"]))           # the rest of the head
+        return ph + self._dp_tail_phases(["y", "yq"] if self.dp_head_splits else ["y"])
+
+    def _dp_tail_phases(self, first_roots=("y",)):
+        """The tail (dp_tail) in the pieces dp_tail_cuts makes, from y (and the cuts still holding y's other
+        gradients) down to the input."""
+        from ..optim import check_tail_cuts
+
+        ph = []
+        tail_cuts = check_tail_cuts(self.dp_tail_cuts)
+        prev = list(first_roots)
+        parent = None
+        hi = None
+        for c in tail_cuts:
+            parent, idx = c.rsplit(".", 1)
+            hi = len(self.get_submodule(parent)) if hi is None else hi
+            ph.append(([f"{parent}.{j}." for j in range(int(idx), hi)], prev, [c]))
+            prev, hi = [c], int(idx)
+        last = [f"{parent}.{j}." for j in range(hi)] if tail_cuts else list(self.dp_tail)
+        ph.append((last, prev, []))
+        return ph
 
     def __init__(self, entropy_bottleneck_channels, init_weights=None):
         super().__init__()
@@ -181,6 +252,9 @@ def _synthesis(channel, N, M):
 
 
 class FactorizedPrior(CompressionModel):
+    # gradient buckets (dp_phases): g_s, the EntropyBottleneck, then g_a in pieces
+    dp_split_head = True
+    _dp_liks = ("lik_y",)
     def __init__(self, N, M, channel=3, **kwargs):
         super().__init__(entropy_bottleneck_channels=M, **kwargs)
         self.g_a = _analysis(channel, N, M)
@@ -195,8 +269,8 @@ class FactorizedPrior(CompressionModel):
     def forward(self, x):
         y = self._dp_cut(self.g_a(x))
         y_hat, y_likelihoods = self.entropy_bottleneck(y)
-        x_hat = self.g_s(y_hat)
-        return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods}}
+        x_hat = self.g_s(self._dp_mark("gs_in", y_hat))
+        return {"x_hat": x_hat, "likelihoods": {"y": self._dp_mark("lik_y", y_likelihoods)}}
 
     @classmethod
     def from_state_dict(cls, state_dict, channel=3):
@@ -223,6 +297,8 @@ class FactorizedPrior(CompressionModel):
 
 
 class ScaleHyperprior(CompressionModel):
+    # gradient buckets (dp_phases): g_s, the hyper path (h_a, h_s, EntropyBottleneck), then g_a in pieces
+    dp_split_head = True
     def __init__(self, N, M, channel=3, **kwargs):
         super().__init__(entropy_bottleneck_channels=N, **kwargs)
         self.g_a = _analysis(channel, N, M)
@@ -248,8 +324,9 @@ class ScaleHyperprior(CompressionModel):
             z_hat, z_likelihoods = self.entropy_bottleneck(z)
             scales_hat = self.h_s(z_hat)
             y_hat, y_likelihoods = self.gaussian_conditional(y_gc, scales_hat)
-            x_hat = self.g_s(y_hat)
-            return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods, "z": z_likelihoods}}
+            x_hat = self.g_s(self._dp_mark("gs_in", y_hat))
+            return {"x_hat": x_hat, "likelihoods": {"y": self._dp_mark("lik_y", y_likelihoods),
+                                                    "z": self._dp_mark("lik_z", z_likelihoods)}}
         main = torch.cuda.current_stream()
         z_noise = _z_noise(self, y)
         side.wait_stream(main)
@@ -260,13 +337,14 @@ class ScaleHyperprior(CompressionModel):
         y_hat, noise = _quantize_y(y, self.training)
         ready = torch.cuda.Event()
         ready.record(main)
-        x_hat = self.g_s(y_hat)
+        x_hat = self.g_s(self._dp_mark("gs_in", y_hat))
         with torch.cuda.stream(side):
             side.wait_event(ready)
             _, y_likelihoods = self.gaussian_conditional(y, scales_hat, noise=noise)
         main.wait_stream(side)
         _cross(main, side, y, noise, (z_likelihoods, y_likelihoods), z_noise)
-        return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods, "z": z_likelihoods}}
+        return {"x_hat": x_hat, "likelihoods": {"y": self._dp_mark("lik_y", y_likelihoods),
+                                                "z": self._dp_mark("lik_z", z_likelihoods)}}
 
     def load_state_dict(self, state_dict, strict: bool = True):
         update_registered_buffers(self.gaussian_conditional, "gaussian_conditional",
@@ -329,8 +407,9 @@ class MeanScaleHyperprior(ScaleHyperprior):
             z_hat, z_likelihoods = self.entropy_bottleneck(z)
             scales_hat, means_hat = ChunkFn.apply(self.h_s(z_hat))
             y_hat, y_likelihoods = self.gaussian_conditional(y_gc, scales_hat, means=means_hat)
-            x_hat = self.g_s(y_hat)
-            return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods, "z": z_likelihoods}}
+            x_hat = self.g_s(self._dp_mark("gs_in", y_hat))
+            return {"x_hat": x_hat, "likelihoods": {"y": self._dp_mark("lik_y", y_likelihoods),
+                                                    "z": self._dp_mark("lik_z", z_likelihoods)}}
         main = torch.cuda.current_stream()
         z_noise = _z_noise(self, y)
         side.wait_stream(main)
@@ -341,13 +420,14 @@ class MeanScaleHyperprior(ScaleHyperprior):
         y_hat, noise = _quantize_y(y, True)         # noise mode ignores the means
         ready = torch.cuda.Event()
         ready.record(main)
-        x_hat = self.g_s(y_hat)
+        x_hat = self.g_s(self._dp_mark("gs_in", y_hat))
         with torch.cuda.stream(side):
             side.wait_event(ready)
             _, y_likelihoods = self.gaussian_conditional(y, scales_hat, means=means_hat, noise=noise)
         main.wait_stream(side)
         _cross(main, side, y, noise, (z_likelihoods, y_likelihoods), z_noise)
-        return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods, "z": z_likelihoods}}
+        return {"x_hat": x_hat, "likelihoods": {"y": self._dp_mark("lik_y", y_likelihoods),
+                                                "z": self._dp_mark("lik_z", z_likelihoods)}}
 
     @torch.no_grad()
     def compress(self, x):
@@ -465,6 +545,9 @@ class _ARCoding:
 
 
 class JointAutoregressiveHierarchicalPriors(_ARCoding, MeanScaleHyperprior):
+    # gradient buckets (dp_phases): g_s (pieces: dp_gs_cuts), the context model + entropy parameters (their
+    # gradients are final once the backward reaches h_s's output, cut "params"), the hyper path, then g_a
+    dp_head_splits = ((("entropy_parameters.", "context_prediction."), "params"),)
     def __init__(self, N=192, M=192, channel=3, **kwargs):
         super().__init__(N=N, M=M, channel=channel, **kwargs)
         self.entropy_parameters = Sequential(
@@ -478,32 +561,35 @@ class JointAutoregressiveHierarchicalPriors(_ARCoding, MeanScaleHyperprior):
         side = _side_stream(y, True)
         if side is None:
             y_ha, y_q, y_gc = fan_out(y, 3, absorb=False)
+            y_q, y_gc = self._dp_mark("yq", y_q, y_gc)   # y as quantize / the GaussianConditional read it
             z = self.h_a(y_ha)
             z_hat, z_likelihoods = self.entropy_bottleneck(z)
-            params = self.h_s(z_hat)
+            params = self._dp_mark("params", self.h_s(z_hat))
             y_hat = self.gaussian_conditional.quantize(y_q, "noise" if self.training else "dequantize")
             y_ctx, y_gs = fan_out(y_hat, absorb=False)
             ctx_params = self.context_prediction(y_ctx)
             gaussian_params = self.entropy_parameters(CatFn.apply(params, ctx_params))
             scales_hat, means_hat = ChunkFn.apply(gaussian_params)
             _, y_likelihoods = self.gaussian_conditional(y_gc, scales_hat, means=means_hat)
-            x_hat = self.g_s(y_gs)
-            return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods, "z": z_likelihoods}}
+            x_hat = self.g_s(self._dp_mark("gs_in", y_gs))
+            return {"x_hat": x_hat, "likelihoods": {"y": self._dp_mark("lik_y", y_likelihoods),
+                                                    "z": self._dp_mark("lik_z", z_likelihoods)}}
         main = torch.cuda.current_stream()
         z_noise = _z_noise(self, y)
         y_ha, y_q, y_gc = fan_out(y, 3, absorb=False)   # y's three gradients: native adds, not ATen's
+        y_q, y_gc = self._dp_mark("yq", y_q, y_gc)
         side.wait_stream(main)
         with torch.cuda.stream(side):
             z = self.h_a(y_ha)
             z_hat, z_likelihoods = self.entropy_bottleneck(z, noise=z_noise)
-            params = self.h_s(z_hat)
+            params = self._dp_mark("params", self.h_s(z_hat))
         # the reference's draws in its order (z, then y_hat's, then the likelihood's)
         y_hat, noise = _quantize_y(y_q, self.training)
         noise2 = _draw_noise(y) if self.training else None
         y_gs, y_ctx = fan_out(y_hat, absorb=False)
         ready = torch.cuda.Event()
         ready.record(main)
-        x_hat = self.g_s(y_gs)
+        x_hat = self.g_s(self._dp_mark("gs_in", y_gs))
         with torch.cuda.stream(side):
             side.wait_event(ready)
             ctx_params = self.context_prediction(y_ctx)
@@ -515,7 +601,8 @@ class JointAutoregressiveHierarchicalPriors(_ARCoding, MeanScaleHyperprior):
         if noise2 is not None:
             noise2.record_stream(side)
         _cross(main, side, y, noise, (z_likelihoods, y_likelihoods), z_noise)
-        return {"x_hat": x_hat, "likelihoods": {"y": y_likelihoods, "z": z_likelihoods}}
+        return {"x_hat": x_hat, "likelihoods": {"y": self._dp_mark("lik_y", y_likelihoods),
+                                                "z": self._dp_mark("lik_z", z_likelihoods)}}
 
     @torch.no_grad()
     def compress(self, x):

@@ -366,11 +366,12 @@ def _jahp_tail(model, N, M):
 def _entropy(model, y):
     z = model.h_a(y)
     z_hat, z_lik = model.entropy_bottleneck(z)
-    params = model.h_s(z_hat)
-    y_hat = model.gaussian_conditional.quantize(y, "noise" if model.training else "dequantize")
+    params = model._dp_mark("params", model.h_s(z_hat))
+    yq = model._dp_mark("yq", y)        # y as quantize / the GaussianConditional read it (Master's dp_phases)
+    y_hat = model.gaussian_conditional.quantize(yq, "noise" if model.training else "dequantize")
     ctx = model.context_prediction(y_hat)
     scales_hat, means_hat = model.entropy_parameters(CatFn.apply(params, ctx)).chunk(2, 1)
-    _, y_lik = model.gaussian_conditional(y, scales_hat, means=means_hat)
+    _, y_lik = model.gaussian_conditional(yq, scales_hat, means=means_hat)
     return y_hat, y_lik, z_lik
 
 
@@ -397,16 +398,29 @@ class Master_compresser(_ARCoding, MeanScaleHyperprior):
                                       master_chl=master_chl)
         self.fdecoder = Feature_decoder(in_channel=64 * 3, out_channel=master_chl, stride=master_stride)
 
+    def dp_phases(self):
+        """Gradient buckets in backward order (compressai.distributed): the synthesis (decoder + fdecoder), the
+        context model + entropy parameters, the hyper path, g_a, then the tail.  guided_align feeds both g_a
+        and fdecoder: its fdecoder branch is a cut of its own ("ga_fd"), so the synthesis phase stops there
+        and the g_a phase carries that gradient on to the tail cut.  g_a's output y is read by the hyper path
+        and (as "yq") by quantize / the GaussianConditional: the context phase stops at "yq", not at y, which
+        the hyper path below its "params" cut also reaches."""
+        return [(["decoder.", "fdecoder."], ["loss"], ["gs_in", "lik_y", "lik_z", "ga_fd"]),
+                (["entropy_parameters.", "context_prediction."], ["gs_in", "lik_y"], ["params", "yq"]),
+                (None, ["params", "lik_z"], ["ga_out"]),
+                (["g_a."], ["ga_out", "yq", "ga_fd"], ["y"]),
+                (list(self.dp_tail), ["y"], [])]
+
     def forward(self, x, guided_hat, guided_hidden):
         x_feature = self.fencoder1(x)
         guided_feature = self.fencoder2(guided_hat)
         guided_align, beta, gamma = self.ch_aligner(x_feature, guided_feature)
         x_feature, guided_align = self._dp_cut(x_feature, guided_align)
-        y = self.g_a(CatFn.apply(x_feature, guided_align))
+        y = self._dp_mark("ga_out", self.g_a(CatFn.apply(x_feature, guided_align)))
         y_hat, y_lik, z_lik = _entropy(self, y)
-        res = self.decoder(y_hat, guided_hidden)
-        out = self.fdecoder(CatFn.apply(res["x_feature_hat"], guided_align))
-        return {"x_hat": out, "likelihoods": {"y": y_lik, "z": z_lik}}
+        res = self.decoder(self._dp_mark("gs_in", y_hat), guided_hidden)
+        out = self.fdecoder(CatFn.apply(res["x_feature_hat"], self._dp_mark("ga_fd", guided_align)))
+        return {"x_hat": out, "likelihoods": {"y": self._dp_mark("lik_y", y_lik), "z": self._dp_mark("lik_z", z_lik)}}
 
     @torch.no_grad()
     def compress(self, x, guided_hat):

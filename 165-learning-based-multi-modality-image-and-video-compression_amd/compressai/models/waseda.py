@@ -21,6 +21,8 @@ class Cheng2020Anchor(JointAutoregressiveHierarchicalPriors):
     # gradient buckets of g_a (compressai.distributed): g_a[4:], g_a[2:4], g_a[1], g_a[0] (the exposed last
     # bucket: ResidualBlockWithStride(3, N), 0.37 M parameters at N = 192)
     dp_tail_cuts = ("g_a.4", "g_a.2", "g_a.1")
+    # g_s[4:] / g_s[:4] at N = 192: 17.5 / 29.5 MB of fp32 gradients
+    dp_gs_cuts = ("g_s.4",)
 
     def __init__(self, N=192, channel=3, **kwargs):
         super().__init__(N=N, M=N, **kwargs)
@@ -55,6 +57,11 @@ class Cheng2020Attention(Cheng2020Anchor):
 
     # g_a[5:] (10.0 MB of fp32 gradients at N = 192), g_a[2:5] (8.6 MB), g_a[1] (2.7 MB), g_a[0] (1.5 MB, exposed)
     dp_tail_cuts = ("g_a.5", "g_a.2", "g_a.1")
+    # g_s[5:] (20.5 MB), g_s[:5] (32.6 MB); then the context model + entropy parameters (11.4 MB) and the hyper
+    # path (31.2 MB): no bucket above 33 MB (the head was one 95.8 MB bucket).  Each phase boundary costs
+    # ~25-35 us of split weight-gradient batches and reduce flushes: the fewest pieces
+    # that keep every bucket under 40 MB
+    dp_gs_cuts = ("g_s.5",)
 
     def __init__(self, N=192, channel=3, **kwargs):
         super().__init__(N=N, **kwargs)

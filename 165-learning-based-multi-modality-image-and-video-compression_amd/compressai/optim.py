@@ -273,20 +273,42 @@ def dp_stage(name: str, tail: Tuple[str, ...], cuts: Tuple[str, ...] = ()) -> in
     return 1 + below
 
 
+def phase_of(name: str, plan) -> int:
+    """Gradient bucket of parameter `name` under a phase plan (CompressionModel.dp_phases(): (prefixes, roots,
+    inputs) per phase): the first phase one of whose prefixes `name` starts with, else the plan's catch-all
+    phase (prefixes None)."""
+    rest = None
+    for k, (prefixes, _, _) in enumerate(plan):
+        if prefixes is None:
+            rest = k if rest is None else rest
+        elif any(name.startswith(p) for p in prefixes):
+            return k
+    if rest is None:
+        raise ValueError(f"parameter {name!r} belongs to no phase of the plan (and no phase takes the rest)")
+    return rest
+
+
 def configure_optimizers(net, lr: float = 1e-4, aux_lr: float = 1e-3, tail: Tuple[str, ...] = (),
-                         zero_grad_in_step: bool = False, tail_cuts: Tuple[str, ...] = ()):
+                         zero_grad_in_step: bool = False, tail_cuts: Tuple[str, ...] = (), phases=None):
     """train.py:111-142: main Adam on all but `.quantiles`, aux Adam on `.quantiles` (sorted by name).
 
     tail: name prefixes whose parameters go last in the main flat buffers (FusedAdam layout); tail_cuts split
     the tail further (dp_stage): the buffer holds the buckets in backward order, head first.  The optimizer's
     ``bucket_bounds`` are the buckets' element offsets ([0, ..., numel]); ``tail_offset`` is where the tail
     starts (distributed.OverlappedAllReduce).
+    phases: a phase plan (CompressionModel.dp_phases()) instead: one bucket per phase, in phase order
+    (distributed.OverlappedAllReduce.for_model reads it back from ``opt.dp_plan``).
     zero_grad_in_step: see FusedAdam (both optimizers)."""
     named = dict(net.named_parameters())
     main, aux = parameter_groups(net)
-    tail_cuts = check_tail_cuts(tail_cuts)
-    stage = [dp_stage(n, tail, tail_cuts) for n in main]
-    nst = 1 + len(tail_cuts) + 1 if tail else 1
+    if phases is not None:
+        phases = [(None if p is None else tuple(p), tuple(r), tuple(i)) for p, r, i in phases]
+        stage = [phase_of(n, phases) for n in main]
+        nst = len(phases)
+    else:
+        tail_cuts = check_tail_cuts(tail_cuts)
+        stage = [dp_stage(n, tail, tail_cuts) for n in main]
+        nst = 1 + len(tail_cuts) + 1 if tail else 1
     layout = [i for s in range(nst) for i, t in enumerate(stage) if t == s]
     opt = FusedAdam((named[n] for n in main), lr=lr, layout=layout, zero_grad_in_step=zero_grad_in_step)
     bounds = [0]
@@ -296,4 +318,5 @@ def configure_optimizers(net, lr: float = 1e-4, aux_lr: float = 1e-3, tail: Tupl
     bounds.append(opt.numel)
     opt.bucket_bounds = bounds
     opt.tail_offset = bounds[1] if len(bounds) > 2 else opt.numel
+    opt.dp_plan = phases
     return opt, FusedAdam((named[n] for n in aux), lr=aux_lr, zero_grad_in_step=zero_grad_in_step)

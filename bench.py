@@ -358,13 +358,13 @@ def main():
     broadcast_parameters_(net)
     torch.cuda.manual_seed(1000 + rank)      # per-rank training noise
     # N > 1: the gradient exchange in buckets, each all-reduced while the backward below it runs
-    # (compressai.distributed.OverlappedAllReduce: the head, then g_a in pieces for the zoo models; the head,
-    # then the feature encoders + channel aligner for Master_compresser)
+    # (compressai.distributed.OverlappedAllReduce over the model's phase plan, CompressionModel.dp_phases():
+    # g_s in pieces, the entropy path, then g_a in pieces for the zoo models)
     overlap = world > 1 and not args.serial_allreduce
     # the reference loop order (zero_grad, forward, backward, step): the Adam kernels consume the gradients
     # and zero_grad() launches nothing (FusedAdam zero_grad_in_step)
-    opt, aux_opt = configure_optimizers(net, tail=net.dp_tail if overlap else (), zero_grad_in_step=not args.keep_grads,
-                                        tail_cuts=tuple(getattr(net, "dp_tail_cuts", ())) if overlap else ())
+    opt, aux_opt = configure_optimizers(net, zero_grad_in_step=not args.keep_grads,
+                                        phases=net.dp_phases() if overlap else None)
     sync = OverlappedAllReduce.for_model(net, opt) if overlap else None
     criterion = RateDistortionLoss(args.quality)
     state = {}
@@ -380,7 +380,7 @@ def main():
             crit = criterion(out, x)
         state["loss"] = crit["loss"].detach()
         if two_phase:
-            sync.backward_head(crit["loss"])    # everything but g_a: the head bucket is final
+            sync.backward_head(crit["loss"])    # phase 0 (the synthesis' outermost piece): bucket 0 is final
         else:
             crit["loss"].backward(loss_seed(crit["loss"]))   # a persistent 1.0 seed: no fill launch
 
@@ -403,7 +403,7 @@ def main():
             allreduce_mean_(opt.flat_grad)
         else:
             fwd(two_phase=True)
-            sync.reduce_head()      # side stream, overlapped with g_a's backward
+            sync.reduce_head()      # side stream, overlapped with the next phase
             sync.backward_tail()
             sync.finish()
         opt_part()
@@ -508,10 +508,9 @@ def main():
                        "model": args.model, "quality": args.quality, "global_batch": args.batch * world,
                        "per_gpu_batch": args.batch, "seq_len": None,
                        "patch": list(MM_IR) if multimodal else args.size, "parallelism": f"dp{world}",
-                       "grad_exchange": (f"{sync.nphases}-bucket all-reduce (head, then "
-                                         f"{'+'.join(p.rstrip('.') for p in net.dp_tail)} in {sync.nphases - 1} "
-                                         f"pieces), bucket i overlapped with backward phase i+1; exposed: the last "
-                                         f"({4 * sync.buckets[-1].numel() / 1e6:.2f} MB)" if sync else
+                       "grad_exchange": (f"{sync.nphases}-bucket all-reduce in backward order (MB: "
+                                         f"{' / '.join(f'{4 * b.numel() / 1e6:.1f}' for b in sync.buckets)}), "
+                                         f"bucket i overlapped with backward phase i+1; exposed: the last" if sync else
                                          "1 all-reduce after backward") if world > 1 else None},
             "final_loss": round(loss, 5), "max_memory_allocated_gb": round(peak_gb, 3),
             "roofline": roof, "dominant_class": dom_class, "step_roofline": step_roof, "cpu_baseline": cpu,

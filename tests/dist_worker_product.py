@@ -60,8 +60,7 @@ def main():
         broadcast_parameters_(guide)                 # replicated, frozen: never exchanged
     mode = os.environ.get("CAI_DIST_MODE", "serial")
     overlap = mode.startswith("overlap")
-    opt, aux_opt = configure_optimizers(net, tail=net.dp_tail if overlap else (),
-                                        tail_cuts=tuple(net.dp_tail_cuts) if overlap else ())
+    opt, aux_opt = configure_optimizers(net, phases=net.dp_phases() if overlap else None)
     sync = OverlappedAllReduce.for_model(net, opt) if overlap else None
     b = inp["x"].shape[0] // world
     sl = slice(rank * b, (rank + 1) * b)
@@ -136,7 +135,12 @@ def main():
     set_noise_source(None)
     if rank == 0:
         main_names, _ = parameter_groups(net)
+        from compressai.optim import phase_of
+
+        plan = getattr(opt, "dp_plan", None)
+        stage = [phase_of(n, plan) for n in main_names] if plan is not None else [0] * len(main_names)
         torch.save({"flat_grad": opt.flat_grad.cpu(), "offsets": list(opt.offsets), "names": main_names,
+                    "stage": stage,
                     "numels": [p.numel() for p in opt.params], "tail_offset": int(opt.tail_offset),
                     "bounds": [int(b) for b in opt.bucket_bounds],
                     "nphases": sync.nphases if sync is not None else 1},

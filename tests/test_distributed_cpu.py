@@ -143,14 +143,14 @@ def _phase_worker(rank, world, port, out_dir, micro):
     xs = [torch.rand(2, 3, 16, 16, generator=torch.Generator().manual_seed(10 * rank + k)) for k in range(micro)]
     # reference: the plain backward of the same loss, one all-reduce
     loss = sum(net(x) for x in xs)
-    sync._cuts = [[] for _ in sync._cuts]
+    sync._cuts = {k: [] for k in sync._cuts}
     ref_flat = torch.autograd.grad(loss, [named[main[i]] for i in order])
     ref_local = torch.cat([g.flatten() for g in ref_flat])
     ref_flat = allreduce_mean_(ref_local.clone())
     # phased: micro-batch forwards accumulate their cuts; every bucket is final after its phase
     flat.zero_()
     loss = sum(net(x) for x in xs)
-    assert [len(c) for c in sync._cuts] == [micro] * 3
+    assert [len(c) for c in sync._cuts.values()] == [micro] * 3
     sync.backward_head(loss)
     done = [flat[bounds[0]:bounds[1]].clone()]
     for i in range(1, sync.nphases):
@@ -158,12 +158,12 @@ def _phase_worker(rank, world, port, out_dir, micro):
         sync.backward_phase(i)
         done.append(flat[bounds[i]:bounds[i + 1]].clone())
     sync.finish()
-    assert all(len(c) == 0 for c in sync._cuts)
+    assert all(len(c) == 0 for c in sync._cuts.values())
     torch.save({"flat": flat, "ref": ref_flat, "ref_local": ref_local, "bounds": bounds, "done": done},
                os.path.join(out_dir, f"r{rank}.pt"))
     # a plain backward outside the phases releases its cuts: nothing leaks into the next step
     net(xs[0]).backward()
-    assert all(len(c) == 0 for c in sync._cuts)
+    assert all(len(c) == 0 for c in sync._cuts.values())
     dist.barrier()
     dist.destroy_process_group()
 
@@ -218,14 +218,14 @@ def test_forward_without_backward_is_pruned():
     sync, flat, params = _toy_sync(net)
     x = torch.rand(2, 3, 16, 16, generator=torch.Generator().manual_seed(1))
     ref = torch.cat([g.flatten() for g in torch.autograd.grad(net(x), params)])
-    sync._cuts = [[] for _ in sync._cuts]
+    sync._cuts = {k: [] for k in sync._cuts}
     sync._nfwd = 0
     flat.zero_()
     _ = net(torch.rand(2, 3, 16, 16))          # logging forward, no backward
     loss = net(x)
-    assert [len(c) for c in sync._cuts] == [2, 2, 2]
+    assert [len(c) for c in sync._cuts.values()] == [2, 2, 2]
     sync.backward_head(loss)
-    assert [len(c) for c in sync._cuts] == [1, 1, 1]
+    assert [len(c) for c in sync._cuts.values()] == [1, 1, 1]
     for i in range(1, sync.nphases):
         sync.backward_phase(i)
     sync.finish()
@@ -251,3 +251,105 @@ def test_tail_cuts_must_descend():
     net = _toy_model()
     with pytest.raises(ValueError):
         configure_optimizers(net, tail=("g_a.",), tail_cuts=("g_a.2", "g_a.4"))
+
+
+def _toy_plan_model():
+    """A CPU stand-in shaped like the context models (JAHP / cheng2020): y = g_a(x) feeds the hyper path
+    (h_a -> h_s -> "params"), the context model and the synthesis; the loss reads x_hat and two likelihoods."""
+    import torch.nn as nn
+
+    class ToyJ(nn.Module):
+        _dp_mark_fn = None
+
+        def __init__(self):
+            super().__init__()
+            self.g_a = nn.Sequential(nn.Conv2d(3, 8, 3, padding=1), nn.Tanh(), nn.Conv2d(8, 8, 3, padding=1),
+                                     nn.Tanh(), nn.Conv2d(8, 6, 3, padding=1))
+            self.h_a = nn.Conv2d(6, 6, 1)
+            self.h_s = nn.Conv2d(6, 6, 1)
+            self.ctx = nn.Conv2d(6, 6, 3, padding=1)
+            self.ep = nn.Conv2d(6, 6, 1)
+            self.g_s = nn.Sequential(nn.Conv2d(6, 8, 3, padding=1), nn.Tanh(), nn.Conv2d(8, 8, 3, padding=1),
+                                     nn.Tanh(), nn.Conv2d(8, 3, 3, padding=1))
+
+        def _dp_mark(self, name, *ts):
+            if self._dp_mark_fn is not None:
+                ts = self._dp_mark_fn(name, *ts)
+            return ts[0] if len(ts) == 1 else ts
+
+        def dp_phases(self):
+            return [(["g_s.2.", "g_s.3.", "g_s.4."], ["loss"], ["g_s.2", "lik_y", "lik_z"]),
+                    (["g_s.0.", "g_s.1."], ["g_s.2"], ["gs_in"]),
+                    (["ep.", "ctx."], ["gs_in", "lik_y"], ["params", "yq"]),
+                    (None, ["params", "lik_z"], ["y"]),
+                    (["g_a.2.", "g_a.3.", "g_a.4."], ["y", "yq"], ["g_a.2"]),
+                    (["g_a.0.", "g_a.1."], ["g_a.2"], [])]
+
+        def forward(self, x):
+            y = self._dp_mark("y", self.g_a(x))
+            z = self.h_a(y)
+            lik_z = torch.sigmoid(z) * 0.9 + 0.05
+            params = self._dp_mark("params", self.h_s(z))
+            yq = self._dp_mark("yq", y)
+            g = self.ep(params + self.ctx(yq))
+            lik_y = torch.sigmoid(g * yq) * 0.9 + 0.05
+            x_hat = self.g_s(self._dp_mark("gs_in", yq))
+            lik_y, lik_z = self._dp_mark("lik_y", lik_y), self._dp_mark("lik_z", lik_z)
+            return (x_hat ** 2).mean() - torch.log(lik_y).mean() - 0.5 * torch.log(lik_z).mean()
+
+    return ToyJ()
+
+
+def test_phase_plan_buckets_final_in_order():
+    """The plan-driven exchange (CompressionModel.dp_phases form: the synthesis in pieces, the context /
+    entropy-parameter stack, the hyper path, g_a in pieces): after phase i, bucket i holds the plain backward's
+    gradient and every later bucket is still untouched; y's gradient arrives in two parts (the hyper path's at
+    y, the context path's at "yq", both roots of the first g_a phase); the likelihood cut lik_z waits two
+    phases for its root.  (A phase whose inputs include y AND the "params" cut above the hyper path would
+    pull that path into the phase: counted twice.)"""
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "165-learning-based-multi-modality-image-and-video-compression_amd"))
+    from compressai.distributed import OverlappedAllReduce, _cut_site
+    from compressai.optim import parameter_groups, phase_of
+
+    torch.manual_seed(0)
+    net = _toy_plan_model()
+    plan = net.dp_phases()
+    main, _ = parameter_groups(net)
+    named = dict(net.named_parameters())
+    stage = [phase_of(n, plan) for n in main]
+    order = [i for s in range(len(plan)) for i, t in enumerate(stage) if t == s]
+    sizes = [named[main[i]].numel() for i in order]
+    offs = [sum(sizes[:k]) for k in range(len(sizes))]
+    bounds = [0] + [min([o for o, i in zip(offs, order) if stage[i] >= s] or [sum(sizes)])
+                    for s in range(1, len(plan))] + [sum(sizes)]
+    assert all(bounds[i] < bounds[i + 1] for i in range(len(plan)))
+    flat = torch.zeros(sum(sizes))
+    for o, i, n in zip(offs, order, sizes):
+        named[main[i]].grad = flat[o:o + n].view_as(named[main[i]])
+    phases = [([named[main[i]] for i in order if stage[i] == k], r, inp) for k, (_, r, inp) in enumerate(plan)]
+    names = {n for _, r, inp in plan for n in (*r, *inp) if n != "loss"}
+    sync = OverlappedAllReduce(flat, bounds, phases=phases, sites={n: _cut_site(net, n) for n in names})
+    assert sync.nphases == len(plan)
+    xs = [torch.rand(2, 3, 12, 12, generator=torch.Generator().manual_seed(k)) for k in range(2)]
+    loss = sum(net(x) for x in xs)
+    ref = torch.cat([g.flatten() for g in torch.autograd.grad(loss, [named[main[i]] for i in order])])
+    sync._cuts = {k: [] for k in sync._cuts}
+    sync._nfwd = 0
+    flat.zero_()
+    loss = sum(net(x) for x in xs)            # two micro-batches: their cuts accumulate
+    assert all(len(c) == 2 for c in sync._cuts.values())
+    for i in range(sync.nphases):
+        if i == 0:
+            sync.backward_head(loss)
+        else:
+            sync.backward_phase(i)
+        b0, b1 = bounds[i], bounds[i + 1]
+        assert torch.allclose(flat[b0:b1], ref[b0:b1], rtol=1e-5, atol=1e-7), i
+        assert not flat[b1:].any(), f"phase {i} wrote a later bucket"
+    sync.finish()
+    assert torch.allclose(flat, ref, rtol=1e-5, atol=1e-7)
+    sync.remove()
+    assert net._dp_mark_fn is None

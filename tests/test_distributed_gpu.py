@@ -69,14 +69,18 @@ def _oracle_case(kind):
 
 @pytest.mark.parametrize("kind,mode", [("c2", "serial"), ("c2", "overlap"), ("c2", "overlap-eager"),
                                        ("cheng2020-attn", "serial"), ("cheng2020-attn", "overlap"),
+                                       ("cheng2020-attn", "overlap-eager"),
                                        ("multimodal", "serial"), ("multimodal", "overlap"),
                                        ("multimodal", "overlap-eager")])
 def test_world2_allreduced_flat_grad_matches_oracle(cuda, tmp_path, kind, mode):
     """serial: one all-reduce after the graph replay (bench.py --serial-allreduce); overlap: the bucketed
-    exchange of compressai.distributed.OverlappedAllReduce (bucket i all-reduced on a side stream while the
-    captured graph of backward phase i + 1 replays: head, then g_a in 3 / 4 pieces for C2 / cheng2020-attn, the
-    feature encoders + channel aligner for C5); overlap-eager: the same without graphs."""
-    from compressai.optim import dp_stage
+    exchange of compressai.distributed.OverlappedAllReduce over the model's phase plan (CompressionModel.
+    dp_phases(): bucket i all-reduced on a side stream while the captured graph of backward phase i + 1
+    replays -- C2: g_s, the hyper path, g_a in 3 pieces; cheng2020-attn: g_s in 2 pieces, the context /
+    entropy-parameter stack, the hyper path, g_a in 4 pieces; C5: the synthesis, the context stack, the hyper
+    path, g_a, the feature encoders + channel aligner); overlap-eager: the same without graphs."""
+    from compressai.models.master import Master_compresser
+    from compressai.zoo import image_models
 
     ref, case = _oracle_case(kind)
     inp, outp = tmp_path / "in.pt", tmp_path / "out.pt"
@@ -102,16 +106,23 @@ def test_world2_allreduced_flat_grad_matches_oracle(cuda, tmp_path, kind, mode):
     flat = res["flat_grad"]
     gmax = max(p.grad.abs().max().item() for p in ref.parameters() if p.grad is not None)
     tail = tuple(("g_a.",) if kind != "multimodal" else ("fencoder1.", "fencoder2.", "ch_aligner."))
-    cuts = {"c2": ("g_a.4", "g_a.2"), "cheng2020-attn": ("g_a.5", "g_a.2", "g_a.1"), "multimodal": ()}[kind]
+    plan = {"c2": lambda: image_models["bmshj2018-hyperprior"](1),
+            "cheng2020-attn": lambda: image_models["cheng2020-attn"](6),
+            "multimodal": lambda: Master_compresser(width=64, height=64, channel=1)}[kind]().dp_phases()
     n_tail = 0
     if mode.startswith("overlap"):
-        assert res["nphases"] == len(cuts) + 2 == len(res["bounds"]) - 1, (res["nphases"], res["bounds"])
-    for name, off, n in zip(res["names"], res["offsets"], res["numels"]):
+        assert res["nphases"] == len(plan) == len(res["bounds"]) - 1, (res["nphases"], res["bounds"])
+        mb = [4 * (res["bounds"][i + 1] - res["bounds"][i]) / 1e6 for i in range(len(plan))]
+        print(f"\n{kind} buckets (MB, backward order): {[round(v, 2) for v in mb]}")
+        if kind == "cheng2020-attn":
+            assert max(mb) <= 40.0, mb      # the head's single 95.8 MB bucket, split
+    for name, off, n, st in zip(res["names"], res["offsets"], res["numels"], res["stage"]):
         g = flat[off:off + n]
         if mode.startswith("overlap"):
-            assert (off >= res["tail_offset"]) == name.startswith(tail), name   # the bucket layout
-            st = dp_stage(name, tail, cuts)
+            # the bucket layout: each parameter inside its phase's bucket, the tail's in the last phases
             assert res["bounds"][st] <= off and off + n <= res["bounds"][st + 1], (name, st, off, res["bounds"])
+            assert (plan[st][0] is not None and any(name.startswith(p) for p in plan[st][0])) or \
+                (plan[st][0] is None and not name.startswith(tail)), (name, st)
             n_tail += name.startswith(tail)
         gr = pr[name].grad
         if gr is None:
