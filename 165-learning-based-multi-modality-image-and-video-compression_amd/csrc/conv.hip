@@ -2962,9 +2962,6 @@ __device__ __forceinline__ int opaque(int v) {
     return v;
 }
 
-#ifndef CAI_WH_PIPE
-#define CAI_WH_PIPE 0
-#endif
 // S = 1: the stride-1 k3 p1 Conv2d (cheng2020's 3x3 convs): one footprint plane, tap kw at cell p + kw.
 // TMR: row fragments per wave -- 4 (128-row tiles), 2 (64-row tiles, for Ng a multiple of 64 but not of 128:
 // C2's g_a[6] / g_s[0]; the 128-row tiles left a third of their rows empty) or 6 (192-row tiles, stride-1 k3 with
@@ -3185,21 +3182,11 @@ __device__ __forceinline__ void wgrad_halo_block(const WgradArgs& a, int wgid, i
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
             if (st + W::NST - 1 < nsteps) issue((U + W::NST - 1) % W::NST);
-#if CAI_WH_PIPE
-            // both K-halves' fragments read up front: the second half's reads are in flight under the first half's
-            // MFMAs instead of exposing their latency after them
-            u32x4 fa[TMR], fb[W::TN], fa1[TMR], fb1[W::TN];
-            rd(ustage, K0(), fa, fb);
-            rd(ustage, K1(), fa1, fb1);
-            mm(fa, fb);
-            mm(fa1, fb1);
-#else
             u32x4 fa[TMR], fb[W::TN];
             rd(ustage, K0(), fa, fb);
             mm(fa, fb);
             rd(ustage, K1(), fa, fb);
             mm(fa, fb);
-#endif
             __builtin_amdgcn_sched_barrier(0);
         };
         one(std::integral_constant<int, 0>());
@@ -4616,9 +4603,6 @@ static void wgrad_split_setup(const cai_conv_geom* g, const WgradPlan& W, WgradA
     a.nsplit = W.S;
     float* bws = nullptr;
     if ((W.fused_bias || W.tbias) && db) bws = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + W.ws_slab);
-#if CAI_WH_NOBIAS   // timing probe only (bias gradients left unwritten)
-    if (W.halo) bws = nullptr;
-#endif
     a.bws = bws;
     a.tb_kh0 = W.tb_kh0; a.tb_kw0 = W.tb_kw0; a.tb_s = g->stride; a.nbias = W.nbias;
     const int bflag = !bws ? 0 : (W.tbias ? WG_TBIAS : WG_BIAS);
