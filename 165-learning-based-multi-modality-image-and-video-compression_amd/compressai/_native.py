@@ -64,6 +64,7 @@ class EbGrads(Structure):
 
 
 JOB_NONE, JOB_WGRAD, JOB_GDN, JOB_EDGE = 0, 1, 2, 3           # cai_reduce_job kinds (include/cai.h)
+GC_SCALES_RELU = 16                                              # cai_gc_bwd mode flag
 
 
 class ReduceJob(Structure):

@@ -29,7 +29,7 @@ import torch
 from . import _ledger
 from ._native import (ACT_LEAKY, ACT_NONE, ACT_RELU, BF16, F32, MASK_BEFORE_RES, MASK_LEAKY, MASK_NONE, MASK_POS,
                       Q_DEQUANTIZE, Q_NOISE,
-                      JOB_EDGE, JOB_GDN, JOB_NONE, JOB_WGRAD, NOISE_BUF, NOISE_DRAW, NOISE_REPLAY, ConvGeom, EbGrads, EbParams, NoiseSrc, RdGrads,
+                      GC_SCALES_RELU, JOB_EDGE, JOB_GDN, JOB_NONE, JOB_WGRAD, NOISE_BUF, NOISE_DRAW, NOISE_REPLAY, ConvGeom, EbGrads, EbParams, NoiseSrc, RdGrads,
                       RdInputs, ReduceJob, ResunitArgs, ResunitWgradArgs, WgradCall, lib)
 
 _VP = ctypes.c_void_p
@@ -1568,8 +1568,10 @@ class GaussianFn(torch.autograd.Function):
     """GaussianConditional.forward (entropy_models.py:715-731) as one fused kernel pair."""
 
     @staticmethod
-    def forward(ctx, x, scales, means, noise, mode: int, scale_bound: float, lik_bound: float):
-        """noise: None (DEQUANTIZE), an fp32 tensor, or a DeviceDraw."""
+    def forward(ctx, x, scales, means, noise, mode: int, scale_bound: float, lik_bound: float,
+                scales_relu: bool = False):
+        """noise: None (DEQUANTIZE), an fp32 tensor, or a DeviceDraw.  scales_relu: the scales are a ReLU's output
+        whose backward mask the caller left to this op (the producing conv ran with act_bwd_downstream)."""
         draw = noise if isinstance(noise, DeviceDraw) else None
         _check_cuda(x, scales, means, None if draw is not None else noise)
         xr, xld, npix, C = as_rows(x)
@@ -1591,6 +1593,7 @@ class GaussianFn(torch.autograd.Function):
                             + (4 if nr is not None else 0)), torch.float32, f"{n_el} elements")
         ctx.save_for_backward(xr, sr, mr, nr)
         ctx.draw = draw
+        ctx.relu = bool(scales_relu)
         ctx.give = _fan_role(x, "give")
         ctx.cfg = (mode, scale_bound, lik_bound, xld, sld, mld, nld, npix, C, x.shape, x.dtype, scales.shape,
                    scales.dtype, means is not None)
@@ -1622,7 +1625,8 @@ class GaussianFn(torch.autograd.Function):
             dm, dmb = empty_rows_like(sshape, sdtype, xr.device) if has_m else (None, None)
         n_el = npix * C
         es_x, es_s = xr.element_size(), sr.element_size()
-        _ledger.run(lambda: lib.cai_gc_bwd(mode, npix, C, _p(xr), dcode(xdtype), xld, _p(sr), sld, _p(mr), mld,
+        gmode = mode | (GC_SCALES_RELU if ctx.relu else 0)
+        _ledger.run(lambda: lib.cai_gc_bwd(gmode, npix, C, _p(xr), dcode(xdtype), xld, _p(sr), sld, _p(mr), mld,
                                            dcode(sdtype), nsrc, sb, lb, _p(gl), glld, _p(gq_r),
                                            dcode(gq_r.dtype) if gq_r is not None else F32, gqld, _p(dxb), C, _p(dsb),
                                            dld, _p(dmb), dld, _stream()),
@@ -1632,7 +1636,7 @@ class GaussianFn(torch.autograd.Function):
                     torch.float32, f"{n_el} elements")
         if ctx.give is not None:    # FanOutFn: x's other consumer adds it (in its dgrad epilogue)
             ctx.give.pending, dx = dx, None
-        return dx, ds, dm, None, None, None, None
+        return dx, ds, dm, None, None, None, None, None
 
 
 def _eb_params(params: Sequence[torch.Tensor], quantiles: torch.Tensor) -> EbParams:

@@ -455,10 +455,12 @@ class GaussianConditional(EntropyModel):
         return torch.Tensor(tuple(float(s) for s in scale_table))
 
     def forward(self, inputs: torch.Tensor, scales: torch.Tensor, means: Optional[torch.Tensor] = None,
-                training: Optional[bool] = None, noise: Optional[torch.Tensor] = None
+                training: Optional[bool] = None, noise: Optional[torch.Tensor] = None, scales_relu: bool = False
                 ) -> Tuple[torch.Tensor, torch.Tensor]:
         """noise: the U(-1/2, 1/2) draw to use in training mode (the models' concurrent forward shares one
-        draw between g_s's input and this likelihood); None draws it here, as the reference does."""
+        draw between g_s's input and this likelihood); None draws it here, as the reference does.
+        scales_relu: the scales are the output of a ReLU whose backward mask this op applies (the producer ran
+        with act_bwd_downstream: ScaleHyperprior's h_s)."""
         if training is None:
             training = self.training
         # the reference's _likelihood broadcasts scales / means against the inputs (entropy_models.py:692-709)
@@ -475,7 +477,7 @@ class GaussianConditional(EntropyModel):
             noise = None
         sb = self._scale_bound_value
         return GaussianFn.apply(inputs, scales, means, noise, Q_NOISE if training else Q_DEQUANTIZE, sb,
-                                self._lik_bound())
+                                self._lik_bound(), bool(scales_relu))
 
     def build_indexes(self, scales: torch.Tensor) -> torch.Tensor:
         scales = torch.clamp_min(scales, self._scale_bound_value)

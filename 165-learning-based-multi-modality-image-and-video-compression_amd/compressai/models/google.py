@@ -101,6 +101,11 @@ def _cross(main, side, y, noise, outs, z_noise=None):
         t.record_stream(main)
 
 
+# ScaleHyperprior: h_s's trailing ReLU masked in the GaussianConditional's backward (CAI_GC_RELU=0: by the conv's
+# own act-backward launch, A/B)
+_GC_RELU = os.environ.get("CAI_GC_RELU", "1") == "1"
+
+
 def get_scale_table(min=SCALES_MIN, max=SCALES_MAX, levels=SCALES_LEVELS):
     return torch.exp(torch.linspace(math.log(min), math.log(max), levels))
 
@@ -322,8 +327,9 @@ class ScaleHyperprior(CompressionModel):
             y_ha, y_gc = fan_out(y)                  # y's two gradients meet in h_a's first dgrad epilogue
             z = self.h_a(y_ha, input_abs=True)       # h_a(|y|)
             z_hat, z_likelihoods = self.entropy_bottleneck(z)
-            scales_hat = self.h_s(z_hat)
-            y_hat, y_likelihoods = self.gaussian_conditional(y_gc, scales_hat)
+            # h_s's trailing ReLU: its backward mask applied by the GaussianConditional's backward
+            scales_hat = self.h_s(z_hat, act_bwd_downstream=_GC_RELU)
+            y_hat, y_likelihoods = self.gaussian_conditional(y_gc, scales_hat, scales_relu=_GC_RELU)
             x_hat = self.g_s(self._dp_mark("gs_in", y_hat))
             return {"x_hat": x_hat, "likelihoods": {"y": self._dp_mark("lik_y", y_likelihoods),
                                                     "z": self._dp_mark("lik_z", z_likelihoods)}}
@@ -333,14 +339,14 @@ class ScaleHyperprior(CompressionModel):
         with torch.cuda.stream(side):
             z = self.h_a(y, input_abs=True)
             z_hat, z_likelihoods = self.entropy_bottleneck(z, noise=z_noise)
-            scales_hat = self.h_s(z_hat)
+            scales_hat = self.h_s(z_hat, act_bwd_downstream=_GC_RELU)
         y_hat, noise = _quantize_y(y, self.training)
         ready = torch.cuda.Event()
         ready.record(main)
         x_hat = self.g_s(self._dp_mark("gs_in", y_hat))
         with torch.cuda.stream(side):
             side.wait_event(ready)
-            _, y_likelihoods = self.gaussian_conditional(y, scales_hat, noise=noise)
+            _, y_likelihoods = self.gaussian_conditional(y, scales_hat, noise=noise, scales_relu=_GC_RELU)
         main.wait_stream(side)
         _cross(main, side, y, noise, (z_likelihoods, y_likelihoods), z_noise)
         return {"x_hat": x_hat, "likelihoods": {"y": self._dp_mark("lik_y", y_likelihoods),

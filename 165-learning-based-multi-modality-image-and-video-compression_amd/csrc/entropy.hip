@@ -185,7 +185,9 @@ __global__ void gc_fwd_kernel(int mode, int64_t n, int C, const void* __restrict
     noise_close(ns, nv);
 }
 
-__global__ void gc_bwd_kernel(int mode, int64_t n, int C, const void* __restrict__ x, int xdt, int xld,
+// relu: the scales are a ReLU's output (ScaleHyperprior's h_s ends in nn.ReLU) and their gradient leaves here with
+// that ReLU's backward mask (scales > 0) applied -- the conv before the ReLU then needs no act-backward launch
+__global__ void gc_bwd_kernel(int mode, int relu, int64_t n, int C, const void* __restrict__ x, int xdt, int xld,
                               const void* __restrict__ sc, int sld, const void* __restrict__ mu, int mld, int smdt,
                               const cai_noise_src ns, float sbound, float lbound,
                               const float* __restrict__ glik, int glld, const void* __restrict__ gq, int gqdt,
@@ -213,6 +215,7 @@ __global__ void gc_bwd_kernel(int mode, int64_t n, int C, const void* __restrict
         const float dav = -(dtu + dtl) / s;
         float dsv = -dtu * (0.5f - av) / (s * s) - dtl * (-0.5f - av) / (s * s);
         if (!(sraw >= sbound || dsv < 0.f)) dsv = 0.f;      // LowerBound(scales) backward
+        if (relu && !(sraw > 0.f)) dsv = 0.f;                // the ReLU before it
         const float sgn = (v > 0.f) ? 1.f : ((v < 0.f) ? -1.f : 0.f);
         const float dv = dav * sgn;
         const float gqv = gq ? ld_any(gq, gqdt, p * gqld + c) : 0.f;
@@ -858,14 +861,16 @@ int cai_gc_bwd(int mode, int64_t npix, int32_t C, const void* x, int x_dtype, in
                float scale_bound, float lik_bound, const float* g_lik, int32_t gl_ld, const void* g_q, int gq_dtype,
                int32_t gq_ld, void* dx, int32_t dx_ld, void* dscales, int32_t ds_ld, void* dmeans, int32_t dm_ld,
                void* stream) {
+    const int relu = (mode & CAI_GC_SCALES_RELU) != 0;
+    mode &= ~CAI_GC_SCALES_RELU;
     CAI_CHECK_ARG(mode == CAI_Q_NOISE || mode == CAI_Q_DEQUANTIZE, "gc_bwd: invalid mode %d", mode);
     CAI_CHECK_ARG(C > 0 && npix >= 0, "gc_bwd: bad arguments");
     const cai_noise_src ns = noise_arg(mode, noise, C, false, "gc_bwd");
     if (ns.kind < 0) return CAI_EINVAL;
     const int64_t n = npix * C;
     if (n == 0) return CAI_OK;
-    hipLaunchKernelGGL(gc_bwd_kernel, dim3(ew_grid(n)), dim3(256), 0, as_stream(stream), mode, n, C, x, x_dtype, x_ld,
-                       scales, s_ld, means, m_ld, sm_dtype, ns, scale_bound, lik_bound, g_lik, gl_ld, g_q,
+    hipLaunchKernelGGL(gc_bwd_kernel, dim3(ew_grid(n)), dim3(256), 0, as_stream(stream), mode, relu, n, C, x, x_dtype,
+                       x_ld, scales, s_ld, means, m_ld, sm_dtype, ns, scale_bound, lik_bound, g_lik, gl_ld, g_q,
                        gq_dtype, gq_ld, dx, dx_ld, dscales, ds_ld, dmeans, dm_ld);
     CAI_LAUNCH_CHECK("gc_bwd");
     return CAI_OK;
@@ -1039,6 +1044,7 @@ __global__ __launch_bounds__(256) void rd_stage2(const float* __restrict__ part,
         out[2] = b;
     }
 }
+
 
 __global__ __launch_bounds__(256) void rd_bwd_kernel(cai_rd_inputs in, float lmbda, float bpp_coef,
                                                      const float* __restrict__ g_loss, const float* __restrict__ g_mse,

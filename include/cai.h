@@ -558,7 +558,10 @@ int cai_gc_fwd(int mode, int64_t npix, int32_t C,
                float scale_bound, float lik_bound,
                void* q, int q_dtype, int32_t q_ld, float* lik, int32_t lik_ld, void* stream);
 /* backward: inputs the gradients wrt lik (fp32, nullable) and wrt q (nullable),
- * outputs dx (x_dtype layout, nullable), dscales, dmeans (sm_dtype, nullable). */
+ * outputs dx (x_dtype layout, nullable), dscales, dmeans (sm_dtype, nullable).
+ * mode | CAI_GC_SCALES_RELU: the scales are a ReLU's output (ScaleHyperprior's h_s ends in nn.ReLU,
+ * models/google.py:282-283 of the reference) and dscales leaves with that ReLU's backward mask (scales > 0) applied. */
+#define CAI_GC_SCALES_RELU 16
 int cai_gc_bwd(int mode, int64_t npix, int32_t C,
                const void* x, int x_dtype, int32_t x_ld,
                const void* scales, int32_t s_ld, const void* means, int32_t m_ld, int sm_dtype,
