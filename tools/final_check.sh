@@ -26,4 +26,7 @@ EOF
 ) || exit 1
 echo "$rep" > $out/fin_${tag}_replay.txt
 bash tools/pmc_traffic.sh $rep || exit 1
+# the big stride-2 convs' counter records: g_a[2] fwd (conv_halo_kernel<5>, 1024 blocks),
+# g_s[4] fwd and g_a[2] dgrad (conv_halo_quad_kernel)
+bash tools/pmc_traffic.sh conv_fwd:1 conv_fwd:12 conv_dgrad:12 || exit 1
 bash tools/bench_models.sh fin_$tag
