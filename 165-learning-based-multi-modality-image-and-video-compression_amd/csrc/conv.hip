@@ -228,6 +228,10 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvArgs& a, const Phas
     }
 }
 
+#ifndef CAI_EPI_MASK_PREFETCH
+#define CAI_EPI_MASK_PREFETCH 1   // A/B: 0 = the per-chunk masked epilogue
+#endif
+
 // Epilogue for TRANSPOSED accumulators (weights as the MFMA's A operand): lane (i16, g_) of tile (tm, tn)
 // holds output channels wn*WTN + tn*16 + 4*g_ + 0..3 of tile row wm*WTM + tm*16 + i16, so the common cases
 // store straight from registers: split-K partials as 16-byte fp32 stores into the slab, bf16 outputs
@@ -367,7 +371,49 @@ __device__ __forceinline__ void conv_epilogue_rows_t(const ConvArgs& a, const Ph
             }
             *reinterpret_cast<f32x4*>(E + row * ES + col) = v;
         }
+    // gradient mask, no residual, bf16 output and aux (the input gradients of LeakyReLU-fed convs): every aux chunk of
+    // this thread's output chunks is loaded up front, before the staging barrier.  In the per-chunk form each aux load
+    // waited behind the previous chunk's store on the shared vmcnt -- one exposed load latency per chunk, the
+    // multimodal trunk's 256-channel input gradients ran 1.4x their forwards' time (-DCAI_EPI_MASK_PREFETCH=0: that form)
+    constexpr int CPR8 = BN / 8, NIT = (BM * CPR8 + NTH - 1) / NTH;
+    const bool mfast = std::is_same<T, bf16>::value && CAI_EPI_MASK_PREFETCH && a.y_vec && a.mask_mode && !a.res &&
+                       a.y_dtype == CAI_BF16 && (a.Cout & 7) == 0 && (a.aux_ld & 7) == 0 &&
+                       (reinterpret_cast<uintptr_t>(a.aux) & 15) == 0;
+    bf16x8 mreg[NIT];
+    if (mfast) {
+        const bf16* AUX = reinterpret_cast<const bf16*>(a.aux);
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int id = tid + it * NTH, row = id / CPR8, n = n0 + (id - row * CPR8) * 8;
+            const int m = id < BM * CPR8 ? rowm(row) : -1;
+            mreg[it] = bf16x8{};
+            if (m >= 0 && n < a.Cout) {
+                int b, oy, ox;
+                out_pixel<T>(a, P, plane, m, b, oy, ox);
+                mreg[it] = *reinterpret_cast<const bf16x8*>(AUX + (((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.aux_ld + n);
+            }
+        }
+    }
     __syncthreads();
+    if (mfast) {
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int id = tid + it * NTH, row = id / CPR8, cc = id - row * CPR8, n = n0 + cc * 8;
+            const int m = id < BM * CPR8 ? rowm(row) : -1;
+            if (m < 0 || n >= a.Cout) continue;
+            const f32x4 lo = *reinterpret_cast<const f32x4*>(E + row * ES + cc * 8);
+            const f32x4 hi = *reinterpret_cast<const f32x4*>(E + row * ES + cc * 8 + 4);
+            const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            bf16x8 h;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) h[e] = (bf16)(v[e] * mask_val(a.mask_mode, (float)mreg[it][e], a.mask_param));
+            int b, oy, ox;
+            out_pixel<T>(a, P, plane, m, b, oy, ox);
+            *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(a.y) + (int64_t)b * a.ysb + (int64_t)oy * a.ysy +
+                                       (int64_t)ox * a.ysx + n) = h;
+        }
+        return;
+    }
     if (a.y_vec) {
         const int VO = a.y_dtype == CAI_BF16 ? 8 : 4;
         const int cpr = BN / VO;
@@ -3548,6 +3594,14 @@ static int small_mmax() {
     }();
     return v;
 }
+// A/B knob CAI_SMALL_CONV_KMAX512 (default: no bound): the K bound of the first rule (M <= 512)
+static int small_kmax512() {
+    static const int v = [] {
+        const char* e = getenv("CAI_SMALL_CONV_KMAX512");
+        return (e && *e) ? atoi(e) : (1 << 30);
+    }();
+    return v;
+}
 static int pick_small(const Plan& P, int dtype, int mmax, int big_ksplit, int big_blocks) {
     if (small_off() || dtype != CAI_BF16 || P.Cin_pad % 32 != 0 || (big_ksplit <= 1 && big_blocks >= 64) ||
         mmax > 8192)
@@ -3557,7 +3611,8 @@ static int pick_small(const Plan& P, int dtype, int mmax, int big_ksplit, int bi
     const int cfg = mmax <= 512 ? SMALL_16x32 : (mmax <= 2048 ? SMALL_32x32 : SMALL_32x64);
     static const int bm[] = {0, 16, 32, 32}, bn[] = {0, 32, 32, 64};
     const int blocks = (mmax + bm[cfg] - 1) / bm[cfg] * ((P.kout_c + bn[cfg] - 1) / bn[cfg]) * P.nphase;
-    if (mmax <= 512 || (kmax <= small_kmax() && (blocks <= 256 || mmax <= small_mmax()))) return cfg;
+    if ((mmax <= 512 && kmax <= small_kmax512()) || (kmax <= small_kmax() && (blocks <= 256 || mmax <= small_mmax())))
+        return cfg;
     return SMALL_NONE;
 }
 
