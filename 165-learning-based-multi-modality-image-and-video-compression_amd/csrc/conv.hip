@@ -229,7 +229,7 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvArgs& a, const Phas
 }
 
 #ifndef CAI_EPI_MASK_PREFETCH
-#define CAI_EPI_MASK_PREFETCH 1   // A/B: 0 = the per-chunk masked epilogue
+#define CAI_EPI_MASK_PREFETCH 2   // A/B: 0 = the per-chunk masked epilogue, 1 = staged through LDS with prefetch
 #endif
 
 // Epilogue for TRANSPOSED accumulators (weights as the MFMA's A operand): lane (i16, g_) of tile (tm, tn)
@@ -243,7 +243,10 @@ __host__ __device__ __forceinline__ bool epi_t_direct(const ConvArgs& a) {
            (!a.mask_mode || ((a.aux_ld & 3) == 0 && (reinterpret_cast<uintptr_t>(a.aux) & 7) == 0));
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int NTH, class RowMap, bool NOLDS = false, bool POST = true>
+// MPF: the mask-prefetch forms below -- instantiated by the stride-1 input-gradient halo kernels only (in the
+// stride-2 gather / phase kernels the extra live registers pushed conv_halo_kernel<5> into 128 bytes of spills)
+template <typename T, int BM, int BN, int WM, int WN, int NTH, class RowMap, bool NOLDS = false, bool POST = true,
+          bool MPF = false>
 __device__ __forceinline__ void conv_epilogue_rows_t(const ConvArgs& a, const PhaseDesc& P, int plane, int n0,
                                                      float* E, const f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
                                                      RowMap rowm, int slab) {
@@ -267,7 +270,52 @@ __device__ __forceinline__ void conv_epilogue_rows_t(const ConvArgs& a, const Ph
         }
         return;
     }
-    // (the mask variant only in the NOLDS tiles: in the 128-channel halo kernels its registers spill the loop)
+    // gradient mask without residual (the input gradients of LeakyReLU / ReLU-fed convs), any tile: straight from the
+    // registers, every mask load (and bias load) issued before the first store -- the loads-behind-stores rule of
+    // section 6; the accumulators' 64 VGPRs + 2 per (tm, tn) mask chunk stay far below the main loop's pressure
+    if (MPF && CAI_EPI_MASK_PREFETCH == 2 && std::is_same<T, bf16>::value && epi_t_direct(a) && a.mask_mode && !a.res) {
+        const bf16* AUX = reinterpret_cast<const bf16*>(a.aux);
+        bf16x4 mv[TM][TN];
+        f32x4 bv[TN];
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+            const int m = rowm(wm * WTM + tm * 16 + i16);
+            int b, oy, ox;
+            out_pixel<T>(a, P, plane, m < 0 ? 0 : m, b, oy, ox);
+            const bf16* arow = AUX + (((int64_t)b * a.out_h + oy) * a.out_w + ox) * a.aux_ld;
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                const int n = n0 + wn * WTN + tn * 16 + 4 * g_;
+                mv[tm][tn] = (m >= 0 && n < a.Cout) ? *reinterpret_cast<const bf16x4*>(arow + n) : bf16x4{};
+            }
+        }
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int n = n0 + wn * WTN + tn * 16 + 4 * g_;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bv[tn][r] = (a.bias && n + r < a.Cout) ? a.bias[n + r] : 0.f;
+        }
+        wait_vmcnt<0>();
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+            const int m = rowm(wm * WTM + tm * 16 + i16);
+            int b, oy, ox;
+            out_pixel<T>(a, P, plane, m < 0 ? 0 : m, b, oy, ox);
+            bf16* Y = reinterpret_cast<bf16*>(a.y) + (int64_t)b * a.ysb + (int64_t)oy * a.ysy + (int64_t)ox * a.ysx;
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                const int n = n0 + wn * WTN + tn * 16 + 4 * g_;
+                bf16x4 h;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    h[r] = (bf16)(apply_act(acc[tm][tn][r] + bv[tn][r], a.act, a.act_param) *
+                                  mask_val(a.mask_mode, (float)mv[tm][tn][r], a.mask_param));
+                if (m >= 0 && n < a.Cout) *reinterpret_cast<bf16x4*>(Y + n) = h;
+            }
+        }
+        return;
+    }
+    // (the general mask variant only in the NOLDS tiles: in the 128-channel halo kernels its registers spill the loop)
     if (NOLDS ? epi_t_direct(a)
               : (a.y_vec && a.y_dtype == CAI_BF16 && !a.mask_mode && (a.Cout & 3) == 0)) {
         f32x4 bv[TN];
@@ -376,7 +424,7 @@ __device__ __forceinline__ void conv_epilogue_rows_t(const ConvArgs& a, const Ph
     // waited behind the previous chunk's store on the shared vmcnt -- one exposed load latency per chunk, the
     // multimodal trunk's 256-channel input gradients ran 1.4x their forwards' time (-DCAI_EPI_MASK_PREFETCH=0: that form)
     constexpr int CPR8 = BN / 8, NIT = (BM * CPR8 + NTH - 1) / NTH;
-    const bool mfast = std::is_same<T, bf16>::value && CAI_EPI_MASK_PREFETCH && a.y_vec && a.mask_mode && !a.res &&
+    const bool mfast = MPF && std::is_same<T, bf16>::value && CAI_EPI_MASK_PREFETCH == 1 && a.y_vec && a.mask_mode && !a.res &&
                        a.y_dtype == CAI_BF16 && (a.Cout & 7) == 0 && (a.aux_ld & 7) == 0 &&
                        (reinterpret_cast<uintptr_t>(a.aux) & 15) == 0;
     bf16x8 mreg[NIT];
@@ -1247,7 +1295,7 @@ struct HaloPhCfg {
 // NA-1 / NC-1 before dy0 / dx0).  GATHER = true: a stride-1 gather convolution (Conv2d k3 s1 forward): tap
 // (ty, tx) = kernel (kh, kw) reads cell (ty, tx) from the origin dy0 = -pad.  n0: the tile's first output
 // channel (grid y).
-template <int NA, int NC, int BN_ = 128, bool GATHER = false>
+template <int NA, int NC, int BN_ = 128, bool GATHER = false, bool MPF = false>
 __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* smem, int ph, int split, int bid,
                                                      int tiles_x, int tiles_y, int n0 = 0) {
     using H = HaloPhCfg<NA, NC, BN_>;
@@ -1414,7 +1462,7 @@ __device__ __forceinline__ void conv_halo_phase_body(const ConvArgs& a, char* sm
         const int oy = ty0 + row / H::TW, ox = tx0 + row % H::TW;
         return (oy < P.OHg && ox < P.OWg) ? b * plane + oy * P.OWg + ox : -1;
     };
-    conv_epilogue_rows_t<bf16, BM, BN, WM, WN, NT, decltype(rowm), (BN > 128), false>(
+    conv_epilogue_rows_t<bf16, BM, BN, WM, WN, NT, decltype(rowm), (BN > 128), false, MPF>(
         a, P, plane, n0, reinterpret_cast<float*>(smem), acc, rowm, ph * a.ksplit + split);
 }
 
@@ -1454,7 +1502,7 @@ __host__ __device__ constexpr int wide_younger(int t, int nstb, int runs, int dp
     return dps * (nstb - 2) + (hi >= lo ? hi - lo + 1 : 0);
 }
 
-template <int NA, int NC, bool GATHER, int BN_ = 192>
+template <int NA, int NC, bool GATHER, int BN_ = 192, bool MPF = false>
 __device__ __forceinline__ void conv_halo_wide_body(const ConvArgs& a, char* smem, int ph, int split, int bid,
                                                     int tiles_x, int tiles_y, int n0) {
     using H = HaloWideCfg<NA, NC, BN_>;
@@ -1596,7 +1644,7 @@ __device__ __forceinline__ void conv_halo_wide_body(const ConvArgs& a, char* sme
         const int oy = ty0 + row / H::TW, ox = tx0 + row % H::TW;
         return (oy < P.OHg && ox < P.OWg) ? b * plane + oy * P.OWg + ox : -1;
     };
-    conv_epilogue_rows_t<bf16, BM, BN, WM, WN, 512, decltype(rowm), (BN > 128), false>(
+    conv_epilogue_rows_t<bf16, BM, BN, WM, WN, 512, decltype(rowm), (BN > 128), false, MPF>(
         a, P, plane, n0, reinterpret_cast<float*>(smem), acc, rowm, ph * a.ksplit + split);
 }
 
@@ -1649,9 +1697,9 @@ __global__ __launch_bounds__(512, 1) void conv_halo_s1_kernel(const ConvArgs a, 
     const int nt = gridDim.x, t = blockIdx.x;
     const int bid = (nt & 7) == 0 ? (t & 7) * (nt >> 3) + (t >> 3) : t;
     if constexpr (DMA)
-        conv_halo_wide_body<3, 3, GATHER, BN>(a, smem, 0, blockIdx.z, bid, tiles_x, tiles_y, blockIdx.y * BN);
+        conv_halo_wide_body<3, 3, GATHER, BN, !GATHER>(a, smem, 0, blockIdx.z, bid, tiles_x, tiles_y, blockIdx.y * BN);
     else
-        conv_halo_phase_body<3, 3, 128, GATHER>(a, smem, 0, blockIdx.z, bid, tiles_x, tiles_y, blockIdx.y * BN);
+        conv_halo_phase_body<3, 3, 128, GATHER, !GATHER>(a, smem, 0, blockIdx.z, bid, tiles_x, tiles_y, blockIdx.y * BN);
 }
 
 // split-K reduce: out = epilogue(sum_s ws[ph*S + s][m][n]) in a fixed order
