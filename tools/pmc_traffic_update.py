@@ -31,6 +31,7 @@ def main():
     line = [l for l in open(log) if l.startswith("{")][-1]
     rl = json.loads(line)
     kernel, shape = rl["kernel"], rl["launch"].split(": ", 1)[1]
+    kind = rl["launch"].split(": ", 1)[0]     # conv_fwd / conv_dgrad / ...: one kernel may serve both directions
     reps = int(rl["timing"].split(",")[1].split()[0])
     base = kernel.split("<")[0].split(" ")[0]
     f = last_dispatches(fetch_dir, "FETCH_SIZE", base, reps)
@@ -39,7 +40,7 @@ def main():
         sys.exit(f"no {base} dispatches with counters")
     f_kib, w_kib = sorted(f)[len(f) // 2], sorted(w)[len(w) // 2]
     rd, wr = 2.0 * f_kib * 1024, w_kib * 1024
-    rec = {"workload": rl["workload"], "kernel": kernel, "shape": shape, "lib_sha256": rl.get("lib_sha256"),
+    rec = {"workload": rl["workload"], "kernel": kernel, "shape": shape, "kind": kind, "lib_sha256": rl.get("lib_sha256"),
            "dispatches": [len(f), len(w)],
            "fetch_size_kib": round(f_kib, 1), "write_size_kib": round(w_kib, 1),
            "read_bytes_per_launch": round(rd), "write_bytes_per_launch": round(wr),
@@ -55,7 +56,7 @@ def main():
         recs = [recs]
     # one record per launch: a re-measurement (of a new build) replaces the old one
     recs = [r for r in recs if not (r.get("workload") == rec["workload"] and r.get("kernel") == kernel
-                                     and r.get("shape") == shape)]
+                                     and r.get("shape") == shape and r.get("kind", kind) == kind)]
     recs.append(rec)
     json.dump(recs, open(path, "w"), indent=1)
     print(json.dumps(rec))
