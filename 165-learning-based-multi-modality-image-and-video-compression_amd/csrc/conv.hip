@@ -1693,13 +1693,13 @@ __global__ __launch_bounds__(512, 1) void conv_halo_phase_kernel(const ConvArgs 
 template <int BN, bool GATHER>
 __global__ __launch_bounds__(512, 1) void conv_halo_s1_kernel(const ConvArgs a, int tiles_x, int tiles_y) {
     constexpr bool DMA = BN > 128;
-    __shared__ __attribute__((aligned(16))) char smem[DMA ? HaloWideCfg<3, 3, BN>::BYTES : HaloPhCfg<3, 3>::BYTES];
+    __shared__ __attribute__((aligned(16))) char smem[DMA ? HaloWideCfg<3, 3, BN>::BYTES : HaloPhCfg<3, 3, BN>::BYTES];
     const int nt = gridDim.x, t = blockIdx.x;
     const int bid = (nt & 7) == 0 ? (t & 7) * (nt >> 3) + (t >> 3) : t;
     if constexpr (DMA)
         conv_halo_wide_body<3, 3, GATHER, BN, !GATHER>(a, smem, 0, blockIdx.z, bid, tiles_x, tiles_y, blockIdx.y * BN);
     else
-        conv_halo_phase_body<3, 3, 128, GATHER, !GATHER>(a, smem, 0, blockIdx.z, bid, tiles_x, tiles_y, blockIdx.y * BN);
+        conv_halo_phase_body<3, 3, BN, GATHER, !GATHER>(a, smem, 0, blockIdx.z, bid, tiles_x, tiles_y, blockIdx.y * BN);
 }
 
 // split-K reduce: out = epilogue(sum_s ws[ph*S + s][m][n]) in a fixed order
@@ -3742,13 +3742,23 @@ static int halo_s1_split_cin() {
     }();
     return v;
 }
+// 64-channel outputs on 256 x 64 halo tiles (conv_halo_s1_kernel<64>: the multimodal trunks' ResidualBlock(64, 64)
+// 3x3 convs at 512x640, 17 each of forward / input gradient per step on conv_glds_kernel<256x64> at 0.10-0.12 of
+// the bf16 peak, re-gathering the input per tap); A/B knob CAI_HALO_S1_BN64=0 keeps them there
+static bool halo_s1_bn64() {
+    static const bool on = [] {
+        const char* e = getenv("CAI_HALO_S1_BN64");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
 static bool halo_s1_ok(const cai_conv_geom* g, const Plan& P, bool glds, bool wide) {
     const int bn = halo_bn(P.kout_c);
     const int64_t tiles = (int64_t)g->batch * ((P.OWg[0] + 31) / 32) * ((P.OHg[0] + 7) / 8) * ((P.kout_c + bn - 1) / bn);
     const bool split_wide = halo_s1_split_cin() > 0 && P.Cin_pad >= halo_s1_split_cin() && tiles >= 64;
     return glds && !halo_off() && !halo_s1_off() && g->stride == 1 && g->kernel == 3 && g->pad == 1 &&
            P.nphase == 1 && P.ntaps[0] == 9 && P.Cin_pad % 64 == 0 && (bn == 128 || wide) && P.OHg[0] >= 8 &&
-           P.OWg[0] >= 32 && (tiles >= 128 || split_wide) && P.kout_c > 64;
+           P.OWg[0] >= 32 && (tiles >= 128 || split_wide) && (P.kout_c > 64 || (P.kout_c == 64 && halo_s1_bn64()));
 }
 
 
@@ -3773,7 +3783,7 @@ static ConvLaunch conv_launch(const cai_conv_geom* g, int dtype, int direction, 
     L.halo_s1 = !L.halo && !L.halo_ph && halo_s1_ok(g, P, L.glds, wide);
     if (L.halo_ph || L.halo_s1) {
         const int np = L.halo_ph ? 4 : 1;
-        L.hbn = halo_bn(P.kout_c);
+        L.hbn = (L.halo_s1 && P.kout_c == 64) ? 64 : halo_bn(P.kout_c);
         L.BM = 256;
         L.BN = L.hbn;
         L.tiles_x = (P.OWg[0] + 31) / 32;
@@ -3900,6 +3910,11 @@ static void launch_conv_halo_phase(const ConvArgs& a, const ConvLaunch& L, hipSt
                 hipLaunchKernelGGL((conv_halo_s1_kernel<192, true>), grid, dim3(512), 0, st, a, L.tiles_x, L.tiles_y);
             else
                 hipLaunchKernelGGL((conv_halo_s1_kernel<192, false>), grid, dim3(512), 0, st, a, L.tiles_x, L.tiles_y);
+        } else if (L.hbn == 64) {
+            if (gather)
+                hipLaunchKernelGGL((conv_halo_s1_kernel<64, true>), grid, dim3(512), 0, st, a, L.tiles_x, L.tiles_y);
+            else
+                hipLaunchKernelGGL((conv_halo_s1_kernel<64, false>), grid, dim3(512), 0, st, a, L.tiles_x, L.tiles_y);
         } else {
             if (gather)
                 hipLaunchKernelGGL((conv_halo_s1_kernel<128, true>), grid, dim3(512), 0, st, a, L.tiles_x, L.tiles_y);
@@ -4138,6 +4153,16 @@ static int wg_min_strips() {
     return v;
 }
 
+// 64-row weight-gradient tiles for the k3 layers with Ng = 64 too (the 128-row tiles left half their rows empty:
+// the multimodal trunks' 64 -> 64 3x3 convs); A/B knob CAI_HALO_WGRAD_K3_ROWS64=0 keeps 128
+static bool halo_wgrad_rows64_k3() {
+    static const bool on = [] {
+        const char* e = getenv("CAI_HALO_WGRAD_K3_ROWS64");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
+
 static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype, bool glds, bool in_tf = false) {
     WgradPlan W{};
     W.glds = glds && dtype == CAI_BF16;
@@ -4185,7 +4210,8 @@ static WgradPlan make_wgrad_plan(const cai_conv_geom* g, int dtype, bool glds, b
             const char* e = getenv("CAI_HALO_WGRAD_ROWS128");
             return e && *e == '1';
         }();
-        W.hrows = (!rows128 && W.halo == 5 && W.Ng % 128 != 0 && W.Ng % 64 == 0) ? 64 : 128;
+        W.hrows = (!rows128 && (W.halo == 5 || (W.Ng == 64 && halo_wgrad_rows64_k3())) && W.Ng % 128 != 0 &&
+                   W.Ng % 64 == 0) ? 64 : 128;
         // 192-row tiles for the stride-1 k3 kernel at Ng = 192 k (cheng2020's 3x3 convs).  A/B knob
         // CAI_HALO_WGRAD_ROWS192=0 keeps 128.
         static const bool rows192 = [] {
@@ -4567,7 +4593,8 @@ const char* cai_conv_kernel_name(const cai_conv_geom* g, int dtype, int directio
         }
         return L.hbn == 192 ? "conv_halo_phase_kernel<192>" : "conv_halo_phase_kernel";
     }
-    if (L.halo_s1) return L.hbn == 192 ? "conv_halo_s1_kernel<192>" : "conv_halo_s1_kernel<128>";
+    if (L.halo_s1)
+        return L.hbn == 192 ? "conv_halo_s1_kernel<192>" : (L.hbn == 64 ? "conv_halo_s1_kernel<64>" : "conv_halo_s1_kernel<128>");
     if (L.small) return L.small == SMALL_16x32 ? "conv_small_kernel<16x32>"
                         : (L.small == SMALL_32x32 ? "conv_small_kernel<32x32>" : "conv_small_kernel<32x64>");
     switch (L.cfg) {

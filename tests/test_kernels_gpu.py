@@ -1323,6 +1323,41 @@ def test_halo_s1_split_k_input_gradient(cuda):
     assert relerr(x.grad.float(), xr.grad) < 1e-2, relerr(x.grad.float(), xr.grad)
 
 
+@pytest.mark.parametrize("H,W", [(256, 320), (130, 150)], ids=["even", "ragged"])
+def test_halo_s1_64_channel_tiles(cuda, H, W):
+    """The multimodal trunks' ResidualBlock(64, 64) 3x3 conv on the 256 x 64 halo tiles (conv_halo_s1_kernel<64>,
+    forward and input gradient) and its weight gradient on 64-row halo tiles, against torch fp32 on the same
+    bf16-rounded operands (relative max 1e-2); ragged: output tiles cut at both image edges."""
+    import ctypes
+
+    from compressai import _native as native
+    from compressai.layers import Conv2d
+
+    torch.manual_seed(H + W)
+    raw = native.lib.load()
+    g = native.ConvGeom(2, 64, H, W, 64, H, W, 3, 1, 1, 0, 0)
+    for d in (0, 1):
+        assert raw.cai_conv_kernel_name(ctypes.byref(g), native.BF16, d, 0).decode() == "conv_halo_s1_kernel<64>"
+    # the halo weight gradient needs whole 64-pixel strips (W % 64 == 0); the ragged case runs the LDS-DMA kernel
+    wname = "wgrad_halo_kernel<3,s1>" if W % 64 == 0 else "wgrad_glds_kernel<256>"
+    assert raw.cai_conv_kernel_name(ctypes.byref(g), native.BF16, 2, 0).decode() == wname
+    mod = Conv2d(64, 64, 3, stride=1, padding=1).to(cuda)
+    x = torch.randn(2, 64, H, W, device=cuda).contiguous(memory_format=torch.channels_last).requires_grad_()
+    gy = torch.randn(2, 64, H, W, device=cuda)
+    with _autocast(True):
+        y = mod(x)
+    y.backward(gy)
+    xr = x.detach().bfloat16().float().requires_grad_()
+    wr = mod.weight.detach().bfloat16().float().requires_grad_()
+    br = mod.bias.detach().clone().requires_grad_()
+    yr = F.conv2d(xr, wr, br, padding=1)
+    yr.backward(gy.bfloat16().float())
+    assert relerr(y.float(), yr) < 1e-2, relerr(y.float(), yr)
+    assert relerr(x.grad.float(), xr.grad) < 1e-2, relerr(x.grad.float(), xr.grad)
+    assert relerr(mod.weight.grad, wr.grad) < 1e-2, relerr(mod.weight.grad, wr.grad)
+    assert relerr(mod.bias.grad, br.grad) < 1e-2, relerr(mod.bias.grad, br.grad)
+
+
 @pytest.mark.parametrize("B,cin,cout,H,bias", [
     (2, 192, 192, 128, True),    # cheng2020's 3x3 convs at 128x128
     (2, 192, 576, 64, True),     # three 192-row tiles
