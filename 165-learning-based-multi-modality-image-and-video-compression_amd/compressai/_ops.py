@@ -844,9 +844,15 @@ def conv_wgrad(g, dt, xpm, xld, in_abs, gpm, gld, wparam, bparam, weight, has_bi
     code = dcode(dt)
     dev = gpm.device
     nbytes = lib.cai_conv_wgrad_workspace_bytes(ctypes.byref(g), code)
-    direct = direct_grad(wparam) and (bparam is None or direct_grad(bparam))
+    # a weight passed as a same-size view of its parameter (Linear's [out, in] weight viewed [out, in, 1, 1]): its
+    # gradient lands in the parameter's flat-buffer slot through the same view (autograd's add into .grad skipped)
+    wbase = getattr(wparam, "_base", None)
+    wdir = wparam if direct_grad(wparam) else (
+        wbase if wbase is not None and wbase.numel() == wparam.numel() and direct_grad(wbase) else None)
+    direct = wdir is not None and (bparam is None or direct_grad(bparam))
     if direct:   # accumulate straight into the optimizer's flat gradient buffer
-        dw, db = wparam.grad, (bparam.grad if bparam is not None else None)
+        dw = wdir.grad if wdir is wparam else wdir.grad.view(wparam.shape)
+        db = bparam.grad if bparam is not None else None
     else:
         dw = torch.empty(weight.shape, dtype=torch.float32, device=dev)
         db = torch.empty(g.out_c, dtype=torch.float32, device=dev) if has_bias else None
