@@ -94,16 +94,86 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const T* __restrict_
     }
 }
 
-__global__ void layernorm_param_reduce(const float* __restrict__ part, int nblk, int C, float* __restrict__ dw,
-                                       float* __restrict__ db, int accumulate) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= 2 * C) return;
+// C <= 128 (the Swin blocks' 96 channels): a lane's <= 2 channels of x / dy stay in registers between the two passes
+// and the dw / db partials accumulate in registers, written to LDS once -- the general kernel above reloads x / dy
+// for the dx pass and read-modify-writes LDS per token (31 us per call on the multimodal 40960 x 96 tokens)
+template <typename T>
+__global__ __launch_bounds__(256) void layernorm_bwd_reg_kernel(const T* __restrict__ x, int xld, const T* __restrict__ dy,
+                                                                int dyld, int ntok, int C, const float* __restrict__ w,
+                                                                const float* __restrict__ mean,
+                                                                const float* __restrict__ rstd, T* __restrict__ dx,
+                                                                int dxld, float* __restrict__ part, int tok_per_block) {
+    extern __shared__ float sm[];   // [4 waves][2][C]
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int c0 = lane, c1 = lane + 64;
+    const bool h0 = c0 < C, h1 = c1 < C;
+    const float w0 = h0 ? w[c0] : 0.f, w1 = h1 ? w[c1] : 0.f;
+    float pw0 = 0.f, pw1 = 0.f, pb0 = 0.f, pb1 = 0.f;
+    const int t0 = blockIdx.x * tok_per_block;
+    const int t1 = min(ntok, t0 + tok_per_block);
+    for (int tok = t0 + wv; tok < t1; tok += 4) {
+        const T* xr = x + (int64_t)tok * xld;
+        const T* gr = dy + (int64_t)tok * dyld;
+        const float mu = mean[tok], rs = rstd[tok];
+        const float x0 = h0 ? ldf(xr, c0) : 0.f, x1 = h1 ? ldf(xr, c1) : 0.f;
+        const float g0 = h0 ? ldf(gr, c0) : 0.f, g1 = h1 ? ldf(gr, c1) : 0.f;
+        const float xh0 = (x0 - mu) * rs, xh1 = (x1 - mu) * rs;
+        const float a = wave_sum(g0 * w0 + g1 * w1);
+        const float bs = wave_sum(g0 * w0 * xh0 + g1 * w1 * xh1);
+        pw0 += g0 * xh0;
+        pw1 += g1 * xh1;
+        pb0 += g0;
+        pb1 += g1;
+        const float ma = a / C, mb = bs / C;
+        T* dr = dx + (int64_t)tok * dxld;
+        if (h0) dr[c0] = from_f32<T>(rs * (g0 * w0 - ma - xh0 * mb));
+        if (h1) dr[c1] = from_f32<T>(rs * (g1 * w1 - ma - xh1 * mb));
+    }
+    float* pw = sm + wv * 2 * C;
+    if (h0) { pw[c0] = pw0; pw[C + c0] = pb0; }
+    if (h1) { pw[c1] = pw1; pw[C + c1] = pb1; }
+    __syncthreads();
+    for (int c = threadIdx.x; c < 2 * C; c += 256) {
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s += sm[k * 2 * C + c];
+        part[(int64_t)blockIdx.x * 2 * C + c] = s;
+    }
+}
+
+// [nblk][2C] partials -> dw / db: a block per 32 columns, 32 row groups of 32 threads (row group g sums rows g,
+// g + 32, ... in order, eight loads in flight), the 32 group sums combined in group order through LDS -- a fixed
+// order, so the result is deterministic.  (One 192-thread block walking all 1024 rows serially took ~65 us per
+// call: 18 calls, 1.2 ms of the multimodal step.)
+constexpr int LNR_COLS = 32, LNR_GROUPS = 32;
+__global__ __launch_bounds__(LNR_COLS * LNR_GROUPS) void layernorm_param_reduce(const float* __restrict__ part,
+                                                                                int nblk, int C, float* __restrict__ dw,
+                                                                                float* __restrict__ db, int accumulate) {
+    __shared__ float red[LNR_GROUPS][LNR_COLS + 1];
+    const int col = threadIdx.x % LNR_COLS, grp = threadIdx.x / LNR_COLS;
+    const int c = blockIdx.x * LNR_COLS + col;
     float s = 0.f;
-    for (int i = 0; i < nblk; ++i) s += part[(int64_t)i * 2 * C + c];
+    if (c < 2 * C) {
+        int i = grp;
+        for (; i + 7 * LNR_GROUPS < nblk; i += 8 * LNR_GROUPS) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = part[(int64_t)(i + j * LNR_GROUPS) * 2 * C + c];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s += v[j];
+        }
+        for (; i < nblk; i += LNR_GROUPS) s += part[(int64_t)i * 2 * C + c];
+    }
+    red[grp][col] = s;
+    __syncthreads();
+    if (grp != 0 || c >= 2 * C) return;
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < LNR_GROUPS; ++g) t += red[g][col];
     float* base = c < C ? dw : db;
     if (base == nullptr) return;
     float* d = base + (c < C ? c : c - C);
-    *d = accumulate ? *d + s : s;
+    *d = accumulate ? *d + t : t;
 }
 
 // --------------------------------------------------------------------------
@@ -508,6 +578,15 @@ int cai_layernorm_fwd(int dtype, const void* x, int32_t x_ld, int64_t ntok, int3
     return CAI_OK;
 }
 
+// A/B knob CAI_LN_BWD_REG=0: the general LayerNorm backward for C <= 128 too
+static bool layernorm_bwd_reg() {
+    static const bool on = [] {
+        const char* e = getenv("CAI_LN_BWD_REG");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
+
 size_t cai_layernorm_bwd_workspace_bytes(int64_t ntok, int32_t C) {
     const int64_t nblk = std::min<int64_t>(1024, (ntok + 63) / 64);
     return (size_t)std::max<int64_t>(nblk, 1) * 2 * C * sizeof(float);
@@ -525,12 +604,17 @@ int cai_layernorm_bwd(int dtype, const void* x, int32_t x_ld, const void* dy, in
     const int per = (int)((ntok + nblk - 1) / nblk);
     float* part = reinterpret_cast<float*>(workspace);
     hipStream_t st = as_stream(stream);
-    DISPATCH_T(dtype, hipLaunchKernelGGL(layernorm_bwd_kernel<T>, dim3(nblk), dim3(256), 4 * 2 * C * sizeof(float), st,
-                                         (const T*)x, x_ld, (const T*)dy, dy_ld, (int)ntok, C, w, mean, rstd, (T*)dx,
-                                         dx_ld, part, per));
+    if (C <= 128 && layernorm_bwd_reg())
+        DISPATCH_T(dtype, hipLaunchKernelGGL(layernorm_bwd_reg_kernel<T>, dim3(nblk), dim3(256), 4 * 2 * C * sizeof(float),
+                                             st, (const T*)x, x_ld, (const T*)dy, dy_ld, (int)ntok, C, w, mean, rstd,
+                                             (T*)dx, dx_ld, part, per));
+    else
+        DISPATCH_T(dtype, hipLaunchKernelGGL(layernorm_bwd_kernel<T>, dim3(nblk), dim3(256), 4 * 2 * C * sizeof(float),
+                                             st, (const T*)x, x_ld, (const T*)dy, dy_ld, (int)ntok, C, w, mean, rstd,
+                                             (T*)dx, dx_ld, part, per));
     if (dw || db)
-        hipLaunchKernelGGL(layernorm_param_reduce, dim3((2 * C + 255) / 256), dim3(256), 0, st, part, nblk, C, dw, db,
-                           accumulate);
+        hipLaunchKernelGGL(layernorm_param_reduce, dim3((2 * C + LNR_COLS - 1) / LNR_COLS), dim3(LNR_COLS * LNR_GROUPS),
+                           0, st, part, nblk, C, dw, db, accumulate);
     CAI_LAUNCH_CHECK("layernorm_bwd");
     return CAI_OK;
 }

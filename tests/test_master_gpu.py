@@ -49,8 +49,11 @@ def _ref_tokens(t):
     return t.flatten(2).transpose(1, 2).contiguous()
 
 
-@pytest.mark.parametrize("C", [96, 64])
-def test_layernorm(cuda, C):
+@pytest.mark.parametrize("C,H,W", [(96, 8, 12), (64, 8, 12), (192, 8, 12), (96, 128, 160)],
+                         ids=["96", "64", "192-general", "96-40960tok"])
+def test_layernorm(cuda, C, H, W):
+    """LayerNorm fwd / bwd against torch fp32.  C <= 128 runs the register backward, 192 the general one; 40960
+    tokens (the multimodal Swin blocks' largest map) give 640 partial blocks for the parameter-gradient reduce."""
     from compressai.models.master import LayerNorm
 
     torch.manual_seed(0)
@@ -59,8 +62,8 @@ def test_layernorm(cuda, C):
         ref.weight.uniform_(0.5, 1.5)
         ref.bias.uniform_(-0.5, 0.5)
     mod = _copy(ref, LayerNorm(C), cuda)
-    x = _tokens(2, C, 8, 12, 1)
-    g = _tokens(2, C, 8, 12, 2)
+    x = _tokens(2, C, H, W, 1)
+    g = _tokens(2, C, H, W, 2)
     xr = _ref_tokens(x).requires_grad_()
     yr = ref(xr)
     yr.backward(_ref_tokens(g))
