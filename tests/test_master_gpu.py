@@ -91,6 +91,42 @@ def test_gelu(cuda):
     assert relerr(xd.grad, xr.grad) < 1e-5
 
 
+def test_gelu_and_channel_affine_bf16(cuda):
+    """The bf16 8-channel-chunk kernels (GELU fwd / bwd, the channel aligner's y = gamma * x + beta and its input
+    gradient) against torch fp32 on the same bf16 operands: relative max 1e-2 (one bf16 rounding of the output)."""
+    from compressai._ops import ChannelAffineFn
+    from compressai.models.master import GELU
+
+    torch.manual_seed(21)
+    x = (torch.randn(2, 96, 16, 20, device=cuda) * 3).bfloat16().contiguous(memory_format=torch.channels_last)
+    g = torch.randn(2, 96, 16, 20, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+    xd = x.clone().requires_grad_()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = GELU()(xd)
+    y.backward(g)
+    xr = x.float().requires_grad_()
+    yr = torch.nn.GELU()(xr)
+    yr.backward(g.float())
+    assert relerr(y.float(), yr) < 1e-2
+    assert relerr(xd.grad.float(), xr.grad) < 1e-2
+
+    f = torch.randn(2, 64, 24, 20, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+    gamma = torch.randn(2, 64, 1, 1, device=cuda, requires_grad=True)
+    beta = torch.randn(2, 64, 1, 1, device=cuda, requires_grad=True)
+    fd = f.clone().requires_grad_()
+    gy = torch.randn(2, 64, 24, 20, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = ChannelAffineFn.apply(fd, gamma, beta)
+    out.backward(gy)
+    fr = f.float().requires_grad_()
+    gr, br = gamma.detach().clone().requires_grad_(), beta.detach().clone().requires_grad_()
+    outr = gr * fr + br
+    outr.backward(gy.float())
+    assert relerr(out.float(), outr) < 1e-2
+    assert relerr(fd.grad.float(), fr.grad) < 1e-2
+    assert relerr(gamma.grad, gr.grad) < 1e-2 and relerr(beta.grad, br.grad) < 1e-2
+
+
 @pytest.mark.parametrize("shift", [0, 2])
 @pytest.mark.parametrize("res", [(8, 8), (8, 12), (12, 8)])
 def test_swin_block(cuda, shift, res):
