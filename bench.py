@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--roofline-only", action="store_true",
                     help="profile one step, then replay only its dominant launch --steps times "
                          "(for rocprofv3 --pmc passes)")
+    ap.add_argument("--two-graphs", action="store_true",
+                    help="one rank: capture the step as two graphs (forward+backward, then clip+Adam+aux) like N > 1 "
+                         "(A/B of the single-graph step)")
     ap.add_argument("--replay", default=None,
                     help="with --roofline-only: replay this launch instead of the dominant one "
                          "('kind:index' of the ops table, e.g. conv_wgrad:3)")
@@ -437,7 +440,14 @@ def main():
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         gA, gB = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        if sync is None:
+        # one rank: the whole step is ONE graph (the gap between two graph launches -- the backward's last reduce to
+        # the clip's first kernel -- measured 8.7 us per C2 step); N > 1 needs the exchange between the two
+        single = sync is None and world == 1 and not args.two_graphs
+        if single:
+            with torch.cuda.graph(gA):
+                fwd_bwd()
+                opt_part()
+        elif sync is None:
             with torch.cuda.graph(gA):
                 fwd_bwd()
         else:
@@ -447,11 +457,14 @@ def main():
             for i, g in enumerate(gT, 1):
                 with torch.cuda.graph(g, pool=gA.pool()):
                     sync.backward_phase(i)
-        with torch.cuda.graph(gB, pool=gA.pool()):
-            opt_part()
+        if not single:
+            with torch.cuda.graph(gB, pool=gA.pool()):
+                opt_part()
 
         def step():
             gA.replay()
+            if single:
+                return
             if sync is None:
                 allreduce_mean_(opt.flat_grad)
             else:
