@@ -228,6 +228,9 @@ __device__ __forceinline__ void conv_epilogue_rows(const ConvArgs& a, const Phas
     }
 }
 
+#ifndef CAI_WG_BIAS_AFTER
+#define CAI_WG_BIAS_AFTER 1   // A/B: 0 = the halo weight gradient's bias sums ahead of each fragment's MFMAs
+#endif
 #ifndef CAI_EPI_MASK_PREFETCH
 #define CAI_EPI_MASK_PREFETCH 2   // A/B: 0 = the per-chunk masked epilogue, 1 = staged through LDS with prefetch
 #endif
@@ -3231,10 +3234,11 @@ __device__ __forceinline__ void wgrad_halo_block(const WgradArgs& a, int wgid, i
             fa[tm] = __builtin_bit_cast(u32x4, av);
         }
     };
+    constexpr bool BIAS_AFTER = CAI_WG_BIAS_AFTER && TMR <= 4;
     auto mm = [&](const u32x4 (&fa)[TMR], const u32x4 (&fb)[W::TN]) {
 #pragma unroll
         for (int tm = 0; tm < TMR; ++tm) {
-            if constexpr ((FLAGS & WG_BIAS) != 0) {
+            if constexpr ((FLAGS & WG_BIAS) != 0 && !BIAS_AFTER) {
                 if (do_bias && (tm & 3) == wc) {   // fragment tm's sums: column-wave tm % 4
                     const bf16x8 h = __builtin_bit_cast(bf16x8, fa[tm]);
                     float sacc = 0.f;
@@ -3245,6 +3249,15 @@ __device__ __forceinline__ void wgrad_halo_block(const WgradArgs& a, int wgid, i
             }
 #pragma unroll
             for (int tn = 0; tn < W::TN; ++tn) acc[tm][tn] = mma16<bf16>(fa[tm], fb[tn], acc[tm][tn]);
+        }
+        // the bias sums behind the step's MFMAs (CAI_WG_BIAS_AFTER): ahead of them they delayed each fragment's issue
+        // (not the 192-row tiles: six A fragments held to the end spill)
+        if constexpr ((FLAGS & WG_BIAS) != 0 && BIAS_AFTER) {
+            if (do_bias) {
+#pragma unroll
+                for (int tm = 0; tm < TMR; ++tm)
+                    if ((tm & 3) == wc) bsum[tm] += sum8_bf16(fa[tm]);
+            }
         }
         // transposed bias sums after the MFMAs: inside the read loop they made each B read wait
         if constexpr ((FLAGS & WG_TBIAS) != 0) {
