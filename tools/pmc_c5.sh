@@ -1,5 +1,5 @@
 #!/bin/bash
-# r06: FETCH_SIZE / WRITE_SIZE of C5's 256->256 stride-1 halo launches (forward, input gradient, weight gradient),
+# FETCH_SIZE / WRITE_SIZE of C5's 256->256 stride-1 halo launches (forward, input gradient, weight gradient),
 # each replayed alone; one counter group per rocprofv3 run
 out=$GRAFT_REPO_ROOT/gpurun_out
 cd /tmp && export TMPDIR=/tmp
