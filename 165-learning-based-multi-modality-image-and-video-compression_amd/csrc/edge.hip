@@ -783,6 +783,127 @@ __global__ __launch_bounds__(NT, 1) void edge_wgrad_dma_kernel(const EdgeArgs A)
             for (int q = 0; q < 4; ++q) P[(t * 16 + 4 * g_ + q) * 128 + (wave * 2 + j) * 16 + i16] = acc[t][j][q];
 }
 
+// Weight gradient, N = 192, the same LDS-DMA ring on 64-column steps (three 40 KB stages): the feature tile as
+// channels 0-127 in the swizzled [64 px][256 B] image and channels 128-191 in a plain [64 px][128 B] one, the three
+// packed superpixel rows [3][68][32 B]; wave w owns the n-tiles 3w .. 3w + 2 (4 + 2 + 2 DMA instructions per wave
+// and step).  (The general kernel below ran the C2' / mbt2018 first layers at ~87 us, 3.5x the N = 128 DMA kernel.)
+constexpr int W2TB = 64;                  // columns per step
+constexpr int W2P0 = W2TB * 256;          // channels 0-127
+constexpr int W2P1 = W2TB * 128;          // channels 128-191
+constexpr int W2SR = (W2TB + 4) * 32;     // one packed superpixel row (66 used)
+constexpr int W2SB = 8 * 1024;            // S region: 3 rows, padded to 8 DMA instructions
+constexpr int W2STAGE = W2P0 + W2P1 + W2SB;
+constexpr int W2G = 8;                    // DMA instructions per wave and step
+
+__global__ __launch_bounds__(NT, 1) void edge_wgrad_dma192_kernel(const EdgeArgs A) {
+    __shared__ __attribute__((aligned(16))) char smem[3 * W2STAGE];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g_ = lane >> 4, i16 = lane & 15, q_ = i16 >> 2, p4 = i16 & 3;
+    const int ncb = (A.Ws + W2TB - 1) / W2TB;
+    const int nch = (A.Hs + A.rch - 1) / A.rch;
+    const int unit = blockIdx.x;
+    const int ch = unit % nch, n = unit / nch;
+    const int a0 = ch * A.rch, a1 = min(a0 + A.rch, A.Hs);
+    const int nsteps = (a1 - a0) * ncb;
+    const char* Pg = reinterpret_cast<const char*>(A.feat);
+    const char* Sg = reinterpret_cast<const char*>(A.sbf);
+
+    auto issue = [&](int st, int stage) {
+        const int a = a0 + st / ncb, b0 = (st % ncb) * W2TB;
+        char* base = smem + stage * W2STAGE;
+        const char* prow = Pg + (((int64_t)n * A.Hs + a) * A.Ws) * A.feat_ld * 2;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {            // channels 0-127: 16 instructions of 4 rows, 4 per wave
+            const int k = i * 4 + wave;
+            const int row = k * 4 + (lane >> 4);
+            const int sl = (lane & 15) ^ ((((lane >> 4) & 3) << 1) | (((k >> 1) & 1) << 3));
+            const int px = b0 + row;
+            glds16(px < A.Ws ? (const void*)(prow + ((int64_t)px * A.feat_ld + sl * 8) * 2) : (const void*)edge_zero_page,
+                   base + k * 1024);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {            // channels 128-191: 8 instructions of 8 rows, 2 per wave
+            const int k = i * 4 + wave;
+            const int row = k * 8 + (lane >> 3);
+            const int px = b0 + row;
+            glds16(px < A.Ws ? (const void*)(prow + ((int64_t)px * A.feat_ld + 128 + (lane & 7) * 8) * 2)
+                             : (const void*)edge_zero_page,
+                   base + W2P0 + k * 1024);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {            // superpixel rows: 8 instructions, 2 per wave
+            const int k = i * 4 + wave;
+            const int off = k * 1024 + lane * 16;
+            const void* src = (const void*)edge_zero_page;
+            if (off < 3 * W2SR) {
+                const int sr = off / W2SR, rem = off - sr * W2SR;
+                const int j = sswz(rem / 32);
+                const int sa = a - 1 + sr, sb = b0 - 1 + j;
+                if (sa >= 0 && sa < A.Hs && sb >= 0 && sb < A.Ws && j < W2TB + 2)
+                    src = (const void*)(Sg + ((((int64_t)n * A.Hs + sa) * A.Ws + sb) * 16) * 2 + (rem & 31));
+            }
+            glds16(src, base + W2P0 + W2P1 + k * 1024);
+        }
+    };
+
+    f32x4 acc[9][3];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[t][0] = acc[t][1] = acc[t][2] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int soff[3][2];
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) soff[dx][h] = sswz(8 * g_ + q_ + dx + 4 * h) * 32 + 8 * p4;
+    if (nsteps > 0) issue(0, 0);
+    if (nsteps > 1) issue(1, 1);
+    for (int st = 0; st < nsteps; ++st) {
+        if (st + 1 < nsteps)
+            wait_vmcnt<W2G>();
+        else
+            wait_vmcnt<0>();
+        wait_lgkmcnt0();
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (st + 2 < nsteps) issue(st + 2, (st + 2) % 3);
+        const char* P0 = smem + (st % 3) * W2STAGE;
+        const char* P1 = P0 + W2P0;
+        const char* Sst = P1 + W2P1;
+#pragma unroll
+        for (int ks = 0; ks < W2TB / 32; ++ks) {
+            const int rr = 32 * ks + 8 * g_ + q_;
+            u32x4 bv[3];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const int nt = wave * 3 + j;
+                if (nt < 8) {
+                    const int col = nt * 16 + 4 * p4;
+                    bv[j] = tr_frag(P0, trswz(rr, col >> 3) + ((col & 7) << 1),
+                                    trswz(rr + 4, col >> 3) + ((col & 7) << 1));
+                } else {
+                    const int col = (nt - 8) * 16 + 4 * p4;
+                    bv[j] = tr_frag(P1, rr * 128 + col * 2, (rr + 4) * 128 + col * 2);
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const char* sbase = Sst + (t / 3) * W2SR + ks * 1024;
+                const u32x4 av = tr_frag(sbase, soff[t % 3][0], soff[t % 3][1]);
+#pragma unroll
+                for (int j = 0; j < 3; ++j) acc[t][j] = mma16<bf16>(av, bv[j], acc[t][j]);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    const int O = 9 * 16 * 192 + 16;
+    float* P = A.part + (int64_t)unit * O;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) P[(t * 16 + 4 * g_ + q) * 192 + (wave * 3 + j) * 16 + i16] = acc[t][j][q];
+}
+
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -821,7 +942,16 @@ int wgrad_units(const EdgeArgs& A, int* rch) {
     return A.B * ((A.Hs + r - 1) / r);
 }
 
-// workspace of the wgrad: [unit partials][packed superpixels (N = 128)][pack column sums]
+// the LDS-DMA weight-gradient kernels: N = 128, and N = 192 (A/B knob CAI_EDGE_WGRAD_DMA192=0: the general kernel)
+bool edge_wgrad_dma(const EdgeArgs& A) {
+    static const bool dma192 = [] {
+        const char* e = std::getenv("CAI_EDGE_WGRAD_DMA192");
+        return !(e && *e == '0');
+    }();
+    return A.N == 128 || (A.N == 192 && dma192);
+}
+
+// workspace of the wgrad: [unit partials][packed superpixels (DMA kernels)][pack column sums]
 struct WgradWs {
     size_t off_sbf, off_cs, total;
     int npack, ipb;
@@ -837,7 +967,7 @@ WgradWs wgrad_ws(const EdgeArgs& A) {
     W.npack = (int)((items + W.ipb - 1) / W.ipb);
     auto up = [](size_t v) { return (v + 255) / 256 * 256; };
     W.off_sbf = up((size_t)units * (9 * 16 * A.N + 16) * sizeof(float));
-    W.off_cs = W.off_sbf + (A.N == 128 ? up((size_t)rows * A.Ws * 32) : 0);
+    W.off_cs = W.off_sbf + (edge_wgrad_dma(A) ? up((size_t)rows * A.Ws * 32) : 0);
     W.total = W.off_cs + up((size_t)W.npack * 16 * sizeof(float));
     return W;
 }
@@ -905,14 +1035,17 @@ void launch_wgrad(EdgeArgs A, char* ws, float* dw, float* db, int accumulate, hi
     J->p[0] = A.part; J->p[2] = dw; J->p[3] = db;
     J->i[0] = A.N; J->i[1] = A.units; J->i[2] = A.mode; J->i[3] = A.k; J->i[4] = A.p; J->i[5] = C;
     J->i[8] = accumulate;
-    if (A.N == 128) {   // packed superpixels + LDS-DMA ring
+    if (edge_wgrad_dma(A)) {   // packed superpixels + LDS-DMA ring
         const WgradWs W = wgrad_ws(A);
         A.sbf = reinterpret_cast<bf16*>(ws + W.off_sbf);
         A.cs_part = reinterpret_cast<float*>(ws + W.off_cs);
         A.npack = W.npack;
         A.ipb = W.ipb;
         edge_pack_s_kernel<C><<<W.npack, 256, 0, st>>>(A);
-        edge_wgrad_dma_kernel<<<A.units, NT, 0, st>>>(A);
+        if (A.N == 128)
+            edge_wgrad_dma_kernel<<<A.units, NT, 0, st>>>(A);
+        else
+            edge_wgrad_dma192_kernel<<<A.units, NT, 0, st>>>(A);
         J->p[1] = A.cs_part; J->i[6] = W.npack; J->i[7] = 16;
     } else {
         edge_wgrad_kernel<C, 3><<<A.units, NT, 0, st>>>(A);
